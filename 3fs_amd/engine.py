@@ -1,0 +1,335 @@
+"""ctypes binding of ``include/h3c_crc.h`` plus the ``ChecksumInfo`` mirror.
+
+Reference interface mirrored here (paths relative to the 3FS checkout):
+
+* ``ChecksumType``            src/fbs/storage/Common.h:66-70
+* ``ChecksumInfo::create``    src/fbs/storage/Common.h:146-177
+* ``ChecksumInfo::combine``   src/fbs/storage/Common.h:179-198 (error 4080 on type mismatch)
+* ``operator==``              src/fbs/storage/Common.h:200
+* fmt formatter (``TYPE#~value``)  src/fbs/storage/Common.h:768-773
+* ``folly::crc32c_combine``   called at src/fbs/storage/Common.h:191
+
+Payload checksums always run on the GPU through ``libh3c_crc.so``.  The only
+host arithmetic is the scalar GF(2) combine, which the reference also does on
+the host (it touches no payload bytes).
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+from dataclasses import dataclass
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+lib_path = os.path.join(_HERE, "_lib", "libh3c_crc.so")
+
+if not os.path.exists(lib_path):
+    raise ImportError(
+        f"{lib_path} is missing: the HIP engine is not built (run `python -c 'import __graft_entry__ as g; g.build()'`). "
+        "There is no CPU fallback."
+    )
+
+lib = ctypes.CDLL(lib_path)
+
+_u8, _u16, _u32, _u64 = ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64
+_vp, _sz, _int = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+
+
+class _Desc(ctypes.Structure):
+    _fields_ = [("ptr", _vp), ("len", _u64), ("start_raw", _u32), ("type", _u8), ("mem", _u8), ("reserved", _u16)]
+
+
+assert ctypes.sizeof(_Desc) == 24
+
+DESC_DTYPE = np.dtype(
+    [("ptr", "<u8"), ("len", "<u8"), ("start_raw", "<u4"), ("type", "u1"), ("mem", "u1"), ("reserved", "<u2")]
+)
+assert DESC_DTYPE.itemsize == 24
+
+
+def _proto(name, restype, *argtypes):
+    f = getattr(lib, name)
+    f.restype = restype
+    f.argtypes = list(argtypes)
+    return f
+
+
+_proto("h3c_crc32c_combine", _u32, _u32, _u32, _u64)
+_proto("h3c_crc32_combine", _u32, _u32, _u32, _u64)
+_proto("h3c_crc32c_shift", _u32, _u32, _u64)
+_proto("h3c_device_count", _int)
+_proto("h3c_init", _int, _int)
+_proto("h3c_last_error", ctypes.c_char_p)
+_proto("h3c_batch_create", _int, _vp, _sz, _vp, _vp, _vp)
+_proto("h3c_batch_verify", _int, _vp, _vp, _sz, _vp, _vp, _vp, _vp)
+_proto("h3c_plan_create", _int, _vp, _sz, _int, ctypes.POINTER(_vp))
+_proto("h3c_plan_run", _int, _vp, _vp, _vp, _vp, _vp, _vp)
+_proto("h3c_plan_bytes", _u64, _vp)
+_proto("h3c_plan_destroy", None, _vp)
+_proto("h3c_batch_combine", _int, _u8, _vp, _vp, _vp, _sz, _vp, _vp)
+_proto("h3c_fill_splitmix", _int, _vp, _u64, _u64, _u64, _u64, _u64, _vp)
+_proto("h3c_profile_enable", None, _int)
+_proto("h3c_profile_read", _int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64), ctypes.POINTER(_u64), _int)
+
+
+class ChecksumType(enum.IntEnum):
+    """``enum class ChecksumType : uint8_t`` (Common.h:66-70)."""
+
+    NONE = 0
+    CRC32C = 1
+    CRC32 = 2
+
+
+class StatusCode(enum.IntEnum):
+    OK = 0
+    kInvalidArg = 3
+    kChunkReadFailed = 4010  # StatusCodeDetails.h:160
+    kChecksumMismatch = 4080  # StatusCodeDetails.h:186
+    kHipError = 9001
+    kNoDevice = 9002
+
+
+class MemKind(enum.IntEnum):
+    DEVICE = 0
+    HOST_PINNED = 1
+    HOST_PAGEABLE = 2
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        self.code = int(code)
+        detail = msg or (lib.h3c_last_error() or b"").decode(errors="replace")
+        try:
+            name = StatusCode(self.code).name
+        except ValueError:
+            name = str(self.code)
+        super().__init__(f"h3c error {name}: {detail}")
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise EngineError(rc)
+
+
+def _stream_handle(stream) -> int:
+    if stream is None:
+        try:
+            import torch
+
+            if torch.cuda.is_available():
+                return torch.cuda.current_stream().cuda_stream
+        except ImportError:  # pragma: no cover
+            pass
+        return 0
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+# ---------------------------------------------------------------- scalar host arithmetic
+
+
+def crc32c_combine(c1: int, c2: int, len2: int) -> int:
+    """``folly::crc32c_combine`` (Common.h:191)."""
+    return lib.h3c_crc32c_combine(c1 & 0xFFFFFFFF, c2 & 0xFFFFFFFF, len2)
+
+
+def crc32_combine(c1: int, c2: int, len2: int) -> int:
+    """``folly::crc32_combine`` (Common.h:195)."""
+    return lib.h3c_crc32_combine(c1 & 0xFFFFFFFF, c2 & 0xFFFFFFFF, len2)
+
+
+def crc32c_shift(crc: int, nbytes: int) -> int:
+    return lib.h3c_crc32c_shift(crc & 0xFFFFFFFF, nbytes)
+
+
+def device_count() -> int:
+    return lib.h3c_device_count()
+
+
+# ---------------------------------------------------------------- payload adapters
+
+
+def _payload(data, length: Optional[int]):
+    """Return (ptr, nbytes, mem, keepalive) for a payload object."""
+    if data is None:
+        return 0, (length or 0), MemKind.HOST_PAGEABLE, None
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        torch = None
+    if torch is not None and isinstance(data, torch.Tensor):
+        if not data.is_contiguous():
+            raise ValueError("payload tensor must be contiguous")
+        nbytes = data.numel() * data.element_size()
+        if data.is_cuda:
+            mem = MemKind.DEVICE
+        else:
+            mem = MemKind.HOST_PINNED if data.is_pinned() else MemKind.HOST_PAGEABLE
+        return data.data_ptr(), nbytes, mem, data
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        arr = np.frombuffer(data, dtype=np.uint8)
+        return arr.ctypes.data if arr.size else 0, arr.size, MemKind.HOST_PAGEABLE, (data, arr)
+    if isinstance(data, np.ndarray):
+        arr = np.ascontiguousarray(data)
+        return arr.ctypes.data if arr.size else 0, arr.nbytes, MemKind.HOST_PAGEABLE, arr
+    raise TypeError(f"unsupported payload type {type(data)!r}")
+
+
+def _desc_array(items: Sequence, type_: int, start: int):
+    descs = np.zeros(len(items), dtype=DESC_DTYPE)
+    keep = []
+    for i, it in enumerate(items):
+        if isinstance(it, tuple):
+            data, length = it[0], it[1]
+            st = it[2] if len(it) > 2 else start
+            ty = it[3] if len(it) > 3 else type_
+        else:
+            data, length, st, ty = it, None, start, type_
+        ptr, nbytes, mem, ka = _payload(data, length)
+        if length is not None:
+            if data is not None and length > nbytes:
+                raise ValueError(f"length {length} exceeds payload size {nbytes}")
+            nbytes = length
+        keep.append(ka)
+        descs[i] = (ptr, nbytes, st & 0xFFFFFFFF, int(ty), int(mem), 0)
+    return descs, keep
+
+
+# ---------------------------------------------------------------- batch API
+
+
+def batch_create(items: Sequence, type_: int = ChecksumType.CRC32C, start: int = 0xFFFFFFFF, stream=None):
+    """ChecksumInfo::create over every item; returns (types uint8[n], raw uint32[n])."""
+    descs, keep = _desc_array(items, type_, start)
+    n = len(descs)
+    out_t = np.zeros(n, dtype=np.uint8)
+    out_v = np.zeros(n, dtype=np.uint32)
+    _check(lib.h3c_batch_create(descs.ctypes.data, n, out_t.ctypes.data, out_v.ctypes.data, _stream_handle(stream)))
+    del keep
+    return out_t, out_v
+
+
+def batch_verify(items: Sequence, expected: Sequence[int], type_: int = ChecksumType.CRC32C,
+                 start: int = 0xFFFFFFFF, stream=None):
+    """Recompute and compare; returns (raw uint32[n], ok bool[n], n_mismatch)."""
+    descs, keep = _desc_array(items, type_, start)
+    n = len(descs)
+    exp = np.ascontiguousarray(np.asarray(expected, dtype=np.uint32))
+    if exp.size != n:
+        raise ValueError("expected must have one entry per item")
+    out_v = np.zeros(n, dtype=np.uint32)
+    ok = np.zeros(n, dtype=np.uint8)
+    mis = _u64(0)
+    _check(lib.h3c_batch_verify(descs.ctypes.data, exp.ctypes.data, n, out_v.ctypes.data, ok.ctypes.data,
+                                ctypes.addressof(mis), _stream_handle(stream)))
+    del keep
+    return out_v, ok.astype(bool), int(mis.value)
+
+
+def device_batch_combine(c1, c2, len2, out, type_: int = ChecksumType.CRC32C, stream=None) -> None:
+    """out[i] = folly::crc32c_combine(c1[i], c2[i], len2[i]) on device (torch cuda tensors)."""
+    n = c1.numel()
+    _check(lib.h3c_batch_combine(int(type_), c1.data_ptr(), c2.data_ptr(), len2.data_ptr(), n, out.data_ptr(),
+                                 _stream_handle(stream)))
+
+
+def fill_splitmix(base, chunk_len: int, nchunks: int, stride: int, seed: int, first_chunk: int = 0,
+                  stream=None) -> None:
+    """Bench/test utility: the same splitmix64 chunk generator as the oracle, written in HBM."""
+    ptr = base if isinstance(base, int) else base.data_ptr()
+    _check(lib.h3c_fill_splitmix(ptr, chunk_len, nchunks, stride, seed, first_chunk, _stream_handle(stream)))
+
+
+def profile_enable(on: bool = True) -> None:
+    lib.h3c_profile_enable(1 if on else 0)
+
+
+def profile_read(reset: bool = False) -> Tuple[float, int, int]:
+    ms, launches, nbytes = ctypes.c_double(0), _u64(0), _u64(0)
+    _check(lib.h3c_profile_read(ctypes.byref(ms), ctypes.byref(launches), ctypes.byref(nbytes), 1 if reset else 0))
+    return ms.value, int(launches.value), int(nbytes.value)
+
+
+class Plan:
+    """Device-resident descriptor set reused across create/verify runs (scrub, resync)."""
+
+    def __init__(self, descs: np.ndarray, device: int):
+        self._h = _vp()
+        self.n = len(descs)
+        self.device = device
+        self._descs = descs
+        _check(lib.h3c_plan_create(descs.ctypes.data, self.n, device, ctypes.byref(self._h)))
+        self.bytes = int(lib.h3c_plan_bytes(self._h))
+
+    @classmethod
+    def uniform(cls, base_ptr: int, chunk_len: int, nchunks: int, stride: Optional[int] = None,
+                start: int = 0xFFFFFFFF, type_: int = ChecksumType.CRC32C, device: int = 0) -> "Plan":
+        stride = chunk_len if stride is None else stride
+        d = np.zeros(nchunks, dtype=DESC_DTYPE)
+        d["ptr"] = base_ptr + np.arange(nchunks, dtype=np.uint64) * np.uint64(stride)
+        d["len"] = chunk_len
+        d["start_raw"] = start & 0xFFFFFFFF
+        d["type"] = int(type_)
+        d["mem"] = int(MemKind.DEVICE)
+        return cls(d, device)
+
+    def run(self, out_raw, expected=None, ok=None, mismatch=None, stream=None) -> None:
+        _check(lib.h3c_plan_run(
+            self._h,
+            expected.data_ptr() if expected is not None else None,
+            out_raw.data_ptr(),
+            ok.data_ptr() if ok is not None else None,
+            mismatch.data_ptr() if mismatch is not None else None,
+            _stream_handle(stream),
+        ))
+
+    def close(self) -> None:
+        if self._h:
+            lib.h3c_plan_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------- ChecksumInfo mirror
+
+
+@dataclass
+class ChecksumInfo:
+    """``hf3fs::storage::ChecksumInfo`` (Common.h:113-201): {type u8, value u32 raw}."""
+
+    type: ChecksumType = ChecksumType.NONE
+    value: int = 0
+
+    kChunkSize = 1 << 20  # Common.h:118
+
+    @staticmethod
+    def create(type_: int, data, length: Optional[int] = None, starting_checksum: int = 0xFFFFFFFF,
+               stream=None) -> "ChecksumInfo":
+        """Common.h:146-177: NONE -> {NONE,0}; empty -> {type, start}; null with length>0 -> {NONE,0}."""
+        t, v = batch_create([(data, length, starting_checksum, int(type_))], int(type_), starting_checksum, stream)
+        return ChecksumInfo(ChecksumType(int(t[0])), int(v[0]))
+
+    def combine(self, o: "ChecksumInfo", length: int) -> None:
+        """Common.h:179-198.  Raises EngineError(kChecksumMismatch) on a type mismatch."""
+        if self.type != ChecksumType.NONE and self.type != o.type:
+            raise EngineError(StatusCode.kChecksumMismatch, f"different type {self} != {o}")
+        if length == 0:
+            return
+        if self.type == ChecksumType.NONE:
+            self.type, self.value = ChecksumType(o.type), o.value
+        elif self.type == ChecksumType.CRC32C:
+            self.value = crc32c_combine(~self.value & 0xFFFFFFFF, o.value, length)
+        elif self.type == ChecksumType.CRC32:
+            self.value = crc32_combine(~self.value & 0xFFFFFFFF, o.value, length)
+
+    def __str__(self) -> str:  # Common.h:768-773
+        return f"{ChecksumType(self.type).name}#{(~self.value) & 0xFFFFFFFF:08X}"

@@ -1,0 +1,131 @@
+/*
+ * h3c_crc.h -- C ABI of the MI355X batched chunk-checksum engine for 3FS.
+ *
+ * Drop-in boundary for the checksum path of the 3FS storage service.  Every
+ * entry point names the reference interface it replaces (paths relative to the
+ * MingWangSong/3FS checkout).  Values use folly's "raw" register convention:
+ * init ~0 by default, no final XOR (std CRC32C = ~raw).
+ *
+ *   folly::crc32c(const uint8_t*, size_t, uint32_t start = ~0U)
+ *       called at src/fbs/storage/Common.h:158
+ *   folly::crc32c_combine(uint32_t, uint32_t, size_t)
+ *       called at src/fbs/storage/Common.h:191
+ *   folly::crc32 / crc32_combine          src/fbs/storage/Common.h:161,195
+ *   ChecksumInfo::create(type, buf, len, start)  src/fbs/storage/Common.h:146-177
+ *   ChecksumInfo::combine(o, len)                src/fbs/storage/Common.h:179-198
+ *   ChunkReplica::update payload verify          src/storage/store/ChunkReplica.cc:193-207
+ *   AioReadJob::setResult (compute/recalculate)  src/storage/aio/BatchReadJob.cc:24-55
+ *
+ * No torch types appear here: plain pointers and sizes.  Streams are
+ * hipStream_t passed as void* (NULL = the device's null stream).
+ *
+ * Thread safety: every function may be called concurrently from many host
+ * threads (the reference calls the CPU path from 32 AIO + 32 update threads,
+ * src/storage/aio/AioReadWorker.h:27, src/storage/update/UpdateWorker.h:15).
+ * Global state is limited to immutable per-device tables built once.
+ */
+#ifndef H3C_CRC_H
+#define H3C_CRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ChecksumType, src/fbs/storage/Common.h:66-70 */
+enum h3c_type { H3C_TYPE_NONE = 0, H3C_TYPE_CRC32C = 1, H3C_TYPE_CRC32 = 2 };
+
+/* Where a descriptor's payload lives. */
+enum h3c_mem { H3C_MEM_DEVICE = 0, H3C_MEM_HOST_PINNED = 1, H3C_MEM_HOST_PAGEABLE = 2 };
+
+/* Return codes (mapped to the reference's StatusCode values). */
+enum h3c_status {
+  H3C_OK = 0,
+  H3C_ERR_INVALID_ARG = 3,            /* StatusCode::kInvalidArg */
+  H3C_ERR_CHUNK_READ_FAILED = 4010,   /* StorageCode::kChunkReadFailed, StatusCodeDetails.h:160 */
+  H3C_ERR_CHECKSUM_MISMATCH = 4080,   /* StorageCode::kChecksumMismatch, StatusCodeDetails.h:186 */
+  H3C_ERR_HIP = 9001,                 /* HIP runtime failure (h3c_last_error() has text) */
+  H3C_ERR_NO_DEVICE = 9002
+};
+
+/* One chunk payload.  `start_raw` is ChecksumInfo::create's startingChecksum
+ * (~0U for a fresh checksum).  `type` is an h3c_type, `mem` an h3c_mem. */
+typedef struct h3c_desc {
+  const void *ptr;
+  uint64_t len;
+  uint32_t start_raw;
+  uint8_t type;
+  uint8_t mem;
+  uint16_t reserved;
+} h3c_desc;
+
+/* ---- scalar host arithmetic (combine is O(log n) GF(2) work, no payload) ---- */
+
+/* folly::crc32c_combine (Common.h:191): shift(c1, len2) ^ c2. */
+uint32_t h3c_crc32c_combine(uint32_t c1, uint32_t c2, uint64_t len2);
+/* folly::crc32_combine (Common.h:195), IEEE polynomial. */
+uint32_t h3c_crc32_combine(uint32_t c1, uint32_t c2, uint64_t len2);
+/* register advanced over `nbytes` zero bytes: crc * x^(8*nbytes) mod P. */
+uint32_t h3c_crc32c_shift(uint32_t crc, uint64_t nbytes);
+
+/* ---- engine lifetime ---- */
+
+int h3c_device_count(void);
+/* Builds the per-device constant tables.  Idempotent, thread-safe.  Every
+ * other GPU entry point calls it implicitly for the current device. */
+int h3c_init(int device);
+const char *h3c_last_error(void); /* thread-local text of the last failure */
+
+/* ---- synchronous batch API (ChecksumInfo semantics, host result arrays) ---- */
+
+/* ChecksumInfo::create for each descriptor (Common.h:146-177):
+ * NONE -> {NONE,0}; len==0 -> {type,start_raw}; ptr==NULL && len>0 -> {NONE,0}.
+ * Device-memory payloads are read in place; host payloads are staged.
+ * Blocks until results are in out_type/out_raw (host arrays, n entries). */
+int h3c_batch_create(const h3c_desc *d, size_t n, uint8_t *out_type, uint32_t *out_raw, void *stream);
+
+/* Recompute and compare against expected_raw (ChunkReplica.cc:193-207,
+ * BatchReadJob.cc:43-54): ok[i] = (create(d[i]) == {d[i].type, expected_raw[i]}).
+ * *n_mismatch receives the count of ok==0.  Returns H3C_OK even when some
+ * chunks mismatch; per-chunk status is in ok[]. */
+int h3c_batch_verify(const h3c_desc *d, const uint32_t *expected_raw, size_t n, uint32_t *out_raw, uint8_t *ok,
+                     uint64_t *n_mismatch, void *stream);
+
+/* ---- asynchronous plan API (device-resident descriptors and results) ---- */
+
+typedef struct h3c_plan h3c_plan;
+
+/* Upload descriptors (all H3C_MEM_DEVICE, on `device`) once; reuse the plan
+ * for repeated create/verify of the same chunk set (scrub / resync). */
+int h3c_plan_create(const h3c_desc *d, size_t n, int device, h3c_plan **out);
+/* Enqueue on `stream`: out_raw_dev[i] (device, n u32).  When expected_raw_dev
+ * is non-NULL also ok_dev[i] (device, n u8) and *mismatch_dev (device u32,
+ * incremented, caller zeroes).  Nothing is synchronised. */
+int h3c_plan_run(h3c_plan *p, const uint32_t *expected_raw_dev, uint32_t *out_raw_dev, uint8_t *ok_dev,
+                 uint32_t *mismatch_dev, void *stream);
+uint64_t h3c_plan_bytes(const h3c_plan *p);
+void h3c_plan_destroy(h3c_plan *p);
+
+/* ---- batched combine on device (folly::crc32c_combine per element) ---- */
+/* out[i] = combine(c1[i], c2[i], len2[i]); all arrays device-resident. */
+int h3c_batch_combine(uint8_t type, const uint32_t *c1_dev, const uint32_t *c2_dev, const uint64_t *len2_dev,
+                      size_t n, uint32_t *out_dev, void *stream);
+
+/* ---- utilities for benches/tests (not on the reference path) ---- */
+
+/* chunk i at base + i*stride gets u64 words splitmix64(seed ^ ((first_chunk+i)<<40) ^ k). */
+int h3c_fill_splitmix(void *base_dev, uint64_t chunk_len, uint64_t nchunks, uint64_t stride, uint64_t seed,
+                      uint64_t first_chunk, void *stream);
+
+/* When enabled, the engine brackets every segment-CRC kernel launch with HIP
+ * events on the launch stream.  h3c_profile_read synchronises those events and
+ * returns the summed kernel time, launch count and payload bytes. */
+void h3c_profile_enable(int on);
+int h3c_profile_read(double *seg_kernel_ms, uint64_t *seg_launches, uint64_t *seg_bytes, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* H3C_CRC_H */

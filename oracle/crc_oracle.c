@@ -1,0 +1,401 @@
+/*
+ * crc_oracle.c -- TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).
+ *
+ * A plain-C restatement of the reference's checksum path.  Nothing in the
+ * product (3fs_amd/, include/) links this file; the HIP engine must fail
+ * loudly rather than fall back to it.
+ *
+ * Sources restated (paths relative to the reference checkout):
+ *   folly::crc32c / crc32c_combine  -- external (third_party/folly is an empty
+ *       submodule, .gitmodules:4-6; pin unrecoverable).  Semantics pinned by the
+ *       reference's own call sites: src/fbs/storage/Common.h:158,191 and the
+ *       combine identity in tests/common/utils/TestFolly.cc:9-18.
+ *   ChecksumInfo::create / combine  -- src/fbs/storage/Common.h:113-201
+ *   ChunkReplica::updateChecksum    -- src/storage/store/ChunkReplica.cc:319-394
+ *   ChunkFileView::checksum         -- src/storage/store/ChunkFileView.cc:92-104
+ *   AioReadJob::setResult checksum  -- src/storage/aio/BatchReadJob.cc:24-55
+ *
+ * Three independent CRC mechanisms (bitwise, byte table, x86 SSE4.2 crc32
+ * instruction) cross-check one another; tests pin them to the standard KATs
+ * and to the constants logged in tests/common/utils/TestFolly.cc:20-21.
+ */
+#include "crc_oracle.h"
+
+#include <nmmintrin.h>
+#include <pthread.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ */
+/* A1: register-level CRC (folly "raw" convention: no final XOR).      */
+/* ------------------------------------------------------------------ */
+
+uint32_t orc_crc32c_bitwise(const uint8_t *d, size_t n, uint32_t start) {
+  uint32_t c = start;
+  for (size_t i = 0; i < n; ++i) {
+    c ^= d[i];
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (ORC_POLY_CRC32C & (0u - (c & 1u)));
+  }
+  return c;
+}
+
+static uint32_t g_tab_c[256], g_tab_ieee[256];
+static uint32_t g_long_shift[4][256], g_short_shift[4][256];
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+
+#define ORC_LONG 8192
+#define ORC_SHORT 256
+
+static void build_byte_table(uint32_t *t, uint32_t poly) {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (poly & (0u - (c & 1u)));
+    t[i] = c;
+  }
+}
+
+static void build_shift_table(uint32_t t[4][256], uint64_t nbytes) {
+  uint32_t m = orc_xpow8n(nbytes, ORC_POLY_CRC32C);
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t b = 0; b < 256; ++b) t[k][b] = orc_gf_mul(b << (8 * k), m, ORC_POLY_CRC32C);
+}
+
+static void init_tables(void) {
+  build_byte_table(g_tab_c, ORC_POLY_CRC32C);
+  build_byte_table(g_tab_ieee, ORC_POLY_CRC32);
+  build_shift_table(g_long_shift, ORC_LONG);
+  build_shift_table(g_short_shift, ORC_SHORT);
+}
+
+uint32_t orc_crc32c_table(const uint8_t *d, size_t n, uint32_t start) {
+  pthread_once(&g_once, init_tables);
+  uint32_t c = start;
+  for (size_t i = 0; i < n; ++i) c = g_tab_c[(c ^ d[i]) & 0xFFu] ^ (c >> 8);
+  return c;
+}
+
+uint32_t orc_crc32_table(const uint8_t *d, size_t n, uint32_t start) {
+  pthread_once(&g_once, init_tables);
+  uint32_t c = start;
+  for (size_t i = 0; i < n; ++i) c = g_tab_ieee[(c ^ d[i]) & 0xFFu] ^ (c >> 8);
+  return c;
+}
+
+uint32_t orc_crc32c_sse42(const uint8_t *d, size_t n, uint32_t start) {
+  uint64_t c = start;
+  while (n && ((uintptr_t)d & 7u)) {
+    c = _mm_crc32_u8((uint32_t)c, *d++);
+    --n;
+  }
+  for (; n >= 8; n -= 8, d += 8) {
+    uint64_t w;
+    memcpy(&w, d, 8);
+    c = _mm_crc32_u64(c, w);
+  }
+  while (n--) c = _mm_crc32_u8((uint32_t)c, *d++);
+  return (uint32_t)c;
+}
+
+static inline uint32_t shift_by_table(uint32_t t[4][256], uint32_t c) {
+  return t[0][c & 0xFFu] ^ t[1][(c >> 8) & 0xFFu] ^ t[2][(c >> 16) & 0xFFu] ^ t[3][c >> 24];
+}
+
+/* Three independent crc32q dependency chains over adjacent blocks, merged by
+ * register shifts -- the structure of folly's SSE4.2 crc32c_hw path (the
+ * instruction has 3-cycle latency / 1-cycle throughput, so 3 chains saturate
+ * it).  Block sizes 8 KiB then 256 B. */
+static inline const uint8_t *three_way(const uint8_t *d, size_t *n, uint64_t *c0p, size_t blk,
+                                       uint32_t t[4][256]) {
+  uint64_t c0 = *c0p;
+  while (*n >= 3 * blk) {
+    uint64_t c1 = 0, c2 = 0;
+    const uint8_t *end = d + blk;
+    do {
+      uint64_t w0, w1, w2;
+      memcpy(&w0, d, 8);
+      memcpy(&w1, d + blk, 8);
+      memcpy(&w2, d + 2 * blk, 8);
+      c0 = _mm_crc32_u64(c0, w0);
+      c1 = _mm_crc32_u64(c1, w1);
+      c2 = _mm_crc32_u64(c2, w2);
+      d += 8;
+    } while (d < end);
+    c0 = shift_by_table(t, (uint32_t)c0) ^ (uint32_t)c1;
+    c0 = shift_by_table(t, (uint32_t)c0) ^ (uint32_t)c2;
+    d += 2 * blk;
+    *n -= 3 * blk;
+  }
+  *c0p = c0;
+  return d;
+}
+
+uint32_t orc_crc32c_sse42_3way(const uint8_t *d, size_t n, uint32_t start) {
+  pthread_once(&g_once, init_tables);
+  uint64_t c = start;
+  while (n && ((uintptr_t)d & 7u)) {
+    c = _mm_crc32_u8((uint32_t)c, *d++);
+    --n;
+  }
+  d = three_way(d, &n, &c, ORC_LONG, g_long_shift);
+  d = three_way(d, &n, &c, ORC_SHORT, g_short_shift);
+  for (; n >= 8; n -= 8, d += 8) {
+    uint64_t w;
+    memcpy(&w, d, 8);
+    c = _mm_crc32_u64(c, w);
+  }
+  while (n--) c = _mm_crc32_u8((uint32_t)c, *d++);
+  return (uint32_t)c;
+}
+
+/* ------------------------------------------------------------------ */
+/* A2: GF(2)[x]/P arithmetic in the reflected representation.          */
+/* bit 31 holds the x^0 coefficient; multiplying by x is a right shift */
+/* with conditional reduction by the reflected polynomial.             */
+/* ------------------------------------------------------------------ */
+
+uint32_t orc_gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
+  uint32_t p = 0;
+  for (int i = 0; i < 32; ++i) {
+    if (a & (0x80000000u >> i)) p ^= b;
+    b = (b >> 1) ^ (poly & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+uint32_t orc_xpow8n(uint64_t n, uint32_t poly) {
+  uint32_t result = 0x80000000u; /* x^0 */
+  uint32_t base = 0x00800000u;   /* x^8 */
+  while (n) {
+    if (n & 1u) result = orc_gf_mul(result, base, poly);
+    base = orc_gf_mul(base, base, poly);
+    n >>= 1;
+  }
+  return result;
+}
+
+uint32_t orc_shift(uint32_t crc, uint64_t nbytes, uint32_t poly) {
+  return orc_gf_mul(crc, orc_xpow8n(nbytes, poly), poly);
+}
+
+/* folly::crc32c_combine(c1, c2, len2): the register after appending len2
+ * bytes whose init-0 register is c2 to a stream whose register is c1.
+ * Pinned by tests/common/utils/TestFolly.cc:16-18. */
+uint32_t orc_crc32c_combine(uint32_t c1, uint32_t c2, uint64_t len2) {
+  return orc_shift(c1, len2, ORC_POLY_CRC32C) ^ c2;
+}
+
+uint32_t orc_crc32_combine(uint32_t c1, uint32_t c2, uint64_t len2) {
+  return orc_shift(c1, len2, ORC_POLY_CRC32) ^ c2;
+}
+
+/* ------------------------------------------------------------------ */
+/* A3/A4: ChecksumInfo (src/fbs/storage/Common.h:146-198).             */
+/* ------------------------------------------------------------------ */
+
+#define ORC_KCHUNK (1u << 20) /* ChecksumInfo::kChunkSize, Common.h:118 */
+
+void orc_checksum_create(uint8_t type, const uint8_t *buf, uint64_t len, uint32_t start, uint8_t *out_type,
+                         uint32_t *out_value) {
+  /* Common.h:150: NONE -> {NONE, 0} */
+  if (type == ORC_NONE) {
+    *out_type = ORC_NONE;
+    *out_value = 0;
+    return;
+  }
+  /* MemoryDataIterator (Common.h:126-144) hands out <=1 MiB pieces; a null
+   * buffer with length>0 yields no bytes -> iterBytes != length -> NONE
+   * (Common.h:166-169). */
+  if (buf == NULL && len > 0) {
+    *out_type = ORC_NONE;
+    *out_value = 0;
+    return;
+  }
+  uint32_t v = start;
+  uint64_t off = 0;
+  while (off < len) {
+    uint64_t piece = len - off < ORC_KCHUNK ? len - off : ORC_KCHUNK;
+    if (type == ORC_CRC32C)
+      v = orc_crc32c_sse42(buf + off, piece, v); /* Common.h:158 */
+    else
+      v = orc_crc32_table(buf + off, piece, v); /* Common.h:161 */
+    off += piece;
+  }
+  *out_type = type;
+  *out_value = v;
+}
+
+int orc_checksum_combine(uint8_t *type, uint32_t *value, uint8_t o_type, uint32_t o_value, uint64_t length) {
+  /* Common.h:180-183 */
+  if (*type != ORC_NONE && *type != o_type) return ORC_ERR_CHECKSUM_MISMATCH;
+  if (length == 0) return ORC_OK; /* Common.h:184 */
+  switch (*type) {
+    case ORC_NONE: /* Common.h:186-188 */
+      *type = o_type;
+      *value = o_value;
+      return ORC_OK;
+    case ORC_CRC32C: /* Common.h:190-192 */
+      *value = orc_crc32c_combine(~*value, o_value, length);
+      return ORC_OK;
+    case ORC_CRC32: /* Common.h:194-196 */
+      *value = orc_crc32_combine(~*value, o_value, length);
+      return ORC_OK;
+  }
+  return ORC_OK;
+}
+
+/* ChunkFileView::checksum(type, size, offset) over an in-memory chunk
+ * (ChunkFileView.cc:92-104): create() over [offset, offset+size); a NONE
+ * result maps to kChunkReadFailed. */
+static int view_checksum(uint8_t type, const uint8_t *chunk, uint64_t size, uint64_t offset, uint8_t *t,
+                         uint32_t *v) {
+  orc_checksum_create(type, size ? chunk + offset : NULL, size, ~0u, t, v);
+  if (*t == ORC_NONE) return ORC_ERR_CHUNK_READ_FAILED;
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* A8: ChunkReplica::updateChecksum (ChunkReplica.cc:319-394).          */
+/* ------------------------------------------------------------------ */
+int orc_update_checksum(orc_chunk_meta *meta, orc_write_io wio, uint32_t chunk_size_before_write, int is_append_write,
+                        const uint8_t *chunk_after_write) {
+  uint8_t ctype = meta->checksum_type;
+  uint32_t cvalue = meta->checksum_value;
+  int combine_checksum = chunk_size_before_write > 0 && is_append_write; /* :326 */
+
+  if (wio.is_truncate_or_extend) { /* :328-332 */
+    orc_checksum_create(meta->checksum_type, NULL, 0, ~0u, &wio.checksum_type, &wio.checksum_value);
+    wio.offset = meta->size;
+    wio.length = 0;
+  }
+
+  if (wio.checksum_type == ORC_NONE || meta->size == 0) { /* :334-336 */
+    meta->checksum_value = 0;
+  } else if (wio.offset == 0 && wio.length == meta->size) { /* :337-339 reuse */
+    meta->checksum_value = wio.checksum_value;
+  } else if (wio.checksum_type == ctype && combine_checksum) { /* :340-355 append */
+    int rc = orc_checksum_combine(&ctype, &cvalue, wio.checksum_type, wio.checksum_value, wio.length);
+    if (rc) return rc;
+    meta->checksum_value = cvalue;
+  } else { /* :356-390 prefix / write / suffix */
+    uint8_t pt, st;
+    uint32_t pv, sv;
+    int rc = view_checksum(wio.checksum_type, chunk_after_write, wio.offset, 0, &pt, &pv);
+    if (rc) return rc;
+    uint32_t end = wio.offset + wio.length;
+    uint32_t suffix_start = end < meta->size ? end : meta->size;
+    uint32_t suffix_len = meta->size - suffix_start;
+    rc = view_checksum(wio.checksum_type, chunk_after_write, suffix_len, suffix_start, &st, &sv);
+    if (rc) return rc;
+    orc_checksum_combine(&pt, &pv, wio.checksum_type, wio.checksum_value, wio.length);
+    orc_checksum_combine(&pt, &pv, st, sv, suffix_len);
+    meta->checksum_value = pv;
+  }
+  meta->checksum_type = wio.checksum_type; /* :392 */
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* A7: AioReadJob::setResult (BatchReadJob.cc:24-55).                   */
+/* ------------------------------------------------------------------ */
+int orc_read_result_checksum(uint8_t batch_type, uint8_t chunk_type, uint32_t chunk_value, uint32_t chunk_len,
+                             uint32_t read_offset, uint32_t read_len, const uint8_t *read_data, int recalculate,
+                             const uint8_t *full_chunk, uint8_t *out_type, uint32_t *out_value) {
+  if (batch_type == ORC_NONE) { /* :28-29 */
+    *out_type = ORC_NONE;
+    *out_value = 0;
+  } else if (batch_type == chunk_type && read_offset == 0 && read_len == chunk_len) { /* :30-31 reuse */
+    *out_type = chunk_type;
+    *out_value = chunk_value;
+  } else { /* :33-34 compute */
+    orc_checksum_create(batch_type, read_data, read_len, ~0u, out_type, out_value);
+  }
+  if (recalculate && read_offset == 0 && read_len == chunk_len) { /* :43-54 */
+    uint8_t rt;
+    uint32_t rv;
+    orc_checksum_create(chunk_type, full_chunk, read_len, ~0u, &rt, &rv);
+    if (rt != chunk_type || rv != chunk_value) return ORC_ERR_CHECKSUM_MISMATCH;
+  }
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* Synthetic data: u64 w[k] = splitmix64(seed ^ (chunk_idx << 40) ^ k),  */
+/* little-endian.                                        */
+/* ------------------------------------------------------------------ */
+uint64_t orc_splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+void orc_fill_splitmix(uint8_t *out, uint64_t len, uint64_t seed, uint64_t chunk_idx) {
+  uint64_t key = seed ^ (chunk_idx << 40);
+  uint64_t nw = len / 8;
+  for (uint64_t k = 0; k < nw; ++k) {
+    uint64_t w = orc_splitmix64(key ^ k);
+    memcpy(out + 8 * k, &w, 8);
+  }
+  if (len % 8) {
+    uint64_t w = orc_splitmix64(key ^ nw);
+    memcpy(out + 8 * nw, &w, len % 8);
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* Batch helper (CPU baseline): equal-size chunks, optional threads.    */
+/* variant 0 = folly-faithful 3-way crc32q, 1 = single crc32q stream,   */
+/* 2 = byte table.  Each chunk goes through ChecksumInfo::create's 1 MiB */
+/* iterator pieces, exactly as Common.h:146-172 chains folly::crc32c.    */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  const uint8_t *base;
+  uint64_t chunk_len, lo, hi;
+  uint32_t start;
+  int variant;
+  uint32_t *out;
+} orc_job;
+
+static uint32_t chunk_crc(const uint8_t *p, uint64_t len, uint32_t start, int variant) {
+  uint32_t v = start;
+  for (uint64_t off = 0; off < len; off += ORC_KCHUNK) {
+    uint64_t piece = len - off < ORC_KCHUNK ? len - off : ORC_KCHUNK;
+    if (variant == 0)
+      v = orc_crc32c_sse42_3way(p + off, piece, v);
+    else if (variant == 1)
+      v = orc_crc32c_sse42(p + off, piece, v);
+    else
+      v = orc_crc32c_table(p + off, piece, v);
+  }
+  return v;
+}
+
+static void *batch_worker(void *arg) {
+  orc_job *j = (orc_job *)arg;
+  for (uint64_t i = j->lo; i < j->hi; ++i)
+    j->out[i] = chunk_crc(j->base + i * j->chunk_len, j->chunk_len, j->start, j->variant);
+  return NULL;
+}
+
+void orc_batch_crc32c(const uint8_t *base, uint64_t chunk_len, uint64_t nchunks, uint32_t start, int nthreads,
+                      int variant, uint32_t *out) {
+  pthread_once(&g_once, init_tables);
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  orc_job jobs[256];
+  for (int t = 0; t < nthreads; ++t) {
+    jobs[t].base = base;
+    jobs[t].chunk_len = chunk_len;
+    jobs[t].lo = nchunks * (uint64_t)t / (uint64_t)nthreads;
+    jobs[t].hi = nchunks * (uint64_t)(t + 1) / (uint64_t)nthreads;
+    jobs[t].start = start;
+    jobs[t].variant = variant;
+    jobs[t].out = out;
+  }
+  if (nthreads == 1) {
+    batch_worker(&jobs[0]);
+    return;
+  }
+  for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}

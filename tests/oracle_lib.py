@@ -1,0 +1,119 @@
+"""ctypes access to the CPU oracle (oracle/crc_oracle.c) -- TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load the
+oracle; it is the checker, never the thing measured or shipped.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+
+NONE, CRC32C, CRC32 = 0, 1, 2
+POLY_CRC32C = 0x82F63B78
+POLY_CRC32 = 0xEDB88320
+
+
+def load():
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    L = ctypes.CDLL(ORACLE_SO)
+    u8, u32, u64, vp, sz = ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t
+    for f in ("orc_crc32c_bitwise", "orc_crc32c_table", "orc_crc32c_sse42", "orc_crc32c_sse42_3way",
+              "orc_crc32_table"):
+        getattr(L, f).restype = u32
+        getattr(L, f).argtypes = [vp, sz, u32]
+    L.orc_gf_mul.restype = u32
+    L.orc_gf_mul.argtypes = [u32, u32, u32]
+    L.orc_xpow8n.restype = u32
+    L.orc_xpow8n.argtypes = [u64, u32]
+    L.orc_shift.restype = u32
+    L.orc_shift.argtypes = [u32, u64, u32]
+    L.orc_crc32c_combine.restype = u32
+    L.orc_crc32c_combine.argtypes = [u32, u32, u64]
+    L.orc_crc32_combine.restype = u32
+    L.orc_crc32_combine.argtypes = [u32, u32, u64]
+    L.orc_checksum_create.restype = None
+    L.orc_checksum_create.argtypes = [u8, vp, u64, u32, ctypes.POINTER(u8), ctypes.POINTER(u32)]
+    L.orc_checksum_combine.restype = ctypes.c_int
+    L.orc_checksum_combine.argtypes = [ctypes.POINTER(u8), ctypes.POINTER(u32), u8, u32, u64]
+    L.orc_splitmix64.restype = u64
+    L.orc_splitmix64.argtypes = [u64]
+    L.orc_fill_splitmix.restype = None
+    L.orc_fill_splitmix.argtypes = [vp, u64, u64, u64]
+    L.orc_batch_crc32c.restype = None
+    L.orc_batch_crc32c.argtypes = [vp, u64, u64, u32, ctypes.c_int, ctypes.c_int, vp]
+    return L
+
+
+class ChunkMeta(ctypes.Structure):
+    _fields_ = [("size", ctypes.c_uint32), ("checksum_type", ctypes.c_uint8), ("checksum_value", ctypes.c_uint32)]
+
+
+class WriteIO(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint32), ("length", ctypes.c_uint32), ("checksum_type", ctypes.c_uint8),
+                ("checksum_value", ctypes.c_uint32), ("is_truncate_or_extend", ctypes.c_uint8)]
+
+
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        _L = load()
+        _L.orc_update_checksum.restype = ctypes.c_int
+        _L.orc_update_checksum.argtypes = [ctypes.POINTER(ChunkMeta), WriteIO, ctypes.c_uint32, ctypes.c_int,
+                                           ctypes.c_void_p]
+    return _L
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data if a.size else None
+
+
+def crc32c(data, start=0xFFFFFFFF, mech="sse42"):
+    a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    return getattr(lib(), f"orc_crc32c_{mech}")(_ptr(a), a.size, start & 0xFFFFFFFF)
+
+
+def crc32(data, start=0xFFFFFFFF):
+    a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    return lib().orc_crc32_table(_ptr(a), a.size, start & 0xFFFFFFFF)
+
+
+def create(type_, data, length=None, start=0xFFFFFFFF):
+    """ChecksumInfo::create restatement -> (type, value)."""
+    t, v = ctypes.c_uint8(0), ctypes.c_uint32(0)
+    if data is None:
+        lib().orc_checksum_create(type_, None, length or 0, start & 0xFFFFFFFF, ctypes.byref(t), ctypes.byref(v))
+    else:
+        a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        n = a.size if length is None else length
+        lib().orc_checksum_create(type_, _ptr(a), n, start & 0xFFFFFFFF, ctypes.byref(t), ctypes.byref(v))
+    return t.value, v.value
+
+
+def combine(t, v, ot, ov, length):
+    """ChecksumInfo::combine restatement -> (rc, type, value)."""
+    tt, vv = ctypes.c_uint8(t), ctypes.c_uint32(v)
+    rc = lib().orc_checksum_combine(ctypes.byref(tt), ctypes.byref(vv), ot, ov & 0xFFFFFFFF, length)
+    return rc, tt.value, vv.value
+
+
+def splitmix_bytes(length, seed, chunk_idx):
+    out = np.empty(length, dtype=np.uint8)
+    lib().orc_fill_splitmix(_ptr(out), length, seed, chunk_idx)
+    return out
+
+
+def update_checksum(meta: dict, wio: dict, size_before: int, is_append: bool, chunk_after: np.ndarray):
+    m = ChunkMeta(meta["size"], meta["type"], meta["value"])
+    w = WriteIO(wio["offset"], wio["length"], wio["type"], wio["value"] & 0xFFFFFFFF, int(wio.get("trunc_ext", 0)))
+    rc = lib().orc_update_checksum(ctypes.byref(m), w, size_before, int(is_append), _ptr(chunk_after))
+    return rc, {"size": m.size, "type": m.checksum_type, "value": m.checksum_value}

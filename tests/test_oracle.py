@@ -1,0 +1,141 @@
+"""The CPU oracle, pinned before anything is checked against it (CPU only).
+
+Pins: standard CRC-32C / CRC-32 check values, the constants logged at
+tests/common/utils/TestFolly.cc:20-21 of the reference, the combine identity of
+TestFolly.cc:9-18, three independent CRC mechanisms agreeing, and the
+whole-chunk CRC after partial writes (TestStorageClientInterface.cc:435).
+"""
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+from golden.gen_golden import materialize
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CRC_VECTORS = json.load(open(os.path.join(HERE, "golden", "crc_vectors.json")))
+COMBINE_VECTORS = json.load(open(os.path.join(HERE, "golden", "combine_vectors.json")))
+UPDATE_TRACES = json.load(open(os.path.join(HERE, "golden", "update_traces.json")))
+MASK = 0xFFFFFFFF
+
+
+def test_standard_check_values():
+    assert orc.crc32c(b"123456789") == 0x1CF96D7C  # raw
+    assert (~orc.crc32c(b"123456789")) & MASK == 0xE3069283  # std
+    assert (~orc.crc32(b"123456789")) & MASK == 0xCBF43926
+
+
+def test_testfolly_constants():
+    # TestFolly.cc:20-21 log ~0x14298C12 (1 MiB of zeros) and ~0x527D5351 (one zero byte).
+    assert orc.crc32c(bytes(1 << 20)) == (~0x14298C12) & MASK
+    assert orc.crc32c(bytes(1)) == (~0x527D5351) & MASK
+    # ...and combine them the way the test does: crc32c_combine(~crc1, crc2, 1)
+    out = orc.lib().orc_crc32c_combine(0x14298C12, (~0x527D5351) & MASK, 1)
+    assert out == orc.crc32c(bytes((1 << 20) + 1), 0xFFFFFFFF) ^ 0  # raw of 1 MiB + 1 zero bytes
+
+
+def test_testfolly_combine_identity():
+    # TestFolly.cc:9-18: combine(crc32c(a,0), crc32c(b,0), |b|) == crc32c(b, start=crc32c(a,0))
+    a, b = b"hello", b"world"
+    c1, c2 = orc.crc32c(a, 0), orc.crc32c(b, 0)
+    assert orc.lib().orc_crc32c_combine(c1, c2, len(b)) == orc.crc32c(b, c1)
+
+
+@pytest.mark.parametrize("case", CRC_VECTORS, ids=lambda c: c["name"])
+def test_golden_crc_vectors_all_mechanisms(case):
+    data = materialize(case)
+    start = case["start"]
+    want = case["crc32c_raw"]
+    assert orc.crc32c(data, start, "table") == want
+    assert orc.crc32c(data, start, "sse42") == want
+    assert orc.crc32c(data, start, "sse42_3way") == want
+    if data.size <= (64 << 10):
+        assert orc.crc32c(data, start, "bitwise") == want
+    assert orc.crc32(data, start) == case["crc32_raw"]
+    if start == 0xFFFFFFFF and data.size <= (4 << 20):
+        assert (~case["crc32_raw"]) & MASK == zlib.crc32(data.tobytes())  # independent IEEE oracle
+    if "kat_crc32c_std" in case:
+        assert (~want) & MASK == case["kat_crc32c_std"]
+
+
+@pytest.mark.parametrize("v", COMBINE_VECTORS)
+def test_golden_combine_vectors(v):
+    assert orc.lib().orc_crc32c_combine(v["c1"], v["c2"], v["len2"]) == v["crc32c"]
+    assert orc.lib().orc_crc32_combine(v["c1"], v["c2"], v["len2"]) == v["crc32"]
+
+
+def test_combine_matches_concatenation_random():
+    rng = np.random.default_rng(1)
+    for _ in range(50):
+        na, nb = int(rng.integers(0, 5000)), int(rng.integers(0, 5000))
+        a = rng.integers(0, 256, na, dtype=np.uint8)
+        b = rng.integers(0, 256, nb, dtype=np.uint8)
+        s = int(rng.integers(0, 1 << 32))
+        ab = np.concatenate([a, b])
+        # raw(init s, A||B) == combine(raw(init s, A), crc0(B), |B|)
+        assert orc.lib().orc_crc32c_combine(orc.crc32c(a, s), orc.crc32c(b, 0), nb) == orc.crc32c(ab, s)
+        # ChecksumInfo::combine on ~0-start values yields raw(A||B) (Common.h:191)
+        rc, t, v = orc.combine(orc.CRC32C, orc.crc32c(a), orc.CRC32C, orc.crc32c(b), nb)
+        if nb:
+            assert rc == 0 and t == orc.CRC32C and v == orc.crc32c(ab)
+
+
+def test_checksum_info_create_semantics():
+    assert orc.create(orc.NONE, b"abc") == (orc.NONE, 0)  # Common.h:150
+    assert orc.create(orc.CRC32C, b"") == (orc.CRC32C, 0xFFFFFFFF)  # empty: {type, start}
+    assert orc.create(orc.CRC32C, b"", start=0x1234) == (orc.CRC32C, 0x1234)
+    assert orc.create(orc.CRC32C, None, 10) == (orc.NONE, 0)  # iterBytes != length (Common.h:166-169)
+    big = orc.splitmix_bytes((3 << 20) + 5, 7, 0)  # chained over 1 MiB iterator pieces
+    assert orc.create(orc.CRC32C, big) == (orc.CRC32C, orc.crc32c(big))
+    assert orc.create(orc.CRC32, big)[1] == orc.crc32(big)
+
+
+def test_checksum_info_combine_semantics():
+    assert orc.combine(orc.CRC32C, 5, orc.CRC32, 7, 10)[0] == 4080  # type mismatch (Common.h:180-183)
+    assert orc.combine(orc.CRC32C, 5, orc.CRC32C, 7, 0) == (0, orc.CRC32C, 5)  # length 0 no-op
+    assert orc.combine(orc.NONE, 0, orc.CRC32C, 7, 10) == (0, orc.CRC32C, 7)  # NONE receiver copies
+    assert orc.combine(orc.NONE, 0, orc.CRC32, 9, 0) == (0, orc.NONE, 0)  # length 0 first
+
+
+@pytest.mark.parametrize("trace", UPDATE_TRACES, ids=lambda t: f"{t['pattern']}_{t['chunk_size']}")
+def test_update_checksum_traces(trace):
+    """ChunkReplica::updateChecksum restated, replayed over the reference test's write shapes.
+
+    After every write the stored chunk checksum must equal crc32c(whole chunk)
+    (TestStorageClientInterface.cc:435)."""
+    chunk = np.zeros(0, dtype=np.uint8)
+    meta = {"size": 0, "type": orc.NONE, "value": 0}
+    for op in trace["ops"]:
+        off, ln = op["offset"], op["length"]
+        data = orc.splitmix_bytes(ln, op["seed"], op["widx"])
+        wt, wv = orc.create(orc.CRC32C, data)
+        assert wv == op["write_crc32c"]
+        size_before = chunk.size
+        is_append = off == size_before  # ChunkReplica.cc:246
+        if off + ln > chunk.size:
+            grown = np.zeros(off + ln, dtype=np.uint8)
+            grown[: chunk.size] = chunk
+            chunk = grown
+        chunk[off: off + ln] = data
+        meta["size"] = chunk.size
+        rc, meta = orc.update_checksum(meta, {"offset": off, "length": ln, "type": wt, "value": wv},
+                                       size_before, is_append, chunk)
+        assert rc == 0
+        assert meta["value"] == op["chunk_crc32c"] == orc.crc32c(chunk)
+
+
+def test_splitmix_generator_matches_python():
+    def sm(x):
+        x = (x + 0x9E3779B97F4A7C15) & ((1 << 64) - 1)
+        x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
+        x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & ((1 << 64) - 1)
+        return x ^ (x >> 31)
+
+    seed, chunk = 20250629, 5
+    got = orc.splitmix_bytes(45, seed, chunk)
+    words = [sm(seed ^ (chunk << 40) ^ k) for k in range(6)]
+    want = b"".join(w.to_bytes(8, "little") for w in words)[:45]
+    assert got.tobytes() == want
