@@ -30,6 +30,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -209,12 +210,15 @@ __device__ __forceinline__ void consume(Streams &st, uint4 v, const char *lb, ui
   st.s3 = row_step(st.s3 ^ v.w, lb, off_lo, off_hi);
 }
 
-constexpr int kUnroll = 4;  // rows in flight per batch (x2 with the prefetch)
+#ifndef H3C_UNROLL
+#define H3C_UNROLL 4
+#endif
+constexpr int kUnroll = H3C_UNROLL;  // rows in flight per batch (x2 with the prefetch)
 
 // init-0 CRC of bytes [S, E) (E > S), computed by one wavefront.
 __device__ uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const char *lb, uint32_t off_lo,
                                  uint32_t off_hi, const uint32_t fix[4], const PolyConsts *__restrict__ pc,
-                                 uint32_t poly) {
+                                 uint32_t poly, uint32_t dbg) {
   const uint64_t E16 = (E + 15) & ~uint64_t(15);
   const uint64_t S16 = S & ~uint64_t(15);
   const uint32_t K = (uint32_t)((E16 - S16 + kRowBytes - 1) / kRowBytes);
@@ -223,42 +227,45 @@ __device__ uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const ch
   Streams st{0, 0, 0, 0};
   // row 0 (masked)
   consume(st, load_masked(base, S, E), lb, off_lo, off_hi);
-  // Rows 1 .. K-2 lie fully inside [S, E).  They are read with buffer loads off a
-  // wave-uniform descriptor whose range ends at row K-1, so a prefetch past the
-  // plain rows returns zeros without touching memory; voffset = 16*lane, the row
-  // offset rides in soffset / the 12-bit immediate.  Two batches of kUnroll rows
-  // ping-pong: one is in flight while the other is consumed.
+  // Rows 1 .. K-2 lie fully inside [S, E).  They are read with saddr-form global
+  // loads: wave-uniform 64-bit row base in SGPRs + per-lane 32-bit offset 16*lane,
+  // so no per-row VGPR address arithmetic.  Prefetch rows are clamped to the last
+  // plain row (every load stays inside the segment; the few clamped re-reads at a
+  // segment's end hit in cache).  One batch of kUnroll rows is in flight while the
+  // previous batch is consumed.
   uint32_t r = 1;
   const uint32_t plain_end = K >= 2 ? K - 1 : 1;
-  if (r + kUnroll <= plain_end) {
-    const uint64_t row0 = __builtin_amdgcn_readfirstlane((uint32_t)(base - 16u * lane)) |
-                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((base - 16u * lane) >> 32)) << 32);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void *>(row0), (short)0, (int)((K - 1) * (uint32_t)kRowBytes), 0x00020000);
+  if (!(dbg & 1u) && r + kUnroll <= plain_end) {
+    // readfirstlane returns int: widen through uint32_t so the low half is not sign-extended.
+    const uint64_t row0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base - 16u * lane)) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((base - 16u * lane) >> 32))
+                           << 32);
+    typedef const char __attribute__((address_space(1))) *gcp;
+    const gcp gbase = (gcp)row0;
     const uint32_t voff = 16u * lane;
+    const uint32_t last = plain_end - 1;
     auto ld = [&](uint32_t row) -> uint4 {
-      const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, (int)(row * (uint32_t)kRowBytes), H3C_LOAD_AUX);
+      row = min(row, last);
+      const gcp rp = gbase + (uint64_t)row * kRowBytes;  // uniform (SGPR) part
+      const v4u v = *(gv4p)(rp + voff);                    // + per-lane 32-bit offset
       return make_uint4(v.x, v.y, v.z, v.w);
     };
-    uint4 a[kUnroll], b[kUnroll];
+    // NOTE: an explicit two-buffer ping-pong form of this loop (no copy) miscompiled
+    // under ROCm 7.2 hipcc -O3 at kUnroll=4 (wrong CRCs from the first pipelined
+    // row; correct at -O1 and at kUnroll=2); this copy form is correct at every
+    // setting tried and the copies are register renames.
+    uint4 a[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) a[u] = ld(r + u);
     for (;;) {
+      uint4 b[kUnroll];
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) b[u] = ld(r + kUnroll + u);
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) consume(st, a[u], lb, off_lo, off_hi);
       r += kUnroll;
-      if (r + kUnroll > plain_end) {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) a[u] = b[u];
-        break;
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) a[u] = ld(r + kUnroll + u);
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) consume(st, b[u], lb, off_lo, off_hi);
-      r += kUnroll;
+      for (int u = 0; u < kUnroll; ++u) a[u] = b[u];
       if (r + kUnroll > plain_end) break;
     }
     // a[] holds rows r .. r+kUnroll-1; fewer than kUnroll plain rows remain.
@@ -287,7 +294,7 @@ __device__ uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const ch
 
 // Kernel A: one wave per segment; waves take contiguous segment ranges.
 __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
-                                                           uint32_t total_segs, uint64_t seg_bytes,
+                                                           uint32_t total_segs, uint64_t seg_bytes, uint32_t dbg,
                                                            const PolyConsts *__restrict__ pc,
                                                            uint32_t *__restrict__ seg_crc) {
   __shared__ uint32_t lds[kLdsWords];
@@ -324,7 +331,7 @@ __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__res
     const uint64_t len = chunks[c].len;
     const uint64_t S = p + k * seg_bytes;
     const uint64_t E = p + min(len, (k + 1) * seg_bytes);
-    const uint32_t v = segment_crc0(S, E, lane, lb, off_lo, off_hi, fix, pc, poly);
+    const uint32_t v = segment_crc0(S, E, lane, lb, off_lo, off_hi, fix, pc, poly, dbg);
     if (lane == 0) seg_crc[s] = v;
   }
 }
@@ -459,6 +466,12 @@ std::atomic<int> g_prof_on{0};
 double g_prof_ms_done = 0;
 uint64_t g_prof_launch_done = 0, g_prof_bytes_done = 0;
 
+// test hook: H3C_DEBUG_FLAGS bit0 disables the pipelined row loop (read per plan)
+uint32_t read_dbg_flags() {
+  const char *e = std::getenv("H3C_DEBUG_FLAGS");
+  return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
+}
+
 struct Group {
   uint8_t type = H3C_TYPE_CRC32C;
   uint32_t nchunks = 0;
@@ -483,6 +496,7 @@ struct h3c_plan {
   size_t n = 0;
   uint64_t seg_bytes = kMaxSegBytes;
   uint64_t bytes = 0;
+  uint32_t dbg = 0;
   std::vector<Group> groups;
   uint32_t *d_segcrc = nullptr;
 };
@@ -549,6 +563,11 @@ int h3c_plan_create(const h3c_desc *d, size_t n, int device, h3c_plan **out) {
   for (size_t i = 0; i < n; ++i)
     if ((d[i].type == H3C_TYPE_CRC32C || d[i].type == H3C_TYPE_CRC32) && d[i].ptr) total += d[i].len;
   p->seg_bytes = pick_seg_bytes(total, g_dev[device].num_cu);
+  p->dbg = read_dbg_flags();
+  if (const char *e = std::getenv("H3C_SEG_BYTES")) {  // test hook: force the segment size
+    const uint64_t v = std::strtoull(e, nullptr, 0);
+    if (v >= kRowBytes && v % kRowBytes == 0) p->seg_bytes = v;
+  }
   p->bytes = total;
 
   std::vector<DevChunk> hc[2];
@@ -657,7 +676,7 @@ int h3c_plan_run(h3c_plan *p, const uint32_t *expected_raw_dev, uint32_t *out_ra
         HIP_TRY(hipEventRecord(rec.a, st));
       }
       hipLaunchKernelGGL(seg_crc_kernel, dim3(blocks), dim3(kThreads), 0, st, g.d_chunks, g.nchunks, g.total_segs,
-                         p->seg_bytes, pc, p->d_segcrc);
+                         p->seg_bytes, p->dbg, pc, p->d_segcrc);
       HIP_TRY(hipGetLastError());
       if (prof) {
         HIP_TRY(hipEventRecord(rec.b, st));

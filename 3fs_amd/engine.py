@@ -24,7 +24,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-lib_path = os.path.join(_HERE, "_lib", "libh3c_crc.so")
+lib_path = os.environ.get("H3C_LIB_PATH") or os.path.join(_HERE, "_lib", "libh3c_crc.so")  # env: test hook
 
 if not os.path.exists(lib_path):
     raise ImportError(

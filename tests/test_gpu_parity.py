@@ -245,3 +245,24 @@ def test_profile_counters(h3c, torch_dev):
     torch.cuda.synchronize()
     assert (out.cpu().numpy().view(np.uint32) == (~0x14298C12) & MASK).all()  # 1 MiB of zeros
     plan.close()
+
+
+@pytest.mark.parametrize("seg", [1024, 4096, 16384, 65536, 262144])
+@pytest.mark.parametrize("dbg", [0, 1])
+def test_forced_segment_sizes_and_paths(h3c, torch_dev, seg, dbg, monkeypatch):
+    """Every segment size and both row-loop paths (pipelined / single-row) agree with the oracle."""
+    torch, dev = torch_dev
+    monkeypatch.setenv("H3C_SEG_BYTES", str(seg))
+    monkeypatch.setenv("H3C_DEBUG_FLAGS", str(dbg))
+    rng = np.random.default_rng(seg + dbg)
+    sizes = [1, 17, 1024, 4096, 5120, 6144, 7168, 9216, 12345, 16384, 16385, 65543, 262144 + 1000,
+             (1 << 20) + 3, 3 << 20]
+    host = rng.integers(0, 256, sum(sizes) + 64, dtype=np.uint8)
+    buf = to_dev(torch, dev, host)
+    items, want, off = [], [], 5  # odd base offset: unaligned chunk starts
+    for n in sizes:
+        items.append((buf[off: off + n], n))
+        want.append(orc.crc32c(host[off: off + n]))
+        off += n
+    _, got = h3c.batch_create(items)
+    assert [int(x) for x in got] == want
