@@ -21,8 +21,9 @@
 //     wave writes the segment's init-0 CRC.
 //   * A finalize kernel folds segment CRCs per chunk with x^(8*seg_bytes) shifts and
 //     applies the starting checksum: raw = crc0 ^ start * x^(8*len).
-//   * Tables live in LDS replicated 32x (entry b, copy c at dword 32*b + c), and lane
-//     l reads copy l%32, so every ds_read_b32 is bank-conflict-free for random bytes.
+//   * Tables live in LDS replicated 32x and lane l reads copy l%32, so every
+//     ds_read_b32 is bank-conflict-free for random bytes; the LDS address of a lookup
+//     is a single v_perm_b32 of the register byte and a per-lane offset.
 //     4 tables x 256 x 32 x 4 B = 128 KiB of the CU's 160 KiB.
 #include <hip/hip_runtime.h>
 
@@ -48,7 +49,7 @@ constexpr int kWavesPerBlock = 16;
 constexpr int kThreads = kWavesPerBlock * 64;
 constexpr int kCopies = 32;
 constexpr int kLdsWords = 4 * 256 * kCopies;  // 32768 dwords = 128 KiB
-constexpr uint64_t kMaxSegBytes = 256u << 10;
+constexpr uint64_t kMaxSegBytes = 1u << 20;
 constexpr uint64_t kMinSegBytes = 16u << 10;
 constexpr int kMaxDevices = 64;
 
@@ -138,21 +139,81 @@ __device__ uint32_t dxpow8n(uint64_t n, const PolyConsts *__restrict__ pc, uint3
   return r;
 }
 
-// One stream step: s' = s * x^(8*1024) given r = s ^ d, via the replicated tables.
-// Byte k of r selects entry b of table k; the LDS byte address is
-// k*32 KiB + b*128 + (lane%32)*4.  off_lo = (lane%32)*4, off_hi = off_lo + 64 KiB
-// keeps every instruction's immediate offset within 16 bits (0 or 32 KiB).
-__device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, uint32_t off_lo, uint32_t off_hi) {
-  const uint32_t a0 = ((r << 7) & 0x7F80u) | off_lo;
-  const uint32_t a1 = ((r >> 1) & 0x7F80u) | off_lo;
-  const uint32_t a2 = ((r >> 9) & 0x7F80u) | off_hi;
-  const uint32_t a3 = ((r >> 17) & 0x7F80u) | off_hi;
+#ifndef H3C_PERM_LAYOUT
+#define H3C_PERM_LAYOUT 1
+#endif
+#ifndef H3C_XOR3_ASM
+#define H3C_XOR3_ASM 1
+#endif
+
+// Per-lane LDS addressing of the replicated tables (see kernel header comment).
+struct LaneLut {
+  uint32_t off[4];
+};
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if H3C_XOR3_ASM
+  uint32_t d;  // gfx950 has no v_xor3_b32; v_bitop3_b32 with truth table 0x96 is a^b^c
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+#else
+  return a ^ b ^ c;
+#endif
+}
+
+#if H3C_PERM_LAYOUT
+// Layout: table t (0..3), entry b, copy c at byte address
+//   (t>>1)*64 KiB + b*256 + (t&1)*128 + c*4,
+// i.e. each 256-byte LDS row holds entry b of two tables x 32 copies.  ds_read_b32
+// banks on (addr/4)%32 = c, so lane l reading copy l%32 never conflicts.  The
+// address is one v_perm_b32: byte1 <- byte k of r, bytes 0 and 2 <- the lane's
+// per-table offset (byte0 = (t&1)<<7 | c<<2, byte2 = t>>1), byte3 <- 0.
+__device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
+  LaneLut L;
+  const uint32_t c4 = (lane & 31u) * 4u;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) L.off[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) << 7) | c4;
+  return L;
+}
+__device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const LaneLut &L) {
+  const uint32_t a0 = __builtin_amdgcn_perm(r, L.off[0], 0x0C020400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(r, L.off[1], 0x0C020500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(r, L.off[2], 0x0C020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(r, L.off[3], 0x0C020700u);
+  const uint32_t t0 = *reinterpret_cast<const uint32_t *>(lb + a0);
+  const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1);
+  const uint32_t t2 = *reinterpret_cast<const uint32_t *>(lb + a2);
+  const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3);
+  return xor3(t0, t1, t2) ^ t3;
+}
+// LDS dword i holds table ((i>>14)<<1 | (i>>5)&1), entry (i>>6)&255.
+__device__ __forceinline__ uint32_t fill_value(const PolyConsts *__restrict__ pc, int i) {
+  return pc->tab[((i >> 14) << 1) | ((i >> 5) & 1)][(i >> 6) & 255];
+}
+#else
+// Layout: table k, entry b, copy c at byte address k*32 KiB + b*128 + c*4.
+__device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
+  LaneLut L;
+  L.off[0] = (lane & 31u) * 4u;
+  L.off[1] = L.off[0] + 65536u;
+  L.off[2] = L.off[3] = 0;
+  return L;
+}
+__device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const LaneLut &L) {
+  const uint32_t a0 = ((r << 7) & 0x7F80u) | L.off[0];
+  const uint32_t a1 = ((r >> 1) & 0x7F80u) | L.off[0];
+  const uint32_t a2 = ((r >> 9) & 0x7F80u) | L.off[1];
+  const uint32_t a3 = ((r >> 17) & 0x7F80u) | L.off[1];
   const uint32_t t0 = *reinterpret_cast<const uint32_t *>(lb + a0);
   const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1 + 32768);
   const uint32_t t2 = *reinterpret_cast<const uint32_t *>(lb + a2);
   const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3 + 32768);
-  return (t0 ^ t1) ^ (t2 ^ t3);
+  return xor3(t0, t1, t2) ^ t3;
 }
+__device__ __forceinline__ uint32_t fill_value(const PolyConsts *__restrict__ pc, int i) {
+  return pc->tab[i >> 13][(i >> 5) & 255];
+}
+#endif
 
 __device__ __forceinline__ uint32_t byte_mask(uint64_t d, uint64_t s, uint64_t e) {
   const uint32_t lo = s > d ? (uint32_t)min<uint64_t>(s - d, 4) : 0u;
@@ -169,12 +230,9 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef const v4u __attribute__((address_space(1))) *gv4p;  // global (not flat) pointer
 
 #ifndef H3C_NT_LOADS
-#define H3C_NT_LOADS 0
+#define H3C_NT_LOADS 1  // streamed payload is read once: nontemporal loads (+9% measured)
 #endif
-// cache-policy bits of the streaming buffer loads (2 = nt)
-#ifndef H3C_LOAD_AUX
-#define H3C_LOAD_AUX 0
-#endif
+
 
 __device__ __forceinline__ uint4 load_row(uint64_t a) {
 #if H3C_NT_LOADS
@@ -203,11 +261,11 @@ struct Streams {
   uint32_t s0, s1, s2, s3;
 };
 
-__device__ __forceinline__ void consume(Streams &st, uint4 v, const char *lb, uint32_t off_lo, uint32_t off_hi) {
-  st.s0 = row_step(st.s0 ^ v.x, lb, off_lo, off_hi);
-  st.s1 = row_step(st.s1 ^ v.y, lb, off_lo, off_hi);
-  st.s2 = row_step(st.s2 ^ v.z, lb, off_lo, off_hi);
-  st.s3 = row_step(st.s3 ^ v.w, lb, off_lo, off_hi);
+__device__ __forceinline__ void consume(Streams &st, uint4 v, const char *lb, const LaneLut &L) {
+  st.s0 = row_step(st.s0 ^ v.x, lb, L);
+  st.s1 = row_step(st.s1 ^ v.y, lb, L);
+  st.s2 = row_step(st.s2 ^ v.z, lb, L);
+  st.s3 = row_step(st.s3 ^ v.w, lb, L);
 }
 
 #ifndef H3C_UNROLL
@@ -216,8 +274,8 @@ __device__ __forceinline__ void consume(Streams &st, uint4 v, const char *lb, ui
 constexpr int kUnroll = H3C_UNROLL;  // rows in flight per batch (x2 with the prefetch)
 
 // init-0 CRC of bytes [S, E) (E > S), computed by one wavefront.
-__device__ uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const char *lb, uint32_t off_lo,
-                                 uint32_t off_hi, const uint32_t fix[4], const PolyConsts *__restrict__ pc,
+__device__ uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const char *lb, const LaneLut &L,
+                                 const uint32_t fix[4], const PolyConsts *__restrict__ pc,
                                  uint32_t poly, uint32_t dbg) {
   const uint64_t E16 = (E + 15) & ~uint64_t(15);
   const uint64_t S16 = S & ~uint64_t(15);
@@ -226,7 +284,7 @@ __device__ uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const ch
 
   Streams st{0, 0, 0, 0};
   // row 0 (masked)
-  consume(st, load_masked(base, S, E), lb, off_lo, off_hi);
+  consume(st, load_masked(base, S, E), lb, L);
   // Rows 1 .. K-2 lie fully inside [S, E).  They are read with saddr-form global
   // loads: wave-uniform 64-bit row base in SGPRs + per-lane 32-bit offset 16*lane,
   // so no per-row VGPR address arithmetic.  Prefetch rows are clamped to the last
@@ -247,7 +305,11 @@ __device__ uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const ch
     auto ld = [&](uint32_t row) -> uint4 {
       row = min(row, last);
       const gcp rp = gbase + (uint64_t)row * kRowBytes;  // uniform (SGPR) part
-      const v4u v = *(gv4p)(rp + voff);                    // + per-lane 32-bit offset
+#if H3C_NT_LOADS
+      const v4u v = __builtin_nontemporal_load((gv4p)(rp + voff));
+#else
+      const v4u v = *(gv4p)(rp + voff);  // + per-lane 32-bit offset
+#endif
       return make_uint4(v.x, v.y, v.z, v.w);
     };
     // NOTE: an explicit two-buffer ping-pong form of this loop (no copy) miscompiled
@@ -262,7 +324,7 @@ __device__ uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const ch
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) b[u] = ld(r + kUnroll + u);
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) consume(st, a[u], lb, off_lo, off_hi);
+      for (int u = 0; u < kUnroll; ++u) consume(st, a[u], lb, L);
       r += kUnroll;
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) a[u] = b[u];
@@ -271,12 +333,12 @@ __device__ uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const ch
     // a[] holds rows r .. r+kUnroll-1; fewer than kUnroll plain rows remain.
 #pragma unroll
     for (int u = 0; u < kUnroll - 1; ++u)
-      if (r + u < plain_end) consume(st, a[u], lb, off_lo, off_hi);
+      if (r + u < plain_end) consume(st, a[u], lb, L);
     r = plain_end;
   }
-  for (; r < plain_end; ++r) consume(st, load_row(base + (uint64_t)r * kRowBytes), lb, off_lo, off_hi);
+  for (; r < plain_end; ++r) consume(st, load_row(base + (uint64_t)r * kRowBytes), lb, L);
   // row K-1 (masked)
-  if (K >= 2) consume(st, load_masked(base + (uint64_t)(K - 1) * kRowBytes, S, E), lb, off_lo, off_hi);
+  if (K >= 2) consume(st, load_masked(base + (uint64_t)(K - 1) * kRowBytes, S, E), lb, L);
 
   // Move every stream back to the 16-byte-rounded end, then to the true end.
   // The per-lane constants are made opaque here so the compiler does not hoist
@@ -298,7 +360,7 @@ __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__res
                                                            const PolyConsts *__restrict__ pc,
                                                            uint32_t *__restrict__ seg_crc) {
   __shared__ uint32_t lds[kLdsWords];
-  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = pc->tab[i >> 13][(i >> 5) & 255];
+  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63;
@@ -314,8 +376,7 @@ __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__res
 #pragma unroll
   for (int j = 0; j < 4; ++j) fix[j] = pc->fix[4 * lane + j];
   const char *lb = reinterpret_cast<const char *>(lds);
-  const uint32_t off_lo = (lane & 31u) * 4u;
-  const uint32_t off_hi = off_lo + 65536u;
+  const LaneLut L = make_lut(lane);
 
   // chunk owning s_lo: last c with seg_begin <= s_lo
   uint32_t lo = 0, hi = nchunks;
@@ -331,7 +392,7 @@ __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__res
     const uint64_t len = chunks[c].len;
     const uint64_t S = p + k * seg_bytes;
     const uint64_t E = p + min(len, (k + 1) * seg_bytes);
-    const uint32_t v = segment_crc0(S, E, lane, lb, off_lo, off_hi, fix, pc, poly, dbg);
+    const uint32_t v = segment_crc0(S, E, lane, lb, L, fix, pc, poly, dbg);
     if (lane == 0) seg_crc[s] = v;
   }
 }
@@ -481,8 +542,8 @@ struct Group {
 };
 
 uint64_t pick_seg_bytes(uint64_t total_bytes, int num_cu) {
-  // Aim for >= 4 segments per wave slot on the chip, within [16 KiB, 256 KiB].
-  const uint64_t slots = (uint64_t)std::max(num_cu, 1) * kWavesPerBlock * 4;
+  // Aim for >= 2 segments per wave slot on the chip, within [16 KiB, 1 MiB].
+  const uint64_t slots = (uint64_t)std::max(num_cu, 1) * kWavesPerBlock * 2;
   uint64_t want = total_bytes / slots;
   uint64_t seg = kMaxSegBytes;
   while (seg > kMinSegBytes && seg > want) seg >>= 1;
