@@ -75,6 +75,25 @@ def cpu_baseline(gpu_raw_first: np.ndarray, chunk_len: int, seconds: float = 8.0
     }
 
 
+def pmc_traffic(bytes_per_launch: int):
+    """HBM bytes per seg_crc_kernel launch from the committed rocprofv3 PMC summary
+    (profiles/*_pmc_summary.json, made by scripts/profile_r1.sh + summarize_prof.py,
+    FETCH_SIZE/WRITE_SIZE in separate passes, gfx950 FETCH_SIZE x2 correction).
+    Only used when that profile was taken on this same per-launch workload."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        t = d.get("pmc", {}).get("traffic_bytes_per_launch")
+        if t and abs(d.get("algorithmic_bytes_per_launch", 0) - bytes_per_launch) < 1:
+            best = (t, os.path.basename(f))
+    return best
+
+
 def _cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -210,6 +229,10 @@ def main() -> int:
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
             },
         }
+        tr = pmc_traffic(int(bytes_per_launch))
+        if tr:
+            res["roofline"]["traffic"] = int(tr[0])
+            res["roofline"]["traffic_source"] = f"profiles/{tr[1]}"
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(stored_host, clen, args.cpu_seconds)
         print(json.dumps(res), flush=True)
