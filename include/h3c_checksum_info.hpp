@@ -1,0 +1,82 @@
+// h3c_checksum_info.hpp -- header-only C++ mirror of hf3fs::storage::ChecksumInfo
+// (src/fbs/storage/Common.h:113-201) over the C ABI in h3c_crc.h.
+//
+// Same names, argument meaning and error behaviour as the reference:
+//   create(type, buf, len, start=~0)  NONE -> {NONE,0}; len 0 -> {type,start};
+//                                     buf==nullptr && len>0 -> {NONE,0}
+//   combine(o, len)                   4080 (kChecksumMismatch) on type mismatch,
+//                                     len 0 no-op, NONE receiver copies o,
+//                                     else value = crc32c_combine(~value, o.value, len)
+//   operator==                        field-wise
+// The payload CRC runs on the GPU; combine is O(log n) host GF(2) arithmetic, as
+// in the reference (folly::crc32c_combine is host code there too).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "h3c_crc.h"
+
+namespace h3c {
+
+enum class ChecksumType : uint8_t { NONE = 0, CRC32C = 1, CRC32 = 2 };
+
+struct ChecksumInfo {
+  ChecksumType type = ChecksumType::NONE;
+  uint32_t value = 0;
+
+  static constexpr size_t kChunkSize = size_t(1) << 20;  // Common.h:118
+
+  // ChecksumInfo::create(type, buffer, length, startingChecksum) (Common.h:174-177).
+  // `mem` says where `buf` lives; `rc` (optional) receives the engine status.
+  static ChecksumInfo create(ChecksumType type, const uint8_t *buf, size_t length, uint32_t start = ~0U,
+                             h3c_mem mem = H3C_MEM_DEVICE, void *stream = nullptr, int *rc = nullptr) {
+    h3c_desc d{buf, (uint64_t)length, start, (uint8_t)type, (uint8_t)mem, 0};
+    uint8_t t = 0;
+    uint32_t v = 0;
+    const int r = h3c_batch_create(&d, 1, &t, &v, stream);
+    if (rc) *rc = r;
+    if (r != H3C_OK) return ChecksumInfo{ChecksumType::NONE, 0U};
+    return ChecksumInfo{(ChecksumType)t, v};
+  }
+
+  // Batched form: one GPU pass over many chunks (the point of the engine).
+  static int createBatch(const std::vector<h3c_desc> &descs, std::vector<ChecksumInfo> &out, void *stream = nullptr) {
+    std::vector<uint8_t> t(descs.size());
+    std::vector<uint32_t> v(descs.size());
+    const int r = h3c_batch_create(descs.data(), descs.size(), t.data(), v.data(), stream);
+    if (r != H3C_OK) return r;
+    out.resize(descs.size());
+    for (size_t i = 0; i < descs.size(); ++i) out[i] = ChecksumInfo{(ChecksumType)t[i], v[i]};
+    return H3C_OK;
+  }
+
+  // ChecksumInfo::combine (Common.h:179-198); returns 0 or H3C_ERR_CHECKSUM_MISMATCH (4080).
+  int combine(const ChecksumInfo &o, size_t length) {
+    if (type != ChecksumType::NONE && type != o.type) return H3C_ERR_CHECKSUM_MISMATCH;
+    if (length == 0) return H3C_OK;
+    switch (type) {
+      case ChecksumType::NONE:
+        *this = o;
+        return H3C_OK;
+      case ChecksumType::CRC32C:
+        value = h3c_crc32c_combine(~value, o.value, length);
+        return H3C_OK;
+      case ChecksumType::CRC32:
+        value = h3c_crc32_combine(~value, o.value, length);
+        return H3C_OK;
+    }
+    return H3C_OK;
+  }
+
+  bool operator==(const ChecksumInfo &o) const { return type == o.type && value == o.value; }
+  bool operator!=(const ChecksumInfo &o) const { return !(*this == o); }
+};
+
+// Rust chunk-engine domain (crate crc32c 0.6.8, Cargo.lock:399-402): std = ~raw
+// (src/storage/store/ChunkEngine.cc:42,66).
+inline uint32_t std_from_raw(uint32_t raw) { return ~raw; }
+inline uint32_t raw_from_std(uint32_t std_value) { return ~std_value; }
+
+}  // namespace h3c

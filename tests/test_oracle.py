@@ -139,3 +139,13 @@ def test_splitmix_generator_matches_python():
     words = [sm(seed ^ (chunk << 40) ^ k) for k in range(6)]
     want = b"".join(w.to_bytes(8, "little") for w in words)[:45]
     assert got.tobytes() == want
+
+
+def test_std_domain_combine():
+    """Rust crc32c-crate domain (std = ~raw, ChunkEngine.cc:42,66): combine is the same shift-XOR."""
+    rng = np.random.default_rng(8)
+    for _ in range(30):
+        a = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8)
+        b = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8)
+        std = lambda x: (~orc.crc32c(x)) & MASK
+        assert orc.lib().orc_crc32c_combine(std(a), std(b), b.size) == std(np.concatenate([a, b]))
