@@ -29,6 +29,8 @@ from .engine import (  # noqa: F401
     lib_path,
     profile_enable,
     profile_read,
+    update_blocks,
+    update_workspace_bytes,
 )
 
 __all__ = [
@@ -49,4 +51,6 @@ __all__ = [
     "lib_path",
     "profile_enable",
     "profile_read",
+    "update_blocks",
+    "update_workspace_bytes",
 ]

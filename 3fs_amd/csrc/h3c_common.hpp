@@ -1,0 +1,349 @@
+// h3c_common.hpp -- device/host building blocks shared by the engine's translation
+// units (h3c_engine.hip: create/verify/combine; h3c_update.hip: partial updates).
+// Everything here has internal linkage (anonymous namespace); the shared runtime
+// state lives behind the h3c_rt:: functions defined in h3c_engine.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "h3c_crc.h"
+
+namespace h3c_rt {
+// Per-device constant block for `type` (H3C_TYPE_CRC32C / H3C_TYPE_CRC32), built on first use.
+const void *device_consts(int dev, int type);
+int device_num_cu(int dev);
+// hipGetDevice + lazy init; returns H3C_OK or an h3c_status.
+int current_device(int *dev);
+void set_error(const char *what, hipError_t e);
+void set_error_text(const char *text);
+}  // namespace h3c_rt
+
+#define HIP_TRY(expr)               \
+  do {                              \
+    hipError_t e_ = (expr);         \
+    if (e_ != hipSuccess) {         \
+      h3c_rt::set_error(#expr, e_); \
+      return H3C_ERR_HIP;           \
+    }                               \
+  } while (0)
+
+namespace {
+
+constexpr uint32_t kPolyCrc32c = 0x82F63B78u;
+constexpr uint32_t kPolyCrc32 = 0xEDB88320u;
+constexpr uint32_t kOne = 0x80000000u;  // x^0 in the reflected representation
+constexpr int kRowBytes = 1024;         // 64 lanes x 16 B
+constexpr int kWavesPerBlock = 16;
+constexpr int kThreads = kWavesPerBlock * 64;
+constexpr int kCopies = 32;
+constexpr int kLdsWords = 4 * 256 * kCopies;  // 32768 dwords = 128 KiB
+constexpr uint64_t kMaxSegBytes = 1u << 20;
+constexpr uint64_t kMinSegBytes = 16u << 10;
+constexpr int kMaxDevices = 64;
+
+// ---------------------------------------------------------------- host GF(2)
+uint32_t hgf_mul(uint32_t a, uint32_t b, uint32_t poly) {
+  uint32_t p = 0;
+  for (int i = 0; i < 32; ++i) {
+    if (a & (kOne >> i)) p ^= b;
+    b = (b >> 1) ^ (poly & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+uint32_t hgf_pow(uint32_t base, uint64_t e, uint32_t poly) {
+  uint32_t r = kOne;
+  while (e) {
+    if (e & 1u) r = hgf_mul(r, base, poly);
+    base = hgf_mul(base, base, poly);
+    e >>= 1;
+  }
+  return r;
+}
+
+uint32_t hxpow8n(uint64_t n, uint32_t poly) { return hgf_pow(0x00800000u /* x^8 */, n, poly); }
+
+// x^-1: the y with y*x == 1.  Multiplying by x is y>>1 ^ (poly if y&1); the
+// result is x^0 (bit 31) only when y&1 and (y>>1)^poly == 1<<31.
+uint32_t hx_inverse(uint32_t poly) { return ((poly ^ kOne) << 1) | 1u; }
+
+// Device-side constant block, one per polynomial per device.
+struct PolyConsts {
+  uint32_t tab[4][256];  // tab[k][b] = (b << 8k) * x^(8*kRowBytes)
+  uint32_t fix[256];     // [4l+j] = x^-(8*(16l+4j))
+  uint32_t fixz[16];     // [z]    = x^-(8z)
+  uint32_t pow8[64];     // [k]    = x^(8*2^k)
+  uint32_t poly;
+  uint32_t pad[3];
+};
+
+inline void build_consts(PolyConsts &pc, uint32_t poly) {
+  std::memset(&pc, 0, sizeof(pc));
+  pc.poly = poly;
+  const uint32_t row = hxpow8n(kRowBytes, poly);
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t b = 0; b < 256; ++b) pc.tab[k][b] = hgf_mul(b << (8 * k), row, poly);
+  const uint32_t xinv8 = hgf_pow(hx_inverse(poly), 8, poly);
+  for (int l = 0; l < 64; ++l)
+    for (int j = 0; j < 4; ++j) pc.fix[4 * l + j] = hgf_pow(xinv8, 16u * l + 4u * j, poly);
+  for (int z = 0; z < 16; ++z) pc.fixz[z] = hgf_pow(xinv8, z, poly);
+  uint32_t p = 0x00800000u;
+  for (int k = 0; k < 64; ++k) {
+    pc.pow8[k] = p;
+    p = hgf_mul(p, p, poly);
+  }
+}
+
+// Device copy of a descriptor (32 B).
+struct DevChunk {
+  uint64_t ptr;
+  uint64_t len;
+  uint32_t start;
+  uint32_t out_idx;
+  uint32_t seg_begin;
+  uint32_t flags;  // bit0: result is {NONE,0}
+};
+constexpr uint32_t kFlagNone = 1u;
+
+// ---------------------------------------------------------------- device GF(2)
+__device__ __forceinline__ uint32_t dgf_mul(uint32_t a, uint32_t b, uint32_t poly) {
+  uint32_t p = 0;
+#pragma unroll 4
+  for (int i = 0; i < 32; ++i) {
+    p ^= b & (0u - ((a >> (31 - i)) & 1u));
+    b = (b >> 1) ^ (poly & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+__device__ uint32_t dxpow8n(uint64_t n, const PolyConsts *__restrict__ pc, uint32_t poly) {
+  uint32_t r = kOne;
+  int k = 0;
+  while (n) {
+    if (n & 1u) r = (r == kOne) ? pc->pow8[k] : dgf_mul(r, pc->pow8[k], poly);
+    n >>= 1;
+    ++k;
+  }
+  return r;
+}
+
+#ifndef H3C_PERM_LAYOUT
+#define H3C_PERM_LAYOUT 1
+#endif
+#ifndef H3C_XOR3_ASM
+#define H3C_XOR3_ASM 1
+#endif
+
+// Per-lane LDS addressing of the replicated tables (see kernel header comment).
+struct LaneLut {
+  uint32_t off[4];
+};
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if H3C_XOR3_ASM
+  uint32_t d;  // gfx950 has no v_xor3_b32; v_bitop3_b32 with truth table 0x96 is a^b^c
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+#else
+  return a ^ b ^ c;
+#endif
+}
+
+#if H3C_PERM_LAYOUT
+// Layout: table t (0..3), entry b, copy c at byte address
+//   (t>>1)*64 KiB + b*256 + (t&1)*128 + c*4,
+// i.e. each 256-byte LDS row holds entry b of two tables x 32 copies.  ds_read_b32
+// banks on (addr/4)%32 = c, so lane l reading copy l%32 never conflicts.  The
+// address is one v_perm_b32: byte1 <- byte k of r, bytes 0 and 2 <- the lane's
+// per-table offset (byte0 = (t&1)<<7 | c<<2, byte2 = t>>1), byte3 <- 0.
+__device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
+  LaneLut L;
+  const uint32_t c4 = (lane & 31u) * 4u;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) L.off[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) << 7) | c4;
+  return L;
+}
+__device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const LaneLut &L) {
+  const uint32_t a0 = __builtin_amdgcn_perm(r, L.off[0], 0x0C020400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(r, L.off[1], 0x0C020500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(r, L.off[2], 0x0C020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(r, L.off[3], 0x0C020700u);
+  const uint32_t t0 = *reinterpret_cast<const uint32_t *>(lb + a0);
+  const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1);
+  const uint32_t t2 = *reinterpret_cast<const uint32_t *>(lb + a2);
+  const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3);
+  return xor3(t0, t1, t2) ^ t3;
+}
+// LDS dword i holds table ((i>>14)<<1 | (i>>5)&1), entry (i>>6)&255.
+__device__ __forceinline__ uint32_t fill_value(const PolyConsts *__restrict__ pc, int i) {
+  return pc->tab[((i >> 14) << 1) | ((i >> 5) & 1)][(i >> 6) & 255];
+}
+#else
+// Layout: table k, entry b, copy c at byte address k*32 KiB + b*128 + c*4.
+__device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
+  LaneLut L;
+  L.off[0] = (lane & 31u) * 4u;
+  L.off[1] = L.off[0] + 65536u;
+  L.off[2] = L.off[3] = 0;
+  return L;
+}
+__device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const LaneLut &L) {
+  const uint32_t a0 = ((r << 7) & 0x7F80u) | L.off[0];
+  const uint32_t a1 = ((r >> 1) & 0x7F80u) | L.off[0];
+  const uint32_t a2 = ((r >> 9) & 0x7F80u) | L.off[1];
+  const uint32_t a3 = ((r >> 17) & 0x7F80u) | L.off[1];
+  const uint32_t t0 = *reinterpret_cast<const uint32_t *>(lb + a0);
+  const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1 + 32768);
+  const uint32_t t2 = *reinterpret_cast<const uint32_t *>(lb + a2);
+  const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3 + 32768);
+  return xor3(t0, t1, t2) ^ t3;
+}
+__device__ __forceinline__ uint32_t fill_value(const PolyConsts *__restrict__ pc, int i) {
+  return pc->tab[i >> 13][(i >> 5) & 255];
+}
+#endif
+
+__device__ __forceinline__ uint32_t byte_mask(uint64_t d, uint64_t s, uint64_t e) {
+  const uint32_t lo = s > d ? (uint32_t)min<uint64_t>(s - d, 4) : 0u;
+  const uint32_t hi = e > d ? (uint32_t)min<uint64_t>(e - d, 4) : 0u;
+  if (hi <= lo) return 0u;
+  const uint32_t hm = hi == 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u);
+  const uint32_t lm = (1u << (8 * lo)) - 1u;
+  return hm & ~lm;
+}
+
+// Edge-row load: bytes outside [s, e) read as zero; a piece with no byte inside
+// is never dereferenced (it may lie outside the allocation).
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef const v4u __attribute__((address_space(1))) *gv4p;  // global (not flat) pointer
+
+#ifndef H3C_NT_LOADS
+#define H3C_NT_LOADS 1  // streamed payload is read once: nontemporal loads (+9% measured)
+#endif
+
+
+__device__ __forceinline__ uint4 load_row(uint64_t a) {
+#if H3C_NT_LOADS
+  const v4u v = __builtin_nontemporal_load((gv4p)a);
+#else
+  const v4u v = *(gv4p)a;
+#endif
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Edge-row load: bytes outside [s, e) read as zero; a piece with no byte inside
+// is never dereferenced (it may lie outside the allocation).
+__device__ __forceinline__ uint4 load_masked(uint64_t a, uint64_t s, uint64_t e) {
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (a + 16 > s && a < e) {
+    v = load_row(a);
+    v.x &= byte_mask(a, s, e);
+    v.y &= byte_mask(a + 4, s, e);
+    v.z &= byte_mask(a + 8, s, e);
+    v.w &= byte_mask(a + 12, s, e);
+  }
+  return v;
+}
+
+struct Streams {
+  uint32_t s0, s1, s2, s3;
+};
+
+__device__ __forceinline__ void consume(Streams &st, uint4 v, const char *lb, const LaneLut &L) {
+  st.s0 = row_step(st.s0 ^ v.x, lb, L);
+  st.s1 = row_step(st.s1 ^ v.y, lb, L);
+  st.s2 = row_step(st.s2 ^ v.z, lb, L);
+  st.s3 = row_step(st.s3 ^ v.w, lb, L);
+}
+
+#ifndef H3C_UNROLL
+#define H3C_UNROLL 4
+#endif
+constexpr int kUnroll = H3C_UNROLL;  // rows in flight per batch (x2 with the prefetch)
+
+// init-0 CRC of bytes [S, E) (E > S), computed by one wavefront.
+__device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const char *lb, const LaneLut &L,
+                                 const uint32_t fix[4], const PolyConsts *__restrict__ pc,
+                                 uint32_t poly, uint32_t dbg) {
+  const uint64_t E16 = (E + 15) & ~uint64_t(15);
+  const uint64_t S16 = S & ~uint64_t(15);
+  const uint32_t K = (uint32_t)((E16 - S16 + kRowBytes - 1) / kRowBytes);
+  const uint64_t base = E16 - (uint64_t)K * kRowBytes + 16u * lane;
+
+  Streams st{0, 0, 0, 0};
+  // row 0 (masked)
+  consume(st, load_masked(base, S, E), lb, L);
+  // Rows 1 .. K-2 lie fully inside [S, E).  They are read with saddr-form global
+  // loads: wave-uniform 64-bit row base in SGPRs + per-lane 32-bit offset 16*lane,
+  // so no per-row VGPR address arithmetic.  Prefetch rows are clamped to the last
+  // plain row (every load stays inside the segment; the few clamped re-reads at a
+  // segment's end hit in cache).  One batch of kUnroll rows is in flight while the
+  // previous batch is consumed.
+  uint32_t r = 1;
+  const uint32_t plain_end = K >= 2 ? K - 1 : 1;
+  if (!(dbg & 1u) && r + kUnroll <= plain_end) {
+    // readfirstlane returns int: widen through uint32_t so the low half is not sign-extended.
+    const uint64_t row0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base - 16u * lane)) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((base - 16u * lane) >> 32))
+                           << 32);
+    typedef const char __attribute__((address_space(1))) *gcp;
+    const gcp gbase = (gcp)row0;
+    const uint32_t voff = 16u * lane;
+    const uint32_t last = plain_end - 1;
+    auto ld = [&](uint32_t row) -> uint4 {
+      row = min(row, last);
+      const gcp rp = gbase + (uint64_t)row * kRowBytes;  // uniform (SGPR) part
+#if H3C_NT_LOADS
+      const v4u v = __builtin_nontemporal_load((gv4p)(rp + voff));
+#else
+      const v4u v = *(gv4p)(rp + voff);  // + per-lane 32-bit offset
+#endif
+      return make_uint4(v.x, v.y, v.z, v.w);
+    };
+    // NOTE: an explicit two-buffer ping-pong form of this loop (no copy) miscompiled
+    // under ROCm 7.2 hipcc -O3 at kUnroll=4 (wrong CRCs from the first pipelined
+    // row; correct at -O1 and at kUnroll=2); this copy form is correct at every
+    // setting tried and the copies are register renames.
+    uint4 a[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) a[u] = ld(r + u);
+    for (;;) {
+      uint4 b[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) b[u] = ld(r + kUnroll + u);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) consume(st, a[u], lb, L);
+      r += kUnroll;
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) a[u] = b[u];
+      if (r + kUnroll > plain_end) break;
+    }
+    // a[] holds rows r .. r+kUnroll-1; fewer than kUnroll plain rows remain.
+#pragma unroll
+    for (int u = 0; u < kUnroll - 1; ++u)
+      if (r + u < plain_end) consume(st, a[u], lb, L);
+    r = plain_end;
+  }
+  for (; r < plain_end; ++r) consume(st, load_row(base + (uint64_t)r * kRowBytes), lb, L);
+  // row K-1 (masked)
+  if (K >= 2) consume(st, load_masked(base + (uint64_t)(K - 1) * kRowBytes, S, E), lb, L);
+
+  // Move every stream back to the 16-byte-rounded end, then to the true end.
+  // The per-lane constants are made opaque here so the compiler does not hoist
+  // 4 x 32 shifted copies of them out of the segment loop (that spills).
+  uint32_t f0 = fix[0], f1 = fix[1], f2 = fix[2], f3 = fix[3];
+  asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
+  uint32_t acc = dgf_mul(f0, st.s0, poly) ^ dgf_mul(f1, st.s1, poly) ^ dgf_mul(f2, st.s2, poly) ^
+                 dgf_mul(f3, st.s3, poly);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
+  const uint32_t z = (uint32_t)(E16 - E);
+  if (z) acc = dgf_mul(acc, pc->fixz[z], poly);
+  return acc;
+}
+
+}  // namespace

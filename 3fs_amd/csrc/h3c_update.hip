@@ -1,0 +1,319 @@
+// h3c_update.hip -- batched partial-update checksums on MI355X (BASELINE config 3).
+//
+// Replaces, for a batch of block-aligned overwrites, the per-write work of
+// ChunkReplica::update + ChunkReplica::updateChecksum (src/storage/store/ChunkReplica.cc:
+// 132-300, 319-394).  For an overwrite inside the chunk the reference re-reads the
+// prefix [0,off) and the suffix [off+len,size) from disk, CRCs them and does two
+// crc32c_combine()s (case iv, :356-390): O(chunk) bytes per write.
+//
+// Here the chunk checksum is updated by linearity instead (CRC is affine over GF(2)):
+//     raw(M') = raw(M) ^ crc0(old ^ new) * x^(8*(L - off - len))
+// so a write costs its own bytes: read new + read old + write back = 12 KiB per 4 KiB
+// block.  Writes are applied in sequence order.  The batch is split into block writes
+// (chunk c, block b, payload i); for each slot (c,b) the "old" data of write i is the
+// payload of the previous write to that slot, or the chunk's original bytes for the
+// first one.  Kernels:
+//   1. keys      key1[i] = slot<<32 | i                 (validates chunk/block ids)
+//   2. rocPRIM radix sort key1 -> writes grouped by slot, in sequence order
+//   3. link      prev[i] (previous writer of the slot) and, for the first writer of a
+//                slot, final[i] = the slot's last writer (whose bytes must end up there)
+//   4. shifts    sh[b] = x^(8*(L-(b+1)*G)) per block index
+//   5. delta     one wave per block write: crc0(new^old) over G bytes with the same
+//                replicated-LDS stride tables as the create kernel, times sh[b];
+//                the first writer of a slot also writes the slot's final bytes back
+//                (it is the only wave that reads the slot's original bytes: no race)
+//   6. rocPRIM radix sort key2 = chunk<<32 | i  -> per-chunk sequence order
+//   7. gather + rocPRIM inclusive_scan_by_key(chunk, XOR) + scatter:
+//        out_raw[i] = raw_in[c] ^ XOR of deltas of writes j<=i to chunk c
+//      i.e. the chunk checksum right after write i, which is what updateChecksum stores.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan_by_key.hpp>
+
+#include "h3c_common.hpp"
+
+namespace {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+struct XorOp {
+  __host__ __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a ^ b; }
+};
+
+uint32_t bits_for(uint64_t v) {  // number of bits to represent values < v
+  uint32_t b = 0;
+  while (b < 64 && (1ull << b) < v) ++b;
+  return b;
+}
+
+__global__ void upd_keys_kernel(const uint32_t *__restrict__ blk_chunk, const uint32_t *__restrict__ blk_index,
+                                uint32_t n, uint32_t nchunks, uint32_t bpc, uint64_t *__restrict__ key1,
+                                uint64_t *__restrict__ key2, uint32_t *__restrict__ err) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t c = blk_chunk[i], b = blk_index[i];
+  if (c >= nchunks || b >= bpc) {  // invalid entry: counted, parked on sentinel slot / chunk, no effect
+    atomicAdd(err, 1u);
+    key1[i] = ((uint64_t)((uint64_t)nchunks * bpc) << 32) | i;
+    key2[i] = ((uint64_t)nchunks << 32) | i;
+    return;
+  }
+  key1[i] = ((uint64_t)((uint64_t)c * bpc + b) << 32) | i;
+  key2[i] = ((uint64_t)c << 32) | i;
+}
+
+__global__ void upd_link_kernel(const uint64_t *__restrict__ sorted1, uint32_t n, uint32_t *__restrict__ prev,
+                                uint32_t *__restrict__ final_of) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint64_t k = sorted1[p];
+  const uint32_t slot = (uint32_t)(k >> 32), i = (uint32_t)k;
+  const bool start = p == 0 || (uint32_t)(sorted1[p - 1] >> 32) != slot;
+  prev[i] = start ? kNone : (uint32_t)sorted1[p - 1];
+  if (start) {  // last position of this slot's run: binary search in [p, n)
+    uint32_t lo = p, hi = n;  // invariant: slot(lo) == slot, slot(hi) > slot or hi == n
+    while (hi - lo > 1) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if ((uint32_t)(sorted1[mid] >> 32) == slot) lo = mid; else hi = mid;
+    }
+    final_of[i] = (uint32_t)sorted1[lo];
+  }
+}
+
+__global__ void upd_shift_kernel(uint32_t bpc, uint64_t chunk_len, uint32_t block_bytes,
+                                 const PolyConsts *__restrict__ pc, uint32_t *__restrict__ sh) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= bpc) return;
+  sh[b] = dxpow8n(chunk_len - (uint64_t)(b + 1) * block_bytes, pc, pc->poly);
+}
+
+// crc0(new ^ old) over `rows` full 1 KiB rows (both 16-byte aligned), by one wave.
+// When `dst` is non-zero the wave also stores the slot's final bytes (from `fin`,
+// which may equal `pnew`) after it has read the old bytes of each batch.
+__device__ uint32_t delta_crc0(uint64_t pnew, uint64_t pold, uint64_t dst, uint64_t fin, uint32_t rows,
+                               uint32_t lane, const char *lb, const LaneLut &L, const uint32_t fix[4],
+                               uint32_t poly) {
+  Streams st{0, 0, 0, 0};
+  const uint64_t lo = 16u * lane;
+  for (uint32_t r0 = 0; r0 < rows; r0 += 4) {
+    const uint32_t nb = min(4u, rows - r0);
+    uint4 vn[4], vo[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (u < (int)nb) {
+        vn[u] = load_row(pnew + (uint64_t)(r0 + u) * kRowBytes + lo);
+        vo[u] = load_row(pold + (uint64_t)(r0 + u) * kRowBytes + lo);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (u < (int)nb) {
+        const uint4 d = make_uint4(vn[u].x ^ vo[u].x, vn[u].y ^ vo[u].y, vn[u].z ^ vo[u].z, vn[u].w ^ vo[u].w);
+        consume(st, d, lb, L);
+      }
+    if (dst) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (u < (int)nb) {
+          const uint4 v = fin == pnew ? vn[u] : load_row(fin + (uint64_t)(r0 + u) * kRowBytes + lo);
+          *reinterpret_cast<uint4 *>(dst + (uint64_t)(r0 + u) * kRowBytes + lo) = v;
+        }
+    }
+  }
+  uint32_t f0 = fix[0], f1 = fix[1], f2 = fix[2], f3 = fix[3];
+  asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
+  uint32_t acc = dgf_mul(f0, st.s0, poly) ^ dgf_mul(f1, st.s1, poly) ^ dgf_mul(f2, st.s2, poly) ^
+                 dgf_mul(f3, st.s3, poly);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
+  return acc;
+}
+
+__global__ __launch_bounds__(kThreads) void upd_delta_kernel(
+    const uint64_t *__restrict__ chunk_base, uint32_t nchunks, uint32_t bpc, uint32_t block_bytes,
+    const uint32_t *__restrict__ blk_chunk, const uint32_t *__restrict__ blk_index, const uint8_t *payload,
+    uint32_t n, const uint32_t *__restrict__ prev, const uint32_t *__restrict__ final_of,
+    const uint32_t *__restrict__ sh, const PolyConsts *__restrict__ pc, uint32_t *__restrict__ delta) {
+  __shared__ uint32_t lds[kLdsWords];
+  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t lo = (uint32_t)(gw * n / nw), hi = (uint32_t)((gw + 1) * n / nw);
+  if (lo >= hi) return;
+  const uint32_t poly = pc->poly;
+  uint32_t fix[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fix[j] = pc->fix[4 * lane + j];
+  const char *lb = reinterpret_cast<const char *>(lds);
+  const LaneLut L = make_lut(lane);
+  const uint32_t rows = block_bytes / kRowBytes;
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t c = blk_chunk[i], b = blk_index[i];
+    uint32_t d = 0;
+    if (c < nchunks && b < bpc) {
+      const uint32_t p = prev[i];
+      const uint64_t slot_addr = chunk_base[c] + (uint64_t)b * block_bytes;
+      const uint64_t pnew = (uint64_t)(uintptr_t)payload + (uint64_t)i * block_bytes;
+      const uint64_t pold = p == kNone ? slot_addr : (uint64_t)(uintptr_t)payload + (uint64_t)p * block_bytes;
+      uint64_t dst = 0, fin = 0;
+      if (p == kNone) {
+        dst = slot_addr;
+        fin = (uint64_t)(uintptr_t)payload + (uint64_t)final_of[i] * block_bytes;
+      }
+      d = dgf_mul(delta_crc0(pnew, pold, dst, fin, rows, lane, lb, L, fix, poly), sh[b], poly);
+    }
+    if (lane == 0) delta[i] = d;
+  }
+}
+
+__global__ void upd_gather_kernel(const uint64_t *__restrict__ sorted2, uint32_t n, const uint32_t *__restrict__ delta,
+                                  uint32_t *__restrict__ ckey, uint32_t *__restrict__ vals) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint64_t k = sorted2[p];
+  ckey[p] = (uint32_t)(k >> 32);
+  vals[p] = delta[(uint32_t)k];
+}
+
+__global__ void upd_scatter_kernel(const uint64_t *__restrict__ sorted2, uint32_t n, uint32_t nchunks,
+                                   const uint32_t *__restrict__ scan,
+                                   const uint32_t *__restrict__ raw_in, uint32_t *__restrict__ out_raw,
+                                   uint32_t *__restrict__ raw_out) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint64_t k = sorted2[p];
+  const uint32_t c = (uint32_t)(k >> 32), i = (uint32_t)k;
+  if (c >= nchunks) {  // invalid entry (sentinel chunk)
+    out_raw[i] = 0;
+    return;
+  }
+  const uint32_t v = raw_in[c] ^ scan[p];
+  out_raw[i] = v;
+  if (p + 1 == n || (uint32_t)(sorted2[p + 1] >> 32) != c) raw_out[c] = v;
+}
+
+struct Workspace {
+  uint64_t *key1, *key1s, *key2, *key2s;
+  uint32_t *prev, *final_of, *delta, *ckey, *vals, *scan, *sh, *err;
+  void *tmp;
+  size_t tmp_bytes;
+};
+
+size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
+
+// Lays out (or, with base == nullptr, sizes) the workspace.
+int layout(void *base, uint32_t n, uint32_t nchunks, uint32_t bpc, Workspace &w, size_t &total) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) -> void * {
+    void *p = base ? static_cast<char *>(base) + off : nullptr;
+    off += align_up(bytes);
+    return p;
+  };
+  w.key1 = (uint64_t *)take(8ull * n);
+  w.key1s = (uint64_t *)take(8ull * n);
+  w.key2 = (uint64_t *)take(8ull * n);
+  w.key2s = (uint64_t *)take(8ull * n);
+  w.prev = (uint32_t *)take(4ull * n);
+  w.final_of = (uint32_t *)take(4ull * n);
+  w.delta = (uint32_t *)take(4ull * n);
+  w.ckey = (uint32_t *)take(4ull * n);
+  w.vals = (uint32_t *)take(4ull * n);
+  w.scan = (uint32_t *)take(4ull * n);
+  w.sh = (uint32_t *)take(4ull * bpc);
+  w.err = (uint32_t *)take(4);
+  size_t s1 = 0, s2 = 0;
+  if (rocprim::radix_sort_keys(nullptr, s1, (uint64_t *)nullptr, (uint64_t *)nullptr, n, 0, 64) != hipSuccess)
+    return H3C_ERR_HIP;
+  if (rocprim::inclusive_scan_by_key(nullptr, s2, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                     (size_t)n, XorOp()) != hipSuccess)
+    return H3C_ERR_HIP;
+  w.tmp_bytes = std::max(s1, s2);
+  w.tmp = take(w.tmp_bytes);
+  total = off;
+  (void)nchunks;
+  return H3C_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t h3c_update_workspace_bytes(uint32_t n_blocks, uint32_t nchunks, uint64_t chunk_len, uint32_t block_bytes) {
+  if (!block_bytes) return 0;
+  Workspace w{};
+  size_t total = 0;
+  if (layout(nullptr, std::max(n_blocks, 1u), nchunks, (uint32_t)(chunk_len / block_bytes), w, total)) return 0;
+  return total;
+}
+
+int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nchunks, uint64_t chunk_len,
+                      uint32_t block_bytes, const uint32_t *chunk_raw_in_dev, const uint32_t *blk_chunk_dev,
+                      const uint32_t *blk_index_dev, const void *payload_dev, uint32_t n_blocks,
+                      uint32_t *out_raw_dev, uint32_t *chunk_raw_out_dev, void *workspace_dev,
+                      size_t workspace_bytes, uint32_t *n_invalid_dev, void *stream) {
+  if (type != H3C_TYPE_CRC32C && type != H3C_TYPE_CRC32) return H3C_ERR_INVALID_ARG;
+  if (!block_bytes || block_bytes % kRowBytes || chunk_len % block_bytes || !nchunks) return H3C_ERR_INVALID_ARG;
+  if ((uint64_t)nchunks * (chunk_len / block_bytes) >= 0xFFFFFFFFull) return H3C_ERR_INVALID_ARG;
+  if (!chunk_base_dev || !chunk_raw_in_dev || !chunk_raw_out_dev) return H3C_ERR_INVALID_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipMemcpyAsync(chunk_raw_out_dev, chunk_raw_in_dev, 4ull * nchunks, hipMemcpyDeviceToDevice, st));
+  if (n_blocks == 0) return H3C_OK;
+  if (!blk_chunk_dev || !blk_index_dev || !payload_dev || !out_raw_dev || !workspace_dev)
+    return H3C_ERR_INVALID_ARG;
+  if (((uintptr_t)payload_dev & 15) != 0) return H3C_ERR_INVALID_ARG;
+  int dev = 0;
+  int rc = h3c_rt::current_device(&dev);
+  if (rc) return rc;
+  const uint32_t bpc = (uint32_t)(chunk_len / block_bytes);
+  Workspace w{};
+  size_t need = 0;
+  rc = layout(workspace_dev, n_blocks, nchunks, bpc, w, need);
+  if (rc) return rc;
+  if (workspace_bytes < need) {
+    h3c_rt::set_error_text("h3c_update_blocks: workspace too small (see h3c_update_workspace_bytes)");
+    return H3C_ERR_INVALID_ARG;
+  }
+  const PolyConsts *pc = static_cast<const PolyConsts *>(h3c_rt::device_consts(dev, type));
+  const uint32_t num_cu = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
+  const uint32_t tb = 256, gb = (n_blocks + tb - 1) / tb;
+
+  HIP_TRY(hipMemsetAsync(w.err, 0, 4, st));
+  hipLaunchKernelGGL(upd_keys_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks, bpc,
+                     w.key1, w.key2, w.err);
+  HIP_TRY(hipGetLastError());
+  const uint32_t slot_bits = bits_for((uint64_t)nchunks * bpc + 1);  // + sentinel slot
+  size_t tmp = w.tmp_bytes;
+  HIP_TRY(rocprim::radix_sort_keys(w.tmp, tmp, w.key1, w.key1s, n_blocks, 0, 32 + slot_bits, st));
+  hipLaunchKernelGGL(upd_link_kernel, dim3(gb), dim3(tb), 0, st, w.key1s, n_blocks, w.prev, w.final_of);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(upd_shift_kernel, dim3((bpc + tb - 1) / tb), dim3(tb), 0, st, bpc, chunk_len, block_bytes, pc,
+                     w.sh);
+  HIP_TRY(hipGetLastError());
+  const uint32_t blocks = std::min<uint32_t>(num_cu, (n_blocks + kWavesPerBlock - 1) / kWavesPerBlock);
+  hipLaunchKernelGGL(upd_delta_kernel, dim3(blocks), dim3(kThreads), 0, st, chunk_base_dev, nchunks, bpc, block_bytes,
+                     blk_chunk_dev, blk_index_dev, static_cast<const uint8_t *>(payload_dev), n_blocks, w.prev,
+                     w.final_of, w.sh, pc, w.delta);
+  HIP_TRY(hipGetLastError());
+  tmp = w.tmp_bytes;
+  HIP_TRY(rocprim::radix_sort_keys(w.tmp, tmp, w.key2, w.key2s, n_blocks, 0, 32 + bits_for((uint64_t)nchunks + 1), st));
+  hipLaunchKernelGGL(upd_gather_kernel, dim3(gb), dim3(tb), 0, st, w.key2s, n_blocks, w.delta, w.ckey, w.vals);
+  HIP_TRY(hipGetLastError());
+  tmp = w.tmp_bytes;
+  HIP_TRY(rocprim::inclusive_scan_by_key(w.tmp, tmp, w.ckey, w.vals, w.scan, (size_t)n_blocks, XorOp(),
+                                         rocprim::equal_to<uint32_t>(), st));
+  hipLaunchKernelGGL(upd_scatter_kernel, dim3(gb), dim3(tb), 0, st, w.key2s, n_blocks, nchunks, w.scan, chunk_raw_in_dev,
+                     out_raw_dev, chunk_raw_out_dev);
+  HIP_TRY(hipGetLastError());
+  if (n_invalid_dev) HIP_TRY(hipMemcpyAsync(n_invalid_dev, w.err, 4, hipMemcpyDeviceToDevice, st));
+  return H3C_OK;
+}
+
+}  // extern "C"

@@ -32,6 +32,15 @@ if not os.path.exists(lib_path):
         "There is no CPU fallback."
     )
 
+# One HIP runtime per process: torch ships its own libamdhip64.so.7 (same soname as
+# /opt/rocm's).  Whichever is loaded first serves everyone, and two copies in one
+# process fight over the device ("no ROCm-capable device").  Load torch's first
+# when torch is present so tensors, streams and this library share it.
+try:  # pragma: no cover - import side effect only
+    import torch as _torch  # noqa: F401
+except ImportError:
+    _torch = None
+
 lib = ctypes.CDLL(lib_path)
 
 _u8, _u16, _u32, _u64 = ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64
@@ -71,6 +80,8 @@ _proto("h3c_plan_bytes", _u64, _vp)
 _proto("h3c_plan_destroy", None, _vp)
 _proto("h3c_batch_combine", _int, _u8, _vp, _vp, _vp, _sz, _vp, _vp)
 _proto("h3c_fill_splitmix", _int, _vp, _u64, _u64, _u64, _u64, _u64, _vp)
+_proto("h3c_update_workspace_bytes", _sz, _u32, _u32, _u64, _u32)
+_proto("h3c_update_blocks", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp)
 _proto("h3c_profile_enable", None, _int)
 _proto("h3c_profile_read", _int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64), ctypes.POINTER(_u64), _int)
 
@@ -242,6 +253,31 @@ def fill_splitmix(base, chunk_len: int, nchunks: int, stride: int, seed: int, fi
     """Bench/test utility: the same splitmix64 chunk generator as the oracle, written in HBM."""
     ptr = base if isinstance(base, int) else base.data_ptr()
     _check(lib.h3c_fill_splitmix(ptr, chunk_len, nchunks, stride, seed, first_chunk, _stream_handle(stream)))
+
+
+def update_workspace_bytes(n_blocks: int, nchunks: int, chunk_len: int, block_bytes: int = 4096) -> int:
+    return int(lib.h3c_update_workspace_bytes(n_blocks, nchunks, chunk_len, block_bytes))
+
+
+def update_blocks(chunk_bases, chunk_len: int, raw_in, blk_chunk, blk_index, payload, out_raw, raw_out,
+                  block_bytes: int = 4096, workspace=None, n_invalid=None, type_: int = ChecksumType.CRC32C,
+                  stream=None) -> None:
+    """Batched ChunkReplica::update + updateChecksum for block-aligned overwrites (h3c_update_blocks).
+
+    All tensors are on the GPU: chunk_bases int64[nchunks] (device addresses), raw_in /
+    raw_out int32[nchunks], blk_chunk / blk_index int32[n], payload uint8[n*block_bytes],
+    out_raw int32[n] (chunk checksum right after each block write)."""
+    import torch
+
+    n, nchunks = blk_chunk.numel(), chunk_bases.numel()
+    ws_bytes = update_workspace_bytes(n, nchunks, chunk_len, block_bytes)
+    if workspace is None:
+        workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=payload.device)
+    _check(lib.h3c_update_blocks(int(type_), chunk_bases.data_ptr(), nchunks, chunk_len, block_bytes,
+                                 raw_in.data_ptr(), blk_chunk.data_ptr(), blk_index.data_ptr(), payload.data_ptr(),
+                                 n, out_raw.data_ptr(), raw_out.data_ptr(), workspace.data_ptr(),
+                                 workspace.numel() * workspace.element_size(),
+                                 n_invalid.data_ptr() if n_invalid is not None else None, _stream_handle(stream)))
 
 
 def profile_enable(on: bool = True) -> None:

@@ -113,6 +113,31 @@ void h3c_plan_destroy(h3c_plan *p);
 int h3c_batch_combine(uint8_t type, const uint32_t *c1_dev, const uint32_t *c2_dev, const uint64_t *len2_dev,
                       size_t n, uint32_t *out_dev, void *stream);
 
+/* ---- batched partial updates (ChunkReplica::update + updateChecksum) ---- */
+
+/* Apply `n_blocks` block-aligned overwrites, in sequence order, to device-resident
+ * chunks and maintain their checksums, replacing the per-write prefix/suffix re-read
+ * + two crc32c_combine()s of ChunkReplica::updateChecksum case (iv)
+ * (src/storage/store/ChunkReplica.cc:356-390) with an O(write) GF(2) delta.
+ *   chunk_base_dev[c]      device address of chunk c (chunk_len bytes, fully written)
+ *   chunk_raw_in_dev[c]    its current raw checksum (ChunkMetadata.checksumValue)
+ *   block write i          overwrites block blk_index_dev[i] (block_bytes at offset
+ *                          blk_index*block_bytes) of chunk blk_chunk_dev[i] with
+ *                          payload_dev + i*block_bytes
+ *   out_raw_dev[i]         the chunk's raw checksum right after write i (what
+ *                          updateChecksum stores), chunk_raw_out_dev[c] the final one.
+ * block_bytes is a multiple of 1024 (3FS writes are 4 KiB-aligned, kAIOAlignSize).
+ * A multi-block write is expanded by the caller into consecutive block writes; its
+ * checksum is out_raw of its last block.  Out-of-range entries have no effect,
+ * out_raw 0, and are counted in *n_invalid_dev (optional).  The chunk bytes are
+ * updated in place.  All arrays are device memory; nothing is synchronised. */
+size_t h3c_update_workspace_bytes(uint32_t n_blocks, uint32_t nchunks, uint64_t chunk_len, uint32_t block_bytes);
+int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nchunks, uint64_t chunk_len,
+                      uint32_t block_bytes, const uint32_t *chunk_raw_in_dev, const uint32_t *blk_chunk_dev,
+                      const uint32_t *blk_index_dev, const void *payload_dev, uint32_t n_blocks,
+                      uint32_t *out_raw_dev, uint32_t *chunk_raw_out_dev, void *workspace_dev,
+                      size_t workspace_bytes, uint32_t *n_invalid_dev, void *stream);
+
 /* ---- utilities for benches/tests (not on the reference path) ---- */
 
 /* chunk i at base + i*stride gets u64 words splitmix64(seed ^ ((first_chunk+i)<<40) ^ k). */

@@ -1,0 +1,177 @@
+"""Batched partial updates on the GPU vs the reference's updateChecksum, replayed write by write.
+
+The oracle replays every write through its restatement of ChunkReplica::updateChecksum
+(src/storage/store/ChunkReplica.cc:319-394, case iv: prefix + write + suffix CRCs and two
+combines over the whole chunk) and the engine must reproduce the stored checksum after
+each write, the final chunk bytes, and the final checksums.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+
+pytestmark = pytest.mark.gpu
+MASK = 0xFFFFFFFF
+G = 4096
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available()
+    return torch, torch.device("cuda:0")
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def i32(arr, torch, dev):
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(arr, dtype=np.uint32)).view(np.int32)).to(dev)
+
+
+def run_case(h3c, torch, dev, nchunks, chunk_len, writes, seed, replay_chunks=None, invalid=()):
+    """writes: list of (chunk, first_block, nblocks).  Returns (ok, details)."""
+    rng = np.random.default_rng(seed)
+    bpc = chunk_len // G
+    chunks = rng.integers(0, 256, (nchunks, chunk_len), dtype=np.uint8)
+    raw0 = np.array([orc.crc32c(chunks[c]) for c in range(nchunks)], dtype=np.uint32)
+    # expand writes into block writes (sequence order); last block index of each write
+    blk_chunk, blk_index, last_of_write = [], [], []
+    for (c, b0, nb) in writes:
+        for k in range(nb):
+            blk_chunk.append(c)
+            blk_index.append(b0 + k)
+        last_of_write.append(len(blk_chunk) - 1)
+    for pos, (c, b) in invalid:  # out-of-range entries inserted at given positions
+        blk_chunk.insert(pos, c)
+        blk_index.insert(pos, b)
+        last_of_write = [x + (1 if x >= pos else 0) for x in last_of_write]
+    n = len(blk_chunk)
+    payload = rng.integers(0, 256, (n, G), dtype=np.uint8)
+
+    dchunks = torch.from_numpy(chunks.copy()).to(dev)
+    bases = torch.tensor([dchunks[c].data_ptr() for c in range(nchunks)], dtype=torch.int64, device=dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    raw_out = torch.zeros(nchunks, dtype=torch.int32, device=dev)
+    ninv = torch.zeros(1, dtype=torch.int32, device=dev)
+    h3c.update_blocks(bases, chunk_len, i32(raw0, torch, dev), i32(blk_chunk, torch, dev),
+                      i32(blk_index, torch, dev), torch.from_numpy(payload).to(dev), out, raw_out,
+                      block_bytes=G, n_invalid=ninv)
+    torch.cuda.synchronize()
+    got = u32(out)
+    got_final = u32(raw_out)
+    got_chunks = dchunks.cpu().numpy()
+
+    # Host replay, write by write, through the updateChecksum restatement.
+    host = chunks.copy()
+    meta = [{"size": chunk_len, "type": orc.CRC32C, "value": int(raw0[c])} for c in range(nchunks)]
+    want = {}
+    valid = [(c < nchunks and b < bpc) for c, b in zip(blk_chunk, blk_index)]
+    replay = set(range(nchunks)) if replay_chunks is None else set(replay_chunks)
+    i = 0
+    for w, (c, b0, nb) in enumerate(writes):
+        # indices of this write's block entries (skip invalid ones interleaved)
+        idx = []
+        while len(idx) < nb:
+            if valid[i]:
+                idx.append(i)
+            i += 1
+        data = np.concatenate([payload[j] for j in idx])
+        off = b0 * G
+        host[c, off: off + nb * G] = data
+        if c in replay:
+            wt, wv = orc.create(orc.CRC32C, data)
+            rc, meta[c] = orc.update_checksum(meta[c], {"offset": off, "length": nb * G, "type": wt, "value": wv},
+                                              chunk_len, off == chunk_len, host[c])
+            assert rc == 0
+            want[idx[-1]] = meta[c]["value"]
+    bad = [(k, hex(int(got[k])), hex(v)) for k, v in want.items() if int(got[k]) != v]
+    assert not bad, bad[:10]
+    assert np.array_equal(got_chunks, host), "chunk bytes after write-back"
+    for c in range(nchunks):
+        assert int(got_final[c]) == orc.crc32c(host[c]), c
+    for k, v in enumerate(valid):
+        if not v:
+            assert int(got[k]) == 0
+    assert int(ninv.item()) == sum(1 for v in valid if not v)
+
+
+def test_update_small_random_with_collisions(h3c, torch_dev):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(1)
+    nchunks, chunk_len = 6, 256 << 10  # 64 blocks per chunk -> many same-slot rewrites
+    writes = [(int(rng.integers(0, nchunks)), int(rng.integers(0, 64)), 1) for _ in range(2500)]
+    run_case(h3c, torch, dev, nchunks, chunk_len, writes, seed=2)
+
+
+def test_update_multiblock_and_reuse_and_invalid(h3c, torch_dev):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(3)
+    nchunks, chunk_len = 4, 128 << 10
+    writes = []
+    for _ in range(600):
+        c = int(rng.integers(0, nchunks))
+        nb = int(rng.integers(1, 6))
+        b0 = int(rng.integers(0, 32 - nb + 1))
+        writes.append((c, b0, nb))
+    writes.append((1, 0, 32))  # whole-chunk overwrite: updateChecksum's reuse case (:337-339)
+    writes.append((1, 3, 2))
+    run_case(h3c, torch, dev, nchunks, chunk_len, writes, seed=4,
+             invalid=[(5, (nchunks, 0)), (77, (0, 999)), (300, (7, 7))])
+
+
+def test_update_single_slot_hammer(h3c, torch_dev):
+    """Every write hits one slot: the longest possible previous-writer chain."""
+    torch, dev = torch_dev
+    run_case(h3c, torch, dev, 2, 64 << 10, [(1, 5, 1)] * 700 + [(0, 15, 1)] * 3, seed=5)
+
+
+def test_update_config3_shape_full_size(h3c, torch_dev):
+    """BASELINE config 3: 100k random 4 KiB writes into 64 x 64 MiB chunks.
+
+    Size-independent checks: every chunk's final checksum equals a fresh GPU create of
+    its final bytes, the bytes equal the host replay, and chunk 0 is replayed write by
+    write through the oracle's updateChecksum."""
+    torch, dev = torch_dev
+    nchunks, chunk_len, nw = 64, 64 << 20, 100_000
+    bpc = chunk_len // G
+    rng = np.random.default_rng(20250629)
+    wc = rng.integers(0, nchunks, nw).astype(np.uint32)
+    wb = rng.integers(0, bpc, nw).astype(np.uint32)
+    dchunks = torch.empty(nchunks * chunk_len, dtype=torch.uint8, device=dev)
+    h3c.fill_splitmix(dchunks, chunk_len, nchunks, chunk_len, 20250629)
+    payload = torch.empty(nw * G, dtype=torch.uint8, device=dev)
+    h3c.fill_splitmix(payload, G, nw, G, 777)
+    plan = h3c.Plan.uniform(dchunks.data_ptr(), chunk_len, nchunks)
+    raw0 = torch.zeros(nchunks, dtype=torch.int32, device=dev)
+    plan.run(raw0)
+    host0 = dchunks[:chunk_len].cpu().numpy().copy()  # chunk 0 before
+    bases = torch.tensor([dchunks.data_ptr() + c * chunk_len for c in range(nchunks)], dtype=torch.int64, device=dev)
+    out = torch.zeros(nw, dtype=torch.int32, device=dev)
+    raw_out = torch.zeros(nchunks, dtype=torch.int32, device=dev)
+    h3c.update_blocks(bases, chunk_len, raw0, i32(wc, torch, dev), i32(wb, torch, dev), payload, out, raw_out)
+    fresh = torch.zeros(nchunks, dtype=torch.int32, device=dev)
+    plan.run(fresh)
+    torch.cuda.synchronize()
+    assert torch.equal(fresh, raw_out)
+    got = u32(out)
+    # chunk 0, write by write, through the oracle's updateChecksum (case iv over 64 MiB)
+    pay = payload.cpu().numpy().reshape(nw, G)
+    host = host0
+    meta = {"size": chunk_len, "type": orc.CRC32C, "value": int(u32(raw0)[0])}
+    idx = np.nonzero(wc == 0)[0]
+    for k in idx[:200]:  # each replay step CRCs 64 MiB on the host
+        off = int(wb[k]) * G
+        host[off: off + G] = pay[k]
+        wt, wv = orc.create(orc.CRC32C, pay[k])
+        rc, meta = orc.update_checksum(meta, {"offset": off, "length": G, "type": wt, "value": wv},
+                                       chunk_len, False, host)
+        assert rc == 0 and int(got[k]) == meta["value"], k
+    # last write of every chunk == its final checksum
+    fin = u32(raw_out)
+    for c in range(nchunks):
+        last = np.nonzero(wc == c)[0][-1]
+        assert int(got[last]) == int(fin[c])
+    plan.close()
