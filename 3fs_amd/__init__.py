@@ -15,6 +15,7 @@ from .engine import (  # noqa: F401
     ChecksumInfo,
     ChecksumType,
     EngineError,
+    HostFed,
     Plan,
     StatusCode,
     batch_create,
@@ -37,6 +38,7 @@ __all__ = [
     "ChecksumInfo",
     "ChecksumType",
     "EngineError",
+    "HostFed",
     "Plan",
     "StatusCode",
     "batch_create",

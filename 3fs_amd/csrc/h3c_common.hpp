@@ -20,6 +20,32 @@ int device_num_cu(int dev);
 int current_device(int *dev);
 void set_error(const char *what, hipError_t e);
 void set_error_text(const char *text);
+// Profiling hooks (h3c_profile_enable): event pair around a launch, per kind.
+struct ProfToken {
+  bool on = false;
+  hipEvent_t a = nullptr, b = nullptr;
+};
+hipError_t prof_begin(hipStream_t st, ProfToken &t);
+hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes);
+
+// Device copy of a descriptor (32 B).
+struct DevChunk {
+  uint64_t ptr;
+  uint64_t len;
+  uint32_t start;
+  uint32_t out_idx;
+  uint32_t seg_begin;
+  uint32_t flags;  // bit0: result is {NONE,0}
+};
+constexpr uint32_t kFlagNone = 1u;
+
+// Segment-CRC + finalize launches over `nchunks` device descriptors (one polynomial
+// group); profiled as `prof_kind` when >= 0.  Defined in h3c_engine.hip.
+int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint32_t nchunks, uint32_t total_segs,
+               uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc, const uint32_t *expected,
+               uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind);
+// Segment size the engine picks for a batch of `total_bytes` on device `dev`.
+uint64_t pick_seg(uint64_t total_bytes, int dev);
 }  // namespace h3c_rt
 
 #define HIP_TRY(expr)               \
@@ -98,16 +124,8 @@ inline void build_consts(PolyConsts &pc, uint32_t poly) {
   }
 }
 
-// Device copy of a descriptor (32 B).
-struct DevChunk {
-  uint64_t ptr;
-  uint64_t len;
-  uint32_t start;
-  uint32_t out_idx;
-  uint32_t seg_begin;
-  uint32_t flags;  // bit0: result is {NONE,0}
-};
-constexpr uint32_t kFlagNone = 1u;
+using h3c_rt::DevChunk;
+using h3c_rt::kFlagNone;
 
 // ---------------------------------------------------------------- device GF(2)
 __device__ __forceinline__ uint32_t dgf_mul(uint32_t a, uint32_t b, uint32_t poly) {

@@ -147,6 +147,7 @@ __global__ void fill_kernel(uint8_t *base, uint64_t chunk_words, uint64_t nchunk
 
 // ---------------------------------------------------------------- host runtime
 thread_local std::string g_last_error;
+uint64_t pick_seg_bytes(uint64_t total_bytes, int num_cu);
 
 void set_error(const char *what, hipError_t e) {
   char buf[512];
@@ -211,16 +212,65 @@ void set_error_text(const char *text) { g_last_error = text; }
 
 namespace {
 
-// ---- profiling (events around seg_crc_kernel) ----
+// ---- profiling: HIP event pairs around the hot kernels, per kind ----
 struct ProfRec {
   hipEvent_t a, b;
   uint64_t bytes;
+  int kind;
 };
+constexpr int kProfKinds = 3;
 std::mutex g_prof_mu;
 std::vector<ProfRec> g_prof;
 std::atomic<int> g_prof_on{0};
-double g_prof_ms_done = 0;
-uint64_t g_prof_launch_done = 0, g_prof_bytes_done = 0;
+double g_prof_ms_done[kProfKinds] = {0, 0, 0};
+uint64_t g_prof_launch_done[kProfKinds] = {0, 0, 0}, g_prof_bytes_done[kProfKinds] = {0, 0, 0};
+
+}  // namespace
+
+namespace h3c_rt {
+hipError_t prof_begin(hipStream_t st, ProfToken &t) {
+  t.on = g_prof_on.load() != 0;
+  if (!t.on) return hipSuccess;
+  hipError_t e = hipEventCreate(&t.a);
+  if (e == hipSuccess) e = hipEventCreate(&t.b);
+  if (e == hipSuccess) e = hipEventRecord(t.a, st);
+  return e;
+}
+hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes) {
+  if (!t.on) return hipSuccess;
+  hipError_t e = hipEventRecord(t.b, st);
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof.push_back(ProfRec{t.a, t.b, bytes, kind});
+  return e;
+}
+
+int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint32_t nchunks, uint32_t total_segs,
+               uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc, const uint32_t *expected,
+               uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind) {
+  const DeviceCtx &ctx = g_dev[dev];
+  const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
+  const uint32_t poly = type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
+  if (total_segs) {
+    const uint32_t blocks = std::min<uint32_t>(ctx.num_cu, (total_segs + kWavesPerBlock - 1) / kWavesPerBlock);
+    ProfToken tok;
+    if (prof_kind >= 0) HIP_TRY(prof_begin(st, tok));
+    hipLaunchKernelGGL(seg_crc_kernel, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, total_segs, seg_bytes,
+                       dbg, pc, d_segcrc);
+    HIP_TRY(hipGetLastError());
+    if (prof_kind >= 0) HIP_TRY(prof_end(st, tok, prof_kind, payload_bytes));
+  }
+  const uint32_t seg_mul = hxpow8n(seg_bytes, poly);
+  const uint32_t fb = (nchunks + 255) / 256;
+  hipLaunchKernelGGL(finalize_kernel, dim3(fb), dim3(256), 0, st, d_chunks, nchunks, total_segs, seg_bytes, seg_mul, pc,
+                     d_segcrc, expected, out_raw, ok, mismatch);
+  HIP_TRY(hipGetLastError());
+  return H3C_OK;
+}
+
+uint64_t pick_seg(uint64_t total_bytes, int dev) { return pick_seg_bytes(total_bytes, device_num_cu(dev)); }
+}  // namespace h3c_rt
+
+namespace {
 
 // test hook: H3C_DEBUG_FLAGS bit0 disables the pipelined row loop (read per plan)
 uint32_t read_dbg_flags() {
@@ -281,26 +331,27 @@ const char *h3c_last_error(void) { return g_last_error.c_str(); }
 
 void h3c_profile_enable(int on) { g_prof_on.store(on ? 1 : 0); }
 
-int h3c_profile_read(double *seg_kernel_ms, uint64_t *seg_launches, uint64_t *seg_bytes, int reset) {
+int h3c_profile_read(int kind, double *kernel_ms, uint64_t *launches, uint64_t *bytes, int reset) {
+  if (kind < 0 || kind >= kProfKinds) return H3C_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(g_prof_mu);
   for (auto &r : g_prof) {
     HIP_TRY(hipEventSynchronize(r.b));
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
-    g_prof_ms_done += ms;
-    g_prof_launch_done += 1;
-    g_prof_bytes_done += r.bytes;
+    g_prof_ms_done[r.kind] += ms;
+    g_prof_launch_done[r.kind] += 1;
+    g_prof_bytes_done[r.kind] += r.bytes;
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
   }
   g_prof.clear();
-  if (seg_kernel_ms) *seg_kernel_ms = g_prof_ms_done;
-  if (seg_launches) *seg_launches = g_prof_launch_done;
-  if (seg_bytes) *seg_bytes = g_prof_bytes_done;
+  if (kernel_ms) *kernel_ms = g_prof_ms_done[kind];
+  if (launches) *launches = g_prof_launch_done[kind];
+  if (bytes) *bytes = g_prof_bytes_done[kind];
   if (reset) {
-    g_prof_ms_done = 0;
-    g_prof_launch_done = 0;
-    g_prof_bytes_done = 0;
+    g_prof_ms_done[kind] = 0;
+    g_prof_launch_done[kind] = 0;
+    g_prof_bytes_done[kind] = 0;
   }
   return H3C_OK;
 }
@@ -418,34 +469,11 @@ int h3c_plan_run(h3c_plan *p, const uint32_t *expected_raw_dev, uint32_t *out_ra
   if (prev != p->device) HIP_TRY(hipSetDevice(p->device));
   const DeviceCtx &ctx = g_dev[p->device];
   int rc = H3C_OK;
+  (void)ctx;
   for (const Group &g : p->groups) {
-    const PolyConsts *pc = ctx.d_consts[g.type == H3C_TYPE_CRC32 ? 1 : 0];
-    const uint32_t poly = g.type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
-    if (g.total_segs) {
-      const uint32_t blocks =
-          std::min<uint32_t>(ctx.num_cu, (g.total_segs + kWavesPerBlock - 1) / kWavesPerBlock);
-      const bool prof = g_prof_on.load() != 0;
-      ProfRec rec{};
-      if (prof) {
-        HIP_TRY(hipEventCreate(&rec.a));
-        HIP_TRY(hipEventCreate(&rec.b));
-        HIP_TRY(hipEventRecord(rec.a, st));
-      }
-      hipLaunchKernelGGL(seg_crc_kernel, dim3(blocks), dim3(kThreads), 0, st, g.d_chunks, g.nchunks, g.total_segs,
-                         p->seg_bytes, p->dbg, pc, p->d_segcrc);
-      HIP_TRY(hipGetLastError());
-      if (prof) {
-        HIP_TRY(hipEventRecord(rec.b, st));
-        rec.bytes = g.bytes;
-        std::lock_guard<std::mutex> lk(g_prof_mu);
-        g_prof.push_back(rec);
-      }
-    }
-    const uint32_t seg_mul = hxpow8n(p->seg_bytes, poly);
-    const uint32_t fb = (g.nchunks + 255) / 256;
-    hipLaunchKernelGGL(finalize_kernel, dim3(fb), dim3(256), 0, st, g.d_chunks, g.nchunks, g.total_segs,
-                       p->seg_bytes, seg_mul, pc, p->d_segcrc, expected_raw_dev, out_raw_dev, ok_dev, mismatch_dev);
-    HIP_TRY(hipGetLastError());
+    rc = h3c_rt::launch_crc(st, p->device, g.type, g.d_chunks, g.nchunks, g.total_segs, g.bytes, p->seg_bytes,
+                            p->dbg, p->d_segcrc, expected_raw_dev, out_raw_dev, ok_dev, mismatch_dev, H3C_PROF_SEG);
+    if (rc) break;
   }
   if (prev != p->device) HIP_TRY(hipSetDevice(prev));
   return rc;

@@ -298,10 +298,14 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
                      w.sh);
   HIP_TRY(hipGetLastError());
   const uint32_t blocks = std::min<uint32_t>(num_cu, (n_blocks + kWavesPerBlock - 1) / kWavesPerBlock);
+  h3c_rt::ProfToken tok;
+  HIP_TRY(h3c_rt::prof_begin(st, tok));
   hipLaunchKernelGGL(upd_delta_kernel, dim3(blocks), dim3(kThreads), 0, st, chunk_base_dev, nchunks, bpc, block_bytes,
                      blk_chunk_dev, blk_index_dev, static_cast<const uint8_t *>(payload_dev), n_blocks, w.prev,
                      w.final_of, w.sh, pc, w.delta);
   HIP_TRY(hipGetLastError());
+  // algorithmic bytes: read new + read old + write back, per block write
+  HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDATE, 3ull * block_bytes * n_blocks));
   tmp = w.tmp_bytes;
   HIP_TRY(rocprim::radix_sort_keys(w.tmp, tmp, w.key2, w.key2s, n_blocks, 0, 32 + bits_for((uint64_t)nchunks + 1), st));
   hipLaunchKernelGGL(upd_gather_kernel, dim3(gb), dim3(tb), 0, st, w.key2s, n_blocks, w.delta, w.ckey, w.vals);

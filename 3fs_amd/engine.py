@@ -82,8 +82,14 @@ _proto("h3c_batch_combine", _int, _u8, _vp, _vp, _vp, _sz, _vp, _vp)
 _proto("h3c_fill_splitmix", _int, _vp, _u64, _u64, _u64, _u64, _u64, _vp)
 _proto("h3c_update_workspace_bytes", _sz, _u32, _u32, _u64, _u32)
 _proto("h3c_update_blocks", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp)
+_proto("h3c_hostfed_create", _int, _int, _u64, ctypes.POINTER(_vp))
+_proto("h3c_hostfed_run", _int, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp)
+_proto("h3c_hostfed_destroy", None, _vp)
 _proto("h3c_profile_enable", None, _int)
-_proto("h3c_profile_read", _int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64), ctypes.POINTER(_u64), _int)
+_proto("h3c_profile_read", _int, _int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64), ctypes.POINTER(_u64),
+       _int)
+
+PROF_SEG, PROF_UPDATE, PROF_HOSTFED = 0, 1, 2
 
 
 class ChecksumType(enum.IntEnum):
@@ -284,9 +290,11 @@ def profile_enable(on: bool = True) -> None:
     lib.h3c_profile_enable(1 if on else 0)
 
 
-def profile_read(reset: bool = False) -> Tuple[float, int, int]:
+def profile_read(reset: bool = False, kind: int = PROF_SEG) -> Tuple[float, int, int]:
+    """(summed ms, launches, algorithmic bytes) of the profiled launches of `kind`."""
     ms, launches, nbytes = ctypes.c_double(0), _u64(0), _u64(0)
-    _check(lib.h3c_profile_read(ctypes.byref(ms), ctypes.byref(launches), ctypes.byref(nbytes), 1 if reset else 0))
+    _check(lib.h3c_profile_read(kind, ctypes.byref(ms), ctypes.byref(launches), ctypes.byref(nbytes),
+                                1 if reset else 0))
     return ms.value, int(launches.value), int(nbytes.value)
 
 
@@ -326,6 +334,45 @@ class Plan:
     def close(self) -> None:
         if self._h:
             lib.h3c_plan_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HostFed:
+    """Host-fed pipeline (h3c_hostfed_*): payloads in (pinned) host memory, H2D copies
+    double-buffered against the CRC kernels."""
+
+    def __init__(self, device: int = 0, window_bytes: int = 64 << 20):
+        self._h = _vp()
+        self.device = device
+        _check(lib.h3c_hostfed_create(device, window_bytes, ctypes.byref(self._h)))
+
+    def run(self, items: Sequence, expected: Optional[Sequence[int]] = None, type_: int = ChecksumType.CRC32C,
+            start: int = 0xFFFFFFFF, stream=None):
+        """Returns raw uint32[n] (create), or (raw, ok bool[n], n_mismatch) with `expected`."""
+        descs, keep = _desc_array(items, type_, start)
+        n = len(descs)
+        out = np.zeros(n, dtype=np.uint32)
+        if expected is None:
+            _check(lib.h3c_hostfed_run(self._h, descs.ctypes.data, n, None, out.ctypes.data, None, None,
+                                       _stream_handle(stream)))
+            return out
+        exp = np.ascontiguousarray(np.asarray(expected, dtype=np.uint32))
+        ok = np.zeros(n, dtype=np.uint8)
+        mis = _u64(0)
+        _check(lib.h3c_hostfed_run(self._h, descs.ctypes.data, n, exp.ctypes.data, out.ctypes.data, ok.ctypes.data,
+                                   ctypes.addressof(mis), _stream_handle(stream)))
+        del keep
+        return out, ok.astype(bool), int(mis.value)
+
+    def close(self) -> None:
+        if self._h:
+            lib.h3c_hostfed_destroy(self._h)
             self._h = _vp()
 
     def __del__(self):  # pragma: no cover

@@ -138,17 +138,36 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
                       uint32_t *out_raw_dev, uint32_t *chunk_raw_out_dev, void *workspace_dev,
                       size_t workspace_bytes, uint32_t *n_invalid_dev, void *stream);
 
+/* ---- host-fed pipeline (payloads in host memory, BASELINE config 5) ---- */
+
+/* A reusable pipeline: two HBM staging windows of `window_bytes` and a copy stream.
+ * h3c_hostfed_run streams the host payloads of `d` (pinned memory recommended:
+ * hipHostMalloc / hipHostRegister'd RDMA buffers) through the windows, overlapping
+ * H2D copies with the CRC kernels, and returns ChecksumInfo::create values (and, with
+ * `expected`, verify flags) in host arrays.  Blocks until done.  One polynomial per
+ * run.  A pipeline object must not be used by two threads at once. */
+typedef struct h3c_hostfed h3c_hostfed;
+int h3c_hostfed_create(int device, uint64_t window_bytes, h3c_hostfed **out);
+int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t *expected_raw, uint32_t *out_raw,
+                    uint8_t *ok, uint64_t *n_mismatch, void *stream);
+void h3c_hostfed_destroy(h3c_hostfed *h);
+
 /* ---- utilities for benches/tests (not on the reference path) ---- */
 
 /* chunk i at base + i*stride gets u64 words splitmix64(seed ^ ((first_chunk+i)<<40) ^ k). */
 int h3c_fill_splitmix(void *base_dev, uint64_t chunk_len, uint64_t nchunks, uint64_t stride, uint64_t seed,
                       uint64_t first_chunk, void *stream);
 
-/* When enabled, the engine brackets every segment-CRC kernel launch with HIP
- * events on the launch stream.  h3c_profile_read synchronises those events and
- * returns the summed kernel time, launch count and payload bytes. */
+/* When enabled, the engine brackets its hot launches with HIP events on the
+ * launch stream.  h3c_profile_read(kind) synchronises those events and returns the
+ * summed time, launch count and algorithmic bytes of that kind. */
+enum h3c_prof_kind {
+  H3C_PROF_SEG = 0,     /* seg_crc_kernel: payload bytes read */
+  H3C_PROF_UPDATE = 1,  /* upd_delta_kernel: 3 x block bytes per block write */
+  H3C_PROF_HOSTFED = 2  /* whole host-fed pipeline (H2D + CRC): payload bytes */
+};
 void h3c_profile_enable(int on);
-int h3c_profile_read(double *seg_kernel_ms, uint64_t *seg_launches, uint64_t *seg_bytes, int reset);
+int h3c_profile_read(int kind, double *ms, uint64_t *launches, uint64_t *bytes, int reset);
 
 #ifdef __cplusplus
 }

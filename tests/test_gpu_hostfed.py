@@ -1,0 +1,75 @@
+"""Host-fed pipeline (BASELINE config 5 shapes) vs the oracle: payloads in host memory."""
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available()
+    return torch, torch.device("cuda:0")
+
+
+def mixed_lengths(rng, n):
+    lens = []
+    for i in range(n):
+        L = (64 << 10) << int(rng.integers(0, 9))  # 64 KiB .. 16 MiB here (sizes bounded for the test)
+        if i % 10 == 3:
+            L -= int(rng.integers(1, 5000))  # ragged tail
+        lens.append(L)
+    return lens
+
+
+@pytest.mark.parametrize("window", [1 << 20, 8 << 20, 64 << 20])
+def test_hostfed_pinned_contiguous(h3c, torch_dev, window):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(window)
+    lens = mixed_lengths(rng, 40)
+    total = sum(lens)
+    pinned = torch.from_numpy(rng.integers(0, 256, total + 64, dtype=np.uint8)).pin_memory()
+    host = pinned.numpy()
+    items, want, off = [], [], 3  # odd start: unaligned host pointers
+    for L in lens:
+        items.append((pinned[off: off + L], L))
+        want.append(orc.crc32c(host[off: off + L]))
+        off += L
+    hf = h3c.HostFed(0, window)
+    got = hf.run(items)
+    assert [int(x) for x in got] == want
+    exp = np.array(want, dtype=np.uint32)
+    bad = [1, 7, 30]
+    exp[bad] ^= 0x10
+    raw, ok, nbad = hf.run(items, expected=exp)
+    assert nbad == 3 and sorted(np.nonzero(~ok)[0].tolist()) == bad
+    hf.close()
+
+
+def test_hostfed_scattered_pageable_and_semantics(h3c, torch_dev):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(9)
+    T = h3c.ChecksumType
+    bufs = [rng.integers(0, 256, int(n), dtype=np.uint8) for n in (0, 1, 15, 1024, 4096 + 3, 3 << 20, 1 << 20)]
+    items = [(b, b.size, 0xFFFFFFFF, T.CRC32C) for b in bufs]
+    items.append((None, 10, 0xFFFFFFFF, T.CRC32C))  # null -> NONE -> 0
+    items.append((bufs[5], 100, 0x1234, T.NONE))  # NONE -> 0
+    items.append((bufs[5], bufs[5].size, 0x5678, T.CRC32C))  # custom start
+    hf = h3c.HostFed(0, 1 << 20)
+    got = hf.run(items)
+    want = [orc.crc32c(b) for b in bufs] + [0, 0, orc.crc32c(bufs[5], 0x5678)]
+    assert [int(x) for x in got] == want
+    hf.close()
+
+
+def test_hostfed_crc32_type(h3c, torch_dev):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(4)
+    bufs = [rng.integers(0, 256, int(n), dtype=np.uint8) for n in (77, 5 << 20, 999999)]
+    hf = h3c.HostFed(0, 2 << 20)
+    got = hf.run(bufs, type_=h3c.ChecksumType.CRC32)
+    assert [int(x) for x in got] == [orc.crc32(b) for b in bufs]
+    hf.close()
