@@ -1,16 +1,23 @@
 #!/usr/bin/env python3
-"""Headline bench: GiB/s of CRC32C-verified 1 MiB chunks (BASELINE.json config 2).
+"""Benchmarks of the MI355X chunk-checksum engine (BASELINE.json configs).
 
-A step = one batch verify of 8192 x 1 MiB device-resident chunks per GPU
-(recompute every chunk's CRC32C, compare against the stored value, count
-mismatches) -- the ChunkReplica::update / AioReadJob::setResult recalculate
-path (src/storage/store/ChunkReplica.cc:193-207, src/storage/aio/BatchReadJob.cc:43-54)
-batched.  Inputs are resident in HBM before the timed region starts.
+Default (the headline, BASELINE config 2): a step = one batch verify of 8192 x 1 MiB
+device-resident chunks per GPU -- recompute every chunk's CRC32C, compare with the
+stored value, count mismatches.  That is ChunkReplica::update's payload verify /
+AioReadJob::setResult's recalculate path (src/storage/store/ChunkReplica.cc:193-207,
+src/storage/aio/BatchReadJob.cc:43-54) batched.  Inputs are resident in HBM before
+the timed region starts.
 
-Multi-GPU: one process per GPU (torchrun), each verifies its own 8192-chunk
-shard; there is no data-path collective (weak scaling).  torch.distributed is
-used only for the barrier and the max-over-ranks time.
+Other workloads (--workload), each printing its own JSON line:
+  update   BASELINE config 3: 100k random 4 KiB writes into 64 x 64 MiB chunks,
+           per-write chunk checksum (ChunkReplica::updateChecksum) -> writes/s
+  hostfed  BASELINE config 5: mixed 64 KiB-64 MiB chunks in pinned host memory,
+           H2D double-buffered against the CRC -> GiB/s (PCIe-inclusive)
+  shard4m  BASELINE config 4: 256 GiB as 4 MiB chunks split over the ranks (strong
+           scaling), generated in HBM in passes
 
+Multi-GPU: one process per GPU (torchrun); chunks are sharded, there is no data-path
+collective.  torch.distributed is used only for the barrier and max-over-ranks time.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -30,14 +37,15 @@ sys.path.insert(0, ROOT)
 
 SEED = 20250629
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
+PCIE_SPEC_GBPS = 63.0  # PCIe Gen5 x16 (spec)
+METRIC = "GiB/s CRC32C verified (1 MiB chunks) at 1/2/4/8 GPUs; % of HBM peak"
 
 
-def cpu_baseline(gpu_raw_first: np.ndarray, chunk_len: int, seconds: float = 8.0) -> dict:
-    """Reference CPU path restated (oracle/, folly-faithful 3-stream SSE4.2 crc32q) on this host.
+# --------------------------------------------------------------------------- helpers
 
-    Sample: 1024 x 1 MiB splitmix chunks (BASELINE config 1), ChecksumInfo::create
-    semantics, 1 host thread, repeated for ~`seconds`.  The same pass also checks
-    the GPU's values for those chunk indices."""
+
+def _oracle():
+    """CPU oracle library (oracle/) -- used only by the cpu_baseline legs."""
     so = os.path.join(ROOT, "oracle", "build", "liboracle.so")
     if not os.path.exists(so):
         import subprocess
@@ -47,6 +55,26 @@ def cpu_baseline(gpu_raw_first: np.ndarray, chunk_len: int, seconds: float = 8.0
     L.orc_fill_splitmix.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
     L.orc_batch_crc32c.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                    ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    return L
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(gpu_raw_first: np.ndarray, chunk_len: int, seconds: float = 8.0) -> dict:
+    """Reference CPU path restated (oracle/, folly-faithful 3-stream SSE4.2 crc32q) on this host.
+
+    Sample: 1024 x 1 MiB splitmix chunks (BASELINE config 1), ChecksumInfo::create
+    semantics, 1 host thread, repeated for ~`seconds`.  The same pass also checks
+    the GPU's values for those chunk indices."""
+    L = _oracle()
     n = 1024
     host = np.empty(n * chunk_len, dtype=np.uint8)
     for c in range(n):
@@ -61,7 +89,6 @@ def cpu_baseline(gpu_raw_first: np.ndarray, chunk_len: int, seconds: float = 8.0
         if el >= seconds:
             break
     gibps = reps * n * chunk_len / el / 2**30
-    match = bool(np.array_equal(out, gpu_raw_first[:n]))
     return {
         "value": round(gibps, 3),
         "unit": "GiB/s",
@@ -69,17 +96,17 @@ def cpu_baseline(gpu_raw_first: np.ndarray, chunk_len: int, seconds: float = 8.0
         "kind": "port",
         "sample": f"{reps} x (1024 x {chunk_len >> 20} MiB splitmix chunks), folly-faithful 3-way SSE4.2 crc32q, "
                   f"1 thread, {el:.1f} s",
-        "gpu_values_match": match,
+        "gpu_values_match": bool(np.array_equal(out, gpu_raw_first[:n])),
         "cpu_model": _cpu_model(),
         "nproc": os.cpu_count(),
     }
 
 
-def pmc_traffic(bytes_per_launch: int):
-    """HBM bytes per seg_crc_kernel launch from the committed rocprofv3 PMC summary
-    (profiles/*_pmc_summary.json, made by scripts/profile_r1.sh + summarize_prof.py,
-    FETCH_SIZE/WRITE_SIZE in separate passes, gfx950 FETCH_SIZE x2 correction).
-    Only used when that profile was taken on this same per-launch workload."""
+def pmc_traffic(bytes_per_launch: int, kernel: str = "seg_crc_kernel"):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/*_pmc_summary.json,
+    scripts/profile_r1.sh + summarize_prof.py: FETCH_SIZE / WRITE_SIZE in separate passes,
+    gfx950 FETCH_SIZE x2).  Only used when that profile was taken on this same per-launch
+    workload."""
     import glob
 
     best = None
@@ -88,20 +115,331 @@ def pmc_traffic(bytes_per_launch: int):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
+        if d.get("kernel", "seg_crc_kernel") != kernel:
+            continue
         t = d.get("pmc", {}).get("traffic_bytes_per_launch")
         if t and abs(d.get("algorithmic_bytes_per_launch", 0) - bytes_per_launch) < 1:
             best = (t, os.path.basename(f))
     return best
 
 
-def _cpu_model() -> str:
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
+class Ctx:
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world > 1:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.local}"))
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device(f"cuda:{self.local}")
+        self.h3c = importlib.import_module("3fs_amd")
+        self.stream = torch.cuda.current_stream()
+
+    def barrier(self):
+        self.torch.cuda.synchronize()
+        if self.world > 1:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def max_over_ranks(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def all_true(self, b: bool) -> bool:
+        if self.world == 1:
+            return b
+        t = self.torch.tensor([1 if b else 0], dtype=self.torch.int32, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    def timed(self, step, steps: int, warmup: int, kind: int):
+        """warmup, barrier, time `steps` calls (max over ranks); returns (elapsed_s, prof)."""
+        for _ in range(warmup):
+            step()
+        self.barrier()
+        self.h3c.profile_read(reset=True, kind=kind)
+        self.h3c.profile_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        self.barrier()
+        t1 = time.perf_counter()
+        self.h3c.profile_enable(False)
+        prof = self.h3c.profile_read(reset=True, kind=kind)
+        return self.max_over_ranks(t1 - t0), prof
+
+
+def roofline(prof, peak: float, unit: str = "GB/s", bound: str = "hbm", kernel: str = "seg_crc_kernel"):
+    ms, launches, nbytes = prof
+    per = nbytes / max(launches, 1)
+    avg_s = ms / 1e3 / max(launches, 1)
+    achieved = per / avg_s / 1e9 if launches and avg_s > 0 else 0.0
+    r = {"bound": bound, "achieved": round(achieved, 1), "peak": peak, "unit": unit,
+         "frac": round(achieved / peak, 4), "traffic": None, "kernel": kernel,
+         "kernel_avg_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": int(per)}
+    tr = pmc_traffic(int(per), kernel)
+    if tr:
+        r["traffic"] = int(tr[0])
+        r["traffic_source"] = f"profiles/{tr[1]}"
+    return r
+
+
+# --------------------------------------------------------------------------- workloads
+
+
+def run_verify(args, cx: Ctx) -> dict:
+    torch, h3c = cx.torch, cx.h3c
+    n, clen = args.chunks, args.chunk_kib << 10
+    buf = torch.empty(n * clen, dtype=torch.uint8, device=cx.dev)
+    h3c.fill_splitmix(buf, clen, n, clen, SEED, first_chunk=cx.rank * n)  # rank r: chunks [r*n, (r+1)*n)
+    torch.cuda.synchronize()
+    plan = h3c.Plan.uniform(buf.data_ptr(), clen, n, device=cx.local)
+    # Stored checksums = a create pass; then corrupt flip_frac of the chunks.
+    stored = torch.zeros(n, dtype=torch.int32, device=cx.dev)
+    plan.run(stored, stream=cx.stream)
+    torch.cuda.synchronize()
+    stored_host = stored.cpu().numpy().view(np.uint32).copy()
+    g = torch.Generator().manual_seed(SEED + cx.rank)
+    nflip = int(n * args.flip_frac)
+    flips = torch.randperm(n, generator=g)[:nflip].sort().values
+    pos = flips * clen + torch.randint(0, clen, (nflip,), generator=g)
+    bits = (1 << torch.randint(0, 8, (nflip,), generator=g)).to(torch.uint8)
+    pos_d = pos.to(cx.dev)
+    buf[pos_d] ^= bits.to(cx.dev)
+
+    out = torch.zeros(n, dtype=torch.int32, device=cx.dev)
+    ok = torch.zeros(n, dtype=torch.uint8, device=cx.dev)
+    mis = torch.zeros(1, dtype=torch.int32, device=cx.dev)
+
+    def step():
+        mis.zero_()
+        plan.run(out, expected=stored, ok=ok, mismatch=mis, stream=cx.stream)
+
+    elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_SEG)
+    bad = np.nonzero(ok.cpu().numpy() == 0)[0]
+    verified = cx.all_true(int(mis.item()) == nflip and np.array_equal(bad, flips.numpy()))
+    plan.close()
+    value = n * clen * args.steps * cx.world / elapsed / 2**30
+    res = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": cx.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 chunks generated in HBM; 5% of chunks carry one flipped bit)",
+        "config": {
+            "workload": f"batched CRC32C verify of {n} x {clen >> 10} KiB device-resident chunks per GPU "
+                        f"(BASELINE config 2)",
+            "chunks_per_gpu": n,
+            "chunk_bytes": clen,
+            "parallelism": f"shard{cx.world}",
+        },
+        "verified": verified,
+        "pct_hbm_peak": round(100.0 * (n * clen) / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 2),
+        "roofline": roofline(prof, HBM_PEAK_GBPS),
+    }
+    if cx.world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(stored_host, clen, args.cpu_seconds)
+    return res
+
+
+def cpu_baseline_update(samples: int = 40) -> dict:
+    """The reference algorithm on the host: ChunkReplica::updateChecksum case (iv) for a 4 KiB
+    overwrite of a 64 MiB chunk = CRC of the prefix + suffix (the whole chunk minus the write)
+    + CRC of the write + 2 combines, prefix/suffix read from memory (not disk).  Timed on
+    `samples` writes and extrapolated to writes/s."""
+    L = _oracle()
+    L.orc_crc32c_sse42_3way.restype = ctypes.c_uint32
+    L.orc_crc32c_sse42_3way.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32]
+    L.orc_crc32c_combine.restype = ctypes.c_uint32
+    L.orc_crc32c_combine.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+    clen, G = 64 << 20, 4096
+    chunk = np.empty(clen, dtype=np.uint8)
+    L.orc_fill_splitmix(chunk.ctypes.data, clen, SEED, 0)
+    rng = np.random.default_rng(1)
+    offs = rng.integers(0, clen // G, samples) * G
+    base = chunk.ctypes.data
+    t0 = time.perf_counter()
+    for off in offs:
+        off = int(off)
+        pre = L.orc_crc32c_sse42_3way(base, off, 0xFFFFFFFF)
+        w = L.orc_crc32c_sse42_3way(base + off, G, 0xFFFFFFFF)
+        suf = L.orc_crc32c_sse42_3way(base + off + G, clen - off - G, 0xFFFFFFFF)
+        v = L.orc_crc32c_combine((~pre) & 0xFFFFFFFF, w, G)
+        v = L.orc_crc32c_combine((~v) & 0xFFFFFFFF, suf, clen - off - G)
+    el = time.perf_counter() - t0
+    return {"value": round(samples / el, 2), "unit": "writes/s", "cores": 1, "kind": "port",
+            "sample": f"{samples} writes of 4 KiB into a 64 MiB chunk via updateChecksum case (iv) "
+                      f"(prefix+write+suffix CRC, 2 combines), {el:.2f} s, extrapolated",
+            "cpu_model": _cpu_model()}
+
+
+def run_update(args, cx: Ctx) -> dict:
+    torch, h3c = cx.torch, cx.h3c
+    nchunks, clen, nw, G = 64, 64 << 20, args.writes, 4096
+    bpc = clen // G
+    chunks = torch.empty(nchunks * clen, dtype=torch.uint8, device=cx.dev)
+    h3c.fill_splitmix(chunks, clen, nchunks, clen, SEED, first_chunk=cx.rank * nchunks)
+    payload = torch.empty(nw * G, dtype=torch.uint8, device=cx.dev)
+    h3c.fill_splitmix(payload, G, nw, G, SEED + 1, first_chunk=cx.rank * nw)
+    g = torch.Generator().manual_seed(SEED + cx.rank)
+    wc = torch.randint(0, nchunks, (nw,), generator=g, dtype=torch.int32).to(cx.dev)
+    wb = torch.randint(0, bpc, (nw,), generator=g, dtype=torch.int32).to(cx.dev)
+    plan = h3c.Plan.uniform(chunks.data_ptr(), clen, nchunks, device=cx.local)
+    raw = [torch.zeros(nchunks, dtype=torch.int32, device=cx.dev) for _ in range(2)]
+    plan.run(raw[0], stream=cx.stream)
+    bases = torch.arange(nchunks, dtype=torch.int64, device=cx.dev) * clen + chunks.data_ptr()
+    out = torch.zeros(nw, dtype=torch.int32, device=cx.dev)
+    ws = torch.empty(h3c.update_workspace_bytes(nw, nchunks, clen, G), dtype=torch.uint8, device=cx.dev)
+    cur = [0]
+
+    def step():  # apply the batch again on top of the previous state: same traffic, new checksums
+        i = cur[0]
+        h3c.update_blocks(bases, clen, raw[i], wc, wb, payload, out, raw[1 - i], block_bytes=G, workspace=ws,
+                          stream=cx.stream)
+        cur[0] = 1 - i
+
+    elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDATE)
+    fresh = torch.zeros(nchunks, dtype=torch.int32, device=cx.dev)
+    plan.run(fresh, stream=cx.stream)
+    torch.cuda.synchronize()
+    verified = cx.all_true(bool(torch.equal(fresh, raw[cur[0]])))
+    plan.close()
+    writes = nw * args.steps * cx.world
+    res = {
+        "metric": "partial-update writes/s (4 KiB writes into 64 MiB chunks, per-write chunk CRC32C)",
+        "value": round(writes / elapsed, 1),
+        "unit": "writes/s",
+        "n_gpus": cx.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64 chunks and payloads in HBM, seeded uniform chunk/offset)",
+        "config": {"workload": f"BASELINE config 3: {nw} random 4 KiB writes into {nchunks} x 64 MiB chunks per GPU",
+                   "parallelism": f"shard{cx.world}"},
+        "verified": verified,
+        "algorithmic_gbps": round(writes * 3 * G / elapsed / 1e9, 1),
+        "roofline": roofline(prof, HBM_PEAK_GBPS, kernel="upd_delta_kernel"),
+    }
+    if cx.world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_update()
+    return res
+
+
+def pcie_h2d_peak(torch, dev, nbytes: int = 1 << 30) -> float:
+    src = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    return 5 * nbytes / (time.perf_counter() - t0) / 1e9
+
+
+def run_hostfed(args, cx: Ctx) -> dict:
+    torch, h3c = cx.torch, cx.h3c
+    rng = np.random.default_rng(SEED + cx.rank)
+    lens, total = [], 0
+    while total < (args.hostfed_gib << 30):
+        L = (64 << 10) << int(rng.integers(0, 11))  # 11 size classes 64 KiB .. 64 MiB
+        if rng.random() < 0.1:
+            L -= int(rng.integers(1, 4096))  # ragged lengths
+        lens.append(L)
+        total += L
+    devbuf = torch.empty(total, dtype=torch.uint8, device=cx.dev)
+    h3c.fill_splitmix(devbuf, total - total % 8, 1, total - total % 8, SEED + 7 + cx.rank)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    _, expected = h3c.batch_create([(devbuf[o: o + L], L) for o, L in zip(offs, lens)])
+    pinned = devbuf.cpu().pin_memory()
+    del devbuf
+    items = [(pinned[o: o + L], L) for o, L in zip(offs, lens)]
+    hf = h3c.HostFed(cx.local, args.window_mib << 20)
+    state = {}
+
+    def step():
+        state["r"] = hf.run(items, expected=expected)
+
+    elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_HOSTFED)
+    _, ok, nbad = state["r"]
+    verified = cx.all_true(nbad == 0 and bool(ok.all()))
+    hf.close()
+    peak = pcie_h2d_peak(torch, cx.dev)
+    value = total * args.steps * cx.world / elapsed / 2**30
+    rl = roofline(prof, round(peak, 1), bound="pcie", kernel="hostfed pipeline (H2D + CRC)")
+    rl["pcie_spec_gbps"] = PCIE_SPEC_GBPS
+    return {
+        "metric": "host-fed GiB/s CRC32C verified (mixed 64 KiB-64 MiB chunks from pinned host memory)",
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": cx.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic: {len(lens)} chunks, {total / 2**30:.2f} GiB pinned host memory per GPU, 10% ragged",
+        "config": {"workload": "BASELINE config 5: host-fed verify, H2D double-buffered against CRC",
+                   "window_bytes": args.window_mib << 20, "parallelism": f"shard{cx.world}"},
+        "verified": verified,
+        "measured_h2d_gbps": round(peak, 1),
+        "roofline": rl,
+    }
+
+
+def run_shard4m(args, cx: Ctx) -> dict:
+    """BASELINE config 4: total_gib as 4 MiB chunks split over the ranks (strong scaling),
+    generated in HBM in passes of <= pass_gib; create (untimed) then timed verify per pass."""
+    torch, h3c = cx.torch, cx.h3c
+    clen = 4 << 20
+    total_chunks = (args.total_gib << 30) // clen
+    per = total_chunks // cx.world
+    first = cx.rank * per
+    pass_chunks = max(1, (args.pass_gib << 30) // clen)
+    buf = torch.empty(min(per, pass_chunks) * clen, dtype=torch.uint8, device=cx.dev)
+    elapsed_total, prof_acc, verified = 0.0, [0.0, 0, 0], True
+    done = 0
+    while done < per:
+        m = min(pass_chunks, per - done)
+        h3c.fill_splitmix(buf, clen, m, clen, SEED, first_chunk=first + done)
+        plan = h3c.Plan.uniform(buf.data_ptr(), clen, m, device=cx.local)
+        stored = torch.zeros(m, dtype=torch.int32, device=cx.dev)
+        plan.run(stored, stream=cx.stream)
+        out = torch.zeros_like(stored)
+        ok = torch.zeros(m, dtype=torch.uint8, device=cx.dev)
+        mis = torch.zeros(1, dtype=torch.int32, device=cx.dev)
+
+        def step():
+            plan.run(out, expected=stored, ok=ok, mismatch=mis, stream=cx.stream)
+
+        el, prof = cx.timed(step, 1, 1 if done == 0 else 0, h3c.engine.PROF_SEG)
+        elapsed_total += el
+        for k in range(3):
+            prof_acc[k] += prof[k]
+        verified = verified and int(mis.item()) == 0
+        plan.close()
+        done += m
+    verified = cx.all_true(verified)
+    value = total_chunks * clen / elapsed_total / 2**30
+    return {
+        "metric": "GiB/s CRC32C verified (4 MiB chunks, 256 GiB total split over the GPUs)",
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": cx.world, "steps": 1, "warmup": 1,
+        "ms_per_step": round(elapsed_total * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic splitmix64 4 MiB chunks generated in HBM in passes",
+        "config": {"workload": f"BASELINE config 4: {args.total_gib} GiB as 4 MiB chunks, "
+                               f"{per} chunks per GPU in passes of <= {pass_chunks}",
+                   "parallelism": f"shard{cx.world}"},
+        "verified": verified,
+        "roofline": roofline(tuple(prof_acc), HBM_PEAK_GBPS),
+    }
 
 
 def main() -> int:
@@ -109,137 +447,28 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=["verify", "update", "hostfed", "shard4m"], default="verify")
     ap.add_argument("--chunks", type=int, default=8192)
     ap.add_argument("--chunk-kib", type=int, default=1024)
     ap.add_argument("--flip-frac", type=float, default=0.05)
+    ap.add_argument("--writes", type=int, default=100_000)
+    ap.add_argument("--hostfed-gib", type=int, default=4)
+    ap.add_argument("--window-mib", type=int, default=64)
+    ap.add_argument("--total-gib", type=int, default=256)
+    ap.add_argument("--pass-gib", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
-
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
-    h3c = importlib.import_module("3fs_amd")
-
-    n, clen = args.chunks, args.chunk_kib << 10
-    buf = torch.empty(n * clen, dtype=torch.uint8, device=dev)
-    # Rank r holds chunk indices [r*n, (r+1)*n): distinct data per GPU.
-    h3c.fill_splitmix(buf, clen, n, clen, SEED, first_chunk=rank * n)
-    torch.cuda.synchronize()
-    plan = h3c.Plan.uniform(buf.data_ptr(), clen, n, device=local)
-    stream = torch.cuda.current_stream()
-
-    # Stored checksums = a create pass; then corrupt flip_frac of the chunks.
-    stored = torch.zeros(n, dtype=torch.int32, device=dev)
-    plan.run(stored, stream=stream)
-    torch.cuda.synchronize()
-    stored_host = stored.cpu().numpy().view(np.uint32).copy()
-    g = torch.Generator().manual_seed(SEED + rank)
-    nflip = int(n * args.flip_frac)
-    flips = torch.randperm(n, generator=g)[:nflip].sort().values
-    pos = flips * clen + torch.randint(0, clen, (nflip,), generator=g)
-    bits = (1 << torch.randint(0, 8, (nflip,), generator=g)).to(torch.uint8)
-    pos_d = pos.to(dev)
-    buf[pos_d] ^= bits.to(dev)
-
-    out = torch.zeros(n, dtype=torch.int32, device=dev)
-    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
-    mis = torch.zeros(1, dtype=torch.int32, device=dev)
-
-    def step():
-        mis.zero_()
-        plan.run(out, expected=stored, ok=ok, mismatch=mis, stream=stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    h3c.profile_read(reset=True)
-    h3c.profile_enable(True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    h3c.profile_enable(False)
-    kern_ms, launches, kbytes = h3c.profile_read(reset=True)
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # Correctness of the timed work: exactly the flipped chunks fail.
-    bad = np.nonzero(ok.cpu().numpy() == 0)[0]
-    verified = int(mis.item()) == nflip and np.array_equal(bad, flips.numpy())
-    if world > 1:
-        vt = torch.tensor([1 if verified else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(vt, op=dist.ReduceOp.MIN)
-        verified = bool(vt.item())
-
-    total_bytes = n * clen * args.steps * world
-    value = total_bytes / elapsed / 2**30
-    bytes_per_launch = kbytes / max(launches, 1)
-    avg_kernel_s = kern_ms / 1e3 / max(launches, 1)
-    achieved = bytes_per_launch / avg_kernel_s / 1e9 if launches else 0.0
-
-    if rank == 0:
-        res = {
-            "metric": "GiB/s CRC32C verified (1 MiB chunks) at 1/2/4/8 GPUs; % of HBM peak",
-            "value": round(value, 2),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (splitmix64 chunks generated in HBM; 5% of chunks carry one flipped bit)",
-            "config": {
-                "workload": f"batched CRC32C verify of {n} x {clen >> 10} KiB device-resident chunks per GPU "
-                            f"(BASELINE config 2)",
-                "chunks_per_gpu": n,
-                "chunk_bytes": clen,
-                "parallelism": f"shard{world}",
-            },
-            "verified": verified,
-            "pct_hbm_peak": round(100.0 * (n * clen) / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 2),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": None,
-                "kernel": "seg_crc_kernel",
-                "kernel_avg_us": round(avg_kernel_s * 1e6, 2),
-                "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            },
-        }
-        tr = pmc_traffic(int(bytes_per_launch))
-        if tr:
-            res["roofline"]["traffic"] = int(tr[0])
-            res["roofline"]["traffic_source"] = f"profiles/{tr[1]}"
-        if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(stored_host, clen, args.cpu_seconds)
+    cx = Ctx()
+    fn = {"verify": run_verify, "update": run_update, "hostfed": run_hostfed, "shard4m": run_shard4m}[args.workload]
+    if args.workload == "hostfed" and args.steps == 50:
+        args.steps, args.warmup = 5, 1
+    res = fn(args, cx)
+    if cx.rank == 0:
         print(json.dumps(res), flush=True)
-    plan.close()
-    if world > 1:
-        dist.destroy_process_group()
-    return 0 if verified else 1
+    if cx.world > 1:
+        cx.dist.destroy_process_group()
+    return 0 if res["verified"] else 1
 
 
 if __name__ == "__main__":
