@@ -42,8 +42,8 @@ constexpr uint32_t kFlagNone = 1u;
 // Segment-CRC + finalize launches over `nchunks` device descriptors (one polynomial
 // group); profiled as `prof_kind` when >= 0.  Defined in h3c_engine.hip.
 int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint32_t nchunks, uint32_t total_segs,
-               uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc, const uint32_t *expected,
-               uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind);
+               uint32_t max_chunk_segs, uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc,
+               const uint32_t *expected, uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind);
 // Segment size the engine picks for a batch of `total_bytes` on device `dev`.
 uint64_t pick_seg(uint64_t total_bytes, int dev);
 }  // namespace h3c_rt

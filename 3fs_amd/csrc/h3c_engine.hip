@@ -87,6 +87,22 @@ __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__res
 }
 
 // Kernel B: per chunk, fold segment CRCs, apply start, optionally compare.
+// Chunks with more segments than this are folded by a whole wave (finalize_big_kernel);
+// one thread folding thousands of segments serially took ~1 ms for a 64 MiB chunk.
+constexpr uint32_t kSmallFold = 16;
+
+__device__ __forceinline__ void finalize_store(const DevChunk &ch, uint32_t raw, const uint32_t *__restrict__ expected,
+                                               uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                               uint32_t *__restrict__ mismatch) {
+  out_raw[ch.out_idx] = raw;
+  if (expected) {
+    const bool good = raw == expected[ch.out_idx];
+    ok[ch.out_idx] = good ? 1 : 0;
+    if (!good && mismatch) atomicAdd(mismatch, 1u);
+  }
+}
+
+// Kernel B: per chunk (one thread), fold segment CRCs, apply start, optionally compare.
 __global__ void finalize_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks, uint32_t total_segs,
                                 uint64_t seg_bytes, uint32_t seg_mul, const PolyConsts *__restrict__ pc,
                                 const uint32_t *__restrict__ seg_crc, const uint32_t *__restrict__ expected,
@@ -100,6 +116,7 @@ __global__ void finalize_kernel(const DevChunk *__restrict__ chunks, uint32_t nc
   if (!(ch.flags & kFlagNone)) {
     const uint32_t b = ch.seg_begin;
     const uint32_t e = (i + 1 < nchunks) ? chunks[i + 1].seg_begin : total_segs;
+    if (e - b > kSmallFold) return;  // finalize_big_kernel's
     uint32_t crc0 = 0;
     if (e > b) {
       crc0 = seg_crc[b];
@@ -111,11 +128,47 @@ __global__ void finalize_kernel(const DevChunk *__restrict__ chunks, uint32_t nc
     }
     raw = crc0 ^ (ch.len ? dgf_mul(ch.start, dxpow8n(ch.len, pc, poly), poly) : ch.start);
   }
-  out_raw[ch.out_idx] = raw;
-  if (expected) {
-    const bool good = raw == expected[ch.out_idx];
-    ok[ch.out_idx] = good ? 1 : 0;
-    if (!good && mismatch) atomicAdd(mismatch, 1u);
+  finalize_store(ch, raw, expected, out_raw, ok, mismatch);
+}
+
+// Kernel B': one wave per chunk with > kSmallFold segments.  The segment CRCs are the
+// coefficients of a polynomial in X = x^(8*seg_bytes) (all but the last segment are
+// full): lane j Horner-evaluates q consecutive coefficients (virtual zeros in front
+// are harmless), then six butterfly levels combine lane results with X^(q*2^t).
+__global__ void finalize_big_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks, uint32_t total_segs,
+                                    uint64_t seg_bytes, uint32_t seg_mul, const PolyConsts *__restrict__ pc,
+                                    const uint32_t *__restrict__ seg_crc, const uint32_t *__restrict__ expected,
+                                    uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                    uint32_t *__restrict__ mismatch) {
+  const uint32_t i = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint32_t j = threadIdx.x & 63;
+  if (i >= nchunks) return;
+  const DevChunk ch = chunks[i];
+  if (ch.flags & kFlagNone) return;
+  const uint32_t b = ch.seg_begin;
+  const uint32_t e = (i + 1 < nchunks) ? chunks[i + 1].seg_begin : total_segs;
+  const uint32_t m = e - b;
+  if (m <= kSmallFold) return;
+  const uint32_t poly = pc->poly;
+  const uint32_t q = (m - 1 + 63) / 64;
+  const int64_t k0 = (int64_t)(m - 1) - (int64_t)(64 - j) * q;
+  uint32_t h = 0;
+  for (uint32_t t = 0; t < q; ++t) {
+    const int64_t k = k0 + t;
+    h = dgf_mul(h, seg_mul, poly) ^ (k >= 0 ? seg_crc[b + (uint32_t)k] : 0u);
+  }
+  uint32_t Y = dxpow8n((uint64_t)q * seg_bytes, pc, poly);
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    const uint32_t other = __shfl_down(h, 1u << t, 64);
+    if ((j & ((2u << t) - 1)) == 0) h = dgf_mul(h, Y, poly) ^ other;
+    Y = dgf_mul(Y, Y, poly);
+  }
+  if (j == 0) {
+    const uint64_t r = ch.len - (uint64_t)(m - 1) * seg_bytes;  // last segment's length
+    const uint32_t crc0 = dgf_mul(h, dxpow8n(r, pc, poly), poly) ^ seg_crc[b + m - 1];
+    const uint32_t raw = crc0 ^ dgf_mul(ch.start, dxpow8n(ch.len, pc, poly), poly);
+    finalize_store(ch, raw, expected, out_raw, ok, mismatch);
   }
 }
 
@@ -245,8 +298,8 @@ hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes
 }
 
 int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint32_t nchunks, uint32_t total_segs,
-               uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc, const uint32_t *expected,
-               uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind) {
+               uint32_t max_chunk_segs, uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc,
+               const uint32_t *expected, uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind) {
   const DeviceCtx &ctx = g_dev[dev];
   const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
   const uint32_t poly = type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
@@ -264,6 +317,12 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
   hipLaunchKernelGGL(finalize_kernel, dim3(fb), dim3(256), 0, st, d_chunks, nchunks, total_segs, seg_bytes, seg_mul, pc,
                      d_segcrc, expected, out_raw, ok, mismatch);
   HIP_TRY(hipGetLastError());
+  if (max_chunk_segs > kSmallFold) {
+    const uint32_t bb = (nchunks + 3) / 4;  // 4 waves (chunks) per 256-thread block
+    hipLaunchKernelGGL(finalize_big_kernel, dim3(bb), dim3(256), 0, st, d_chunks, nchunks, total_segs, seg_bytes,
+                       seg_mul, pc, d_segcrc, expected, out_raw, ok, mismatch);
+    HIP_TRY(hipGetLastError());
+  }
   return H3C_OK;
 }
 
@@ -282,6 +341,7 @@ struct Group {
   uint8_t type = H3C_TYPE_CRC32C;
   uint32_t nchunks = 0;
   uint32_t total_segs = 0;
+  uint32_t max_chunk_segs = 0;
   uint64_t bytes = 0;
   DevChunk *d_chunks = nullptr;
 };
@@ -378,7 +438,7 @@ int h3c_plan_create(const h3c_desc *d, size_t n, int device, h3c_plan **out) {
   p->bytes = total;
 
   std::vector<DevChunk> hc[2];
-  uint32_t segs[2] = {0, 0};
+  uint32_t segs[2] = {0, 0}, max_segs_chunk[2] = {0, 0};
   uint64_t bytes[2] = {0, 0};
   for (size_t i = 0; i < n; ++i) {
     const h3c_desc &x = d[i];
@@ -407,6 +467,7 @@ int h3c_plan_create(const h3c_desc *d, size_t n, int device, h3c_plan **out) {
         return H3C_ERR_INVALID_ARG;
       }
       segs[g] += (uint32_t)ns;
+      max_segs_chunk[g] = std::max(max_segs_chunk[g], (uint32_t)ns);
       bytes[g] += x.len;
     }
     hc[g].push_back(c);
@@ -418,6 +479,7 @@ int h3c_plan_create(const h3c_desc *d, size_t n, int device, h3c_plan **out) {
     gr.type = g == 0 ? H3C_TYPE_CRC32C : H3C_TYPE_CRC32;
     gr.nchunks = (uint32_t)hc[g].size();
     gr.total_segs = segs[g];
+    gr.max_chunk_segs = max_segs_chunk[g];
     gr.bytes = bytes[g];
     hipError_t e = hipMalloc(&gr.d_chunks, hc[g].size() * sizeof(DevChunk));
     if (e == hipSuccess)
@@ -471,8 +533,9 @@ int h3c_plan_run(h3c_plan *p, const uint32_t *expected_raw_dev, uint32_t *out_ra
   int rc = H3C_OK;
   (void)ctx;
   for (const Group &g : p->groups) {
-    rc = h3c_rt::launch_crc(st, p->device, g.type, g.d_chunks, g.nchunks, g.total_segs, g.bytes, p->seg_bytes,
-                            p->dbg, p->d_segcrc, expected_raw_dev, out_raw_dev, ok_dev, mismatch_dev, H3C_PROF_SEG);
+    rc = h3c_rt::launch_crc(st, p->device, g.type, g.d_chunks, g.nchunks, g.total_segs, g.max_chunk_segs, g.bytes,
+                            p->seg_bytes, p->dbg, p->d_segcrc, expected_raw_dev, out_raw_dev, ok_dev, mismatch_dev,
+                            H3C_PROF_SEG);
     if (rc) break;
   }
   if (prev != p->device) HIP_TRY(hipSetDevice(prev));

@@ -31,7 +31,7 @@ struct Run {  // one hipMemcpyAsync
 
 struct Window {
   uint32_t piece_begin, piece_end;  // pieces [begin, end) in the global piece array
-  uint32_t total_segs;
+  uint32_t total_segs, max_piece_segs;
   uint64_t bytes;
   std::vector<Run> runs;
 };
@@ -230,12 +230,15 @@ int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t 
   size_t max_segs = 0;
   for (size_t wi = 0; wi < wins.size(); ++wi) {
     Window &win = wins[wi];
-    uint32_t segs = 0;
+    uint32_t segs = 0, mx = 0;
     for (uint32_t p = win.piece_begin; p < win.piece_end; ++p) {
       pieces[p].seg_begin = segs;
       pieces[p].ptr += (uint64_t)(uintptr_t)h->stage[wi & 1];
-      segs += (uint32_t)((pieces[p].len + seg_bytes - 1) / seg_bytes);
+      const uint32_t ns = (uint32_t)((pieces[p].len + seg_bytes - 1) / seg_bytes);
+      segs += ns;
+      mx = std::max(mx, ns);
     }
+    win.max_piece_segs = mx;
     win.total_segs = segs;
     max_segs = std::max<size_t>(max_segs, segs);
   }
@@ -288,7 +291,8 @@ int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t 
     HIP_TRY(hipEventRecord(h->copied[b], h->copy_st));
     HIP_TRY(hipStreamWaitEvent(st, h->copied[b], 0));
     const int rc = h3c_rt::launch_crc(st, h->device, type, h->d_pieces + win.piece_begin,
-                                      win.piece_end - win.piece_begin, win.total_segs, win.bytes, seg_bytes, 0,
+                                      win.piece_end - win.piece_begin, win.total_segs, win.max_piece_segs, win.bytes,
+                                      seg_bytes, 0,
                                       h->d_segcrc[b], nullptr, h->d_piece_crc, nullptr, nullptr, -1);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(h->freed[b], st));
