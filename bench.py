@@ -131,9 +131,16 @@ class Ctx:
         self.torch, self.dist = torch, dist
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
-        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # one process per GPU; modulo only matters for single-GPU rehearsals of N>1
+        self.local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
         if self.world > 1:
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.local}"))
+            # Control plane only (barrier, max-over-ranks time, verified flag): no data
+            # path collective exists, so gloo on CPU tensors is enough; set
+            # H3C_DIST_BACKEND=nccl to use RCCL instead.
+            backend = os.environ.get("H3C_DIST_BACKEND", "gloo")
+            kw = {"device_id": torch.device(f"cuda:{self.local}")} if backend == "nccl" else {}
+            dist.init_process_group(backend, **kw)
+            self.cdev = torch.device(f"cuda:{self.local}") if backend == "nccl" else torch.device("cpu")
         torch.cuda.set_device(self.local)
         self.dev = torch.device(f"cuda:{self.local}")
         self.h3c = importlib.import_module("3fs_amd")
@@ -148,14 +155,14 @@ class Ctx:
     def max_over_ranks(self, v: float) -> float:
         if self.world == 1:
             return v
-        t = self.torch.tensor([v], dtype=self.torch.float64, device=self.dev)
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=self.cdev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
     def all_true(self, b: bool) -> bool:
         if self.world == 1:
             return b
-        t = self.torch.tensor([1 if b else 0], dtype=self.torch.int32, device=self.dev)
+        t = self.torch.tensor([1 if b else 0], dtype=self.torch.int32, device=self.cdev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
         return bool(t.item())
 
