@@ -105,7 +105,13 @@ struct PolyConsts {
   uint32_t pow8[64];     // [k]    = x^(8*2^k)
   uint32_t poly;
   uint32_t pad[3];
+  // Byte tables for multiplying by the 7 constants of the wave fold (wave_fold_tab):
+  // red[0] = x^-32 (one dword back), red[1+k] = x^-(8*16*2^k) (2^k lanes back), k = 0..5.
+  // red[m][k][b] = (b << 8k) * C_m, so a*C_m = XOR_k red[m][k][byte k of a].
+  uint32_t red[7][4][256];
 };
+constexpr int kRedTables = 7;
+constexpr int kRedWords = kRedTables * 4 * 256;  // 7168 dwords = 28 KiB of LDS
 
 inline void build_consts(PolyConsts &pc, uint32_t poly) {
   std::memset(&pc, 0, sizeof(pc));
@@ -121,6 +127,11 @@ inline void build_consts(PolyConsts &pc, uint32_t poly) {
   for (int k = 0; k < 64; ++k) {
     pc.pow8[k] = p;
     p = hgf_mul(p, p, poly);
+  }
+  for (int m = 0; m < kRedTables; ++m) {
+    const uint32_t c = hgf_pow(xinv8, m == 0 ? 4u : 16u << (m - 1), poly);
+    for (int k = 0; k < 4; ++k)
+      for (uint32_t b = 0; b < 256; ++b) pc.red[m][k][b] = hgf_mul(b << (8 * k), c, poly);
   }
 }
 
@@ -362,6 +373,32 @@ __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, c
   const uint32_t z = (uint32_t)(E16 - E);
   if (z) acc = dgf_mul(acc, pc->fixz[z], poly);
   return acc;
+}
+
+// a * C for the constant whose byte tables start at `t` (4 x 256 dwords in LDS).
+__device__ __forceinline__ uint32_t tab_mul(uint32_t a, const uint32_t *t) {
+  return xor3(t[a & 255u], t[256u + ((a >> 8) & 255u)], t[512u + ((a >> 16) & 255u)]) ^ t[768u + (a >> 24)];
+}
+
+// Fold a wave's 256 stream states into the init-0 CRC of the rows they walked:
+//   acc = XOR_{l,j} s(l,j) * x^-(8*(16l+4j))
+// (stream (l,j) ended 16l+4j bytes past the 16-byte-rounded end).  Instead of 4 general
+// GF(2) multiplies by per-lane constants (~200 VALU ops each), every multiply here is by
+// one of 7 wave-uniform constants via byte tables in LDS (`red` = the 7168 dwords laid out
+// as PolyConsts::red): a Horner pass over the lane's 4 streams with x^-32, then a 6-level
+// shuffle tree whose level k folds lane l+2^k into lane l with x^-(128*2^k).  Lanes that
+// no longer carry a partial sum skip the lookups (fewer LDS bank conflicts).  The result
+// is valid in lane 0 only.
+__device__ __forceinline__ uint32_t wave_fold_tab(const Streams &st, uint32_t lane, const uint32_t *red) {
+  uint32_t v = tab_mul(st.s3, red) ^ st.s2;
+  v = tab_mul(v, red) ^ st.s1;
+  v = tab_mul(v, red) ^ st.s0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const uint32_t o = __shfl_down(v, 1u << k, 64);
+    if ((lane & ((2u << k) - 1u)) == 0) v ^= tab_mul(o, red + 1024 * (k + 1));
+  }
+  return v;
 }
 
 }  // namespace

@@ -13,17 +13,20 @@
 // (chunk c, block b, payload i); for each slot (c,b) the "old" data of write i is the
 // payload of the previous write to that slot, or the chunk's original bytes for the
 // first one.  Kernels:
-//   1. keys      key1[i] = slot<<32 | i                 (validates chunk/block ids)
-//   2. rocPRIM radix sort key1 -> writes grouped by slot, in sequence order
+//   1. keys      slot[i] = chunk*bpc + block, chunk[i]   (validates chunk/block ids)
+//   2. rocPRIM stable radix sort_pairs (slot, i) over the slot's bits only
+//                -> writes grouped by slot, in sequence order
 //   3. link      prev[i] (previous writer of the slot) and, for the first writer of a
 //                slot, final[i] = the slot's last writer (whose bytes must end up there)
-//   4. shifts    sh[b] = x^(8*(L-(b+1)*G)) per block index
+//   4. shifts    sh[b] = x^(8*(L-(b+1)*G)) per block index, cached per chunk geometry
 //   5. delta     one wave per block write: crc0(new^old) over G bytes with the same
-//                replicated-LDS stride tables as the create kernel, times sh[b];
+//                replicated-LDS stride tables as the create kernel, folded across the
+//                wave with table multiplies by uniform constants (wave_fold_tab);
 //                the first writer of a slot also writes the slot's final bytes back
 //                (it is the only wave that reads the slot's original bytes: no race)
-//   6. rocPRIM radix sort key2 = chunk<<32 | i  -> per-chunk sequence order
-//   7. gather + rocPRIM inclusive_scan_by_key(chunk, XOR) + scatter:
+//   6. rocPRIM stable radix sort_pairs (chunk, i)  -> per-chunk sequence order
+//   7. gather (one thread per write: delta * sh[b]) + rocPRIM
+//      inclusive_scan_by_key(chunk, XOR) + scatter:
 //        out_raw[i] = raw_in[c] ^ XOR of deltas of writes j<=i to chunk c
 //      i.e. the chunk checksum right after write i, which is what updateChecksum stores.
 #include <hip/hip_runtime.h>
@@ -31,7 +34,10 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan_by_key.hpp>
@@ -58,6 +64,14 @@ __device__ __forceinline__ void store_row(uint64_t a, uint4 v) {
 #define H3C_UPD_EXPERIMENT 0  // timing-only builds: bit0 skips write-back, bit1 skips the CRC math
 #endif
 
+// rocPRIM picks merge sort below this many items.  Forcing its onesweep radix passes
+// (limit 0) measured slower at 100k items: 4 x 23 us lookback-bound iterations.
+#ifndef H3C_SORT_MERGE_LIMIT
+#define H3C_SORT_MERGE_LIMIT (1024 * 1024)
+#endif
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, H3C_SORT_MERGE_LIMIT>;
+
 struct XorOp {
   __host__ __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a ^ b; }
 };
@@ -69,36 +83,39 @@ uint32_t bits_for(uint64_t v) {  // number of bits to represent values < v
 }
 
 __global__ void upd_keys_kernel(const uint32_t *__restrict__ blk_chunk, const uint32_t *__restrict__ blk_index,
-                                uint32_t n, uint32_t nchunks, uint32_t bpc, uint64_t *__restrict__ key1,
-                                uint64_t *__restrict__ key2, uint32_t *__restrict__ err) {
+                                uint32_t n, uint32_t nchunks, uint32_t bpc, uint32_t *__restrict__ kslot,
+                                uint32_t *__restrict__ kchunk, uint32_t *__restrict__ iota,
+                                uint32_t *__restrict__ err) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t c = blk_chunk[i], b = blk_index[i];
+  iota[i] = i;
   if (c >= nchunks || b >= bpc) {  // invalid entry: counted, parked on sentinel slot / chunk, no effect
     atomicAdd(err, 1u);
-    key1[i] = ((uint64_t)((uint64_t)nchunks * bpc) << 32) | i;
-    key2[i] = ((uint64_t)nchunks << 32) | i;
+    kslot[i] = nchunks * bpc;
+    kchunk[i] = nchunks;
     return;
   }
-  key1[i] = ((uint64_t)((uint64_t)c * bpc + b) << 32) | i;
-  key2[i] = ((uint64_t)c << 32) | i;
+  kslot[i] = c * bpc + b;
+  kchunk[i] = c;
 }
 
-__global__ void upd_link_kernel(const uint64_t *__restrict__ sorted1, uint32_t n, uint32_t *__restrict__ prev,
-                                uint32_t *__restrict__ final_of) {
+// On the stable sort by slot: prev[i] = previous writer of i's slot (or none), and for
+// the first writer of a slot, final_of[i] = the slot's last writer.
+__global__ void upd_link_kernel(const uint32_t *__restrict__ slot_s, const uint32_t *__restrict__ idx1, uint32_t n,
+                                uint32_t *__restrict__ prev, uint32_t *__restrict__ final_of) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
-  const uint64_t k = sorted1[p];
-  const uint32_t slot = (uint32_t)(k >> 32), i = (uint32_t)k;
-  const bool start = p == 0 || (uint32_t)(sorted1[p - 1] >> 32) != slot;
-  prev[i] = start ? kNone : (uint32_t)sorted1[p - 1];
+  const uint32_t slot = slot_s[p], i = idx1[p];
+  const bool start = p == 0 || slot_s[p - 1] != slot;
+  prev[i] = start ? kNone : idx1[p - 1];
   if (start) {  // last position of this slot's run: binary search in [p, n)
     uint32_t lo = p, hi = n;  // invariant: slot(lo) == slot, slot(hi) > slot or hi == n
     while (hi - lo > 1) {
       const uint32_t mid = lo + (hi - lo) / 2;
-      if ((uint32_t)(sorted1[mid] >> 32) == slot) lo = mid; else hi = mid;
+      if (slot_s[mid] == slot) lo = mid; else hi = mid;
     }
-    final_of[i] = (uint32_t)sorted1[lo];
+    final_of[i] = idx1[lo];
   }
 }
 
@@ -109,12 +126,12 @@ __global__ void upd_shift_kernel(uint32_t bpc, uint64_t chunk_len, uint32_t bloc
   sh[b] = dxpow8n(chunk_len - (uint64_t)(b + 1) * block_bytes, pc, pc->poly);
 }
 
-// crc0(new ^ old) over `rows` full 1 KiB rows (both 16-byte aligned), by one wave.
+// crc0(new ^ old) over `rows` full 1 KiB rows (both 16-byte aligned), by one wave
+// (valid in lane 0).
 // When `dst` is non-zero the wave also stores the slot's final bytes (from `fin`,
 // which may equal `pnew`) after it has read the old bytes of each batch.
 __device__ uint32_t delta_crc0(uint64_t pnew, uint64_t pold, uint64_t dst, uint64_t fin, uint32_t rows,
-                               uint32_t lane, const char *lb, const LaneLut &L, const uint32_t fix[4],
-                               uint32_t poly) {
+                               uint32_t lane, const char *lb, const LaneLut &L, const uint32_t *red) {
   Streams st{0, 0, 0, 0};
   const uint64_t lo = 16u * lane;
   for (uint32_t r0 = 0; r0 < rows; r0 += 4) {
@@ -141,33 +158,26 @@ __device__ uint32_t delta_crc0(uint64_t pnew, uint64_t pold, uint64_t dst, uint6
         }
     }
   }
-  uint32_t f0 = fix[0], f1 = fix[1], f2 = fix[2], f3 = fix[3];
-  asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
-  uint32_t acc = dgf_mul(f0, st.s0, poly) ^ dgf_mul(f1, st.s1, poly) ^ dgf_mul(f2, st.s2, poly) ^
-                 dgf_mul(f3, st.s3, poly);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
-  return acc;
+  return wave_fold_tab(st, lane, red);
 }
 
 __global__ __launch_bounds__(kThreads) void upd_delta_kernel(
     const uint64_t *__restrict__ chunk_base, uint32_t nchunks, uint32_t bpc, uint32_t block_bytes,
     const uint32_t *__restrict__ blk_chunk, const uint32_t *__restrict__ blk_index, const uint8_t *payload,
     uint32_t n, const uint32_t *__restrict__ prev, const uint32_t *__restrict__ final_of,
-    const uint32_t *__restrict__ sh, const PolyConsts *__restrict__ pc, uint32_t *__restrict__ delta) {
-  __shared__ uint32_t lds[kLdsWords];
+    const PolyConsts *__restrict__ pc, uint32_t *__restrict__ delta) {
+  __shared__ uint32_t lds[kLdsWords + kRedWords];
   for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
+  const uint32_t *red_g = &pc->red[0][0][0];
+  for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
   __syncthreads();
+  const uint32_t *red = lds + kLdsWords;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint32_t lo = (uint32_t)(gw * n / nw), hi = (uint32_t)((gw + 1) * n / nw);
   if (lo >= hi) return;
-  const uint32_t poly = pc->poly;
-  uint32_t fix[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) fix[j] = pc->fix[4 * lane + j];
   const char *lb = reinterpret_cast<const char *>(lds);
   const LaneLut L = make_lut(lane);
   const uint32_t rows = block_bytes / kRowBytes;
@@ -193,7 +203,7 @@ __global__ __launch_bounds__(kThreads) void upd_delta_kernel(
       uint32_t b;
       uint32_t d = 0;
       if (job_of(i, pnew, pold, dst, fin, b))
-        d = dgf_mul(delta_crc0(pnew, pold, dst, fin, rows, lane, lb, L, fix, poly), sh[b], poly);
+        d = delta_crc0(pnew, pold, dst, fin, rows, lane, lb, L, red);
       if (lane == 0) delta[i] = d;
     }
     return;
@@ -210,7 +220,6 @@ __global__ __launch_bounds__(kThreads) void upd_delta_kernel(
     const uint32_t k = g0 + lane;
     uint32_t m_ok = 0;
     uint64_t m_new = 0, m_old = 0, m_dst = 0, m_fin = 0;
-    uint32_t m_sh = 0;
     if (lane < cnt) {
       const uint32_t c = blk_chunk[k], bb = blk_index[k];
       if (c < nchunks && bb < bpc) {
@@ -223,7 +232,6 @@ __global__ __launch_bounds__(kThreads) void upd_delta_kernel(
           m_dst = slot;
           m_fin = pay + (uint64_t)final_of[k] * block_bytes;
         }
-        m_sh = sh[bb];
       }
     }
     auto rl64 = [](uint64_t v, uint32_t t) -> uint64_t {
@@ -271,13 +279,7 @@ __global__ __launch_bounds__(kThreads) void upd_delta_kernel(
             store_row(dst + u * kRowBytes + lo16, v);
           }
         }
-        uint32_t f0 = fix[0], f1 = fix[1], f2 = fix[2], f3 = fix[3];
-        asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
-        uint32_t acc = dgf_mul(f0, st.s0, poly) ^ dgf_mul(f1, st.s1, poly) ^ dgf_mul(f2, st.s2, poly) ^
-                       dgf_mul(f3, st.s3, poly);
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
-        d = dgf_mul(acc, (uint32_t)__builtin_amdgcn_readlane(m_sh, t), poly);
+        d = wave_fold_tab(st, lane, red);  // lane 0; the block's x^(8*bytes after it) is applied in gather
       }
       if (lane == 0) delta[g0 + t] = d;
       valid = nvalid;
@@ -292,35 +294,132 @@ __global__ __launch_bounds__(kThreads) void upd_delta_kernel(
   }
 }
 
-__global__ void upd_gather_kernel(const uint64_t *__restrict__ sorted2, uint32_t n, const uint32_t *__restrict__ delta,
-                                  uint32_t *__restrict__ ckey, uint32_t *__restrict__ vals) {
+// vals[p] = delta of the p-th write in (chunk, sequence) order, moved to its place in
+// the chunk: crc0(new ^ old) * x^(8*(L - (b+1)*G)).  One thread per write.
+__global__ void upd_gather_kernel(const uint32_t *__restrict__ chunk_s, const uint32_t *__restrict__ idx2, uint32_t n,
+                                  uint32_t nchunks, const uint32_t *__restrict__ blk_index,
+                                  const uint32_t *__restrict__ delta, const uint32_t *__restrict__ sh, uint32_t poly,
+                                  uint32_t *__restrict__ vals) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
-  const uint64_t k = sorted2[p];
-  ckey[p] = (uint32_t)(k >> 32);
-  vals[p] = delta[(uint32_t)k];
+  const uint32_t i = idx2[p];
+  vals[p] = chunk_s[p] < nchunks ? dgf_mul(delta[i], sh[blk_index[i]], poly) : 0u;  // sentinel: invalid entry
 }
 
-__global__ void upd_scatter_kernel(const uint64_t *__restrict__ sorted2, uint32_t n, uint32_t nchunks,
-                                   const uint32_t *__restrict__ scan,
+__global__ void upd_scatter_kernel(const uint32_t *__restrict__ chunk_s, const uint32_t *__restrict__ idx2, uint32_t n,
+                                   uint32_t nchunks, const uint32_t *__restrict__ scan,
                                    const uint32_t *__restrict__ raw_in, uint32_t *__restrict__ out_raw,
                                    uint32_t *__restrict__ raw_out) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
-  const uint64_t k = sorted2[p];
-  const uint32_t c = (uint32_t)(k >> 32), i = (uint32_t)k;
+  const uint32_t c = chunk_s[p], i = idx2[p];
   if (c >= nchunks) {  // invalid entry (sentinel chunk)
     out_raw[i] = 0;
     return;
   }
   const uint32_t v = raw_in[c] ^ scan[p];
   out_raw[i] = v;
-  if (p + 1 == n || (uint32_t)(sorted2[p + 1] >> 32) != c) raw_out[c] = v;
+  if (p + 1 == n || chunk_s[p + 1] != c) raw_out[c] = v;
+}
+
+// ---- per-chunk prefix XOR in sequence order without a second sort (dense tiles) ----
+// Writes are cut into tiles of kTile consecutive sequence positions.  Used when
+// ntiles * nchunks is small (the dense per-tile aggregate matrix stays a few MB).
+constexpr uint32_t kTile = 256;
+
+// One workgroup per tile.  v_i = delta_i * sh[b_i] (0 for an invalid entry);
+// inpre[i] = XOR of v_j over tile writes j <= i to the same chunk; agg row `tile`
+// [c] = XOR of v_j over all tile writes to chunk c (0 when none).
+__global__ __launch_bounds__(kTile) void upd_tile_kernel(const uint32_t *__restrict__ blk_chunk,
+                                                         const uint32_t *__restrict__ blk_index, uint32_t n,
+                                                         uint32_t nchunks, uint32_t bpc,
+                                                         const uint32_t *__restrict__ delta,
+                                                         const uint32_t *__restrict__ sh, uint32_t poly,
+                                                         uint32_t *__restrict__ inpre, uint32_t *__restrict__ agg) {
+  __shared__ uint32_t cid[kTile], val[kTile];
+  const uint32_t t = threadIdx.x, i0 = blockIdx.x * kTile, i = i0 + t;
+  uint32_t c = kNone, v = 0;
+  if (i < n) {
+    const uint32_t cc = blk_chunk[i], b = blk_index[i];
+    if (cc < nchunks && b < bpc) {
+      c = cc;
+      v = dgf_mul(delta[i], sh[b], poly);
+    }
+  }
+  cid[t] = c;
+  val[t] = v;
+  uint32_t *row = agg + (uint64_t)blockIdx.x * nchunks;
+  for (uint32_t k = t; k < nchunks; k += kTile) row[k] = 0;
+  __syncthreads();  // LDS tile loaded, row zeroed (workgroup-scope fence)
+  const uint32_t cnt = min(kTile, n - i0);
+  uint32_t acc = 0;
+  bool last = true;
+  for (uint32_t u = 0; u < cnt; ++u) {  // uniform loop: broadcast LDS reads
+    const uint32_t cu = cid[u], vu = val[u];
+    if (cu == c) {
+      if (u <= t) acc ^= vu;
+      else last = false;
+    }
+  }
+  if (i < n) inpre[i] = acc;
+  if (c != kNone && last) row[c] = acc;  // the tile's last write to c carries the aggregate
+}
+
+// One workgroup per chunk: exclusive XOR scan of its agg column over tiles into
+// colpre, and the chunk's final checksum.
+__global__ __launch_bounds__(kTile) void upd_column_kernel(const uint32_t *__restrict__ agg, uint32_t ntiles,
+                                                           uint32_t nchunks, const uint32_t *__restrict__ raw_in,
+                                                           uint32_t *__restrict__ colpre,
+                                                           uint32_t *__restrict__ raw_out) {
+  __shared__ uint32_t part[kTile / 64];
+  const uint32_t c = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < ntiles; base += kTile) {
+    const uint32_t r = base + t;
+    const uint32_t x = r < ntiles ? agg[(uint64_t)r * nchunks + c] : 0u;
+    uint32_t inc = x;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc ^= y;
+    }
+    if (lane == 63) part[wave] = inc;
+    __syncthreads();
+    uint32_t before = carry;
+    for (uint32_t w = 0; w < wave; ++w) before ^= part[w];
+    uint32_t total = carry;
+    for (uint32_t w = 0; w < kTile / 64; ++w) total ^= part[w];
+    if (r < ntiles) colpre[(uint64_t)r * nchunks + c] = before ^ inc ^ x;  // exclusive
+    carry = total;
+    __syncthreads();
+  }
+  if (t == 0) raw_out[c] = raw_in[c] ^ carry;
+}
+
+// One thread per write: the chunk checksum right after it.
+__global__ void upd_apply_kernel(const uint32_t *__restrict__ blk_chunk, const uint32_t *__restrict__ blk_index,
+                                 uint32_t n, uint32_t nchunks, uint32_t bpc, const uint32_t *__restrict__ raw_in,
+                                 const uint32_t *__restrict__ colpre, const uint32_t *__restrict__ inpre,
+                                 uint32_t *__restrict__ out_raw) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t c = blk_chunk[i], b = blk_index[i];
+  out_raw[i] = (c < nchunks && b < bpc) ? raw_in[c] ^ colpre[(uint64_t)(i / kTile) * nchunks + c] ^ inpre[i] : 0u;
+}
+
+// Dense tile path unless the aggregate matrix would be large (or a test forces the
+// sort path with H3C_UPD_SCAN=sort).
+bool use_tiles(uint32_t n, uint32_t nchunks) {
+  if (const char *e = std::getenv("H3C_UPD_SCAN"))
+    if (std::strcmp(e, "sort") == 0) return false;
+  const uint64_t ntiles = (n + kTile - 1) / kTile;
+  return ntiles * nchunks <= (1ull << 22);
 }
 
 struct Workspace {
-  uint64_t *key1, *key1s, *key2, *key2s;
-  uint32_t *prev, *final_of, *delta, *ckey, *vals, *scan, *sh, *err;
+  uint32_t *kslot, *kslot_s, *kchunk, *kchunk_s, *iota, *idx1, *idx2;
+  uint32_t *prev, *final_of, *delta, *vals, *scan, *sh, *err;
+  uint32_t *agg, *colpre;  // dense tile path: ntiles x nchunks each
   void *tmp;
   size_t tmp_bytes;
 };
@@ -335,20 +434,17 @@ int layout(void *base, uint32_t n, uint32_t nchunks, uint32_t bpc, Workspace &w,
     off += align_up(bytes);
     return p;
   };
-  w.key1 = (uint64_t *)take(8ull * n);
-  w.key1s = (uint64_t *)take(8ull * n);
-  w.key2 = (uint64_t *)take(8ull * n);
-  w.key2s = (uint64_t *)take(8ull * n);
-  w.prev = (uint32_t *)take(4ull * n);
-  w.final_of = (uint32_t *)take(4ull * n);
-  w.delta = (uint32_t *)take(4ull * n);
-  w.ckey = (uint32_t *)take(4ull * n);
-  w.vals = (uint32_t *)take(4ull * n);
-  w.scan = (uint32_t *)take(4ull * n);
+  uint32_t **arrays[] = {&w.kslot, &w.kslot_s, &w.kchunk, &w.kchunk_s, &w.iota, &w.idx1,
+                         &w.idx2,  &w.prev,    &w.final_of, &w.delta, &w.vals, &w.scan};
+  for (uint32_t **a : arrays) *a = (uint32_t *)take(4ull * n);
   w.sh = (uint32_t *)take(4ull * bpc);
   w.err = (uint32_t *)take(4);
+  const uint64_t tiles_cells = use_tiles(n, nchunks) ? (uint64_t)((n + kTile - 1) / kTile) * nchunks : 0;
+  w.agg = (uint32_t *)take(4ull * tiles_cells);
+  w.colpre = (uint32_t *)take(4ull * tiles_cells);
   size_t s1 = 0, s2 = 0;
-  if (rocprim::radix_sort_keys(nullptr, s1, (uint64_t *)nullptr, (uint64_t *)nullptr, n, 0, 64) != hipSuccess)
+  if (rocprim::radix_sort_pairs<SortConfig>(nullptr, s1, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                (uint32_t *)nullptr, n, 0, 32) != hipSuccess)
     return H3C_ERR_HIP;
   if (rocprim::inclusive_scan_by_key(nullptr, s2, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                      (size_t)n, XorOp()) != hipSuccess)
@@ -356,7 +452,45 @@ int layout(void *base, uint32_t n, uint32_t nchunks, uint32_t bpc, Workspace &w,
   w.tmp_bytes = std::max(s1, s2);
   w.tmp = take(w.tmp_bytes);
   total = off;
-  (void)nchunks;
+  return H3C_OK;
+}
+
+// Per-(device, polynomial, chunk_len, block_bytes) block-shift tables sh[b] =
+// x^(8*(L-(b+1)*G)), built once and kept for the process ("precomputed per chunk
+// size").  Entries are never freed, so a table handed out stays valid; the cache is
+// bounded, and a miss past the bound computes into the caller's workspace instead.
+struct ShiftEntry {
+  int dev;
+  int type;
+  uint64_t chunk_len;
+  uint32_t block_bytes;
+  uint32_t *table;
+};
+std::mutex g_shift_mu;
+std::vector<ShiftEntry> g_shift_cache;
+constexpr size_t kShiftCacheMax = 16;
+
+int shift_table(int dev, uint8_t type, uint64_t chunk_len, uint32_t block_bytes, const PolyConsts *pc,
+                uint32_t *scratch, hipStream_t st, const uint32_t **out) {
+  const uint32_t bpc = (uint32_t)(chunk_len / block_bytes);
+  const uint32_t tb = 256;
+  std::lock_guard<std::mutex> lk(g_shift_mu);
+  for (const ShiftEntry &e : g_shift_cache)
+    if (e.dev == dev && e.type == type && e.chunk_len == chunk_len && e.block_bytes == block_bytes) {
+      *out = e.table;
+      return H3C_OK;
+    }
+  uint32_t *table = scratch;
+  const bool keep = g_shift_cache.size() < kShiftCacheMax;
+  if (keep) HIP_TRY(hipMalloc(&table, 4ull * bpc));
+  hipLaunchKernelGGL(upd_shift_kernel, dim3((bpc + tb - 1) / tb), dim3(tb), 0, st, bpc, chunk_len, block_bytes, pc,
+                     table);
+  HIP_TRY(hipGetLastError());
+  if (keep) {  // publish only once the table is complete: other threads use it on other streams
+    HIP_TRY(hipStreamSynchronize(st));
+    g_shift_cache.push_back({dev, type, chunk_len, block_bytes, table});
+  }
+  *out = table;
   return H3C_OK;
 }
 
@@ -379,7 +513,8 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
                       size_t workspace_bytes, uint32_t *n_invalid_dev, void *stream) {
   if (type != H3C_TYPE_CRC32C && type != H3C_TYPE_CRC32) return H3C_ERR_INVALID_ARG;
   if (!block_bytes || block_bytes % kRowBytes || chunk_len % block_bytes || !nchunks) return H3C_ERR_INVALID_ARG;
-  if ((uint64_t)nchunks * (chunk_len / block_bytes) >= 0xFFFFFFFFull) return H3C_ERR_INVALID_ARG;
+  if ((uint64_t)nchunks * (chunk_len / block_bytes) >= 0xFFFFFFFFull || n_blocks == 0xFFFFFFFFu)
+    return H3C_ERR_INVALID_ARG;
   if (!chunk_base_dev || !chunk_raw_in_dev || !chunk_raw_out_dev) return H3C_ERR_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(hipMemcpyAsync(chunk_raw_out_dev, chunk_raw_in_dev, 4ull * nchunks, hipMemcpyDeviceToDevice, st));
@@ -405,35 +540,53 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
 
   HIP_TRY(hipMemsetAsync(w.err, 0, 4, st));
   hipLaunchKernelGGL(upd_keys_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks, bpc,
-                     w.key1, w.key2, w.err);
+                     w.kslot, w.kchunk, w.iota, w.err);
   HIP_TRY(hipGetLastError());
-  const uint32_t slot_bits = bits_for((uint64_t)nchunks * bpc + 1);  // + sentinel slot
+  // Stable radix sorts of (key, sequence index) over only the key's bits: by slot
+  // (chunk, block) for the previous-writer links, by chunk for the per-chunk scan.
   size_t tmp = w.tmp_bytes;
-  HIP_TRY(rocprim::radix_sort_keys(w.tmp, tmp, w.key1, w.key1s, n_blocks, 0, 32 + slot_bits, st));
-  hipLaunchKernelGGL(upd_link_kernel, dim3(gb), dim3(tb), 0, st, w.key1s, n_blocks, w.prev, w.final_of);
+  HIP_TRY(rocprim::radix_sort_pairs<SortConfig>(w.tmp, tmp, w.kslot, w.kslot_s, w.iota, w.idx1, n_blocks, 0,
+                                    bits_for((uint64_t)nchunks * bpc + 1), st));
+  hipLaunchKernelGGL(upd_link_kernel, dim3(gb), dim3(tb), 0, st, w.kslot_s, w.idx1, n_blocks, w.prev, w.final_of);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(upd_shift_kernel, dim3((bpc + tb - 1) / tb), dim3(tb), 0, st, bpc, chunk_len, block_bytes, pc,
-                     w.sh);
-  HIP_TRY(hipGetLastError());
+  const uint32_t *sh = nullptr;
+  rc = shift_table(dev, type, chunk_len, block_bytes, pc, w.sh, st, &sh);
+  if (rc) return rc;
   const uint32_t blocks = std::min<uint32_t>(num_cu, (n_blocks + kWavesPerBlock - 1) / kWavesPerBlock);
   h3c_rt::ProfToken tok;
   HIP_TRY(h3c_rt::prof_begin(st, tok));
   hipLaunchKernelGGL(upd_delta_kernel, dim3(blocks), dim3(kThreads), 0, st, chunk_base_dev, nchunks, bpc, block_bytes,
                      blk_chunk_dev, blk_index_dev, static_cast<const uint8_t *>(payload_dev), n_blocks, w.prev,
-                     w.final_of, w.sh, pc, w.delta);
+                     w.final_of, pc, w.delta);
   HIP_TRY(hipGetLastError());
   // algorithmic bytes: read new + read old + write back, per block write
   HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDATE, 3ull * block_bytes * n_blocks));
-  tmp = w.tmp_bytes;
-  HIP_TRY(rocprim::radix_sort_keys(w.tmp, tmp, w.key2, w.key2s, n_blocks, 0, 32 + bits_for((uint64_t)nchunks + 1), st));
-  hipLaunchKernelGGL(upd_gather_kernel, dim3(gb), dim3(tb), 0, st, w.key2s, n_blocks, w.delta, w.ckey, w.vals);
-  HIP_TRY(hipGetLastError());
-  tmp = w.tmp_bytes;
-  HIP_TRY(rocprim::inclusive_scan_by_key(w.tmp, tmp, w.ckey, w.vals, w.scan, (size_t)n_blocks, XorOp(),
-                                         rocprim::equal_to<uint32_t>(), st));
-  hipLaunchKernelGGL(upd_scatter_kernel, dim3(gb), dim3(tb), 0, st, w.key2s, n_blocks, nchunks, w.scan, chunk_raw_in_dev,
-                     out_raw_dev, chunk_raw_out_dev);
-  HIP_TRY(hipGetLastError());
+  const uint32_t poly = type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
+  if (use_tiles(n_blocks, nchunks)) {
+    const uint32_t ntiles = (n_blocks + kTile - 1) / kTile;
+    hipLaunchKernelGGL(upd_tile_kernel, dim3(ntiles), dim3(kTile), 0, st, blk_chunk_dev, blk_index_dev, n_blocks,
+                       nchunks, bpc, w.delta, sh, poly, w.scan, w.agg);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(upd_column_kernel, dim3(nchunks), dim3(kTile), 0, st, w.agg, ntiles, nchunks, chunk_raw_in_dev,
+                       w.colpre, chunk_raw_out_dev);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(upd_apply_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks,
+                       bpc, chunk_raw_in_dev, w.colpre, w.scan, out_raw_dev);
+    HIP_TRY(hipGetLastError());
+  } else {
+    tmp = w.tmp_bytes;
+    HIP_TRY(rocprim::radix_sort_pairs<SortConfig>(w.tmp, tmp, w.kchunk, w.kchunk_s, w.iota, w.idx2, n_blocks, 0,
+                                                  bits_for((uint64_t)nchunks + 1), st));
+    hipLaunchKernelGGL(upd_gather_kernel, dim3(gb), dim3(tb), 0, st, w.kchunk_s, w.idx2, n_blocks, nchunks,
+                       blk_index_dev, w.delta, sh, poly, w.vals);
+    HIP_TRY(hipGetLastError());
+    tmp = w.tmp_bytes;
+    HIP_TRY(rocprim::inclusive_scan_by_key(w.tmp, tmp, w.kchunk_s, w.vals, w.scan, (size_t)n_blocks, XorOp(),
+                                           rocprim::equal_to<uint32_t>(), st));
+    hipLaunchKernelGGL(upd_scatter_kernel, dim3(gb), dim3(tb), 0, st, w.kchunk_s, w.idx2, n_blocks, nchunks, w.scan,
+                       chunk_raw_in_dev, out_raw_dev, chunk_raw_out_dev);
+    HIP_TRY(hipGetLastError());
+  }
   if (n_invalid_dev) HIP_TRY(hipMemcpyAsync(n_invalid_dev, w.err, 4, hipMemcpyDeviceToDevice, st));
   return H3C_OK;
 }

@@ -98,7 +98,18 @@ def run_case(h3c, torch, dev, nchunks, chunk_len, writes, seed, replay_chunks=No
     assert int(ninv.item()) == sum(1 for v in valid if not v)
 
 
-def test_update_small_random_with_collisions(h3c, torch_dev):
+@pytest.fixture(params=["tiles", "sort"])
+def scan_mode(request, monkeypatch):
+    """Both per-chunk scan paths: dense tiles (default at these sizes) and the rocPRIM
+    sort + scan_by_key fallback for many chunks (forced by H3C_UPD_SCAN=sort)."""
+    if request.param == "sort":
+        monkeypatch.setenv("H3C_UPD_SCAN", "sort")
+    else:
+        monkeypatch.delenv("H3C_UPD_SCAN", raising=False)
+    return request.param
+
+
+def test_update_small_random_with_collisions(h3c, torch_dev, scan_mode):
     torch, dev = torch_dev
     rng = np.random.default_rng(1)
     nchunks, chunk_len = 6, 256 << 10  # 64 blocks per chunk -> many same-slot rewrites
@@ -106,7 +117,7 @@ def test_update_small_random_with_collisions(h3c, torch_dev):
     run_case(h3c, torch, dev, nchunks, chunk_len, writes, seed=2)
 
 
-def test_update_multiblock_and_reuse_and_invalid(h3c, torch_dev):
+def test_update_multiblock_and_reuse_and_invalid(h3c, torch_dev, scan_mode):
     torch, dev = torch_dev
     rng = np.random.default_rng(3)
     nchunks, chunk_len = 4, 128 << 10
@@ -122,7 +133,7 @@ def test_update_multiblock_and_reuse_and_invalid(h3c, torch_dev):
              invalid=[(5, (nchunks, 0)), (77, (0, 999)), (300, (7, 7))])
 
 
-def test_update_single_slot_hammer(h3c, torch_dev):
+def test_update_single_slot_hammer(h3c, torch_dev, scan_mode):
     """Every write hits one slot: the longest possible previous-writer chain."""
     torch, dev = torch_dev
     run_case(h3c, torch, dev, 2, 64 << 10, [(1, 5, 1)] * 700 + [(0, 15, 1)] * 3, seed=5)
