@@ -31,7 +31,14 @@ from .engine import (  # noqa: F401
     profile_enable,
     profile_read,
     update_blocks,
+    update_ios,
     update_workspace_bytes,
+    CHUNK_STATE_DTYPE,
+    UPDATE_IO_DTYPE,
+    UPDATE_RESULT_DTYPE,
+    UPD_WRITE,
+    UPD_TRUNCATE,
+    UPD_EXTEND,
 )
 
 __all__ = [
@@ -54,5 +61,12 @@ __all__ = [
     "profile_enable",
     "profile_read",
     "update_blocks",
+    "update_ios",
     "update_workspace_bytes",
+    "CHUNK_STATE_DTYPE",
+    "UPDATE_IO_DTYPE",
+    "UPDATE_RESULT_DTYPE",
+    "UPD_WRITE",
+    "UPD_TRUNCATE",
+    "UPD_EXTEND",
 ]

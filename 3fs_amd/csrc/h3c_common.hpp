@@ -103,6 +103,7 @@ struct PolyConsts {
   uint32_t fix[256];     // [4l+j] = x^-(8*(16l+4j))
   uint32_t fixz[16];     // [z]    = x^-(8z)
   uint32_t pow8[64];     // [k]    = x^(8*2^k)
+  uint32_t ipow8[64];    // [k]    = x^-(8*2^k)  (x is invertible mod P: P has a constant term)
   uint32_t poly;
   uint32_t pad[3];
   // Byte tables for multiplying by the 7 constants of the wave fold (wave_fold_tab):
@@ -123,10 +124,12 @@ inline void build_consts(PolyConsts &pc, uint32_t poly) {
   for (int l = 0; l < 64; ++l)
     for (int j = 0; j < 4; ++j) pc.fix[4 * l + j] = hgf_pow(xinv8, 16u * l + 4u * j, poly);
   for (int z = 0; z < 16; ++z) pc.fixz[z] = hgf_pow(xinv8, z, poly);
-  uint32_t p = 0x00800000u;
+  uint32_t p = 0x00800000u, q = xinv8;
   for (int k = 0; k < 64; ++k) {
     pc.pow8[k] = p;
+    pc.ipow8[k] = q;
     p = hgf_mul(p, p, poly);
+    q = hgf_mul(q, q, poly);
   }
   for (int m = 0; m < kRedTables; ++m) {
     const uint32_t c = hgf_pow(xinv8, m == 0 ? 4u : 16u << (m - 1), poly);
@@ -155,6 +158,20 @@ __device__ uint32_t dxpow8n(uint64_t n, const PolyConsts *__restrict__ pc, uint3
   while (n) {
     if (n & 1u) r = (r == kOne) ? pc->pow8[k] : dgf_mul(r, pc->pow8[k], poly);
     n >>= 1;
+    ++k;
+  }
+  return r;
+}
+
+// x^(8n) for a signed byte count n (negative: the inverse shift, used when a chunk shrinks).
+__device__ inline uint32_t dxpow8s(int64_t n, const PolyConsts *__restrict__ pc, uint32_t poly) {
+  if (n >= 0) return dxpow8n((uint64_t)n, pc, poly);
+  uint64_t m = (uint64_t)(-n);
+  uint32_t r = kOne;
+  int k = 0;
+  while (m) {
+    if (m & 1u) r = (r == kOne) ? pc->ipow8[k] : dgf_mul(r, pc->ipow8[k], poly);
+    m >>= 1;
     ++k;
   }
   return r;

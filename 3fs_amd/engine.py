@@ -82,6 +82,7 @@ _proto("h3c_batch_combine", _int, _u8, _vp, _vp, _vp, _sz, _vp, _vp)
 _proto("h3c_fill_splitmix", _int, _vp, _u64, _u64, _u64, _u64, _u64, _vp)
 _proto("h3c_update_workspace_bytes", _sz, _u32, _u32, _u64, _u32)
 _proto("h3c_update_blocks", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp)
+_proto("h3c_update_ios", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp)
 _proto("h3c_hostfed_create", _int, _int, _u64, ctypes.POINTER(_vp))
 _proto("h3c_hostfed_run", _int, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp)
 _proto("h3c_hostfed_destroy", None, _vp)
@@ -284,6 +285,38 @@ def update_blocks(chunk_bases, chunk_len: int, raw_in, blk_chunk, blk_index, pay
                                  n, out_raw.data_ptr(), raw_out.data_ptr(), workspace.data_ptr(),
                                  workspace.numel() * workspace.element_size(),
                                  n_invalid.data_ptr() if n_invalid is not None else None, _stream_handle(stream)))
+
+
+# ---------------------------------------------------------------- general updates (h3c_update_ios)
+
+UPD_WRITE, UPD_TRUNCATE, UPD_EXTEND = 1, 4, 8  # UpdateType (Common.h:51-58)
+UPD_STD_DOMAIN = 1  # flag: Rust chunk engine semantics (std-domain values)
+
+CHUNK_STATE_DTYPE = np.dtype([("base", "<u8"), ("chunk_size", "<u4"), ("size", "<u4"), ("value", "<u4"),
+                              ("type", "u1"), ("reserved", "u1", 3)])
+UPDATE_IO_DTYPE = np.dtype([("payload", "<u8"), ("chunk", "<u4"), ("offset", "<u4"), ("length", "<u4"),
+                            ("checksum_value", "<u4"), ("checksum_type", "u1"), ("kind", "u1"),
+                            ("reserved", "u1", 6)])
+UPDATE_RESULT_DTYPE = np.dtype([("status", "<u4"), ("size", "<u4"), ("value", "<u4"), ("type", "u1"),
+                                ("reserved", "u1", 3)])
+assert CHUNK_STATE_DTYPE.itemsize == 24 and UPDATE_IO_DTYPE.itemsize == 32 and UPDATE_RESULT_DTYPE.itemsize == 16
+
+
+def update_ios(chunks: np.ndarray, ios: np.ndarray, type_: int = ChecksumType.CRC32C, std_domain: bool = False,
+               stream=None) -> np.ndarray:
+    """Batched ChunkReplica::update + updateChecksum for any mix of WRITE / TRUNCATE / EXTEND
+    (h3c_update_ios).  `chunks` (CHUNK_STATE_DTYPE, updated in place: size / type / value)
+    and `ios` (UPDATE_IO_DTYPE) are host arrays whose `base` / `payload` fields are device
+    addresses.  Returns one UPDATE_RESULT_DTYPE record per op: status 0 / 3 kInvalidArg /
+    4080 kChecksumMismatch, chunk size after, and result.checksum (type, value)."""
+    if chunks.dtype != CHUNK_STATE_DTYPE or ios.dtype != UPDATE_IO_DTYPE:
+        raise TypeError("chunks / ios must use CHUNK_STATE_DTYPE / UPDATE_IO_DTYPE")
+    if not (chunks.flags.c_contiguous and ios.flags.c_contiguous):
+        raise ValueError("chunks / ios must be contiguous")
+    res = np.zeros(len(ios), dtype=UPDATE_RESULT_DTYPE)
+    _check(lib.h3c_update_ios(int(type_), chunks.ctypes.data, len(chunks), ios.ctypes.data, len(ios),
+                              res.ctypes.data, UPD_STD_DOMAIN if std_domain else 0, _stream_handle(stream)))
+    return res
 
 
 def profile_enable(on: bool = True) -> None:

@@ -138,6 +138,60 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
                       uint32_t *out_raw_dev, uint32_t *chunk_raw_out_dev, void *workspace_dev,
                       size_t workspace_bytes, uint32_t *n_invalid_dev, void *stream);
 
+/* ---- general batched updates: every UpdateIO case of ChunkReplica::update ---- */
+
+/* UpdateType (src/fbs/storage/Common.h:51-58); REMOVE / COMMIT touch no checksum. */
+enum h3c_update_kind { H3C_UPD_WRITE = 1, H3C_UPD_TRUNCATE = 4, H3C_UPD_EXTEND = 8 };
+
+/* ChunkMetadata fields on the path (Common.h:662-676) plus where the bytes live. */
+typedef struct h3c_chunk_state {
+  uint64_t base;       /* device address of the chunk bytes, capacity chunk_size */
+  uint32_t chunk_size; /* innerFileId.chunkSize: the write bound */
+  uint32_t size;       /* meta.size            (in / out) */
+  uint32_t value;      /* meta.checksumValue   (in / out; raw, std with H3C_UPD_STD_DOMAIN) */
+  uint8_t type;        /* meta.checksumType    (in / out) */
+  uint8_t reserved[3];
+} h3c_chunk_state;
+
+/* UpdateIO fields on the path (Common.h:326-345). */
+typedef struct h3c_update_io {
+  uint64_t payload;        /* device address of `length` bytes (WRITE) */
+  uint32_t chunk;          /* index into the chunk table */
+  uint32_t offset;
+  uint32_t length;         /* WRITE: bytes; TRUNCATE / EXTEND: the new chunk length */
+  uint32_t checksum_value; /* the client's ChecksumInfo of the payload */
+  uint8_t checksum_type;
+  uint8_t kind;            /* h3c_update_kind */
+  uint8_t reserved[6];
+} h3c_update_io;
+
+typedef struct h3c_update_result {
+  uint32_t status; /* H3C_OK, H3C_ERR_INVALID_ARG (range, :140-145), H3C_ERR_CHECKSUM_MISMATCH (:193-207) */
+  uint32_t size;   /* meta.size after the op */
+  uint32_t value;  /* result.checksum after the op (meta.checksum(), ChunkReplica.cc:313) */
+  uint8_t type;
+  uint8_t reserved[3];
+} h3c_update_result;
+
+/* flags */
+#define H3C_UPD_STD_DOMAIN 1u /* Rust chunk engine (chunk_engine/src/alloc/chunk.rs:89-281): values are
+                                 std-domain crc32c and every applied op leaves crc32c(content) */
+
+/* Apply `n` UpdateIOs in sequence order to device-resident chunks, replacing
+ * ChunkReplica::update's per-op payload verify (ChunkReplica.cc:193-207), zero fill,
+ * write / truncate / extend (:256-294) and updateChecksum (:319-394, all four cases)
+ * -- or, with H3C_UPD_STD_DOMAIN, Chunk::safe_write / copy_on_write's checksum.
+ * Arbitrary offsets and lengths; writes to the same bytes are ordered.  The chunk
+ * checksum is maintained by GF(2) deltas: a write costs its own bytes plus the
+ * overwritten bytes, a truncate the cut tail; a chunk whose stored checksum is not of
+ * `poly_type` (e.g. NONE) is CRC'd once.  A stored checksum of `poly_type` is trusted,
+ * as the reference's append case trusts it.  Client checksums must be NONE or
+ * `poly_type` (the client's chunk_checksum_type), else the op fails with
+ * H3C_ERR_INVALID_ARG.  `chunks` and `results` are host arrays; chunk bytes are
+ * updated in place on device.  Synchronous on `stream`. */
+int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios, uint32_t n,
+                   h3c_update_result *results, uint32_t flags, void *stream);
+
 /* ---- host-fed pipeline (payloads in host memory, BASELINE config 5) ---- */
 
 /* A reusable pipeline: two HBM staging windows of `window_bytes` and a copy stream.

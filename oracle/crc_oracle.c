@@ -294,6 +294,65 @@ int orc_update_checksum(orc_chunk_meta *meta, orc_write_io wio, uint32_t chunk_s
 }
 
 /* ------------------------------------------------------------------ */
+/* A6 + A8: ChunkReplica::update (ChunkReplica.cc:131-317) for WRITE,   */
+/* TRUNCATE and EXTEND, with the chunk file modelled as a byte array.   */
+/* ------------------------------------------------------------------ */
+int orc_chunk_replica_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chunk_size, const orc_update_io *io,
+                             const uint8_t *payload, orc_update_result *res) {
+  res->status = ORC_OK;
+  res->size = meta->size;
+  res->type = ORC_NONE; /* IOResult default until :171 */
+  res->value = 0;
+  /* :140-145 range check (not for REMOVE) */
+  if (io->offset >= chunk_size || (uint64_t)io->offset + io->length > chunk_size) {
+    res->status = 3; /* StatusCode::kInvalidArg */
+    return res->status;
+  }
+  res->type = meta->checksum_type; /* :171 result.checksum = meta.checksum() */
+  res->value = meta->checksum_value;
+  /* :193-207 verify the client's checksum of the payload */
+  if (io->checksum_type != ORC_NONE && io->length != 0) {
+    uint8_t t;
+    uint32_t v;
+    orc_checksum_create(io->checksum_type, payload, io->length, ~0u, &t, &v);
+    if (t != io->checksum_type || v != io->checksum_value) {
+      res->status = ORC_ERR_CHECKSUM_MISMATCH;
+      return res->status;
+    }
+  }
+  const int is_append = io->offset == meta->size; /* :244 */
+  const uint32_t size_before = meta->size;       /* :256 */
+  if (io->kind == ORC_UPD_TRUNCATE || io->kind == ORC_UPD_EXTEND) { /* :260-273 */
+    if (io->length <= meta->size) {
+      if (io->kind == ORC_UPD_TRUNCATE) meta->size = io->length;
+    } else { /* extend with zeros */
+      memset(chunk + meta->size, 0, io->length - meta->size);
+      meta->size = io->length;
+    }
+  } else { /* :281-291 WRITE: zero fill a gap, then the write */
+    if (meta->size < io->offset) memset(chunk + meta->size, 0, io->offset - meta->size);
+    if (io->length) memcpy(chunk + io->offset, payload, io->length);
+    const uint32_t end = io->offset + io->length; /* doRealWrite :124 */
+    if (end > meta->size) meta->size = end;
+  }
+  orc_write_io w;
+  w.offset = io->offset;
+  w.length = io->length;
+  w.checksum_type = io->checksum_type;
+  w.checksum_value = io->checksum_value;
+  w.is_truncate_or_extend = io->kind != ORC_UPD_WRITE;
+  int rc = orc_update_checksum(meta, w, size_before, is_append, chunk); /* :297 */
+  if (rc) {
+    res->status = rc;
+    return rc;
+  }
+  res->size = meta->size;
+  res->type = meta->checksum_type; /* :313 result.checksum = meta.checksum() */
+  res->value = meta->checksum_value;
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------ */
 /* A7: AioReadJob::setResult (BatchReadJob.cc:24-55).                   */
 /* ------------------------------------------------------------------ */
 int orc_read_result_checksum(uint8_t batch_type, uint8_t chunk_type, uint32_t chunk_value, uint32_t chunk_len,

@@ -65,6 +65,27 @@ typedef struct {
 int orc_update_checksum(orc_chunk_meta *meta, orc_write_io wio, uint32_t chunk_size_before_write, int is_append_write,
                         const uint8_t *chunk_after_write);
 
+/* --- A6 + A8: ChunkReplica::update restated over an in-memory chunk ---
+ * One UpdateIO (WRITE / TRUNCATE / EXTEND) applied to `chunk` (capacity chunk_size):
+ * range check, client-checksum verify, zero fill of gaps, the write / truncate /
+ * extend itself, then updateChecksum.  `meta` is updated in place. */
+enum { ORC_UPD_WRITE = 1, ORC_UPD_TRUNCATE = 4, ORC_UPD_EXTEND = 8 };
+typedef struct {
+  uint8_t kind; /* UpdateType */
+  uint32_t offset;
+  uint32_t length;
+  uint8_t checksum_type;
+  uint32_t checksum_value;
+} orc_update_io;
+typedef struct {
+  int status;    /* 0, 3 kInvalidArg, 4080 kChecksumMismatch */
+  uint32_t size; /* meta.size after */
+  uint8_t type;  /* result.checksum */
+  uint32_t value;
+} orc_update_result;
+int orc_chunk_replica_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chunk_size, const orc_update_io *io,
+                             const uint8_t *payload, orc_update_result *res);
+
 /* --- A7: AioReadJob::setResult checksum selection (recalculate path) --- */
 int orc_read_result_checksum(uint8_t batch_type, uint8_t chunk_type, uint32_t chunk_value, uint32_t chunk_len,
                              uint32_t read_offset, uint32_t read_len, const uint8_t *read_data,

@@ -117,3 +117,39 @@ def update_checksum(meta: dict, wio: dict, size_before: int, is_append: bool, ch
     w = WriteIO(wio["offset"], wio["length"], wio["type"], wio["value"] & 0xFFFFFFFF, int(wio.get("trunc_ext", 0)))
     rc = lib().orc_update_checksum(ctypes.byref(m), w, size_before, int(is_append), _ptr(chunk_after))
     return rc, {"size": m.size, "type": m.checksum_type, "value": m.checksum_value}
+
+
+UPD_WRITE, UPD_TRUNCATE, UPD_EXTEND = 1, 4, 8  # UpdateType (Common.h:51-58)
+
+
+class UpdateIO(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint8), ("offset", ctypes.c_uint32), ("length", ctypes.c_uint32),
+                ("checksum_type", ctypes.c_uint8), ("checksum_value", ctypes.c_uint32)]
+
+
+class UpdateResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int), ("size", ctypes.c_uint32), ("type", ctypes.c_uint8),
+                ("value", ctypes.c_uint32)]
+
+
+def replica_update(meta: dict, chunk: np.ndarray, chunk_size: int, io: dict, payload=None):
+    """ChunkReplica::update restatement (A6 + A8): applies one UpdateIO to `chunk` in place.
+
+    Returns (result dict, new meta dict)."""
+    L = lib()
+    if not hasattr(L, "_replica_update_bound"):
+        L.orc_chunk_replica_update.restype = ctypes.c_int
+        L.orc_chunk_replica_update.argtypes = [ctypes.POINTER(ChunkMeta), ctypes.c_void_p, ctypes.c_uint32,
+                                               ctypes.POINTER(UpdateIO), ctypes.c_void_p,
+                                               ctypes.POINTER(UpdateResult)]
+        L._replica_update_bound = True
+    m = ChunkMeta(meta["size"], meta["type"], meta["value"] & 0xFFFFFFFF)
+    u = UpdateIO(io["kind"], io["offset"], io["length"], io["type"], io["value"] & 0xFFFFFFFF)
+    r = UpdateResult()
+    pay = None
+    if payload is not None and len(payload):
+        pay = np.ascontiguousarray(payload, dtype=np.uint8)
+    L.orc_chunk_replica_update(ctypes.byref(m), chunk.ctypes.data, chunk_size, ctypes.byref(u),
+                               pay.ctypes.data if pay is not None else None, ctypes.byref(r))
+    return ({"status": r.status, "size": r.size, "type": r.type, "value": r.value},
+            {"size": m.size, "type": m.checksum_type, "value": m.checksum_value})

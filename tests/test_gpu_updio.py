@@ -1,0 +1,272 @@
+"""General batched updates on the GPU (h3c_update_ios) vs the reference's ChunkReplica::update.
+
+Every op is replayed through the oracle's restatement of ChunkReplica::update
+(src/storage/store/ChunkReplica.cc:131-317: range check, client-checksum verify, zero
+fill, write / truncate / extend, and updateChecksum's four cases, :319-394) on a host
+copy of the chunks.  The engine must reproduce each op's status, size and stored
+checksum, the final chunk bytes and the final chunk metadata.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+
+pytestmark = pytest.mark.gpu
+MASK = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available()
+    return torch, torch.device("cuda:0")
+
+
+class Scenario:
+    """Chunks in one HBM slab, payloads in another, and the oracle's host replica."""
+
+    def __init__(self, h3c, torch, dev, nchunks, chunk_size, rng, init="mixed"):
+        self.h3c, self.torch, self.dev, self.rng = h3c, torch, dev, rng
+        self.nchunks, self.chunk_size = nchunks, chunk_size
+        self.host = np.zeros((nchunks, chunk_size), dtype=np.uint8)
+        self.meta = []
+        for c in range(nchunks):
+            kind = init if init != "mixed" else ["empty", "crc", "none", "crc"][c % 4]
+            size = 0 if kind == "empty" else int(rng.integers(1, chunk_size + 1))
+            self.host[c, :size] = rng.integers(0, 256, size, dtype=np.uint8)
+            if kind == "crc":
+                self.meta.append({"size": size, "type": orc.CRC32C, "value": orc.crc32c(self.host[c, :size])})
+            elif kind == "none":
+                self.meta.append({"size": size, "type": orc.NONE, "value": 0})
+            else:
+                self.meta.append({"size": 0, "type": orc.CRC32C, "value": 0})
+        self.slab = torch.from_numpy(self.host.copy()).to(dev)
+        self.init_meta = [dict(m) for m in self.meta]
+        self.ops, self.payloads, self.expect = [], [], []
+
+    def add(self, kind, chunk, offset, length, ctype=orc.CRC32C, good=True, payload=None):
+        if payload is None and kind == orc.UPD_WRITE:
+            payload = self.rng.integers(0, 256, length, dtype=np.uint8)
+        value = 0
+        if ctype != orc.NONE:
+            value = orc.create(ctype, payload if payload is not None else b"", length)[1] if kind == orc.UPD_WRITE \
+                else 0
+            if not good:
+                value ^= 0x10
+        io = {"kind": kind, "offset": offset, "length": length, "type": ctype, "value": value}
+        self.ops.append((chunk, io))
+        self.payloads.append(payload)
+        if chunk < self.nchunks:
+            res, self.meta[chunk] = orc.replica_update(self.meta[chunk], self.host[chunk], self.chunk_size, io,
+                                                       payload)
+        else:
+            res = {"status": 3, "size": 0, "type": 0, "value": 0}
+        self.expect.append(res)
+        return res
+
+    def run(self):
+        torch, h3c = self.torch, self.h3c
+        # payloads packed at odd offsets so payload and chunk alignments differ
+        offs, total = [], 0
+        for p in self.payloads:
+            total += int(self.rng.integers(0, 17))
+            offs.append(total)
+            total += 0 if p is None else len(p)
+        pay = np.zeros(max(total, 1), dtype=np.uint8)
+        for o, p in zip(offs, self.payloads):
+            if p is not None:
+                pay[o:o + len(p)] = p
+        dpay = torch.from_numpy(pay).to(self.dev)
+        chunks = np.zeros(self.nchunks, dtype=h3c.CHUNK_STATE_DTYPE)
+        for c, m in enumerate(self.init_meta):
+            chunks[c] = (self.slab.data_ptr() + c * self.chunk_size, self.chunk_size, m["size"], m["value"], m["type"],
+                         0)
+        ios = np.zeros(len(self.ops), dtype=h3c.UPDATE_IO_DTYPE)
+        for i, ((c, io), o, p) in enumerate(zip(self.ops, offs, self.payloads)):
+            ios[i] = (dpay.data_ptr() + o if p is not None else 0, c, io["offset"], io["length"], io["value"],
+                      io["type"], io["kind"], 0)
+        res = h3c.update_ios(chunks, ios)
+        torch.cuda.synchronize()
+        return chunks, res
+
+    def check(self, chunks, res):
+        bad = []
+        for i, (r, e) in enumerate(zip(res, self.expect)):
+            got = (int(r["status"]), int(r["size"]), int(r["type"]), int(r["value"]))
+            want = (e["status"], e["size"], e["type"], e["value"] & MASK)
+            if got != want:
+                bad.append((i, self.ops[i], got, want))
+        assert not bad, bad[:5]
+        dev_bytes = self.slab.cpu().numpy()
+        for c, m in enumerate(self.meta):
+            assert (int(chunks[c]["size"]), int(chunks[c]["type"]), int(chunks[c]["value"])) == \
+                (m["size"], m["type"], m["value"] & MASK), c
+            assert np.array_equal(dev_bytes[c, :m["size"]], self.host[c, :m["size"]]), f"chunk {c} bytes"
+
+
+def random_scenario(h3c, torch, dev, rng, nchunks, chunk_size, nops, align=1, hot=None):
+    sc = Scenario(h3c, torch, dev, nchunks, chunk_size, rng)
+    for _ in range(nops):
+        c = int(rng.integers(0, nchunks))
+        size = sc.meta[c]["size"]
+        u = rng.random()
+        if u < 0.55:  # write somewhere (maybe past the end: gap)
+            if hot is not None:
+                off = int(rng.integers(0, hot))
+            else:
+                off = int(rng.integers(0, chunk_size))
+            off -= off % align
+            length = int(rng.integers(0, min(chunk_size - off, 3 * 4096) + 1))
+            ctype = orc.CRC32C if rng.random() > 0.1 else orc.NONE
+            sc.add(orc.UPD_WRITE, c, off, length, ctype, good=rng.random() > 0.05)
+        elif u < 0.70:  # append at the current end
+            if size >= chunk_size:
+                continue
+            length = int(rng.integers(1, min(chunk_size - size, 8192) + 1))
+            sc.add(orc.UPD_WRITE, c, size, length)
+        elif u < 0.78:  # whole-chunk overwrite from 0 (updateChecksum reuse case)
+            length = int(rng.integers(1, chunk_size + 1))
+            sc.add(orc.UPD_WRITE, c, 0, length)
+        elif u < 0.86:
+            sc.add(orc.UPD_TRUNCATE, c, 0, int(rng.integers(0, chunk_size + 1)), orc.NONE)
+        elif u < 0.93:
+            sc.add(orc.UPD_EXTEND, c, 0, int(rng.integers(0, chunk_size + 1)), orc.NONE)
+        elif u < 0.97:  # out of range -> kInvalidArg
+            sc.add(orc.UPD_WRITE, c, chunk_size - 10, 20)
+        else:  # zero-length write past the end (grows the chunk with zeros)
+            sc.add(orc.UPD_WRITE, c, int(rng.integers(0, chunk_size)), 0)
+    return sc
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_updio_random_mixed_ops(h3c, torch_dev, seed):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(seed)
+    sc = random_scenario(h3c, torch, dev, rng, nchunks=8, chunk_size=64 << 10, nops=400)
+    sc.check(*sc.run())
+
+
+def test_updio_hot_region_conflicts(h3c, torch_dev):
+    """Many overlapping writes into the first 16 KiB of two chunks: long epoch chains."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(11)
+    sc = random_scenario(h3c, torch, dev, rng, nchunks=2, chunk_size=32 << 10, nops=300, hot=16 << 10)
+    sc.check(*sc.run())
+
+
+def test_updio_block_aligned_large(h3c, torch_dev):
+    """4 KiB-aligned writes into 1 MiB chunks (the storage service's common shape)."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(5)
+    sc = Scenario(h3c, torch, dev, 6, 1 << 20, rng, init="crc")
+    for _ in range(1500):
+        c = int(rng.integers(0, 6))
+        b = int(rng.integers(0, 256))
+        nb = int(rng.integers(1, 5))
+        nb = min(nb, 256 - b)
+        sc.add(orc.UPD_WRITE, c, b * 4096, nb * 4096)
+    sc.check(*sc.run())
+
+
+def test_updio_edge_cases(h3c, torch_dev):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(7)
+    cs = 40000  # not a multiple of 16 or 4096
+    sc = Scenario(h3c, torch, dev, 4, cs, rng, init="mixed")
+    sc.add(orc.UPD_WRITE, 0, 0, 0)                       # empty chunk, zero-length write
+    sc.add(orc.UPD_WRITE, 0, 5, 3)                       # gap of 5 zeros on an empty chunk
+    sc.add(orc.UPD_WRITE, 0, 8, 1)                       # append 1 byte
+    sc.add(orc.UPD_WRITE, 0, 0, 9)                       # full overwrite (reuse)
+    sc.add(orc.UPD_WRITE, 0, 0, 9, good=False)           # client checksum mismatch -> 4080
+    sc.add(orc.UPD_TRUNCATE, 0, 0, 0, orc.NONE)          # truncate to empty -> value 0
+    sc.add(orc.UPD_EXTEND, 0, 0, 777, orc.NONE)          # extend an empty chunk
+    sc.add(orc.UPD_WRITE, 2, 17, 100, orc.NONE)          # NONE-type write on a NONE chunk
+    sc.add(orc.UPD_WRITE, 2, 3, 50)                      # typed write on a NONE chunk: full CRC (INIT)
+    sc.add(orc.UPD_WRITE, 1, cs - 1, 1)                  # last byte of the chunk
+    sc.add(orc.UPD_WRITE, 1, cs, 1)                      # offset == chunkSize -> kInvalidArg
+    sc.add(orc.UPD_TRUNCATE, 1, 0, cs + 1, orc.NONE)     # length > chunkSize -> kInvalidArg
+    sc.add(orc.UPD_TRUNCATE, 3, 0, 1, orc.NONE)          # shrink to 1 byte
+    sc.add(orc.UPD_WRITE, 3, 30000, 5000)                # big gap after a truncate (stale bytes -> zeros)
+    sc.add(orc.UPD_EXTEND, 3, 0, 10, orc.NONE)           # extend shorter than size: no-op
+    sc.add(orc.UPD_TRUNCATE, 3, 0, 35000, orc.NONE)      # truncate = same size: no-op
+    sc.add(orc.UPD_WRITE, 3, 0, cs)                      # whole chunk
+    sc.check(*sc.run())
+
+
+def test_updio_invalid_chunk_index(h3c, torch_dev):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(8)
+    sc = Scenario(h3c, torch, dev, 2, 8192, rng, init="crc")
+    sc.add(orc.UPD_WRITE, 0, 10, 10)
+    sc.add(orc.UPD_WRITE, 5, 0, 10)  # chunk index out of the table
+    sc.add(orc.UPD_WRITE, 1, 10, 10)
+    sc.check(*sc.run())
+
+
+def test_updio_std_domain_rust_engine(h3c, torch_dev):
+    """H3C_UPD_STD_DOMAIN: Rust chunk engine (chunk.rs:89-281, engine.rs:297-312) -- values
+    are std crc32c and every applied op leaves crc32c(content) (no NONE/empty zero case)."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(9)
+    cs = 128 << 10
+    n = 4
+    host = np.zeros((n, cs), dtype=np.uint8)
+    sizes = [0, 5000, cs, 77]
+    for c, s in enumerate(sizes):
+        host[c, :s] = rng.integers(0, 256, s, dtype=np.uint8)
+    slab = torch.from_numpy(host.copy()).to(dev)
+    chunks = np.zeros(n, dtype=h3c.CHUNK_STATE_DTYPE)
+    for c, s in enumerate(sizes):
+        std = (~orc.crc32c(host[c, :s])) & MASK
+        chunks[c] = (slab.data_ptr() + c * cs, cs, s, std, 1, 0)
+    ops, pays, want = [], [], []
+    size = list(sizes)
+    for k in range(200):
+        c = int(rng.integers(0, n))
+        if rng.random() < 0.8:
+            off = int(rng.integers(0, cs))
+            ln = int(rng.integers(0, min(cs - off, 9000) + 1))
+            p = rng.integers(0, 256, ln, dtype=np.uint8)
+            std = (~orc.crc32c(p)) & MASK
+            ok = rng.random() > 0.1
+            ops.append((c, 1, off, ln, std if ok else std ^ 1, 1))
+            pays.append(p)
+            if ok or ln == 0:
+                if off > size[c]:
+                    host[c, size[c]:off] = 0
+                host[c, off:off + ln] = p
+                size[c] = max(size[c], off + ln)
+                want.append((0, size[c], (~orc.crc32c(host[c, :size[c]])) & MASK))
+            else:
+                want.append((4080, size[c], None))
+        else:
+            t = int(rng.integers(0, cs + 1))
+            ops.append((c, 4, 0, t, 0, 0))
+            pays.append(None)
+            if t > size[c]:
+                host[c, size[c]:t] = 0
+            size[c] = t
+            want.append((0, size[c], (~orc.crc32c(host[c, :size[c]])) & MASK))
+    tot = sum(len(p) for p in pays if p is not None)
+    pay = np.zeros(max(tot, 1), dtype=np.uint8)
+    offs, o = [], 0
+    for p in pays:
+        offs.append(o)
+        if p is not None:
+            pay[o:o + len(p)] = p
+            o += len(p)
+    dpay = torch.from_numpy(pay).to(dev)
+    ios = np.zeros(len(ops), dtype=h3c.UPDATE_IO_DTYPE)
+    for i, ((c, kind, off, ln, val, ty), po, p) in enumerate(zip(ops, offs, pays)):
+        ios[i] = (dpay.data_ptr() + po if p is not None else 0, c, off, ln, val, ty, kind, 0)
+    res = h3c.update_ios(chunks, ios, std_domain=True)
+    for i, (r, (st, sz, v)) in enumerate(zip(res, want)):
+        assert int(r["status"]) == st and int(r["size"]) == sz, (i, r, st, sz)
+        if v is not None:
+            assert int(r["value"]) == v and int(r["type"]) == 1, i
+    got = slab.cpu().numpy()
+    for c in range(n):
+        assert int(chunks[c]["size"]) == size[c]
+        assert int(chunks[c]["value"]) == (~orc.crc32c(host[c, :size[c]])) & MASK
+        assert np.array_equal(got[c, :size[c]], host[c, :size[c]])

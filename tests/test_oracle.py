@@ -149,3 +149,61 @@ def test_std_domain_combine():
         b = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8)
         std = lambda x: (~orc.crc32c(x)) & MASK
         assert orc.lib().orc_crc32c_combine(std(a), std(b), b.size) == std(np.concatenate([a, b]))
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_replica_update_restatement_relational_pin(seed):
+    """The reference pins chunk checksums only relationally: after every write the stored
+    checksum equals crc32c of the whole chunk (TestStorageClientInterface.cc:431-459).
+    Replay random WRITE / TRUNCATE / EXTEND sequences through the ChunkReplica::update
+    restatement and check that relation, the zero of updateChecksum case (i), the
+    kInvalidArg range check and the client-checksum verify."""
+    rng = np.random.default_rng(seed)
+    cs = 20000
+    chunk = np.zeros(cs, dtype=np.uint8)
+    model = np.zeros(0, dtype=np.uint8)
+    meta = {"size": 0, "type": orc.NONE, "value": 0}
+    for _ in range(300):
+        u = rng.random()
+        if u < 0.6:
+            off = int(rng.integers(0, cs))
+            ln = int(rng.integers(0, min(cs - off, 3000) + 1))
+            p = rng.integers(0, 256, ln, dtype=np.uint8)
+            ty = orc.CRC32C if rng.random() > 0.15 else orc.NONE
+            val = orc.create(ty, p, ln)[1] if ty else 0
+            good = rng.random() > 0.1 or ty == orc.NONE or ln == 0
+            io = {"kind": orc.UPD_WRITE, "offset": off, "length": ln, "type": ty, "value": val if good else val ^ 4}
+            res, meta2 = orc.replica_update(meta, chunk, cs, io, p)
+            if not good:
+                assert res["status"] == 4080 and meta2 == meta
+                continue
+            assert res["status"] == 0
+            if off > model.size:
+                model = np.concatenate([model, np.zeros(off - model.size, dtype=np.uint8)])
+            if off + ln > model.size:
+                model = np.concatenate([model, np.zeros(off + ln - model.size, dtype=np.uint8)])
+            model[off:off + ln] = p
+        elif u < 0.8:
+            kind = orc.UPD_TRUNCATE if rng.random() < 0.5 else orc.UPD_EXTEND
+            t = int(rng.integers(0, cs + 1))
+            res, meta2 = orc.replica_update(meta, chunk, cs, {"kind": kind, "offset": 0, "length": t, "type": 0,
+                                                              "value": 0})
+            assert res["status"] == 0
+            if t > model.size:
+                model = np.concatenate([model, np.zeros(t - model.size, dtype=np.uint8)])
+            elif kind == orc.UPD_TRUNCATE:
+                model = model[:t].copy()
+        else:
+            res, meta2 = orc.replica_update(meta, chunk, cs, {"kind": orc.UPD_WRITE, "offset": cs - 5, "length": 9,
+                                                              "type": 1, "value": 0},
+                                            np.zeros(9, dtype=np.uint8))
+            assert res["status"] == 3 and meta2 == meta
+            continue
+        meta = meta2
+        assert meta["size"] == model.size == res["size"]
+        assert np.array_equal(chunk[:model.size], model)
+        if meta["type"] == orc.NONE or model.size == 0:
+            assert meta["value"] == 0
+        else:
+            assert meta["value"] == orc.crc32c(model)
+        assert (res["type"], res["value"]) == (meta["type"], meta["value"])
