@@ -83,6 +83,13 @@ _proto("h3c_fill_splitmix", _int, _vp, _u64, _u64, _u64, _u64, _u64, _vp)
 _proto("h3c_update_workspace_bytes", _sz, _u32, _u32, _u64, _u32)
 _proto("h3c_update_blocks", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp)
 _proto("h3c_update_ios", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp)
+_proto("h3c_serde_checksum_mark", _u32, _u32, _int)
+_proto("h3c_batch_serde_checksum", _int, _vp, _sz, _vp, _vp, _vp)
+_proto("h3c_batch_serde_verify", _int, _vp, _sz, _vp, _vp, _vp, _vp)
+_proto("h3c_std_crc32c_combine", _u32, _u32, _u32, _u64)
+_proto("h3c_batch_std_crc32c", _int, _vp, _sz, _vp, _vp, _vp)
+_proto("h3c_checksum_combine", _int, ctypes.POINTER(_u8), ctypes.POINTER(_u32), _u8, _u32, _u64)
+_proto("h3c_combine_fold", _int, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp)
 _proto("h3c_hostfed_create", _int, _int, _u64, ctypes.POINTER(_vp))
 _proto("h3c_hostfed_run", _int, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp)
 _proto("h3c_hostfed_destroy", None, _vp)
@@ -435,17 +442,13 @@ class ChecksumInfo:
         return ChecksumInfo(ChecksumType(int(t[0])), int(v[0]))
 
     def combine(self, o: "ChecksumInfo", length: int) -> None:
-        """Common.h:179-198.  Raises EngineError(kChecksumMismatch) on a type mismatch."""
-        if self.type != ChecksumType.NONE and self.type != o.type:
-            raise EngineError(StatusCode.kChecksumMismatch, f"different type {self} != {o}")
-        if length == 0:
-            return
-        if self.type == ChecksumType.NONE:
-            self.type, self.value = ChecksumType(o.type), o.value
-        elif self.type == ChecksumType.CRC32C:
-            self.value = crc32c_combine(~self.value & 0xFFFFFFFF, o.value, length)
-        elif self.type == ChecksumType.CRC32:
-            self.value = crc32_combine(~self.value & 0xFFFFFFFF, o.value, length)
+        """Common.h:179-198 (h3c_checksum_combine).  Raises EngineError(kChecksumMismatch)
+        on a type mismatch; length 0 is a no-op; a NONE receiver copies `o`."""
+        t, v = _u8(int(self.type)), _u32(self.value & 0xFFFFFFFF)
+        rc = lib.h3c_checksum_combine(ctypes.byref(t), ctypes.byref(v), int(o.type), o.value & 0xFFFFFFFF, length)
+        if rc:
+            raise EngineError(rc, f"different type {self} != {o}")
+        self.type, self.value = ChecksumType(t.value), int(v.value)
 
     def __str__(self) -> str:  # Common.h:768-773
         return f"{ChecksumType(self.type).name}#{(~self.value) & 0xFFFFFFFF:08X}"

@@ -192,6 +192,35 @@ typedef struct h3c_update_result {
 int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios, uint32_t n,
                    h3c_update_result *results, uint32_t flags, void *stream);
 
+/* ---- adjacent formats on the same kernels ---- */
+
+/* RPC message checksum, Checksum::calcSerde (src/common/net/MessageHeader.h:32-37):
+ * folly::crc32c(data, size, 0) with its low 8 bits replaced by 0x86 | compressed. */
+uint32_t h3c_serde_checksum_mark(uint32_t crc0, int compressed);
+int h3c_batch_serde_checksum(const h3c_desc *d, size_t n, const uint8_t *compressed /* NULL = none */,
+                             uint32_t *out, void *stream);
+/* Processor::unpackSerdeMsg's check (src/common/net/Processor.h:113-117): ok[i] = the
+ * recomputed calcSerde (compressed flag = bit 0 of received[i]) equals received[i]. */
+int h3c_batch_serde_verify(const h3c_desc *d, size_t n, const uint32_t *received, uint8_t *ok, uint64_t *n_bad,
+                           void *stream);
+
+/* Rust crc32c crate 0.6.8 as the chunk engine uses it (std domain, std = ~raw;
+ * chunk_engine/src/alloc/chunk.rs:152-269, core/engine.rs:297-312):
+ * crc32c::crc32c_combine, and crc32c::crc32c (append_to == NULL) /
+ * crc32c::crc32c_append(append_to[i], data) per descriptor (type is ignored). */
+uint32_t h3c_std_crc32c_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+int h3c_batch_std_crc32c(const h3c_desc *d, size_t n, const uint32_t *append_to, uint32_t *out_std, void *stream);
+
+/* ChecksumInfo::combine (src/fbs/storage/Common.h:179-198) on a {type, value} pair:
+ * H3C_ERR_CHECKSUM_MISMATCH (4080) on a type mismatch, no-op for length 0, a NONE
+ * receiver copies o. */
+int h3c_checksum_combine(uint8_t *type, uint32_t *value, uint8_t o_type, uint32_t o_value, uint64_t length);
+/* The client's fold of split-read results (src/client/storage/StorageClientImpl.cc:1607-1633):
+ * group g = pieces [group_begin[g], group_begin[g+1]); the first piece's checksum,
+ * then combine(piece_k, lens[k]) for the rest.  status[g] = 0 or the combine error. */
+int h3c_combine_fold(const uint8_t *types, const uint32_t *values, const uint64_t *lens, const uint64_t *group_begin,
+                     size_t ngroups, uint8_t *out_type, uint32_t *out_value, uint32_t *status);
+
 /* ---- host-fed pipeline (payloads in host memory, BASELINE config 5) ---- */
 
 /* A reusable pipeline: two HBM staging windows of `window_bytes` and a copy stream.

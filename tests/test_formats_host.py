@@ -1,0 +1,75 @@
+"""Host-side pieces of the adjacent formats (no GPU): ChecksumInfo::combine as a C function,
+the client's split-read fold, the Rust-crate std combine and the calcSerde low-byte mark,
+each against the oracle restatement."""
+import importlib
+
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+
+MASK = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def client(h3c):
+    return importlib.import_module("3fs_amd.client")
+
+
+def test_checksum_combine_c_matches_oracle(h3c):
+    rng = np.random.default_rng(3)
+    for _ in range(400):
+        t, ot = int(rng.integers(0, 3)), int(rng.integers(0, 3))
+        v, ov = int(rng.integers(0, 1 << 32)), int(rng.integers(0, 1 << 32))
+        ln = int(rng.choice([0, 1, 7, 4096, 1 << 20, int(rng.integers(0, 1 << 26))]))
+        want = orc.combine(t, v, ot, ov, ln)
+        info = h3c.ChecksumInfo(h3c.ChecksumType(t), v)
+        try:
+            info.combine(h3c.ChecksumInfo(h3c.ChecksumType(ot), ov), ln)
+            rc = 0
+        except h3c.EngineError as e:
+            rc = e.code
+        assert rc == want[0]
+        if rc == 0:
+            assert (int(info.type), info.value) == (want[1], want[2])
+
+
+def test_split_read_fold_matches_whole_buffer(h3c, client):
+    """StorageClientImpl.cc:1607-1633: folding the pieces' checksums gives the whole read's."""
+    rng = np.random.default_rng(4)
+    groups, wants = [], []
+    for _ in range(20):
+        data = rng.integers(0, 256, int(rng.integers(1, 50000)), dtype=np.uint8)
+        cuts = sorted(set(int(x) for x in rng.integers(1, data.size, int(rng.integers(0, 6))))) if data.size > 1 else []
+        bounds = [0] + cuts + [data.size]
+        pieces = []
+        for a, b in zip(bounds, bounds[1:]):
+            pieces.append((h3c.ChecksumInfo(h3c.ChecksumType.CRC32C, orc.crc32c(data[a:b])), b - a))
+        groups.append(pieces)
+        wants.append(orc.crc32c(data))
+    # a group with a type mismatch fails with kChecksumMismatch
+    groups.append([(h3c.ChecksumInfo(h3c.ChecksumType.CRC32C, 1), 10), (h3c.ChecksumInfo(h3c.ChecksumType.CRC32, 2), 5)])
+    infos, status = client.fold_split_reads(groups)
+    for k, w in enumerate(wants):
+        assert status[k] == 0 and infos[k].type == h3c.ChecksumType.CRC32C and infos[k].value == w
+    assert status[-1] == 4080
+
+
+def test_std_combine_matches_oracle(h3c):
+    fm = importlib.import_module("3fs_amd.formats")
+    rng = np.random.default_rng(5)
+    for _ in range(50):
+        a = rng.integers(0, 256, int(rng.integers(0, 5000)), dtype=np.uint8)
+        b = rng.integers(0, 256, int(rng.integers(0, 5000)), dtype=np.uint8)
+        std = lambda x: (~orc.crc32c(x)) & MASK  # noqa: E731
+        assert fm.rust_crc32c.crc32c_combine(std(a), std(b), b.size) == std(np.concatenate([a, b]))
+
+
+def test_serde_mark():
+    h3c = importlib.import_module("3fs_amd")
+    for crc0 in (0, 0xFFFFFFFF, 0x12345678, 0xDEADBE01):
+        for comp in (0, 1):
+            m = h3c.lib.h3c_serde_checksum_mark(crc0, comp)
+            assert m == (crc0 & ~0xFF) | 0x86 | comp
+            fm = importlib.import_module("3fs_amd.formats")
+            assert fm.is_serde_message(m) and fm.is_compressed(m) == bool(comp)
