@@ -30,6 +30,7 @@ from .engine import (  # noqa: F401
     lib_path,
     profile_enable,
     profile_read,
+    read_results,
     update_blocks,
     update_ios,
     update_workspace_bytes,
@@ -60,6 +61,7 @@ __all__ = [
     "lib_path",
     "profile_enable",
     "profile_read",
+    "read_results",
     "update_blocks",
     "update_ios",
     "update_workspace_bytes",

@@ -7,6 +7,8 @@
 //     crc32c / crc32c_append / crc32c_combine (chunk_engine/src/alloc/chunk.rs:152-269).
 //   * ChecksumInfo::combine as a C function (src/fbs/storage/Common.h:179-198) and the
 //     client's fold of split-read checksums (src/client/storage/StorageClientImpl.cc:1607-1633).
+//   * the read path's checksum selection + recalculate verify, AioReadJob::setResult
+//     (src/storage/aio/BatchReadJob.cc:24-55), for a batch of completed read jobs.
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -119,6 +121,52 @@ int h3c_combine_fold(const uint8_t *types, const uint32_t *values, const uint64_
     out_type[g] = t;
     out_value[g] = v;
     status[g] = s;
+  }
+  return H3C_OK;
+}
+
+int h3c_batch_read_result(uint8_t batch_type, const h3c_read_job *jobs, size_t n, uint8_t *out_type,
+                          uint32_t *out_value, uint32_t *status, void *stream) {
+  if (n == 0) return H3C_OK;
+  if (!jobs || !out_type || !out_value || !status) return H3C_ERR_INVALID_ARG;
+  if (batch_type > H3C_TYPE_CRC32) return H3C_ERR_INVALID_ARG;
+  // one batch of payload CRCs: the read-data checksums (:33-34) and the full-chunk
+  // recalculations (:43-44)
+  std::vector<h3c_desc> dd;
+  std::vector<int64_t> compute_at(n, -1), recalc_at(n, -1);
+  for (size_t i = 0; i < n; ++i) {
+    const h3c_read_job &j = jobs[i];
+    const bool full = j.offset == 0 && j.length == j.chunk_len;
+    if (batch_type != H3C_TYPE_NONE && !(batch_type == j.chunk_type && full)) {
+      compute_at[i] = (int64_t)dd.size();
+      dd.push_back(h3c_desc{j.data, j.length, 0xFFFFFFFFu, batch_type, j.mem, 0});
+    }
+    if (j.recalculate && full) {
+      recalc_at[i] = (int64_t)dd.size();
+      dd.push_back(h3c_desc{j.data, j.length, 0xFFFFFFFFu, j.chunk_type, j.mem, 0});
+    }
+  }
+  std::vector<uint8_t> t(dd.size());
+  std::vector<uint32_t> v(dd.size());
+  if (!dd.empty()) {
+    const int rc = h3c_batch_create(dd.data(), dd.size(), t.data(), v.data(), stream);
+    if (rc) return rc;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const h3c_read_job &j = jobs[i];
+    status[i] = H3C_OK;
+    if (batch_type == H3C_TYPE_NONE) {  // :28-29
+      out_type[i] = H3C_TYPE_NONE;
+      out_value[i] = 0;
+    } else if (compute_at[i] < 0) {  // :30-31 full chunk of the same type: the stored checksum
+      out_type[i] = j.chunk_type;
+      out_value[i] = j.chunk_value;
+    } else {  // :33-34
+      out_type[i] = t[compute_at[i]];
+      out_value[i] = v[compute_at[i]];
+    }
+    if (recalc_at[i] >= 0 && (t[recalc_at[i]] != j.chunk_type || v[recalc_at[i]] != j.chunk_value))
+      status[i] = H3C_ERR_CHECKSUM_MISMATCH;  // :45-53
   }
   return H3C_OK;
 }

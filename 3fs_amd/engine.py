@@ -90,6 +90,7 @@ _proto("h3c_std_crc32c_combine", _u32, _u32, _u32, _u64)
 _proto("h3c_batch_std_crc32c", _int, _vp, _sz, _vp, _vp, _vp)
 _proto("h3c_checksum_combine", _int, ctypes.POINTER(_u8), ctypes.POINTER(_u32), _u8, _u32, _u64)
 _proto("h3c_combine_fold", _int, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp)
+_proto("h3c_batch_read_result", _int, _u8, _vp, _sz, _vp, _vp, _vp, _vp)
 _proto("h3c_hostfed_create", _int, _int, _u64, ctypes.POINTER(_vp))
 _proto("h3c_hostfed_run", _int, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp)
 _proto("h3c_hostfed_destroy", None, _vp)
@@ -324,6 +325,35 @@ def update_ios(chunks: np.ndarray, ios: np.ndarray, type_: int = ChecksumType.CR
     _check(lib.h3c_update_ios(int(type_), chunks.ctypes.data, len(chunks), ios.ctypes.data, len(ios),
                               res.ctypes.data, UPD_STD_DOMAIN if std_domain else 0, _stream_handle(stream)))
     return res
+
+
+READ_JOB_DTYPE = np.dtype([("data", "<u8"), ("length", "<u8"), ("chunk_len", "<u8"), ("offset", "<u4"),
+                           ("chunk_value", "<u4"), ("chunk_type", "u1"), ("mem", "u1"), ("recalculate", "u1"),
+                           ("reserved", "u1", 5)])
+assert READ_JOB_DTYPE.itemsize == 40
+
+
+def read_results(batch_type: int, jobs: Sequence, stream=None):
+    """AioReadJob::setResult (BatchReadJob.cc:24-55) for a batch of completed reads.
+
+    jobs[i] = (data, length, chunk_len, offset, stored ChecksumInfo, recalculate).  Returns
+    (list of result ChecksumInfo, status uint32[n]: 0 or 4080 from the recalculate check)."""
+    arr = np.zeros(len(jobs), dtype=READ_JOB_DTYPE)
+    keep = []
+    for i, (data, length, chunk_len, offset, ck, recalc) in enumerate(jobs):
+        ptr, nbytes, mem, ka = _payload(data, length)
+        if data is not None and length > nbytes:
+            raise ValueError("length exceeds the read buffer")
+        keep.append(ka)
+        arr[i] = (ptr, length, chunk_len, offset, ck.value & 0xFFFFFFFF, int(ck.type), int(mem), int(bool(recalc)), 0)
+    n = len(arr)
+    ot = np.zeros(n, dtype=np.uint8)
+    ov = np.zeros(n, dtype=np.uint32)
+    st = np.zeros(n, dtype=np.uint32)
+    _check(lib.h3c_batch_read_result(int(batch_type), arr.ctypes.data, n, ot.ctypes.data, ov.ctypes.data,
+                                     st.ctypes.data, _stream_handle(stream)))
+    del keep
+    return [ChecksumInfo(ChecksumType(int(a)), int(b)) for a, b in zip(ot, ov)], st
 
 
 def profile_enable(on: bool = True) -> None:

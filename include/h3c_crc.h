@@ -221,6 +221,28 @@ int h3c_checksum_combine(uint8_t *type, uint32_t *value, uint8_t o_type, uint32_
 int h3c_combine_fold(const uint8_t *types, const uint32_t *values, const uint64_t *lens, const uint64_t *group_begin,
                      size_t ngroups, uint8_t *out_type, uint32_t *out_value, uint32_t *status);
 
+/* ---- read path: AioReadJob::setResult (src/storage/aio/BatchReadJob.cc:24-55) ---- */
+
+/* One completed read job. */
+typedef struct h3c_read_job {
+  const void *data;     /* the bytes read (localbuf + headLength) */
+  uint64_t length;      /* *lengthInfo */
+  uint64_t chunk_len;   /* state.chunkLen */
+  uint32_t offset;      /* readIO.offset */
+  uint32_t chunk_value; /* state.chunkChecksum.value */
+  uint8_t chunk_type;   /* state.chunkChecksum.type */
+  uint8_t mem;          /* h3c_mem of data */
+  uint8_t recalculate;  /* batch.recalculateChecksum() (resync reads, ReliableForwarding.cc:179-180) */
+  uint8_t reserved[5];
+} h3c_read_job;
+
+/* result.checksum per job: {NONE,0} for a NONE batch; the stored chunk checksum when the
+ * whole chunk is read with its own type; else create(batch_type, data, length).  With
+ * `recalculate`, a whole-chunk read is re-checksummed with the stored type and a
+ * difference sets status[i] = H3C_ERR_CHECKSUM_MISMATCH (4080). */
+int h3c_batch_read_result(uint8_t batch_type, const h3c_read_job *jobs, size_t n, uint8_t *out_type,
+                          uint32_t *out_value, uint32_t *status, void *stream);
+
 /* ---- host-fed pipeline (payloads in host memory, BASELINE config 5) ---- */
 
 /* A reusable pipeline: two HBM staging windows of `window_bytes` and a copy stream.

@@ -153,3 +153,20 @@ def replica_update(meta: dict, chunk: np.ndarray, chunk_size: int, io: dict, pay
                                pay.ctypes.data if pay is not None else None, ctypes.byref(r))
     return ({"status": r.status, "size": r.size, "type": r.type, "value": r.value},
             {"size": m.size, "type": m.checksum_type, "value": m.checksum_value})
+
+
+def read_result_checksum(batch_type, chunk_type, chunk_value, chunk_len, offset, length, data, recalculate, full):
+    """AioReadJob::setResult restatement -> (status, type, value)."""
+    L = lib()
+    if not hasattr(L, "_read_result_bound"):
+        u8, u32 = ctypes.c_uint8, ctypes.c_uint32
+        L.orc_read_result_checksum.restype = ctypes.c_int
+        L.orc_read_result_checksum.argtypes = [u8, u8, u32, u32, u32, u32, ctypes.c_void_p, ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.POINTER(u8), ctypes.POINTER(u32)]
+        L._read_result_bound = True
+    t, v = ctypes.c_uint8(0), ctypes.c_uint32(0)
+    d = np.ascontiguousarray(data, dtype=np.uint8)
+    f = np.ascontiguousarray(full, dtype=np.uint8)
+    rc = L.orc_read_result_checksum(batch_type, chunk_type, chunk_value & 0xFFFFFFFF, chunk_len, offset, length,
+                                    _ptr(d), int(recalculate), _ptr(f), ctypes.byref(t), ctypes.byref(v))
+    return rc, t.value, v.value

@@ -112,3 +112,33 @@ def test_scrub_finds_corrupted_chunks(h3c, torch_dev):
     differ, only_l, only_r = scrub.diff_checksums({1: stored[1], 2: stored[2], 5: stored[5]},
                                                   {1: stored[1], 2: stored[3], 6: stored[6]})
     assert differ == [2] and only_l == [5] and only_r == [6]
+
+
+def test_read_results_match_setresult_oracle(h3c, torch_dev):
+    """AioReadJob::setResult (BatchReadJob.cc:24-55): NONE batch, whole-chunk reuse, partial
+    read checksum, recalculate verify (stored value corrupt -> 4080)."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(6)
+    jobs, want = [], []
+    for k in range(60):
+        cl = int(rng.integers(1, 300000))
+        chunk = rng.integers(0, 256, cl, dtype=np.uint8)
+        ctype = [orc.CRC32C, orc.CRC32, orc.NONE][k % 3]
+        stored = orc.create(ctype, chunk)[1] if ctype else 0
+        if k % 7 == 3:
+            stored ^= 0x8  # corrupt stored checksum
+        full_read = k % 2 == 0
+        off = 0 if full_read else int(rng.integers(0, cl))
+        ln = cl if full_read else int(rng.integers(0, cl - off + 1))
+        data = chunk[off:off + ln]
+        bt = [orc.CRC32C, orc.CRC32C, orc.CRC32, orc.NONE][k % 4]
+        recalc = k % 5 != 1
+        want.append(orc.read_result_checksum(bt, ctype, stored, cl, off, ln, data, recalc, chunk))
+        dd = torch.from_numpy(np.ascontiguousarray(data)).to(dev) if k % 3 else np.ascontiguousarray(data)
+        jobs.append((bt, (dd, ln, cl, off, h3c.ChecksumInfo(h3c.ChecksumType(ctype), stored), recalc)))
+    for bt in (orc.NONE, orc.CRC32C, orc.CRC32):
+        idx = [i for i, (b, _) in enumerate(jobs) if b == bt]
+        infos, st = h3c.read_results(bt, [jobs[i][1] for i in idx])
+        for k, i in enumerate(idx):
+            rc, t, v = want[i]
+            assert (int(st[k]), int(infos[k].type), infos[k].value) == (rc, t, v), i
