@@ -34,9 +34,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
-#include <unordered_map>
 #include <vector>
 
 #include <rocprim/device/device_scan_by_key.hpp>
@@ -180,6 +182,62 @@ void add_job(CrcBatch &b, uint64_t ptr, uint64_t len, uint32_t start, uint32_t o
   b.chunks.push_back(c);
 }
 
+// Open-addressing map (chunk, 4 KiB block) -> last epoch + 1 that touched it.
+class BlockEpochs {
+ public:
+  explicit BlockEpochs(size_t expect) { reset(expect); }
+  uint32_t get(uint64_t k) const {
+    for (uint64_t h = slot(k);; h = (h + 1) & mask_) {
+      if (keys_[h] == k) return vals_[h];
+      if (keys_[h] == kEmpty) return 0;
+    }
+  }
+  void put(uint64_t k, uint32_t v) {
+    if (2 * (used_ + 1) > keys_.size()) grow();
+    for (uint64_t h = slot(k);; h = (h + 1) & mask_) {
+      if (keys_[h] == k) {
+        vals_[h] = v;
+        return;
+      }
+      if (keys_[h] == kEmpty) {
+        keys_[h] = k;
+        vals_[h] = v;
+        ++used_;
+        return;
+      }
+    }
+  }
+
+ private:
+  static constexpr uint64_t kEmpty = ~0ull;
+  uint64_t slot(uint64_t k) const { return ((k * 0x9E3779B97F4A7C15ull) >> shift_) & mask_; }
+  void reset(size_t expect) {
+    size_t cap = 1024;
+    int bits = 10;
+    while (cap < 2 * expect) {
+      cap <<= 1;
+      ++bits;
+    }
+    keys_.assign(cap, kEmpty);
+    vals_.assign(cap, 0);
+    mask_ = cap - 1;
+    shift_ = 64 - bits;
+    used_ = 0;
+  }
+  void grow() {
+    std::vector<uint64_t> k = std::move(keys_);
+    std::vector<uint32_t> v = std::move(vals_);
+    reset(k.size());
+    for (size_t i = 0; i < k.size(); ++i)
+      if (k[i] != kEmpty) put(k[i], v[i]);
+  }
+  std::vector<uint64_t> keys_;
+  std::vector<uint32_t> vals_;
+  uint64_t mask_ = 0;
+  int shift_ = 0;
+  size_t used_ = 0;
+};
+
 enum class Src : uint8_t { kInitial, kZero, kTrue };
 
 struct Track {
@@ -188,6 +246,18 @@ struct Track {
   Src src = Src::kInitial;
   uint32_t true_pos = 0;   // scan position whose CRC is the stored value (Src::kTrue)
   bool started = false;    // has a scan segment
+};
+
+// H3C_UPDIO_TIMING=1: per-phase wall times on stderr (tuning aid).
+struct PhaseClock {
+  bool on = std::getenv("H3C_UPDIO_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(const char *what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[updio] %-10s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
 };
 
 struct OpOut {
@@ -211,6 +281,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   const PolyConsts *pc = static_cast<const PolyConsts *>(h3c_rt::device_consts(dev, poly_type));
   const uint32_t poly = poly_type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
 
+  PhaseClock clk;
   // ---- per-op validation (range :140-145, kind, client checksum type) ----
   std::vector<uint32_t> status(n, H3C_OK);
   for (uint32_t i = 0; i < n; ++i) {
@@ -262,6 +333,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     if (err) return err;
   }
 
+  clk.mark("A payload");
   // ---- B. host pass: verify, sizes, cases, epochs, byte jobs, affine elements ----
   std::vector<Track> tr(nchunks);
   for (uint32_t c = 0; c < nchunks; ++c) {
@@ -269,14 +341,15 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     tr[c].type = chunks[c].type;
   }
   // chunk-major scan layout: positions are assigned after the pass
-  std::vector<std::vector<uint32_t>> chunk_elems(nchunks);  // element ids per chunk, in sequence order
   std::vector<AffIn> elems;
   std::vector<uint32_t> elem_chunk;
   std::vector<OpOut> outs(n);
   std::vector<uint32_t> raw0(nchunks, 0);
   std::vector<CrcBatch> ep_crc;
   std::vector<std::vector<CopyPiece>> ep_copy;
-  std::unordered_map<uint64_t, uint32_t> last_touch;  // (chunk, block) -> epoch + 1
+  BlockEpochs last_touch(n + 1024);
+  elems.reserve(n + 64);
+  elem_chunk.reserve(n + 64);
   uint32_t njobs = 0;
   uint64_t job_bytes_total = 0;
   for (uint32_t i = 0; i < n; ++i)
@@ -288,10 +361,9 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     uint32_t e = 0;
     const uint64_t b0 = a / kConflictBlock, b1 = (b - 1) / kConflictBlock;
     for (uint64_t k = b0; k <= b1; ++k) {
-      auto it = last_touch.find(((uint64_t)c << 32) | k);
-      if (it != last_touch.end()) e = std::max(e, it->second);
+      e = std::max(e, last_touch.get(((uint64_t)c << 32) | k));
     }
-    for (uint64_t k = b0; k <= b1; ++k) last_touch[((uint64_t)c << 32) | k] = e + 1;
+    for (uint64_t k = b0; k <= b1; ++k) last_touch.put(((uint64_t)c << 32) | k, e + 1);
     if (ep_crc.size() <= e) {
       ep_crc.resize(e + 1);
       ep_copy.resize(e + 1);
@@ -306,7 +378,6 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     const uint32_t id = (uint32_t)elems.size();
     elems.push_back(a);
     elem_chunk.push_back(c);
-    chunk_elems[c].push_back(id);
     return id;
   };
 
@@ -395,19 +466,21 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     outs[i] = OpOut{t.src, t.true_pos, c};
   }
 
+  clk.mark("B host");
   // ---- C-D. device: epochs, affine scan ----
   const uint32_t npos = (uint32_t)elems.size();
   std::vector<uint32_t> pos_of(npos), keys(npos);
   std::vector<AffIn> lay(npos);
-  {
-    uint32_t p = 0;
-    for (uint32_t c = 0; c < nchunks; ++c)
-      for (uint32_t id : chunk_elems[c]) {
-        pos_of[id] = p;
-        keys[p] = c;
-        lay[p] = elems[id];
-        ++p;
-      }
+  {  // stable counting sort of the elements by chunk: (chunk, sequence) order
+    std::vector<uint32_t> start(nchunks + 1, 0);
+    for (uint32_t id = 0; id < npos; ++id) ++start[elem_chunk[id] + 1];
+    for (uint32_t c = 0; c < nchunks; ++c) start[c + 1] += start[c];
+    for (uint32_t id = 0; id < npos; ++id) {
+      const uint32_t c = elem_chunk[id], p = start[c]++;
+      pos_of[id] = p;
+      keys[p] = c;
+      lay[p] = elems[id];
+    }
   }
   std::vector<uint32_t> truev(npos, 0);
   if (npos) {
@@ -495,6 +568,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     }
   }
 
+  clk.mark("C-D device");
   // ---- E. results and final chunk states ----
   std::vector<uint32_t> init_value(nchunks);
   std::vector<uint8_t> init_type(nchunks);
@@ -544,5 +618,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     chunks[c].type = std_domain ? poly_type : tr[c].type;
     chunks[c].value = value_of(tr[c].src, tr[c].true_pos, c);
   }
+  clk.mark("E results");
+  if (clk.on) std::fprintf(stderr, "[updio] epochs %zu, crc jobs %u, elements %u\n", ep_crc.size(), njobs, npos);
   return H3C_OK;
 }
