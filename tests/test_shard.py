@@ -79,3 +79,72 @@ def test_gloo_world2_sharded_verify():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(r[1] and r[2] for r in res), res
+
+
+def test_partition_updates_keeps_chunks_on_one_rank():
+    rng = np.random.default_rng(1)
+    nchunks = 37
+    cb = rng.integers(1 << 20, 64 << 20, nchunks).tolist()
+    ops = rng.integers(-1, nchunks + 2, 5000).tolist()
+    for world in (1, 2, 3, 8):
+        parts = shard.partition_updates(ops, cb, world)
+        seen = np.concatenate(parts)
+        assert sorted(seen.tolist()) == list(range(len(ops)))
+        owner = {}
+        for r, idx in enumerate(parts):
+            assert np.all(np.diff(idx) > 0)  # sequence order kept
+            for i in idx:
+                c = ops[i]
+                if 0 <= c < nchunks:
+                    assert owner.setdefault(c, r) == r
+
+
+def _upd_worker(rank, world, port, q):
+    """Each rank replays its chunks' ops through the ChunkReplica::update restatement; the
+    gathered per-op results must equal a single-rank replay of the whole sequence."""
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(9)
+        nchunks, cs = 6, 16384
+        ops = []
+        for _ in range(400):
+            c = int(rng.integers(0, nchunks))
+            off = int(rng.integers(0, cs))
+            ln = int(rng.integers(0, min(cs - off, 3000) + 1))
+            p = rng.integers(0, 256, ln, dtype=np.uint8)
+            ops.append((c, {"kind": orc.UPD_WRITE, "offset": off, "length": ln, "type": orc.CRC32C,
+                            "value": orc.create(orc.CRC32C, p, ln)[1]}, p))
+
+        def replay(idx):
+            chunks = np.zeros((nchunks, cs), dtype=np.uint8)
+            meta = [{"size": 0, "type": orc.NONE, "value": 0} for _ in range(nchunks)]
+            out = np.zeros(len(idx), dtype=np.int64)
+            for k, i in enumerate(idx):
+                c, io, p = ops[i]
+                res, meta[c] = orc.replica_update(meta[c], chunks[c], cs, io, p)
+                out[k] = (res["status"] << 40) | (res["size"] << 32) | res["value"]
+            return out
+
+        got = shard.run_sharded_updates([o[0] for o in ops], [cs] * nchunks, replay, rank, world)
+        want = replay(list(range(len(ops))))
+        q.put((rank, bool(np.array_equal(got, want))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_updates():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_upd_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] for r in res), res
