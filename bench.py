@@ -383,7 +383,10 @@ def run_updio(args, cx: Ctx) -> dict:
     last = {}
 
     def step():
+        t = time.perf_counter()
         last["res"] = h3c.update_ios(state, ios, stream=cx.stream)
+        if os.environ.get("H3C_UPDIO_TIMING"):
+            print(f"[bench] update_ios {1e3 * (time.perf_counter() - t):.3f} ms", file=sys.stderr, flush=True)
 
     elapsed, _ = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDATE)
     fresh = torch.zeros(nchunks, dtype=torch.int32, device=cx.dev)
