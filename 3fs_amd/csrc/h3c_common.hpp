@@ -28,6 +28,46 @@ struct ProfToken {
 hipError_t prof_begin(hipStream_t st, ProfToken &t);
 hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes);
 
+// Pinned host staging for the synchronous entry points.  Every host<->device transfer
+// of host-side metadata or pageable payloads goes through one of these: a pageable
+// hipMemcpyAsync into stream-ordered (hipMallocAsync) memory was measured to deliver
+// stale bytes to the next kernel under ROCm 7.2's runtime, a pinned source never.
+// Buffers come from a process-wide pool (mutex-protected, grow-only; one lease per
+// concurrent call) and go back to it when the lease ends, after the call's final
+// stream synchronisation.
+// Device scratch for the synchronous entry points, from a per-device pool of hipMalloc'd
+// buffers (grow-only, reused; one lease per concurrent call, returned after the call's
+// final stream synchronisation).  Stream-ordered hipMallocAsync pools were measured to
+// hand kernels stale bytes under ROCm 7.2's runtime; a plain pooled hipMalloc never.
+class DeviceLease {
+ public:
+  DeviceLease(int dev, size_t bytes);
+  ~DeviceLease();
+  DeviceLease(const DeviceLease &) = delete;
+  DeviceLease &operator=(const DeviceLease &) = delete;
+  char *data() const { return p_; }
+  bool ok() const { return p_ != nullptr; }
+
+ private:
+  int dev_ = 0;
+  char *p_ = nullptr;
+  size_t cap_ = 0;
+};
+
+class PinnedLease {
+ public:
+  explicit PinnedLease(size_t bytes);
+  ~PinnedLease();
+  PinnedLease(const PinnedLease &) = delete;
+  PinnedLease &operator=(const PinnedLease &) = delete;
+  char *data() const { return p_; }
+  bool ok() const { return p_ != nullptr; }
+
+ private:
+  char *p_ = nullptr;
+  size_t cap_ = 0;
+};
+
 // Device copy of a descriptor (32 B).
 struct DevChunk {
   uint64_t ptr;

@@ -280,7 +280,88 @@ uint64_t g_prof_launch_done[kProfKinds] = {0, 0, 0}, g_prof_bytes_done[kProfKind
 
 }  // namespace
 
+namespace {
+std::mutex g_pin_mu;
+std::vector<std::pair<char *, size_t>> g_pin_free;  // pooled pinned buffers
+constexpr size_t kPinPoolMax = 256u << 20;            // larger leases are freed, not pooled
+}  // namespace
+
+namespace {
+std::mutex g_dev_pool_mu;
+std::vector<std::pair<char *, size_t>> g_dev_pool[kMaxDevices];
+constexpr size_t kDevPoolMax = 1ull << 30;  // larger leases are freed, not pooled
+}  // namespace
+
 namespace h3c_rt {
+DeviceLease::DeviceLease(int dev, size_t bytes) : dev_(dev) {
+  bytes = std::max<size_t>(bytes, 4096);
+  if (dev < 0 || dev >= kMaxDevices) return;
+  {
+    std::lock_guard<std::mutex> lk(g_dev_pool_mu);
+    auto &pool = g_dev_pool[dev];
+    size_t best = pool.size();
+    for (size_t i = 0; i < pool.size(); ++i)
+      if (pool[i].second >= bytes && (best == pool.size() || pool[i].second < pool[best].second)) best = i;
+    if (best != pool.size()) {
+      p_ = pool[best].first;
+      cap_ = pool[best].second;
+      pool.erase(pool.begin() + (ptrdiff_t)best);
+      return;
+    }
+  }
+  const size_t cap = (bytes + (2u << 20) - 1) & ~size_t((2u << 20) - 1);
+  const hipError_t e = hipMalloc(reinterpret_cast<void **>(&p_), cap);
+  if (e != hipSuccess) {
+    set_error("hipMalloc (scratch)", e);
+    p_ = nullptr;
+    return;
+  }
+  cap_ = cap;
+}
+DeviceLease::~DeviceLease() {
+  if (!p_) return;
+  if (cap_ > kDevPoolMax) {
+    (void)hipFree(p_);
+    return;
+  }
+  std::lock_guard<std::mutex> lk(g_dev_pool_mu);
+  g_dev_pool[dev_].emplace_back(p_, cap_);
+}
+
+PinnedLease::PinnedLease(size_t bytes) {
+  bytes = std::max<size_t>(bytes, 4096);
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    size_t best = g_pin_free.size();
+    for (size_t i = 0; i < g_pin_free.size(); ++i)
+      if (g_pin_free[i].second >= bytes && (best == g_pin_free.size() || g_pin_free[i].second < g_pin_free[best].second))
+        best = i;
+    if (best != g_pin_free.size()) {
+      p_ = g_pin_free[best].first;
+      cap_ = g_pin_free[best].second;
+      g_pin_free.erase(g_pin_free.begin() + (ptrdiff_t)best);
+      return;
+    }
+  }
+  const size_t cap = (bytes + (1u << 20) - 1) & ~size_t((1u << 20) - 1);
+  const hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&p_), cap, 0);
+  if (e != hipSuccess) {
+    set_error("hipHostMalloc (staging)", e);
+    p_ = nullptr;
+    return;
+  }
+  cap_ = cap;
+}
+PinnedLease::~PinnedLease() {
+  if (!p_) return;
+  if (cap_ > kPinPoolMax) {
+    (void)hipHostFree(p_);
+    return;
+  }
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pin_free.emplace_back(p_, cap_);
+}
+
 hipError_t prof_begin(hipStream_t st, ProfToken &t) {
   t.on = g_prof_on.load() != 0;
   if (!t.on) return hipSuccess;
@@ -355,6 +436,48 @@ uint64_t pick_seg_bytes(uint64_t total_bytes, int num_cu) {
   return seg;
 }
 
+}  // namespace
+
+namespace {
+// Splits descriptors into one DevChunk list per polynomial with segment numbering;
+// shared by h3c_plan_create and the synchronous batch path.
+struct GroupLayout {
+  std::vector<DevChunk> hc[2];
+  uint32_t segs[2] = {0, 0}, max_segs[2] = {0, 0};
+  uint64_t bytes[2] = {0, 0};
+};
+
+int layout_groups(const h3c_desc *d, size_t n, uint64_t seg_bytes, GroupLayout &g) {
+  for (size_t i = 0; i < n; ++i) {
+    const h3c_desc &x = d[i];
+    DevChunk c{};
+    c.out_idx = (uint32_t)i;
+    c.start = x.start_raw;
+    const int k = x.type == H3C_TYPE_CRC32 ? 1 : 0;
+    const bool none = !(x.type == H3C_TYPE_CRC32C || x.type == H3C_TYPE_CRC32) || (x.ptr == nullptr && x.len > 0);
+    if (!none && x.len > 0 && x.mem != H3C_MEM_DEVICE) {
+      g_last_error = "descriptors must be device-resident";
+      return H3C_ERR_INVALID_ARG;
+    }
+    c.seg_begin = g.segs[k];
+    if (none) {
+      c.flags = kFlagNone;
+    } else {
+      c.ptr = (uint64_t)(uintptr_t)x.ptr;
+      c.len = x.len;
+      const uint64_t ns = (x.len + seg_bytes - 1) / seg_bytes;
+      if (g.segs[k] + ns > 0xFFFFFFF0u) {
+        g_last_error = "too many segments";
+        return H3C_ERR_INVALID_ARG;
+      }
+      g.segs[k] += (uint32_t)ns;
+      g.max_segs[k] = std::max(g.max_segs[k], (uint32_t)ns);
+      g.bytes[k] += x.len;
+    }
+    g.hc[k].push_back(c);
+  }
+  return H3C_OK;
+}
 }  // namespace
 
 struct h3c_plan {
@@ -437,41 +560,16 @@ int h3c_plan_create(const h3c_desc *d, size_t n, int device, h3c_plan **out) {
   }
   p->bytes = total;
 
-  std::vector<DevChunk> hc[2];
-  uint32_t segs[2] = {0, 0}, max_segs_chunk[2] = {0, 0};
-  uint64_t bytes[2] = {0, 0};
-  for (size_t i = 0; i < n; ++i) {
-    const h3c_desc &x = d[i];
-    DevChunk c{};
-    c.out_idx = (uint32_t)i;
-    c.start = x.start_raw;
-    int g = x.type == H3C_TYPE_CRC32 ? 1 : 0;
-    const bool none = !(x.type == H3C_TYPE_CRC32C || x.type == H3C_TYPE_CRC32) || (x.ptr == nullptr && x.len > 0);
-    if (!none && x.len > 0 && x.mem != H3C_MEM_DEVICE) {
-      delete p;
-      (void)hipSetDevice(prev);
-      g_last_error = "h3c_plan_create: descriptors must be device-resident";
-      return H3C_ERR_INVALID_ARG;
-    }
-    c.seg_begin = segs[g];
-    if (none) {
-      c.flags = kFlagNone;
-    } else {
-      c.ptr = (uint64_t)(uintptr_t)x.ptr;
-      c.len = x.len;
-      const uint64_t ns = (x.len + p->seg_bytes - 1) / p->seg_bytes;
-      if (segs[g] + ns > 0xFFFFFFF0u) {
-        delete p;
-        (void)hipSetDevice(prev);
-        g_last_error = "h3c_plan_create: too many segments";
-        return H3C_ERR_INVALID_ARG;
-      }
-      segs[g] += (uint32_t)ns;
-      max_segs_chunk[g] = std::max(max_segs_chunk[g], (uint32_t)ns);
-      bytes[g] += x.len;
-    }
-    hc[g].push_back(c);
+  GroupLayout gl;
+  rc = layout_groups(d, n, p->seg_bytes, gl);
+  if (rc) {
+    delete p;
+    (void)hipSetDevice(prev);
+    return rc;
   }
+  std::vector<DevChunk> *hc = gl.hc;
+  uint32_t *segs = gl.segs, *max_segs_chunk = gl.max_segs;
+  uint64_t *bytes = gl.bytes;
   uint32_t max_segs = 0;
   for (int g = 0; g < 2; ++g) {
     if (hc[g].empty()) continue;
@@ -542,84 +640,124 @@ int h3c_plan_run(h3c_plan *p, const uint32_t *expected_raw_dev, uint32_t *out_ra
   return rc;
 }
 
-// Synchronous API: stage host payloads, run a temporary plan, copy results back.
+// Synchronous API: stage host payloads through a pinned lease into a pooled device lease
+// and run the kernels on the caller's stream.  Neither lease allocates in steady state,
+// so concurrent callers on their own streams never force a device-wide synchronisation
+// (hipMalloc / hipFree would; hipMallocAsync pools are not used, see DeviceLease).
 static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uint8_t *out_type, uint32_t *out_raw,
                       uint8_t *ok, uint64_t *n_mismatch, void *stream) {
   if (n == 0) {
     if (n_mismatch) *n_mismatch = 0;
     return H3C_OK;
   }
-  if (!d || !out_raw) return H3C_ERR_INVALID_ARG;
+  if (!d || !out_raw || n > 0xFFFFFFF0u) return H3C_ERR_INVALID_ARG;
   int dev = 0;
   int rc = current_device(&dev);
   if (rc) return rc;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 
-  // Stage host payloads into one device buffer.
   std::vector<h3c_desc> dd(d, d + n);
-  uint64_t host_bytes = 0;
-  for (auto &x : dd)
-    if (x.mem != H3C_MEM_DEVICE && x.ptr && x.len && (x.type == H3C_TYPE_CRC32C || x.type == H3C_TYPE_CRC32))
-      host_bytes += (x.len + 255) & ~uint64_t(255);
-  uint8_t *stage = nullptr;
-  uint32_t *d_out = nullptr, *d_exp = nullptr, *d_mis = nullptr;
-  uint8_t *d_ok = nullptr;
-  h3c_plan *plan = nullptr;
-  auto cleanup = [&]() {
-    if (plan) h3c_plan_destroy(plan);
-    if (stage) (void)hipFree(stage);
-    if (d_out) (void)hipFree(d_out);
-    if (d_exp) (void)hipFree(d_exp);
-    if (d_ok) (void)hipFree(d_ok);
-    if (d_mis) (void)hipFree(d_mis);
+  uint64_t host_bytes = 0, total = 0;
+  for (auto &x : dd) {
+    const bool crc = x.ptr && x.len && (x.type == H3C_TYPE_CRC32C || x.type == H3C_TYPE_CRC32);
+    if (crc && x.mem != H3C_MEM_DEVICE) host_bytes += (x.len + 255) & ~uint64_t(255);
+    if (crc) total += x.len;
+  }
+  uint64_t seg_bytes = pick_seg_bytes(total, g_dev[dev].num_cu);
+  if (const char *e = std::getenv("H3C_SEG_BYTES")) {  // test hook: force the segment size
+    const uint64_t v = std::strtoull(e, nullptr, 0);
+    if (v >= kRowBytes && v % kRowBytes == 0) seg_bytes = v;
+  }
+  // staging offsets first (descriptor pointers are rewritten to the arena below)
+  auto align = [](uint64_t v) { return (v + 255) & ~uint64_t(255); };
+  const uint64_t off_stage = 0;
+  GroupLayout gl;
+  {
+    // layout with placeholder pointers for staged payloads (device-ness is all that matters)
+    std::vector<h3c_desc> probe(dd);
+    for (auto &x : probe)
+      if (x.mem != H3C_MEM_DEVICE) x.mem = H3C_MEM_DEVICE;
+    rc = layout_groups(probe.data(), n, seg_bytes, gl);
+    if (rc) return rc;
+  }
+  const uint64_t off_chunks0 = align(off_stage + host_bytes);
+  const uint64_t off_chunks1 = align(off_chunks0 + gl.hc[0].size() * sizeof(DevChunk));
+  const uint64_t off_seg = align(off_chunks1 + gl.hc[1].size() * sizeof(DevChunk));
+  const uint64_t off_out = align(off_seg + 4ull * std::max(gl.segs[0], gl.segs[1]));
+  const uint64_t off_exp = align(off_out + 4ull * n);
+  const uint64_t off_ok = align(off_exp + (expected ? 4ull * n : 0));
+  const uint64_t off_mis = align(off_ok + (expected ? n : 0));
+  const uint64_t arena_bytes = off_mis + 256;
+  char *arena = nullptr;
+  // pinned staging: [host payloads | expected | DevChunk lists | results out | ok | mismatch]
+  const uint64_t p_exp = align(host_bytes), p_chunks = align(p_exp + (expected ? 4ull * n : 0));
+  const uint64_t p_out = align(p_chunks + (gl.hc[0].size() + gl.hc[1].size()) * sizeof(DevChunk));
+  const uint64_t p_ok = align(p_out + 4ull * n), p_mis = align(p_ok + n), p_end = p_mis + 256;
+  h3c_rt::PinnedLease pin(p_end);
+  if (!pin.ok()) return H3C_ERR_HIP;
+  char *const pb = pin.data();
+  h3c_rt::DeviceLease scratch(dev, arena_bytes);
+  if (!scratch.ok()) return H3C_ERR_HIP;
+  arena = scratch.data();
+  auto h2d = [&](void *dst, uint64_t pin_off, const void *src, size_t len) -> hipError_t {
+    std::memcpy(pb + pin_off, src, len);
+    return hipMemcpyAsync(dst, pb + pin_off, len, hipMemcpyHostToDevice, st);
   };
-#define SYNC_TRY(expr)        \
-  do {                        \
-    hipError_t e_ = (expr);   \
-    if (e_ != hipSuccess) {   \
-      set_error(#expr, e_);   \
-      cleanup();              \
-      return H3C_ERR_HIP;     \
-    }                         \
-  } while (0)
-  if (host_bytes) {
-    SYNC_TRY(hipMalloc(&stage, host_bytes));
-    uint64_t off = 0;
-    for (auto &x : dd) {
+  uint32_t mis = 0;
+  auto body = [&]() -> int {
+    // stage host payloads and point their DevChunks at the staged copies
+    uint64_t off = off_stage;
+    std::vector<uint64_t> staged(n, 0);
+    for (size_t i = 0; i < n; ++i) {
+      const h3c_desc &x = dd[i];
       if (x.mem != H3C_MEM_DEVICE && x.ptr && x.len && (x.type == H3C_TYPE_CRC32C || x.type == H3C_TYPE_CRC32)) {
-        SYNC_TRY(hipMemcpyAsync(stage + off, x.ptr, x.len, hipMemcpyHostToDevice, st));
-        x.ptr = stage + off;
-        x.mem = H3C_MEM_DEVICE;
+        HIP_TRY(h2d(arena + off, off, x.ptr, x.len));  // staging and arena share offsets
+        staged[i] = (uint64_t)(uintptr_t)(arena + off);
         off += (x.len + 255) & ~uint64_t(255);
       }
     }
+    for (int k = 0; k < 2; ++k)
+      for (DevChunk &c : gl.hc[k])
+        if (staged[c.out_idx]) c.ptr = staged[c.out_idx];
+    DevChunk *d_chunks[2] = {reinterpret_cast<DevChunk *>(arena + off_chunks0),
+                             reinterpret_cast<DevChunk *>(arena + off_chunks1)};
+    uint32_t *d_seg = reinterpret_cast<uint32_t *>(arena + off_seg);
+    uint32_t *d_out = reinterpret_cast<uint32_t *>(arena + off_out);
+    uint32_t *d_exp = expected ? reinterpret_cast<uint32_t *>(arena + off_exp) : nullptr;
+    uint8_t *d_ok = expected ? reinterpret_cast<uint8_t *>(arena + off_ok) : nullptr;
+    uint32_t *d_mis = expected ? reinterpret_cast<uint32_t *>(arena + off_mis) : nullptr;
+    if (expected) {
+      HIP_TRY(h2d(d_exp, p_exp, expected, 4ull * n));
+      HIP_TRY(hipMemsetAsync(d_mis, 0, 4, st));
+    }
+    for (int k = 0; k < 2; ++k) {
+      if (gl.hc[k].empty()) continue;
+      HIP_TRY(h2d(d_chunks[k], p_chunks + (k ? gl.hc[0].size() * sizeof(DevChunk) : 0), gl.hc[k].data(),
+                  gl.hc[k].size() * sizeof(DevChunk)));
+      const int r = h3c_rt::launch_crc(st, dev, k == 0 ? H3C_TYPE_CRC32C : H3C_TYPE_CRC32, d_chunks[k],
+                                       (uint32_t)gl.hc[k].size(), gl.segs[k], gl.max_segs[k], gl.bytes[k], seg_bytes,
+                                       read_dbg_flags(), d_seg, d_exp, d_out, d_ok, d_mis, H3C_PROF_SEG);
+      if (r) return r;
+    }
+    HIP_TRY(hipMemcpyAsync(pb + p_out, d_out, 4ull * n, hipMemcpyDeviceToHost, st));
+    if (expected) {
+      HIP_TRY(hipMemcpyAsync(pb + p_ok, d_ok, n, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(pb + p_mis, d_mis, 4, hipMemcpyDeviceToHost, st));
+    }
+    return H3C_OK;
+  };
+  rc = body();
+  const hipError_t se = hipStreamSynchronize(st);  // the leases are reused only after this
+  if (rc) return rc;
+  if (se != hipSuccess) {
+    set_error("batch_sync: hipStreamSynchronize", se);
+    return H3C_ERR_HIP;
   }
-  rc = h3c_plan_create(dd.data(), n, dev, &plan);
-  if (rc) {
-    cleanup();
-    return rc;
-  }
-  SYNC_TRY(hipMalloc(&d_out, n * sizeof(uint32_t)));
+  std::memcpy(out_raw, pb + p_out, 4ull * n);
   if (expected) {
-    SYNC_TRY(hipMalloc(&d_exp, n * sizeof(uint32_t)));
-    SYNC_TRY(hipMalloc(&d_ok, n));
-    SYNC_TRY(hipMalloc(&d_mis, sizeof(uint32_t)));
-    SYNC_TRY(hipMemcpyAsync(d_exp, expected, n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    SYNC_TRY(hipMemsetAsync(d_mis, 0, sizeof(uint32_t), st));
+    std::memcpy(ok, pb + p_ok, n);
+    std::memcpy(&mis, pb + p_mis, 4);
   }
-  rc = h3c_plan_run(plan, d_exp, d_out, d_ok, d_mis, stream);
-  if (rc) {
-    cleanup();
-    return rc;
-  }
-  SYNC_TRY(hipMemcpyAsync(out_raw, d_out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  uint32_t mis = 0;
-  if (expected) {
-    SYNC_TRY(hipMemcpyAsync(ok, d_ok, n, hipMemcpyDeviceToHost, st));
-    SYNC_TRY(hipMemcpyAsync(&mis, d_mis, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  }
-  SYNC_TRY(hipStreamSynchronize(st));
-#undef SYNC_TRY
   if (out_type)
     for (size_t i = 0; i < n; ++i) {
       const bool valid = (d[i].type == H3C_TYPE_CRC32C || d[i].type == H3C_TYPE_CRC32) &&
@@ -627,7 +765,6 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
       out_type[i] = valid ? d[i].type : (uint8_t)H3C_TYPE_NONE;
     }
   if (n_mismatch) *n_mismatch = mis;
-  cleanup();
   return H3C_OK;
 }
 

@@ -264,16 +264,29 @@ int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t 
     HIP_TRY(grow(h->d_mis, dummy, 1));
     h->chunk_cap = n;
   }
-  if (!pieces.empty()) {
-    HIP_TRY(hipMemcpyAsync(h->d_pieces, pieces.data(), pieces.size() * sizeof(h3c_rt::DevChunk),
-                           hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(h->d_piece_len, piece_len.data(), piece_len.size() * 8, hipMemcpyHostToDevice, st));
+  // descriptor uploads and result downloads through pinned staging (h3c_rt::PinnedLease)
+  const size_t up[4] = {pieces.size() * sizeof(h3c_rt::DevChunk), piece_len.size() * 8, n * sizeof(FoldChunk),
+                        expected ? n * 4 : 0};
+  const void *up_src[4] = {pieces.data(), piece_len.data(), fold.data(), expected};
+  void *up_dst[4] = {h->d_pieces, h->d_piece_len, h->d_fold, h->d_exp};
+  size_t pin_off[5], pin_bytes = 0;
+  for (int k = 0; k < 4; ++k) {
+    pin_off[k] = pin_bytes;
+    pin_bytes += (up[k] + 255) & ~size_t(255);
   }
-  HIP_TRY(hipMemcpyAsync(h->d_fold, fold.data(), n * sizeof(FoldChunk), hipMemcpyHostToDevice, st));
-  if (expected) {
-    HIP_TRY(hipMemcpyAsync(h->d_exp, expected, n * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(h->d_mis, 0, 4, st));
-  }
+  pin_off[4] = pin_bytes;  // results: out (4n) | ok (n) | mismatch (4)
+  h3c_rt::PinnedLease pin(pin_bytes + ((n * 4 + 255) & ~size_t(255)) + ((n + 255) & ~size_t(255)) + 256);
+  if (!pin.ok()) return H3C_ERR_HIP;
+  char *const pb = pin.data();
+  char *const pr_out = pb + pin_off[4];
+  char *const pr_ok = pr_out + ((n * 4 + 255) & ~size_t(255));
+  char *const pr_mis = pr_ok + ((n + 255) & ~size_t(255));
+  for (int k = 0; k < 4; ++k)
+    if (up[k]) {
+      std::memcpy(pb + pin_off[k], up_src[k], up[k]);
+      HIP_TRY(hipMemcpyAsync(up_dst[k], pb + pin_off[k], up[k], hipMemcpyHostToDevice, st));
+    }
+  if (expected) HIP_TRY(hipMemsetAsync(h->d_mis, 0, 4, st));
 
   // ---- the pipeline ----
   h3c_rt::ProfToken tok;
@@ -302,13 +315,18 @@ int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t 
                      h->d_piece_crc, h->d_piece_len, pc, expected ? h->d_exp : nullptr, h->d_out, h->d_ok, h->d_mis);
   HIP_TRY(hipGetLastError());
   HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_HOSTFED, total));
-  HIP_TRY(hipMemcpyAsync(out_raw, h->d_out, n * 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(pr_out, h->d_out, n * 4, hipMemcpyDeviceToHost, st));
   uint32_t mis = 0;
   if (expected) {
-    HIP_TRY(hipMemcpyAsync(ok, h->d_ok, n, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(&mis, h->d_mis, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(pr_ok, h->d_ok, n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(pr_mis, h->d_mis, 4, hipMemcpyDeviceToHost, st));
   }
   HIP_TRY(hipStreamSynchronize(st));
+  std::memcpy(out_raw, pr_out, n * 4);
+  if (expected) {
+    std::memcpy(ok, pr_ok, n);
+    std::memcpy(&mis, pr_mis, 4);
+  }
   if (n_mismatch) *n_mismatch = mis;
   if (prev != h->device) HIP_TRY(hipSetDevice(prev));
   return H3C_OK;

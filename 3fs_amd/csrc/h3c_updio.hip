@@ -149,7 +149,8 @@ __global__ void updio_true_kernel(const Aff *__restrict__ scan, const uint32_t *
   out[p] = dgf_mul(raw0[key[p]], a.m, poly) ^ a.e;
 }
 
-// Device arena for one call: every buffer is carved from one hipMallocAsync.
+// Device arena for one call: every buffer is carved from one pooled device lease
+// (h3c_rt::DeviceLease; hipMallocAsync pools gave kernels stale bytes under ROCm 7.2).
 struct Arena {
   char *base = nullptr;
   size_t off = 0;
@@ -310,27 +311,35 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
       add_job(pay, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg_a);
   if (!pay.chunks.empty()) {
     Arena a;
-    const size_t bytes = pay.chunks.size() * sizeof(DevChunk) + 4ull * pay.total_segs + 4ull * n + 3 * 256;
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&a.base), bytes, st));
-    DevChunk *d_chunks = a.take<DevChunk>(pay.chunks.size());
+    const size_t nc = pay.chunks.size();
+    const size_t bytes = nc * sizeof(DevChunk) + 4ull * pay.total_segs + 4ull * n + 3 * 256;
+    // pinned staging (see h3c_rt::PinnedLease): [DevChunks | payload CRCs back]
+    const size_t pin_raw = (nc * sizeof(DevChunk) + 255) & ~size_t(255);
+    h3c_rt::PinnedLease pin(pin_raw + 4ull * n);
+    if (!pin.ok()) return H3C_ERR_HIP;
+    std::memcpy(pin.data(), pay.chunks.data(), nc * sizeof(DevChunk));
+    h3c_rt::DeviceLease scratch(dev, bytes);
+    if (!scratch.ok()) return H3C_ERR_HIP;
+    a.base = scratch.data();
+    DevChunk *d_chunks = a.take<DevChunk>(nc);
     uint32_t *d_seg = a.take<uint32_t>(pay.total_segs);
     uint32_t *d_raw = a.take<uint32_t>(n);
     int err = H3C_OK;
-    hipError_t e = hipMemcpyAsync(d_chunks, pay.chunks.data(), pay.chunks.size() * sizeof(DevChunk),
-                                  hipMemcpyHostToDevice, st);
+    hipError_t e = hipMemcpyAsync(d_chunks, pin.data(), nc * sizeof(DevChunk), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemsetAsync(d_raw, 0xFF, 4ull * n, st);
     if (e == hipSuccess) {
-      err = h3c_rt::launch_crc(st, dev, poly_type, d_chunks, (uint32_t)pay.chunks.size(), pay.total_segs,
-                               pay.max_segs, pay.bytes, seg_a, 0, d_seg, nullptr, d_raw, nullptr, nullptr, -1);
-      if (!err) e = hipMemcpyAsync(payraw.data(), d_raw, 4ull * n, hipMemcpyDeviceToHost, st);
+      err = h3c_rt::launch_crc(st, dev, poly_type, d_chunks, (uint32_t)nc, pay.total_segs, pay.max_segs, pay.bytes,
+                               seg_a, 0, d_seg, nullptr, d_raw, nullptr, nullptr, -1);
+      if (!err) e = hipMemcpyAsync(pin.data() + pin_raw, d_raw, 4ull * n, hipMemcpyDeviceToHost, st);
     }
-    (void)hipFreeAsync(a.base, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    const hipError_t se = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = se;
     if (e != hipSuccess) {
       h3c_rt::set_error("h3c_update_ios: payload checksums", e);
       return H3C_ERR_HIP;
     }
     if (err) return err;
+    std::memcpy(payraw.data(), pin.data() + pin_raw, 4ull * n);
   }
 
   clk.mark("A payload");
@@ -498,7 +507,9 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
                          4ull * std::max(njobs, 1u) + 4ull * n + npos * (sizeof(AffIn) + 2 * sizeof(Aff) + 8) +
                          4ull * nchunks + scan_tmp + 16 * 256;
     Arena a;
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&a.base), bytes, st));
+    h3c_rt::DeviceLease scratch(dev, bytes);
+    if (!scratch.ok()) return H3C_ERR_HIP;
+    a.base = scratch.data();
     DevChunk *d_crc = a.take<DevChunk>(crc_chunks);
     CopyPiece *d_copy = a.take<CopyPiece>(copy_pieces);
     uint32_t *d_seg = a.take<uint32_t>(max_segs);
@@ -520,17 +531,26 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
       all_crc.insert(all_crc.end(), ep_crc[e].chunks.begin(), ep_crc[e].chunks.end());
       all_copy.insert(all_copy.end(), ep_copy[e].begin(), ep_copy[e].end());
     }
+    // pinned staging for every upload and the result download (see h3c_rt::PinnedLease)
+    const size_t up[6] = {crc_chunks * sizeof(DevChunk), copy_pieces * sizeof(CopyPiece), 4ull * n,
+                          npos * sizeof(AffIn), 4ull * npos, 4ull * nchunks};
+    const void *src[6] = {all_crc.data(), all_copy.data(), payraw.data(), lay.data(), keys.data(), raw0.data()};
+    void *dst[6] = {d_crc, d_copy, d_payraw, d_in, d_keys, d_raw0};
+    size_t pin_bytes = 0, pin_off[7];
+    for (int k = 0; k < 6; ++k) {
+      pin_off[k] = pin_bytes;
+      pin_bytes += (up[k] + 255) & ~size_t(255);
+    }
+    pin_off[6] = pin_bytes;
+    h3c_rt::PinnedLease pin(pin_bytes + 4ull * npos);
+    if (!pin.ok()) return H3C_ERR_HIP;
     int err = H3C_OK;
     auto body = [&]() -> int {
-      if (crc_chunks)
-        HIP_TRY(hipMemcpyAsync(d_crc, all_crc.data(), crc_chunks * sizeof(DevChunk), hipMemcpyHostToDevice, st));
-      if (copy_pieces)
-        HIP_TRY(hipMemcpyAsync(d_copy, all_copy.data(), copy_pieces * sizeof(CopyPiece), hipMemcpyHostToDevice,
-                               st));
-      HIP_TRY(hipMemcpyAsync(d_payraw, payraw.data(), 4ull * n, hipMemcpyHostToDevice, st));
-      HIP_TRY(hipMemcpyAsync(d_in, lay.data(), npos * sizeof(AffIn), hipMemcpyHostToDevice, st));
-      HIP_TRY(hipMemcpyAsync(d_keys, keys.data(), 4ull * npos, hipMemcpyHostToDevice, st));
-      HIP_TRY(hipMemcpyAsync(d_raw0, raw0.data(), 4ull * nchunks, hipMemcpyHostToDevice, st));
+      for (int k = 0; k < 6; ++k)
+        if (up[k]) {
+          std::memcpy(pin.data() + pin_off[k], src[k], up[k]);
+          HIP_TRY(hipMemcpyAsync(dst[k], pin.data() + pin_off[k], up[k], hipMemcpyHostToDevice, st));
+        }
       size_t co = 0, po = 0;
       for (size_t e = 0; e < ep_crc.size(); ++e) {
         const CrcBatch &b = ep_crc[e];
@@ -555,17 +575,17 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
                                              rocprim::equal_to<uint32_t>(), st));
       hipLaunchKernelGGL(updio_true_kernel, dim3(gb), dim3(tb), 0, st, d_scan, d_keys, npos, d_raw0, poly, d_true);
       HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(truev.data(), d_true, 4ull * npos, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(pin.data() + pin_off[6], d_true, 4ull * npos, hipMemcpyDeviceToHost, st));
       return H3C_OK;
     };
     err = body();
-    (void)hipFreeAsync(a.base, st);
-    const hipError_t e = hipStreamSynchronize(st);
+    const hipError_t e = hipStreamSynchronize(st);  // the leases are reused only after this
     if (err) return err;
     if (e != hipSuccess) {
       h3c_rt::set_error("h3c_update_ios", e);
       return H3C_ERR_HIP;
     }
+    std::memcpy(truev.data(), pin.data() + pin_off[6], 4ull * npos);
   }
 
   clk.mark("C-D device");

@@ -2,6 +2,7 @@
 // usage: checksum_info_test cpu|gpu     (gpu mode needs a HIP device)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -71,6 +72,54 @@ static void gpu_tests() {
   std::vector<ChecksumInfo> out;
   CHECK(ChecksumInfo::createBatch(ds, out) == 0);
   for (int k = 0; k < 64; ++k) CHECK(out[k].value == orc_crc32c_sse42(host.data() + k * 4096, 4096 + k, ~0U));
+  // Repeated synchronous calls under /opt/rocm's runtime (the storage service's runtime):
+  // pageable and device payloads, null and own streams.  Guards the scratch-allocation
+  // path (hipMallocAsync pools handed kernels stale bytes here; profiles/r01b_hip_alloc_coherence.txt).
+  hipStream_t own;
+  CHECK(hipStreamCreate(&own) == hipSuccess);
+  for (int it = 0; it < 200; ++it) {
+    const size_t len = 1 + rng() % (1u << 20);
+    const size_t off = rng() % 64;
+    void *st = (it & 1) ? (void *)own : nullptr;
+    const bool host_src = (it & 2) != 0;
+    h3c_desc d{host_src ? (const void *)(host.data() + off) : (const void *)(dev + off), len, ~0U, 1,
+               (uint8_t)(host_src ? H3C_MEM_HOST_PAGEABLE : H3C_MEM_DEVICE), 0};
+    uint8_t t = 0;
+    uint32_t v = 0;
+    CHECK(h3c_batch_create(&d, 1, &t, &v, st) == 0);
+    CHECK(v == orc_crc32c_sse42(host.data() + off, len, ~0U));
+  }
+  // h3c_update_ios from C++: appends and overwrites, then the chunk checksum equals a fresh CRC.
+  {
+    const uint32_t cs = 1u << 20;
+    uint8_t *chunk = nullptr, *pay = nullptr;
+    CHECK(hipMalloc(&chunk, cs) == hipSuccess);
+    CHECK(hipMalloc(&pay, 64 * 8192) == hipSuccess);
+    std::vector<uint8_t> model(cs, 0), hp(64 * 8192);
+    for (auto &c : hp) c = (uint8_t)rng();
+    CHECK(hipMemcpy(pay, hp.data(), hp.size(), hipMemcpyHostToDevice) == hipSuccess);
+    h3c_chunk_state cst{(uint64_t)(uintptr_t)chunk, cs, 0, 0, 1, {0, 0, 0}};
+    std::vector<h3c_update_io> ios;
+    uint32_t size = 0;
+    for (int k = 0; k < 64; ++k) {
+      const uint32_t len = 1 + rng() % 8192;
+      const uint32_t o = (k % 3 == 0 || size == 0) ? size : (uint32_t)(rng() % size);
+      const uint8_t *p = hp.data() + k * 8192;
+      ios.push_back(h3c_update_io{(uint64_t)(uintptr_t)(pay + k * 8192), 0, o, len, orc_crc32c_sse42(p, len, ~0U), 1,
+                                  H3C_UPD_WRITE, {0, 0, 0, 0, 0, 0}});
+      std::memcpy(model.data() + o, p, len);
+      size = std::max(size, o + len);
+    }
+    std::vector<h3c_update_result> res(ios.size());
+    CHECK(h3c_update_ios(H3C_TYPE_CRC32C, &cst, 1, ios.data(), (uint32_t)ios.size(), res.data(), 0, own) == 0);
+    for (auto &r : res) CHECK(r.status == 0);
+    CHECK(cst.size == size && cst.type == 1);
+    CHECK(cst.value == orc_crc32c_sse42(model.data(), size, ~0U));
+    CHECK(res.back().value == cst.value);
+    (void)hipFree(chunk);
+    (void)hipFree(pay);
+  }
+  (void)hipStreamDestroy(own);
   (void)hipFree(dev);
 }
 

@@ -1,0 +1,141 @@
+"""The shim's threading contract: entry points are called concurrently
+from many host threads (32 AIO + 32 update threads in the reference,
+src/storage/aio/AioReadWorker.h:27, src/storage/update/UpdateWorker.h:15), each with its
+own stream.  ctypes releases the GIL during the calls, so these threads really overlap.
+Also: a device-resident plan is capturable into a HIP graph (a scrub pass replayed with
+one launch)."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+
+pytestmark = pytest.mark.gpu
+MASK = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available()
+    return torch, torch.device("cuda:0")
+
+
+def test_concurrent_threads_own_streams(h3c, torch_dev):
+    torch, dev = torch_dev
+    nthreads, per = 16, 24
+    rng = np.random.default_rng(1)
+    host = [[rng.integers(0, 256, int(rng.integers(1, 3 << 20)), dtype=np.uint8) for _ in range(per)]
+            for _ in range(nthreads)]
+    want = [[orc.crc32c(d) for d in hs] for hs in host]
+    dev_bufs = [[torch.from_numpy(d).to(dev) for d in hs] for hs in host]
+    torch.cuda.synchronize()
+    errors, results = [], [None] * nthreads
+    start = threading.Barrier(nthreads)
+
+    def work(k):
+        try:
+            s = torch.cuda.Stream(device=dev)
+            start.wait()
+            for it in range(3):
+                exp = list(want[k])
+                exp[it] ^= 1  # one mismatch per round
+                raw, ok, nbad = h3c.batch_verify(dev_bufs[k], exp, stream=s)
+                if nbad != 1 or ok[it] or list(map(int, raw)) != want[k]:
+                    errors.append((k, it, nbad))
+                # host-staged payloads and the general update path on the same thread
+                t, v = h3c.batch_create(host[k][:4], stream=s)
+                if list(map(int, v)) != want[k][:4]:
+                    errors.append((k, it, "host"))
+            results[k] = True
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    threads = [threading.Thread(target=work, args=(k,)) for k in range(nthreads)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors[:5]
+    assert all(results)
+
+
+def test_concurrent_update_batches_distinct_chunks(h3c, torch_dev):
+    """Update threads each own a chunk set (the reference shards update jobs by chunk)."""
+    torch, dev = torch_dev
+    nthreads, nchunks, cl = 8, 4, 1 << 20
+    G = 4096
+    slabs, states, ioss, pays, finals = [], [], [], [], []
+    rng = np.random.default_rng(2)
+    for k in range(nthreads):
+        slab = torch.empty(nchunks * cl, dtype=torch.uint8, device=dev)
+        h3c.fill_splitmix(slab, cl, nchunks, cl, 100 + k)
+        host = slab.cpu().numpy().reshape(nchunks, cl).copy()
+        st = np.zeros(nchunks, dtype=h3c.CHUNK_STATE_DTYPE)
+        for c in range(nchunks):
+            st[c] = (slab.data_ptr() + c * cl, cl, cl, orc.crc32c(host[c]), 1, 0)
+        nw = 300
+        pay = rng.integers(0, 256, (nw, G), dtype=np.uint8)
+        io = np.zeros(nw, dtype=h3c.UPDATE_IO_DTYPE)
+        dpay = torch.from_numpy(pay.reshape(-1)).to(dev)
+        for i in range(nw):
+            c, b = int(rng.integers(0, nchunks)), int(rng.integers(0, cl // G))
+            io[i] = (dpay.data_ptr() + i * G, c, b * G, G, orc.crc32c(pay[i]), 1, h3c.UPD_WRITE, 0)
+            host[c, b * G:(b + 1) * G] = pay[i]
+        slabs.append(slab)
+        states.append(st)
+        ioss.append(io)
+        pays.append(dpay)
+        finals.append([orc.crc32c(host[c]) for c in range(nchunks)])
+    torch.cuda.synchronize()
+    errors = []
+
+    def work(k):
+        try:
+            s = torch.cuda.Stream(device=dev)
+            res = h3c.update_ios(states[k], ioss[k], stream=s)
+            if not (res["status"] == 0).all() or list(map(int, states[k]["value"])) != finals[k]:
+                errors.append(k)
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    threads = [threading.Thread(target=work, args=(k,)) for k in range(nthreads)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+
+
+def test_plan_run_captured_in_hip_graph(h3c, torch_dev):
+    """A scrub pass (plan_run: seg + finalize kernels, no host sync) captured once into a
+    HIP graph and replayed; every replay sees the current bytes."""
+    torch, dev = torch_dev
+    n, cl = 256, 256 << 10
+    slab = torch.empty(n * cl, dtype=torch.uint8, device=dev)
+    h3c.fill_splitmix(slab, cl, n, cl, 7)
+    plan = h3c.Plan.uniform(slab.data_ptr(), cl, n)
+    want = torch.zeros(n, dtype=torch.int32, device=dev)
+    plan.run(want)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    mis = torch.zeros(1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            mis.zero_()
+            plan.run(out, want, ok, mis, stream=s)
+    g.replay()
+    torch.cuda.synchronize()
+    assert int(mis.item()) == 0 and torch.equal(out, want)
+    slab[5 * cl + 17] ^= 1
+    slab[200 * cl] ^= 0x80
+    g.replay()
+    torch.cuda.synchronize()
+    assert int(mis.item()) == 2
+    assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == [5, 200]
+    plan.close()
