@@ -90,14 +90,14 @@ __global__ void upd_keys_kernel(const uint32_t *__restrict__ blk_chunk, const ui
   if (i >= n) return;
   const uint32_t c = blk_chunk[i], b = blk_index[i];
   iota[i] = i;
-  if (c >= nchunks || b >= bpc) {  // invalid entry: counted, parked on sentinel slot / chunk, no effect
-    atomicAdd(err, 1u);
+  if (c >= nchunks || b >= bpc) {  // invalid entry: parked on the sentinel slot / chunk, no effect
+    if (err) atomicAdd(err, 1u);  // sort path counts here, tile path in upd_tile_kernel
     kslot[i] = nchunks * bpc;
-    kchunk[i] = nchunks;
+    if (kchunk) kchunk[i] = nchunks;
     return;
   }
   kslot[i] = c * bpc + b;
-  kchunk[i] = c;
+  if (kchunk) kchunk[i] = c;
 }
 
 // On the stable sort by slot: prev[i] = previous writer of i's slot (or none), and for
@@ -335,22 +335,28 @@ __global__ __launch_bounds__(kTile) void upd_tile_kernel(const uint32_t *__restr
                                                          uint32_t nchunks, uint32_t bpc,
                                                          const uint32_t *__restrict__ delta,
                                                          const uint32_t *__restrict__ sh, uint32_t poly,
-                                                         uint32_t *__restrict__ inpre, uint32_t *__restrict__ agg) {
+                                                         uint32_t *__restrict__ inpre, uint32_t *__restrict__ agg,
+                                                         uint32_t *__restrict__ tile_invalid) {
   __shared__ uint32_t cid[kTile], val[kTile];
   const uint32_t t = threadIdx.x, i0 = blockIdx.x * kTile, i = i0 + t;
   uint32_t c = kNone, v = 0;
+  bool invalid = false;
   if (i < n) {
     const uint32_t cc = blk_chunk[i], b = blk_index[i];
     if (cc < nchunks && b < bpc) {
       c = cc;
       v = dgf_mul(delta[i], sh[b], poly);
+    } else {
+      invalid = true;
     }
   }
   cid[t] = c;
   val[t] = v;
   uint32_t *row = agg + (uint64_t)blockIdx.x * nchunks;
   for (uint32_t k = t; k < nchunks; k += kTile) row[k] = 0;
-  __syncthreads();  // LDS tile loaded, row zeroed (workgroup-scope fence)
+  // LDS tile loaded, row zeroed (workgroup-scope fence); count the tile's invalid entries
+  const int ninv = __syncthreads_count(invalid);
+  if (t == 0) tile_invalid[blockIdx.x] = (uint32_t)ninv;
   const uint32_t cnt = min(kTile, n - i0);
   uint32_t acc = 0;
   bool last = true;
@@ -370,9 +376,21 @@ __global__ __launch_bounds__(kTile) void upd_tile_kernel(const uint32_t *__restr
 __global__ __launch_bounds__(kTile) void upd_column_kernel(const uint32_t *__restrict__ agg, uint32_t ntiles,
                                                            uint32_t nchunks, const uint32_t *__restrict__ raw_in,
                                                            uint32_t *__restrict__ colpre,
-                                                           uint32_t *__restrict__ raw_out) {
+                                                           uint32_t *__restrict__ raw_out,
+                                                           const uint32_t *__restrict__ tile_invalid,
+                                                           uint32_t *__restrict__ n_invalid) {
   __shared__ uint32_t part[kTile / 64];
   const uint32_t c = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (c == 0 && n_invalid) {  // workgroup 0 also totals the invalid entries
+    uint32_t s = 0;
+    for (uint32_t r = t; r < ntiles; r += kTile) s += tile_invalid[r];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) part[wave] = s;
+    __syncthreads();
+    if (t == 0) *n_invalid = part[0] + part[1] + part[2] + part[3];
+    __syncthreads();
+  }
   uint32_t carry = 0;
   for (uint32_t base = 0; base < ntiles; base += kTile) {
     const uint32_t r = base + t;
@@ -420,6 +438,7 @@ struct Workspace {
   uint32_t *kslot, *kslot_s, *kchunk, *kchunk_s, *iota, *idx1, *idx2;
   uint32_t *prev, *final_of, *delta, *vals, *scan, *sh, *err;
   uint32_t *agg, *colpre;  // dense tile path: ntiles x nchunks each
+  uint32_t *tile_invalid;  // dense tile path: per-tile invalid-entry counts
   void *tmp;
   size_t tmp_bytes;
 };
@@ -442,6 +461,7 @@ int layout(void *base, uint32_t n, uint32_t nchunks, uint32_t bpc, Workspace &w,
   const uint64_t tiles_cells = use_tiles(n, nchunks) ? (uint64_t)((n + kTile - 1) / kTile) * nchunks : 0;
   w.agg = (uint32_t *)take(4ull * tiles_cells);
   w.colpre = (uint32_t *)take(4ull * tiles_cells);
+  w.tile_invalid = (uint32_t *)take(4ull * ((n + kTile - 1) / kTile));
   size_t s1 = 0, s2 = 0;
   if (rocprim::radix_sort_pairs<SortConfig>(nullptr, s1, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                 (uint32_t *)nullptr, n, 0, 32) != hipSuccess)
@@ -517,8 +537,11 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
     return H3C_ERR_INVALID_ARG;
   if (!chunk_base_dev || !chunk_raw_in_dev || !chunk_raw_out_dev) return H3C_ERR_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  HIP_TRY(hipMemcpyAsync(chunk_raw_out_dev, chunk_raw_in_dev, 4ull * nchunks, hipMemcpyDeviceToDevice, st));
-  if (n_blocks == 0) return H3C_OK;
+  if (n_blocks == 0) {
+    HIP_TRY(hipMemcpyAsync(chunk_raw_out_dev, chunk_raw_in_dev, 4ull * nchunks, hipMemcpyDeviceToDevice, st));
+    if (n_invalid_dev) HIP_TRY(hipMemsetAsync(n_invalid_dev, 0, 4, st));
+    return H3C_OK;
+  }
   if (!blk_chunk_dev || !blk_index_dev || !payload_dev || !out_raw_dev || !workspace_dev)
     return H3C_ERR_INVALID_ARG;
   if (((uintptr_t)payload_dev & 15) != 0) return H3C_ERR_INVALID_ARG;
@@ -538,9 +561,13 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
   const uint32_t num_cu = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
   const uint32_t tb = 256, gb = (n_blocks + tb - 1) / tb;
 
-  HIP_TRY(hipMemsetAsync(w.err, 0, 4, st));
+  const bool tiles = use_tiles(n_blocks, nchunks);
+  if (!tiles) {  // sort path: chunks without writes keep raw_in; invalid entries counted atomically
+    HIP_TRY(hipMemcpyAsync(chunk_raw_out_dev, chunk_raw_in_dev, 4ull * nchunks, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemsetAsync(w.err, 0, 4, st));
+  }
   hipLaunchKernelGGL(upd_keys_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks, bpc,
-                     w.kslot, w.kchunk, w.iota, w.err);
+                     w.kslot, tiles ? nullptr : w.kchunk, w.iota, tiles ? nullptr : w.err);
   HIP_TRY(hipGetLastError());
   // Stable radix sorts of (key, sequence index) over only the key's bits: by slot
   // (chunk, block) for the previous-writer links, by chunk for the per-chunk scan.
@@ -562,13 +589,13 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
   // algorithmic bytes: read new + read old + write back, per block write
   HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDATE, 3ull * block_bytes * n_blocks));
   const uint32_t poly = type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
-  if (use_tiles(n_blocks, nchunks)) {
+  if (tiles) {
     const uint32_t ntiles = (n_blocks + kTile - 1) / kTile;
     hipLaunchKernelGGL(upd_tile_kernel, dim3(ntiles), dim3(kTile), 0, st, blk_chunk_dev, blk_index_dev, n_blocks,
-                       nchunks, bpc, w.delta, sh, poly, w.scan, w.agg);
+                       nchunks, bpc, w.delta, sh, poly, w.scan, w.agg, w.tile_invalid);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(upd_column_kernel, dim3(nchunks), dim3(kTile), 0, st, w.agg, ntiles, nchunks, chunk_raw_in_dev,
-                       w.colpre, chunk_raw_out_dev);
+                       w.colpre, chunk_raw_out_dev, w.tile_invalid, n_invalid_dev);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(upd_apply_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks,
                        bpc, chunk_raw_in_dev, w.colpre, w.scan, out_raw_dev);
@@ -586,8 +613,8 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
     hipLaunchKernelGGL(upd_scatter_kernel, dim3(gb), dim3(tb), 0, st, w.kchunk_s, w.idx2, n_blocks, nchunks, w.scan,
                        chunk_raw_in_dev, out_raw_dev, chunk_raw_out_dev);
     HIP_TRY(hipGetLastError());
+    if (n_invalid_dev) HIP_TRY(hipMemcpyAsync(n_invalid_dev, w.err, 4, hipMemcpyDeviceToDevice, st));
   }
-  if (n_invalid_dev) HIP_TRY(hipMemcpyAsync(n_invalid_dev, w.err, 4, hipMemcpyDeviceToDevice, st));
   return H3C_OK;
 }
 
