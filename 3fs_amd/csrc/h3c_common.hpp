@@ -76,6 +76,8 @@ struct DevChunk {
   uint32_t out_idx;
   uint32_t seg_begin;
   uint32_t flags;  // bit0: result is {NONE,0}
+  uint32_t xlen;   // x^(8*len): applies `start` (set_fold_consts)
+  uint32_t xlast;  // x^(8*r), r = the last segment's length: folds the segments
 };
 constexpr uint32_t kFlagNone = 1u;
 
@@ -133,6 +135,22 @@ uint32_t hgf_pow(uint32_t base, uint64_t e, uint32_t poly) {
 
 uint32_t hxpow8n(uint64_t n, uint32_t poly) { return hgf_pow(0x00800000u /* x^8 */, n, poly); }
 
+// x^(8n) with a small per-thread memo (batches repeat a few chunk lengths).
+uint32_t hxpow8n_memo(uint64_t n, uint32_t poly) {
+  struct Entry {
+    uint64_t n;
+    uint32_t poly, v;
+  };
+  thread_local Entry memo[64] = {};
+  thread_local bool used[64] = {};
+  const uint32_t h = (uint32_t)((n * 0x9E3779B97F4A7C15ull) >> 58) ^ (poly & 63u);
+  Entry &e = memo[h & 63];
+  if (used[h & 63] && e.n == n && e.poly == poly) return e.v;
+  e = Entry{n, poly, hxpow8n(n, poly)};
+  used[h & 63] = true;
+  return e.v;
+}
+
 // x^-1: the y with y*x == 1.  Multiplying by x is y>>1 ^ (poly if y&1); the
 // result is x^0 (bit 31) only when y&1 and (y>>1)^poly == 1<<31.
 uint32_t hx_inverse(uint32_t poly) { return ((poly ^ kOne) << 1) | 1u; }
@@ -180,6 +198,14 @@ inline void build_consts(PolyConsts &pc, uint32_t poly) {
 
 using h3c_rt::DevChunk;
 using h3c_rt::kFlagNone;
+
+// The finalize kernels' per-chunk shift constants, computed on the host once per
+// distinct length instead of ~26 bit-serial GF(2) multiplies per chunk on the device.
+inline void set_fold_consts(DevChunk &c, uint64_t seg_bytes, uint32_t poly) {
+  c.xlen = hxpow8n_memo(c.len, poly);
+  const uint64_t m = (c.len + seg_bytes - 1) / seg_bytes;
+  c.xlast = m ? hxpow8n_memo(c.len - (m - 1) * seg_bytes, poly) : kOne;
+}
 
 // ---------------------------------------------------------------- device GF(2)
 __device__ __forceinline__ uint32_t dgf_mul(uint32_t a, uint32_t b, uint32_t poly) {
@@ -346,19 +372,63 @@ __device__ __forceinline__ void consume(Streams &st, uint4 v, const char *lb, co
   st.s3 = row_step(st.s3 ^ v.w, lb, L);
 }
 
+// a * C for the constant whose byte tables start at `t` (4 x 256 dwords in LDS).
+__device__ __forceinline__ uint32_t tab_mul(uint32_t a, const uint32_t *t) {
+  return xor3(t[a & 255u], t[256u + ((a >> 8) & 255u)], t[512u + ((a >> 16) & 255u)]) ^ t[768u + (a >> 24)];
+}
+
+// Fold a wave's 256 stream states into the init-0 CRC of the rows they walked:
+//   acc = XOR_{l,j} s(l,j) * x^-(8*(16l+4j))
+// (stream (l,j) ended 16l+4j bytes past the 16-byte-rounded end).  Instead of 4 general
+// GF(2) multiplies by per-lane constants (~200 VALU ops each), every multiply here is by
+// one of 7 wave-uniform constants via byte tables in LDS (`red` = the 7168 dwords laid out
+// as PolyConsts::red): a Horner pass over the lane's 4 streams with x^-32, then a 6-level
+// shuffle tree whose level k folds lane l+2^k into lane l with x^-(128*2^k).  Lanes that
+// no longer carry a partial sum skip the lookups (fewer LDS bank conflicts).  The result
+// is valid in lane 0 only.
+__device__ __forceinline__ uint32_t wave_fold_tab(const Streams &st, uint32_t lane, const uint32_t *red) {
+  uint32_t v = tab_mul(st.s3, red) ^ st.s2;
+  v = tab_mul(v, red) ^ st.s1;
+  v = tab_mul(v, red) ^ st.s0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const uint32_t o = __shfl_down(v, 1u << k, 64);
+    if ((lane & ((2u << k) - 1u)) == 0) v ^= tab_mul(o, red + 1024 * (k + 1));
+  }
+  return v;
+}
+
+
 #ifndef H3C_UNROLL
 #define H3C_UNROLL 4
 #endif
 constexpr int kUnroll = H3C_UNROLL;  // rows in flight per batch (x2 with the prefetch)
 
-// init-0 CRC of bytes [S, E) (E > S), computed by one wavefront.
+#ifndef H3C_SEG_ABS_ROWS
+#define H3C_SEG_ABS_ROWS 1  // rows on absolute 1 KiB boundaries (else: ending at the segment end)
+#endif
+#ifndef H3C_SEG_FOLD_TAB
+#define H3C_SEG_FOLD_TAB 1  // table-driven wave fold (else: 4 bit-serial GF(2) multiplies per lane)
+#endif
+
+// init-0 CRC of bytes [S, E) (E > S), computed by one wavefront; valid in lane 0.
+// The rows are the 1 KiB blocks [A, B) of absolute addresses covering [S, E), so every
+// row load is 8 whole 128-byte lines whatever the payload's alignment; the first and
+// last rows are masked (bytes outside [S, E) read as zero and pieces with no payload
+// byte are never dereferenced).  Leading zeros do not change an init-0 CRC; the
+// B - E trailing zeros are removed at the end with one multiply by x^-(8(B-E)).
 __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const char *lb, const LaneLut &L,
-                                 const uint32_t fix[4], const PolyConsts *__restrict__ pc,
-                                 uint32_t poly, uint32_t dbg) {
-  const uint64_t E16 = (E + 15) & ~uint64_t(15);
-  const uint64_t S16 = S & ~uint64_t(15);
-  const uint32_t K = (uint32_t)((E16 - S16 + kRowBytes - 1) / kRowBytes);
-  const uint64_t base = E16 - (uint64_t)K * kRowBytes + 16u * lane;
+                                        const uint32_t fix[4], const uint32_t *red,
+                                        const PolyConsts *__restrict__ pc, uint32_t poly, uint32_t dbg) {
+#if H3C_SEG_ABS_ROWS
+  const uint64_t A = S & ~uint64_t(kRowBytes - 1);
+  const uint64_t B = (E + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
+#else
+  const uint64_t B = (E + 15) & ~uint64_t(15);
+  const uint64_t A = B - ((B - (S & ~uint64_t(15)) + kRowBytes - 1) / kRowBytes) * kRowBytes;
+#endif
+  const uint32_t K = (uint32_t)((B - A) / kRowBytes);
+  const uint64_t base = A + 16u * lane;
 
   Streams st{0, 0, 0, 0};
   // row 0 (masked)
@@ -373,9 +443,8 @@ __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, c
   const uint32_t plain_end = K >= 2 ? K - 1 : 1;
   if (!(dbg & 1u) && r + kUnroll <= plain_end) {
     // readfirstlane returns int: widen through uint32_t so the low half is not sign-extended.
-    const uint64_t row0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base - 16u * lane)) |
-                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((base - 16u * lane) >> 32))
-                           << 32);
+    const uint64_t row0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)A) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(A >> 32)) << 32);
     typedef const char __attribute__((address_space(1))) *gcp;
     const gcp gbase = (gcp)row0;
     const uint32_t voff = 16u * lane;
@@ -418,44 +487,26 @@ __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, c
   // row K-1 (masked)
   if (K >= 2) consume(st, load_masked(base + (uint64_t)(K - 1) * kRowBytes, S, E), lb, L);
 
-  // Move every stream back to the 16-byte-rounded end, then to the true end.
-  // The per-lane constants are made opaque here so the compiler does not hoist
-  // 4 x 32 shifted copies of them out of the segment loop (that spills).
+  // Move every stream back to B (stream (l, j) ends 16l + 4j bytes past it).
+#if H3C_SEG_FOLD_TAB
+  (void)fix;
+  uint32_t acc = wave_fold_tab(st, lane, red);
+#else
+  (void)red;
+  // The per-lane constants are made opaque so the compiler does not hoist 4 x 32
+  // shifted copies of them out of the segment loop (that spills).
   uint32_t f0 = fix[0], f1 = fix[1], f2 = fix[2], f3 = fix[3];
   asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
   uint32_t acc = dgf_mul(f0, st.s0, poly) ^ dgf_mul(f1, st.s1, poly) ^ dgf_mul(f2, st.s2, poly) ^
                  dgf_mul(f3, st.s3, poly);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
-  const uint32_t z = (uint32_t)(E16 - E);
-  if (z) acc = dgf_mul(acc, pc->fixz[z], poly);
+#endif
+  // ... then drop the B - E trailing zeros: x^-(8*pad) = x^-(8*16*(pad>>4)) * x^-(8*(pad&15))
+  const uint32_t pad = (uint32_t)(B - E);
+  if (pad >> 4) acc = dgf_mul(acc, pc->fix[4 * (pad >> 4)], poly);
+  if (pad & 15) acc = dgf_mul(acc, pc->fixz[pad & 15], poly);
   return acc;
-}
-
-// a * C for the constant whose byte tables start at `t` (4 x 256 dwords in LDS).
-__device__ __forceinline__ uint32_t tab_mul(uint32_t a, const uint32_t *t) {
-  return xor3(t[a & 255u], t[256u + ((a >> 8) & 255u)], t[512u + ((a >> 16) & 255u)]) ^ t[768u + (a >> 24)];
-}
-
-// Fold a wave's 256 stream states into the init-0 CRC of the rows they walked:
-//   acc = XOR_{l,j} s(l,j) * x^-(8*(16l+4j))
-// (stream (l,j) ended 16l+4j bytes past the 16-byte-rounded end).  Instead of 4 general
-// GF(2) multiplies by per-lane constants (~200 VALU ops each), every multiply here is by
-// one of 7 wave-uniform constants via byte tables in LDS (`red` = the 7168 dwords laid out
-// as PolyConsts::red): a Horner pass over the lane's 4 streams with x^-32, then a 6-level
-// shuffle tree whose level k folds lane l+2^k into lane l with x^-(128*2^k).  Lanes that
-// no longer carry a partial sum skip the lookups (fewer LDS bank conflicts).  The result
-// is valid in lane 0 only.
-__device__ __forceinline__ uint32_t wave_fold_tab(const Streams &st, uint32_t lane, const uint32_t *red) {
-  uint32_t v = tab_mul(st.s3, red) ^ st.s2;
-  v = tab_mul(v, red) ^ st.s1;
-  v = tab_mul(v, red) ^ st.s0;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const uint32_t o = __shfl_down(v, 1u << k, 64);
-    if ((lane & ((2u << k) - 1u)) == 0) v ^= tab_mul(o, red + 1024 * (k + 1));
-  }
-  return v;
 }
 
 }  // namespace

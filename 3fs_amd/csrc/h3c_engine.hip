@@ -48,9 +48,14 @@ __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__res
                                                            uint32_t total_segs, uint64_t seg_bytes, uint32_t dbg,
                                                            const PolyConsts *__restrict__ pc,
                                                            uint32_t *__restrict__ seg_crc) {
-  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint32_t lds[kLdsWords + (H3C_SEG_FOLD_TAB ? kRedWords : 0)];
   for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
+#if H3C_SEG_FOLD_TAB
+  const uint32_t *red_g = &pc->red[0][0][0];
+  for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
+#endif
   __syncthreads();
+  const uint32_t *red = lds + kLdsWords;
 
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -81,7 +86,7 @@ __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__res
     const uint64_t len = chunks[c].len;
     const uint64_t S = p + k * seg_bytes;
     const uint64_t E = p + min(len, (k + 1) * seg_bytes);
-    const uint32_t v = segment_crc0(S, E, lane, lb, L, fix, pc, poly, dbg);
+    const uint32_t v = segment_crc0(S, E, lane, lb, L, fix, red, pc, poly, dbg);
     if (lane == 0) seg_crc[s] = v;
   }
 }
@@ -102,16 +107,28 @@ __device__ __forceinline__ void finalize_store(const DevChunk &ch, uint32_t raw,
   }
 }
 
+// Byte tables of the multiply by X = x^(8*seg_bytes) (the fold of full segments), built
+// per workgroup in LDS: tab_mul(h, T) = h * X with 4 lookups instead of a ~200-op
+// bit-serial multiply.
+__device__ __forceinline__ void build_seg_table(uint32_t *T, uint32_t seg_mul, uint32_t poly) {
+  for (uint32_t k = threadIdx.x; k < 1024; k += blockDim.x) T[k] = dgf_mul((k & 255u) << (8 * (k >> 8)), seg_mul, poly);
+  __syncthreads();
+}
+
 // Kernel B: per chunk (one thread), fold segment CRCs, apply start, optionally compare.
-__global__ void finalize_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks, uint32_t total_segs,
-                                uint64_t seg_bytes, uint32_t seg_mul, const PolyConsts *__restrict__ pc,
-                                const uint32_t *__restrict__ seg_crc, const uint32_t *__restrict__ expected,
-                                uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
-                                uint32_t *__restrict__ mismatch) {
+__global__ __launch_bounds__(256) void finalize_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+                                                       uint32_t total_segs, uint32_t seg_mul,
+                                                       const PolyConsts *__restrict__ pc,
+                                                       const uint32_t *__restrict__ seg_crc,
+                                                       const uint32_t *__restrict__ expected,
+                                                       uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                                       uint32_t *__restrict__ mismatch) {
+  __shared__ uint32_t T[1024];
+  const uint32_t poly = pc->poly;
+  build_seg_table(T, seg_mul, poly);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nchunks) return;
   const DevChunk ch = chunks[i];
-  const uint32_t poly = pc->poly;
   uint32_t raw = 0;
   if (!(ch.flags & kFlagNone)) {
     const uint32_t b = ch.seg_begin;
@@ -120,26 +137,28 @@ __global__ void finalize_kernel(const DevChunk *__restrict__ chunks, uint32_t nc
     uint32_t crc0 = 0;
     if (e > b) {
       crc0 = seg_crc[b];
-      for (uint32_t s = b + 1; s < e; ++s) {
-        const uint64_t seg_len = min<uint64_t>(seg_bytes, ch.len - (uint64_t)(s - b) * seg_bytes);
-        const uint32_t m = seg_len == seg_bytes ? seg_mul : dxpow8n(seg_len, pc, poly);
-        crc0 = dgf_mul(crc0, m, poly) ^ seg_crc[s];
-      }
+      for (uint32_t s = b + 1; s + 1 < e; ++s) crc0 = tab_mul(crc0, T) ^ seg_crc[s];  // full segments
+      if (e - b >= 2) crc0 = dgf_mul(crc0, ch.xlast, poly) ^ seg_crc[e - 1];          // the last one
     }
-    raw = crc0 ^ (ch.len ? dgf_mul(ch.start, dxpow8n(ch.len, pc, poly), poly) : ch.start);
+    raw = crc0 ^ (ch.start ? dgf_mul(ch.start, ch.xlen, poly) : 0u);
   }
   finalize_store(ch, raw, expected, out_raw, ok, mismatch);
 }
 
-// Kernel B': one wave per chunk with > kSmallFold segments.  The segment CRCs are the
-// coefficients of a polynomial in X = x^(8*seg_bytes) (all but the last segment are
-// full): lane j Horner-evaluates q consecutive coefficients (virtual zeros in front
-// are harmless), then six butterfly levels combine lane results with X^(q*2^t).
-__global__ void finalize_big_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks, uint32_t total_segs,
-                                    uint64_t seg_bytes, uint32_t seg_mul, const PolyConsts *__restrict__ pc,
-                                    const uint32_t *__restrict__ seg_crc, const uint32_t *__restrict__ expected,
-                                    uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
-                                    uint32_t *__restrict__ mismatch) {
+// Kernel B': one wave per chunk with > kSmallFold segments.  The full segments' CRCs are
+// the coefficients of a polynomial in X = x^(8*seg_bytes): lane j Horner-evaluates q
+// consecutive coefficients (virtual zeros in front are harmless), then six butterfly
+// levels combine lane results with X^(q*2^t); the last segment joins with x^(8r).
+__global__ __launch_bounds__(256) void finalize_big_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+                                                           uint32_t total_segs, uint64_t seg_bytes, uint32_t seg_mul,
+                                                           const PolyConsts *__restrict__ pc,
+                                                           const uint32_t *__restrict__ seg_crc,
+                                                           const uint32_t *__restrict__ expected,
+                                                           uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                                           uint32_t *__restrict__ mismatch) {
+  __shared__ uint32_t T[1024];
+  const uint32_t poly = pc->poly;
+  build_seg_table(T, seg_mul, poly);
   const uint32_t i = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const uint32_t j = threadIdx.x & 63;
   if (i >= nchunks) return;
@@ -149,13 +168,12 @@ __global__ void finalize_big_kernel(const DevChunk *__restrict__ chunks, uint32_
   const uint32_t e = (i + 1 < nchunks) ? chunks[i + 1].seg_begin : total_segs;
   const uint32_t m = e - b;
   if (m <= kSmallFold) return;
-  const uint32_t poly = pc->poly;
   const uint32_t q = (m - 1 + 63) / 64;
   const int64_t k0 = (int64_t)(m - 1) - (int64_t)(64 - j) * q;
   uint32_t h = 0;
   for (uint32_t t = 0; t < q; ++t) {
     const int64_t k = k0 + t;
-    h = dgf_mul(h, seg_mul, poly) ^ (k >= 0 ? seg_crc[b + (uint32_t)k] : 0u);
+    h = tab_mul(h, T) ^ (k >= 0 ? seg_crc[b + (uint32_t)k] : 0u);
   }
   uint32_t Y = dxpow8n((uint64_t)q * seg_bytes, pc, poly);
 #pragma unroll
@@ -165,9 +183,8 @@ __global__ void finalize_big_kernel(const DevChunk *__restrict__ chunks, uint32_
     Y = dgf_mul(Y, Y, poly);
   }
   if (j == 0) {
-    const uint64_t r = ch.len - (uint64_t)(m - 1) * seg_bytes;  // last segment's length
-    const uint32_t crc0 = dgf_mul(h, dxpow8n(r, pc, poly), poly) ^ seg_crc[b + m - 1];
-    const uint32_t raw = crc0 ^ dgf_mul(ch.start, dxpow8n(ch.len, pc, poly), poly);
+    const uint32_t crc0 = dgf_mul(h, ch.xlast, poly) ^ seg_crc[b + m - 1];
+    const uint32_t raw = crc0 ^ (ch.start ? dgf_mul(ch.start, ch.xlen, poly) : 0u);
     finalize_store(ch, raw, expected, out_raw, ok, mismatch);
   }
 }
@@ -395,7 +412,7 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
   }
   const uint32_t seg_mul = hxpow8n(seg_bytes, poly);
   const uint32_t fb = (nchunks + 255) / 256;
-  hipLaunchKernelGGL(finalize_kernel, dim3(fb), dim3(256), 0, st, d_chunks, nchunks, total_segs, seg_bytes, seg_mul, pc,
+  hipLaunchKernelGGL(finalize_kernel, dim3(fb), dim3(256), 0, st, d_chunks, nchunks, total_segs, seg_mul, pc,
                      d_segcrc, expected, out_raw, ok, mismatch);
   HIP_TRY(hipGetLastError());
   if (max_chunk_segs > kSmallFold) {
@@ -428,12 +445,40 @@ struct Group {
 };
 
 uint64_t pick_seg_bytes(uint64_t total_bytes, int num_cu) {
-  // Aim for >= 2 segments per wave slot on the chip, within [16 KiB, 1 MiB].
-  const uint64_t slots = (uint64_t)std::max(num_cu, 1) * kWavesPerBlock * 2;
+  // Without the chunk lengths: aim for >= 8 segments per wave slot, within [16 KiB, 1 MiB].
+  const uint64_t slots = (uint64_t)std::max(num_cu, 1) * kWavesPerBlock * 8;
   uint64_t want = total_bytes / slots;
   uint64_t seg = kMaxSegBytes;
   while (seg > kMinSegBytes && seg > want) seg >>= 1;
   return seg;
+}
+
+// With the chunk lengths: waves take contiguous segment ranges by count, so the
+// slowest wave carries ceil(S / waves) segments.  Take the largest power of two in
+// [16 KiB, 1 MiB] whose balance total / (waves * ceil(S / waves) * seg) is >= 97 %
+// (larger segments mean fewer per-segment pipeline drains): 1 MiB for 8192 x 1 MiB
+// chunks (exactly 2 per wave), 256 KiB for a mixed 64 KiB-64 MiB batch (with 1 MiB
+// segments some waves got a third one: 6.2 vs 6.7 TB/s).
+uint64_t pick_seg_for(const h3c_desc *d, size_t n, int num_cu) {
+  const uint64_t waves = (uint64_t)std::max(num_cu, 1) * kWavesPerBlock;
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i)
+    if ((d[i].type == H3C_TYPE_CRC32C || d[i].type == H3C_TYPE_CRC32) && d[i].ptr) total += d[i].len;
+  if (total == 0) return kMinSegBytes;
+  uint64_t best = kMinSegBytes;
+  double best_eff = -1;
+  for (uint64_t seg = kMaxSegBytes; seg >= kMinSegBytes; seg >>= 1) {
+    uint64_t segs = 0;
+    for (size_t i = 0; i < n; ++i)
+      if ((d[i].type == H3C_TYPE_CRC32C || d[i].type == H3C_TYPE_CRC32) && d[i].ptr) segs += (d[i].len + seg - 1) / seg;
+    const double eff = (double)total / ((double)waves * (double)((segs + waves - 1) / waves) * (double)seg);
+    if (eff >= 0.97) return seg;
+    if (eff > best_eff) {
+      best_eff = eff;
+      best = seg;
+    }
+  }
+  return best;
 }
 
 }  // namespace
@@ -472,6 +517,7 @@ int layout_groups(const h3c_desc *d, size_t n, uint64_t seg_bytes, GroupLayout &
       }
       g.segs[k] += (uint32_t)ns;
       g.max_segs[k] = std::max(g.max_segs[k], (uint32_t)ns);
+      set_fold_consts(c, seg_bytes, k ? kPolyCrc32 : kPolyCrc32c);
       g.bytes[k] += x.len;
     }
     g.hc[k].push_back(c);
@@ -552,7 +598,7 @@ int h3c_plan_create(const h3c_desc *d, size_t n, int device, h3c_plan **out) {
   uint64_t total = 0;
   for (size_t i = 0; i < n; ++i)
     if ((d[i].type == H3C_TYPE_CRC32C || d[i].type == H3C_TYPE_CRC32) && d[i].ptr) total += d[i].len;
-  p->seg_bytes = pick_seg_bytes(total, g_dev[device].num_cu);
+  p->seg_bytes = pick_seg_for(d, n, g_dev[device].num_cu);
   p->dbg = read_dbg_flags();
   if (const char *e = std::getenv("H3C_SEG_BYTES")) {  // test hook: force the segment size
     const uint64_t v = std::strtoull(e, nullptr, 0);
@@ -657,13 +703,12 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 
   std::vector<h3c_desc> dd(d, d + n);
-  uint64_t host_bytes = 0, total = 0;
+  uint64_t host_bytes = 0;
   for (auto &x : dd) {
     const bool crc = x.ptr && x.len && (x.type == H3C_TYPE_CRC32C || x.type == H3C_TYPE_CRC32);
     if (crc && x.mem != H3C_MEM_DEVICE) host_bytes += (x.len + 255) & ~uint64_t(255);
-    if (crc) total += x.len;
   }
-  uint64_t seg_bytes = pick_seg_bytes(total, g_dev[dev].num_cu);
+  uint64_t seg_bytes = pick_seg_for(d, n, g_dev[dev].num_cu);
   if (const char *e = std::getenv("H3C_SEG_BYTES")) {  // test hook: force the segment size
     const uint64_t v = std::strtoull(e, nullptr, 0);
     if (v >= kRowBytes && v % kRowBytes == 0) seg_bytes = v;

@@ -234,6 +234,7 @@ int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t 
     for (uint32_t p = win.piece_begin; p < win.piece_end; ++p) {
       pieces[p].seg_begin = segs;
       pieces[p].ptr += (uint64_t)(uintptr_t)h->stage[wi & 1];
+      set_fold_consts(pieces[p], seg_bytes, type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c);
       const uint32_t ns = (uint32_t)((pieces[p].len + seg_bytes - 1) / seg_bytes);
       segs += ns;
       mx = std::max(mx, ns);

@@ -169,13 +169,15 @@ struct CrcBatch {
   uint64_t bytes = 0;
 };
 
-void add_job(CrcBatch &b, uint64_t ptr, uint64_t len, uint32_t start, uint32_t out_idx, uint64_t seg_bytes) {
+void add_job(CrcBatch &b, uint64_t ptr, uint64_t len, uint32_t start, uint32_t out_idx, uint64_t seg_bytes,
+             uint32_t poly) {
   DevChunk c{};
   c.ptr = ptr;
   c.len = len;
   c.start = start;
   c.out_idx = out_idx;
   c.seg_begin = b.total_segs;
+  set_fold_consts(c, seg_bytes, poly);
   const uint32_t ns = (uint32_t)((len + seg_bytes - 1) / seg_bytes);
   b.total_segs += ns;
   b.max_segs = std::max(b.max_segs, ns);
@@ -308,7 +310,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   CrcBatch pay;
   for (uint32_t i = 0; i < n; ++i)
     if (status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
-      add_job(pay, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg_a);
+      add_job(pay, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg_a, poly);
   if (!pay.chunks.empty()) {
     Arena a;
     const size_t nc = pay.chunks.size();
@@ -414,7 +416,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
         raw0[c] = std_domain ? ~cs.value : cs.value;
       } else {
         const uint32_t e = epoch_for(c, 0, cs.size);
-        add_job(ep_crc[e], base, cs.size, 0u, njobs, seg_j);
+        add_job(ep_crc[e], base, cs.size, 0u, njobs, seg_j, poly);
         AffIn a{};
         a.kind = kAffInit;
         a.len = cs.size;
@@ -433,7 +435,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
       const uint32_t e = epoch_for(c, std::min(o, nb), (o > nb || len) ? o + len : 0);
       if (o < nb && len) {
         const uint64_t end = std::min(o + len, nb);
-        add_job(ep_crc[e], base + o, end - o, 0u, njobs, seg_j);
+        add_job(ep_crc[e], base + o, end - o, 0u, njobs, seg_j, poly);
         a.job = njobs++;
         a.pad = o + len - end;
       }
@@ -449,7 +451,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
       if (l < nb && io.kind == H3C_UPD_TRUNCATE) {
         na = l;
         const uint32_t e = epoch_for(c, l, nb);
-        add_job(ep_crc[e], base + l, nb - l, 0u, njobs, seg_j);
+        add_job(ep_crc[e], base + l, nb - l, 0u, njobs, seg_j, poly);
         a.kind = kAffTrunc;
         a.job = njobs++;
       } else if (l > nb) {
