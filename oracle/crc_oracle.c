@@ -147,6 +147,107 @@ uint32_t orc_crc32c_sse42_3way(const uint8_t *d, size_t n, uint32_t start) {
 }
 
 /* ------------------------------------------------------------------ */
+/* Best-case CPU (not the reference's path): carry-less-multiply folding */
+/* with AVX-512 VPCLMULQDQ (16 x 128-bit accumulators, 256 B per step),  */
+/* reduced to 32 bits with two crc32q.  The accumulator holds a virtual  */
+/* 16-byte message: loaded little-endian, integer bit q <-> x^(127-q).   */
+/* A 64-bit clmul of two such bit-reversed operands yields the product   */
+/* times x, so folding X = Xh*x^64 + Xl forward by F bits uses           */
+/* Xh * x^(F+63) and Xl * x^(F-1) (each constant reversed into the top   */
+/* half of a 64-bit lane).  Constants are derived with orc_gf_mul.       */
+/* ------------------------------------------------------------------ */
+#include <immintrin.h>
+
+static uint32_t xpow_bits(uint64_t k) { /* x^k mod P (CRC32C), reflected */
+  uint32_t r = 0x80000000u, b = 0x40000000u;
+  while (k) {
+    if (k & 1u) r = orc_gf_mul(r, b, ORC_POLY_CRC32C);
+    b = orc_gf_mul(b, b, ORC_POLY_CRC32C);
+    k >>= 1;
+  }
+  return r;
+}
+static uint64_t g_fold[8][2]; /* [0] 2048, [1] 1536, [2] 1024, [3] 512, [4] 384, [5] 256, [6] 128 bits */
+static pthread_once_t g_fold_once = PTHREAD_ONCE_INIT;
+static void init_fold(void) {
+  static const uint64_t F[7] = {2048, 1536, 1024, 512, 384, 256, 128};
+  for (int i = 0; i < 7; ++i) {
+    g_fold[i][0] = (uint64_t)xpow_bits(F[i] + 63) << 32; /* multiplies the low qword (high degrees) */
+    g_fold[i][1] = (uint64_t)xpow_bits(F[i] - 1) << 32;  /* multiplies the high qword */
+  }
+}
+
+__attribute__((target("pclmul,sse4.2"))) static inline __m128i fold128(__m128i x, int f, __m128i d) {
+  const __m128i k = _mm_set_epi64x((long long)g_fold[f][1], (long long)g_fold[f][0]);
+  return _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(x, k, 0x00), _mm_clmulepi64_si128(x, k, 0x11)), d);
+}
+
+__attribute__((target("avx512f,avx512vl,vpclmulqdq,pclmul,sse4.2"))) static uint32_t crc32c_vpclmul(
+    const uint8_t *d, size_t n, uint32_t start) {
+  uint64_t c = start;
+  if (n < 512) {
+    for (; n >= 8; n -= 8, d += 8) {
+      uint64_t w;
+      memcpy(&w, d, 8);
+      c = _mm_crc32_u64(c, w);
+    }
+    while (n--) c = _mm_crc32_u8((uint32_t)c, *d++);
+    return (uint32_t)c;
+  }
+  pthread_once(&g_fold_once, init_fold);
+  __m512i x0 = _mm512_loadu_si512((const void *)d), x1 = _mm512_loadu_si512((const void *)(d + 64));
+  __m512i x2 = _mm512_loadu_si512((const void *)(d + 128)), x3 = _mm512_loadu_si512((const void *)(d + 192));
+  x0 = _mm512_xor_si512(x0, _mm512_zextsi128_si512(_mm_cvtsi32_si128((int)start)));
+  d += 256;
+  n -= 256;
+  const __m512i k2048 = _mm512_broadcast_i32x4(_mm_set_epi64x((long long)g_fold[0][1], (long long)g_fold[0][0]));
+#define FOLD512(x, k, v) _mm512_ternarylogic_epi64(_mm512_clmulepi64_epi128(x, k, 0x00), \
+                                                   _mm512_clmulepi64_epi128(x, k, 0x11), v, 0x96)
+  while (n >= 256) {
+    x0 = FOLD512(x0, k2048, _mm512_loadu_si512((const void *)d));
+    x1 = FOLD512(x1, k2048, _mm512_loadu_si512((const void *)(d + 64)));
+    x2 = FOLD512(x2, k2048, _mm512_loadu_si512((const void *)(d + 128)));
+    x3 = FOLD512(x3, k2048, _mm512_loadu_si512((const void *)(d + 192)));
+    d += 256;
+    n -= 256;
+  }
+  /* 4 zmm -> 1: x0 by 1536 bits, x1 by 1024, x2 by 512, onto x3 */
+  const __m512i k1536 = _mm512_broadcast_i32x4(_mm_set_epi64x((long long)g_fold[1][1], (long long)g_fold[1][0]));
+  const __m512i k1024 = _mm512_broadcast_i32x4(_mm_set_epi64x((long long)g_fold[2][1], (long long)g_fold[2][0]));
+  const __m512i k512 = _mm512_broadcast_i32x4(_mm_set_epi64x((long long)g_fold[3][1], (long long)g_fold[3][0]));
+  __m512i a = FOLD512(x0, k1536, x3);
+  a = FOLD512(x1, k1024, a);
+  a = FOLD512(x2, k512, a);
+#undef FOLD512
+  /* 4 lanes -> 1: lane 0 by 384 bits, lane 1 by 256, lane 2 by 128, onto lane 3 */
+  __m128i r = _mm512_extracti32x4_epi32(a, 3);
+  r = fold128(_mm512_extracti32x4_epi32(a, 0), 4, r);
+  r = fold128(_mm512_extracti32x4_epi32(a, 1), 5, r);
+  r = fold128(_mm512_extracti32x4_epi32(a, 2), 6, r);
+  for (; n >= 16; n -= 16, d += 16) r = fold128(r, 6, _mm_loadu_si128((const __m128i *)d));
+  /* the accumulator is a 16-byte message: its CRC (init 0), then the tail */
+  c = _mm_crc32_u64(0, (uint64_t)_mm_cvtsi128_si64(r));
+  c = _mm_crc32_u64(c, (uint64_t)_mm_extract_epi64(r, 1));
+  for (; n >= 8; n -= 8, d += 8) {
+    uint64_t w;
+    memcpy(&w, d, 8);
+    c = _mm_crc32_u64(c, w);
+  }
+  while (n--) c = _mm_crc32_u8((uint32_t)c, *d++);
+  return (uint32_t)c;
+}
+
+int orc_has_vpclmul(void) {
+  __builtin_cpu_init();
+  return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("vpclmulqdq");
+}
+
+uint32_t orc_crc32c_vpclmul(const uint8_t *d, size_t n, uint32_t start) {
+  if (!orc_has_vpclmul()) return orc_crc32c_sse42_3way(d, n, start);
+  return crc32c_vpclmul(d, n, start);
+}
+
+/* ------------------------------------------------------------------ */
 /* A2: GF(2)[x]/P arithmetic in the reflected representation.          */
 /* bit 31 holds the x^0 coefficient; multiplying by x is a right shift */
 /* with conditional reduction by the reflected polynomial.             */
@@ -403,7 +504,7 @@ void orc_fill_splitmix(uint8_t *out, uint64_t len, uint64_t seed, uint64_t chunk
 /* ------------------------------------------------------------------ */
 /* Batch helper (CPU baseline): equal-size chunks, optional threads.    */
 /* variant 0 = folly-faithful 3-way crc32q, 1 = single crc32q stream,   */
-/* 2 = byte table.  Each chunk goes through ChecksumInfo::create's 1 MiB */
+/* 2 = byte table, 3 = VPCLMULQDQ folding (best-case CPU).  Each chunk goes through ChecksumInfo::create's 1 MiB */
 /* iterator pieces, exactly as Common.h:146-172 chains folly::crc32c.    */
 /* ------------------------------------------------------------------ */
 typedef struct {
@@ -422,6 +523,8 @@ static uint32_t chunk_crc(const uint8_t *p, uint64_t len, uint32_t start, int va
       v = orc_crc32c_sse42_3way(p + off, piece, v);
     else if (variant == 1)
       v = orc_crc32c_sse42(p + off, piece, v);
+    else if (variant == 3)
+      v = orc_crc32c_vpclmul(p + off, piece, v);
     else
       v = orc_crc32c_table(p + off, piece, v);
   }

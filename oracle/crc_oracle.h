@@ -34,6 +34,10 @@ uint32_t orc_crc32c_sse42(const uint8_t *d, size_t n, uint32_t start);
  * This is the CPU baseline ("port" of folly's SSE4.2 crc32c_hw). */
 uint32_t orc_crc32c_sse42_3way(const uint8_t *d, size_t n, uint32_t start);
 uint32_t orc_crc32_table(const uint8_t *d, size_t n, uint32_t start);
+/* Best-case CPU (not the reference's path): AVX-512 VPCLMULQDQ folding + crc32q
+ * reduction; falls back to the 3-way path without AVX-512 / VPCLMULQDQ. */
+uint32_t orc_crc32c_vpclmul(const uint8_t *d, size_t n, uint32_t start);
+int orc_has_vpclmul(void);
 
 /* --- A2: GF(2) shift / combine --- */
 uint32_t orc_gf_mul(uint32_t a, uint32_t b, uint32_t poly);

@@ -207,3 +207,20 @@ def test_replica_update_restatement_relational_pin(seed):
         else:
             assert meta["value"] == orc.crc32c(model)
         assert (res["type"], res["value"]) == (meta["type"], meta["value"])
+
+
+def test_vpclmul_best_case_cpu_variant_matches():
+    """The best-case CPU variant (VPCLMULQDQ folding, not the reference's path) is bit-exact
+    with the table restatement at every length around its 512 B / 256 B / 16 B boundaries."""
+    import ctypes
+
+    L = orc.lib()
+    L.orc_crc32c_vpclmul.restype = ctypes.c_uint32
+    L.orc_crc32c_vpclmul.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32]
+    rng = np.random.default_rng(31)
+    sizes = list(range(0, 40)) + [255, 256, 257, 511, 512, 513, 767, 768, 1023, 1024, 1040, 4096 + 7,
+                                  (1 << 20) + 13]
+    for n in sizes:
+        a = rng.integers(0, 256, n, dtype=np.uint8)
+        for st in (0xFFFFFFFF, 0, 0xDEADBEEF):
+            assert L.orc_crc32c_vpclmul(a.ctypes.data if n else None, n, st) == orc.crc32c(a, st, mech="table")
