@@ -92,7 +92,7 @@ def cpu_baseline(gpu_raw_first: np.ndarray, chunk_len: int, seconds: float = 8.0
     gibps = reps * n * chunk_len / el / 2**30
     # context only (BASELINE.md "all-cores run"): the same restatement on every core this
     # process may use (the GPU box grants a share of the host, not all of nproc)
-    threads = max(1, min(len(os.sched_getaffinity(0)), 64))
+    threads = max(1, min(len(os.sched_getaffinity(0)), 16))  # the GPU box grants 16 CPUs per GPU
     reps_mt, t0 = 0, time.perf_counter()
     while True:
         L.orc_batch_crc32c(host.ctypes.data, chunk_len, n, 0xFFFFFFFF, threads, 0, out.ctypes.data)
