@@ -407,6 +407,12 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
         continue;
       }
     }
+    // TRUNCATE / EXTEND store a checksum of the chunk's own type (:328-332); one of the
+    // other polynomial cannot be derived from this batch's CRC state (documented limit).
+    if (io.kind != H3C_UPD_WRITE && !std_domain && t.type != H3C_TYPE_NONE && t.type != poly_type) {
+      status[i] = H3C_ERR_INVALID_ARG;
+      continue;
+    }
     if (!t.started) {  // the chunk's scan segment starts from a known CRC or an INIT reset
       t.started = true;
       const h3c_chunk_state &cs = chunks[c];

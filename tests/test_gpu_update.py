@@ -186,3 +186,32 @@ def test_update_config3_shape_full_size(h3c, torch_dev):
         last = np.nonzero(wc == c)[0][-1]
         assert int(got[last]) == int(fin[c])
     plan.close()
+
+
+def test_update_blocks_crc32_ieee(h3c, torch_dev):
+    """ChecksumType::CRC32 (IEEE polynomial, Common.h:161,195) through the block-update path:
+    the chunk checksum after every write equals crc32 of the whole chunk."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(12)
+    nchunks, chunk_len = 3, 64 << 10
+    bpc = chunk_len // G
+    chunks = rng.integers(0, 256, (nchunks, chunk_len), dtype=np.uint8)
+    raw0 = np.array([orc.crc32(chunks[c]) for c in range(nchunks)], dtype=np.uint32)
+    nw = 200
+    wc = rng.integers(0, nchunks, nw).astype(np.uint32)
+    wb = rng.integers(0, bpc, nw).astype(np.uint32)
+    pay = rng.integers(0, 256, (nw, G), dtype=np.uint8)
+    d = torch.from_numpy(chunks.copy()).to(dev)
+    bases = torch.tensor([d[c].data_ptr() for c in range(nchunks)], dtype=torch.int64, device=dev)
+    out = torch.zeros(nw, dtype=torch.int32, device=dev)
+    raw_out = torch.zeros(nchunks, dtype=torch.int32, device=dev)
+    h3c.update_blocks(bases, chunk_len, i32(raw0, torch, dev), i32(wc, torch, dev), i32(wb, torch, dev),
+                      torch.from_numpy(pay).to(dev), out, raw_out, type_=h3c.ChecksumType.CRC32)
+    torch.cuda.synchronize()
+    got = u32(out)
+    host = chunks.copy()
+    for k in range(nw):
+        c, b = int(wc[k]), int(wb[k])
+        host[c, b * G:(b + 1) * G] = pay[k]
+        assert int(got[k]) == orc.crc32(host[c]), k
+    assert np.array_equal(d.cpu().numpy(), host)

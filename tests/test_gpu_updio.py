@@ -26,7 +26,7 @@ def torch_dev():
 class Scenario:
     """Chunks in one HBM slab, payloads in another, and the oracle's host replica."""
 
-    def __init__(self, h3c, torch, dev, nchunks, chunk_size, rng, init="mixed"):
+    def __init__(self, h3c, torch, dev, nchunks, chunk_size, rng, init="mixed", empty_type=orc.CRC32C):
         self.h3c, self.torch, self.dev, self.rng = h3c, torch, dev, rng
         self.nchunks, self.chunk_size = nchunks, chunk_size
         self.host = np.zeros((nchunks, chunk_size), dtype=np.uint8)
@@ -40,7 +40,7 @@ class Scenario:
             elif kind == "none":
                 self.meta.append({"size": size, "type": orc.NONE, "value": 0})
             else:
-                self.meta.append({"size": 0, "type": orc.CRC32C, "value": 0})
+                self.meta.append({"size": 0, "type": empty_type, "value": 0})
         self.slab = torch.from_numpy(self.host.copy()).to(dev)
         self.init_meta = [dict(m) for m in self.meta]
         self.ops, self.payloads, self.expect = [], [], []
@@ -305,3 +305,57 @@ def test_updio_reference_write_patterns_golden(h3c, torch_dev):
     torch.cuda.synchronize()
     for i, (r, (sz, ck)) in enumerate(zip(res, want)):
         assert (int(r["status"]), int(r["size"]), int(r["type"]), int(r["value"])) == (0, sz, 1, ck), i
+
+
+def test_updio_crc32_ieee_polynomial(h3c, torch_dev):
+    """A CRC32 (IEEE) batch: the oracle's ChunkReplica::update replay with type CRC32."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(13)
+    cs = 48 << 10
+    sc = Scenario(h3c, torch, dev, 3, cs, rng, init="empty", empty_type=orc.CRC32)
+    for _ in range(150):
+        c = int(rng.integers(0, 3))
+        u = rng.random()
+        if u < 0.7:
+            off = int(rng.integers(0, cs))
+            sc.add(orc.UPD_WRITE, c, off, int(rng.integers(0, min(cs - off, 5000) + 1)), orc.CRC32)
+        elif u < 0.85:
+            sc.add(orc.UPD_TRUNCATE, c, 0, int(rng.integers(0, cs + 1)), orc.NONE)
+        else:
+            sc.add(orc.UPD_EXTEND, c, 0, int(rng.integers(0, cs + 1)), orc.NONE)
+    torch_, h = sc.torch, sc.h3c
+    # run with the CRC32 polynomial
+    offs, total = [], 0
+    for p in sc.payloads:
+        offs.append(total)
+        total += 0 if p is None else len(p)
+    pay = np.zeros(max(total, 1), dtype=np.uint8)
+    for o, p in zip(offs, sc.payloads):
+        if p is not None:
+            pay[o:o + len(p)] = p
+    dpay = torch_.from_numpy(pay).to(dev)
+    chunks = np.zeros(3, dtype=h.CHUNK_STATE_DTYPE)
+    for c, m in enumerate(sc.init_meta):
+        chunks[c] = (sc.slab.data_ptr() + c * cs, cs, m["size"], m["value"], m["type"], 0)
+    ios = np.zeros(len(sc.ops), dtype=h.UPDATE_IO_DTYPE)
+    for i, ((c, io), o, p) in enumerate(zip(sc.ops, offs, sc.payloads)):
+        ios[i] = (dpay.data_ptr() + o if p is not None else 0, c, io["offset"], io["length"], io["value"], io["type"],
+                  io["kind"], 0)
+    res = h.update_ios(chunks, ios, type_=h.ChecksumType.CRC32)
+    torch_.cuda.synchronize()
+    sc.check(chunks, res)
+
+
+def test_updio_truncate_of_other_polynomial_chunk_is_rejected(h3c, torch_dev):
+    """Documented limit: TRUNCATE / EXTEND of a chunk stored under the other polynomial fails
+    with kInvalidArg instead of storing a checksum the batch cannot derive."""
+    torch, dev = torch_dev
+    slab = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    chunks = np.zeros(1, dtype=h3c.CHUNK_STATE_DTYPE)
+    chunks[0] = (slab.data_ptr(), 4096, 100, orc.crc32(np.zeros(100, dtype=np.uint8)), 2, 0)  # stored CRC32
+    ios = np.zeros(2, dtype=h3c.UPDATE_IO_DTYPE)
+    ios[0] = (0, 0, 0, 50, 0, 0, h3c.UPD_TRUNCATE, 0)
+    ios[1] = (0, 0, 0, 200, 0, 0, h3c.UPD_EXTEND, 0)
+    res = h3c.update_ios(chunks, ios)  # batch polynomial CRC32C
+    assert list(res["status"]) == [3, 3]
+    assert int(chunks[0]["size"]) == 100 and int(chunks[0]["type"]) == 2
