@@ -76,16 +76,23 @@ struct DevChunk {
   uint32_t out_idx;
   uint32_t seg_begin;
   uint32_t flags;  // bit0: result is {NONE,0}
-  uint32_t xlen;   // x^(8*len): applies `start` (set_fold_consts)
+  uint32_t xstart; // start * x^(8*len): the init's share of the raw CRC (set_fold_consts)
   uint32_t xlast;  // x^(8*r), r = the last segment's length: folds the segments
 };
 constexpr uint32_t kFlagNone = 1u;
 
 // Segment-CRC + finalize launches over `nchunks` device descriptors (one polynomial
 // group); profiled as `prof_kind` when >= 0.  Defined in h3c_engine.hip.
+// small_rows != 0: every chunk is exactly one segment of at most small_rows (<= 8) 1 KiB
+// rows and none is NONE-flagged -- seg_small_kernel then computes and stores the results.
 int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint32_t nchunks, uint32_t total_segs,
                uint32_t max_chunk_segs, uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc,
-               const uint32_t *expected, uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind);
+               const uint32_t *expected, uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind,
+               uint32_t small_rows = 0);
+// Rows (1 KiB, absolute alignment) a byte range touches.
+inline uint32_t host_rows(uint64_t ptr, uint64_t len) {
+  return len ? (uint32_t)((((ptr + len + 1023) & ~uint64_t(1023)) - (ptr & ~uint64_t(1023))) / 1024) : 0;
+}
 // Segment size the engine picks for a batch of `total_bytes` on device `dev`.
 uint64_t pick_seg(uint64_t total_bytes, int dev);
 }  // namespace h3c_rt
@@ -199,10 +206,23 @@ inline void build_consts(PolyConsts &pc, uint32_t poly) {
 using h3c_rt::DevChunk;
 using h3c_rt::kFlagNone;
 
+// start * x^(8n) with a one-entry per-thread memo (batches repeat one start and length).
+inline uint32_t hstart_shift(uint32_t start, uint64_t n, uint32_t poly) {
+  if (!start) return 0;
+  thread_local uint64_t m_n = ~0ull;
+  thread_local uint32_t m_start = 0, m_poly = 0, m_v = 0;
+  if (n == m_n && start == m_start && poly == m_poly) return m_v;
+  m_v = hgf_mul(start, hxpow8n_memo(n, poly), poly);
+  m_n = n;
+  m_start = start;
+  m_poly = poly;
+  return m_v;
+}
+
 // The finalize kernels' per-chunk shift constants, computed on the host once per
-// distinct length instead of ~26 bit-serial GF(2) multiplies per chunk on the device.
+// distinct (start, length) instead of ~26 bit-serial GF(2) multiplies per chunk on the device.
 inline void set_fold_consts(DevChunk &c, uint64_t seg_bytes, uint32_t poly) {
-  c.xlen = hxpow8n_memo(c.len, poly);
+  c.xstart = hstart_shift(c.start, c.len, poly);
   const uint64_t m = (c.len + seg_bytes - 1) / seg_bytes;
   c.xlast = m ? hxpow8n_memo(c.len - (m - 1) * seg_bytes, poly) : kOne;
 }
@@ -399,9 +419,36 @@ __device__ __forceinline__ uint32_t wave_fold_tab(const Streams &st, uint32_t la
 }
 
 
+// N independent wave folds interleaved (N chunks' stream sets): the same arithmetic as
+// wave_fold_tab, but the LDS-latency-bound Horner / tree chains of N chunks overlap.
+template <int N>
+__device__ __forceinline__ void wave_fold_tab_n(const Streams (&st)[N], uint32_t lane, const uint32_t *red,
+                                                uint32_t (&out)[N]) {
+  uint32_t v[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = tab_mul(st[j].s3, red) ^ st[j].s2;
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = tab_mul(v[j], red) ^ st[j].s1;
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = tab_mul(v[j], red) ^ st[j].s0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    uint32_t o[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) o[j] = __shfl_down(v[j], 1u << k, 64);
+    if ((lane & ((2u << k) - 1u)) == 0) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) v[j] ^= tab_mul(o[j], red + 1024 * (k + 1));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) out[j] = v[j];
+}
+
 #ifndef H3C_UNROLL
 #define H3C_UNROLL 4
 #endif
+constexpr uint32_t kSmallRows = 8;  // segments of at most this many rows load all rows at once
 constexpr int kUnroll = H3C_UNROLL;  // rows in flight per batch (x2 with the prefetch)
 
 #ifndef H3C_SEG_ABS_ROWS
@@ -431,17 +478,37 @@ __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, c
   const uint64_t base = A + 16u * lane;
 
   Streams st{0, 0, 0, 0};
-  // row 0 (masked)
-  consume(st, load_masked(base, S, E), lb, L);
+  uint32_t r = 1;
+  const uint32_t plain_end = K >= 2 ? K - 1 : 1;
+  bool tail_done = false;
+  if (!(dbg & 1u) && K >= 2 && K <= kSmallRows) {
+    // A short segment (<= kSmallRows rows, e.g. a 4 KiB read or write buffer): issue
+    // every row load before the first is consumed -- one memory round trip per segment
+    // instead of one per row.
+    uint4 v[kSmallRows];
+    v[0] = load_masked(base, S, E);
+#pragma unroll
+    for (uint32_t u = 1; u + 1 < kSmallRows; ++u)
+      if (u < plain_end) v[u] = load_row(base + (uint64_t)u * kRowBytes);
+    v[kSmallRows - 1] = load_masked(base + (uint64_t)(K - 1) * kRowBytes, S, E);
+    consume(st, v[0], lb, L);
+#pragma unroll
+    for (uint32_t u = 1; u + 1 < kSmallRows; ++u)
+      if (u < plain_end) consume(st, v[u], lb, L);
+    consume(st, v[kSmallRows - 1], lb, L);
+    r = plain_end;
+    tail_done = true;
+  } else {
+    // row 0 (masked)
+    consume(st, load_masked(base, S, E), lb, L);
+  }
   // Rows 1 .. K-2 lie fully inside [S, E).  They are read with saddr-form global
   // loads: wave-uniform 64-bit row base in SGPRs + per-lane 32-bit offset 16*lane,
   // so no per-row VGPR address arithmetic.  Prefetch rows are clamped to the last
   // plain row (every load stays inside the segment; the few clamped re-reads at a
   // segment's end hit in cache).  One batch of kUnroll rows is in flight while the
   // previous batch is consumed.
-  uint32_t r = 1;
-  const uint32_t plain_end = K >= 2 ? K - 1 : 1;
-  if (!(dbg & 1u) && r + kUnroll <= plain_end) {
+  if (!tail_done && !(dbg & 1u) && r + kUnroll <= plain_end) {
     // readfirstlane returns int: widen through uint32_t so the low half is not sign-extended.
     const uint64_t row0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)A) |
                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(A >> 32)) << 32);
@@ -485,7 +552,7 @@ __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, c
   }
   for (; r < plain_end; ++r) consume(st, load_row(base + (uint64_t)r * kRowBytes), lb, L);
   // row K-1 (masked)
-  if (K >= 2) consume(st, load_masked(base + (uint64_t)(K - 1) * kRowBytes, S, E), lb, L);
+  if (K >= 2 && !tail_done) consume(st, load_masked(base + (uint64_t)(K - 1) * kRowBytes, S, E), lb, L);
 
   // Move every stream back to B (stream (l, j) ends 16l + 4j bytes past it).
 #if H3C_SEG_FOLD_TAB

@@ -41,6 +41,10 @@
 
 #include "h3c_common.hpp"
 
+#ifndef H3C_SMALL_EXP
+#define H3C_SMALL_EXP 0  // timing-only builds of seg_small_kernel: bit0 no lookups, bit1 no fold
+#endif
+
 namespace {
 
 // Kernel A: one wave per segment; waves take contiguous segment ranges.
@@ -91,6 +95,145 @@ __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__res
   }
 }
 
+// Kernel A': batches whose every chunk is one short segment (<= kSmallRows rows, e.g. 4 KiB
+// read / write buffers).  Per segment the big kernel pays dependent metadata loads and a
+// drained pipeline; here a wave loads the descriptors of 64 chunks at once (lane k holds
+// chunk k's), issues the next chunk's rows before folding the current one, and writes the
+// final raw value (and verify flag) itself -- no finalize launch.
+__device__ __forceinline__ uint32_t small_rows(uint64_t S, uint64_t E) {
+  return (uint32_t)((((E + kRowBytes - 1) & ~uint64_t(kRowBytes - 1)) - (S & ~uint64_t(kRowBytes - 1))) / kRowBytes);
+}
+// All R row loads of a chunk, unconditionally (a fixed count keeps the compiler's vmcnt
+// bookkeeping exact, so the next chunk's loads stay in flight while this one is folded):
+// rows past the chunk's last re-read it (cache hits).  Whole 1 KiB rows are read; they
+// never leave the 4 KiB pages that hold payload bytes, and bytes outside [S, E) are
+// masked off when the row is consumed.
+template <int R>
+__device__ __forceinline__ void small_load(uint64_t S, uint64_t E, uint32_t lane, uint4 (&v)[R]) {
+  const uint64_t base = (S & ~uint64_t(kRowBytes - 1)) + 16u * lane;
+  const uint32_t K = small_rows(S, E);
+#pragma unroll
+  for (int u = 0; u < R; ++u) v[u] = load_row(base + (uint64_t)min((uint32_t)u, K - 1) * kRowBytes);
+}
+__device__ __forceinline__ uint4 mask_row(uint4 v, uint64_t a, uint64_t S, uint64_t E) {
+  v.x &= byte_mask(a, S, E);
+  v.y &= byte_mask(a + 4, S, E);
+  v.z &= byte_mask(a + 8, S, E);
+  v.w &= byte_mask(a + 12, S, E);
+  return v;
+}
+
+template <int R>
+__global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+                                                             const PolyConsts *__restrict__ pc,
+                                                             const uint32_t *__restrict__ expected,
+                                                             uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                                             uint32_t *__restrict__ mismatch) {
+  __shared__ uint32_t lds[kLdsWords + kRedWords];
+  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
+  const uint32_t *red_g = &pc->red[0][0][0];
+  for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  __syncthreads();
+  const uint32_t *red = lds + kLdsWords;
+  const char *lb = reinterpret_cast<const char *>(lds);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t lo = (uint32_t)(gw * nchunks / nw), hi = (uint32_t)((gw + 1) * nchunks / nw);
+  if (lo >= hi) return;
+  const uint32_t poly = pc->poly;
+  const LaneLut L = make_lut(lane);
+  auto rl64 = [](uint64_t v, uint32_t t) -> uint64_t {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32);
+  };
+  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
+    const uint32_t cnt = min(64u, hi - g0);
+    uint64_t m_ptr = 0, m_len = 0;
+    uint32_t m_xs = 0, m_out = 0, m_exp = 0;
+    if (lane < cnt) {
+      const DevChunk &ch = chunks[g0 + lane];
+      m_ptr = ch.ptr;
+      m_len = ch.len;
+      m_xs = ch.xstart;
+      m_out = ch.out_idx;
+      if (expected) m_exp = expected[m_out];  // with the descriptors: no load on the per-chunk path
+    }
+    uint64_t S = rl64(m_ptr, 0), E = S + rl64(m_len, 0);
+    uint4 cur[R];
+    small_load<R>(S, E, lane, cur);
+    // Chunks in groups of kFoldGroup: each chunk's rows are folded into its stream set as
+    // they arrive (the next chunk's loads in flight), then the group's wave folds run
+    // interleaved.
+    constexpr int kFoldGroup = R <= 4 ? 4 : 2;  // R = 8 with 4 groups spills
+    for (uint32_t t0 = 0; t0 < cnt; t0 += kFoldGroup) {
+      Streams st[kFoldGroup];
+      uint64_t gS[kFoldGroup], gE[kFoldGroup];
+#pragma unroll
+      for (int j = 0; j < kFoldGroup; ++j) {
+        st[j] = Streams{0, 0, 0, 0};
+        gS[j] = S;
+        gE[j] = E;
+        const uint32_t t = t0 + j;
+        if (t < cnt) {
+          uint4 nxt[R];
+          uint64_t nS = S, nE = E;
+          if (t + 1 < cnt) {
+            nS = rl64(m_ptr, t + 1);
+            nE = nS + rl64(m_len, t + 1);
+          }
+          small_load<R>(nS, nE, lane, nxt);  // unconditional (the last one re-reads the current chunk)
+          const uint32_t K = small_rows(S, E);
+          const uint64_t base = (S & ~uint64_t(kRowBytes - 1)) + 16u * lane;
+#if H3C_SMALL_EXP & 1  // timing experiment: no table lookups
+#pragma unroll
+          for (int u = 0; u < R; ++u) st[j].s0 ^= cur[u].x ^ cur[u].y ^ cur[u].z ^ cur[u].w;
+#else
+#pragma unroll
+          for (int u = 0; u < R; ++u)
+            if ((uint32_t)u < K) {
+              uint4 x = cur[u];
+              if (u == 0 || (uint32_t)u + 1 == K) x = mask_row(x, base + (uint64_t)u * kRowBytes, S, E);
+              consume(st[j], x, lb, L);
+            }
+#endif
+          S = nS;
+          E = nE;
+#pragma unroll
+          for (int u = 0; u < R; ++u) cur[u] = nxt[u];
+        }
+      }
+      uint32_t acc[kFoldGroup];
+#if H3C_SMALL_EXP & 2  // timing experiment: no wave fold
+#pragma unroll
+      for (int j = 0; j < kFoldGroup; ++j) acc[j] = st[j].s0 ^ st[j].s1 ^ st[j].s2 ^ st[j].s3;
+#else
+      wave_fold_tab_n<kFoldGroup>(st, lane, red, acc);
+#endif
+#pragma unroll
+      for (int j = 0; j < kFoldGroup; ++j) {
+        const uint32_t t = t0 + j;
+        if (t >= cnt) break;
+        uint32_t a = acc[j];
+        const uint32_t pad = (uint32_t)(((gE[j] + kRowBytes - 1) & ~uint64_t(kRowBytes - 1)) - gE[j]);
+        if (pad >> 4) a = dgf_mul(a, pc->fix[4 * (pad >> 4)], poly);
+        if (pad & 15) a = dgf_mul(a, pc->fixz[pad & 15], poly);
+        if (lane == 0) {
+          const uint32_t raw = a ^ (uint32_t)__builtin_amdgcn_readlane(m_xs, t);
+          const uint32_t o = (uint32_t)__builtin_amdgcn_readlane(m_out, t);
+          out_raw[o] = raw;
+          if (expected) {
+            const bool good = raw == (uint32_t)__builtin_amdgcn_readlane(m_exp, t);
+            ok[o] = good ? 1 : 0;
+            if (!good && mismatch) atomicAdd(mismatch, 1u);
+          }
+        }
+      }
+    }
+  }
+}
+
 // Kernel B: per chunk, fold segment CRCs, apply start, optionally compare.
 // Chunks with more segments than this are folded by a whole wave (finalize_big_kernel);
 // one thread folding thousands of segments serially took ~1 ms for a 64 MiB chunk.
@@ -117,7 +260,7 @@ __device__ __forceinline__ void build_seg_table(uint32_t *T, uint32_t seg_mul, u
 
 // Kernel B: per chunk (one thread), fold segment CRCs, apply start, optionally compare.
 __global__ __launch_bounds__(256) void finalize_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
-                                                       uint32_t total_segs, uint32_t seg_mul,
+                                                       uint32_t total_segs, uint32_t seg_mul, uint32_t need_table,
                                                        const PolyConsts *__restrict__ pc,
                                                        const uint32_t *__restrict__ seg_crc,
                                                        const uint32_t *__restrict__ expected,
@@ -125,7 +268,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(const DevChunk *__restric
                                                        uint32_t *__restrict__ mismatch) {
   __shared__ uint32_t T[1024];
   const uint32_t poly = pc->poly;
-  build_seg_table(T, seg_mul, poly);
+  if (need_table) build_seg_table(T, seg_mul, poly);  // only chunks of >= 3 segments use it
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nchunks) return;
   const DevChunk ch = chunks[i];
@@ -140,7 +283,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(const DevChunk *__restric
       for (uint32_t s = b + 1; s + 1 < e; ++s) crc0 = tab_mul(crc0, T) ^ seg_crc[s];  // full segments
       if (e - b >= 2) crc0 = dgf_mul(crc0, ch.xlast, poly) ^ seg_crc[e - 1];          // the last one
     }
-    raw = crc0 ^ (ch.start ? dgf_mul(ch.start, ch.xlen, poly) : 0u);
+    raw = crc0 ^ ch.xstart;
   }
   finalize_store(ch, raw, expected, out_raw, ok, mismatch);
 }
@@ -184,7 +327,7 @@ __global__ __launch_bounds__(256) void finalize_big_kernel(const DevChunk *__res
   }
   if (j == 0) {
     const uint32_t crc0 = dgf_mul(h, ch.xlast, poly) ^ seg_crc[b + m - 1];
-    const uint32_t raw = crc0 ^ (ch.start ? dgf_mul(ch.start, ch.xlen, poly) : 0u);
+    const uint32_t raw = crc0 ^ ch.xstart;
     finalize_store(ch, raw, expected, out_raw, ok, mismatch);
   }
 }
@@ -397,10 +540,25 @@ hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes
 
 int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint32_t nchunks, uint32_t total_segs,
                uint32_t max_chunk_segs, uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc,
-               const uint32_t *expected, uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind) {
+               const uint32_t *expected, uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind,
+               uint32_t small_rows) {
   const DeviceCtx &ctx = g_dev[dev];
   const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
   const uint32_t poly = type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
+  if (small_rows && nchunks && !(dbg & 2u)) {  // test hook: H3C_DEBUG_FLAGS bit1 disables it
+    const uint32_t blocks = std::min<uint32_t>(ctx.num_cu, (nchunks + kWavesPerBlock - 1) / kWavesPerBlock);
+    ProfToken tok;
+    if (prof_kind >= 0) HIP_TRY(prof_begin(st, tok));
+    if (small_rows <= 4)
+      hipLaunchKernelGGL(seg_small_kernel<4>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
+                         out_raw, ok, mismatch);
+    else
+      hipLaunchKernelGGL(seg_small_kernel<8>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
+                         out_raw, ok, mismatch);
+    HIP_TRY(hipGetLastError());
+    if (prof_kind >= 0) HIP_TRY(prof_end(st, tok, prof_kind, payload_bytes));
+    return H3C_OK;
+  }
   if (total_segs) {
     const uint32_t blocks = std::min<uint32_t>(ctx.num_cu, (total_segs + kWavesPerBlock - 1) / kWavesPerBlock);
     ProfToken tok;
@@ -412,8 +570,8 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
   }
   const uint32_t seg_mul = hxpow8n(seg_bytes, poly);
   const uint32_t fb = (nchunks + 255) / 256;
-  hipLaunchKernelGGL(finalize_kernel, dim3(fb), dim3(256), 0, st, d_chunks, nchunks, total_segs, seg_mul, pc,
-                     d_segcrc, expected, out_raw, ok, mismatch);
+  hipLaunchKernelGGL(finalize_kernel, dim3(fb), dim3(256), 0, st, d_chunks, nchunks, total_segs, seg_mul,
+                     max_chunk_segs >= 3 ? 1u : 0u, pc, d_segcrc, expected, out_raw, ok, mismatch);
   HIP_TRY(hipGetLastError());
   if (max_chunk_segs > kSmallFold) {
     const uint32_t bb = (nchunks + 3) / 4;  // 4 waves (chunks) per 256-thread block
@@ -441,6 +599,7 @@ struct Group {
   uint32_t total_segs = 0;
   uint32_t max_chunk_segs = 0;
   uint64_t bytes = 0;
+  uint32_t small = 0;  // seg_small_kernel rows (0: general kernels)
   DevChunk *d_chunks = nullptr;
 };
 
@@ -490,7 +649,23 @@ struct GroupLayout {
   std::vector<DevChunk> hc[2];
   uint32_t segs[2] = {0, 0}, max_segs[2] = {0, 0};
   uint64_t bytes[2] = {0, 0};
+  // every chunk one short segment: its largest row count (seg_small_kernel), else 0
+  uint32_t small[2] = {0, 0};
 };
+
+// Recomputes GroupLayout::small from the final device pointers.
+void mark_small(GroupLayout &g) {
+  for (int k = 0; k < 2; ++k) {
+    bool all = !g.hc[k].empty() && g.max_segs[k] == 1;
+    uint32_t rows = 0;
+    for (const DevChunk &c : g.hc[k]) {
+      const uint32_t r = h3c_rt::host_rows(c.ptr, c.len);
+      if ((c.flags & kFlagNone) || c.len == 0 || r > kSmallRows) all = false;
+      rows = std::max(rows, r);
+    }
+    g.small[k] = all ? rows : 0;
+  }
+}
 
 int layout_groups(const h3c_desc *d, size_t n, uint64_t seg_bytes, GroupLayout &g) {
   for (size_t i = 0; i < n; ++i) {
@@ -522,6 +697,7 @@ int layout_groups(const h3c_desc *d, size_t n, uint64_t seg_bytes, GroupLayout &
     }
     g.hc[k].push_back(c);
   }
+  mark_small(g);
   return H3C_OK;
 }
 }  // namespace
@@ -625,6 +801,7 @@ int h3c_plan_create(const h3c_desc *d, size_t n, int device, h3c_plan **out) {
     gr.total_segs = segs[g];
     gr.max_chunk_segs = max_segs_chunk[g];
     gr.bytes = bytes[g];
+    gr.small = gl.small[g];
     hipError_t e = hipMalloc(&gr.d_chunks, hc[g].size() * sizeof(DevChunk));
     if (e == hipSuccess)
       e = hipMemcpy(gr.d_chunks, hc[g].data(), hc[g].size() * sizeof(DevChunk), hipMemcpyHostToDevice);
@@ -679,7 +856,7 @@ int h3c_plan_run(h3c_plan *p, const uint32_t *expected_raw_dev, uint32_t *out_ra
   for (const Group &g : p->groups) {
     rc = h3c_rt::launch_crc(st, p->device, g.type, g.d_chunks, g.nchunks, g.total_segs, g.max_chunk_segs, g.bytes,
                             p->seg_bytes, p->dbg, p->d_segcrc, expected_raw_dev, out_raw_dev, ok_dev, mismatch_dev,
-                            H3C_PROF_SEG);
+                            H3C_PROF_SEG, g.small);
     if (rc) break;
   }
   if (prev != p->device) HIP_TRY(hipSetDevice(prev));
@@ -764,6 +941,7 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
     for (int k = 0; k < 2; ++k)
       for (DevChunk &c : gl.hc[k])
         if (staged[c.out_idx]) c.ptr = staged[c.out_idx];
+    mark_small(gl);  // staged copies have their own alignment
     DevChunk *d_chunks[2] = {reinterpret_cast<DevChunk *>(arena + off_chunks0),
                              reinterpret_cast<DevChunk *>(arena + off_chunks1)};
     uint32_t *d_seg = reinterpret_cast<uint32_t *>(arena + off_seg);
@@ -781,7 +959,8 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
                   gl.hc[k].size() * sizeof(DevChunk)));
       const int r = h3c_rt::launch_crc(st, dev, k == 0 ? H3C_TYPE_CRC32C : H3C_TYPE_CRC32, d_chunks[k],
                                        (uint32_t)gl.hc[k].size(), gl.segs[k], gl.max_segs[k], gl.bytes[k], seg_bytes,
-                                       read_dbg_flags(), d_seg, d_exp, d_out, d_ok, d_mis, H3C_PROF_SEG);
+                                       read_dbg_flags(), d_seg, d_exp, d_out, d_ok, d_mis, H3C_PROF_SEG,
+                                       gl.small[k]);
       if (r) return r;
     }
     HIP_TRY(hipMemcpyAsync(pb + p_out, d_out, 4ull * n, hipMemcpyDeviceToHost, st));

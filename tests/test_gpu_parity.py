@@ -266,3 +266,43 @@ def test_forced_segment_sizes_and_paths(h3c, torch_dev, seg, dbg, monkeypatch):
         off += n
     _, got = h3c.batch_create(items)
     assert [int(x) for x in got] == want
+
+
+@pytest.mark.parametrize("flags", ["0", "2"])
+def test_small_chunk_batches(h3c, torch_dev, monkeypatch, flags):
+    """Batches whose every chunk is one short segment run seg_small_kernel (flags 0); flags 2
+    (H3C_DEBUG_FLAGS bit1) forces the general kernel on the same batches.  Sizes 1 B..7 KiB at
+    every alignment, device-resident and host-staged, create and verify."""
+    monkeypatch.setenv("H3C_DEBUG_FLAGS", flags)
+    torch, dev = torch_dev
+    rng = np.random.default_rng(41)
+    host = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
+    buf = to_dev(torch, dev, host)
+    for trial in range(3):
+        n = [1, 700, 5000][trial]
+        items, want, hitems = [], [], []
+        for _ in range(n):
+            ln = int(rng.choice([1, 15, 16, 17, 1023, 1024, 1025, 4096, int(rng.integers(1, 7 * 1024))]))
+            off = int(rng.integers(0, (8 << 20) - ln))
+            items.append((buf[off: off + ln], ln))
+            hitems.append((host[off: off + ln], ln))
+            want.append(orc.crc32c(host[off: off + ln]))
+        t, v = h3c.batch_create(items)
+        assert [int(x) for x in v] == want
+        exp = list(want)
+        bad = sorted(set(int(x) for x in rng.integers(0, n, max(1, n // 50))))
+        for b in bad:
+            exp[b] ^= 0x1000
+        raw, ok, nbad = h3c.batch_verify(items, exp)
+        assert nbad == len(bad) and sorted(np.nonzero(~ok)[0].tolist()) == bad
+        t, v = h3c.batch_create(hitems[:300])  # host-staged copies (own alignment)
+        assert [int(x) for x in v] == want[:300]
+    # a device plan of 4 KiB chunks (the small kernel on the asynchronous path)
+    plan = h3c.Plan.uniform(buf.data_ptr(), 4096, 2048)
+    out = torch.zeros(2048, dtype=torch.int32, device=dev)
+    plan.run(out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    for k in range(0, 2048, 97):
+        assert int(got[k]) == orc.crc32c(host[k * 4096:(k + 1) * 4096])
+    plan.close()
