@@ -20,7 +20,9 @@ from .engine import (  # noqa: F401
     StatusCode,
     batch_create,
     batch_verify,
+    crc32,
     crc32_combine,
+    crc32c,
     crc32c_combine,
     crc32c_shift,
     device_batch_combine,
@@ -51,7 +53,9 @@ __all__ = [
     "StatusCode",
     "batch_create",
     "batch_verify",
+    "crc32",
     "crc32_combine",
+    "crc32c",
     "crc32c_combine",
     "crc32c_shift",
     "device_batch_combine",

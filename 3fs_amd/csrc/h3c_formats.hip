@@ -9,6 +9,8 @@
 //     client's fold of split-read checksums (src/client/storage/StorageClientImpl.cc:1607-1633).
 //   * the read path's checksum selection + recalculate verify, AioReadJob::setResult
 //     (src/storage/aio/BatchReadJob.cc:24-55), for a batch of completed read jobs.
+#include <hip/hip_runtime.h>
+
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -32,7 +34,32 @@ int create_with(const h3c_desc *d, size_t n, const uint32_t *append_std, uint32_
 }
 }  // namespace
 
+namespace {
+// Where `p` lives: device memory (read in place) or host memory (staged).
+uint8_t mem_kind(const void *p) {
+  hipPointerAttribute_t a;
+  if (p && hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeDevice) return H3C_MEM_DEVICE;
+  (void)hipGetLastError();  // a plain host pointer is not an error
+  return H3C_MEM_HOST_PAGEABLE;
+}
+
+int one(uint8_t type, const void *data, size_t n, uint32_t start_raw, uint32_t *out_raw, void *stream) {
+  if (!out_raw || (!data && n)) return H3C_ERR_INVALID_ARG;
+  const h3c_desc d{data, n, start_raw, type, mem_kind(data), 0};
+  uint8_t t = 0;
+  return h3c_batch_create(&d, 1, &t, out_raw, stream);
+}
+}  // namespace
+
 extern "C" {
+
+int h3c_crc32c(const void *data, size_t n, uint32_t start_raw, uint32_t *out_raw, void *stream) {
+  return one(H3C_TYPE_CRC32C, data, n, start_raw, out_raw, stream);
+}
+
+int h3c_crc32(const void *data, size_t n, uint32_t start_raw, uint32_t *out_raw, void *stream) {
+  return one(H3C_TYPE_CRC32, data, n, start_raw, out_raw, stream);
+}
 
 uint32_t h3c_serde_checksum_mark(uint32_t crc0, int compressed) { return serde_mark(crc0, compressed); }
 

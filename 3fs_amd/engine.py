@@ -91,6 +91,8 @@ _proto("h3c_batch_std_crc32c", _int, _vp, _sz, _vp, _vp, _vp)
 _proto("h3c_checksum_combine", _int, ctypes.POINTER(_u8), ctypes.POINTER(_u32), _u8, _u32, _u64)
 _proto("h3c_combine_fold", _int, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp)
 _proto("h3c_batch_read_result", _int, _u8, _vp, _sz, _vp, _vp, _vp, _vp)
+_proto("h3c_crc32c", _int, _vp, _sz, _u32, ctypes.POINTER(_u32), _vp)
+_proto("h3c_crc32", _int, _vp, _sz, _u32, ctypes.POINTER(_u32), _vp)
 _proto("h3c_hostfed_create", _int, _int, _u64, ctypes.POINTER(_vp))
 _proto("h3c_hostfed_run", _int, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp)
 _proto("h3c_hostfed_destroy", None, _vp)
@@ -166,6 +168,24 @@ def crc32c_combine(c1: int, c2: int, len2: int) -> int:
 def crc32_combine(c1: int, c2: int, len2: int) -> int:
     """``folly::crc32_combine`` (Common.h:195)."""
     return lib.h3c_crc32_combine(c1 & 0xFFFFFFFF, c2 & 0xFFFFFFFF, len2)
+
+
+def crc32c(data, start: int = 0xFFFFFFFF, stream=None) -> int:
+    """``folly::crc32c(data, n, start)`` (raw register) computed on the GPU (h3c_crc32c)."""
+    ptr, nbytes, _, keep = _payload(data, None)
+    out = _u32(0)
+    _check(lib.h3c_crc32c(ptr or None, nbytes, start & 0xFFFFFFFF, ctypes.byref(out), _stream_handle(stream)))
+    del keep
+    return int(out.value)
+
+
+def crc32(data, start: int = 0xFFFFFFFF, stream=None) -> int:
+    """``folly::crc32(data, n, start)`` (raw register, IEEE polynomial) on the GPU."""
+    ptr, nbytes, _, keep = _payload(data, None)
+    out = _u32(0)
+    _check(lib.h3c_crc32(ptr or None, nbytes, start & 0xFFFFFFFF, ctypes.byref(out), _stream_handle(stream)))
+    del keep
+    return int(out.value)
 
 
 def crc32c_shift(crc: int, nbytes: int) -> int:

@@ -70,6 +70,13 @@ uint32_t h3c_crc32_combine(uint32_t c1, uint32_t c2, uint64_t len2);
 /* register advanced over `nbytes` zero bytes: crc * x^(8*nbytes) mod P. */
 uint32_t h3c_crc32c_shift(uint32_t crc, uint64_t nbytes);
 
+/* folly::crc32c(data, n, start) / folly::crc32(...) (Common.h:158,161) for one buffer, on
+ * the GPU: device memory is read in place, host memory is staged (the kind is detected
+ * with hipPointerGetAttributes).  *out_raw receives the raw register (no final XOR).
+ * Synchronous; for many buffers use h3c_batch_create. */
+int h3c_crc32c(const void *data, size_t n, uint32_t start_raw, uint32_t *out_raw, void *stream);
+int h3c_crc32(const void *data, size_t n, uint32_t start_raw, uint32_t *out_raw, void *stream);
+
 /* ---- engine lifetime ---- */
 
 int h3c_device_count(void);

@@ -142,3 +142,17 @@ def test_read_results_match_setresult_oracle(h3c, torch_dev):
         for k, i in enumerate(idx):
             rc, t, v = want[i]
             assert (int(st[k]), int(infos[k].type), infos[k].value) == (rc, t, v), i
+
+
+def test_scalar_folly_shaped_entry_points(h3c, torch_dev):
+    """h3c_crc32c / h3c_crc32: folly::crc32c / crc32 (Common.h:158,161) for one buffer,
+    host or device memory detected by pointer attributes."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(8)
+    for n in (0, 1, 9, 4096, 100003):
+        a = rng.integers(0, 256, n, dtype=np.uint8)
+        for start in (0xFFFFFFFF, 0, 0xABCDEF01):
+            assert h3c.crc32c(a, start) == orc.crc32c(a, start)
+            assert h3c.crc32c(torch.from_numpy(a).to(dev), start) == orc.crc32c(a, start)
+            assert h3c.crc32(a, start) == orc.crc32(a, start)
+    assert (~h3c.crc32c(b"123456789")) & MASK == 0xE3069283
