@@ -1,0 +1,150 @@
+// h3c_storage.hpp -- header-only C++ mirror of the 3FS storage types on the checksum path,
+// over the C ABI in h3c_crc.h.  Names, argument meaning and error codes follow the
+// reference so a storage-service maintainer (or a test) can write against it the way
+// the reference's own code reads:
+//
+//   UpdateType / UpdateIO / ChunkMetadata / IOResult   src/fbs/storage/Common.h:51-58,221-250,326-345,662-676
+//   ChunkReplicaBatch::update                          ChunkReplica::update + updateChecksum
+//                                                      (src/storage/store/ChunkReplica.cc:131-394), batched
+//   BatchReadResults::setResults                       AioReadJob::setResult (src/storage/aio/BatchReadJob.cc:24-55)
+//   Checksum::calcSerde                                src/common/net/MessageHeader.h:32-37
+//
+// Every payload byte is checksummed on the GPU; the classes hold no device state.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "h3c_checksum_info.hpp"
+#include "h3c_crc.h"
+
+namespace h3c {
+
+// StatusCode / StorageCode values used on the path (src/common/utils/StatusCodeDetails.h).
+enum StatusCode : uint32_t {
+  kOK = 0,
+  kInvalidArg = 3,
+  kChunkReadFailed = 4010,
+  kChecksumMismatch = 4080,
+};
+
+// UpdateType (Common.h:51-58).
+enum class UpdateType : uint8_t { INVALID = 0, WRITE = 1, REMOVE = 2, TRUNCATE = 4, EXTEND = 8 };
+
+// UpdateIO fields on the path (Common.h:326-345); `chunk` indexes the batch's chunk table
+// (the reference keys by GlobalKey), `data` is the payload's device address.
+struct UpdateIO {
+  uint32_t offset = 0;
+  uint32_t length = 0;
+  uint32_t chunk = 0;
+  UpdateType updateType = UpdateType::WRITE;
+  ChecksumInfo checksum;
+  const uint8_t *data = nullptr;
+
+  bool isWrite() const { return updateType == UpdateType::WRITE; }
+  bool isTruncate() const { return updateType == UpdateType::TRUNCATE; }
+  bool isExtend() const { return updateType == UpdateType::EXTEND; }
+};
+
+// ChunkMetadata fields on the path (Common.h:662-676) + where the chunk's bytes live.
+struct ChunkMetadata {
+  uint8_t *bytes = nullptr;  // device memory, capacity chunkSize
+  uint32_t chunkSize = 0;    // innerFileId.chunkSize
+  uint32_t size = 0;
+  ChecksumType checksumType = ChecksumType::NONE;
+  uint32_t checksumValue = 0;
+  ChecksumInfo checksum() const { return ChecksumInfo{checksumType, checksumValue}; }
+};
+
+// IOResult subset (Common.h:221-250).  lengthInfo is the error, or its value: the bytes
+// written for a WRITE, meta.size for TRUNCATE / EXTEND (ChunkReplica.cc:259-292), the bytes
+// read for a read.  chunkLength is meta.size after an update (not part of IOResult).
+struct IOResult {
+  uint32_t status = kOK;     // lengthInfo's error, or kOK
+  uint32_t length = 0;       // lengthInfo's value
+  ChecksumInfo checksum;     // result.checksum (meta.checksum() after an update)
+  uint32_t chunkLength = 0;
+  bool ok() const { return status == kOK; }
+};
+
+// ChunkReplica::update + updateChecksum for a batch of UpdateIOs in sequence order.
+struct ChunkReplicaBatch {
+  // `metas` are updated in place (size / checksumType / checksumValue), chunk bytes on
+  // device.  `checksumType` is the batch's polynomial (the client's chunk_checksum_type).
+  static int update(std::vector<ChunkMetadata> &metas, const std::vector<UpdateIO> &ios,
+                    std::vector<IOResult> &results, ChecksumType checksumType = ChecksumType::CRC32C,
+                    void *stream = nullptr) {
+    std::vector<h3c_chunk_state> cs(metas.size());
+    for (size_t c = 0; c < metas.size(); ++c)
+      cs[c] = h3c_chunk_state{(uint64_t)(uintptr_t)metas[c].bytes, metas[c].chunkSize, metas[c].size,
+                              metas[c].checksumValue, (uint8_t)metas[c].checksumType, {0, 0, 0}};
+    std::vector<h3c_update_io> io(ios.size());
+    for (size_t i = 0; i < ios.size(); ++i)
+      io[i] = h3c_update_io{(uint64_t)(uintptr_t)ios[i].data, ios[i].chunk, ios[i].offset, ios[i].length,
+                            ios[i].checksum.value, (uint8_t)ios[i].checksum.type, (uint8_t)ios[i].updateType,
+                            {0, 0, 0, 0, 0, 0}};
+    std::vector<h3c_update_result> res(ios.size());
+    const int rc = h3c_update_ios((uint8_t)checksumType, cs.data(), (uint32_t)cs.size(), io.data(),
+                                  (uint32_t)io.size(), res.data(), 0, stream);
+    if (rc != H3C_OK) return rc;
+    results.resize(ios.size());
+    for (size_t i = 0; i < ios.size(); ++i) {
+      const uint32_t len = res[i].status != H3C_OK ? 0 : ios[i].isWrite() ? ios[i].length : res[i].size;
+      results[i] = IOResult{res[i].status, len, ChecksumInfo{(ChecksumType)res[i].type, res[i].value}, res[i].size};
+    }
+    for (size_t c = 0; c < metas.size(); ++c) {
+      metas[c].size = cs[c].size;
+      metas[c].checksumType = (ChecksumType)cs[c].type;
+      metas[c].checksumValue = cs[c].value;
+    }
+    return H3C_OK;
+  }
+};
+
+// One completed read of a BatchReadJob (AioReadJob's state on the path).
+struct ReadJob {
+  const uint8_t *data = nullptr;  // localbuf + headLength
+  h3c_mem mem = H3C_MEM_DEVICE;
+  uint32_t offset = 0;            // readIO.offset
+  uint32_t length = 0;            // *lengthInfo
+  uint32_t chunkLen = 0;          // state.chunkLen
+  ChecksumInfo chunkChecksum;     // state.chunkChecksum
+};
+
+// AioReadJob::setResult's checksum selection + recalculate verify for a batch.
+struct BatchReadResults {
+  static int setResults(ChecksumType batchType, bool recalculateChecksum, const std::vector<ReadJob> &jobs,
+                        std::vector<IOResult> &results, void *stream = nullptr) {
+    std::vector<h3c_read_job> j(jobs.size());
+    for (size_t i = 0; i < jobs.size(); ++i)
+      j[i] = h3c_read_job{jobs[i].data, jobs[i].length, jobs[i].chunkLen, jobs[i].offset, jobs[i].chunkChecksum.value,
+                          (uint8_t)jobs[i].chunkChecksum.type, (uint8_t)jobs[i].mem,
+                          (uint8_t)(recalculateChecksum ? 1 : 0), {0, 0, 0, 0, 0}};
+    std::vector<uint8_t> t(jobs.size());
+    std::vector<uint32_t> v(jobs.size()), st(jobs.size());
+    const int rc = h3c_batch_read_result((uint8_t)batchType, j.data(), j.size(), t.data(), v.data(), st.data(), stream);
+    if (rc != H3C_OK) return rc;
+    results.resize(jobs.size());
+    for (size_t i = 0; i < jobs.size(); ++i)
+      results[i] = IOResult{st[i], jobs[i].length, ChecksumInfo{(ChecksumType)t[i], v[i]}, jobs[i].chunkLen};
+    return H3C_OK;
+  }
+};
+
+// hf3fs::net::Checksum (MessageHeader.h:32-37).
+struct Checksum {
+  static constexpr uint8_t kSerdeMessageMagicNum = 0x86;  // MessageHeader.h:14
+  static uint32_t calcSerde(const uint8_t *data, size_t size, bool compressed = false, h3c_mem mem = H3C_MEM_HOST_PAGEABLE,
+                            int *rc = nullptr) {
+    h3c_desc d{data, size, 0, (uint8_t)ChecksumType::CRC32C, (uint8_t)mem, 0};
+    const uint8_t comp = compressed ? 1 : 0;
+    uint32_t out = 0;
+    const int r = h3c_batch_serde_checksum(&d, 1, &comp, &out, nullptr);
+    if (rc) *rc = r;
+    return out;
+  }
+  static bool isCompressed(uint32_t checksum) { return checksum & 1; }  // MessageHeader.h:26
+};
+
+}  // namespace h3c
