@@ -13,22 +13,23 @@
 // (chunk c, block b, payload i); for each slot (c,b) the "old" data of write i is the
 // payload of the previous write to that slot, or the chunk's original bytes for the
 // first one.  Kernels:
-//   1. keys      slot[i] = chunk*bpc + block, chunk[i]   (validates chunk/block ids)
-//   2. rocPRIM stable radix sort_pairs (slot, i) over the slot's bits only
-//                -> writes grouped by slot, in sequence order
-//   3. link      prev[i] (previous writer of the slot) and, for the first writer of a
-//                slot, final[i] = the slot's last writer (whose bytes must end up there)
-//   4. shifts    sh[b] = x^(8*(L-(b+1)*G)) per block index, cached per chunk geometry
-//   5. delta     one wave per block write: crc0(new^old) over G bytes with the same
+//   1. tlink     per tile of 256 consecutive writes: an LDS match gives each write its
+//                previous writer of the same slot (c,b) inside the tile; the tile's last
+//                writer of a slot joins that slot's list in a hash table
+//   2. resolve   a write with no predecessor in its tile takes the largest listed index
+//                below its own (prev[i]); a slot's first writer also gets final[i] = the
+//                slot's last writer (whose bytes must end up there).  No sort.
+//   3. shifts    sh[b] = x^(8*(L-(b+1)*G)) per block index, cached per chunk geometry
+//   4. delta     one wave per block write: crc0(new^old) over G bytes with the same
 //                replicated-LDS stride tables as the create kernel, folded across the
 //                wave with table multiplies by uniform constants (wave_fold_tab);
 //                the first writer of a slot also writes the slot's final bytes back
 //                (it is the only wave that reads the slot's original bytes: no race)
-//   6. rocPRIM stable radix sort_pairs (chunk, i)  -> per-chunk sequence order
-//   7. gather (one thread per write: delta * sh[b]) + rocPRIM
-//      inclusive_scan_by_key(chunk, XOR) + scatter:
-//        out_raw[i] = raw_in[c] ^ XOR of deltas of writes j<=i to chunk c
+//   5. per-chunk prefix XOR in sequence order:
+//        out_raw[i] = raw_in[c] ^ XOR of delta_j * sh[b_j] over writes j<=i to chunk c
 //      i.e. the chunk checksum right after write i, which is what updateChecksum stores.
+//      Dense tiles (tile / column / apply kernels) when tiles x chunks is small, else a
+//      rocPRIM stable sort by chunk + inclusive_scan_by_key(XOR) + scatter.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -82,41 +83,108 @@ uint32_t bits_for(uint64_t v) {  // number of bits to represent values < v
   return b;
 }
 
+// Sort path only: chunk keys and sequence indices for the per-chunk scan.
 __global__ void upd_keys_kernel(const uint32_t *__restrict__ blk_chunk, const uint32_t *__restrict__ blk_index,
-                                uint32_t n, uint32_t nchunks, uint32_t bpc, uint32_t *__restrict__ kslot,
-                                uint32_t *__restrict__ kchunk, uint32_t *__restrict__ iota,
-                                uint32_t *__restrict__ err) {
+                                uint32_t n, uint32_t nchunks, uint32_t bpc, uint32_t *__restrict__ kchunk,
+                                uint32_t *__restrict__ iota, uint32_t *__restrict__ err) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t c = blk_chunk[i], b = blk_index[i];
   iota[i] = i;
-  if (c >= nchunks || b >= bpc) {  // invalid entry: parked on the sentinel slot / chunk, no effect
-    if (err) atomicAdd(err, 1u);  // sort path counts here, tile path in upd_tile_kernel
-    kslot[i] = nchunks * bpc;
-    if (kchunk) kchunk[i] = nchunks;
-    return;
-  }
-  kslot[i] = c * bpc + b;
-  if (kchunk) kchunk[i] = c;
+  const bool bad = c >= nchunks || b >= bpc;  // invalid entry: parked on the sentinel chunk, no effect
+  if (bad) atomicAdd(err, 1u);
+  kchunk[i] = bad ? nchunks : c;
 }
 
-// On the stable sort by slot: prev[i] = previous writer of i's slot (or none), and for
-// the first writer of a slot, final_of[i] = the slot's last writer.
-__global__ void upd_link_kernel(const uint32_t *__restrict__ slot_s, const uint32_t *__restrict__ idx1, uint32_t n,
-                                uint32_t *__restrict__ prev, uint32_t *__restrict__ final_of) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const uint32_t slot = slot_s[p], i = idx1[p];
-  const bool start = p == 0 || slot_s[p - 1] != slot;
-  prev[i] = start ? kNone : idx1[p - 1];
-  if (start) {  // last position of this slot's run: binary search in [p, n)
-    uint32_t lo = p, hi = n;  // invariant: slot(lo) == slot, slot(hi) > slot or hi == n
-    while (hi - lo > 1) {
-      const uint32_t mid = lo + (hi - lo) / 2;
-      if (slot_s[mid] == slot) lo = mid; else hi = mid;
-    }
-    final_of[i] = idx1[lo];
+// ---- previous-writer links without a sort (tile match + hash of per-tile last writers) ----
+// Writes are cut into tiles of kLinkTile consecutive sequence positions.  Within a tile
+// each write finds its previous writer of the same slot by an LDS match.  Each tile's last
+// writer of a slot is pushed (one atomicExch) on the list of its hash bucket (key = chunk *
+// bpc + block); a bucket's list may also hold other slots' writers, told apart by their
+// stored key.  A write with no predecessor in its tile then takes the largest listed index
+// of its slot below its own: a list holds at most one entry per tile and slot, so the walk
+// stays short even when every write hammers one slot.  (A returning atomicCAS costs about
+// twice an atomicExch here: scripts/atomic_probe.hip.)
+constexpr uint32_t kLinkTile = 256;
+
+__device__ __forceinline__ uint32_t slot_hash(uint32_t key, uint32_t mask) { return (key * 0x9E3779B1u >> 7) & mask; }
+
+// In-tile grouping by key: an LDS open-addressing table (2 x tile entries) whose entries
+// head unordered lists of the tile positions holding that key.  Returns the list head of
+// `key` (kNone keys are not inserted).  Collisions inside a tile are rare, so the lists
+// are short; one hammered key gives one list of the whole tile.
+template <uint32_t kT>
+struct TileGroups {
+  uint32_t key[2 * kT], head[2 * kT], next[kT];
+};
+
+template <uint32_t kT>
+__device__ __forceinline__ uint32_t tile_group(TileGroups<kT> &g, uint32_t t, uint32_t key) {
+  for (uint32_t e = t; e < 2 * kT; e += kT) {
+    g.key[e] = kNone;
+    g.head[e] = kNone;
   }
+  __syncthreads();
+  uint32_t h = kNone;
+  if (key != kNone) {
+    h = (key * 0x9E3779B1u >> 16) & (2 * kT - 1);
+    for (;;) {
+      const uint32_t k = atomicCAS(&g.key[h], kNone, key);
+      if (k == kNone || k == key) break;
+      h = (h + 1) & (2 * kT - 1);
+    }
+    g.next[t] = atomicExch(&g.head[h], t);
+  }
+  __syncthreads();
+  return h == kNone ? kNone : g.head[h];
+}
+
+__global__ __launch_bounds__(kLinkTile) void upd_tlink_kernel(const uint32_t *__restrict__ blk_chunk,
+                                                              const uint32_t *__restrict__ blk_index, uint32_t n,
+                                                              uint32_t nchunks, uint32_t bpc, uint32_t *hhead,
+                                                              uint32_t hmask, uint32_t *__restrict__ nkey,
+                                                              uint32_t *__restrict__ next, uint32_t *__restrict__ prev) {
+  __shared__ TileGroups<kLinkTile> g;
+  const uint32_t t = threadIdx.x, i0 = blockIdx.x * kLinkTile, i = i0 + t;
+  uint32_t key = kNone;
+  if (i < n) {
+    const uint32_t c = blk_chunk[i], b = blk_index[i];
+    if (c < nchunks && b < bpc) key = c * bpc + b;
+  }
+  const uint32_t head = tile_group(g, t, key);
+  uint32_t pin = kNone;
+  bool last = true;
+  for (uint32_t u = head; u != kNone; u = g.next[u]) {
+    if (u < t && (pin == kNone || u > pin)) pin = u;
+    if (u > t) last = false;
+  }
+  if (i < n) prev[i] = pin == kNone ? kNone : i0 + pin;
+  if (key != kNone && last) {  // push i on its bucket's list
+    nkey[i] = key;
+    next[i] = atomicExch(&hhead[slot_hash(key, hmask)], i);
+  }
+}
+
+// prev[i] for writes with no predecessor in their tile, and final_of[i] (the slot's last
+// writer) for each slot's first writer.
+__global__ void upd_resolve_kernel(const uint32_t *__restrict__ blk_chunk, const uint32_t *__restrict__ blk_index,
+                                   uint32_t n, uint32_t nchunks, uint32_t bpc, const uint32_t *__restrict__ hhead,
+                                   uint32_t hmask, const uint32_t *__restrict__ nkey,
+                                   const uint32_t *__restrict__ next, uint32_t *__restrict__ prev,
+                                   uint32_t *__restrict__ final_of) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || prev[i] != kNone) return;
+  const uint32_t c = blk_chunk[i], b = blk_index[i];
+  if (c >= nchunks || b >= bpc) return;
+  const uint32_t key = c * bpc + b;
+  uint32_t p = kNone, fmax = i;  // i's tile's last writer of the slot is on the list
+  for (uint32_t j = hhead[slot_hash(key, hmask)]; j != kNone; j = next[j]) {
+    if (nkey[j] != key) continue;
+    if (j < i && (p == kNone || j > p)) p = j;
+    fmax = max(fmax, j);
+  }
+  prev[i] = p;
+  if (p == kNone) final_of[i] = fmax;
 }
 
 __global__ void upd_shift_kernel(uint32_t bpc, uint64_t chunk_len, uint32_t block_bytes,
@@ -337,8 +405,9 @@ __global__ __launch_bounds__(kTile) void upd_tile_kernel(const uint32_t *__restr
                                                          const uint32_t *__restrict__ sh, uint32_t poly,
                                                          uint32_t *__restrict__ inpre, uint32_t *__restrict__ agg,
                                                          uint32_t *__restrict__ tile_invalid) {
-  __shared__ uint32_t cid[kTile], val[kTile];
-  const uint32_t t = threadIdx.x, i0 = blockIdx.x * kTile, i = i0 + t;
+  __shared__ TileGroups<kTile> g;
+  __shared__ uint32_t val[kTile];
+  const uint32_t t = threadIdx.x, i = blockIdx.x * kTile + t;
   uint32_t c = kNone, v = 0;
   bool invalid = false;
   if (i < n) {
@@ -350,22 +419,17 @@ __global__ __launch_bounds__(kTile) void upd_tile_kernel(const uint32_t *__restr
       invalid = true;
     }
   }
-  cid[t] = c;
   val[t] = v;
   uint32_t *row = agg + (uint64_t)blockIdx.x * nchunks;
   for (uint32_t k = t; k < nchunks; k += kTile) row[k] = 0;
-  // LDS tile loaded, row zeroed (workgroup-scope fence); count the tile's invalid entries
-  const int ninv = __syncthreads_count(invalid);
+  const int ninv = __syncthreads_count(invalid);  // also orders val[] and the row zeroing
   if (t == 0) tile_invalid[blockIdx.x] = (uint32_t)ninv;
-  const uint32_t cnt = min(kTile, n - i0);
+  const uint32_t head = tile_group(g, t, c);
   uint32_t acc = 0;
   bool last = true;
-  for (uint32_t u = 0; u < cnt; ++u) {  // uniform loop: broadcast LDS reads
-    const uint32_t cu = cid[u], vu = val[u];
-    if (cu == c) {
-      if (u <= t) acc ^= vu;
-      else last = false;
-    }
+  for (uint32_t u = head; u != kNone; u = g.next[u]) {  // the tile's writes to chunk c
+    if (u <= t) acc ^= val[u];
+    else last = false;
   }
   if (i < n) inpre[i] = acc;
   if (c != kNone && last) row[c] = acc;  // the tile's last write to c carries the aggregate
@@ -435,8 +499,10 @@ bool use_tiles(uint32_t n, uint32_t nchunks) {
 }
 
 struct Workspace {
-  uint32_t *kslot, *kslot_s, *kchunk, *kchunk_s, *iota, *idx1, *idx2;
-  uint32_t *prev, *final_of, *delta, *vals, *scan, *sh, *err;
+  uint32_t *kchunk, *kchunk_s, *iota, *idx2;
+  uint32_t *prev, *final_of, *next, *delta, *vals, *scan, *sh, *err;
+  uint32_t *hhead, *nkey;  // link hash: hcap bucket list heads; per-write slot key of listed writes
+  uint32_t hcap;
   uint32_t *agg, *colpre;  // dense tile path: ntiles x nchunks each
   uint32_t *tile_invalid;  // dense tile path: per-tile invalid-entry counts
   void *tmp;
@@ -453,9 +519,13 @@ int layout(void *base, uint32_t n, uint32_t nchunks, uint32_t bpc, Workspace &w,
     off += align_up(bytes);
     return p;
   };
-  uint32_t **arrays[] = {&w.kslot, &w.kslot_s, &w.kchunk, &w.kchunk_s, &w.iota, &w.idx1,
-                         &w.idx2,  &w.prev,    &w.final_of, &w.delta, &w.vals, &w.scan};
+  uint32_t **arrays[] = {&w.kchunk, &w.kchunk_s, &w.iota,  &w.idx2, &w.prev,
+                         &w.final_of, &w.next,    &w.delta, &w.vals, &w.scan};
   for (uint32_t **a : arrays) *a = (uint32_t *)take(4ull * n);
+  w.nkey = (uint32_t *)take(4ull * n);
+  w.hcap = 256;
+  while (w.hcap < n) w.hcap <<= 1;
+  w.hhead = (uint32_t *)take(4ull * w.hcap);
   w.sh = (uint32_t *)take(4ull * bpc);
   w.err = (uint32_t *)take(4);
   const uint64_t tiles_cells = use_tiles(n, nchunks) ? (uint64_t)((n + kTile - 1) / kTile) * nchunks : 0;
@@ -566,16 +636,16 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
     HIP_TRY(hipMemcpyAsync(chunk_raw_out_dev, chunk_raw_in_dev, 4ull * nchunks, hipMemcpyDeviceToDevice, st));
     HIP_TRY(hipMemsetAsync(w.err, 0, 4, st));
   }
-  hipLaunchKernelGGL(upd_keys_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks, bpc,
-                     w.kslot, tiles ? nullptr : w.kchunk, w.iota, tiles ? nullptr : w.err);
+  // previous-writer links: tile match + hash of per-tile last writers (no sort)
+  HIP_TRY(hipMemsetAsync(w.hhead, 0xFF, 4ull * w.hcap, st));
+  const uint32_t nlt = (n_blocks + kLinkTile - 1) / kLinkTile;
+  hipLaunchKernelGGL(upd_tlink_kernel, dim3(nlt), dim3(kLinkTile), 0, st, blk_chunk_dev, blk_index_dev, n_blocks,
+                     nchunks, bpc, w.hhead, w.hcap - 1, w.nkey, w.next, w.prev);
   HIP_TRY(hipGetLastError());
-  // Stable radix sorts of (key, sequence index) over only the key's bits: by slot
-  // (chunk, block) for the previous-writer links, by chunk for the per-chunk scan.
+  hipLaunchKernelGGL(upd_resolve_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks,
+                     bpc, w.hhead, w.hcap - 1, w.nkey, w.next, w.prev, w.final_of);
+  HIP_TRY(hipGetLastError());
   size_t tmp = w.tmp_bytes;
-  HIP_TRY(rocprim::radix_sort_pairs<SortConfig>(w.tmp, tmp, w.kslot, w.kslot_s, w.iota, w.idx1, n_blocks, 0,
-                                    bits_for((uint64_t)nchunks * bpc + 1), st));
-  hipLaunchKernelGGL(upd_link_kernel, dim3(gb), dim3(tb), 0, st, w.kslot_s, w.idx1, n_blocks, w.prev, w.final_of);
-  HIP_TRY(hipGetLastError());
   const uint32_t *sh = nullptr;
   rc = shift_table(dev, type, chunk_len, block_bytes, pc, w.sh, st, &sh);
   if (rc) return rc;
@@ -601,6 +671,10 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
                        bpc, chunk_raw_in_dev, w.colpre, w.scan, out_raw_dev);
     HIP_TRY(hipGetLastError());
   } else {
+    hipLaunchKernelGGL(upd_keys_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks,
+                       bpc, w.kchunk, w.iota, w.err);
+    HIP_TRY(hipGetLastError());
+    // stable radix sort of (chunk, sequence index) for the per-chunk scan
     tmp = w.tmp_bytes;
     HIP_TRY(rocprim::radix_sort_pairs<SortConfig>(w.tmp, tmp, w.kchunk, w.kchunk_s, w.iota, w.idx2, n_blocks, 0,
                                                   bits_for((uint64_t)nchunks + 1), st));
