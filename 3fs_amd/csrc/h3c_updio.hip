@@ -16,13 +16,16 @@
 //   TRUNCATE to t < n:   r' = (r ^ crc0(old[t, n))) * x^(-8(n-t))
 //   grow to t > n (TRUNCATE or EXTEND, zero fill): r' = r * x^(8(t-n))
 //   INIT (the chunk's stored checksum is not of this polynomial): r' = crc of [0, n)
-// Pipeline:
-//   A. payload CRCs of every WRITE (seg_crc_kernel via launch_crc) -> host: the
-//      client-checksum verify decides which ops apply (a rejected op changes nothing).
+// Pipeline (one host <-> device round trip per batch):
+//   A. payload CRC jobs of every WRITE (seg_crc_kernel via launch_crc), run on the device
+//      ahead of the update in the same stream.
 //   B. host pass in sequence order: sizes, the reference's case analysis, and byte
 //      jobs (old-range / cut-tail CRCs, payload copies, zero fills).  Jobs that touch
 //      the same 4 KiB block are put in successive epochs (conflict levels); within an
-//      epoch no two ops share a block.
+//      epoch no two ops share a block.  The pass is speculative: it assumes every client
+//      checksum matches (a rejected op changes nothing); the device checks them after A
+//      and, on a mismatch, the copy kernels write nothing and the batch is redone with
+//      the payload CRCs known.
 //   C. per epoch: one launch_crc over the epoch's CRC jobs (reads the chunk before
 //      this epoch's writes), then one copy kernel.
 //   D. per op an affine element (M, E); rocPRIM inclusive_scan_by_key over
@@ -53,15 +56,14 @@ constexpr uint64_t kCopyPiece = 256u << 10;
 
 enum : uint32_t { kAffNop = 0, kAffInit = 1, kAffWrite = 2, kAffTrunc = 3, kAffGrow = 4 };
 
-struct AffIn {
-  int64_t delta;   // n' - n
-  uint64_t len;    // WRITE: payload bytes; INIT: chunk bytes
-  uint64_t pad;    // WRITE: zero bytes after the old range (o + len - e)
-  uint64_t tail;   // WRITE: bytes after the write in the new chunk (n' - o - len)
+struct AffIn {  // every length is below the chunk size (32 bits)
+  uint32_t nb, na; // chunk length before / after the op
+  uint32_t len;    // WRITE: payload bytes; INIT: chunk bytes
+  uint32_t pad;    // WRITE: zero bytes after the old range (o + len - e)
+  uint32_t tail;   // WRITE: bytes after the write in the new chunk (n' - o - len)
   uint32_t job;    // CRC job (old range / cut tail / whole chunk) or kNoJob
   uint32_t op;     // WRITE: op index (payload CRC)
   uint32_t kind;
-  uint32_t pad2;
 };
 
 struct Aff {
@@ -88,9 +90,31 @@ struct CopyPiece {
   uint64_t dst, src, len;  // src == 0: zero fill
 };
 
+// A client checksum to check against the payload's CRC on the device (speculative pass).
+struct VerifyItem {
+  uint32_t op, want;
+};
+
+// bad[1 + k] = item k's payload CRC differs from the client's; bad[0] = any did.
+__global__ void updio_verify_kernel(const VerifyItem *__restrict__ items, uint32_t nver,
+                                    const uint32_t *__restrict__ payraw, uint32_t std_domain,
+                                    uint32_t *__restrict__ bad) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nver) return;
+  const VerifyItem it = items[k];
+  const uint32_t got = std_domain ? ~payraw[it.op] : payraw[it.op];
+  if (got != it.want) {
+    bad[1 + k] = 1;
+    atomicOr(bad, 1u);
+  }
+}
+
 // One workgroup per piece (<= kCopyPiece bytes).  16-byte vector body when source and
-// destination share their alignment (or for zero fill), bytes otherwise.
-__global__ __launch_bounds__(256) void updio_copy_kernel(const CopyPiece *__restrict__ pieces) {
+// destination share their alignment (or for zero fill), bytes otherwise.  Nothing is
+// written when `gate` is set (a client checksum failed in the speculative pass).
+__global__ __launch_bounds__(256) void updio_copy_kernel(const CopyPiece *__restrict__ pieces,
+                                                         const uint32_t *__restrict__ gate) {
+  if (gate && *gate) return;
   const CopyPiece pc = pieces[blockIdx.x];
   uint8_t *d = reinterpret_cast<uint8_t *>(pc.dst);
   const uint8_t *s = reinterpret_cast<const uint8_t *>(pc.src);
@@ -124,16 +148,16 @@ __global__ void updio_aff_kernel(const AffIn *__restrict__ in, uint32_t npos, co
     case kAffWrite: {
       uint32_t d = payraw[a.op] ^ dgf_mul(0xFFFFFFFFu, dxpow8n(a.len, pc, poly), poly);  // crc0(payload)
       if (a.job != kNoJob) d ^= dgf_mul(jobcrc[a.job], dxpow8n(a.pad, pc, poly), poly);
-      r.m = dxpow8s(a.delta, pc, poly);
+      r.m = dxpow8s((int64_t)a.na - (int64_t)a.nb, pc, poly);
       r.e = dgf_mul(d, dxpow8n(a.tail, pc, poly), poly);
       break;
     }
     case kAffTrunc:
-      r.m = dxpow8s(a.delta, pc, poly);
+      r.m = dxpow8s((int64_t)a.na - (int64_t)a.nb, pc, poly);
       r.e = dgf_mul(jobcrc[a.job], r.m, poly);
       break;
     case kAffGrow:
-      r.m = dxpow8s(a.delta, pc, poly);
+      r.m = dxpow8s((int64_t)a.na - (int64_t)a.nb, pc, poly);
       break;
     default:
       break;
@@ -189,55 +213,81 @@ void add_job(CrcBatch &b, uint64_t ptr, uint64_t len, uint32_t start, uint32_t o
 class BlockEpochs {
  public:
   explicit BlockEpochs(size_t expect) { reset(expect); }
+  // Empties the map for `expect` keys.  Entries carry the generation that wrote them, so
+  // emptying a table that is already large enough is one increment, not a clear.
+  void reset(size_t expect) {
+    used_ = 0;
+    if (!tab_.empty() && 2 * expect <= tab_.size() && gen_ != 0xFFFFFFFFu) {
+      ++gen_;
+      return;
+    }
+    size_t cap = std::max<size_t>(1024, tab_.size());
+    while (cap < 2 * expect) cap <<= 1;
+    tab_.assign(cap, Entry{0, 0, 0});
+    mask_ = cap - 1;
+    shift_ = 64 - __builtin_ctzll(cap);
+    gen_ = 1;
+  }
   uint32_t get(uint64_t k) const {
     for (uint64_t h = slot(k);; h = (h + 1) & mask_) {
-      if (keys_[h] == k) return vals_[h];
-      if (keys_[h] == kEmpty) return 0;
+      const Entry &e = tab_[h];
+      if (e.gen != gen_) return 0;
+      if (e.key == k) return e.val;
     }
   }
-  void put(uint64_t k, uint32_t v) {
-    if (2 * (used_ + 1) > keys_.size()) grow();
+  // The value of `k`, inserted as 0 when absent.  References stay valid until the next
+  // call that may grow the table: reserve(count) first.
+  uint32_t &at(uint64_t k) {
     for (uint64_t h = slot(k);; h = (h + 1) & mask_) {
-      if (keys_[h] == k) {
-        vals_[h] = v;
+      Entry &e = tab_[h];
+      if (e.gen != gen_) {
+        e = Entry{k, 0, gen_};
+        ++used_;
+        return e.val;
+      }
+      if (e.key == k) return e.val;
+    }
+  }
+  void reserve(size_t more) {
+    while (2 * (used_ + more) > tab_.size()) grow();
+  }
+  void put(uint64_t k, uint32_t v) {
+    if (2 * (used_ + 1) > tab_.size()) grow();
+    for (uint64_t h = slot(k);; h = (h + 1) & mask_) {
+      Entry &e = tab_[h];
+      if (e.gen != gen_) {
+        e = Entry{k, v, gen_};
+        ++used_;
         return;
       }
-      if (keys_[h] == kEmpty) {
-        keys_[h] = k;
-        vals_[h] = v;
-        ++used_;
+      if (e.key == k) {
+        e.val = v;
         return;
       }
     }
   }
 
  private:
-  static constexpr uint64_t kEmpty = ~0ull;
+  struct Entry {
+    uint64_t key;
+    uint32_t val, gen;
+  };
   uint64_t slot(uint64_t k) const { return ((k * 0x9E3779B97F4A7C15ull) >> shift_) & mask_; }
-  void reset(size_t expect) {
-    size_t cap = 1024;
-    int bits = 10;
-    while (cap < 2 * expect) {
-      cap <<= 1;
-      ++bits;
-    }
-    keys_.assign(cap, kEmpty);
-    vals_.assign(cap, 0);
-    mask_ = cap - 1;
-    shift_ = 64 - bits;
-    used_ = 0;
-  }
   void grow() {
-    std::vector<uint64_t> k = std::move(keys_);
-    std::vector<uint32_t> v = std::move(vals_);
-    reset(k.size());
-    for (size_t i = 0; i < k.size(); ++i)
-      if (k[i] != kEmpty) put(k[i], v[i]);
+    std::vector<Entry> old = std::move(tab_);
+    const uint32_t g = gen_;
+    tab_.assign(old.size() * 2, Entry{0, 0, 0});
+    mask_ = tab_.size() - 1;
+    shift_ = 64 - __builtin_ctzll(tab_.size());
+    gen_ = 1;
+    used_ = 0;
+    for (const Entry &e : old)
+      if (e.gen == g) put(e.key, e.val);
   }
-  std::vector<uint64_t> keys_;
-  std::vector<uint32_t> vals_;
+  std::vector<Entry> tab_;
   uint64_t mask_ = 0;
   int shift_ = 0;
+  uint32_t gen_ = 0;
   size_t used_ = 0;
 };
 
@@ -269,6 +319,205 @@ struct OpOut {
   uint32_t chunk = 0;
 };
 
+// Output of the host pass (B) for one attempt.
+struct HostPass {
+  std::vector<Track> tr;
+  std::vector<uint32_t> cur;  // next free scan position per chunk
+  std::vector<OpOut> outs;
+  std::vector<uint32_t> raw0;
+  std::vector<CrcBatch> ep_crc;
+  std::vector<std::vector<CopyPiece>> ep_copy;
+  std::vector<VerifyItem> verify;  // speculative attempt: client checksums checked on the device
+  uint32_t njobs = 0;
+  size_t nep = 0;  // epochs in use (ep_crc / ep_copy keep their storage across calls)
+  BlockEpochs last_touch{0};
+};
+
+// Per-thread host scratch, reused across calls: the pass touches tens of MB of host
+// vectors per 100k ops, and fresh allocations each call cost page faults of the same
+// order as the pass itself.
+struct UpdioScratch {
+  HostPass P;
+  CrcBatch pay;
+  std::vector<uint32_t> status, payraw, truev, start;
+};
+
+// Scan positions in (chunk, sequence) order, laid out before the pass: chunk c owns
+// [start[c], start[c+1]), one slot per op that passed validation plus one for an INIT
+// reset when the chunk's stored checksum is not of this polynomial.  Slots the pass does
+// not use (rejected ops) stay identity elements.  Returns the slot count.
+uint32_t plan_positions(uint8_t poly_type, const h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
+                        uint32_t n, const std::vector<uint32_t> &status, std::vector<uint32_t> &start) {
+  start.assign(nchunks + 1, 0);
+  for (uint32_t i = 0; i < n; ++i)
+    if (status[i] != H3C_ERR_INVALID_ARG) ++start[ios[i].chunk + 1];
+  for (uint32_t c = 0; c < nchunks; ++c) {
+    if (start[c + 1] && chunks[c].size != 0 && chunks[c].type != poly_type) ++start[c + 1];
+    start[c + 1] += start[c];
+  }
+  return start[nchunks];
+}
+
+// B. the host pass in sequence order.  `payraw` == nullptr: speculative (every WRITE's
+// client checksum is assumed to match and queued for the device check); otherwise the
+// payload CRCs are known and `status` already carries every mismatch.
+void host_pass(uint8_t poly_type, uint32_t poly, bool std_domain, const h3c_chunk_state *chunks, uint32_t nchunks,
+               const h3c_update_io *ios, uint32_t n, std::vector<uint32_t> &status, const uint32_t *payraw,
+               uint64_t seg_j, const std::vector<uint32_t> &start, AffIn *lay, uint32_t *keys, HostPass &P) {
+  P.tr.assign(nchunks, Track{});
+  for (uint32_t c = 0; c < nchunks; ++c) {
+    P.tr[c].size = chunks[c].size;
+    P.tr[c].type = chunks[c].type;
+  }
+  P.cur.assign(start.begin(), start.end() - 1);
+  P.outs.assign(n, OpOut{});
+  P.raw0.assign(nchunks, 0);
+  for (size_t e = 0; e < P.nep; ++e) {
+    P.ep_crc[e].chunks.clear();
+    P.ep_crc[e].total_segs = P.ep_crc[e].max_segs = 0;
+    P.ep_crc[e].bytes = 0;
+    P.ep_copy[e].clear();
+  }
+  P.nep = 0;
+  P.verify.clear();
+  P.njobs = 0;
+  BlockEpochs &last_touch = P.last_touch;
+  last_touch.reset(n + 1024);
+
+  auto epoch_for = [&](uint32_t c, uint64_t a, uint64_t b) -> uint32_t {  // touched [a, b)
+    if (b <= a) return 0;
+    uint32_t e = 0;
+    const uint64_t b0 = a / kConflictBlock, b1 = (b - 1) / kConflictBlock;
+    if (b0 == b1) {  // one block: a single probe
+      last_touch.reserve(1);
+      uint32_t &v = last_touch.at(((uint64_t)c << 32) | b0);
+      e = v++;
+    } else {
+      for (uint64_t k = b0; k <= b1; ++k) e = std::max(e, last_touch.get(((uint64_t)c << 32) | k));
+      for (uint64_t k = b0; k <= b1; ++k) last_touch.put(((uint64_t)c << 32) | k, e + 1);
+    }
+    if (P.nep <= e) {
+      P.nep = e + 1;
+      if (P.ep_crc.size() < P.nep) {
+        P.ep_crc.resize(P.nep);
+        P.ep_copy.resize(P.nep);
+      }
+    }
+    return e;
+  };
+  auto add_copy = [&](uint32_t e, uint64_t dst, uint64_t src, uint64_t len) {
+    for (uint64_t k = 0; k < len; k += kCopyPiece)
+      P.ep_copy[e].push_back(CopyPiece{dst + k, src ? src + k : 0, std::min(kCopyPiece, len - k)});
+  };
+  auto new_elem = [&](uint32_t c, const AffIn &a) -> uint32_t {
+    const uint32_t p = P.cur[c]++;
+    lay[p] = a;
+    return p;
+  };
+
+  for (uint32_t i = 0; i < n; ++i) {
+    if (status[i] == H3C_ERR_INVALID_ARG) continue;
+    const h3c_update_io &io = ios[i];
+    const uint32_t c = io.chunk;
+    Track &t = P.tr[c];
+    const uint64_t base = chunks[c].base;
+    // A6: the client's checksum of the payload (:193-207); TRUNCATE / EXTEND carry NONE.
+    if (status[i] == H3C_OK && io.checksum_type != H3C_TYPE_NONE && io.length != 0) {
+      if (io.kind != H3C_UPD_WRITE) {
+        status[i] = H3C_ERR_CHECKSUM_MISMATCH;
+      } else if (payraw) {
+        const uint32_t got = std_domain ? ~payraw[i] : payraw[i];
+        if (got != io.checksum_value) status[i] = H3C_ERR_CHECKSUM_MISMATCH;
+      } else {
+        P.verify.push_back(VerifyItem{i, io.checksum_value});
+      }
+    }
+    if (status[i] == H3C_ERR_CHECKSUM_MISMATCH) {  // rejected: nothing changes
+      P.outs[i] = OpOut{t.src, t.true_pos, c};
+      continue;
+    }
+    // TRUNCATE / EXTEND store a checksum of the chunk's own type (:328-332); one of the
+    // other polynomial cannot be derived from this batch's CRC state (documented limit).
+    if (io.kind != H3C_UPD_WRITE && !std_domain && t.type != H3C_TYPE_NONE && t.type != poly_type) {
+      status[i] = H3C_ERR_INVALID_ARG;
+      continue;
+    }
+    if (!t.started) {  // the chunk's scan segment starts from a known CRC or an INIT reset
+      t.started = true;
+      const h3c_chunk_state &cs = chunks[c];
+      if (cs.size == 0) {
+        P.raw0[c] = 0xFFFFFFFFu;  // raw CRC of no bytes
+      } else if (cs.type == poly_type) {
+        P.raw0[c] = std_domain ? ~cs.value : cs.value;
+      } else {
+        const uint32_t e = epoch_for(c, 0, cs.size);
+        add_job(P.ep_crc[e], base, cs.size, 0u, P.njobs, seg_j, poly);
+        AffIn a{};
+        a.kind = kAffInit;
+        a.len = cs.size;
+        a.job = P.njobs++;
+        new_elem(c, a);
+      }
+    }
+    const uint64_t nb = t.size;
+    uint64_t na = nb;
+    AffIn a{};
+    a.job = kNoJob;
+    uint8_t type_after = t.type;
+    if (io.kind == H3C_UPD_WRITE) {  // :281-291, doRealWrite :124
+      const uint64_t o = io.offset, len = io.length;
+      na = std::max<uint64_t>(nb, o + len);
+      const uint32_t e = epoch_for(c, std::min(o, nb), (o > nb || len) ? o + len : 0);
+      if (o < nb && len) {
+        const uint64_t end = std::min(o + len, nb);
+        add_job(P.ep_crc[e], base + o, end - o, 0u, P.njobs, seg_j, poly);
+        a.job = P.njobs++;
+        a.pad = (uint32_t)(o + len - end);
+      }
+      if (o > nb) add_copy(e, base + nb, 0, o - nb);
+      if (len) add_copy(e, base + o, io.payload, len);
+      a.kind = kAffWrite;
+      a.len = (uint32_t)len;
+      a.tail = (uint32_t)(na - o - len);
+      a.op = i;
+      type_after = io.checksum_type;
+    } else {  // TRUNCATE / EXTEND (:260-273)
+      const uint64_t l = io.length;
+      if (l < nb && io.kind == H3C_UPD_TRUNCATE) {
+        na = l;
+        const uint32_t e = epoch_for(c, l, nb);
+        add_job(P.ep_crc[e], base + l, nb - l, 0u, P.njobs, seg_j, poly);
+        a.kind = kAffTrunc;
+        a.job = P.njobs++;
+      } else if (l > nb) {
+        na = l;
+        const uint32_t e = epoch_for(c, nb, l);
+        add_copy(e, base + nb, 0, l - nb);
+        a.kind = kAffGrow;
+      } else {
+        a.kind = kAffNop;
+      }
+    }
+    a.nb = (uint32_t)nb;
+    a.na = (uint32_t)na;
+    const uint32_t id = new_elem(c, a);
+    t.size = (uint32_t)na;
+    t.type = type_after;
+    // updateChecksum: case (i) stores 0 (:334-336); (ii)-(iv) the chunk's CRC.
+    if (!std_domain && (type_after == H3C_TYPE_NONE || na == 0)) {
+      t.src = Src::kZero;
+    } else {
+      t.src = Src::kTrue;
+      t.true_pos = id;  // scan position
+    }
+    P.outs[i] = OpOut{t.src, t.true_pos, c};
+  }
+  for (uint32_t c = 0; c < nchunks; ++c) {
+    for (uint32_t p = P.cur[c]; p < start[c + 1]; ++p) lay[p] = AffIn{0, 0, 0, 0, 0, kNoJob, 0, kAffNop};
+    for (uint32_t p = start[c]; p < start[c + 1]; ++p) keys[p] = c;
+  }
+}
+
 }  // namespace
 
 extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
@@ -285,8 +534,11 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   const uint32_t poly = poly_type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
 
   PhaseClock clk;
+  thread_local UpdioScratch ws;
   // ---- per-op validation (range :140-145, kind, client checksum type) ----
-  std::vector<uint32_t> status(n, H3C_OK);
+  std::vector<uint32_t> &status = ws.status;
+  status.assign(n, H3C_OK);
+  uint64_t pay_bytes = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const h3c_update_io &io = ios[i];
     const bool kind_ok = io.kind == H3C_UPD_WRITE || io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND;
@@ -297,231 +549,72 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     const h3c_chunk_state &c = chunks[io.chunk];
     if (io.offset >= c.chunk_size || (uint64_t)io.offset + io.length > c.chunk_size || !c.base ||
         (io.checksum_type != H3C_TYPE_NONE && io.checksum_type != poly_type) ||
-        (io.kind == H3C_UPD_WRITE && io.length && !io.payload))
-      status[i] = H3C_ERR_INVALID_ARG;
-  }
-
-  // ---- A. payload CRCs (raw, init ~0) of every valid WRITE ----
-  std::vector<uint32_t> payraw(n, 0xFFFFFFFFu);
-  uint64_t pay_bytes = 0;
-  for (uint32_t i = 0; i < n; ++i)
-    if (status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE) pay_bytes += ios[i].length;
-  const uint64_t seg_a = h3c_rt::pick_seg(pay_bytes, dev);
-  CrcBatch pay;
-  for (uint32_t i = 0; i < n; ++i)
-    if (status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
-      add_job(pay, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg_a, poly);
-  if (!pay.chunks.empty()) {
-    Arena a;
-    const size_t nc = pay.chunks.size();
-    const size_t bytes = nc * sizeof(DevChunk) + 4ull * pay.total_segs + 4ull * n + 3 * 256;
-    // pinned staging (see h3c_rt::PinnedLease): [DevChunks | payload CRCs back]
-    const size_t pin_raw = (nc * sizeof(DevChunk) + 255) & ~size_t(255);
-    h3c_rt::PinnedLease pin(pin_raw + 4ull * n);
-    if (!pin.ok()) return H3C_ERR_HIP;
-    std::memcpy(pin.data(), pay.chunks.data(), nc * sizeof(DevChunk));
-    h3c_rt::DeviceLease scratch(dev, bytes);
-    if (!scratch.ok()) return H3C_ERR_HIP;
-    a.base = scratch.data();
-    DevChunk *d_chunks = a.take<DevChunk>(nc);
-    uint32_t *d_seg = a.take<uint32_t>(pay.total_segs);
-    uint32_t *d_raw = a.take<uint32_t>(n);
-    int err = H3C_OK;
-    hipError_t e = hipMemcpyAsync(d_chunks, pin.data(), nc * sizeof(DevChunk), hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemsetAsync(d_raw, 0xFF, 4ull * n, st);
-    if (e == hipSuccess) {
-      err = h3c_rt::launch_crc(st, dev, poly_type, d_chunks, (uint32_t)nc, pay.total_segs, pay.max_segs, pay.bytes,
-                               seg_a, 0, d_seg, nullptr, d_raw, nullptr, nullptr, -1);
-      if (!err) e = hipMemcpyAsync(pin.data() + pin_raw, d_raw, 4ull * n, hipMemcpyDeviceToHost, st);
-    }
-    const hipError_t se = hipStreamSynchronize(st);
-    if (e == hipSuccess) e = se;
-    if (e != hipSuccess) {
-      h3c_rt::set_error("h3c_update_ios: payload checksums", e);
-      return H3C_ERR_HIP;
-    }
-    if (err) return err;
-    std::memcpy(payraw.data(), pin.data() + pin_raw, 4ull * n);
-  }
-
-  clk.mark("A payload");
-  // ---- B. host pass: verify, sizes, cases, epochs, byte jobs, affine elements ----
-  std::vector<Track> tr(nchunks);
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    tr[c].size = chunks[c].size;
-    tr[c].type = chunks[c].type;
-  }
-  // chunk-major scan layout: positions are assigned after the pass
-  std::vector<AffIn> elems;
-  std::vector<uint32_t> elem_chunk;
-  std::vector<OpOut> outs(n);
-  std::vector<uint32_t> raw0(nchunks, 0);
-  std::vector<CrcBatch> ep_crc;
-  std::vector<std::vector<CopyPiece>> ep_copy;
-  BlockEpochs last_touch(n + 1024);
-  elems.reserve(n + 64);
-  elem_chunk.reserve(n + 64);
-  uint32_t njobs = 0;
-  uint64_t job_bytes_total = 0;
-  for (uint32_t i = 0; i < n; ++i)
-    if (status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE) job_bytes_total += ios[i].length;
-  const uint64_t seg_j = h3c_rt::pick_seg(job_bytes_total, dev);
-
-  auto epoch_for = [&](uint32_t c, uint64_t a, uint64_t b) -> uint32_t {  // touched [a, b)
-    if (b <= a) return 0;
-    uint32_t e = 0;
-    const uint64_t b0 = a / kConflictBlock, b1 = (b - 1) / kConflictBlock;
-    for (uint64_t k = b0; k <= b1; ++k) {
-      e = std::max(e, last_touch.get(((uint64_t)c << 32) | k));
-    }
-    for (uint64_t k = b0; k <= b1; ++k) last_touch.put(((uint64_t)c << 32) | k, e + 1);
-    if (ep_crc.size() <= e) {
-      ep_crc.resize(e + 1);
-      ep_copy.resize(e + 1);
-    }
-    return e;
-  };
-  auto add_copy = [&](uint32_t e, uint64_t dst, uint64_t src, uint64_t len) {
-    for (uint64_t k = 0; k < len; k += kCopyPiece)
-      ep_copy[e].push_back(CopyPiece{dst + k, src ? src + k : 0, std::min(kCopyPiece, len - k)});
-  };
-  auto new_elem = [&](uint32_t c, const AffIn &a) -> uint32_t {
-    const uint32_t id = (uint32_t)elems.size();
-    elems.push_back(a);
-    elem_chunk.push_back(c);
-    return id;
-  };
-
-  for (uint32_t i = 0; i < n; ++i) {
-    if (status[i] != H3C_OK) continue;
-    const h3c_update_io &io = ios[i];
-    const uint32_t c = io.chunk;
-    Track &t = tr[c];
-    const uint64_t base = chunks[c].base;
-    // A6: the client's checksum of the payload (:193-207); TRUNCATE / EXTEND carry NONE.
-    if (io.checksum_type != H3C_TYPE_NONE && io.length != 0) {
-      const uint32_t want = io.kind == H3C_UPD_WRITE ? (std_domain ? ~payraw[i] : payraw[i]) : 0u;
-      if (io.kind != H3C_UPD_WRITE || want != io.checksum_value) {
-        status[i] = H3C_ERR_CHECKSUM_MISMATCH;
-        outs[i] = OpOut{t.src, t.true_pos, c};
-        continue;
-      }
-    }
-    // TRUNCATE / EXTEND store a checksum of the chunk's own type (:328-332); one of the
-    // other polynomial cannot be derived from this batch's CRC state (documented limit).
-    if (io.kind != H3C_UPD_WRITE && !std_domain && t.type != H3C_TYPE_NONE && t.type != poly_type) {
+        (io.kind == H3C_UPD_WRITE && io.length && !io.payload)) {
       status[i] = H3C_ERR_INVALID_ARG;
       continue;
     }
-    if (!t.started) {  // the chunk's scan segment starts from a known CRC or an INIT reset
-      t.started = true;
-      const h3c_chunk_state &cs = chunks[c];
-      if (cs.size == 0) {
-        raw0[c] = 0xFFFFFFFFu;  // raw CRC of no bytes
-      } else if (cs.type == poly_type) {
-        raw0[c] = std_domain ? ~cs.value : cs.value;
-      } else {
-        const uint32_t e = epoch_for(c, 0, cs.size);
-        add_job(ep_crc[e], base, cs.size, 0u, njobs, seg_j, poly);
-        AffIn a{};
-        a.kind = kAffInit;
-        a.len = cs.size;
-        a.job = njobs++;
-        new_elem(c, a);
-      }
-    }
-    const uint64_t nb = t.size;
-    uint64_t na = nb;
-    AffIn a{};
-    a.job = kNoJob;
-    uint8_t type_after = t.type;
-    if (io.kind == H3C_UPD_WRITE) {  // :281-291, doRealWrite :124
-      const uint64_t o = io.offset, len = io.length;
-      na = std::max<uint64_t>(nb, o + len);
-      const uint32_t e = epoch_for(c, std::min(o, nb), (o > nb || len) ? o + len : 0);
-      if (o < nb && len) {
-        const uint64_t end = std::min(o + len, nb);
-        add_job(ep_crc[e], base + o, end - o, 0u, njobs, seg_j, poly);
-        a.job = njobs++;
-        a.pad = o + len - end;
-      }
-      if (o > nb) add_copy(e, base + nb, 0, o - nb);
-      if (len) add_copy(e, base + o, io.payload, len);
-      a.kind = kAffWrite;
-      a.len = len;
-      a.tail = na - o - len;
-      a.op = i;
-      type_after = io.checksum_type;
-    } else {  // TRUNCATE / EXTEND (:260-273)
-      const uint64_t l = io.length;
-      if (l < nb && io.kind == H3C_UPD_TRUNCATE) {
-        na = l;
-        const uint32_t e = epoch_for(c, l, nb);
-        add_job(ep_crc[e], base + l, nb - l, 0u, njobs, seg_j, poly);
-        a.kind = kAffTrunc;
-        a.job = njobs++;
-      } else if (l > nb) {
-        na = l;
-        const uint32_t e = epoch_for(c, nb, l);
-        add_copy(e, base + nb, 0, l - nb);
-        a.kind = kAffGrow;
-      } else {
-        a.kind = kAffNop;
-      }
-    }
-    a.delta = (int64_t)na - (int64_t)nb;
-    const uint32_t id = new_elem(c, a);
-    t.size = (uint32_t)na;
-    t.type = type_after;
-    // updateChecksum: case (i) stores 0 (:334-336); (ii)-(iv) the chunk's CRC.
-    if (!std_domain && (type_after == H3C_TYPE_NONE || na == 0)) {
-      t.src = Src::kZero;
-    } else {
-      t.src = Src::kTrue;
-      t.true_pos = id;  // element id; mapped to a scan position below
-    }
-    outs[i] = OpOut{t.src, t.true_pos, c};
+    if (io.kind == H3C_UPD_WRITE) pay_bytes += io.length;
   }
+  // A. payload CRC jobs (raw, init ~0) of every valid WRITE: run on the device in the same
+  // stream as the update itself; the old-range CRC jobs of B use the same segment size.
+  const uint64_t seg = h3c_rt::pick_seg(pay_bytes, dev);
+  CrcBatch &pay = ws.pay;
+  pay.chunks.clear();
+  pay.total_segs = pay.max_segs = 0;
+  pay.bytes = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
+      add_job(pay, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg, poly);
+  clk.mark("A prepare");
 
-  clk.mark("B host");
-  // ---- C-D. device: epochs, affine scan ----
-  const uint32_t npos = (uint32_t)elems.size();
-  std::vector<uint32_t> pos_of(npos), keys(npos);
-  std::vector<AffIn> lay(npos);
-  {  // stable counting sort of the elements by chunk: (chunk, sequence) order
-    std::vector<uint32_t> start(nchunks + 1, 0);
-    for (uint32_t id = 0; id < npos; ++id) ++start[elem_chunk[id] + 1];
-    for (uint32_t c = 0; c < nchunks; ++c) start[c + 1] += start[c];
-    for (uint32_t id = 0; id < npos; ++id) {
-      const uint32_t c = elem_chunk[id], p = start[c]++;
-      pos_of[id] = p;
-      keys[p] = c;
-      lay[p] = elems[id];
-    }
-  }
-  std::vector<uint32_t> truev(npos, 0);
-  if (npos) {
+  // B + C-D, speculatively first: the host pass assumes every client checksum matches and
+  // the device checks them before any byte is written (the copy kernels are gated on the
+  // check).  A mismatch (rare: a corrupted transfer) costs a second attempt with the
+  // payload CRCs known.  One host <-> device round trip per batch in the common case.
+  HostPass &P = ws.P;
+  std::vector<uint32_t> &payraw = ws.payraw;  // known payload CRCs (second attempt only)
+  std::vector<uint32_t> &truev = ws.truev;
+  // scan elements and keys are written by the pass straight into pinned staging
+  const uint32_t npos = plan_positions(poly_type, chunks, nchunks, ios, n, status, ws.start);
+  const size_t lay_bytes = ((size_t)npos * sizeof(AffIn) + 255) & ~size_t(255);
+  h3c_rt::PinnedLease pin_el(lay_bytes + 4ull * npos + 256);
+  if (!pin_el.ok()) return H3C_ERR_HIP;
+  AffIn *lay = reinterpret_cast<AffIn *>(pin_el.data());
+  uint32_t *keys = reinterpret_cast<uint32_t *>(pin_el.data() + lay_bytes);
+  truev.assign(npos, 0);
+  for (int attempt = 0;; ++attempt) {
+    const bool spec = attempt == 0;
+    host_pass(poly_type, poly, std_domain, chunks, nchunks, ios, n, status, spec ? nullptr : payraw.data(), seg,
+              ws.start, lay, keys, P);
+    clk.mark("B host");
+    // ---- C-D. device: payload CRCs + check (speculative), epochs, affine scan ----
+    const uint32_t nver = (uint32_t)P.verify.size();
     size_t scan_tmp = 0;
-    HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, scan_tmp, (uint32_t *)nullptr, (Aff *)nullptr, (Aff *)nullptr,
-                                           (size_t)npos, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
+    if (npos)
+      HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, scan_tmp, (uint32_t *)nullptr, (Aff *)nullptr, (Aff *)nullptr,
+                                             (size_t)npos, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
     size_t crc_chunks = 0, copy_pieces = 0;
-    uint32_t max_segs = 0;
-    for (size_t e = 0; e < ep_crc.size(); ++e) {
-      crc_chunks += ep_crc[e].chunks.size();
-      copy_pieces += ep_copy[e].size();
-      max_segs = std::max(max_segs, ep_crc[e].total_segs);
+    uint32_t max_segs = spec ? pay.total_segs : 0;
+    for (size_t e = 0; e < P.nep; ++e) {
+      crc_chunks += P.ep_crc[e].chunks.size();
+      copy_pieces += P.ep_copy[e].size();
+      max_segs = std::max(max_segs, P.ep_crc[e].total_segs);
     }
-    const size_t bytes = crc_chunks * sizeof(DevChunk) + copy_pieces * sizeof(CopyPiece) + 4ull * max_segs +
-                         4ull * std::max(njobs, 1u) + 4ull * n + npos * (sizeof(AffIn) + 2 * sizeof(Aff) + 8) +
-                         4ull * nchunks + scan_tmp + 16 * 256;
+    const size_t npay = spec ? pay.chunks.size() : 0;
     Arena a;
+    const size_t bytes = (npay + crc_chunks) * sizeof(DevChunk) + copy_pieces * sizeof(CopyPiece) +
+                         nver * sizeof(VerifyItem) + 4ull * max_segs + 4ull * std::max(P.njobs, 1u) + 4ull * n +
+                         npos * (sizeof(AffIn) + 2 * sizeof(Aff) + 8) + 4ull * nchunks + 4ull * nver + scan_tmp +
+                         16 * 256;
     h3c_rt::DeviceLease scratch(dev, bytes);
     if (!scratch.ok()) return H3C_ERR_HIP;
     a.base = scratch.data();
+    DevChunk *d_pay = a.take<DevChunk>(npay);
     DevChunk *d_crc = a.take<DevChunk>(crc_chunks);
     CopyPiece *d_copy = a.take<CopyPiece>(copy_pieces);
+    VerifyItem *d_ver = a.take<VerifyItem>(nver);
     uint32_t *d_seg = a.take<uint32_t>(max_segs);
-    uint32_t *d_jobcrc = a.take<uint32_t>(std::max(njobs, 1u));
+    uint32_t *d_jobcrc = a.take<uint32_t>(std::max(P.njobs, 1u));
     uint32_t *d_payraw = a.take<uint32_t>(n);
     AffIn *d_in = a.take<AffIn>(npos);
     Aff *d_aff = a.take<Aff>(npos);
@@ -529,61 +622,93 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     uint32_t *d_keys = a.take<uint32_t>(npos);
     uint32_t *d_true = a.take<uint32_t>(npos);
     uint32_t *d_raw0 = a.take<uint32_t>(nchunks);
+    uint32_t *d_bad = a.take<uint32_t>(1 + nver);  // [0]: any mismatch (gates the copies); [1+k]: item k
     void *d_tmp = a.take<char>(scan_tmp);
-    // flatten per-epoch descriptors (host copies stay alive until the final sync)
-    std::vector<DevChunk> all_crc;
-    std::vector<CopyPiece> all_copy;
-    all_crc.reserve(crc_chunks);
-    all_copy.reserve(copy_pieces);
-    for (size_t e = 0; e < ep_crc.size(); ++e) {
-      all_crc.insert(all_crc.end(), ep_crc[e].chunks.begin(), ep_crc[e].chunks.end());
-      all_copy.insert(all_copy.end(), ep_copy[e].begin(), ep_copy[e].end());
-    }
-    // pinned staging for every upload and the result download (see h3c_rt::PinnedLease)
-    const size_t up[6] = {crc_chunks * sizeof(DevChunk), copy_pieces * sizeof(CopyPiece), 4ull * n,
-                          npos * sizeof(AffIn), 4ull * npos, 4ull * nchunks};
-    const void *src[6] = {all_crc.data(), all_copy.data(), payraw.data(), lay.data(), keys.data(), raw0.data()};
-    void *dst[6] = {d_crc, d_copy, d_payraw, d_in, d_keys, d_raw0};
-    size_t pin_bytes = 0, pin_off[7];
-    for (int k = 0; k < 6; ++k) {
-      pin_off[k] = pin_bytes;
-      pin_bytes += (up[k] + 255) & ~size_t(255);
-    }
-    pin_off[6] = pin_bytes;
-    h3c_rt::PinnedLease pin(pin_bytes + 4ull * npos);
+
+    // pinned staging: uploads [pay | crc jobs | copies | verify | payraw | raw0] (the scan
+    // elements and keys are already in pin_el), downloads [true values | mismatch flags |
+    // payload CRCs]
+    enum { kPay, kCrc, kCopy, kVer, kPayraw, kRaw0, kUp, kTrue = kUp, kBad, kPayBack, kAll };
+    size_t len[kAll] = {npay * sizeof(DevChunk), crc_chunks * sizeof(DevChunk), copy_pieces * sizeof(CopyPiece),
+                        nver * sizeof(VerifyItem), spec ? 0 : 4ull * n, 4ull * nchunks, 4ull * npos,
+                        spec ? 4ull * (1 + nver) : 0, spec ? 4ull * n : 0};
+    void *dst[kUp] = {d_pay, d_crc, d_copy, d_ver, d_payraw, d_raw0};
+    size_t off[kAll + 1];
+    off[0] = 0;
+    for (int k = 0; k < kAll; ++k) off[k + 1] = off[k] + ((len[k] + 255) & ~size_t(255));
+    h3c_rt::PinnedLease pin(off[kAll]);
     if (!pin.ok()) return H3C_ERR_HIP;
+    char *hp = pin.data();
+    if (npay) std::memcpy(hp + off[kPay], pay.chunks.data(), len[kPay]);
+    {
+      char *pc_crc = hp + off[kCrc], *pc_copy = hp + off[kCopy];
+      for (size_t e = 0; e < P.nep; ++e) {
+        const size_t bc = P.ep_crc[e].chunks.size() * sizeof(DevChunk), bp = P.ep_copy[e].size() * sizeof(CopyPiece);
+        if (bc) std::memcpy(pc_crc, P.ep_crc[e].chunks.data(), bc);
+        if (bp) std::memcpy(pc_copy, P.ep_copy[e].data(), bp);
+        pc_crc += bc;
+        pc_copy += bp;
+      }
+    }
+    if (nver) std::memcpy(hp + off[kVer], P.verify.data(), len[kVer]);
+    if (!spec) std::memcpy(hp + off[kPayraw], payraw.data(), len[kPayraw]);
+    std::memcpy(hp + off[kRaw0], P.raw0.data(), len[kRaw0]);
+
     int err = H3C_OK;
     auto body = [&]() -> int {
-      for (int k = 0; k < 6; ++k)
-        if (up[k]) {
-          std::memcpy(pin.data() + pin_off[k], src[k], up[k]);
-          HIP_TRY(hipMemcpyAsync(dst[k], pin.data() + pin_off[k], up[k], hipMemcpyHostToDevice, st));
+      for (int k = 0; k < kUp; ++k)
+        if (len[k]) HIP_TRY(hipMemcpyAsync(dst[k], hp + off[k], len[k], hipMemcpyHostToDevice, st));
+      if (npos) {
+        HIP_TRY(hipMemcpyAsync(d_in, lay, npos * sizeof(AffIn), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d_keys, keys, 4ull * npos, hipMemcpyHostToDevice, st));
+      }
+      if (spec) {
+        HIP_TRY(hipMemsetAsync(d_bad, 0, 4ull * (1 + nver), st));
+        HIP_TRY(hipMemsetAsync(d_payraw, 0xFF, 4ull * n, st));
+        if (npay) {
+          const int r = h3c_rt::launch_crc(st, dev, poly_type, d_pay, (uint32_t)npay, pay.total_segs, pay.max_segs,
+                                           pay.bytes, seg, 0, d_seg, nullptr, d_payraw, nullptr, nullptr, -1);
+          if (r) return r;
         }
+        if (nver) {
+          hipLaunchKernelGGL(updio_verify_kernel, dim3((nver + 255) / 256), dim3(256), 0, st, d_ver, nver, d_payraw,
+                             std_domain ? 1u : 0u, d_bad);
+          HIP_TRY(hipGetLastError());
+        }
+      }
+      const uint32_t *gate = spec ? d_bad : nullptr;
       size_t co = 0, po = 0;
-      for (size_t e = 0; e < ep_crc.size(); ++e) {
-        const CrcBatch &b = ep_crc[e];
+      for (size_t e = 0; e < P.nep; ++e) {
+        const CrcBatch &b = P.ep_crc[e];
         if (!b.chunks.empty()) {
           const int r = h3c_rt::launch_crc(st, dev, poly_type, d_crc + co, (uint32_t)b.chunks.size(), b.total_segs,
-                                           b.max_segs, b.bytes, seg_j, 0, d_seg, nullptr, d_jobcrc, nullptr, nullptr,
+                                           b.max_segs, b.bytes, seg, 0, d_seg, nullptr, d_jobcrc, nullptr, nullptr,
                                            -1);
           if (r) return r;
         }
-        if (!ep_copy[e].empty()) {
-          hipLaunchKernelGGL(updio_copy_kernel, dim3((uint32_t)ep_copy[e].size()), dim3(256), 0, st, d_copy + po);
+        if (!P.ep_copy[e].empty()) {
+          hipLaunchKernelGGL(updio_copy_kernel, dim3((uint32_t)P.ep_copy[e].size()), dim3(256), 0, st, d_copy + po,
+                             gate);
           HIP_TRY(hipGetLastError());
         }
         co += b.chunks.size();
-        po += ep_copy[e].size();
+        po += P.ep_copy[e].size();
       }
-      const uint32_t tb = 256, gb = (npos + tb - 1) / tb;
-      hipLaunchKernelGGL(updio_aff_kernel, dim3(gb), dim3(tb), 0, st, d_in, npos, d_payraw, d_jobcrc, pc, d_aff);
-      HIP_TRY(hipGetLastError());
-      size_t tmp = scan_tmp;
-      HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, tmp, d_keys, d_aff, d_scan, (size_t)npos, AffOp{poly},
-                                             rocprim::equal_to<uint32_t>(), st));
-      hipLaunchKernelGGL(updio_true_kernel, dim3(gb), dim3(tb), 0, st, d_scan, d_keys, npos, d_raw0, poly, d_true);
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(pin.data() + pin_off[6], d_true, 4ull * npos, hipMemcpyDeviceToHost, st));
+      if (npos) {
+        const uint32_t tb = 256, gb = (npos + tb - 1) / tb;
+        hipLaunchKernelGGL(updio_aff_kernel, dim3(gb), dim3(tb), 0, st, d_in, npos, d_payraw, d_jobcrc, pc, d_aff);
+        HIP_TRY(hipGetLastError());
+        size_t tmp = scan_tmp;
+        HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, tmp, d_keys, d_aff, d_scan, (size_t)npos, AffOp{poly},
+                                               rocprim::equal_to<uint32_t>(), st));
+        hipLaunchKernelGGL(updio_true_kernel, dim3(gb), dim3(tb), 0, st, d_scan, d_keys, npos, d_raw0, poly, d_true);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(hp + off[kTrue], d_true, len[kTrue], hipMemcpyDeviceToHost, st));
+      }
+      if (spec) {
+        HIP_TRY(hipMemcpyAsync(hp + off[kBad], d_bad, len[kBad], hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(hp + off[kPayBack], d_payraw, len[kPayBack], hipMemcpyDeviceToHost, st));
+      }
       return H3C_OK;
     };
     err = body();
@@ -593,21 +718,28 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
       h3c_rt::set_error("h3c_update_ios", e);
       return H3C_ERR_HIP;
     }
-    std::memcpy(truev.data(), pin.data() + pin_off[6], 4ull * npos);
+    clk.mark("C-D device");
+    if (spec) {
+      const uint32_t *bad = reinterpret_cast<const uint32_t *>(hp + off[kBad]);
+      if (bad[0]) {  // a client checksum did not match: nothing was written; redo with them known
+        payraw.assign(n, 0xFFFFFFFFu);
+        std::memcpy(payraw.data(), hp + off[kPayBack], 4ull * n);
+        for (uint32_t k = 0; k < nver; ++k)
+          if (bad[1 + k]) status[P.verify[k].op] = H3C_ERR_CHECKSUM_MISMATCH;
+        continue;
+      }
+    }
+    if (npos) std::memcpy(truev.data(), hp + off[kTrue], 4ull * npos);
+    break;
   }
 
-  clk.mark("C-D device");
   // ---- E. results and final chunk states ----
   std::vector<uint32_t> init_value(nchunks);
-  std::vector<uint8_t> init_type(nchunks);
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    init_value[c] = chunks[c].value;
-    init_type[c] = chunks[c].type;
-  }
+  for (uint32_t c = 0; c < nchunks; ++c) init_value[c] = chunks[c].value;
   auto value_of = [&](Src s, uint32_t id, uint32_t c) -> uint32_t {
     if (s == Src::kZero) return 0u;
     if (s == Src::kInitial) return init_value[c];
-    const uint32_t raw = truev[pos_of[id]];
+    const uint32_t raw = truev[id];
     return std_domain ? ~raw : raw;
   };
   // replay types and sizes in sequence order for per-op results
@@ -638,15 +770,58 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     }
     r.size = size_now[c];
     r.type = (std_domain && status[i] == H3C_OK) ? poly_type : type_now[c];
-    r.value = value_of(outs[i].src, outs[i].pos, c);
+    r.value = value_of(P.outs[i].src, P.outs[i].pos, c);
   }
   for (uint32_t c = 0; c < nchunks; ++c) {
-    if (!tr[c].started) continue;
-    chunks[c].size = tr[c].size;
-    chunks[c].type = std_domain ? poly_type : tr[c].type;
-    chunks[c].value = value_of(tr[c].src, tr[c].true_pos, c);
+    if (!P.tr[c].started) continue;
+    chunks[c].size = P.tr[c].size;
+    chunks[c].type = std_domain ? poly_type : P.tr[c].type;
+    chunks[c].value = value_of(P.tr[c].src, P.tr[c].true_pos, c);
   }
   clk.mark("E results");
-  if (clk.on) std::fprintf(stderr, "[updio] epochs %zu, crc jobs %u, elements %u\n", ep_crc.size(), njobs, npos);
+  if (clk.on)
+    std::fprintf(stderr, "[updio] epochs %zu, crc jobs %u, elements %u\n", P.nep, P.njobs, npos);
   return H3C_OK;
+}
+
+// Diagnostic hook, no device work: host time of one speculative h3c_update_ios pass over
+// `ios` (payload-job build, position plan, host pass B), the fastest of `reps`; the phase
+// split goes to stderr with H3C_UPDIO_TIMING.  Used to tune the host pass without a GPU.
+extern "C" double h3c_diag_updio_host_ms(uint8_t poly_type, const h3c_chunk_state *chunks, uint32_t nchunks,
+                                         const h3c_update_io *ios, uint32_t n, int reps) {
+  const uint32_t poly = poly_type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
+  thread_local UpdioScratch ws;
+  double total = 0, t_a = 0, t_b = 0;
+  std::vector<AffIn> lay;
+  std::vector<uint32_t> keys;
+  for (int r = 0; r < reps; ++r) {
+    const auto t0 = std::chrono::steady_clock::now();
+    ws.status.assign(n, H3C_OK);
+    for (uint32_t i = 0; i < n; ++i)
+      if (ios[i].chunk >= nchunks) ws.status[i] = H3C_ERR_INVALID_ARG;
+    const uint64_t seg = 1u << 20;
+    CrcBatch &pay = ws.pay;
+    pay.chunks.clear();
+    pay.total_segs = pay.max_segs = 0;
+    pay.bytes = 0;
+    for (uint32_t i = 0; i < n; ++i)
+      if (ws.status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
+        add_job(pay, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg, poly);
+    const uint32_t npos = plan_positions(poly_type, chunks, nchunks, ios, n, ws.status, ws.start);
+    lay.resize(npos);
+    keys.resize(npos);
+    const auto t1 = std::chrono::steady_clock::now();
+    host_pass(poly_type, poly, false, chunks, nchunks, ios, n, ws.status, nullptr, seg, ws.start, lay.data(),
+              keys.data(), ws.P);
+    const auto t2 = std::chrono::steady_clock::now();
+    using ms = std::chrono::duration<double, std::milli>;
+    if (r == 0 || ms(t2 - t0).count() < total) {  // the fastest repetition
+      t_a = ms(t1 - t0).count();
+      t_b = ms(t2 - t1).count();
+      total = ms(t2 - t0).count();
+    }
+  }
+  if (std::getenv("H3C_UPDIO_TIMING"))
+    std::fprintf(stderr, "[updio host] payload jobs + plan %.3f ms, pass %.3f ms\n", t_a, t_b);
+  return total;
 }
