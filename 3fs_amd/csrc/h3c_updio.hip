@@ -42,6 +42,11 @@
 #include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include <rocprim/device/device_scan_by_key.hpp>
@@ -193,103 +198,52 @@ struct CrcBatch {
   uint64_t bytes = 0;
 };
 
-void add_job(CrcBatch &b, uint64_t ptr, uint64_t len, uint32_t start, uint32_t out_idx, uint64_t seg_bytes,
-             uint32_t poly) {
+// set_fold_consts with a one-entry cache per constant: a batch's jobs mostly share one
+// length, and the shared memo behind set_fold_consts is thread_local (a TLS lookup per call
+// in a shared library).  One cache per thread and call (the polynomial is fixed).
+struct FoldCache {
+  uint64_t r = ~0ull, n = ~0ull;
+  uint32_t vr = 0, start = 0, vs = 0;
+  void set(DevChunk &c, uint64_t seg_bytes, uint32_t poly) {
+    const uint64_t m = (c.len + seg_bytes - 1) / seg_bytes;
+    if (!m) {
+      c.xlast = kOne;
+    } else {
+      const uint64_t rem = c.len - (m - 1) * seg_bytes;
+      if (rem != r) {
+        r = rem;
+        vr = hxpow8n_memo(rem, poly);
+      }
+      c.xlast = vr;
+    }
+    if (!c.start) {
+      c.xstart = 0;
+    } else {
+      if (c.len != n || c.start != start) {
+        n = c.len;
+        start = c.start;
+        vs = hstart_shift(c.start, c.len, poly);
+      }
+      c.xstart = vs;
+    }
+  }
+};
+
+void add_job(CrcBatch &b, FoldCache &fc, uint64_t ptr, uint64_t len, uint32_t start, uint32_t out_idx,
+             uint64_t seg_bytes, uint32_t poly) {
   DevChunk c{};
   c.ptr = ptr;
   c.len = len;
   c.start = start;
   c.out_idx = out_idx;
   c.seg_begin = b.total_segs;
-  set_fold_consts(c, seg_bytes, poly);
+  fc.set(c, seg_bytes, poly);
   const uint32_t ns = (uint32_t)((len + seg_bytes - 1) / seg_bytes);
   b.total_segs += ns;
   b.max_segs = std::max(b.max_segs, ns);
   b.bytes += len;
   b.chunks.push_back(c);
 }
-
-// Open-addressing map (chunk, 4 KiB block) -> last epoch + 1 that touched it.
-class BlockEpochs {
- public:
-  explicit BlockEpochs(size_t expect) { reset(expect); }
-  // Empties the map for `expect` keys.  Entries carry the generation that wrote them, so
-  // emptying a table that is already large enough is one increment, not a clear.
-  void reset(size_t expect) {
-    used_ = 0;
-    if (!tab_.empty() && 2 * expect <= tab_.size() && gen_ != 0xFFFFFFFFu) {
-      ++gen_;
-      return;
-    }
-    size_t cap = std::max<size_t>(1024, tab_.size());
-    while (cap < 2 * expect) cap <<= 1;
-    tab_.assign(cap, Entry{0, 0, 0});
-    mask_ = cap - 1;
-    shift_ = 64 - __builtin_ctzll(cap);
-    gen_ = 1;
-  }
-  uint32_t get(uint64_t k) const {
-    for (uint64_t h = slot(k);; h = (h + 1) & mask_) {
-      const Entry &e = tab_[h];
-      if (e.gen != gen_) return 0;
-      if (e.key == k) return e.val;
-    }
-  }
-  // The value of `k`, inserted as 0 when absent.  References stay valid until the next
-  // call that may grow the table: reserve(count) first.
-  uint32_t &at(uint64_t k) {
-    for (uint64_t h = slot(k);; h = (h + 1) & mask_) {
-      Entry &e = tab_[h];
-      if (e.gen != gen_) {
-        e = Entry{k, 0, gen_};
-        ++used_;
-        return e.val;
-      }
-      if (e.key == k) return e.val;
-    }
-  }
-  void reserve(size_t more) {
-    while (2 * (used_ + more) > tab_.size()) grow();
-  }
-  void put(uint64_t k, uint32_t v) {
-    if (2 * (used_ + 1) > tab_.size()) grow();
-    for (uint64_t h = slot(k);; h = (h + 1) & mask_) {
-      Entry &e = tab_[h];
-      if (e.gen != gen_) {
-        e = Entry{k, v, gen_};
-        ++used_;
-        return;
-      }
-      if (e.key == k) {
-        e.val = v;
-        return;
-      }
-    }
-  }
-
- private:
-  struct Entry {
-    uint64_t key;
-    uint32_t val, gen;
-  };
-  uint64_t slot(uint64_t k) const { return ((k * 0x9E3779B97F4A7C15ull) >> shift_) & mask_; }
-  void grow() {
-    std::vector<Entry> old = std::move(tab_);
-    const uint32_t g = gen_;
-    tab_.assign(old.size() * 2, Entry{0, 0, 0});
-    mask_ = tab_.size() - 1;
-    shift_ = 64 - __builtin_ctzll(tab_.size());
-    gen_ = 1;
-    used_ = 0;
-    for (const Entry &e : old)
-      if (e.gen == g) put(e.key, e.val);
-  }
-  std::vector<Entry> tab_;
-  uint64_t mask_ = 0;
-  int shift_ = 0;
-  uint32_t gen_ = 0;
-  size_t used_ = 0;
-};
 
 enum class Src : uint8_t { kInitial, kZero, kTrue };
 
@@ -319,27 +273,137 @@ struct OpOut {
   uint32_t chunk = 0;
 };
 
-// Output of the host pass (B) for one attempt.
-struct HostPass {
+// Chunk- and op-indexed state of the host pass.  With T threads, thread t owns a
+// contiguous range of chunks (and their ops), so every write here is to a disjoint entry.
+struct PassShared {
   std::vector<Track> tr;
   std::vector<uint32_t> cur;  // next free scan position per chunk
   std::vector<OpOut> outs;
   std::vector<uint32_t> raw0;
+};
+
+// One thread's job lists.  Job ids are local until the merge adds the thread's base.
+struct PassLocal {
   std::vector<CrcBatch> ep_crc;
   std::vector<std::vector<CopyPiece>> ep_copy;
   std::vector<VerifyItem> verify;  // speculative attempt: client checksums checked on the device
   uint32_t njobs = 0;
   size_t nep = 0;  // epochs in use (ep_crc / ep_copy keep their storage across calls)
-  BlockEpochs last_touch{0};
+  // last epoch + 1 per 4 KiB block of the chunk being processed, tagged with `gen` (one
+  // generation per chunk, so nothing is cleared between chunks)
+  std::vector<uint64_t> blk;
+  uint32_t gen = 0;
+  void next_chunk(uint64_t blocks) {
+    if (blk.size() < blocks || gen == 0xFFFFFFFFu) {
+      blk.assign(std::max<uint64_t>(blocks, blk.size()), 0);
+      gen = 0;
+    }
+    ++gen;
+  }
+  void clear() {
+    for (size_t e = 0; e < nep; ++e) {
+      ep_crc[e].chunks.clear();
+      ep_crc[e].total_segs = ep_crc[e].max_segs = 0;
+      ep_crc[e].bytes = 0;
+      ep_copy[e].clear();
+    }
+    nep = 0;
+    verify.clear();
+    njobs = 0;
+  }
 };
+
+// A persistent worker pool for the host pass (one per calling thread, so concurrent
+// callers never wait on each other).  run(n, fn) calls fn(0..n-1); the caller runs fn(0).
+class HostPool {
+ public:
+  explicit HostPool(unsigned workers) {
+    for (unsigned w = 0; w < workers; ++w) th_.emplace_back([this, w] { loop(w + 1); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (std::thread &t : th_) t.join();
+  }
+  unsigned size() const { return (unsigned)th_.size() + 1; }
+  void run(unsigned n, const std::function<void(unsigned)> &fn) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_ = n;
+      pending_ = n - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+  }
+
+ private:
+  void loop(unsigned id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(unsigned)> *fn;
+      unsigned n;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        fn = fn_;
+        n = n_;
+      }
+      if (id < n) {
+        (*fn)(id);
+        std::lock_guard<std::mutex> lk(mu_);
+        if (--pending_ == 0) done_.notify_one();
+      }
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(unsigned)> *fn_ = nullptr;
+  unsigned n_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+// Threads for the host pass: 1 below kParallelOps ops, else H3C_HOST_THREADS (default 8).
+constexpr uint32_t kParallelOps = 16384;
+unsigned pass_threads(uint32_t n) {
+  if (n < kParallelOps) return 1;
+  static const unsigned t = [] {
+    const char *e = std::getenv("H3C_HOST_THREADS");
+    const int v = e ? std::atoi(e) : 8;
+    return (unsigned)std::min(std::max(v, 1), 32);
+  }();
+  return t;
+}
+
+void run_threads(unsigned T, const std::function<void(unsigned)> &fn) {
+  if (T <= 1) {
+    fn(0);
+    return;
+  }
+  thread_local std::unique_ptr<HostPool> pool;
+  if (!pool || pool->size() < T) pool.reset(new HostPool(T - 1));
+  pool->run(T, fn);
+}
 
 // Per-thread host scratch, reused across calls: the pass touches tens of MB of host
 // vectors per 100k ops, and fresh allocations each call cost page faults of the same
 // order as the pass itself.
 struct UpdioScratch {
-  HostPass P;
+  PassShared S;
+  std::vector<PassLocal> L;
   CrcBatch pay;
-  std::vector<uint32_t> status, payraw, truev, start;
+  std::vector<uint32_t> status, payraw, truev, start, opstart, order, cut;
 };
 
 // Scan positions in (chunk, sequence) order, laid out before the pass: chunk c owns
@@ -358,68 +422,95 @@ uint32_t plan_positions(uint8_t poly_type, const h3c_chunk_state *chunks, uint32
   return start[nchunks];
 }
 
-// B. the host pass in sequence order.  `payraw` == nullptr: speculative (every WRITE's
-// client checksum is assumed to match and queued for the device check); otherwise the
-// payload CRCs are known and `status` already carries every mismatch.
-void host_pass(uint8_t poly_type, uint32_t poly, bool std_domain, const h3c_chunk_state *chunks, uint32_t nchunks,
-               const h3c_update_io *ios, uint32_t n, std::vector<uint32_t> &status, const uint32_t *payraw,
-               uint64_t seg_j, const std::vector<uint32_t> &start, AffIn *lay, uint32_t *keys, HostPass &P) {
-  P.tr.assign(nchunks, Track{});
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    P.tr[c].size = chunks[c].size;
-    P.tr[c].type = chunks[c].type;
-  }
-  P.cur.assign(start.begin(), start.end() - 1);
-  P.outs.assign(n, OpOut{});
-  P.raw0.assign(nchunks, 0);
-  for (size_t e = 0; e < P.nep; ++e) {
-    P.ep_crc[e].chunks.clear();
-    P.ep_crc[e].total_segs = P.ep_crc[e].max_segs = 0;
-    P.ep_crc[e].bytes = 0;
-    P.ep_copy[e].clear();
-  }
-  P.nep = 0;
-  P.verify.clear();
-  P.njobs = 0;
-  BlockEpochs &last_touch = P.last_touch;
-  last_touch.reset(n + 1024);
+// Op indices grouped by chunk, each group in sequence order (a stable counting sort):
+// the ops of chunk c are order[opstart[c] .. opstart[c+1]).  Ops naming no chunk of the
+// batch are left out; other invalid ops stay (their result reports the chunk's size).
+void group_ops(const h3c_update_io *ios, uint32_t n, uint32_t nchunks, std::vector<uint32_t> &opstart,
+               std::vector<uint32_t> &order) {
+  opstart.assign(nchunks + 1, 0);
+  for (uint32_t i = 0; i < n; ++i)
+    if (ios[i].chunk < nchunks) ++opstart[ios[i].chunk + 1];
+  for (uint32_t c = 0; c < nchunks; ++c) opstart[c + 1] += opstart[c];
+  order.resize(opstart[nchunks]);
+  std::vector<uint32_t> fill(opstart.begin(), opstart.end() - 1);
+  for (uint32_t i = 0; i < n; ++i)
+    if (ios[i].chunk < nchunks) order[fill[ios[i].chunk]++] = i;
+}
 
-  auto epoch_for = [&](uint32_t c, uint64_t a, uint64_t b) -> uint32_t {  // touched [a, b)
+// Thread t's chunks [cut[t], cut[t+1]): contiguous ranges of about n/T ops each.
+void cut_chunks(const std::vector<uint32_t> &opstart, uint32_t nchunks, unsigned T, std::vector<uint32_t> &cut) {
+  cut.assign(T + 1, nchunks);
+  cut[0] = 0;
+  const uint64_t total = opstart[nchunks];
+  uint32_t c = 0;
+  for (unsigned t = 1; t < T; ++t) {
+    const uint64_t want = total * t / T;
+    while (c < nchunks && opstart[c] < want) ++c;
+    cut[t] = std::max(c, cut[t - 1]);
+  }
+}
+
+// B. the host pass over chunks [clo, chi), each chunk's ops in sequence order.
+// `payraw` == nullptr: speculative (every WRITE's client checksum is assumed to match and
+// queued for the device check); otherwise the payload CRCs are known and `status` already
+// carries every mismatch.  S.outs (indexed like `order`, so each thread writes one
+// contiguous range: no false sharing) must hold order.size() entries and S.tr / S.cur /
+// S.raw0 nchunks;
+// this thread fills its own.
+void host_pass(uint8_t poly_type, uint32_t poly, bool std_domain, const h3c_chunk_state *chunks,
+               const h3c_update_io *ios, uint32_t *status, const uint32_t *payraw, uint64_t seg_j,
+               const uint32_t *start, const uint32_t *opstart, const uint32_t *order, AffIn *lay, uint32_t *keys,
+               uint32_t clo, uint32_t chi, PassShared &S, PassLocal &L) {
+  for (uint32_t c = clo; c < chi; ++c) {
+    S.tr[c] = Track{};
+    S.tr[c].size = chunks[c].size;
+    S.tr[c].type = chunks[c].type;
+    S.cur[c] = start[c];
+    S.raw0[c] = 0;
+  }
+  L.clear();
+  FoldCache fc;
+
+  auto epoch_for = [&](uint32_t c, uint64_t a, uint64_t b) -> uint32_t {  // touched [a, b) of chunk c
+    (void)c;
     if (b <= a) return 0;
     uint32_t e = 0;
     const uint64_t b0 = a / kConflictBlock, b1 = (b - 1) / kConflictBlock;
-    if (b0 == b1) {  // one block: a single probe
-      last_touch.reserve(1);
-      uint32_t &v = last_touch.at(((uint64_t)c << 32) | b0);
-      e = v++;
-    } else {
-      for (uint64_t k = b0; k <= b1; ++k) e = std::max(e, last_touch.get(((uint64_t)c << 32) | k));
-      for (uint64_t k = b0; k <= b1; ++k) last_touch.put(((uint64_t)c << 32) | k, e + 1);
-    }
-    if (P.nep <= e) {
-      P.nep = e + 1;
-      if (P.ep_crc.size() < P.nep) {
-        P.ep_crc.resize(P.nep);
-        P.ep_copy.resize(P.nep);
+    const uint64_t tag = (uint64_t)L.gen << 32;
+    for (uint64_t k = b0; k <= b1; ++k)
+      if ((L.blk[k] & ~0xFFFFFFFFull) == tag) e = std::max(e, (uint32_t)L.blk[k]);
+    for (uint64_t k = b0; k <= b1; ++k) L.blk[k] = tag | (e + 1);
+    if (L.nep <= e) {
+      L.nep = e + 1;
+      if (L.ep_crc.size() < L.nep) {
+        L.ep_crc.resize(L.nep);
+        L.ep_copy.resize(L.nep);
       }
     }
     return e;
   };
   auto add_copy = [&](uint32_t e, uint64_t dst, uint64_t src, uint64_t len) {
     for (uint64_t k = 0; k < len; k += kCopyPiece)
-      P.ep_copy[e].push_back(CopyPiece{dst + k, src ? src + k : 0, std::min(kCopyPiece, len - k)});
+      L.ep_copy[e].push_back(CopyPiece{dst + k, src ? src + k : 0, std::min(kCopyPiece, len - k)});
   };
   auto new_elem = [&](uint32_t c, const AffIn &a) -> uint32_t {
-    const uint32_t p = P.cur[c]++;
+    const uint32_t p = S.cur[c]++;
     lay[p] = a;
     return p;
   };
 
-  for (uint32_t i = 0; i < n; ++i) {
-    if (status[i] == H3C_ERR_INVALID_ARG) continue;
+  const uint32_t kend = opstart[chi];
+  for (uint32_t k = opstart[clo]; k < kend; ++k) {
+    if (k + 16 < kend) {  // ops are visited in chunk order: their records are scattered
+      __builtin_prefetch(&ios[order[k + 16]]);
+      __builtin_prefetch(&status[order[k + 16]]);
+    }
+    const uint32_t i = order[k];
     const h3c_update_io &io = ios[i];
     const uint32_t c = io.chunk;
-    Track &t = P.tr[c];
+    if (k == opstart[c]) L.next_chunk(((uint64_t)chunks[c].chunk_size + kConflictBlock - 1) / kConflictBlock);
+    if (status[i] == H3C_ERR_INVALID_ARG) continue;  // (marked by an earlier attempt)
+    Track &tk = S.tr[c];
     const uint64_t base = chunks[c].base;
     // A6: the client's checksum of the payload (:193-207); TRUNCATE / EXTEND carry NONE.
     if (status[i] == H3C_OK && io.checksum_type != H3C_TYPE_NONE && io.length != 0) {
@@ -429,49 +520,49 @@ void host_pass(uint8_t poly_type, uint32_t poly, bool std_domain, const h3c_chun
         const uint32_t got = std_domain ? ~payraw[i] : payraw[i];
         if (got != io.checksum_value) status[i] = H3C_ERR_CHECKSUM_MISMATCH;
       } else {
-        P.verify.push_back(VerifyItem{i, io.checksum_value});
+        L.verify.push_back(VerifyItem{i, io.checksum_value});
       }
     }
     if (status[i] == H3C_ERR_CHECKSUM_MISMATCH) {  // rejected: nothing changes
-      P.outs[i] = OpOut{t.src, t.true_pos, c};
+      S.outs[k] = OpOut{tk.src, tk.true_pos, c};
       continue;
     }
     // TRUNCATE / EXTEND store a checksum of the chunk's own type (:328-332); one of the
     // other polynomial cannot be derived from this batch's CRC state (documented limit).
-    if (io.kind != H3C_UPD_WRITE && !std_domain && t.type != H3C_TYPE_NONE && t.type != poly_type) {
+    if (io.kind != H3C_UPD_WRITE && !std_domain && tk.type != H3C_TYPE_NONE && tk.type != poly_type) {
       status[i] = H3C_ERR_INVALID_ARG;
       continue;
     }
-    if (!t.started) {  // the chunk's scan segment starts from a known CRC or an INIT reset
-      t.started = true;
+    if (!tk.started) {  // the chunk's scan segment starts from a known CRC or an INIT reset
+      tk.started = true;
       const h3c_chunk_state &cs = chunks[c];
       if (cs.size == 0) {
-        P.raw0[c] = 0xFFFFFFFFu;  // raw CRC of no bytes
+        S.raw0[c] = 0xFFFFFFFFu;  // raw CRC of no bytes
       } else if (cs.type == poly_type) {
-        P.raw0[c] = std_domain ? ~cs.value : cs.value;
+        S.raw0[c] = std_domain ? ~cs.value : cs.value;
       } else {
         const uint32_t e = epoch_for(c, 0, cs.size);
-        add_job(P.ep_crc[e], base, cs.size, 0u, P.njobs, seg_j, poly);
+        add_job(L.ep_crc[e], fc, base, cs.size, 0u, L.njobs, seg_j, poly);
         AffIn a{};
         a.kind = kAffInit;
         a.len = cs.size;
-        a.job = P.njobs++;
+        a.job = L.njobs++;
         new_elem(c, a);
       }
     }
-    const uint64_t nb = t.size;
+    const uint64_t nb = tk.size;
     uint64_t na = nb;
     AffIn a{};
     a.job = kNoJob;
-    uint8_t type_after = t.type;
+    uint8_t type_after = tk.type;
     if (io.kind == H3C_UPD_WRITE) {  // :281-291, doRealWrite :124
       const uint64_t o = io.offset, len = io.length;
       na = std::max<uint64_t>(nb, o + len);
       const uint32_t e = epoch_for(c, std::min(o, nb), (o > nb || len) ? o + len : 0);
       if (o < nb && len) {
         const uint64_t end = std::min(o + len, nb);
-        add_job(P.ep_crc[e], base + o, end - o, 0u, P.njobs, seg_j, poly);
-        a.job = P.njobs++;
+        add_job(L.ep_crc[e], fc, base + o, end - o, 0u, L.njobs, seg_j, poly);
+        a.job = L.njobs++;
         a.pad = (uint32_t)(o + len - end);
       }
       if (o > nb) add_copy(e, base + nb, 0, o - nb);
@@ -486,9 +577,9 @@ void host_pass(uint8_t poly_type, uint32_t poly, bool std_domain, const h3c_chun
       if (l < nb && io.kind == H3C_UPD_TRUNCATE) {
         na = l;
         const uint32_t e = epoch_for(c, l, nb);
-        add_job(P.ep_crc[e], base + l, nb - l, 0u, P.njobs, seg_j, poly);
+        add_job(L.ep_crc[e], fc, base + l, nb - l, 0u, L.njobs, seg_j, poly);
         a.kind = kAffTrunc;
-        a.job = P.njobs++;
+        a.job = L.njobs++;
       } else if (l > nb) {
         na = l;
         const uint32_t e = epoch_for(c, nb, l);
@@ -501,21 +592,102 @@ void host_pass(uint8_t poly_type, uint32_t poly, bool std_domain, const h3c_chun
     a.nb = (uint32_t)nb;
     a.na = (uint32_t)na;
     const uint32_t id = new_elem(c, a);
-    t.size = (uint32_t)na;
-    t.type = type_after;
+    tk.size = (uint32_t)na;
+    tk.type = type_after;
     // updateChecksum: case (i) stores 0 (:334-336); (ii)-(iv) the chunk's CRC.
     if (!std_domain && (type_after == H3C_TYPE_NONE || na == 0)) {
-      t.src = Src::kZero;
+      tk.src = Src::kZero;
     } else {
-      t.src = Src::kTrue;
-      t.true_pos = id;  // scan position
+      tk.src = Src::kTrue;
+      tk.true_pos = id;  // scan position
     }
-    P.outs[i] = OpOut{t.src, t.true_pos, c};
+    S.outs[k] = OpOut{tk.src, tk.true_pos, c};
   }
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    for (uint32_t p = P.cur[c]; p < start[c + 1]; ++p) lay[p] = AffIn{0, 0, 0, 0, 0, kNoJob, 0, kAffNop};
+  for (uint32_t c = clo; c < chi; ++c) {
+    for (uint32_t p = S.cur[c]; p < start[c + 1]; ++p) lay[p] = AffIn{0, 0, 0, 0, 0, kNoJob, 0, kAffNop};
     for (uint32_t p = start[c]; p < start[c + 1]; ++p) keys[p] = c;
   }
+}
+
+// Where the threads' lists go in the flattened per-epoch arrays (epoch-major, then thread).
+struct PassMerge {
+  size_t nep = 0, crc_total = 0, copy_total = 0, ver_total = 0;
+  uint32_t njobs = 0, max_segs = 0;
+  std::vector<uint32_t> job_base;             // [t]
+  std::vector<size_t> ver_off;                // [t]
+  std::vector<size_t> crc_off, copy_off;      // [e * T + t]
+  std::vector<uint32_t> seg_base;             // [e * T + t]: segments of earlier threads in epoch e
+  std::vector<CrcBatch> ep;                   // per-epoch totals (chunks unused)
+  std::vector<size_t> ep_crc_begin, ep_copy_begin, ep_copy_count;
+
+  void build(const std::vector<PassLocal> &L, unsigned T) {
+    nep = 0;
+    for (unsigned t = 0; t < T; ++t) nep = std::max(nep, L[t].nep);
+    job_base.assign(T, 0);
+    ver_off.assign(T, 0);
+    njobs = 0;
+    ver_total = 0;
+    for (unsigned t = 0; t < T; ++t) {
+      job_base[t] = njobs;
+      njobs += L[t].njobs;
+      ver_off[t] = ver_total;
+      ver_total += L[t].verify.size();
+    }
+    crc_off.assign(nep * T, 0);
+    copy_off.assign(nep * T, 0);
+    seg_base.assign(nep * T, 0);
+    ep.assign(nep, CrcBatch{});
+    ep_crc_begin.assign(nep, 0);
+    ep_copy_begin.assign(nep, 0);
+    ep_copy_count.assign(nep, 0);
+    crc_total = copy_total = 0;
+    max_segs = 0;
+    for (size_t e = 0; e < nep; ++e) {
+      ep_crc_begin[e] = crc_total;
+      ep_copy_begin[e] = copy_total;
+      for (unsigned t = 0; t < T; ++t) {
+        crc_off[e * T + t] = crc_total;
+        copy_off[e * T + t] = copy_total;
+        seg_base[e * T + t] = ep[e].total_segs;
+        if (e < L[t].nep) {
+          const CrcBatch &b = L[t].ep_crc[e];
+          crc_total += b.chunks.size();
+          copy_total += L[t].ep_copy[e].size();
+          ep[e].total_segs += b.total_segs;
+          ep[e].max_segs = std::max(ep[e].max_segs, b.max_segs);
+          ep[e].bytes += b.bytes;
+        }
+      }
+      ep_copy_count[e] = copy_total - ep_copy_begin[e];
+      max_segs = std::max(max_segs, ep[e].total_segs);
+    }
+  }
+  size_t ep_crc_count(size_t e) const { return (e + 1 < nep ? ep_crc_begin[e + 1] : crc_total) - ep_crc_begin[e]; }
+};
+
+// Phase 2 of the pass, per thread: its lists into the pinned staging with global job ids
+// and epoch-relative segment indices, and its scan elements' job ids made global.
+void pass_publish(const PassLocal &L, const PassMerge &M, unsigned t, unsigned T, uint32_t clo, uint32_t chi,
+                  const uint32_t *start, const PassShared &S, AffIn *lay, DevChunk *crc, CopyPiece *copy,
+                  VerifyItem *ver) {
+  const uint32_t jb = M.job_base[t];
+  for (size_t e = 0; e < L.nep; ++e) {
+    DevChunk *dst = crc + M.crc_off[e * T + t];
+    const uint32_t sb = M.seg_base[e * T + t];
+    for (const DevChunk &d : L.ep_crc[e].chunks) {
+      *dst = d;
+      dst->out_idx += jb;
+      dst->seg_begin += sb;
+      ++dst;
+    }
+    if (!L.ep_copy[e].empty())
+      std::memcpy(copy + M.copy_off[e * T + t], L.ep_copy[e].data(), L.ep_copy[e].size() * sizeof(CopyPiece));
+  }
+  if (!L.verify.empty()) std::memcpy(ver + M.ver_off[t], L.verify.data(), L.verify.size() * sizeof(VerifyItem));
+  if (jb)
+    for (uint32_t c = clo; c < chi; ++c)
+      for (uint32_t p = start[c]; p < S.cur[c]; ++p)
+        if (lay[p].job != kNoJob) lay[p].job += jb;
 }
 
 }  // namespace
@@ -534,7 +706,8 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   const uint32_t poly = poly_type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
 
   PhaseClock clk;
-  thread_local UpdioScratch ws;
+  thread_local UpdioScratch tls_ws;
+  UpdioScratch &ws = tls_ws;  // a local name: lambdas run on pool threads must not name the thread_local
   // ---- per-op validation (range :140-145, kind, client checksum type) ----
   std::vector<uint32_t> &status = ws.status;
   status.assign(n, H3C_OK);
@@ -562,16 +735,19 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   pay.chunks.clear();
   pay.total_segs = pay.max_segs = 0;
   pay.bytes = 0;
+  FoldCache fc;
   for (uint32_t i = 0; i < n; ++i)
     if (status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
-      add_job(pay, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg, poly);
+      add_job(pay, fc, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg, poly);
   clk.mark("A prepare");
 
   // B + C-D, speculatively first: the host pass assumes every client checksum matches and
   // the device checks them before any byte is written (the copy kernels are gated on the
   // check).  A mismatch (rare: a corrupted transfer) costs a second attempt with the
   // payload CRCs known.  One host <-> device round trip per batch in the common case.
-  HostPass &P = ws.P;
+  const unsigned T = std::max(1u, std::min<unsigned>(pass_threads(n), nchunks));
+  PassShared &S = ws.S;
+  if (ws.L.size() < T) ws.L.resize(T);
   std::vector<uint32_t> &payraw = ws.payraw;  // known payload CRCs (second attempt only)
   std::vector<uint32_t> &truev = ws.truev;
   // scan elements and keys are written by the pass straight into pinned staging
@@ -582,28 +758,34 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   AffIn *lay = reinterpret_cast<AffIn *>(pin_el.data());
   uint32_t *keys = reinterpret_cast<uint32_t *>(pin_el.data() + lay_bytes);
   truev.assign(npos, 0);
+  S.tr.resize(nchunks);
+  S.cur.resize(nchunks);
+  S.raw0.resize(nchunks);
+  group_ops(ios, n, nchunks, ws.opstart, ws.order);
+  S.outs.assign(ws.order.size(), OpOut{});
+  cut_chunks(ws.opstart, nchunks, T, ws.cut);
+  PassMerge M;
   for (int attempt = 0;; ++attempt) {
     const bool spec = attempt == 0;
-    host_pass(poly_type, poly, std_domain, chunks, nchunks, ios, n, status, spec ? nullptr : payraw.data(), seg,
-              ws.start, lay, keys, P);
+    run_threads(T, [&](unsigned t) {
+      host_pass(poly_type, poly, std_domain, chunks, ios, status.data(), spec ? nullptr : payraw.data(), seg,
+                ws.start.data(), ws.opstart.data(), ws.order.data(), lay, keys, ws.cut[t], ws.cut[t + 1], S,
+                ws.L[t]);
+    });
+    M.build(ws.L, T);
     clk.mark("B host");
     // ---- C-D. device: payload CRCs + check (speculative), epochs, affine scan ----
-    const uint32_t nver = (uint32_t)P.verify.size();
+    const uint32_t nver = (uint32_t)M.ver_total;
     size_t scan_tmp = 0;
     if (npos)
       HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, scan_tmp, (uint32_t *)nullptr, (Aff *)nullptr, (Aff *)nullptr,
                                              (size_t)npos, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
-    size_t crc_chunks = 0, copy_pieces = 0;
-    uint32_t max_segs = spec ? pay.total_segs : 0;
-    for (size_t e = 0; e < P.nep; ++e) {
-      crc_chunks += P.ep_crc[e].chunks.size();
-      copy_pieces += P.ep_copy[e].size();
-      max_segs = std::max(max_segs, P.ep_crc[e].total_segs);
-    }
+    const size_t crc_chunks = M.crc_total, copy_pieces = M.copy_total;
+    const uint32_t max_segs = std::max(spec ? pay.total_segs : 0u, M.max_segs);
     const size_t npay = spec ? pay.chunks.size() : 0;
     Arena a;
     const size_t bytes = (npay + crc_chunks) * sizeof(DevChunk) + copy_pieces * sizeof(CopyPiece) +
-                         nver * sizeof(VerifyItem) + 4ull * max_segs + 4ull * std::max(P.njobs, 1u) + 4ull * n +
+                         nver * sizeof(VerifyItem) + 4ull * max_segs + 4ull * std::max(M.njobs, 1u) + 4ull * n +
                          npos * (sizeof(AffIn) + 2 * sizeof(Aff) + 8) + 4ull * nchunks + 4ull * nver + scan_tmp +
                          16 * 256;
     h3c_rt::DeviceLease scratch(dev, bytes);
@@ -614,7 +796,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     CopyPiece *d_copy = a.take<CopyPiece>(copy_pieces);
     VerifyItem *d_ver = a.take<VerifyItem>(nver);
     uint32_t *d_seg = a.take<uint32_t>(max_segs);
-    uint32_t *d_jobcrc = a.take<uint32_t>(std::max(P.njobs, 1u));
+    uint32_t *d_jobcrc = a.take<uint32_t>(std::max(M.njobs, 1u));
     uint32_t *d_payraw = a.take<uint32_t>(n);
     AffIn *d_in = a.take<AffIn>(npos);
     Aff *d_aff = a.take<Aff>(npos);
@@ -640,19 +822,14 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     if (!pin.ok()) return H3C_ERR_HIP;
     char *hp = pin.data();
     if (npay) std::memcpy(hp + off[kPay], pay.chunks.data(), len[kPay]);
-    {
-      char *pc_crc = hp + off[kCrc], *pc_copy = hp + off[kCopy];
-      for (size_t e = 0; e < P.nep; ++e) {
-        const size_t bc = P.ep_crc[e].chunks.size() * sizeof(DevChunk), bp = P.ep_copy[e].size() * sizeof(CopyPiece);
-        if (bc) std::memcpy(pc_crc, P.ep_crc[e].chunks.data(), bc);
-        if (bp) std::memcpy(pc_copy, P.ep_copy[e].data(), bp);
-        pc_crc += bc;
-        pc_copy += bp;
-      }
-    }
-    if (nver) std::memcpy(hp + off[kVer], P.verify.data(), len[kVer]);
+    run_threads(T, [&](unsigned t) {
+      pass_publish(ws.L[t], M, t, T, ws.cut[t], ws.cut[t + 1], ws.start.data(), S, lay,
+                   reinterpret_cast<DevChunk *>(hp + off[kCrc]),
+                   reinterpret_cast<CopyPiece *>(hp + off[kCopy]), reinterpret_cast<VerifyItem *>(hp + off[kVer]));
+    });
     if (!spec) std::memcpy(hp + off[kPayraw], payraw.data(), len[kPayraw]);
-    std::memcpy(hp + off[kRaw0], P.raw0.data(), len[kRaw0]);
+    std::memcpy(hp + off[kRaw0], S.raw0.data(), len[kRaw0]);
+    const VerifyItem *ver_host = reinterpret_cast<const VerifyItem *>(hp + off[kVer]);
 
     int err = H3C_OK;
     auto body = [&]() -> int {
@@ -677,22 +854,20 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
         }
       }
       const uint32_t *gate = spec ? d_bad : nullptr;
-      size_t co = 0, po = 0;
-      for (size_t e = 0; e < P.nep; ++e) {
-        const CrcBatch &b = P.ep_crc[e];
-        if (!b.chunks.empty()) {
-          const int r = h3c_rt::launch_crc(st, dev, poly_type, d_crc + co, (uint32_t)b.chunks.size(), b.total_segs,
+      for (size_t e = 0; e < M.nep; ++e) {
+        const size_t nc = M.ep_crc_count(e);
+        if (nc) {
+          const CrcBatch &b = M.ep[e];
+          const int r = h3c_rt::launch_crc(st, dev, poly_type, d_crc + M.ep_crc_begin[e], (uint32_t)nc, b.total_segs,
                                            b.max_segs, b.bytes, seg, 0, d_seg, nullptr, d_jobcrc, nullptr, nullptr,
                                            -1);
           if (r) return r;
         }
-        if (!P.ep_copy[e].empty()) {
-          hipLaunchKernelGGL(updio_copy_kernel, dim3((uint32_t)P.ep_copy[e].size()), dim3(256), 0, st, d_copy + po,
-                             gate);
+        if (M.ep_copy_count[e]) {
+          hipLaunchKernelGGL(updio_copy_kernel, dim3((uint32_t)M.ep_copy_count[e]), dim3(256), 0, st,
+                             d_copy + M.ep_copy_begin[e], gate);
           HIP_TRY(hipGetLastError());
         }
-        co += b.chunks.size();
-        po += P.ep_copy[e].size();
       }
       if (npos) {
         const uint32_t tb = 256, gb = (npos + tb - 1) / tb;
@@ -725,7 +900,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
         payraw.assign(n, 0xFFFFFFFFu);
         std::memcpy(payraw.data(), hp + off[kPayBack], 4ull * n);
         for (uint32_t k = 0; k < nver; ++k)
-          if (bad[1 + k]) status[P.verify[k].op] = H3C_ERR_CHECKSUM_MISMATCH;
+          if (bad[1 + k]) status[ver_host[k].op] = H3C_ERR_CHECKSUM_MISMATCH;
         continue;
       }
     }
@@ -733,67 +908,75 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     break;
   }
 
-  // ---- E. results and final chunk states ----
-  std::vector<uint32_t> init_value(nchunks);
-  for (uint32_t c = 0; c < nchunks; ++c) init_value[c] = chunks[c].value;
-  auto value_of = [&](Src s, uint32_t id, uint32_t c) -> uint32_t {
-    if (s == Src::kZero) return 0u;
-    if (s == Src::kInitial) return init_value[c];
-    const uint32_t raw = truev[id];
-    return std_domain ? ~raw : raw;
-  };
-  // replay types and sizes in sequence order for per-op results
-  std::vector<uint32_t> size_now(nchunks);
-  std::vector<uint8_t> type_now(nchunks);
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    size_now[c] = chunks[c].size;
-    type_now[c] = chunks[c].type;
-  }
-  for (uint32_t i = 0; i < n; ++i) {
-    h3c_update_result &r = results[i];
-    std::memset(&r, 0, sizeof(r));
-    r.status = status[i];
-    const h3c_update_io &io = ios[i];
-    if (status[i] == H3C_ERR_INVALID_ARG) {  // IOResult default {NONE, 0}
-      r.size = io.chunk < nchunks ? size_now[io.chunk] : 0;
-      continue;
+  // ---- E. results and final chunk states, per chunk range on the pass's threads ----
+  for (uint32_t i = 0; i < n; ++i)
+    if (ios[i].chunk >= nchunks) {  // IOResult default {NONE, 0}
+      std::memset(&results[i], 0, sizeof(h3c_update_result));
+      results[i].status = status[i];
     }
-    const uint32_t c = io.chunk;
-    if (status[i] == H3C_OK) {
-      // size after the op (replayed exactly as in the pass)
-      const uint64_t nb = size_now[c];
-      uint64_t na = nb;
-      if (io.kind == H3C_UPD_WRITE) na = std::max<uint64_t>(nb, (uint64_t)io.offset + io.length);
-      else if (io.kind == H3C_UPD_TRUNCATE || io.length > nb) na = io.length;
-      size_now[c] = (uint32_t)na;
-      if (io.kind == H3C_UPD_WRITE) type_now[c] = io.checksum_type;
+  run_threads(T, [&](unsigned t) {
+    for (uint32_t c = ws.cut[t]; c < ws.cut[t + 1]; ++c) {
+      const uint32_t init_value = chunks[c].value;
+      auto value_of = [&](Src src, uint32_t pos) -> uint32_t {
+        if (src == Src::kZero) return 0u;
+        if (src == Src::kInitial) return init_value;
+        return std_domain ? ~truev[pos] : truev[pos];
+      };
+      // replay sizes and types in sequence order for per-op results
+      uint32_t size_now = chunks[c].size;
+      uint8_t type_now = chunks[c].type;
+      for (uint32_t k = ws.opstart[c]; k < ws.opstart[c + 1]; ++k) {
+        const uint32_t i = ws.order[k];
+        const h3c_update_io &io = ios[i];
+        h3c_update_result &r = results[i];
+        std::memset(&r, 0, sizeof(r));
+        r.status = status[i];
+        if (status[i] == H3C_ERR_INVALID_ARG) {  // IOResult default {NONE, 0}
+          r.size = size_now;
+          continue;
+        }
+        if (status[i] == H3C_OK) {  // size after the op (as in the pass)
+          uint64_t na = size_now;
+          if (io.kind == H3C_UPD_WRITE) na = std::max<uint64_t>(size_now, (uint64_t)io.offset + io.length);
+          else if (io.kind == H3C_UPD_TRUNCATE || io.length > size_now) na = io.length;
+          size_now = (uint32_t)na;
+          if (io.kind == H3C_UPD_WRITE) type_now = io.checksum_type;
+        }
+        r.size = size_now;
+        r.type = (std_domain && status[i] == H3C_OK) ? poly_type : type_now;
+        r.value = value_of(S.outs[k].src, S.outs[k].pos);
+      }
+      if (S.tr[c].started) {
+        chunks[c].size = S.tr[c].size;
+        chunks[c].type = std_domain ? poly_type : S.tr[c].type;
+        chunks[c].value = value_of(S.tr[c].src, S.tr[c].true_pos);
+      }
     }
-    r.size = size_now[c];
-    r.type = (std_domain && status[i] == H3C_OK) ? poly_type : type_now[c];
-    r.value = value_of(P.outs[i].src, P.outs[i].pos, c);
-  }
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    if (!P.tr[c].started) continue;
-    chunks[c].size = P.tr[c].size;
-    chunks[c].type = std_domain ? poly_type : P.tr[c].type;
-    chunks[c].value = value_of(P.tr[c].src, P.tr[c].true_pos, c);
-  }
+  });
   clk.mark("E results");
   if (clk.on)
-    std::fprintf(stderr, "[updio] epochs %zu, crc jobs %u, elements %u\n", P.nep, P.njobs, npos);
+    std::fprintf(stderr, "[updio] threads %u, epochs %zu, crc jobs %u, elements %u\n", T, M.nep, M.njobs, npos);
   return H3C_OK;
 }
 
 // Diagnostic hook, no device work: host time of one speculative h3c_update_ios pass over
-// `ios` (payload-job build, position plan, host pass B), the fastest of `reps`; the phase
-// split goes to stderr with H3C_UPDIO_TIMING.  Used to tune the host pass without a GPU.
+// `ios` (payload-job build, position plan, op grouping, host pass B with its merge and
+// publication into staging), the fastest of `reps`; the phase split goes to stderr with
+// H3C_UPDIO_TIMING.  Used to tune the host pass without a GPU.
 extern "C" double h3c_diag_updio_host_ms(uint8_t poly_type, const h3c_chunk_state *chunks, uint32_t nchunks,
                                          const h3c_update_io *ios, uint32_t n, int reps) {
   const uint32_t poly = poly_type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
-  thread_local UpdioScratch ws;
-  double total = 0, t_a = 0, t_b = 0;
+  thread_local UpdioScratch tls_ws;
+  UpdioScratch &ws = tls_ws;
+  double total = 0, t_a = 0, t_b = 0, t_c = 0;
   std::vector<AffIn> lay;
   std::vector<uint32_t> keys;
+  std::vector<DevChunk> crc;
+  std::vector<CopyPiece> copy;
+  std::vector<VerifyItem> ver;
+  const unsigned T = std::max(1u, std::min<unsigned>(pass_threads(n), nchunks));
+  if (ws.L.size() < T) ws.L.resize(T);
+  PassMerge M;
   for (int r = 0; r < reps; ++r) {
     const auto t0 = std::chrono::steady_clock::now();
     ws.status.assign(n, H3C_OK);
@@ -804,24 +987,49 @@ extern "C" double h3c_diag_updio_host_ms(uint8_t poly_type, const h3c_chunk_stat
     pay.chunks.clear();
     pay.total_segs = pay.max_segs = 0;
     pay.bytes = 0;
+    FoldCache fc;
     for (uint32_t i = 0; i < n; ++i)
       if (ws.status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
-        add_job(pay, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg, poly);
+        add_job(pay, fc, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg, poly);
     const uint32_t npos = plan_positions(poly_type, chunks, nchunks, ios, n, ws.status, ws.start);
     lay.resize(npos);
     keys.resize(npos);
+    ws.S.tr.resize(nchunks);
+    ws.S.cur.resize(nchunks);
+    ws.S.raw0.resize(nchunks);
+    group_ops(ios, n, nchunks, ws.opstart, ws.order);
+    ws.S.outs.assign(ws.order.size(), OpOut{});
+    cut_chunks(ws.opstart, nchunks, T, ws.cut);
     const auto t1 = std::chrono::steady_clock::now();
-    host_pass(poly_type, poly, false, chunks, nchunks, ios, n, ws.status, nullptr, seg, ws.start, lay.data(),
-              keys.data(), ws.P);
+    std::vector<double> busy(T, 0.0);
+    run_threads(T, [&](unsigned t) {
+      const auto b0 = std::chrono::steady_clock::now();
+      host_pass(poly_type, poly, false, chunks, ios, ws.status.data(), nullptr, seg, ws.start.data(),
+                ws.opstart.data(), ws.order.data(), lay.data(), keys.data(), ws.cut[t], ws.cut[t + 1], ws.S, ws.L[t]);
+      busy[t] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b0).count();
+    });
+    if (std::getenv("H3C_UPDIO_BUSY") && r == reps - 1)
+      for (unsigned t = 0; t < T; ++t) std::fprintf(stderr, "  thread %u busy %.3f ms\n", t, busy[t]);
+    M.build(ws.L, T);
     const auto t2 = std::chrono::steady_clock::now();
+    crc.resize(M.crc_total);
+    copy.resize(M.copy_total);
+    ver.resize(M.ver_total);
+    run_threads(T, [&](unsigned t) {
+      pass_publish(ws.L[t], M, t, T, ws.cut[t], ws.cut[t + 1], ws.start.data(), ws.S, lay.data(), crc.data(),
+                   copy.data(), ver.data());
+    });
+    const auto t3 = std::chrono::steady_clock::now();
     using ms = std::chrono::duration<double, std::milli>;
-    if (r == 0 || ms(t2 - t0).count() < total) {  // the fastest repetition
+    if (r == 0 || ms(t3 - t0).count() < total) {  // the fastest repetition
       t_a = ms(t1 - t0).count();
       t_b = ms(t2 - t1).count();
-      total = ms(t2 - t0).count();
+      t_c = ms(t3 - t2).count();
+      total = ms(t3 - t0).count();
     }
   }
   if (std::getenv("H3C_UPDIO_TIMING"))
-    std::fprintf(stderr, "[updio host] payload jobs + plan %.3f ms, pass %.3f ms\n", t_a, t_b);
+    std::fprintf(stderr, "[updio host] threads %u: payload jobs + plan + grouping %.3f ms, pass %.3f ms, publish %.3f ms\n",
+                 T, t_a, t_b, t_c);
   return total;
 }
