@@ -49,6 +49,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include <rocprim/device/device_scan_by_key.hpp>
 
 #include "h3c_common.hpp"
@@ -392,7 +394,12 @@ void run_threads(unsigned T, const std::function<void(unsigned)> &fn) {
     return;
   }
   thread_local std::unique_ptr<HostPool> pool;
-  if (!pool || pool->size() < T) pool.reset(new HostPool(T - 1));
+  thread_local pid_t owner = 0;
+  if (pool && owner != getpid()) (void)pool.release();  // forked child: the workers do not exist here
+  if (!pool || pool->size() < T) {
+    pool.reset(new HostPool(T - 1));
+    owner = getpid();
+  }
   pool->run(T, fn);
 }
 

@@ -147,6 +147,16 @@ def test_updio_random_mixed_ops(h3c, torch_dev, seed):
     sc.check(*sc.run())
 
 
+def test_updio_large_batch_parallel_host_pass(h3c, torch_dev):
+    """20000 mixed ops over 24 chunks: past the 16384-op threshold the host pass runs on the
+    worker pool, one contiguous chunk range per thread (and a few client checksums fail, so
+    the speculative attempt is redone)."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(20)
+    sc = random_scenario(h3c, torch, dev, rng, nchunks=24, chunk_size=64 << 10, nops=20000)
+    sc.check(*sc.run())
+
+
 def test_updio_hot_region_conflicts(h3c, torch_dev):
     """Many overlapping writes into the first 16 KiB of two chunks: long epoch chains."""
     torch, dev = torch_dev
