@@ -282,6 +282,12 @@ enum h3c_prof_kind {
 void h3c_profile_enable(int on);
 int h3c_profile_read(int kind, double *ms, uint64_t *launches, uint64_t *bytes, int reset);
 
+/* Host time (ms, fastest of `reps`) of h3c_update_ios's host side for these ops with no
+ * device work: payload-job build, scan layout, the host pass and its merge.  A tuning aid
+ * (scripts/updio_hostbench.py); `base` / `payload` fields are never dereferenced. */
+double h3c_diag_updio_host_ms(uint8_t poly_type, const h3c_chunk_state *chunks, uint32_t nchunks,
+                              const h3c_update_io *ios, uint32_t n, int reps);
+
 #ifdef __cplusplus
 }
 #endif
