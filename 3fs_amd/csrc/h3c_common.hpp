@@ -112,6 +112,7 @@ constexpr uint32_t kPolyCrc32c = 0x82F63B78u;
 constexpr uint32_t kPolyCrc32 = 0xEDB88320u;
 constexpr uint32_t kOne = 0x80000000u;  // x^0 in the reflected representation
 constexpr int kRowBytes = 1024;         // 64 lanes x 16 B
+constexpr int kQuadRowBytes = 256;      // small-chunk kernel: 16 lanes x 16 B per chunk, 4 chunks per wave
 constexpr int kWavesPerBlock = 16;
 constexpr int kThreads = kWavesPerBlock * 64;
 constexpr int kCopies = 32;
@@ -175,6 +176,7 @@ struct PolyConsts {
   // red[0] = x^-32 (one dword back), red[1+k] = x^-(8*16*2^k) (2^k lanes back), k = 0..5.
   // red[m][k][b] = (b << 8k) * C_m, so a*C_m = XOR_k red[m][k][byte k of a].
   uint32_t red[7][4][256];
+  uint32_t tabq[4][256];  // tabq[k][b] = (b << 8k) * x^(8*kQuadRowBytes): the small-chunk kernel's rows
 };
 constexpr int kRedTables = 7;
 constexpr int kRedWords = kRedTables * 4 * 256;  // 7168 dwords = 28 KiB of LDS
@@ -185,6 +187,9 @@ inline void build_consts(PolyConsts &pc, uint32_t poly) {
   const uint32_t row = hxpow8n(kRowBytes, poly);
   for (int k = 0; k < 4; ++k)
     for (uint32_t b = 0; b < 256; ++b) pc.tab[k][b] = hgf_mul(b << (8 * k), row, poly);
+  const uint32_t qrow = hxpow8n(kQuadRowBytes, poly);
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t b = 0; b < 256; ++b) pc.tabq[k][b] = hgf_mul(b << (8 * k), qrow, poly);
   const uint32_t xinv8 = hgf_pow(hx_inverse(poly), 8, poly);
   for (int l = 0; l < 64; ++l)
     for (int j = 0; j < 4; ++j) pc.fix[4 * l + j] = hgf_pow(xinv8, 16u * l + 4u * j, poly);
@@ -311,8 +316,8 @@ __device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const L
   return xor3(t0, t1, t2) ^ t3;
 }
 // LDS dword i holds table ((i>>14)<<1 | (i>>5)&1), entry (i>>6)&255.
-__device__ __forceinline__ uint32_t fill_value(const PolyConsts *__restrict__ pc, int i) {
-  return pc->tab[((i >> 14) << 1) | ((i >> 5) & 1)][(i >> 6) & 255];
+__device__ __forceinline__ uint32_t fill_value_of(const uint32_t (*tab)[256], int i) {
+  return tab[((i >> 14) << 1) | ((i >> 5) & 1)][(i >> 6) & 255];
 }
 #else
 // Layout: table k, entry b, copy c at byte address k*32 KiB + b*128 + c*4.
@@ -334,10 +339,14 @@ __device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const L
   const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3 + 32768);
   return xor3(t0, t1, t2) ^ t3;
 }
-__device__ __forceinline__ uint32_t fill_value(const PolyConsts *__restrict__ pc, int i) {
-  return pc->tab[i >> 13][(i >> 5) & 255];
+__device__ __forceinline__ uint32_t fill_value_of(const uint32_t (*tab)[256], int i) {
+  return tab[i >> 13][(i >> 5) & 255];
 }
 #endif
+// The LDS image of the 1 KiB-stride tables (rows of 64 lanes x 16 B).
+__device__ __forceinline__ uint32_t fill_value(const PolyConsts *__restrict__ pc, int i) {
+  return fill_value_of(pc->tab, i);
+}
 
 __device__ __forceinline__ uint32_t byte_mask(uint64_t d, uint64_t s, uint64_t e) {
   const uint32_t lo = s > d ? (uint32_t)min<uint64_t>(s - d, 4) : 0u;

@@ -194,7 +194,9 @@ __global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__r
           for (int u = 0; u < R; ++u)
             if ((uint32_t)u < K) {
               uint4 x = cur[u];
-              if (u == 0 || (uint32_t)u + 1 == K) x = mask_row(x, base + (uint64_t)u * kRowBytes, S, E);
+              // masks only where the chunk starts or ends inside a row (uniform branches)
+              if ((u == 0 && (S & (kRowBytes - 1))) || ((uint32_t)u + 1 == K && (E & (kRowBytes - 1))))
+                x = mask_row(x, base + (uint64_t)u * kRowBytes, S, E);
               consume(st[j], x, lb, L);
             }
 #endif
@@ -230,6 +232,138 @@ __global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__r
           }
         }
       }
+    }
+  }
+}
+
+// Kernel A'': the same batches with four chunks per wave.  A 16-lane group owns one chunk
+// and walks it in 256-byte rows (16 lanes x 16 B, tables with stride x^(8*256)); the four
+// groups' Horner passes and their 4-level shuffle trees run in the same instructions, so a
+// 4 KiB chunk pays a quarter of a wave fold instead of a whole one (the fold was about a
+// third of seg_small_kernel's instructions per chunk).
+#ifndef H3C_SMALL_QUAD
+#define H3C_SMALL_QUAD 1
+#endif
+constexpr int kQuadBatch = 4;  // rows per load batch (two batches in flight)
+
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
+
+__global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+                                                           const PolyConsts *__restrict__ pc,
+                                                           const uint32_t *__restrict__ expected,
+                                                           uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                                           uint32_t *__restrict__ mismatch) {
+  constexpr int kRed = 5 * 1024;  // x^-32 and the 4 tree levels x^-(128 * 2^k), k = 0..3
+  __shared__ uint32_t lds[kLdsWords + kRed];
+  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value_of(pc->tabq, i);
+  const uint32_t *red_g = &pc->red[0][0][0];
+  for (int i = threadIdx.x; i < kRed; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  __syncthreads();
+  const uint32_t *red = lds + kLdsWords;
+  const char *lb = reinterpret_cast<const char *>(lds);
+  const uint32_t lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t lo = (uint32_t)(gw * nchunks / nw), hi = (uint32_t)((gw + 1) * nchunks / nw);
+  if (lo >= hi) return;
+  const uint32_t poly = pc->poly;
+  const LaneLut L = make_lut(lane);
+  constexpr uint64_t kQ = kQuadRowBytes;
+  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
+    const uint32_t cnt = min(64u, hi - g0);
+    uint32_t m_plo = 0, m_phi = 0, m_len = 0, m_xs = 0, m_out = 0, m_exp = 0;
+    if (lane < cnt) {  // lane k holds chunk g0 + k's descriptor
+      const DevChunk &ch = chunks[g0 + lane];
+      m_plo = (uint32_t)ch.ptr;
+      m_phi = (uint32_t)(ch.ptr >> 32);
+      m_len = (uint32_t)ch.len;  // one short segment: below 4 GiB
+      m_xs = ch.xstart;
+      m_out = ch.out_idx;
+      if (expected) m_exp = expected[m_out];
+    }
+    // quad q0's chunk for this group: start, end, row count, this lane's first address
+    auto quad = [&](uint32_t q, uint64_t &S, uint64_t &E, uint32_t &K, uint64_t &la, uint32_t &src) {
+      const uint32_t t = q + grp;
+      const bool valid = t < cnt;
+      src = valid ? t : q;
+      S = (uint64_t)shfl32(m_plo, src) | ((uint64_t)shfl32(m_phi, src) << 32);
+      E = S + shfl32(m_len, src);
+      const uint64_t base = S & ~(kQ - 1);
+      K = valid ? (uint32_t)((E - base + kQ - 1) / kQ) : 0u;
+      la = base + 16u * gl;
+    };
+    uint64_t S, E, la;
+    uint32_t K, src;
+    quad(0, S, E, K, la, src);
+    uint4 cur[kQuadBatch], nxt[kQuadBatch];
+#pragma unroll
+    for (int b = 0; b < kQuadBatch; ++b)
+      cur[b] = (uint32_t)b < K ? load_row(la + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+    for (uint32_t q0 = 0; q0 < cnt; q0 += 4) {
+      const bool valid = q0 + grp < cnt;
+      // the next quad's first batch is loaded during this quad's last batch and fold
+      uint64_t S1 = S, E1 = E, la1 = la;
+      uint32_t K1 = 0, src1 = src;
+      if (q0 + 4 < cnt) quad(q0 + 4, S1, E1, K1, la1, src1);
+      const uint32_t kmax = max(max(__builtin_amdgcn_readlane(K, 0), __builtin_amdgcn_readlane(K, 16)),
+                                max(__builtin_amdgcn_readlane(K, 32), __builtin_amdgcn_readlane(K, 48)));
+      Streams st{0, 0, 0, 0};
+      for (uint32_t u0 = 0; u0 < kmax; u0 += kQuadBatch) {
+        const uint32_t n0 = u0 + kQuadBatch;
+        if (n0 < kmax) {  // the next batch in flight while this one is consumed
+#pragma unroll
+          for (int b = 0; b < kQuadBatch; ++b)
+            nxt[b] = n0 + b < K ? load_row(la + (uint64_t)(n0 + b) * kQ) : make_uint4(0, 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int b = 0; b < kQuadBatch; ++b)
+            nxt[b] = (uint32_t)b < K1 ? load_row(la1 + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int b = 0; b < kQuadBatch; ++b) {
+          const uint32_t u = u0 + b;
+          if (u < K) {
+            uint4 x = cur[b];
+            if ((u == 0 && (S & (kQ - 1))) || (u + 1 == K && (E & (kQ - 1))))
+              x = mask_row(x, la + (uint64_t)u * kQ, S, E);
+            consume(st, x, lb, L);
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < kQuadBatch; ++b) cur[b] = nxt[b];
+      }
+      // fold each group's 64 stream states: Horner over the lane's 4 streams with x^-32,
+      // then 4 shuffle levels inside the group (lane gl + 2^k is 16 * 2^k bytes further)
+      uint32_t v = tab_mul(st.s3, red) ^ st.s2;
+      v = tab_mul(v, red) ^ st.s1;
+      v = tab_mul(v, red) ^ st.s0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t o = (uint32_t)__shfl_down((int)v, 1u << k, 16);
+        if ((gl & ((2u << k) - 1u)) == 0) v ^= tab_mul(o, red + 1024 * (k + 1));
+      }
+      // the bytes of the last row past E were walked as zeros: remove them
+      const uint32_t pad = (uint32_t)(((E + kQ - 1) & ~(kQ - 1)) - E);
+      if (gl == 0 && valid) {
+        if (pad >> 4) v = dgf_mul(v, pc->fix[4 * (pad >> 4)], poly);
+        if (pad & 15) v = dgf_mul(v, pc->fixz[pad & 15], poly);
+      }
+      const uint32_t xs = shfl32(m_xs, src), o = shfl32(m_out, src), want = shfl32(m_exp, src);
+      if (gl == 0 && valid) {
+        const uint32_t raw = v ^ xs;
+        out_raw[o] = raw;
+        if (expected) {
+          const bool good = raw == want;
+          ok[o] = good ? 1 : 0;
+          if (!good && mismatch) atomicAdd(mismatch, 1u);
+        }
+      }
+      S = S1;
+      E = E1;
+      K = K1;
+      la = la1;
+      src = src1;
     }
   }
 }
@@ -549,7 +683,10 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
     const uint32_t blocks = std::min<uint32_t>(ctx.num_cu, (nchunks + kWavesPerBlock - 1) / kWavesPerBlock);
     ProfToken tok;
     if (prof_kind >= 0) HIP_TRY(prof_begin(st, tok));
-    if (small_rows <= 4)
+    if (H3C_SMALL_QUAD)
+      hipLaunchKernelGGL(seg_quad_kernel, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
+                         out_raw, ok, mismatch);
+    else if (small_rows <= 4)
       hipLaunchKernelGGL(seg_small_kernel<4>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
                          out_raw, ok, mismatch);
     else
