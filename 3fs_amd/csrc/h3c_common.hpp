@@ -83,8 +83,9 @@ constexpr uint32_t kFlagNone = 1u;
 
 // Segment-CRC + finalize launches over `nchunks` device descriptors (one polynomial
 // group); profiled as `prof_kind` when >= 0.  Defined in h3c_engine.hip.
-// small_rows != 0: every chunk is exactly one segment of at most small_rows (<= 8) 1 KiB
-// rows and none is NONE-flagged -- seg_small_kernel then computes and stores the results.
+// small_rows != 0: every chunk is exactly one segment of at most small_rows 1 KiB rows
+// (see small_rows_for) and none is NONE-flagged -- the small-chunk kernel then computes
+// and stores the results.
 int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint32_t nchunks, uint32_t total_segs,
                uint32_t max_chunk_segs, uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc,
                const uint32_t *expected, uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind,
@@ -93,6 +94,11 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
 inline uint32_t host_rows(uint64_t ptr, uint64_t len) {
   return len ? (uint32_t)((((ptr + len + 1023) & ~uint64_t(1023)) - (ptr & ~uint64_t(1023))) / 1024) : 0;
 }
+// launch_crc's small_rows for host descriptors `c` (laid out with max_segs segments per
+// chunk at most): their largest row count when all qualify for the small-chunk kernel, else 0.
+uint32_t small_rows_for(const DevChunk *c, size_t n, uint32_t max_segs);
+// The same from bounds alone: chunks of at most max_len bytes in at most max_segs segments.
+uint32_t small_rows_bound(uint64_t max_len, uint32_t max_segs);
 // Segment size the engine picks for a batch of `total_bytes` on device `dev`.
 uint64_t pick_seg(uint64_t total_bytes, int dev);
 }  // namespace h3c_rt

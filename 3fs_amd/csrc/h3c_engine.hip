@@ -719,6 +719,30 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
   return H3C_OK;
 }
 
+// Chunks of at most this many 1 KiB rows take the small-chunk kernel when every chunk of
+// the batch is one segment: seg_quad_kernel beats the segment kernel + finalize up to
+// 16 KiB chunks and loses from 32 KiB (profiles/r01d_small_path_threshold.txt).
+#ifndef H3C_SMALL_PATH_ROWS
+#define H3C_SMALL_PATH_ROWS (H3C_SMALL_QUAD ? 16 : 8)
+#endif
+constexpr uint32_t kSmallPathRows = H3C_SMALL_PATH_ROWS;
+
+uint32_t small_rows_bound(uint64_t max_len, uint32_t max_segs) {
+  // a range of len bytes touches at most floor(len / 1 KiB) + 2 rows, 1 + ceil for aligned
+  return max_segs == 1 && max_len && max_len <= (uint64_t)(kSmallPathRows - 1) * 1024u ? kSmallPathRows : 0;
+}
+
+uint32_t small_rows_for(const DevChunk *c, size_t n, uint32_t max_segs) {
+  if (!n || max_segs != 1) return 0;
+  uint32_t rows = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t r = host_rows(c[i].ptr, c[i].len);
+    if ((c[i].flags & kFlagNone) || c[i].len == 0 || r > kSmallPathRows) return 0;
+    rows = std::max(rows, r);
+  }
+  return rows;
+}
+
 uint64_t pick_seg(uint64_t total_bytes, int dev) { return pick_seg_bytes(total_bytes, device_num_cu(dev)); }
 }  // namespace h3c_rt
 
@@ -792,16 +816,7 @@ struct GroupLayout {
 
 // Recomputes GroupLayout::small from the final device pointers.
 void mark_small(GroupLayout &g) {
-  for (int k = 0; k < 2; ++k) {
-    bool all = !g.hc[k].empty() && g.max_segs[k] == 1;
-    uint32_t rows = 0;
-    for (const DevChunk &c : g.hc[k]) {
-      const uint32_t r = h3c_rt::host_rows(c.ptr, c.len);
-      if ((c.flags & kFlagNone) || c.len == 0 || r > kSmallRows) all = false;
-      rows = std::max(rows, r);
-    }
-    g.small[k] = all ? rows : 0;
-  }
+  for (int k = 0; k < 2; ++k) g.small[k] = h3c_rt::small_rows_for(g.hc[k].data(), g.hc[k].size(), g.max_segs[k]);
 }
 
 int layout_groups(const h3c_desc *d, size_t n, uint64_t seg_bytes, GroupLayout &g) {

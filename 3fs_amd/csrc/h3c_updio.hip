@@ -197,7 +197,7 @@ struct Arena {
 struct CrcBatch {
   std::vector<DevChunk> chunks;
   uint32_t total_segs = 0, max_segs = 0;
-  uint64_t bytes = 0;
+  uint64_t bytes = 0, max_len = 0;
 };
 
 // set_fold_consts with a one-entry cache per constant: a batch's jobs mostly share one
@@ -244,6 +244,7 @@ void add_job(CrcBatch &b, FoldCache &fc, uint64_t ptr, uint64_t len, uint32_t st
   b.total_segs += ns;
   b.max_segs = std::max(b.max_segs, ns);
   b.bytes += len;
+  b.max_len = std::max(b.max_len, len);
   b.chunks.push_back(c);
 }
 
@@ -306,7 +307,7 @@ struct PassLocal {
     for (size_t e = 0; e < nep; ++e) {
       ep_crc[e].chunks.clear();
       ep_crc[e].total_segs = ep_crc[e].max_segs = 0;
-      ep_crc[e].bytes = 0;
+      ep_crc[e].bytes = ep_crc[e].max_len = 0;
       ep_copy[e].clear();
     }
     nep = 0;
@@ -663,6 +664,7 @@ struct PassMerge {
           ep[e].total_segs += b.total_segs;
           ep[e].max_segs = std::max(ep[e].max_segs, b.max_segs);
           ep[e].bytes += b.bytes;
+          ep[e].max_len = std::max(ep[e].max_len, b.max_len);
         }
       }
       ep_copy_count[e] = copy_total - ep_copy_begin[e];
@@ -741,7 +743,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   CrcBatch &pay = ws.pay;
   pay.chunks.clear();
   pay.total_segs = pay.max_segs = 0;
-  pay.bytes = 0;
+  pay.bytes = pay.max_len = 0;
   FoldCache fc;
   for (uint32_t i = 0; i < n; ++i)
     if (status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
@@ -851,7 +853,8 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
         HIP_TRY(hipMemsetAsync(d_payraw, 0xFF, 4ull * n, st));
         if (npay) {
           const int r = h3c_rt::launch_crc(st, dev, poly_type, d_pay, (uint32_t)npay, pay.total_segs, pay.max_segs,
-                                           pay.bytes, seg, 0, d_seg, nullptr, d_payraw, nullptr, nullptr, -1);
+                                           pay.bytes, seg, 0, d_seg, nullptr, d_payraw, nullptr, nullptr, -1,
+                                           h3c_rt::small_rows_bound(pay.max_len, pay.max_segs));
           if (r) return r;
         }
         if (nver) {
@@ -867,7 +870,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
           const CrcBatch &b = M.ep[e];
           const int r = h3c_rt::launch_crc(st, dev, poly_type, d_crc + M.ep_crc_begin[e], (uint32_t)nc, b.total_segs,
                                            b.max_segs, b.bytes, seg, 0, d_seg, nullptr, d_jobcrc, nullptr, nullptr,
-                                           -1);
+                                           -1, h3c_rt::small_rows_bound(b.max_len, b.max_segs));
           if (r) return r;
         }
         if (M.ep_copy_count[e]) {
@@ -993,7 +996,7 @@ extern "C" double h3c_diag_updio_host_ms(uint8_t poly_type, const h3c_chunk_stat
     CrcBatch &pay = ws.pay;
     pay.chunks.clear();
     pay.total_segs = pay.max_segs = 0;
-    pay.bytes = 0;
+    pay.bytes = pay.max_len = 0;
     FoldCache fc;
     for (uint32_t i = 0; i < n; ++i)
       if (ws.status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
