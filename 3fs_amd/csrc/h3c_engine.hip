@@ -244,7 +244,10 @@ __global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__r
 #ifndef H3C_SMALL_QUAD
 #define H3C_SMALL_QUAD 1
 #endif
-constexpr int kQuadBatch = 4;  // rows per load batch (two batches in flight)
+#ifndef H3C_QUAD_BATCH
+#define H3C_QUAD_BATCH 4
+#endif
+constexpr int kQuadBatch = H3C_QUAD_BATCH;  // rows per load batch (two batches in flight)
 
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
 

@@ -53,3 +53,27 @@ for k in sorted(set(fetch) | set(write)):
     rb = 2 * 1024 * sum(fr) / len(fr) if fr else float("nan")
     wb = 1024 * sum(wr) / len(wr) if wr else float("nan")
     print(f"{k:62s} {rb:18.0f} {wb:16.0f}")
+
+# --json KERNEL ALG_BYTES WORKLOAD: also write the profiles/*_pmc_summary.json form that
+# bench.py's roofline() reads for `traffic` (per launch, same corrections).
+if len(sys.argv) > 2 and sys.argv[2] == "--json":
+    import json
+
+    kern, alg, workload, out = sys.argv[3], int(sys.argv[4]), sys.argv[5], sys.argv[6]
+    row = next(r for r in csv.DictReader(open(stats)) if short(r["Name"]) == kern)
+    fr, wr = fetch.get(kern, []), write.get(kern, [])
+    rb = 2 * 1024 * sum(fr) / len(fr)
+    wb = 1024 * sum(wr) / len(wr)
+    json.dump({
+        "kernel": kern,
+        kern: {"calls": int(row["Calls"]), "avg_us": float(row["AverageNs"]) / 1e3,
+               "min_us": float(row["MinNs"]) / 1e3, "pct_gpu_time": float(row["Percentage"])},
+        "pmc": {"FETCH_SIZE_kib_raw": sum(fr) / len(fr), "WRITE_SIZE_kib": sum(wr) / len(wr),
+                "hbm_read_bytes_per_launch": rb, "hbm_write_bytes_per_launch": wb,
+                "correction": "FETCH_SIZE x1024 x2 (gfx950 reports half of a wide streaming read); WRITE_SIZE x1024",
+                "traffic_bytes_per_launch": rb + wb},
+        "algorithmic_bytes_per_launch": alg,
+        "workload": workload,
+        "command": "scripts/profile.sh (rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE; --pmc WRITE_SIZE) + "
+                   "scripts/summarize_kernels.py --json",
+    }, open(out, "w"), indent=1)
