@@ -3,7 +3,7 @@
 Reference interface mirrored here (paths relative to the 3FS checkout):
 
 * ``ChecksumType``            src/fbs/storage/Common.h:66-70
-* ``ChecksumInfo::create``    src/fbs/storage/Common.h:146-177
+* ``ChecksumInfo::create``    src/fbs/storage/Common.h:146-177 (buffer and DataIterator forms)
 * ``ChecksumInfo::combine``   src/fbs/storage/Common.h:179-198 (error 4080 on type mismatch)
 * ``operator==``              src/fbs/storage/Common.h:200
 * fmt formatter (``TYPE#~value``)  src/fbs/storage/Common.h:768-773
@@ -490,6 +490,46 @@ class ChecksumInfo:
         """Common.h:146-177: NONE -> {NONE,0}; empty -> {type, start}; null with length>0 -> {NONE,0}."""
         t, v = batch_create([(data, length, starting_checksum, int(type_))], int(type_), starting_checksum, stream)
         return ChecksumInfo(ChecksumType(int(t[0])), int(v[0]))
+
+    @staticmethod
+    def memory_data_iterator(buffer, length: int):
+        """MemoryDataIterator (Common.h:126-144): (piece, size) slices of at most kChunkSize,
+        then (None, 0)."""
+        off = 0
+        while off < length:
+            size = min(length - off, ChecksumInfo.kChunkSize)
+            yield buffer[off: off + size], size
+            off += size
+        yield None, 0
+
+    @staticmethod
+    def create_from_iterator(type_: int, pieces, length: int, starting_checksum: int = 0xFFFFFFFF,
+                             stream=None) -> "ChecksumInfo":
+        """ChecksumInfo::create(type, DataIterator*, length, start) (Common.h:146-172): pieces
+        (data, size) are taken while data is not None and fewer than `length` bytes were taken
+        (a piece is taken whole); a byte count other than `length` gives {NONE, 0}.  The
+        pieces are checksummed in one GPU batch -- the first from `starting_checksum`, the
+        others from 0 -- and chained with the combine shift (crc32c_combine), which equals
+        the reference's sequential chain."""
+        if int(type_) == ChecksumType.NONE:
+            return ChecksumInfo(ChecksumType.NONE, 0)
+        items, total = [], 0
+        for data, size in pieces:
+            if data is None or total >= length:
+                break
+            total += size
+            if size:
+                items.append((data, size, starting_checksum if not items else 0, int(type_)))
+        if total != length:
+            return ChecksumInfo(ChecksumType.NONE, 0)
+        if not items:
+            return ChecksumInfo(ChecksumType(int(type_)), starting_checksum & 0xFFFFFFFF)
+        _, v = batch_create(items, int(type_), starting_checksum, stream)
+        comb = lib.h3c_crc32c_combine if int(type_) == ChecksumType.CRC32C else lib.h3c_crc32_combine
+        acc = int(v[0])
+        for k in range(1, len(items)):
+            acc = int(comb(acc, int(v[k]), items[k][1]))
+        return ChecksumInfo(ChecksumType(int(type_)), acc)
 
     def combine(self, o: "ChecksumInfo", length: int) -> None:
         """Common.h:179-198 (h3c_checksum_combine).  Raises EngineError(kChecksumMismatch)

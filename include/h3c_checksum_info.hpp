@@ -14,6 +14,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 #include "h3c_crc.h"
@@ -27,6 +28,62 @@ struct ChecksumInfo {
   uint32_t value = 0;
 
   static constexpr size_t kChunkSize = size_t(1) << 20;  // Common.h:118
+
+  // ChecksumInfo::DataIterator / MemoryDataIterator (Common.h:120-144): next() yields
+  // pieces, {nullptr, 0} at the end; the memory iterator slices at kChunkSize.
+  class DataIterator {
+   public:
+    virtual ~DataIterator() = default;
+    virtual std::pair<const uint8_t *, size_t> next() = 0;
+  };
+  class MemoryDataIterator : public DataIterator {
+   public:
+    MemoryDataIterator(const uint8_t *buffer, size_t length) : buffer_(buffer), length_(length) {}
+    std::pair<const uint8_t *, size_t> next() override {
+      if (length_ == 0) return {nullptr, 0};
+      const uint8_t *data = buffer_;
+      const size_t size = length_ < kChunkSize ? length_ : kChunkSize;
+      buffer_ += size;
+      length_ -= size;
+      return {data, size};
+    }
+
+   private:
+    const uint8_t *buffer_;
+    size_t length_;
+  };
+
+  // ChecksumInfo::create(type, DataIterator*, length, startingChecksum) (Common.h:146-172):
+  // pieces are taken while the piece pointer is non-null and fewer than `length` bytes
+  // were taken (a piece is always taken whole); a byte count other than `length` gives
+  // {NONE, 0}.  The pieces (all of memory kind `mem`) are checksummed in one batch on the
+  // GPU -- the first from `start`, the others from 0 -- and chained with the combine
+  // shift, which equals the reference's sequential crc32c(piece, previous) chain.
+  static ChecksumInfo create(ChecksumType type, DataIterator *iter, size_t length, uint32_t start = ~0U,
+                             h3c_mem mem = H3C_MEM_DEVICE, void *stream = nullptr, int *rc = nullptr) {
+    if (rc) *rc = H3C_OK;
+    if (type == ChecksumType::NONE) return ChecksumInfo{ChecksumType::NONE, 0U};
+    std::vector<h3c_desc> pieces;
+    size_t iter_bytes = 0;
+    for (auto data = iter->next(); data.first != nullptr && iter_bytes < length; data = iter->next()) {
+      iter_bytes += data.second;
+      if (data.second)
+        pieces.push_back(h3c_desc{data.first, (uint64_t)data.second, pieces.empty() ? start : 0u, (uint8_t)type,
+                                  (uint8_t)mem, 0});
+    }
+    if (iter_bytes != length) return ChecksumInfo{ChecksumType::NONE, 0U};
+    if (pieces.empty()) return ChecksumInfo{type, start};
+    std::vector<uint8_t> t(pieces.size());
+    std::vector<uint32_t> v(pieces.size());
+    const int r = h3c_batch_create(pieces.data(), pieces.size(), t.data(), v.data(), stream);
+    if (rc) *rc = r;
+    if (r != H3C_OK) return ChecksumInfo{ChecksumType::NONE, 0U};
+    uint32_t acc = v[0];
+    for (size_t k = 1; k < pieces.size(); ++k)
+      acc = type == ChecksumType::CRC32C ? h3c_crc32c_combine(acc, v[k], pieces[k].len)
+                                         : h3c_crc32_combine(acc, v[k], pieces[k].len);
+    return ChecksumInfo{type, acc};
+  }
 
   // ChecksumInfo::create(type, buffer, length, startingChecksum) (Common.h:174-177).
   // `mem` says where `buf` lives; `rc` (optional) receives the engine status.

@@ -60,8 +60,8 @@ static void gpu_tests() {
   ChecksumInfo i = ChecksumInfo::create(ChecksumType::CRC32, dev, 1000);
   CHECK(i.type == ChecksumType::CRC32 && i.value == orc_crc32_table(host.data(), 1000, ~0U));
   CHECK(ChecksumInfo::create(ChecksumType::NONE, dev, 10) == ChecksumInfo{});
-  CHECK((ChecksumInfo::create(ChecksumType::CRC32C, nullptr, 10) == ChecksumInfo{}));
-  CHECK((ChecksumInfo::create(ChecksumType::CRC32C, nullptr, 0) == ChecksumInfo{ChecksumType::CRC32C, ~0U}));
+  CHECK((ChecksumInfo::create(ChecksumType::CRC32C, (const uint8_t *)nullptr, 10) == ChecksumInfo{}));
+  CHECK((ChecksumInfo::create(ChecksumType::CRC32C, (const uint8_t *)nullptr, 0) == ChecksumInfo{ChecksumType::CRC32C, ~0U}));
   // split + combine == whole (Common.h:191 semantics)
   ChecksumInfo p = ChecksumInfo::create(ChecksumType::CRC32C, dev, 1 << 20);
   ChecksumInfo q = ChecksumInfo::create(ChecksumType::CRC32C, dev + (1 << 20), n - (1 << 20));

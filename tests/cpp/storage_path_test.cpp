@@ -12,6 +12,8 @@
 //   truncate_extend_errors     TRUNCATE / EXTEND / range / mismatch cases (ChunkReplica.cc:131-294)
 //   recalculate_read           AioReadJob::setResult's recalculate verify (BatchReadJob.cc:43-55)
 //   serde                      Checksum::calcSerde (MessageHeader.h:32-37)
+//   data_iterator              ChecksumInfo::create over a DataIterator (Common.h:120-172):
+//                              1 MiB memory slices, ragged pieces, short / overlong iteration
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -294,9 +296,61 @@ static void serde(bool gpu) {
   }
 }
 
+// Pieces handed out from a list (a ChunkDataIterator stand-in: 1 MiB preads, a short read
+// ends the data early).
+struct ListIterator : ChecksumInfo::DataIterator {
+  std::vector<std::pair<const uint8_t *, size_t>> pieces;
+  size_t k = 0;
+  std::pair<const uint8_t *, size_t> next() override {
+    return k < pieces.size() ? pieces[k++] : std::pair<const uint8_t *, size_t>{nullptr, 0};
+  }
+};
+
+static void data_iterator(bool gpu) {
+  // host-only cases: NONE, and byte counts that do not add up to the length
+  ListIterator none;
+  none.pieces = {{(const uint8_t *)"abc", 3}};
+  CHECK((ChecksumInfo::create(ChecksumType::NONE, &none, 3) == ChecksumInfo{}));
+  ListIterator shortread;
+  static const uint8_t bytes[8] = {1, 2, 3, 4, 5, 6, 7, 8};
+  shortread.pieces = {{bytes, 4}};
+  CHECK((ChecksumInfo::create(ChecksumType::CRC32C, &shortread, 8, ~0U, H3C_MEM_HOST_PAGEABLE) == ChecksumInfo{}));
+  ListIterator empty;
+  CHECK((ChecksumInfo::create(ChecksumType::CRC32C, &empty, 0, 0x1234) == ChecksumInfo{ChecksumType::CRC32C, 0x1234}));
+  if (!gpu) return;
+  const size_t n = (5u << 20) + 777;
+  std::vector<uint8_t> host(n);
+  std::mt19937_64 rng(146);
+  for (auto &b : host) b = (uint8_t)rng();
+  uint8_t *dev = nullptr;
+  CHECK(hipMalloc(&dev, n) == hipSuccess);
+  CHECK(hipMemcpy(dev, host.data(), n, hipMemcpyHostToDevice) == hipSuccess);
+  for (ChecksumType t : {ChecksumType::CRC32C, ChecksumType::CRC32}) {
+    const uint32_t want = t == ChecksumType::CRC32C ? folly_crc32c(host.data(), n, 0xABCDEF01u)
+                                                    : orc_crc32_table(host.data(), n, 0xABCDEF01u);
+    ChecksumInfo::MemoryDataIterator mem(dev, n);  // 1 MiB slices, as ChunkFileView reads
+    int rc = -1;
+    CHECK((ChecksumInfo::create(t, &mem, n, 0xABCDEF01u, H3C_MEM_DEVICE, nullptr, &rc) == ChecksumInfo{t, want}));
+    CHECK(rc == H3C_OK);
+    ListIterator ragged;  // uneven pieces, a zero-size one in the middle
+    size_t off = 0;
+    for (size_t len : {size_t(1), size_t(4095), size_t(0), size_t(3u << 20), size_t(123457)}) {
+      ragged.pieces.push_back({dev + off, len});
+      off += len;
+    }
+    ragged.pieces.push_back({dev + off, n - off});
+    CHECK((ChecksumInfo::create(t, &ragged, n, 0xABCDEF01u) == ChecksumInfo{t, want}));
+    ListIterator over;  // the last piece runs past `length`: taken whole, then the count mismatches
+    over.pieces = {{dev, 1000}, {dev + 1000, 1000}};
+    CHECK((ChecksumInfo::create(t, &over, 1500) == ChecksumInfo{}));
+  }
+  (void)hipFree(dev);
+}
+
 int main(int argc, char **argv) {
   const bool gpu = argc > 1 && std::string(argv[1]) == "gpu";
   serde(false);
+  data_iterator(gpu);
   if (gpu) {
     verify_checksum_patterns(1 << 20);
     verify_checksum_patterns(512 << 10);

@@ -156,3 +156,29 @@ def test_scalar_folly_shaped_entry_points(h3c, torch_dev):
             assert h3c.crc32c(torch.from_numpy(a).to(dev), start) == orc.crc32c(a, start)
             assert h3c.crc32(a, start) == orc.crc32(a, start)
     assert (~h3c.crc32c(b"123456789")) & MASK == 0xE3069283
+
+
+def test_create_over_data_iterator(h3c, torch_dev):
+    """ChecksumInfo::create(type, DataIterator*, length, start) (Common.h:120-172): the 1 MiB
+    MemoryDataIterator, ragged pieces (ChunkFileView's preads), and byte counts that do not
+    add up (a short read, or a last piece past `length`) -> {NONE, 0}."""
+    torch, dev = torch_dev
+    CI, T = h3c.ChecksumInfo, h3c.ChecksumType
+    rng = np.random.default_rng(146)
+    n = (3 << 20) + 4321
+    host = rng.integers(0, 256, n, dtype=np.uint8)
+    buf = torch.from_numpy(host).to(dev)
+    for t, ref in ((T.CRC32C, orc.crc32c), (T.CRC32, orc.crc32)):
+        want = ref(host, 0x1234567)
+        got = CI.create_from_iterator(t, CI.memory_data_iterator(buf, n), n, 0x1234567)
+        assert (got.type, got.value) == (t, want)
+        cuts = [0, 1, 4097, 4097, (1 << 20) + 5, n]  # a zero-size piece in the middle
+        pieces = [(buf[a:b], b - a) for a, b in zip(cuts, cuts[1:])] + [(None, 0)]
+        got = CI.create_from_iterator(t, iter(pieces), n, 0x1234567)
+        assert (got.type, got.value) == (t, want)
+        short = [(buf[:1000], 1000), (None, 0)]
+        assert CI.create_from_iterator(t, iter(short), 2000) == CI(T.NONE, 0)
+        over = [(buf[:1000], 1000), (buf[1000:2000], 1000), (None, 0)]
+        assert CI.create_from_iterator(t, iter(over), 1500) == CI(T.NONE, 0)
+        assert CI.create_from_iterator(t, iter([(None, 0)]), 0, 77) == CI(t, 77)
+    assert CI.create_from_iterator(T.NONE, iter([(buf, n)]), n) == CI(T.NONE, 0)
