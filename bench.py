@@ -209,6 +209,15 @@ class Ctx:
         return self.max_over_ranks(t1 - t0), prof
 
 
+# Measured ceilings of the access patterns themselves (no CRC work), for context beside the
+# 8 TB/s spec peak: streaming reads of per-wave contiguous segments (scripts/readbw.hip) and
+# the update kernel's random 4 KiB read-modify-write (scripts/rmwbw.hip).
+PATTERN_CEILING = {
+    "seg_crc_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
+    "upd_delta_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
+}
+
+
 def roofline(prof, peak: float, unit: str = "GB/s", bound: str = "hbm", kernel: str = "seg_crc_kernel"):
     ms, launches, nbytes = prof
     per = nbytes / max(launches, 1)
@@ -221,6 +230,9 @@ def roofline(prof, peak: float, unit: str = "GB/s", bound: str = "hbm", kernel: 
     if tr:
         r["traffic"] = int(tr[0])
         r["traffic_source"] = f"profiles/{tr[1]}"
+    if kernel in PATTERN_CEILING:
+        ceil, src = PATTERN_CEILING[kernel]
+        r["pattern_ceiling"] = {"achieved": ceil, "frac": round(achieved / ceil, 4), "source": src}
     return r
 
 
