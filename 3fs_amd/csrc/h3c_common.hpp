@@ -183,6 +183,7 @@ struct PolyConsts {
   // red[m][k][b] = (b << 8k) * C_m, so a*C_m = XOR_k red[m][k][byte k of a].
   uint32_t red[7][4][256];
   uint32_t tabq[4][256];  // tabq[k][b] = (b << 8k) * x^(8*kQuadRowBytes): the small-chunk kernel's rows
+  uint32_t tabo[4][256];  // tabo[k][b] = (b << 8k) * x^(8*128): its 8-lane (128-byte row) variant
 };
 constexpr int kRedTables = 7;
 constexpr int kRedWords = kRedTables * 4 * 256;  // 7168 dwords = 28 KiB of LDS
@@ -196,6 +197,9 @@ inline void build_consts(PolyConsts &pc, uint32_t poly) {
   const uint32_t qrow = hxpow8n(kQuadRowBytes, poly);
   for (int k = 0; k < 4; ++k)
     for (uint32_t b = 0; b < 256; ++b) pc.tabq[k][b] = hgf_mul(b << (8 * k), qrow, poly);
+  const uint32_t orow = hxpow8n(128, poly);
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t b = 0; b < 256; ++b) pc.tabo[k][b] = hgf_mul(b << (8 * k), orow, poly);
   const uint32_t xinv8 = hgf_pow(hx_inverse(poly), 8, poly);
   for (int l = 0; l < 64; ++l)
     for (int j = 0; j < 4; ++j) pc.fix[4 * l + j] = hgf_pow(xinv8, 16u * l + 4u * j, poly);

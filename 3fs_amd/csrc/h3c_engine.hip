@@ -251,20 +251,25 @@ constexpr int kQuadBatch = H3C_QUAD_BATCH;  // rows per load batch (two batches 
 
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
 
+// G lanes per chunk (16: 256-byte rows, four chunks per wave; 8: 128-byte rows, eight).
+template <int G>
 __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                            const PolyConsts *__restrict__ pc,
                                                            const uint32_t *__restrict__ expected,
                                                            uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
                                                            uint32_t *__restrict__ mismatch) {
-  constexpr int kRed = 5 * 1024;  // x^-32 and the 4 tree levels x^-(128 * 2^k), k = 0..3
+  static_assert(G == 8 || G == 16, "8 or 16 lanes per chunk");
+  constexpr int kLevels = G == 16 ? 4 : 3;  // shuffle-tree levels inside a group
+  constexpr uint32_t NG = 64 / G;           // chunks per wave step
+  constexpr int kRed = (1 + kLevels) * 1024;  // x^-32 and the tree levels x^-(128 * 2^k)
   __shared__ uint32_t lds[kLdsWords + kRed];
-  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value_of(pc->tabq, i);
+  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value_of(G == 16 ? pc->tabq : pc->tabo, i);
   const uint32_t *red_g = &pc->red[0][0][0];
   for (int i = threadIdx.x; i < kRed; i += kThreads) lds[kLdsWords + i] = red_g[i];
   __syncthreads();
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
-  const uint32_t lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
+  const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
@@ -272,7 +277,7 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
   if (lo >= hi) return;
   const uint32_t poly = pc->poly;
   const LaneLut L = make_lut(lane);
-  constexpr uint64_t kQ = kQuadRowBytes;
+  constexpr uint64_t kQ = 16u * G;
   for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
     const uint32_t cnt = min(64u, hi - g0);
     uint32_t m_plo = 0, m_phi = 0, m_len = 0, m_xs = 0, m_out = 0, m_exp = 0;
@@ -303,14 +308,15 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
 #pragma unroll
     for (int b = 0; b < kQuadBatch; ++b)
       cur[b] = (uint32_t)b < K ? load_row(la + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
-    for (uint32_t q0 = 0; q0 < cnt; q0 += 4) {
+    for (uint32_t q0 = 0; q0 < cnt; q0 += NG) {
       const bool valid = q0 + grp < cnt;
       // the next quad's first batch is loaded during this quad's last batch and fold
       uint64_t S1 = S, E1 = E, la1 = la;
       uint32_t K1 = 0, src1 = src;
-      if (q0 + 4 < cnt) quad(q0 + 4, S1, E1, K1, la1, src1);
-      const uint32_t kmax = max(max(__builtin_amdgcn_readlane(K, 0), __builtin_amdgcn_readlane(K, 16)),
-                                max(__builtin_amdgcn_readlane(K, 32), __builtin_amdgcn_readlane(K, 48)));
+      if (q0 + NG < cnt) quad(q0 + NG, S1, E1, K1, la1, src1);
+      uint32_t kmax = 0;
+#pragma unroll
+      for (uint32_t g = 0; g < NG; ++g) kmax = max(kmax, (uint32_t)__builtin_amdgcn_readlane(K, g * G));
       Streams st{0, 0, 0, 0};
       for (uint32_t u0 = 0; u0 < kmax; u0 += kQuadBatch) {
         const uint32_t n0 = u0 + kQuadBatch;
@@ -342,8 +348,8 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
       v = tab_mul(v, red) ^ st.s1;
       v = tab_mul(v, red) ^ st.s0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t o = (uint32_t)__shfl_down((int)v, 1u << k, 16);
+      for (int k = 0; k < kLevels; ++k) {
+        const uint32_t o = (uint32_t)__shfl_down((int)v, 1u << k, G);
         if ((gl & ((2u << k) - 1u)) == 0) v ^= tab_mul(o, red + 1024 * (k + 1));
       }
       // the bytes of the last row past E were walked as zeros: remove them
@@ -687,8 +693,14 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
     ProfToken tok;
     if (prof_kind >= 0) HIP_TRY(prof_begin(st, tok));
     if (H3C_SMALL_QUAD)
-      hipLaunchKernelGGL(seg_quad_kernel, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
-                         out_raw, ok, mismatch);
+      // 8 lanes per chunk up to ~5 KiB chunks (+5 % at 4 KiB), 16 above (+2 % at 8 KiB):
+      // profiles/r01d_small_lanes_ab.txt
+      if (small_rows <= 6)
+        hipLaunchKernelGGL(seg_quad_kernel<8>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
+                           out_raw, ok, mismatch);
+      else
+        hipLaunchKernelGGL(seg_quad_kernel<16>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
+                           out_raw, ok, mismatch);
     else if (small_rows <= 4)
       hipLaunchKernelGGL(seg_small_kernel<4>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
                          out_raw, ok, mismatch);
@@ -731,8 +743,9 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
 constexpr uint32_t kSmallPathRows = H3C_SMALL_PATH_ROWS;
 
 uint32_t small_rows_bound(uint64_t max_len, uint32_t max_segs) {
-  // a range of len bytes touches at most floor(len / 1 KiB) + 2 rows, 1 + ceil for aligned
-  return max_segs == 1 && max_len && max_len <= (uint64_t)(kSmallPathRows - 1) * 1024u ? kSmallPathRows : 0;
+  // a range of len bytes touches at most floor(len / 1 KiB) + 2 rows of 1 KiB
+  const uint64_t rows = max_len / 1024u + 2u;
+  return max_segs == 1 && max_len && rows <= kSmallPathRows ? (uint32_t)rows : 0;
 }
 
 uint32_t small_rows_for(const DevChunk *c, size_t n, uint32_t max_segs) {
