@@ -15,7 +15,9 @@ from .engine import (  # noqa: F401
     ChecksumInfo,
     ChecksumType,
     EngineError,
+    HostBuffer,
     HostFed,
+    device_numa_node,
     Plan,
     StatusCode,
     batch_create,
@@ -48,7 +50,9 @@ __all__ = [
     "ChecksumInfo",
     "ChecksumType",
     "EngineError",
+    "HostBuffer",
     "HostFed",
+    "device_numa_node",
     "Plan",
     "StatusCode",
     "batch_create",

@@ -15,9 +15,17 @@
 // against the expected values (ChunkReplica.cc:193-207 / BatchReadJob.cc:43-54).
 #include <hip/hip_runtime.h>
 
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cctype>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "h3c_common.hpp"
@@ -334,3 +342,85 @@ int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t 
 }
 
 }  // extern "C"
+
+// ---- NUMA-local pinned host buffers ----
+// The reference's payloads sit in RDMA-registered BufferPool memory
+// (src/storage/service/StorageOperator.cc:546-558, configs/storage_main.toml:218-222).
+// For a host-fed GPU, those pages belong on the NUMA node of the GPU's PCIe root, or every
+// H2D transfer crosses the socket interconnect.
+namespace {
+std::mutex g_host_mu;
+std::unordered_map<void *, size_t> g_host_bufs;
+
+int read_numa_node(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return -1;
+  for (char *c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+  char path[160];
+  std::snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE *f = std::fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (std::fscanf(f, "%d", &node) != 1) node = -1;
+  std::fclose(f);
+  return node;
+}
+}  // namespace
+
+extern "C" int h3c_device_numa_node(int device) { return read_numa_node(device); }
+
+extern "C" int h3c_host_alloc(int device, uint64_t bytes, void **out, int *node_out) {
+  if (!out || !bytes) return H3C_ERR_INVALID_ARG;
+  *out = nullptr;
+  int rc = h3c_init(device);
+  if (rc) return rc;
+  const long page = sysconf(_SC_PAGESIZE);
+  const size_t len = (size_t)((bytes + page - 1) / page * page);
+  void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) {
+    h3c_rt::set_error_text("h3c_host_alloc: mmap failed");
+    return H3C_ERR_HIP;
+  }
+  int node = read_numa_node(device);
+  if (node >= 0 && node < 1024) {  // prefer the GPU's node; the kernel falls back when it is full
+    unsigned long mask[1024 / (8 * sizeof(unsigned long))] = {0};
+    mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
+    const long MPOL_PREFERRED_ = 1;
+    if (syscall(SYS_mbind, p, len, MPOL_PREFERRED_, mask, (unsigned long)1024, 0u) != 0) node = -1;
+  } else {
+    node = -1;
+  }
+  std::memset(p, 0, len);  // fault the pages in under that policy
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(device);
+  const hipError_t e = hipHostRegister(p, len, hipHostRegisterDefault);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) {
+    munmap(p, len);
+    h3c_rt::set_error("h3c_host_alloc: hipHostRegister", e);
+    return H3C_ERR_HIP;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    g_host_bufs[p] = len;
+  }
+  *out = p;
+  if (node_out) *node_out = node;
+  return H3C_OK;
+}
+
+extern "C" int h3c_host_free(void *p) {
+  if (!p) return H3C_OK;
+  size_t len = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    auto it = g_host_bufs.find(p);
+    if (it == g_host_bufs.end()) return H3C_ERR_INVALID_ARG;
+    len = it->second;
+    g_host_bufs.erase(it);
+  }
+  (void)hipHostUnregister(p);
+  munmap(p, len);
+  return H3C_OK;
+}

@@ -96,6 +96,9 @@ _proto("h3c_crc32", _int, _vp, _sz, _u32, ctypes.POINTER(_u32), _vp)
 _proto("h3c_hostfed_create", _int, _int, _u64, ctypes.POINTER(_vp))
 _proto("h3c_hostfed_run", _int, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp)
 _proto("h3c_hostfed_destroy", None, _vp)
+_proto("h3c_host_alloc", _int, _int, _u64, ctypes.POINTER(_vp), ctypes.POINTER(_int))
+_proto("h3c_host_free", _int, _vp)
+_proto("h3c_device_numa_node", _int, _int)
 _proto("h3c_profile_enable", None, _int)
 _proto("h3c_profile_read", _int, _int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64), ctypes.POINTER(_u64),
        _int)
@@ -221,7 +224,9 @@ def _payload(data, length: Optional[int]):
         return arr.ctypes.data if arr.size else 0, arr.size, MemKind.HOST_PAGEABLE, (data, arr)
     if isinstance(data, np.ndarray):
         arr = np.ascontiguousarray(data)
-        return arr.ctypes.data if arr.size else 0, arr.nbytes, MemKind.HOST_PAGEABLE, arr
+        ptr = arr.ctypes.data if arr.size else 0
+        mem = MemKind.HOST_PINNED if _in_host_buffer(ptr, arr.nbytes) else MemKind.HOST_PAGEABLE
+        return ptr, arr.nbytes, mem, arr
     raise TypeError(f"unsupported payload type {type(data)!r}")
 
 
@@ -431,6 +436,38 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+_host_ranges = {}  # HostBuffer address -> size (numpy views into them are pinned payloads)
+
+
+def _in_host_buffer(ptr: int, nbytes: int) -> bool:
+    return any(a <= ptr and ptr + nbytes <= a + n for a, n in _host_ranges.items())
+
+
+def device_numa_node(device: int = 0) -> int:
+    """NUMA node of the GPU's PCIe root (h3c_device_numa_node), -1 when unknown."""
+    return lib.h3c_device_numa_node(device)
+
+
+class HostBuffer:
+    """Pinned host memory on the GPU's NUMA node (h3c_host_alloc): the host-fed analogue
+    of the storage service's RDMA BufferPool.  `array` is a uint8 numpy view; slices of it
+    are passed as pinned payloads."""
+
+    def __init__(self, device: int, nbytes: int):
+        p, node = _vp(), _int(-1)
+        _check(lib.h3c_host_alloc(device, nbytes, ctypes.byref(p), ctypes.byref(node)))
+        self.ptr, self.nbytes, self.node = int(p.value), int(nbytes), int(node.value)
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.ptr))
+        _host_ranges[self.ptr] = self.nbytes
+
+    def close(self) -> None:
+        if self.ptr:
+            _host_ranges.pop(self.ptr, None)
+            self.array = None
+            _check(lib.h3c_host_free(self.ptr))
+            self.ptr = 0
 
 
 class HostFed:

@@ -261,6 +261,15 @@ int h3c_batch_read_result(uint8_t batch_type, const h3c_read_job *jobs, size_t n
  * run.  A pipeline object must not be used by two threads at once. */
 typedef struct h3c_hostfed h3c_hostfed;
 int h3c_hostfed_create(int device, uint64_t window_bytes, h3c_hostfed **out);
+/* Pinned host memory on the NUMA node of `device`'s PCIe root (NUMA-local
+ * pinned buffers per GPU for config 5), the host-fed analogue of the storage service's
+ * RDMA BufferPool (src/storage/service/StorageOperator.cc:546-558): anonymous pages bound
+ * with mbind(MPOL_PREFERRED), faulted in, then hipHostRegister'd.  *node receives the
+ * node, or -1 when it is unknown (the memory is then pinned without a binding).  Release
+ * with h3c_host_free. */
+int h3c_host_alloc(int device, uint64_t bytes, void **out, int *node);
+int h3c_host_free(void *p);
+int h3c_device_numa_node(int device); /* -1: unknown */
 int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t *expected_raw, uint32_t *out_raw,
                     uint8_t *ok, uint64_t *n_mismatch, void *stream);
 void h3c_hostfed_destroy(h3c_hostfed *h);

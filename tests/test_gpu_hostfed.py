@@ -73,3 +73,33 @@ def test_hostfed_crc32_type(h3c, torch_dev):
     got = hf.run(bufs, type_=h3c.ChecksumType.CRC32)
     assert [int(x) for x in got] == [orc.crc32(b) for b in bufs]
     hf.close()
+
+
+def test_hostfed_numa_local_host_buffer(h3c, torch_dev):
+    """h3c_host_alloc: pinned pages on the GPU's NUMA node.  The buffer
+    reports the node the device sits on (or -1 with no binding), its numpy slices go to the
+    pipeline as pinned payloads, and the results match the oracle."""
+    from importlib import import_module
+
+    eng = import_module("3fs_amd.engine")
+    torch, dev = torch_dev
+    rng = np.random.default_rng(5)
+    lens = mixed_lengths(rng, 24)
+    total = sum(lens) + 64
+    hb = h3c.HostBuffer(0, total)
+    try:
+        assert hb.node in (-1, h3c.device_numa_node(0))
+        hb.array[:] = rng.integers(0, 256, total, dtype=np.uint8)
+        items, want, off = [], [], 5
+        for L in lens:
+            items.append((hb.array[off: off + L], L))
+            want.append(orc.crc32c(hb.array[off: off + L]))
+            off += L
+        assert eng._payload(items[0][0], None)[2] == eng.MemKind.HOST_PINNED
+        hf = h3c.HostFed(0, 8 << 20)
+        raw, ok, nbad = hf.run(items, expected=want)
+        hf.close()
+        assert nbad == 0 and ok.all() and [int(x) for x in raw] == want
+    finally:
+        hb.close()
+    assert not eng._in_host_buffer(hb.ptr or 1, 1)
