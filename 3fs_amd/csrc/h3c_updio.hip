@@ -705,6 +705,11 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
                               uint32_t n, h3c_update_result *results, uint32_t flags, void *stream) {
   if (poly_type != H3C_TYPE_CRC32C && poly_type != H3C_TYPE_CRC32) return H3C_ERR_INVALID_ARG;
   if ((n && (!ios || !results)) || (nchunks && !chunks) || n >= 0x7FFFFFFFu) return H3C_ERR_INVALID_ARG;
+  for (uint32_t c = 0; c < nchunks; ++c)  // a chunk longer than its capacity is a caller bug
+    if (chunks[c].size > chunks[c].chunk_size) {
+      h3c_rt::set_error_text("h3c_update_ios: a chunk's size exceeds its chunk_size");
+      return H3C_ERR_INVALID_ARG;
+    }
   if (n == 0) return H3C_OK;
   const bool std_domain = (flags & H3C_UPD_STD_DOMAIN) != 0;
   int dev = 0;

@@ -196,7 +196,8 @@ typedef struct h3c_update_result {
  * `poly_type` (the client's chunk_checksum_type), else the op fails with
  * H3C_ERR_INVALID_ARG; so does a TRUNCATE / EXTEND of a chunk whose stored checksum is
  * of the other polynomial.  `chunks` and `results` are host arrays; chunk bytes are
- * updated in place on device.  Synchronous on `stream`. */
+ * updated in place on device.  Synchronous on `stream`.  A chunk whose size exceeds its
+ * chunk_size fails the whole call with H3C_ERR_INVALID_ARG, before any work. */
 int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios, uint32_t n,
                    h3c_update_result *results, uint32_t flags, void *stream);
 

@@ -85,3 +85,20 @@ def test_no_gpu_fails_loudly(h3c):
     with pytest.raises(h3c.EngineError) as ei:
         h3c.batch_create([b"abc"])
     assert ei.value.code in (9001, 9002)
+
+
+def test_update_ios_rejects_inconsistent_chunk_state(h3c):
+    """A chunk state whose size exceeds its chunk_size is a caller bug: the whole call fails
+    with kInvalidArg before any device work (so this runs without a GPU)."""
+    import numpy as np
+
+    chunks = np.zeros(2, dtype=h3c.CHUNK_STATE_DTYPE)
+    chunks["base"] = 1 << 40
+    chunks["chunk_size"] = 4096
+    chunks["size"] = [4096, 4097]
+    chunks["type"] = 1
+    ios = np.zeros(1, dtype=h3c.UPDATE_IO_DTYPE)
+    ios["kind"] = h3c.UPD_WRITE
+    with pytest.raises(h3c.EngineError) as ei:
+        h3c.update_ios(chunks, ios)
+    assert ei.value.code == 3
