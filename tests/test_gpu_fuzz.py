@@ -21,12 +21,16 @@ def torch_dev():
     return torch, torch.device("cuda:0")
 
 
-def random_batch(rng, n, pool_bytes, small_only=False):
-    """n descriptors (offset, length, type, start, mem) into a pool of pool_bytes."""
+def random_batch(rng, n, pool_bytes, small_only=0):
+    """n descriptors (offset, length, type, start, mem) into a pool of pool_bytes; with
+    small_only, lengths up to that many bytes, all device-resident and typed (a batch the
+    small-chunk kernel takes whole: 8-lane groups up to ~5 KiB, 16-lane groups above)."""
     out = []
     for _ in range(n):
         u = rng.random()
-        if small_only or u < 0.45:
+        if small_only:
+            ln = int(rng.integers(1, small_only + 1))
+        elif u < 0.45:
             ln = int(rng.integers(1, 16 << 10))
         elif u < 0.55:
             ln = 0
@@ -52,7 +56,7 @@ def test_fuzz_mixed_batches_create_and_verify(h3c, torch_dev, seed):
     host = rng.integers(0, 256, pool, dtype=np.uint8)
     dbuf = torch.from_numpy(host).to(dev)
     pinned = torch.from_numpy(host).pin_memory()
-    for small_only in (False, True):
+    for small_only in (0, 4096, 8192):
         batch = random_batch(rng, 300, pool, small_only)
         items, want = [], []
         for off, ln, t, start, mem in batch:
@@ -83,7 +87,7 @@ def test_fuzz_device_plan_matches_batch(h3c, torch_dev):
     pool = 24 << 20
     host = rng.integers(0, 256, pool, dtype=np.uint8)
     dbuf = torch.from_numpy(host).to(dev)
-    for small_only in (False, True):
+    for small_only in (0, 4096, 8192):
         batch = [b for b in random_batch(rng, 400, pool, small_only) if b[4] == "dev" and b[2] != 0]
         d = np.zeros(len(batch), dtype=h3c.engine.DESC_DTYPE)
         for i, (off, ln, t, start, _) in enumerate(batch):
