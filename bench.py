@@ -214,6 +214,7 @@ class Ctx:
 # the update kernel's random 4 KiB read-modify-write (scripts/rmwbw.hip).
 PATTERN_CEILING = {
     "seg_crc_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
+    "seg_quad_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
     "upd_delta_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
 }
 
@@ -286,15 +287,16 @@ def run_verify(args, cx: Ctx) -> dict:
         "dtype": "u8",
         "data": "synthetic (splitmix64 chunks generated in HBM; 5% of chunks carry one flipped bit)",
         "config": {
-            "workload": f"batched CRC32C verify of {n} x {clen >> 10} KiB device-resident chunks per GPU "
-                        f"(BASELINE config 2)",
+            "workload": f"batched CRC32C verify of {n} x {clen >> 10} KiB device-resident chunks per GPU"
+                        + (" (BASELINE config 2)" if (n, clen) == (8192, 1 << 20) else " (chunk-size sweep)"),
             "chunks_per_gpu": n,
             "chunk_bytes": clen,
             "parallelism": f"shard{cx.world}",
         },
         "verified": verified,
         "pct_hbm_peak": round(100.0 * (n * clen) / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 2),
-        "roofline": roofline(prof, HBM_PEAK_GBPS),
+        # chunks of <= 16 KiB (one segment each) run the small-chunk kernel
+        "roofline": roofline(prof, HBM_PEAK_GBPS, kernel="seg_quad_kernel" if clen <= (16 << 10) else "seg_crc_kernel"),
     }
     if cx.world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(stored_host, clen, args.cpu_seconds)

@@ -22,6 +22,8 @@ def short(name):
             if key in name:
                 return "rocprim::" + key
         return "rocprim::" + name[:40]
+    if name.startswith("void "):  # template kernels carry their return type
+        name = name[5:]
     return name.split("(")[0].split("<")[0][:60]
 
 
