@@ -411,6 +411,7 @@ struct UpdioScratch {
   PassShared S;
   std::vector<PassLocal> L;
   CrcBatch pay;
+  std::vector<CrcBatch> pay_parts;  // payload CRC jobs per op range
   std::vector<uint32_t> status, payraw, truev, start, opstart, order, cut;
 };
 
@@ -722,44 +723,72 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   PhaseClock clk;
   thread_local UpdioScratch tls_ws;
   UpdioScratch &ws = tls_ws;  // a local name: lambdas run on pool threads must not name the thread_local
-  // ---- per-op validation (range :140-145, kind, client checksum type) ----
+  const unsigned T = std::max(1u, std::min<unsigned>(pass_threads(n), nchunks));
+  // ---- per-op validation (range :140-145, kind, client checksum type), by op range ----
   std::vector<uint32_t> &status = ws.status;
-  status.assign(n, H3C_OK);
+  status.resize(n);
+  std::vector<uint64_t> part_bytes(T, 0);
+  run_threads(T, [&](unsigned t) {
+    const uint32_t i0 = (uint32_t)((uint64_t)n * t / T), i1 = (uint32_t)((uint64_t)n * (t + 1) / T);
+    uint64_t pb = 0;
+    for (uint32_t i = i0; i < i1; ++i) {
+      const h3c_update_io &io = ios[i];
+      status[i] = H3C_OK;
+      const bool kind_ok = io.kind == H3C_UPD_WRITE || io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND;
+      if (io.chunk >= nchunks || !kind_ok) {
+        status[i] = H3C_ERR_INVALID_ARG;
+        continue;
+      }
+      const h3c_chunk_state &c = chunks[io.chunk];
+      if (io.offset >= c.chunk_size || (uint64_t)io.offset + io.length > c.chunk_size || !c.base ||
+          (io.checksum_type != H3C_TYPE_NONE && io.checksum_type != poly_type) ||
+          (io.kind == H3C_UPD_WRITE && io.length && !io.payload)) {
+        status[i] = H3C_ERR_INVALID_ARG;
+        continue;
+      }
+      if (io.kind == H3C_UPD_WRITE) pb += io.length;
+    }
+    part_bytes[t] = pb;
+  });
   uint64_t pay_bytes = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    const h3c_update_io &io = ios[i];
-    const bool kind_ok = io.kind == H3C_UPD_WRITE || io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND;
-    if (io.chunk >= nchunks || !kind_ok) {
-      status[i] = H3C_ERR_INVALID_ARG;
-      continue;
-    }
-    const h3c_chunk_state &c = chunks[io.chunk];
-    if (io.offset >= c.chunk_size || (uint64_t)io.offset + io.length > c.chunk_size || !c.base ||
-        (io.checksum_type != H3C_TYPE_NONE && io.checksum_type != poly_type) ||
-        (io.kind == H3C_UPD_WRITE && io.length && !io.payload)) {
-      status[i] = H3C_ERR_INVALID_ARG;
-      continue;
-    }
-    if (io.kind == H3C_UPD_WRITE) pay_bytes += io.length;
-  }
-  // A. payload CRC jobs (raw, init ~0) of every valid WRITE: run on the device in the same
-  // stream as the update itself; the old-range CRC jobs of B use the same segment size.
+  for (unsigned t = 0; t < T; ++t) pay_bytes += part_bytes[t];
+  // A. payload CRC jobs (raw, init ~0) of every valid WRITE, built per op range: run on the
+  // device in the same stream as the update itself; the old-range CRC jobs of B use the
+  // same segment size.  `pay` holds the totals; the parts are published into staging.
   const uint64_t seg = h3c_rt::pick_seg(pay_bytes, dev);
-  CrcBatch &pay = ws.pay;
+  if (ws.pay_parts.size() < T) ws.pay_parts.resize(T);
+  run_threads(T, [&](unsigned t) {
+    CrcBatch &b = ws.pay_parts[t];
+    b.chunks.clear();
+    b.total_segs = b.max_segs = 0;
+    b.bytes = b.max_len = 0;
+    FoldCache fc;
+    const uint32_t i0 = (uint32_t)((uint64_t)n * t / T), i1 = (uint32_t)((uint64_t)n * (t + 1) / T);
+    for (uint32_t i = i0; i < i1; ++i)
+      if (status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
+        add_job(b, fc, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg, poly);
+  });
+  CrcBatch &pay = ws.pay;  // totals only (its chunk list stays empty)
   pay.chunks.clear();
   pay.total_segs = pay.max_segs = 0;
   pay.bytes = pay.max_len = 0;
-  FoldCache fc;
-  for (uint32_t i = 0; i < n; ++i)
-    if (status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
-      add_job(pay, fc, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg, poly);
+  std::vector<size_t> pay_off(T + 1, 0);
+  std::vector<uint32_t> pay_seg_base(T, 0);
+  for (unsigned t = 0; t < T; ++t) {
+    const CrcBatch &b = ws.pay_parts[t];
+    pay_off[t + 1] = pay_off[t] + b.chunks.size();
+    pay_seg_base[t] = pay.total_segs;
+    pay.total_segs += b.total_segs;
+    pay.max_segs = std::max(pay.max_segs, b.max_segs);
+    pay.bytes += b.bytes;
+    pay.max_len = std::max(pay.max_len, b.max_len);
+  }
   clk.mark("A prepare");
 
   // B + C-D, speculatively first: the host pass assumes every client checksum matches and
   // the device checks them before any byte is written (the copy kernels are gated on the
   // check).  A mismatch (rare: a corrupted transfer) costs a second attempt with the
   // payload CRCs known.  One host <-> device round trip per batch in the common case.
-  const unsigned T = std::max(1u, std::min<unsigned>(pass_threads(n), nchunks));
   PassShared &S = ws.S;
   if (ws.L.size() < T) ws.L.resize(T);
   std::vector<uint32_t> &payraw = ws.payraw;  // known payload CRCs (second attempt only)
@@ -796,7 +825,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
                                              (size_t)npos, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
     const size_t crc_chunks = M.crc_total, copy_pieces = M.copy_total;
     const uint32_t max_segs = std::max(spec ? pay.total_segs : 0u, M.max_segs);
-    const size_t npay = spec ? pay.chunks.size() : 0;
+    const size_t npay = spec ? pay_off[T] : 0;
     Arena a;
     const size_t bytes = (npay + crc_chunks) * sizeof(DevChunk) + copy_pieces * sizeof(CopyPiece) +
                          nver * sizeof(VerifyItem) + 4ull * max_segs + 4ull * std::max(M.njobs, 1u) + 4ull * n +
@@ -835,7 +864,15 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     h3c_rt::PinnedLease pin(off[kAll]);
     if (!pin.ok()) return H3C_ERR_HIP;
     char *hp = pin.data();
-    if (npay) std::memcpy(hp + off[kPay], pay.chunks.data(), len[kPay]);
+    if (npay)
+      run_threads(T, [&](unsigned t) {
+        DevChunk *dst = reinterpret_cast<DevChunk *>(hp + off[kPay]) + pay_off[t];
+        for (const DevChunk &d : ws.pay_parts[t].chunks) {
+          *dst = d;
+          dst->seg_begin += pay_seg_base[t];
+          ++dst;
+        }
+      });
     run_threads(T, [&](unsigned t) {
       pass_publish(ws.L[t], M, t, T, ws.cut[t], ws.cut[t + 1], ws.start.data(), S, lay,
                    reinterpret_cast<DevChunk *>(hp + off[kCrc]),
@@ -974,7 +1011,8 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   return H3C_OK;
 }
 
-// Diagnostic hook, no device work: host time of one speculative h3c_update_ios pass over
+// Diagnostic hook, no device work (the payload-job build here is single-threaded; the
+// call itself builds it per op range on the pool): host time of one speculative h3c_update_ios pass over
 // `ios` (payload-job build, position plan, op grouping, host pass B with its merge and
 // publication into staging), the fastest of `reps`; the phase split goes to stderr with
 // H3C_UPDIO_TIMING.  Used to tune the host pass without a GPU.
