@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -404,6 +405,15 @@ void run_threads(unsigned T, const std::function<void(unsigned)> &fn) {
   pool->run(T, fn);
 }
 
+// fn(k) for k in [0, ntasks) on T pool threads that pull tasks from a shared counter: a
+// thread the OS runs slowly (the GPU boxes share their cores) takes fewer tasks.
+void run_tasks(unsigned T, unsigned ntasks, const std::function<void(unsigned)> &fn) {
+  std::atomic<unsigned> next{0};
+  run_threads(std::min(T, ntasks), [&](unsigned) {
+    for (unsigned k; (k = next.fetch_add(1, std::memory_order_relaxed)) < ntasks;) fn(k);
+  });
+}
+
 // Per-thread host scratch, reused across calls: the pass touches tens of MB of host
 // vectors per 100k ops, and fresh allocations each call cost page faults of the same
 // order as the pass itself.
@@ -470,14 +480,11 @@ void host_pass(uint8_t poly_type, uint32_t poly, bool std_domain, const h3c_chun
                const h3c_update_io *ios, uint32_t *status, const uint32_t *payraw, uint64_t seg_j,
                const uint32_t *start, const uint32_t *opstart, const uint32_t *order, AffIn *lay, uint32_t *keys,
                uint32_t clo, uint32_t chi, PassShared &S, PassLocal &L) {
-  for (uint32_t c = clo; c < chi; ++c) {
-    S.tr[c] = Track{};
-    S.tr[c].size = chunks[c].size;
-    S.tr[c].type = chunks[c].type;
-    S.cur[c] = start[c];
-    S.raw0[c] = 0;
-  }
   L.clear();
+  // The current chunk's state lives in locals and is stored once per chunk: S.tr / S.cur /
+  // S.raw0 entries of neighbouring chunks share cache lines across threads.
+  Track tk;
+  uint32_t cur = 0, raw0 = 0;
   FoldCache fc;
 
   auto epoch_for = [&](uint32_t c, uint64_t a, uint64_t b) -> uint32_t {  // touched [a, b) of chunk c
@@ -502,118 +509,124 @@ void host_pass(uint8_t poly_type, uint32_t poly, bool std_domain, const h3c_chun
     for (uint64_t k = 0; k < len; k += kCopyPiece)
       L.ep_copy[e].push_back(CopyPiece{dst + k, src ? src + k : 0, std::min(kCopyPiece, len - k)});
   };
-  auto new_elem = [&](uint32_t c, const AffIn &a) -> uint32_t {
-    const uint32_t p = S.cur[c]++;
+  auto new_elem = [&](const AffIn &a) -> uint32_t {
+    const uint32_t p = cur++;
     lay[p] = a;
     return p;
   };
 
   const uint32_t kend = opstart[chi];
-  for (uint32_t k = opstart[clo]; k < kend; ++k) {
-    if (k + 16 < kend) {  // ops are visited in chunk order: their records are scattered
-      __builtin_prefetch(&ios[order[k + 16]]);
-      __builtin_prefetch(&status[order[k + 16]]);
-    }
-    const uint32_t i = order[k];
-    const h3c_update_io &io = ios[i];
-    const uint32_t c = io.chunk;
-    if (k == opstart[c]) L.next_chunk(((uint64_t)chunks[c].chunk_size + kConflictBlock - 1) / kConflictBlock);
-    if (status[i] == H3C_ERR_INVALID_ARG) continue;  // (marked by an earlier attempt)
-    Track &tk = S.tr[c];
-    const uint64_t base = chunks[c].base;
-    // A6: the client's checksum of the payload (:193-207); TRUNCATE / EXTEND carry NONE.
-    if (status[i] == H3C_OK && io.checksum_type != H3C_TYPE_NONE && io.length != 0) {
-      if (io.kind != H3C_UPD_WRITE) {
-        status[i] = H3C_ERR_CHECKSUM_MISMATCH;
-      } else if (payraw) {
-        const uint32_t got = std_domain ? ~payraw[i] : payraw[i];
-        if (got != io.checksum_value) status[i] = H3C_ERR_CHECKSUM_MISMATCH;
-      } else {
-        L.verify.push_back(VerifyItem{i, io.checksum_value});
-      }
-    }
-    if (status[i] == H3C_ERR_CHECKSUM_MISMATCH) {  // rejected: nothing changes
-      S.outs[k] = OpOut{tk.src, tk.true_pos, c};
-      continue;
-    }
-    // TRUNCATE / EXTEND store a checksum of the chunk's own type (:328-332); one of the
-    // other polynomial cannot be derived from this batch's CRC state (documented limit).
-    if (io.kind != H3C_UPD_WRITE && !std_domain && tk.type != H3C_TYPE_NONE && tk.type != poly_type) {
-      status[i] = H3C_ERR_INVALID_ARG;
-      continue;
-    }
-    if (!tk.started) {  // the chunk's scan segment starts from a known CRC or an INIT reset
-      tk.started = true;
-      const h3c_chunk_state &cs = chunks[c];
-      if (cs.size == 0) {
-        S.raw0[c] = 0xFFFFFFFFu;  // raw CRC of no bytes
-      } else if (cs.type == poly_type) {
-        S.raw0[c] = std_domain ? ~cs.value : cs.value;
-      } else {
-        const uint32_t e = epoch_for(c, 0, cs.size);
-        add_job(L.ep_crc[e], fc, base, cs.size, 0u, L.njobs, seg_j, poly);
-        AffIn a{};
-        a.kind = kAffInit;
-        a.len = cs.size;
-        a.job = L.njobs++;
-        new_elem(c, a);
-      }
-    }
-    const uint64_t nb = tk.size;
-    uint64_t na = nb;
-    AffIn a{};
-    a.job = kNoJob;
-    uint8_t type_after = tk.type;
-    if (io.kind == H3C_UPD_WRITE) {  // :281-291, doRealWrite :124
-      const uint64_t o = io.offset, len = io.length;
-      na = std::max<uint64_t>(nb, o + len);
-      const uint32_t e = epoch_for(c, std::min(o, nb), (o > nb || len) ? o + len : 0);
-      if (o < nb && len) {
-        const uint64_t end = std::min(o + len, nb);
-        add_job(L.ep_crc[e], fc, base + o, end - o, 0u, L.njobs, seg_j, poly);
-        a.job = L.njobs++;
-        a.pad = (uint32_t)(o + len - end);
-      }
-      if (o > nb) add_copy(e, base + nb, 0, o - nb);
-      if (len) add_copy(e, base + o, io.payload, len);
-      a.kind = kAffWrite;
-      a.len = (uint32_t)len;
-      a.tail = (uint32_t)(na - o - len);
-      a.op = i;
-      type_after = io.checksum_type;
-    } else {  // TRUNCATE / EXTEND (:260-273)
-      const uint64_t l = io.length;
-      if (l < nb && io.kind == H3C_UPD_TRUNCATE) {
-        na = l;
-        const uint32_t e = epoch_for(c, l, nb);
-        add_job(L.ep_crc[e], fc, base + l, nb - l, 0u, L.njobs, seg_j, poly);
-        a.kind = kAffTrunc;
-        a.job = L.njobs++;
-      } else if (l > nb) {
-        na = l;
-        const uint32_t e = epoch_for(c, nb, l);
-        add_copy(e, base + nb, 0, l - nb);
-        a.kind = kAffGrow;
-      } else {
-        a.kind = kAffNop;
-      }
-    }
-    a.nb = (uint32_t)nb;
-    a.na = (uint32_t)na;
-    const uint32_t id = new_elem(c, a);
-    tk.size = (uint32_t)na;
-    tk.type = type_after;
-    // updateChecksum: case (i) stores 0 (:334-336); (ii)-(iv) the chunk's CRC.
-    if (!std_domain && (type_after == H3C_TYPE_NONE || na == 0)) {
-      tk.src = Src::kZero;
-    } else {
-      tk.src = Src::kTrue;
-      tk.true_pos = id;  // scan position
-    }
-    S.outs[k] = OpOut{tk.src, tk.true_pos, c};
-  }
   for (uint32_t c = clo; c < chi; ++c) {
-    for (uint32_t p = S.cur[c]; p < start[c + 1]; ++p) lay[p] = AffIn{0, 0, 0, 0, 0, kNoJob, 0, kAffNop};
+    tk = Track{};
+    tk.size = chunks[c].size;
+    tk.type = chunks[c].type;
+    cur = start[c];
+    raw0 = 0;
+    L.next_chunk(((uint64_t)chunks[c].chunk_size + kConflictBlock - 1) / kConflictBlock);
+    for (uint32_t k = opstart[c]; k < opstart[c + 1]; ++k) {
+      if (k + 16 < kend) {  // ops are visited in chunk order: their records are scattered
+        __builtin_prefetch(&ios[order[k + 16]]);
+        __builtin_prefetch(&status[order[k + 16]]);
+      }
+      const uint32_t i = order[k];
+      const h3c_update_io &io = ios[i];
+      if (status[i] == H3C_ERR_INVALID_ARG) continue;  // (marked by an earlier attempt)
+      const uint64_t base = chunks[c].base;
+      // A6: the client's checksum of the payload (:193-207); TRUNCATE / EXTEND carry NONE.
+      if (status[i] == H3C_OK && io.checksum_type != H3C_TYPE_NONE && io.length != 0) {
+        if (io.kind != H3C_UPD_WRITE) {
+          status[i] = H3C_ERR_CHECKSUM_MISMATCH;
+        } else if (payraw) {
+          const uint32_t got = std_domain ? ~payraw[i] : payraw[i];
+          if (got != io.checksum_value) status[i] = H3C_ERR_CHECKSUM_MISMATCH;
+        } else {
+          L.verify.push_back(VerifyItem{i, io.checksum_value});
+        }
+      }
+      if (status[i] == H3C_ERR_CHECKSUM_MISMATCH) {  // rejected: nothing changes
+        S.outs[k] = OpOut{tk.src, tk.true_pos, c};
+        continue;
+      }
+      // TRUNCATE / EXTEND store a checksum of the chunk's own type (:328-332); one of the
+      // other polynomial cannot be derived from this batch's CRC state (documented limit).
+      if (io.kind != H3C_UPD_WRITE && !std_domain && tk.type != H3C_TYPE_NONE && tk.type != poly_type) {
+        status[i] = H3C_ERR_INVALID_ARG;
+        continue;
+      }
+      if (!tk.started) {  // the chunk's scan segment starts from a known CRC or an INIT reset
+        tk.started = true;
+        const h3c_chunk_state &cs = chunks[c];
+        if (cs.size == 0) {
+          raw0 = 0xFFFFFFFFu;  // raw CRC of no bytes
+        } else if (cs.type == poly_type) {
+          raw0 = std_domain ? ~cs.value : cs.value;
+        } else {
+          const uint32_t e = epoch_for(c, 0, cs.size);
+          add_job(L.ep_crc[e], fc, base, cs.size, 0u, L.njobs, seg_j, poly);
+          AffIn a{};
+          a.kind = kAffInit;
+          a.len = cs.size;
+          a.job = L.njobs++;
+          new_elem(a);
+        }
+      }
+      const uint64_t nb = tk.size;
+      uint64_t na = nb;
+      AffIn a{};
+      a.job = kNoJob;
+      uint8_t type_after = tk.type;
+      if (io.kind == H3C_UPD_WRITE) {  // :281-291, doRealWrite :124
+        const uint64_t o = io.offset, len = io.length;
+        na = std::max<uint64_t>(nb, o + len);
+        const uint32_t e = epoch_for(c, std::min(o, nb), (o > nb || len) ? o + len : 0);
+        if (o < nb && len) {
+          const uint64_t end = std::min(o + len, nb);
+          add_job(L.ep_crc[e], fc, base + o, end - o, 0u, L.njobs, seg_j, poly);
+          a.job = L.njobs++;
+          a.pad = (uint32_t)(o + len - end);
+        }
+        if (o > nb) add_copy(e, base + nb, 0, o - nb);
+        if (len) add_copy(e, base + o, io.payload, len);
+        a.kind = kAffWrite;
+        a.len = (uint32_t)len;
+        a.tail = (uint32_t)(na - o - len);
+        a.op = i;
+        type_after = io.checksum_type;
+      } else {  // TRUNCATE / EXTEND (:260-273)
+        const uint64_t l = io.length;
+        if (l < nb && io.kind == H3C_UPD_TRUNCATE) {
+          na = l;
+          const uint32_t e = epoch_for(c, l, nb);
+          add_job(L.ep_crc[e], fc, base + l, nb - l, 0u, L.njobs, seg_j, poly);
+          a.kind = kAffTrunc;
+          a.job = L.njobs++;
+        } else if (l > nb) {
+          na = l;
+          const uint32_t e = epoch_for(c, nb, l);
+          add_copy(e, base + nb, 0, l - nb);
+          a.kind = kAffGrow;
+        } else {
+          a.kind = kAffNop;
+        }
+      }
+      a.nb = (uint32_t)nb;
+      a.na = (uint32_t)na;
+      const uint32_t id = new_elem(a);
+      tk.size = (uint32_t)na;
+      tk.type = type_after;
+      // updateChecksum: case (i) stores 0 (:334-336); (ii)-(iv) the chunk's CRC.
+      if (!std_domain && (type_after == H3C_TYPE_NONE || na == 0)) {
+        tk.src = Src::kZero;
+      } else {
+        tk.src = Src::kTrue;
+        tk.true_pos = id;  // scan position
+      }
+      S.outs[k] = OpOut{tk.src, tk.true_pos, c};
+    }
+    S.tr[c] = tk;
+    S.cur[c] = cur;
+    S.raw0[c] = raw0;
+    for (uint32_t p = cur; p < start[c + 1]; ++p) lay[p] = AffIn{0, 0, 0, 0, 0, kNoJob, 0, kAffNop};
     for (uint32_t p = start[c]; p < start[c + 1]; ++p) keys[p] = c;
   }
 }
@@ -790,7 +803,9 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   // check).  A mismatch (rare: a corrupted transfer) costs a second attempt with the
   // payload CRCs known.  One host <-> device round trip per batch in the common case.
   PassShared &S = ws.S;
-  if (ws.L.size() < T) ws.L.resize(T);
+  // the pass runs as NT chunk-range tasks (4 per thread) pulled by the T threads
+  const unsigned NT = std::max(1u, std::min<unsigned>(T == 1 ? 1u : 4u * T, nchunks));
+  if (ws.L.size() < NT) ws.L.resize(NT);
   std::vector<uint32_t> &payraw = ws.payraw;  // known payload CRCs (second attempt only)
   std::vector<uint32_t> &truev = ws.truev;
   // scan elements and keys are written by the pass straight into pinned staging
@@ -806,17 +821,18 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   S.raw0.resize(nchunks);
   group_ops(ios, n, nchunks, ws.opstart, ws.order);
   S.outs.assign(ws.order.size(), OpOut{});
-  cut_chunks(ws.opstart, nchunks, T, ws.cut);
+  cut_chunks(ws.opstart, nchunks, NT, ws.cut);
+  clk.mark("B layout");
   PassMerge M;
   for (int attempt = 0;; ++attempt) {
     const bool spec = attempt == 0;
-    run_threads(T, [&](unsigned t) {
+    run_tasks(T, NT, [&](unsigned k) {
       host_pass(poly_type, poly, std_domain, chunks, ios, status.data(), spec ? nullptr : payraw.data(), seg,
-                ws.start.data(), ws.opstart.data(), ws.order.data(), lay, keys, ws.cut[t], ws.cut[t + 1], S,
-                ws.L[t]);
+                ws.start.data(), ws.opstart.data(), ws.order.data(), lay, keys, ws.cut[k], ws.cut[k + 1], S,
+                ws.L[k]);
     });
-    M.build(ws.L, T);
-    clk.mark("B host");
+    M.build(ws.L, NT);
+    clk.mark("B pass");
     // ---- C-D. device: payload CRCs + check (speculative), epochs, affine scan ----
     const uint32_t nver = (uint32_t)M.ver_total;
     size_t scan_tmp = 0;
@@ -873,8 +889,8 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
           ++dst;
         }
       });
-    run_threads(T, [&](unsigned t) {
-      pass_publish(ws.L[t], M, t, T, ws.cut[t], ws.cut[t + 1], ws.start.data(), S, lay,
+    run_tasks(T, NT, [&](unsigned k) {
+      pass_publish(ws.L[k], M, k, NT, ws.cut[k], ws.cut[k + 1], ws.start.data(), S, lay,
                    reinterpret_cast<DevChunk *>(hp + off[kCrc]),
                    reinterpret_cast<CopyPiece *>(hp + off[kCopy]), reinterpret_cast<VerifyItem *>(hp + off[kVer]));
     });
@@ -966,8 +982,8 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
       std::memset(&results[i], 0, sizeof(h3c_update_result));
       results[i].status = status[i];
     }
-  run_threads(T, [&](unsigned t) {
-    for (uint32_t c = ws.cut[t]; c < ws.cut[t + 1]; ++c) {
+  run_tasks(T, NT, [&](unsigned k) {
+    for (uint32_t c = ws.cut[k]; c < ws.cut[k + 1]; ++c) {
       const uint32_t init_value = chunks[c].value;
       auto value_of = [&](Src src, uint32_t pos) -> uint32_t {
         if (src == Src::kZero) return 0u;
@@ -1007,7 +1023,8 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   });
   clk.mark("E results");
   if (clk.on)
-    std::fprintf(stderr, "[updio] threads %u, epochs %zu, crc jobs %u, elements %u\n", T, M.nep, M.njobs, npos);
+    std::fprintf(stderr, "[updio] threads %u, tasks %u, epochs %zu, crc jobs %u, elements %u\n", T, NT, M.nep,
+                 M.njobs, npos);
   return H3C_OK;
 }
 
@@ -1028,7 +1045,8 @@ extern "C" double h3c_diag_updio_host_ms(uint8_t poly_type, const h3c_chunk_stat
   std::vector<CopyPiece> copy;
   std::vector<VerifyItem> ver;
   const unsigned T = std::max(1u, std::min<unsigned>(pass_threads(n), nchunks));
-  if (ws.L.size() < T) ws.L.resize(T);
+  const unsigned NT = std::max(1u, std::min<unsigned>(T == 1 ? 1u : 4u * T, nchunks));
+  if (ws.L.size() < NT) ws.L.resize(NT);
   PassMerge M;
   for (int r = 0; r < reps; ++r) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -1052,24 +1070,24 @@ extern "C" double h3c_diag_updio_host_ms(uint8_t poly_type, const h3c_chunk_stat
     ws.S.raw0.resize(nchunks);
     group_ops(ios, n, nchunks, ws.opstart, ws.order);
     ws.S.outs.assign(ws.order.size(), OpOut{});
-    cut_chunks(ws.opstart, nchunks, T, ws.cut);
+    cut_chunks(ws.opstart, nchunks, NT, ws.cut);
     const auto t1 = std::chrono::steady_clock::now();
-    std::vector<double> busy(T, 0.0);
-    run_threads(T, [&](unsigned t) {
+    std::vector<double> busy(NT, 0.0);
+    run_tasks(T, NT, [&](unsigned k) {
       const auto b0 = std::chrono::steady_clock::now();
       host_pass(poly_type, poly, false, chunks, ios, ws.status.data(), nullptr, seg, ws.start.data(),
-                ws.opstart.data(), ws.order.data(), lay.data(), keys.data(), ws.cut[t], ws.cut[t + 1], ws.S, ws.L[t]);
-      busy[t] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b0).count();
+                ws.opstart.data(), ws.order.data(), lay.data(), keys.data(), ws.cut[k], ws.cut[k + 1], ws.S, ws.L[k]);
+      busy[k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b0).count();
     });
     if (std::getenv("H3C_UPDIO_BUSY") && r == reps - 1)
-      for (unsigned t = 0; t < T; ++t) std::fprintf(stderr, "  thread %u busy %.3f ms\n", t, busy[t]);
-    M.build(ws.L, T);
+      for (unsigned k = 0; k < NT; ++k) std::fprintf(stderr, "  task %u busy %.3f ms\n", k, busy[k]);
+    M.build(ws.L, NT);
     const auto t2 = std::chrono::steady_clock::now();
     crc.resize(M.crc_total);
     copy.resize(M.copy_total);
     ver.resize(M.ver_total);
-    run_threads(T, [&](unsigned t) {
-      pass_publish(ws.L[t], M, t, T, ws.cut[t], ws.cut[t + 1], ws.start.data(), ws.S, lay.data(), crc.data(),
+    run_tasks(T, NT, [&](unsigned k) {
+      pass_publish(ws.L[k], M, k, NT, ws.cut[k], ws.cut[k + 1], ws.start.data(), ws.S, lay.data(), crc.data(),
                    copy.data(), ver.data());
     });
     const auto t3 = std::chrono::steady_clock::now();
