@@ -422,7 +422,7 @@ struct UpdioScratch {
   std::vector<PassLocal> L;
   CrcBatch pay;
   std::vector<CrcBatch> pay_parts;  // payload CRC jobs per op range
-  std::vector<uint32_t> status, payraw, truev, start, opstart, order, cut;
+  std::vector<uint32_t> status, payraw, truev, start, opstart, order, cut, hist;
 };
 
 // Scan positions in (chunk, sequence) order, laid out before the pass: chunk c owns
@@ -454,6 +454,63 @@ void group_ops(const h3c_update_io *ios, uint32_t n, uint32_t nchunks, std::vect
   std::vector<uint32_t> fill(opstart.begin(), opstart.end() - 1);
   for (uint32_t i = 0; i < n; ++i)
     if (ios[i].chunk < nchunks) order[fill[ios[i].chunk]++] = i;
+}
+
+// plan_positions + group_ops in one parallel counting sort (per-op-range histograms,
+// prefix, stable scatter) when the per-thread histograms are small against the batch.
+void layout_ops(uint8_t poly_type, const h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
+                uint32_t n, const std::vector<uint32_t> &status, unsigned T, std::vector<uint32_t> &start,
+                std::vector<uint32_t> &opstart, std::vector<uint32_t> &order, std::vector<uint32_t> &hist) {
+  if (T <= 1 || (uint64_t)nchunks * 4 > n) {
+    plan_positions(poly_type, chunks, nchunks, ios, n, status, start);
+    group_ops(ios, n, nchunks, opstart, order);
+    return;
+  }
+  // hist[t][c]: ops of range t naming chunk c; hist[T + t][c]: of those, the ones that passed validation
+  hist.resize((size_t)2 * T * nchunks);
+  auto range = [&](unsigned t, uint32_t &i0, uint32_t &i1) {
+    i0 = (uint32_t)((uint64_t)n * t / T);
+    i1 = (uint32_t)((uint64_t)n * (t + 1) / T);
+  };
+  run_threads(T, [&](unsigned t) {
+    uint32_t *all = &hist[(size_t)t * nchunks], *ok = &hist[(size_t)(T + t) * nchunks];
+    std::fill(all, all + nchunks, 0u);
+    std::fill(ok, ok + nchunks, 0u);
+    uint32_t i0, i1;
+    range(t, i0, i1);
+    for (uint32_t i = i0; i < i1; ++i) {
+      const uint32_t c = ios[i].chunk;
+      if (c >= nchunks) continue;
+      ++all[c];
+      ok[c] += status[i] != H3C_ERR_INVALID_ARG;
+    }
+  });
+  start.resize(nchunks + 1);
+  opstart.resize(nchunks + 1);
+  uint32_t pos = 0, op = 0;
+  for (uint32_t c = 0; c < nchunks; ++c) {
+    start[c] = pos;
+    opstart[c] = op;
+    uint32_t nok = 0;
+    for (unsigned t = 0; t < T; ++t) {
+      uint32_t &a = hist[(size_t)t * nchunks + c];
+      const uint32_t na = a;
+      a = op;  // becomes range t's scatter base for chunk c
+      op += na;
+      nok += hist[(size_t)(T + t) * nchunks + c];
+    }
+    pos += nok + (nok && chunks[c].size != 0 && chunks[c].type != poly_type ? 1u : 0u);
+  }
+  start[nchunks] = pos;
+  opstart[nchunks] = op;
+  order.resize(op);
+  run_threads(T, [&](unsigned t) {
+    uint32_t *base = &hist[(size_t)t * nchunks];
+    uint32_t i0, i1;
+    range(t, i0, i1);
+    for (uint32_t i = i0; i < i1; ++i)
+      if (ios[i].chunk < nchunks) order[base[ios[i].chunk]++] = i;
+  });
 }
 
 // Thread t's chunks [cut[t], cut[t+1]): contiguous ranges of about n/T ops each.
@@ -809,18 +866,18 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   std::vector<uint32_t> &payraw = ws.payraw;  // known payload CRCs (second attempt only)
   std::vector<uint32_t> &truev = ws.truev;
   // scan elements and keys are written by the pass straight into pinned staging
-  const uint32_t npos = plan_positions(poly_type, chunks, nchunks, ios, n, status, ws.start);
+  layout_ops(poly_type, chunks, nchunks, ios, n, status, T, ws.start, ws.opstart, ws.order, ws.hist);
+  const uint32_t npos = ws.start[nchunks];
   const size_t lay_bytes = ((size_t)npos * sizeof(AffIn) + 255) & ~size_t(255);
   h3c_rt::PinnedLease pin_el(lay_bytes + 4ull * npos + 256);
   if (!pin_el.ok()) return H3C_ERR_HIP;
   AffIn *lay = reinterpret_cast<AffIn *>(pin_el.data());
   uint32_t *keys = reinterpret_cast<uint32_t *>(pin_el.data() + lay_bytes);
-  truev.assign(npos, 0);
+  truev.resize(npos);  // every entry is filled from the device before it is read
   S.tr.resize(nchunks);
   S.cur.resize(nchunks);
   S.raw0.resize(nchunks);
-  group_ops(ios, n, nchunks, ws.opstart, ws.order);
-  S.outs.assign(ws.order.size(), OpOut{});
+  S.outs.resize(ws.order.size());  // written by the pass for every op it accepts, read only for those
   cut_chunks(ws.opstart, nchunks, NT, ws.cut);
   clk.mark("B layout");
   PassMerge M;

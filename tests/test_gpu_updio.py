@@ -154,6 +154,11 @@ def test_updio_large_batch_parallel_host_pass(h3c, torch_dev):
     torch, dev = torch_dev
     rng = np.random.default_rng(20)
     sc = random_scenario(h3c, torch, dev, rng, nchunks=24, chunk_size=64 << 10, nops=20000)
+    for k in range(40):  # ops naming no chunk of the batch, spread through the sequence
+        sc.add(orc.UPD_WRITE, 24 + k % 3, 0, 10)
+        for _ in range(int(rng.integers(1, 400))):
+            c = int(rng.integers(0, 24))
+            sc.add(orc.UPD_WRITE, c, int(rng.integers(0, 60 << 10)), int(rng.integers(0, 4096)))
     sc.check(*sc.run())
 
 
