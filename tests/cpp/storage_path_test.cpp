@@ -11,6 +11,7 @@
 //                              every result against orc_chunk_replica_update op by op
 //   truncate_extend_errors     TRUNCATE / EXTEND / range / mismatch cases (ChunkReplica.cc:131-294)
 //   recalculate_read           AioReadJob::setResult's recalculate verify (BatchReadJob.cc:43-55)
+//   large_parallel_batch       20000 mixed UpdateIOs (the parallel host pass) vs the replica oracle
 //   serde                      Checksum::calcSerde (MessageHeader.h:32-37)
 //   data_iterator              ChecksumInfo::create over a DataIterator (Common.h:120-172):
 //                              1 MiB memory slices, ragged pieces, short / overlong iteration
@@ -296,6 +297,66 @@ static void serde(bool gpu) {
   }
 }
 
+// A batch past the 16384-op threshold, so the host pass runs on the worker pool: random
+// WRITE / TRUNCATE / EXTEND over 24 chunks (a few with bad client checksums, a few naming
+// no chunk), every result against orc_chunk_replica_update op by op.
+static void large_parallel_batch() {
+  const uint32_t nch = 24, cs = 64 << 10, nops = 20000;
+  std::mt19937_64 rng(2024);
+  DeviceChunks store(nch, cs);
+  std::vector<uint8_t> pool(1 << 20);
+  for (auto &b : pool) b = (uint8_t)rng();
+  uint8_t *dpool = nullptr;
+  CHECK(hipMalloc(&dpool, pool.size()) == hipSuccess);
+  CHECK(hipMemcpy(dpool, pool.data(), pool.size(), hipMemcpyHostToDevice) == hipSuccess);
+  std::vector<UpdateIO> ios(nops);
+  std::vector<uint32_t> src(nops, 0);
+  for (uint32_t i = 0; i < nops; ++i) {
+    UpdateIO &io = ios[i];
+    io.chunk = (uint32_t)(rng() % nch);
+    if (i % 997 == 5) io.chunk = nch + (uint32_t)(rng() % 3);  // no such chunk
+    const uint32_t u = (uint32_t)(rng() % 100);
+    if (u < 80) {
+      io.offset = (uint32_t)(rng() % cs);
+      io.length = (uint32_t)(rng() % std::min<uint32_t>(cs - io.offset, 9000));
+      src[i] = (uint32_t)(rng() % (pool.size() - 9000));
+      io.data = dpool + src[i];
+      if (rng() % 10) {
+        io.checksum = ChecksumInfo{ChecksumType::CRC32C, folly_crc32c(pool.data() + src[i], io.length)};
+        if (rng() % 50 == 0) io.checksum.value ^= 4;  // corrupted in flight
+      }
+    } else {
+      io.updateType = u < 90 ? UpdateType::TRUNCATE : UpdateType::EXTEND;
+      io.length = (uint32_t)(rng() % (cs + 1));
+    }
+  }
+  std::vector<IOResult> res;
+  CHECK(ChunkReplicaBatch::update(store.metas, ios, res) == H3C_OK);
+  std::vector<std::vector<uint8_t>> host(nch, std::vector<uint8_t>(cs, 0));
+  std::vector<orc_chunk_meta> om(nch, orc_chunk_meta{0, 0, 0});
+  size_t bad = 0;
+  for (uint32_t i = 0; i < nops; ++i) {
+    const UpdateIO &io = ios[i];
+    if (io.chunk >= nch) {
+      CHECK(res[i].status == kInvalidArg);
+      continue;
+    }
+    orc_update_io oi{(uint8_t)io.updateType, io.offset, io.length, (uint8_t)io.checksum.type, io.checksum.value};
+    orc_update_result orr;
+    orc_chunk_replica_update(&om[io.chunk], host[io.chunk].data(), cs, &oi,
+                             io.isWrite() ? pool.data() + src[i] : nullptr, &orr);
+    if ((uint32_t)orr.status != res[i].status || orr.size != res[i].chunkLength ||
+        (orr.status == 0 && orr.value != res[i].checksum.value))
+      ++bad;
+  }
+  CHECK(bad == 0);
+  for (uint32_t c = 0; c < nch; ++c) {
+    CHECK(store.metas[c].size == om[c].size && store.metas[c].checksumValue == om[c].checksum_value);
+    CHECK(d2h(store.metas[c].bytes, om[c].size) == std::vector<uint8_t>(host[c].begin(), host[c].begin() + om[c].size));
+  }
+  (void)hipFree(dpool);
+}
+
 // Pieces handed out from a list (a ChunkDataIterator stand-in: 1 MiB preads, a short read
 // ends the data early).
 struct ListIterator : ChecksumInfo::DataIterator {
@@ -357,6 +418,7 @@ int main(int argc, char **argv) {
     batched_vs_replica(1 << 20);
     truncate_extend_errors();
     recalculate_read();
+    large_parallel_batch();
     serde(true);
   }
   if (fails) {
