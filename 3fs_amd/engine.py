@@ -577,5 +577,34 @@ class ChecksumInfo:
             raise EngineError(rc, f"different type {self} != {o}")
         self.type, self.value = ChecksumType(t.value), int(v.value)
 
+    def serialize(self) -> bytes:
+        """serde binary form (src/common/serde/Serde.h:267-290, DownwardBytes): Varint32 table
+        length, then type (1 byte) and value (4 bytes, little endian); TestCommonStruct.cc:46-56
+        pins the size (6) and the round trip."""
+        return bytes([5, int(self.type)]) + int(self.value & 0xFFFFFFFF).to_bytes(4, "little")
+
+    @staticmethod
+    def deserialize(data: bytes) -> "ChecksumInfo":
+        """Inverse of serialize; fields missing at the end of the table keep their defaults
+        (Serde.h:499-507).  Raises EngineError(kInvalidArg) on a short or malformed buffer."""
+        tlen, k, shift = 0, 0, 0
+        while True:
+            if k >= len(data) or shift > 28:
+                raise EngineError(StatusCode.kInvalidArg, "serde: short varint")
+            tlen |= (data[k] & 0x7F) << shift
+            k += 1
+            if not data[k - 1] & 0x80:
+                break
+            shift += 7
+        if tlen > len(data) - k or 1 < tlen < 5:
+            raise EngineError(StatusCode.kInvalidArg, "serde: short table")
+        t = data[k: k + tlen]
+        o = ChecksumInfo()
+        if tlen >= 1:
+            o.type = ChecksumType(t[0])
+        if tlen >= 5:
+            o.value = int.from_bytes(t[1:5], "little")
+        return o
+
     def __str__(self) -> str:  # Common.h:768-773
         return f"{ChecksumType(self.type).name}#{(~self.value) & 0xFFFFFFFF:08X}"

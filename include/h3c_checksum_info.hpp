@@ -14,6 +14,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -124,6 +125,35 @@ struct ChecksumInfo {
         value = h3c_crc32_combine(~value, o.value, length);
         return H3C_OK;
     }
+    return H3C_OK;
+  }
+
+  // serde binary form (src/common/serde/Serde.h:267-290, DownwardBytes): a Varint32 table
+  // length, then the fields in order -- type (1 byte), value (4 bytes, little endian).
+  // TestCommonStruct.cc:46-56 pins the size (1 + 1 + 4) and the round trip.
+  std::string serialize() const {
+    std::string out(6, '\0');
+    out[0] = 5;
+    out[1] = (char)type;
+    for (int k = 0; k < 4; ++k) out[2 + k] = (char)((value >> (8 * k)) & 0xFF);
+    return out;
+  }
+  // Returns 0, or H3C_ERR_INVALID_ARG for a short or malformed buffer; fields missing at
+  // the end of the table keep their values (Serde.h:499-507).
+  static int deserialize(ChecksumInfo &o, const void *data, size_t len) {
+    const uint8_t *p = static_cast<const uint8_t *>(data);
+    uint64_t tlen = 0;
+    size_t k = 0;
+    for (int shift = 0;; shift += 7) {  // Varint32 length prefix
+      if (k >= len || shift > 28) return H3C_ERR_INVALID_ARG;
+      tlen |= (uint64_t)(p[k] & 0x7F) << shift;
+      if (!(p[k++] & 0x80)) break;
+    }
+    if (tlen > len - k) return H3C_ERR_INVALID_ARG;
+    const uint8_t *t = p + k;
+    if (tlen >= 1) o.type = (ChecksumType)t[0];
+    if (tlen >= 5) o.value = (uint32_t)t[1] | (uint32_t)t[2] << 8 | (uint32_t)t[3] << 16 | (uint32_t)t[4] << 24;
+    else if (tlen > 1) return H3C_ERR_INVALID_ARG;  // a truncated value field
     return H3C_OK;
   }
 

@@ -38,6 +38,15 @@ static void cpu_tests() {
   ChecksumInfo z{ChecksumType::CRC32C, 5};
   CHECK(z.combine({ChecksumType::CRC32C, 9}, 0) == 0 && z.value == 5);
   CHECK(z.combine({ChecksumType::CRC32, 9}, 4) == 4080);
+  // serde (TestCommonStruct.cc:46-56): 1 + 1 + 4 bytes, round trip
+  {
+    ChecksumInfo ser{ChecksumType::CRC32, 0xff};
+    const std::string out = ser.serialize();
+    CHECK(out.size() == 1 + 1 + 4);
+    ChecksumInfo des;
+    CHECK(ChecksumInfo::deserialize(des, out.data(), out.size()) == 0 && des == ser);
+    CHECK(ChecksumInfo::deserialize(des, out.data(), 3) != 0);
+  }
   // TestFolly.cc:9-18
   uint32_t c1 = orc_crc32c_table((const uint8_t *)"hello", 5, 0), c2 = orc_crc32c_table((const uint8_t *)"world", 5, 0);
   CHECK(h3c_crc32c_combine(c1, c2, 5) == orc_crc32c_table((const uint8_t *)"world", 5, c1));

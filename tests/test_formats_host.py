@@ -73,3 +73,21 @@ def test_serde_mark():
             assert m == (crc0 & ~0xFF) | 0x86 | comp
             fm = importlib.import_module("3fs_amd.formats")
             assert fm.is_serde_message(m) and fm.is_compressed(m) == bool(comp)
+
+
+def test_checksum_info_serde_roundtrip(h3c):
+    """ChecksumInfo serde (TestCommonStruct.cc:46-56): {CRC32, 0xff} serializes to 1 + 1 + 4
+    bytes and deserializes back equal.  The byte layout (Varint32 table length, then type and
+    little-endian value) is restated from Serde.h; the reference test pins size and round
+    trip only."""
+    CI, T = h3c.ChecksumInfo, h3c.ChecksumType
+    ser = CI(T.CRC32, 0xFF)
+    out = ser.serialize()
+    assert len(out) == 1 + 1 + 4 and out == b"\x05\x02\xff\x00\x00\x00"
+    assert CI.deserialize(out) == ser
+    for t, v in ((T.CRC32C, 0xE3069283 ^ 0xFFFFFFFF), (T.NONE, 0)):
+        assert CI.deserialize(CI(t, v).serialize()) == CI(t, v)
+    assert CI.deserialize(b"\x01\x01") == CI(T.CRC32C, 0)  # missing trailing field keeps its default
+    for bad in (b"", b"\x80", b"\x05\x02\xff", b"\x03\x01\x00\x00"):
+        with pytest.raises(h3c.EngineError):
+            CI.deserialize(bad)
