@@ -90,6 +90,10 @@ __host__ __device__ inline uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly
 struct AffOp {  // apply a, then b
   uint32_t poly;
   __host__ __device__ Aff operator()(const Aff &a, const Aff &b) const {
+    // most ops leave the chunk length unchanged (m = 1: overwrites inside the chunk), and
+    // then composing them is a XOR, not two bit-serial GF(2) multiplies
+    if (b.m == kOne) return Aff{a.m, a.e ^ b.e};
+    if (a.m == kOne) return Aff{b.m, gf_mul(a.e, b.m, poly) ^ b.e};
     return Aff{gf_mul(a.m, b.m, poly), gf_mul(a.e, b.m, poly) ^ b.e};
   }
 };
@@ -178,7 +182,8 @@ __global__ void updio_true_kernel(const Aff *__restrict__ scan, const uint32_t *
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npos) return;
   const Aff a = scan[p];
-  out[p] = dgf_mul(raw0[key[p]], a.m, poly) ^ a.e;
+  const uint32_t r0 = raw0[key[p]];
+  out[p] = (a.m == kOne ? r0 : dgf_mul(r0, a.m, poly)) ^ a.e;
 }
 
 // Device arena for one call: every buffer is carved from one pooled device lease
