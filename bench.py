@@ -479,11 +479,18 @@ def run_hostfed(args, cx: Ctx) -> dict:
     h3c.fill_splitmix(devbuf, total - total % 8, 1, total - total % 8, SEED + 7 + cx.rank)
     offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
     _, expected = h3c.batch_create([(devbuf[o: o + L], L) for o, L in zip(offs, lens)])
-    # NUMA-local pinned host memory: pages on the GPU's node, registered
-    hb = h3c.engine.HostBuffer(cx.local, total)
-    torch.from_numpy(hb.array).copy_(devbuf)
+    # NUMA-local pinned host memory: pages on the GPU's node, registered.
+    # If the host refuses the registration, torch's pinned memory instead (node unknown), so
+    # every rank still reaches the same collectives.
+    try:
+        hb = h3c.engine.HostBuffer(cx.local, total)
+        host = hb.array
+        torch.from_numpy(host).copy_(devbuf)
+    except h3c.EngineError:
+        hb = None
+        host = devbuf.cpu().pin_memory()
     del devbuf
-    items = [(hb.array[o: o + L], L) for o, L in zip(offs, lens)]
+    items = [(host[o: o + L], L) for o, L in zip(offs, lens)]
     hf = h3c.HostFed(cx.local, args.window_mib << 20)
     state = {}
 
@@ -494,9 +501,10 @@ def run_hostfed(args, cx: Ctx) -> dict:
     _, ok, nbad = state["r"]
     verified = cx.all_true(nbad == 0 and bool(ok.all()))
     hf.close()
-    items = None
-    node = hb.node
-    hb.close()
+    items = host = None
+    node = hb.node if hb is not None else -1
+    if hb is not None:
+        hb.close()
     peak = pcie_h2d_peak(torch, cx.dev)
     value = total * args.steps * cx.world / elapsed / 2**30
     rl = roofline(prof, round(peak, 1), bound="pcie", kernel="hostfed pipeline (H2D + CRC)")
