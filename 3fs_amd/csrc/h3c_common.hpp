@@ -184,6 +184,7 @@ struct PolyConsts {
   uint32_t red[7][4][256];
   uint32_t tabq[4][256];  // tabq[k][b] = (b << 8k) * x^(8*kQuadRowBytes): the small-chunk kernel's rows
   uint32_t tabo[4][256];  // tabo[k][b] = (b << 8k) * x^(8*128): its 8-lane (128-byte row) variant
+  uint32_t tabf[4][256];  // tabf[k][b] = (b << 8k) * x^(8*64): its 4-lane (64-byte row) variant
 };
 constexpr int kRedTables = 7;
 constexpr int kRedWords = kRedTables * 4 * 256;  // 7168 dwords = 28 KiB of LDS
@@ -200,6 +201,9 @@ inline void build_consts(PolyConsts &pc, uint32_t poly) {
   const uint32_t orow = hxpow8n(128, poly);
   for (int k = 0; k < 4; ++k)
     for (uint32_t b = 0; b < 256; ++b) pc.tabo[k][b] = hgf_mul(b << (8 * k), orow, poly);
+  const uint32_t frow = hxpow8n(64, poly);
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t b = 0; b < 256; ++b) pc.tabf[k][b] = hgf_mul(b << (8 * k), frow, poly);
   const uint32_t xinv8 = hgf_pow(hx_inverse(poly), 8, poly);
   for (int l = 0; l < 64; ++l)
     for (int j = 0; j < 4; ++j) pc.fix[4 * l + j] = hgf_pow(xinv8, 16u * l + 4u * j, poly);

@@ -236,13 +236,17 @@ __global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__r
   }
 }
 
-// Kernel A'': the same batches with four chunks per wave.  A 16-lane group owns one chunk
-// and walks it in 256-byte rows (16 lanes x 16 B, tables with stride x^(8*256)); the four
-// groups' Horner passes and their 4-level shuffle trees run in the same instructions, so a
-// 4 KiB chunk pays a quarter of a wave fold instead of a whole one (the fold was about a
-// third of seg_small_kernel's instructions per chunk).
+// Kernel A'': the same batches with several chunks per wave.  A group of G lanes owns one
+// chunk and walks it in rows of 16*G bytes (tables with stride x^(8*16*G)); the 64/G
+// groups' Horner passes and their log2(G)-level shuffle trees run in the same
+// instructions, so a chunk pays G/64 of a wave fold instead of a whole one (the fold was
+// about a third of seg_small_kernel's instructions per chunk).  G = 4 for chunks up to
+// ~5 KiB, 16 above.
 #ifndef H3C_SMALL_QUAD
 #define H3C_SMALL_QUAD 1
+#endif
+#ifndef H3C_SMALL_LANES_LO
+#define H3C_SMALL_LANES_LO 4  // lanes per chunk for chunks of at most 6 rows of 1 KiB (4 or 8)
 #endif
 #ifndef H3C_QUAD_BATCH
 #define H3C_QUAD_BATCH 4
@@ -258,12 +262,13 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
                                                            const uint32_t *__restrict__ expected,
                                                            uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
                                                            uint32_t *__restrict__ mismatch) {
-  static_assert(G == 8 || G == 16, "8 or 16 lanes per chunk");
-  constexpr int kLevels = G == 16 ? 4 : 3;  // shuffle-tree levels inside a group
+  static_assert(G == 4 || G == 8 || G == 16, "4, 8 or 16 lanes per chunk");
+  constexpr int kLevels = G == 16 ? 4 : G == 8 ? 3 : 2;  // shuffle-tree levels inside a group
   constexpr uint32_t NG = 64 / G;           // chunks per wave step
   constexpr int kRed = (1 + kLevels) * 1024;  // x^-32 and the tree levels x^-(128 * 2^k)
   __shared__ uint32_t lds[kLdsWords + kRed];
-  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value_of(G == 16 ? pc->tabq : pc->tabo, i);
+  for (int i = threadIdx.x; i < kLdsWords; i += kThreads)
+    lds[i] = fill_value_of(G == 16 ? pc->tabq : G == 8 ? pc->tabo : pc->tabf, i);
   const uint32_t *red_g = &pc->red[0][0][0];
   for (int i = threadIdx.x; i < kRed; i += kThreads) lds[kLdsWords + i] = red_g[i];
   __syncthreads();
@@ -693,11 +698,11 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
     ProfToken tok;
     if (prof_kind >= 0) HIP_TRY(prof_begin(st, tok));
     if (H3C_SMALL_QUAD)
-      // 8 lanes per chunk up to ~5 KiB chunks (+5 % at 4 KiB), 16 above (+2 % at 8 KiB):
-      // profiles/r01d_small_lanes_ab.txt
+      // up to ~5 KiB chunks 4 lanes per chunk (4 KiB: +8 % over 8 lanes, +13 % over 16);
+      // 16 lanes above (4 lanes lose 10 % at 8 and 16 KiB): profiles/r01d_small_lanes_ab.txt
       if (small_rows <= 6)
-        hipLaunchKernelGGL(seg_quad_kernel<8>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
-                           out_raw, ok, mismatch);
+        hipLaunchKernelGGL(seg_quad_kernel<H3C_SMALL_LANES_LO>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks,
+                           pc, expected, out_raw, ok, mismatch);
       else
         hipLaunchKernelGGL(seg_quad_kernel<16>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
                            out_raw, ok, mismatch);

@@ -4,7 +4,7 @@
 # usage: VARIANTS="smallold" scripts/ab_small.sh
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 for rep in 1 2; do
-  for kib in 4 8; do
+  for kib in ${SIZES:-4 8}; do
     for v in cur $VARIANTS; do
       lib=$R/3fs_amd/_lib/libh3c_crc.so
       [ "$v" != cur ] && lib=$R/3fs_amd/_lib/variants/lib_$v.so
