@@ -248,6 +248,15 @@ __global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__r
 #ifndef H3C_SMALL_LANES_LO
 #define H3C_SMALL_LANES_LO 4  // lanes per chunk for chunks of at most 6 rows of 1 KiB (4 or 8)
 #endif
+#ifndef H3C_SMALL_PIECES_LO
+#define H3C_SMALL_PIECES_LO 1  // 16-byte pieces per lane and row there (1 or 2)
+#endif
+#ifndef H3C_SMALL_LANES_HI
+#define H3C_SMALL_LANES_HI 16  // lanes per chunk above that
+#endif
+#ifndef H3C_SMALL_PIECES_HI
+#define H3C_SMALL_PIECES_HI 1
+#endif
 #ifndef H3C_QUAD_BATCH
 #define H3C_QUAD_BATCH 4
 #endif
@@ -255,20 +264,25 @@ constexpr int kQuadBatch = H3C_QUAD_BATCH;  // rows per load batch (two batches 
 
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
 
-// G lanes per chunk (16: 256-byte rows, four chunks per wave; 8: 128-byte rows, eight).
-template <int G>
+// G lanes per chunk, each reading W adjacent 16-byte pieces of a row of 16*G*W bytes
+// (16 x 1: 256-byte rows, four chunks per wave; 4 x 1: 64-byte rows, sixteen chunks).
+template <int G, int W>
 __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                            const PolyConsts *__restrict__ pc,
                                                            const uint32_t *__restrict__ expected,
                                                            uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
                                                            uint32_t *__restrict__ mismatch) {
   static_assert(G == 4 || G == 8 || G == 16, "4, 8 or 16 lanes per chunk");
+  static_assert(W == 1 || W == 2, "one or two 16-byte pieces per lane and row");
+  static_assert(G * W <= 16, "rows of at most 256 bytes");
   constexpr int kLevels = G == 16 ? 4 : G == 8 ? 3 : 2;  // shuffle-tree levels inside a group
-  constexpr uint32_t NG = 64 / G;           // chunks per wave step
-  constexpr int kRed = (1 + kLevels) * 1024;  // x^-32 and the tree levels x^-(128 * 2^k)
+  constexpr int kLw = W == 2 ? 1 : 0;                    // log2(W)
+  constexpr uint32_t NG = 64 / G;                        // chunks per wave step
+  constexpr int kRed = (1 + kLw + kLevels) * 1024;       // x^-32, x^-128 (W = 2), the tree levels
+  constexpr uint64_t kQ = 16u * G * W;                   // row bytes
   __shared__ uint32_t lds[kLdsWords + kRed];
   for (int i = threadIdx.x; i < kLdsWords; i += kThreads)
-    lds[i] = fill_value_of(G == 16 ? pc->tabq : G == 8 ? pc->tabo : pc->tabf, i);
+    lds[i] = fill_value_of(kQ == 256 ? pc->tabq : kQ == 128 ? pc->tabo : pc->tabf, i);
   const uint32_t *red_g = &pc->red[0][0][0];
   for (int i = threadIdx.x; i < kRed; i += kThreads) lds[kLdsWords + i] = red_g[i];
   __syncthreads();
@@ -282,80 +296,113 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
   if (lo >= hi) return;
   const uint32_t poly = pc->poly;
   const LaneLut L = make_lut(lane);
-  constexpr uint64_t kQ = 16u * G;
-  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
-    const uint32_t cnt = min(64u, hi - g0);
-    uint32_t m_plo = 0, m_phi = 0, m_len = 0, m_xs = 0, m_out = 0, m_exp = 0;
-    if (lane < cnt) {  // lane k holds chunk g0 + k's descriptor
-      const DevChunk &ch = chunks[g0 + lane];
-      m_plo = (uint32_t)ch.ptr;
-      m_phi = (uint32_t)(ch.ptr >> 32);
-      m_len = (uint32_t)ch.len;  // one short segment: below 4 GiB
-      m_xs = ch.xstart;
-      m_out = ch.out_idx;
-      if (expected) m_exp = expected[m_out];
+  // Descriptors come in groups of 64 (lane k holds chunk g0 + k's).  The next group's are
+  // loaded when a group starts, so the last quad of a group can already load the first
+  // rows of the next group's first quad: the row pipeline never drains between groups.
+  struct Desc {
+    uint32_t plo, phi, len, xs, out, cnt;
+  };
+  auto load_desc = [&](uint32_t g) {
+    Desc d{0, 0, 0, 0, 0, g < hi ? min(64u, hi - g) : 0u};
+    if (lane < d.cnt) {
+      const DevChunk &ch = chunks[g + lane];
+      d.plo = (uint32_t)ch.ptr;
+      d.phi = (uint32_t)(ch.ptr >> 32);
+      d.len = (uint32_t)ch.len;  // one short segment: below 4 GiB
+      d.xs = ch.xstart;
+      d.out = ch.out_idx;
     }
-    // quad q0's chunk for this group: start, end, row count, this lane's first address
-    auto quad = [&](uint32_t q, uint64_t &S, uint64_t &E, uint32_t &K, uint64_t &la, uint32_t &src) {
-      const uint32_t t = q + grp;
-      const bool valid = t < cnt;
-      src = valid ? t : q;
-      S = (uint64_t)shfl32(m_plo, src) | ((uint64_t)shfl32(m_phi, src) << 32);
-      E = S + shfl32(m_len, src);
-      const uint64_t base = S & ~(kQ - 1);
-      K = valid ? (uint32_t)((E - base + kQ - 1) / kQ) : 0u;
-      la = base + 16u * gl;
-    };
-    uint64_t S, E, la;
-    uint32_t K, src;
-    quad(0, S, E, K, la, src);
-    uint4 cur[kQuadBatch], nxt[kQuadBatch];
+    return d;
+  };
+  // quad q's chunk for this group of lanes: start, end, row count, this lane's first address
+  auto quad = [&](const Desc &d, uint32_t q, uint64_t &S, uint64_t &E, uint32_t &K, uint64_t &la, uint32_t &src) {
+    const uint32_t t = q + grp;
+    const bool valid = t < d.cnt;
+    src = valid ? t : q;
+    S = (uint64_t)shfl32(d.plo, src) | ((uint64_t)shfl32(d.phi, src) << 32);
+    E = S + shfl32(d.len, src);
+    const uint64_t base = S & ~(kQ - 1);
+    K = valid ? (uint32_t)((E - base + kQ - 1) / kQ) : 0u;
+    la = base + 16u * W * gl;
+  };
+  Desc m = load_desc(lo);
+  uint64_t S, E, la;
+  uint32_t K, src;
+  quad(m, 0, S, E, K, la, src);
+  uint4 cur[kQuadBatch][W], nxt[kQuadBatch][W];
 #pragma unroll
-    for (int b = 0; b < kQuadBatch; ++b)
-      cur[b] = (uint32_t)b < K ? load_row(la + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+  for (int b = 0; b < kQuadBatch; ++b)
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      cur[b][w] = (uint32_t)b < K ? load_row(la + (uint64_t)b * kQ + 16u * w) : make_uint4(0, 0, 0, 0);
+  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
+    const uint32_t cnt = m.cnt;
+    const Desc n = load_desc(hi - g0 > 64 ? g0 + 64 : hi);
+    const uint32_t m_exp = expected && lane < cnt ? expected[m.out] : 0u;
     for (uint32_t q0 = 0; q0 < cnt; q0 += NG) {
       const bool valid = q0 + grp < cnt;
-      // the next quad's first batch is loaded during this quad's last batch and fold
+      // the next quad's first batch (in this group or the next) is loaded during this
+      // quad's last batch and fold
       uint64_t S1 = S, E1 = E, la1 = la;
       uint32_t K1 = 0, src1 = src;
-      if (q0 + NG < cnt) quad(q0 + NG, S1, E1, K1, la1, src1);
+      if (q0 + NG < cnt)
+        quad(m, q0 + NG, S1, E1, K1, la1, src1);
+      else if (n.cnt)
+        quad(n, 0, S1, E1, K1, la1, src1);
       uint32_t kmax = 0;
 #pragma unroll
       for (uint32_t g = 0; g < NG; ++g) kmax = max(kmax, (uint32_t)__builtin_amdgcn_readlane(K, g * G));
-      Streams st{0, 0, 0, 0};
+      Streams st[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) st[w] = Streams{0, 0, 0, 0};
       for (uint32_t u0 = 0; u0 < kmax; u0 += kQuadBatch) {
         const uint32_t n0 = u0 + kQuadBatch;
         if (n0 < kmax) {  // the next batch in flight while this one is consumed
 #pragma unroll
           for (int b = 0; b < kQuadBatch; ++b)
-            nxt[b] = n0 + b < K ? load_row(la + (uint64_t)(n0 + b) * kQ) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+              nxt[b][w] = n0 + b < K ? load_row(la + (uint64_t)(n0 + b) * kQ + 16u * w) : make_uint4(0, 0, 0, 0);
         } else {
 #pragma unroll
           for (int b = 0; b < kQuadBatch; ++b)
-            nxt[b] = (uint32_t)b < K1 ? load_row(la1 + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+              nxt[b][w] = (uint32_t)b < K1 ? load_row(la1 + (uint64_t)b * kQ + 16u * w) : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int b = 0; b < kQuadBatch; ++b) {
           const uint32_t u = u0 + b;
           if (u < K) {
-            uint4 x = cur[b];
-            if ((u == 0 && (S & (kQ - 1))) || (u + 1 == K && (E & (kQ - 1))))
-              x = mask_row(x, la + (uint64_t)u * kQ, S, E);
-            consume(st, x, lb, L);
+            const bool edge = (u == 0 && (S & (kQ - 1))) || (u + 1 == K && (E & (kQ - 1)));
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+              uint4 x = cur[b][w];
+              if (edge) x = mask_row(x, la + (uint64_t)u * kQ + 16u * w, S, E);
+              consume(st[w], x, lb, L);
+            }
           }
         }
 #pragma unroll
-        for (int b = 0; b < kQuadBatch; ++b) cur[b] = nxt[b];
+        for (int b = 0; b < kQuadBatch; ++b)
+#pragma unroll
+          for (int w = 0; w < W; ++w) cur[b][w] = nxt[b][w];
       }
-      // fold each group's 64 stream states: Horner over the lane's 4 streams with x^-32,
-      // then 4 shuffle levels inside the group (lane gl + 2^k is 16 * 2^k bytes further)
-      uint32_t v = tab_mul(st.s3, red) ^ st.s2;
-      v = tab_mul(v, red) ^ st.s1;
-      v = tab_mul(v, red) ^ st.s0;
+      // fold each group's stream states: Horner over a piece's 4 streams with x^-32, the
+      // lane's second piece (16 bytes further) with x^-128, then log2(G) shuffle levels
+      // inside the group (lane gl + 2^k is 16 * W * 2^k bytes further)
+      uint32_t v = 0;
+#pragma unroll
+      for (int w = W - 1; w >= 0; --w) {
+        if (w != W - 1) v = tab_mul(v, red + 1024);
+        uint32_t p = tab_mul(st[w].s3, red) ^ st[w].s2;
+        p = tab_mul(p, red) ^ st[w].s1;
+        v ^= tab_mul(p, red) ^ st[w].s0;
+      }
 #pragma unroll
       for (int k = 0; k < kLevels; ++k) {
         const uint32_t o = (uint32_t)__shfl_down((int)v, 1u << k, G);
-        if ((gl & ((2u << k) - 1u)) == 0) v ^= tab_mul(o, red + 1024 * (k + 1));
+        if ((gl & ((2u << k) - 1u)) == 0) v ^= tab_mul(o, red + 1024 * (k + 1 + kLw));
       }
       // the bytes of the last row past E were walked as zeros: remove them
       const uint32_t pad = (uint32_t)(((E + kQ - 1) & ~(kQ - 1)) - E);
@@ -363,7 +410,7 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
         if (pad >> 4) v = dgf_mul(v, pc->fix[4 * (pad >> 4)], poly);
         if (pad & 15) v = dgf_mul(v, pc->fixz[pad & 15], poly);
       }
-      const uint32_t xs = shfl32(m_xs, src), o = shfl32(m_out, src), want = shfl32(m_exp, src);
+      const uint32_t xs = shfl32(m.xs, src), o = shfl32(m.out, src), want = shfl32(m_exp, src);
       if (gl == 0 && valid) {
         const uint32_t raw = v ^ xs;
         out_raw[o] = raw;
@@ -379,6 +426,7 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
       la = la1;
       src = src1;
     }
+    m = n;
   }
 }
 
@@ -701,10 +749,10 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
       // up to ~5 KiB chunks 4 lanes per chunk (4 KiB: +8 % over 8 lanes, +13 % over 16);
       // 16 lanes above (4 lanes lose 10 % at 8 and 16 KiB): profiles/r01d_small_lanes_ab.txt
       if (small_rows <= 6)
-        hipLaunchKernelGGL(seg_quad_kernel<H3C_SMALL_LANES_LO>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks,
+        hipLaunchKernelGGL((seg_quad_kernel<H3C_SMALL_LANES_LO, H3C_SMALL_PIECES_LO>), dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks,
                            pc, expected, out_raw, ok, mismatch);
       else
-        hipLaunchKernelGGL(seg_quad_kernel<16>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
+        hipLaunchKernelGGL((seg_quad_kernel<H3C_SMALL_LANES_HI, H3C_SMALL_PIECES_HI>), dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
                            out_raw, ok, mismatch);
     else if (small_rows <= 4)
       hipLaunchKernelGGL(seg_small_kernel<4>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,

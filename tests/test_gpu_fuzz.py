@@ -100,3 +100,48 @@ def test_fuzz_device_plan_matches_batch(h3c, torch_dev):
         plan.close()
         for i, (off, ln, t, start, _) in enumerate(batch):
             assert int(got[i]) == orc.create(t, host[off: off + ln], ln, start)[1], i
+
+
+@pytest.mark.parametrize("maxlen", [5000, 15000])
+def test_small_kernel_many_groups_per_wave(h3c, torch_dev, maxlen):
+    """300k ragged small chunks in one plan: each wave of the small-chunk kernel walks
+    several 64-chunk descriptor groups, so the next group's descriptors and first rows are
+    fetched across group boundaries.  Lengths up to ~5 KiB take the 4-lane groups, up to
+    16 rows of 1 KiB the 16-lane groups; random offsets, starting values, and a verify pass with a
+    few flipped expected values."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(500 + maxlen)
+    pool = 64 << 20
+    host = rng.integers(0, 256, pool, dtype=np.uint8)
+    dbuf = torch.from_numpy(host).to(dev)
+    n = 300_000
+    lens = rng.integers(1, maxlen + 1, n).astype(np.uint64)
+    offs = (rng.random(n) * (pool - lens)).astype(np.uint64)
+    starts = rng.choice(np.array([0xFFFFFFFF, 0, 0x12345678], dtype=np.uint32), n)
+    d = np.zeros(n, dtype=h3c.engine.DESC_DTYPE)
+    d["ptr"] = np.uint64(dbuf.data_ptr()) + offs
+    d["len"] = lens
+    d["start_raw"] = starts
+    d["type"] = int(h3c.ChecksumType.CRC32C)
+    d["mem"] = int(h3c.engine.MemKind.DEVICE)
+    base = host.ctypes.data
+    f = orc.lib().orc_crc32c_sse42
+    want = np.array([f(base + int(o), int(ln), int(s)) for o, ln, s in zip(offs, lens, starts)], dtype=np.uint32)
+    plan = h3c.Plan(d, 0)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    plan.run(out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    bad_at = np.nonzero(got != want)[0]
+    assert bad_at.size == 0, (bad_at[:5].tolist(), bad_at.size)
+    exp = want.copy()
+    flip = np.unique(rng.integers(0, n, 40))
+    exp[flip] ^= np.uint32(1 << 7)
+    exp_t = torch.from_numpy(exp.view(np.int32)).to(dev)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    mism = torch.zeros(1, dtype=torch.int32, device=dev)
+    plan.run(out, expected=exp_t, ok=ok, mismatch=mism)
+    torch.cuda.synchronize()
+    plan.close()
+    assert np.array_equal(np.nonzero(ok.cpu().numpy() == 0)[0], flip)
+    assert int(mism.item()) == flip.size
