@@ -34,6 +34,7 @@
 //      case (i) (write type NONE or empty chunk) stores 0; cases (ii)-(iv) store the
 //      CRC of the chunk after the op (reuse and combine equal it given a consistent
 //      stored checksum; the client checksum was verified in A).
+#include <sched.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -383,13 +384,20 @@ class HostPool {
   bool stop_ = false;
 };
 
-// Threads for the host pass: 1 below kParallelOps ops, else H3C_HOST_THREADS (default 8).
+// Threads for the host pass: 1 below kParallelOps ops, else H3C_HOST_THREADS, by default
+// 16 capped by the CPUs this process may run on (16 threads: 41 M writes/s against 31 M
+// with 8 on the GPU box's 16-core share, profiles/r01d_updio_host_threads_ab.txt).  A
+// service calling from many threads at once should lower it: each calling thread keeps
+// its own pool.
 constexpr uint32_t kParallelOps = 16384;
 unsigned pass_threads(uint32_t n) {
   if (n < kParallelOps) return 1;
   static const unsigned t = [] {
     const char *e = std::getenv("H3C_HOST_THREADS");
-    const int v = e ? std::atoi(e) : 8;
+    int v = 16;
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) v = std::min(v, std::max(CPU_COUNT(&cs), 1));
+    if (e) v = std::atoi(e);
     return (unsigned)std::min(std::max(v, 1), 32);
   }();
   return t;
