@@ -189,6 +189,16 @@ __global__ void updio_true_kernel(const Aff *__restrict__ scan, const uint32_t *
 
 // Device arena for one call: every buffer is carved from one pooled device lease
 // (h3c_rt::DeviceLease; hipMallocAsync pools gave kernels stale bytes under ROCm 7.2).
+// Waits for the stream on scope exit while armed: device work reading or writing leased
+// buffers must finish before the leases go back to their pools (early error returns).
+struct StreamDrain {
+  hipStream_t st;
+  bool armed = false;
+  ~StreamDrain() {
+    if (armed) (void)hipStreamSynchronize(st);
+  }
+};
+
 struct Arena {
   char *base = nullptr;
   size_t off = 0;
@@ -866,6 +876,37 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     pay.bytes += b.bytes;
     pay.max_len = std::max(pay.max_len, b.max_len);
   }
+  // The speculative attempt's payload CRCs need nothing from the host pass: they are
+  // uploaded and launched now, so the device works through them while B runs on the host.
+  const size_t npay = pay_off[T];
+  h3c_rt::DeviceLease pay_dev(dev, (npay * sizeof(DevChunk) + 4ull * std::max(pay.total_segs, 1u) + 4ull * n) +
+                                       3 * 256);
+  h3c_rt::PinnedLease pay_pin(npay * sizeof(DevChunk) + 256);
+  if (!pay_dev.ok() || !pay_pin.ok()) return H3C_ERR_HIP;
+  StreamDrain drain{st};  // declared after the leases: every return below waits for the stream first
+  Arena pa;
+  pa.base = pay_dev.data();
+  DevChunk *d_pay = pa.take<DevChunk>(npay);
+  uint32_t *d_payseg = pa.take<uint32_t>(std::max(pay.total_segs, 1u));
+  uint32_t *d_payraw_spec = pa.take<uint32_t>(n);
+  if (npay)
+    run_threads(T, [&](unsigned t) {
+      DevChunk *dst = reinterpret_cast<DevChunk *>(pay_pin.data()) + pay_off[t];
+      for (const DevChunk &d : ws.pay_parts[t].chunks) {
+        *dst = d;
+        dst->seg_begin += pay_seg_base[t];
+        ++dst;
+      }
+    });
+  drain.armed = true;
+  HIP_TRY(hipMemsetAsync(d_payraw_spec, 0xFF, 4ull * n, st));
+  if (npay) {
+    HIP_TRY(hipMemcpyAsync(d_pay, pay_pin.data(), npay * sizeof(DevChunk), hipMemcpyHostToDevice, st));
+    const int r = h3c_rt::launch_crc(st, dev, poly_type, d_pay, (uint32_t)npay, pay.total_segs, pay.max_segs, pay.bytes,
+                                     seg, 0, d_payseg, nullptr, d_payraw_spec, nullptr, nullptr, -1,
+                                     h3c_rt::small_rows_bound(pay.max_len, pay.max_segs));
+    if (r) return r;
+  }
   clk.mark("A prepare");
 
   // B + C-D, speculatively first: the host pass assumes every client checksum matches and
@@ -910,23 +951,21 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
       HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, scan_tmp, (uint32_t *)nullptr, (Aff *)nullptr, (Aff *)nullptr,
                                              (size_t)npos, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
     const size_t crc_chunks = M.crc_total, copy_pieces = M.copy_total;
-    const uint32_t max_segs = std::max(spec ? pay.total_segs : 0u, M.max_segs);
-    const size_t npay = spec ? pay_off[T] : 0;
+    const uint32_t max_segs = M.max_segs;
     Arena a;
-    const size_t bytes = (npay + crc_chunks) * sizeof(DevChunk) + copy_pieces * sizeof(CopyPiece) +
+    const size_t bytes = crc_chunks * sizeof(DevChunk) + copy_pieces * sizeof(CopyPiece) +
                          nver * sizeof(VerifyItem) + 4ull * max_segs + 4ull * std::max(M.njobs, 1u) + 4ull * n +
                          npos * (sizeof(AffIn) + 2 * sizeof(Aff) + 8) + 4ull * nchunks + 4ull * nver + scan_tmp +
                          16 * 256;
     h3c_rt::DeviceLease scratch(dev, bytes);
     if (!scratch.ok()) return H3C_ERR_HIP;
     a.base = scratch.data();
-    DevChunk *d_pay = a.take<DevChunk>(npay);
     DevChunk *d_crc = a.take<DevChunk>(crc_chunks);
     CopyPiece *d_copy = a.take<CopyPiece>(copy_pieces);
     VerifyItem *d_ver = a.take<VerifyItem>(nver);
     uint32_t *d_seg = a.take<uint32_t>(max_segs);
     uint32_t *d_jobcrc = a.take<uint32_t>(std::max(M.njobs, 1u));
-    uint32_t *d_payraw = a.take<uint32_t>(n);
+    uint32_t *d_payraw = spec ? d_payraw_spec : a.take<uint32_t>(n);
     AffIn *d_in = a.take<AffIn>(npos);
     Aff *d_aff = a.take<Aff>(npos);
     Aff *d_scan = a.take<Aff>(npos);
@@ -936,29 +975,20 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     uint32_t *d_bad = a.take<uint32_t>(1 + nver);  // [0]: any mismatch (gates the copies); [1+k]: item k
     void *d_tmp = a.take<char>(scan_tmp);
 
-    // pinned staging: uploads [pay | crc jobs | copies | verify | payraw | raw0] (the scan
+    // pinned staging: uploads [crc jobs | copies | verify | payraw | raw0] (the scan
     // elements and keys are already in pin_el), downloads [true values | mismatch flags |
     // payload CRCs]
-    enum { kPay, kCrc, kCopy, kVer, kPayraw, kRaw0, kUp, kTrue = kUp, kBad, kPayBack, kAll };
-    size_t len[kAll] = {npay * sizeof(DevChunk), crc_chunks * sizeof(DevChunk), copy_pieces * sizeof(CopyPiece),
+    enum { kCrc, kCopy, kVer, kPayraw, kRaw0, kUp, kTrue = kUp, kBad, kPayBack, kAll };
+    size_t len[kAll] = {crc_chunks * sizeof(DevChunk), copy_pieces * sizeof(CopyPiece),
                         nver * sizeof(VerifyItem), spec ? 0 : 4ull * n, 4ull * nchunks, 4ull * npos,
                         spec ? 4ull * (1 + nver) : 0, spec ? 4ull * n : 0};
-    void *dst[kUp] = {d_pay, d_crc, d_copy, d_ver, d_payraw, d_raw0};
+    void *dst[kUp] = {d_crc, d_copy, d_ver, d_payraw, d_raw0};
     size_t off[kAll + 1];
     off[0] = 0;
     for (int k = 0; k < kAll; ++k) off[k + 1] = off[k] + ((len[k] + 255) & ~size_t(255));
     h3c_rt::PinnedLease pin(off[kAll]);
     if (!pin.ok()) return H3C_ERR_HIP;
     char *hp = pin.data();
-    if (npay)
-      run_threads(T, [&](unsigned t) {
-        DevChunk *dst = reinterpret_cast<DevChunk *>(hp + off[kPay]) + pay_off[t];
-        for (const DevChunk &d : ws.pay_parts[t].chunks) {
-          *dst = d;
-          dst->seg_begin += pay_seg_base[t];
-          ++dst;
-        }
-      });
     run_tasks(T, NT, [&](unsigned k) {
       pass_publish(ws.L[k], M, k, NT, ws.cut[k], ws.cut[k + 1], ws.start.data(), S, lay,
                    reinterpret_cast<DevChunk *>(hp + off[kCrc]),
@@ -976,15 +1006,8 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
         HIP_TRY(hipMemcpyAsync(d_in, lay, npos * sizeof(AffIn), hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemcpyAsync(d_keys, keys, 4ull * npos, hipMemcpyHostToDevice, st));
       }
-      if (spec) {
+      if (spec) {  // the payload CRCs were launched before the host pass
         HIP_TRY(hipMemsetAsync(d_bad, 0, 4ull * (1 + nver), st));
-        HIP_TRY(hipMemsetAsync(d_payraw, 0xFF, 4ull * n, st));
-        if (npay) {
-          const int r = h3c_rt::launch_crc(st, dev, poly_type, d_pay, (uint32_t)npay, pay.total_segs, pay.max_segs,
-                                           pay.bytes, seg, 0, d_seg, nullptr, d_payraw, nullptr, nullptr, -1,
-                                           h3c_rt::small_rows_bound(pay.max_len, pay.max_segs));
-          if (r) return r;
-        }
         if (nver) {
           hipLaunchKernelGGL(updio_verify_kernel, dim3((nver + 255) / 256), dim3(256), 0, st, d_ver, nver, d_payraw,
                              std_domain ? 1u : 0u, d_bad);
@@ -1026,6 +1049,7 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     };
     err = body();
     const hipError_t e = hipStreamSynchronize(st);  // the leases are reused only after this
+    drain.armed = false;
     if (err) return err;
     if (e != hipSuccess) {
       h3c_rt::set_error("h3c_update_ios", e);
