@@ -68,6 +68,29 @@ class PinnedLease {
   size_t cap_ = 0;
 };
 
+// Waits for `st` on scope exit while armed: device work that reads or writes leased
+// buffers must finish before the leases go back to their pools, on every return path.
+// Declare it after the leases it protects (destructors run in reverse order).
+struct StreamDrain {
+  hipStream_t st;
+  bool armed = false;
+  ~StreamDrain() {
+    if (armed) (void)hipStreamSynchronize(st);
+  }
+};
+
+// Restores the caller's current device on scope exit (entry points that switch to a
+// plan's / pipeline's device must not leave the caller on it after an early error).
+struct DeviceRestore {
+  int prev = -1;
+  ~DeviceRestore() {
+    if (prev >= 0) {
+      int cur = -1;
+      if (hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+  }
+};
+
 // Device copy of a descriptor (32 B).
 struct DevChunk {
   uint64_t ptr;

@@ -164,9 +164,9 @@ int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t 
   if (n_mismatch) *n_mismatch = 0;
   if (n == 0) return H3C_OK;
   if (n > 0xFFFFFFF0u) return H3C_ERR_INVALID_ARG;
-  int prev = 0;
-  HIP_TRY(hipGetDevice(&prev));
-  if (prev != h->device) HIP_TRY(hipSetDevice(h->device));
+  h3c_rt::DeviceRestore restore;  // every return below puts the caller back on its device
+  HIP_TRY(hipGetDevice(&restore.prev));
+  if (restore.prev != h->device) HIP_TRY(hipSetDevice(h->device));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   uint8_t type = 0;  // one polynomial per run (the batch API splits mixed batches)
   for (size_t i = 0; i < n; ++i)
@@ -290,6 +290,10 @@ int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t 
   char *const pr_out = pb + pin_off[4];
   char *const pr_ok = pr_out + ((n * 4 + 255) & ~size_t(255));
   char *const pr_mis = pr_ok + ((n + 255) & ~size_t(255));
+  // from the first async copy on, an early return must wait for the copy stream and `st`
+  // before `pin` goes back to the pool (another thread could lease it mid-transfer)
+  h3c_rt::StreamDrain drain_st{st, true};
+  h3c_rt::StreamDrain drain_copy{h->copy_st, true};
   for (int k = 0; k < 4; ++k)
     if (up[k]) {
       std::memcpy(pb + pin_off[k], up_src[k], up[k]);
@@ -331,13 +335,13 @@ int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t 
     HIP_TRY(hipMemcpyAsync(pr_mis, h->d_mis, 4, hipMemcpyDeviceToHost, st));
   }
   HIP_TRY(hipStreamSynchronize(st));
+  drain_st.armed = drain_copy.armed = false;
   std::memcpy(out_raw, pr_out, n * 4);
   if (expected) {
     std::memcpy(ok, pr_ok, n);
     std::memcpy(&mis, pr_mis, 4);
   }
   if (n_mismatch) *n_mismatch = mis;
-  if (prev != h->device) HIP_TRY(hipSetDevice(prev));
   return H3C_OK;
 }
 

@@ -187,18 +187,10 @@ __global__ void updio_true_kernel(const Aff *__restrict__ scan, const uint32_t *
   out[p] = (a.m == kOne ? r0 : dgf_mul(r0, a.m, poly)) ^ a.e;
 }
 
+using h3c_rt::StreamDrain;
+
 // Device arena for one call: every buffer is carved from one pooled device lease
 // (h3c_rt::DeviceLease; hipMallocAsync pools gave kernels stale bytes under ROCm 7.2).
-// Waits for the stream on scope exit while armed: device work reading or writing leased
-// buffers must finish before the leases go back to their pools (early error returns).
-struct StreamDrain {
-  hipStream_t st;
-  bool armed = false;
-  ~StreamDrain() {
-    if (armed) (void)hipStreamSynchronize(st);
-  }
-};
-
 struct Arena {
   char *base = nullptr;
   size_t off = 0;

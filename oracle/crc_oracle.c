@@ -14,6 +14,9 @@
  *   ChunkReplica::updateChecksum    -- src/storage/store/ChunkReplica.cc:319-394
  *   ChunkFileView::checksum         -- src/storage/store/ChunkFileView.cc:92-104
  *   AioReadJob::setResult checksum  -- src/storage/aio/BatchReadJob.cc:24-55
+ *   ChunkReplica::update            -- src/storage/store/ChunkReplica.cc:131-317
+ *   Rust Engine::update_chunk       -- src/storage/chunk_engine/src/core/engine.rs:288-429,
+ *       Chunk::copy_on_write / safe_write (src/storage/chunk_engine/src/alloc/chunk.rs:89-281)
  *
  * Three independent CRC mechanisms (bitwise, byte table, x86 SSE4.2 crc32
  * instruction) cross-check one another; tests pin them to the standard KATs
@@ -356,8 +359,8 @@ static int view_checksum(uint8_t type, const uint8_t *chunk, uint64_t size, uint
 /* ------------------------------------------------------------------ */
 /* A8: ChunkReplica::updateChecksum (ChunkReplica.cc:319-394).          */
 /* ------------------------------------------------------------------ */
-int orc_update_checksum(orc_chunk_meta *meta, orc_write_io wio, uint32_t chunk_size_before_write, int is_append_write,
-                        const uint8_t *chunk_after_write) {
+int orc_update_checksum_case(orc_chunk_meta *meta, orc_write_io wio, uint32_t chunk_size_before_write,
+                             int is_append_write, const uint8_t *chunk_after_write, int *ucase) {
   uint8_t ctype = meta->checksum_type;
   uint32_t cvalue = meta->checksum_value;
   int combine_checksum = chunk_size_before_write > 0 && is_append_write; /* :326 */
@@ -370,12 +373,15 @@ int orc_update_checksum(orc_chunk_meta *meta, orc_write_io wio, uint32_t chunk_s
 
   if (wio.checksum_type == ORC_NONE || meta->size == 0) { /* :334-336 */
     meta->checksum_value = 0;
+    if (ucase) *ucase = ORC_CASE_NONE;
   } else if (wio.offset == 0 && wio.length == meta->size) { /* :337-339 reuse */
     meta->checksum_value = wio.checksum_value;
+    if (ucase) *ucase = ORC_CASE_REUSE;
   } else if (wio.checksum_type == ctype && combine_checksum) { /* :340-355 append */
     int rc = orc_checksum_combine(&ctype, &cvalue, wio.checksum_type, wio.checksum_value, wio.length);
     if (rc) return rc;
     meta->checksum_value = cvalue;
+    if (ucase) *ucase = ORC_CASE_COMBINE;
   } else { /* :356-390 prefix / write / suffix */
     uint8_t pt, st;
     uint32_t pv, sv;
@@ -389,27 +395,40 @@ int orc_update_checksum(orc_chunk_meta *meta, orc_write_io wio, uint32_t chunk_s
     orc_checksum_combine(&pt, &pv, wio.checksum_type, wio.checksum_value, wio.length);
     orc_checksum_combine(&pt, &pv, st, sv, suffix_len);
     meta->checksum_value = pv;
+    if (ucase) *ucase = ORC_CASE_READ_CHUNK;
   }
   meta->checksum_type = wio.checksum_type; /* :392 */
   return ORC_OK;
 }
 
+int orc_update_checksum(orc_chunk_meta *meta, orc_write_io wio, uint32_t chunk_size_before_write, int is_append_write,
+                        const uint8_t *chunk_after_write) {
+  return orc_update_checksum_case(meta, wio, chunk_size_before_write, is_append_write, chunk_after_write, NULL);
+}
+
 /* ------------------------------------------------------------------ */
 /* A6 + A8: ChunkReplica::update (ChunkReplica.cc:131-317) for WRITE,   */
-/* TRUNCATE and EXTEND, with the chunk file modelled as a byte array.   */
+/* REMOVE, TRUNCATE and EXTEND (plus options.isSyncing), and            */
+/* ChunkReplica::commit's (no-)effect on the checksum (:397-467), with  */
+/* the chunk file modelled as a byte array.                             */
 /* ------------------------------------------------------------------ */
 int orc_chunk_replica_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chunk_size, const orc_update_io *io,
                              const uint8_t *payload, orc_update_result *res) {
   res->status = ORC_OK;
   res->size = meta->size;
-  res->type = ORC_NONE; /* IOResult default until :171 */
+  res->type = ORC_NONE; /* IOResult default until :174 */
   res->value = 0;
+  res->ucase = ORC_CASE_NOT_RUN;
+  if (io->kind == ORC_UPD_COMMIT) { /* ChunkReplica::commit sets no checksum (:397-467) */
+    return ORC_OK;
+  }
+  const int is_remove = io->kind == ORC_UPD_REMOVE;
   /* :140-145 range check (not for REMOVE) */
-  if (io->offset >= chunk_size || (uint64_t)io->offset + io->length > chunk_size) {
+  if (!is_remove && (io->offset >= chunk_size || (uint64_t)io->offset + io->length > chunk_size)) {
     res->status = 3; /* StatusCode::kInvalidArg */
     return res->status;
   }
-  res->type = meta->checksum_type; /* :171 result.checksum = meta.checksum() */
+  res->type = meta->checksum_type; /* :174 result.checksum = meta.checksum() */
   res->value = meta->checksum_value;
   /* :193-207 verify the client's checksum of the payload */
   if (io->checksum_type != ORC_NONE && io->length != 0) {
@@ -421,7 +440,7 @@ int orc_chunk_replica_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chun
       return res->status;
     }
   }
-  const int is_append = io->offset == meta->size; /* :244 */
+  const int is_append = io->offset == meta->size; /* :246 */
   const uint32_t size_before = meta->size;       /* :256 */
   if (io->kind == ORC_UPD_TRUNCATE || io->kind == ORC_UPD_EXTEND) { /* :260-273 */
     if (io->length <= meta->size) {
@@ -430,26 +449,143 @@ int orc_chunk_replica_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chun
       memset(chunk + meta->size, 0, io->length - meta->size);
       meta->size = io->length;
     }
+  } else if (is_remove) { /* :274-279: no bytes change */
   } else { /* :281-291 WRITE: zero fill a gap, then the write */
     if (meta->size < io->offset) memset(chunk + meta->size, 0, io->offset - meta->size);
     if (io->length) memcpy(chunk + io->offset, payload, io->length);
     const uint32_t end = io->offset + io->length; /* doRealWrite :124 */
     if (end > meta->size) meta->size = end;
+    if (io->syncing) meta->size = io->length; /* :289 options.isSyncing: full-chunk replace */
   }
   orc_write_io w;
   w.offset = io->offset;
   w.length = io->length;
   w.checksum_type = io->checksum_type;
   w.checksum_value = io->checksum_value;
-  w.is_truncate_or_extend = io->kind != ORC_UPD_WRITE;
-  int rc = orc_update_checksum(meta, w, size_before, is_append, chunk); /* :297 */
+  w.is_truncate_or_extend = io->kind == ORC_UPD_TRUNCATE || io->kind == ORC_UPD_EXTEND;
+  int rc = orc_update_checksum_case(meta, w, size_before, is_append, chunk, &res->ucase); /* :298 */
   if (rc) {
     res->status = rc;
     return rc;
   }
   res->size = meta->size;
-  res->type = meta->checksum_type; /* :313 result.checksum = meta.checksum() */
+  res->type = meta->checksum_type; /* :311 result.checksum = meta.checksum() */
   res->value = meta->checksum_value;
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* A10 + A11: the Rust chunk engine's update in the std domain:         */
+/* ChunkEngine::update's request mapping (src/storage/store/            */
+/* ChunkEngine.cc:32-52, 61-67), Engine::update_chunk                   */
+/* (src/storage/chunk_engine/src/core/engine.rs:288-429) and            */
+/* Chunk::copy_on_write / safe_write (src/storage/chunk_engine/src/     */
+/* alloc/chunk.rs:89-281), with the chunk's capacity = chunk_size       */
+/* (offset + length past it is rejected before, like the C++ range      */
+/* check).  meta->checksum_value is the std-domain crc32c (crate        */
+/* 0.6.8: std = ~raw).  `payload_aligned` is is_aligned_buf's pointer   */
+/* half (aligned.rs:47-49): it only changes the combine counter.        */
+/* ------------------------------------------------------------------ */
+#define ORC_ALIGN 4096u /* ALIGN_SIZE, chunk_engine/src/utils/aligned.rs:4 */
+
+static uint32_t std_append(uint32_t std_c, const uint8_t *d, uint64_t n) { /* crc32c::crc32c_append */
+  return ~orc_crc32c_table(d, n, ~std_c);
+}
+
+int orc_chunk_engine_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chunk_size, const orc_update_io *io,
+                            const uint8_t *payload, int payload_aligned, orc_update_result *res,
+                            orc_engine_counters *cnt) {
+  res->status = ORC_OK;
+  res->size = meta->size;
+  res->type = ORC_CRC32C;
+  res->value = ~meta->checksum_value; /* ChunkEngine.cc:66: {CRC32C, ~out_checksum} */
+  res->ucase = ORC_CASE_NOT_RUN;
+  if (io->kind == ORC_UPD_COMMIT) return ORC_OK; /* no checksum effect */
+  if (io->kind != ORC_UPD_REMOVE && (io->offset >= chunk_size || (uint64_t)io->offset + io->length > chunk_size)) {
+    res->status = 3;
+    res->type = ORC_NONE;
+    res->value = 0;
+    return res->status;
+  }
+  /* ChunkEngine.cc:33-52: the request */
+  const int is_truncate = io->kind == ORC_UPD_TRUNCATE;
+  const int is_remove = io->kind == ORC_UPD_REMOVE;
+  const int is_write = io->kind == ORC_UPD_WRITE;
+  uint32_t req_len = is_write ? io->length : 0;
+  uint32_t req_off = is_write ? io->offset : io->length;
+  const uint8_t *data = req_len ? payload : NULL;
+  uint32_t req_checksum = 0;
+  int without_checksum = 0;
+  if (io->checksum_type == ORC_CRC32C) req_checksum = ~io->checksum_value;
+  else if (payload) without_checksum = 1;
+  /* engine.rs:297-312: verify the payload */
+  if (req_len) {
+    const uint32_t c = std_append(0, data, req_len);
+    if (without_checksum) req_checksum = c;
+    else if (c != req_checksum) {
+      /* the error returns before out_checksum is set (engine.rs:303 vs :324): it stays 0, and
+       * ChunkEngine.cc:66 reports {CRC32C, ~0} */
+      res->status = ORC_ERR_CHECKSUM_MISMATCH;
+      res->value = 0xFFFFFFFFu;
+      return res->status;
+    }
+  }
+  const uint32_t len = meta->size;
+  if (is_remove) { /* engine.rs:376: the old chunk, unchanged */
+    res->ucase = ORC_CASE_KEEP;
+    return ORC_OK;
+  }
+  if (io->syncing || (req_len > 0 && req_off < len)) { /* engine.rs:377-391 copy_on_write */
+    const uint32_t new_len = len > req_off + req_len ? len : req_off + req_len;
+    const int skip_read = io->syncing || (req_off == 0 && req_len >= len); /* chunk.rs:112 */
+    if (len < req_off) memset(chunk + len, 0, req_off - len);
+    if (req_len) memcpy(chunk + req_off, data, req_len);
+    uint32_t ck;
+    if (skip_read) {
+      ck = req_checksum; /* chunk.rs:152-154 */
+      if (cnt) cnt->reuse++;
+      res->ucase = ORC_CASE_REUSE;
+    } else {
+      ck = std_append(0, chunk, new_len); /* chunk.rs:156-157 */
+      if (cnt) cnt->recalculate++;
+      res->ucase = ORC_CASE_READ_CHUNK;
+    }
+    meta->size = io->syncing ? req_off + req_len : new_len; /* chunk.rs:166-170 */
+    meta->checksum_value = ck;
+  } else { /* safe_write, chunk.rs:176-281 */
+    res->ucase = ORC_CASE_KEEP;
+    if (is_truncate && req_off < len) { /* :184-197 */
+      meta->size = req_off;
+      meta->checksum_value = std_append(0, chunk, req_off);
+      if (cnt) cnt->recalculate++;
+      res->ucase = ORC_CASE_READ_CHUNK;
+    } else if (len % ORC_ALIGN == 0 && req_off % ORC_ALIGN == 0 &&
+               (req_len == 0 || (payload_aligned && req_len % ORC_ALIGN == 0))) { /* :200-234 */
+      if (req_off > len) {
+        memset(chunk + len, 0, req_off - len);
+        meta->checksum_value = std_append(meta->checksum_value, chunk + len, req_off - len);
+        meta->size = req_off;
+        if (cnt) cnt->combine++;
+        res->ucase = ORC_CASE_COMBINE;
+      }
+      if (req_len) {
+        memcpy(chunk + req_off, data, req_len);
+        meta->checksum_value = orc_crc32c_combine(meta->checksum_value, req_checksum, req_len);
+        meta->size = req_off + req_len;
+        if (cnt) cnt->combine++;
+        res->ucase = ORC_CASE_COMBINE;
+      }
+    } else if (len < req_off + req_len) { /* :235-276 */
+      if (len < req_off) memset(chunk + len, 0, req_off - len);
+      if (req_len) memcpy(chunk + req_off, data, req_len);
+      meta->checksum_value = std_append(meta->checksum_value, chunk + len, req_off + req_len - len);
+      meta->size = req_off + req_len;
+      if (cnt) cnt->combine++;
+      res->ucase = ORC_CASE_COMBINE;
+    }
+  }
+  res->size = meta->size;
+  res->value = ~meta->checksum_value;
   return ORC_OK;
 }
 

@@ -68,27 +68,43 @@ typedef struct {
 
 int orc_update_checksum(orc_chunk_meta *meta, orc_write_io wio, uint32_t chunk_size_before_write, int is_append_write,
                         const uint8_t *chunk_after_write);
+/* which branch of updateChecksum ran: the reference's counters
+ * storage.chunk_update.checksum_{none,reuse,combine,read_chunk} (ChunkReplica.cc:25-28,336-389) */
+enum { ORC_CASE_NOT_RUN = 0, ORC_CASE_NONE = 1, ORC_CASE_REUSE = 2, ORC_CASE_COMBINE = 3, ORC_CASE_READ_CHUNK = 4,
+       ORC_CASE_KEEP = 5 /* Rust engine: checksum untouched */ };
+int orc_update_checksum_case(orc_chunk_meta *meta, orc_write_io wio, uint32_t chunk_size_before_write,
+                             int is_append_write, const uint8_t *chunk_after_write, int *ucase);
 
 /* --- A6 + A8: ChunkReplica::update restated over an in-memory chunk ---
  * One UpdateIO (WRITE / TRUNCATE / EXTEND) applied to `chunk` (capacity chunk_size):
  * range check, client-checksum verify, zero fill of gaps, the write / truncate /
  * extend itself, then updateChecksum.  `meta` is updated in place. */
-enum { ORC_UPD_WRITE = 1, ORC_UPD_TRUNCATE = 4, ORC_UPD_EXTEND = 8 };
+enum { ORC_UPD_WRITE = 1, ORC_UPD_REMOVE = 2, ORC_UPD_TRUNCATE = 4, ORC_UPD_EXTEND = 8, ORC_UPD_COMMIT = 16 };
 typedef struct {
-  uint8_t kind; /* UpdateType */
+  uint8_t kind; /* UpdateType (Common.h:51-58) */
   uint32_t offset;
   uint32_t length;
   uint8_t checksum_type;
   uint32_t checksum_value;
+  uint8_t syncing; /* UpdateOptions.isSyncing (ChunkReplica.cc:211-215, 289) */
 } orc_update_io;
 typedef struct {
   int status;    /* 0, 3 kInvalidArg, 4080 kChecksumMismatch */
   uint32_t size; /* meta.size after */
   uint8_t type;  /* result.checksum */
   uint32_t value;
+  int ucase; /* ORC_CASE_*: the counter the op increments */
 } orc_update_result;
 int orc_chunk_replica_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chunk_size, const orc_update_io *io,
                              const uint8_t *payload, orc_update_result *res);
+
+/* --- A10 + A11: Rust chunk engine update (std domain; meta->checksum_value is std) --- */
+typedef struct {
+  uint64_t reuse, combine, recalculate; /* metrics.rs:12-14 checksum_{reuse,combine,recalculate} */
+} orc_engine_counters;
+int orc_chunk_engine_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chunk_size, const orc_update_io *io,
+                            const uint8_t *payload, int payload_aligned, orc_update_result *res,
+                            orc_engine_counters *cnt);
 
 /* --- A7: AioReadJob::setResult checksum selection (recalculate path) --- */
 int orc_read_result_checksum(uint8_t batch_type, uint8_t chunk_type, uint32_t chunk_value, uint32_t chunk_len,

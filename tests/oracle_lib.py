@@ -119,39 +119,76 @@ def update_checksum(meta: dict, wio: dict, size_before: int, is_append: bool, ch
     return rc, {"size": m.size, "type": m.checksum_type, "value": m.checksum_value}
 
 
-UPD_WRITE, UPD_TRUNCATE, UPD_EXTEND = 1, 4, 8  # UpdateType (Common.h:51-58)
+UPD_WRITE, UPD_REMOVE, UPD_TRUNCATE, UPD_EXTEND, UPD_COMMIT = 1, 2, 4, 8, 16  # UpdateType (Common.h:51-58)
+# updateChecksum branch taken (ChunkReplica.cc:25-28 counters); KEEP: Rust engine left the checksum alone
+CASE_NOT_RUN, CASE_NONE, CASE_REUSE, CASE_COMBINE, CASE_READ_CHUNK, CASE_KEEP = range(6)
 
 
 class UpdateIO(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_uint8), ("offset", ctypes.c_uint32), ("length", ctypes.c_uint32),
-                ("checksum_type", ctypes.c_uint8), ("checksum_value", ctypes.c_uint32)]
+                ("checksum_type", ctypes.c_uint8), ("checksum_value", ctypes.c_uint32), ("syncing", ctypes.c_uint8)]
 
 
 class UpdateResult(ctypes.Structure):
     _fields_ = [("status", ctypes.c_int), ("size", ctypes.c_uint32), ("type", ctypes.c_uint8),
-                ("value", ctypes.c_uint32)]
+                ("value", ctypes.c_uint32), ("ucase", ctypes.c_int)]
 
 
-def replica_update(meta: dict, chunk: np.ndarray, chunk_size: int, io: dict, payload=None):
-    """ChunkReplica::update restatement (A6 + A8): applies one UpdateIO to `chunk` in place.
+class EngineCounters(ctypes.Structure):
+    _fields_ = [("reuse", ctypes.c_uint64), ("combine", ctypes.c_uint64), ("recalculate", ctypes.c_uint64)]
 
-    Returns (result dict, new meta dict)."""
-    L = lib()
+
+def _bind_update(L):
     if not hasattr(L, "_replica_update_bound"):
         L.orc_chunk_replica_update.restype = ctypes.c_int
         L.orc_chunk_replica_update.argtypes = [ctypes.POINTER(ChunkMeta), ctypes.c_void_p, ctypes.c_uint32,
                                                ctypes.POINTER(UpdateIO), ctypes.c_void_p,
                                                ctypes.POINTER(UpdateResult)]
+        L.orc_chunk_engine_update.restype = ctypes.c_int
+        L.orc_chunk_engine_update.argtypes = [ctypes.POINTER(ChunkMeta), ctypes.c_void_p, ctypes.c_uint32,
+                                              ctypes.POINTER(UpdateIO), ctypes.c_void_p, ctypes.c_int,
+                                              ctypes.POINTER(UpdateResult), ctypes.POINTER(EngineCounters)]
         L._replica_update_bound = True
+
+
+def _update_args(meta, io, payload):
     m = ChunkMeta(meta["size"], meta["type"], meta["value"] & 0xFFFFFFFF)
-    u = UpdateIO(io["kind"], io["offset"], io["length"], io["type"], io["value"] & 0xFFFFFFFF)
-    r = UpdateResult()
+    u = UpdateIO(io["kind"], io["offset"], io["length"], io["type"], io["value"] & 0xFFFFFFFF,
+                 int(bool(io.get("syncing", 0))))
     pay = None
     if payload is not None and len(payload):
         pay = np.ascontiguousarray(payload, dtype=np.uint8)
+    return m, u, pay
+
+
+def replica_update(meta: dict, chunk: np.ndarray, chunk_size: int, io: dict, payload=None):
+    """ChunkReplica::update restatement (A6 + A8): applies one UpdateIO to `chunk` in place.
+
+    io = {kind, offset, length, type, value[, syncing]}.  Returns (result dict with the
+    updateChecksum branch in "ucase", new meta dict)."""
+    L = lib()
+    _bind_update(L)
+    m, u, pay = _update_args(meta, io, payload)
+    r = UpdateResult()
     L.orc_chunk_replica_update(ctypes.byref(m), chunk.ctypes.data, chunk_size, ctypes.byref(u),
                                pay.ctypes.data if pay is not None else None, ctypes.byref(r))
-    return ({"status": r.status, "size": r.size, "type": r.type, "value": r.value},
+    return ({"status": r.status, "size": r.size, "type": r.type, "value": r.value, "ucase": r.ucase},
+            {"size": m.size, "type": m.checksum_type, "value": m.checksum_value})
+
+
+def engine_update(meta: dict, chunk: np.ndarray, chunk_size: int, io: dict, payload=None, payload_aligned=False,
+                  counters: EngineCounters = None):
+    """Rust chunk engine restatement (ChunkEngine.cc:15-80, engine.rs:288-429, chunk.rs:89-281):
+    meta["value"] is the std-domain crc32c; results are {CRC32C, ~std} as ChunkEngine.cc:66
+    reports them.  `counters` (EngineCounters) accumulates metrics.rs's checksum counters."""
+    L = lib()
+    _bind_update(L)
+    m, u, pay = _update_args(meta, io, payload)
+    r = UpdateResult()
+    L.orc_chunk_engine_update(ctypes.byref(m), chunk.ctypes.data, chunk_size, ctypes.byref(u),
+                              pay.ctypes.data if pay is not None else None, int(bool(payload_aligned)),
+                              ctypes.byref(r), ctypes.byref(counters) if counters is not None else None)
+    return ({"status": r.status, "size": r.size, "type": r.type, "value": r.value, "ucase": r.ucase},
             {"size": m.size, "type": m.checksum_type, "value": m.checksum_value})
 
 

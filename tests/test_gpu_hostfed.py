@@ -103,3 +103,48 @@ def test_hostfed_numa_local_host_buffer(h3c, torch_dev):
     finally:
         hb.close()
     assert not eng._in_host_buffer(hb.ptr or 1, 1)
+
+
+def test_hostfed_mixed_types_error_leaves_device_and_pipeline_usable(h3c, torch_dev):
+    """A mixed CRC32C / CRC32 run fails with kInvalidArg before any transfer; the caller stays
+    on its device and the pipeline keeps working (the early returns restore the device and
+    drain the streams before the pinned lease is pooled again)."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(12)
+    a = rng.integers(0, 256, 5000, dtype=np.uint8)
+    b = rng.integers(0, 256, 7000, dtype=np.uint8)
+    T = h3c.ChecksumType
+    hf = h3c.HostFed(0, 1 << 20)
+    before = torch.cuda.current_device()
+    with pytest.raises(h3c.EngineError) as ei:
+        hf.run([(a, a.size, 0xFFFFFFFF, T.CRC32C), (b, b.size, 0xFFFFFFFF, T.CRC32)])
+    assert ei.value.code == 3
+    assert torch.cuda.current_device() == before
+    got = hf.run([a, b])
+    assert [int(x) for x in got] == [orc.crc32c(a), orc.crc32c(b)]
+    hf.close()
+
+
+@pytest.mark.parametrize("window", [8 << 20, 64 << 20])
+def test_hostfed_32_and_64_mib_chunks(h3c, torch_dev, window):
+    """Config 5's upper size classes: 32 and 64 MiB chunks (split across the staging windows
+    when larger than one), a ragged 64 MiB - 4093 B chunk, and small ones between them."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(window + 1)
+    lens = [32 << 20, 64 << 20, 65536, (64 << 20) - 4093, 1 << 20, 32 << 20]
+    total = sum(lens) + 16
+    pinned = torch.empty(total, dtype=torch.uint8).pin_memory()
+    host = pinned.numpy()
+    host[:] = rng.integers(0, 256, total, dtype=np.uint8)
+    items, want, off = [], [], 7
+    for L in lens:
+        items.append((pinned[off: off + L], L))
+        want.append(orc.crc32c(host[off: off + L]))
+        off += L
+    hf = h3c.HostFed(0, window)
+    exp = np.array(want, dtype=np.uint32)
+    exp[1] ^= 1
+    raw, ok, nbad = hf.run(items, expected=exp)
+    hf.close()
+    assert [int(x) for x in raw] == want
+    assert nbad == 1 and np.nonzero(~ok)[0].tolist() == [1]

@@ -224,3 +224,111 @@ def test_vpclmul_best_case_cpu_variant_matches():
         a = rng.integers(0, 256, n, dtype=np.uint8)
         for st in (0xFFFFFFFF, 0, 0xDEADBEEF):
             assert L.orc_crc32c_vpclmul(a.ctypes.data if n else None, n, st) == orc.crc32c(a, st, mech="table")
+
+
+def _std(crc_raw):
+    return (~crc_raw) & 0xFFFFFFFF
+
+
+def test_replica_remove_commit_and_syncing_restatement():
+    """REMOVE (doRemove builds {offset 0, length 0, NONE}, StorageOperator.cc:808-815) runs
+    updateChecksum case (i): {NONE, 0}, size and bytes unchanged.  COMMIT sets no checksum
+    (ChunkReplica::commit, :397-467).  A syncing full-chunk write (ReliableForwarding.cc:203-207)
+    sets meta.size = length (:289) and takes the reuse branch (:337-339)."""
+    rng = np.random.default_rng(1)
+    cs = 16384
+    chunk = np.zeros(cs, dtype=np.uint8)
+    chunk[:9000] = rng.integers(0, 256, 9000, dtype=np.uint8)
+    meta = {"size": 9000, "type": orc.CRC32C, "value": orc.crc32c(chunk[:9000])}
+    res, m2 = orc.replica_update(dict(meta), chunk, cs, {"kind": orc.UPD_COMMIT, "offset": 0, "length": 0,
+                                                         "type": 0, "value": 0})
+    assert res == {"status": 0, "size": 9000, "type": 0, "value": 0, "ucase": orc.CASE_NOT_RUN} and m2 == meta
+    p = rng.integers(0, 256, 5000, dtype=np.uint8)
+    res, m3 = orc.replica_update(dict(meta), chunk, cs, {"kind": orc.UPD_WRITE, "offset": 0, "length": 5000,
+                                                         "type": orc.CRC32C, "value": orc.crc32c(p),
+                                                         "syncing": 1}, p)
+    assert res["status"] == 0 and res["ucase"] == orc.CASE_REUSE
+    assert m3 == {"size": 5000, "type": orc.CRC32C, "value": orc.crc32c(p)}
+    res, m4 = orc.replica_update(dict(m3), chunk, cs, {"kind": orc.UPD_REMOVE, "offset": 0, "length": 0,
+                                                       "type": 0, "value": 0})
+    assert res == {"status": 0, "size": 5000, "type": 0, "value": 0, "ucase": orc.CASE_NONE}
+    assert m4 == {"size": 5000, "type": 0, "value": 0}
+
+
+def test_replica_stale_stored_checksum_semantics():
+    """What the reference stores when meta.checksumValue disagrees with the bytes: an append
+    combines with the stale value (:340-355, the error is carried, shifted), the prefix /
+    suffix case re-reads the bytes (:356-390, the error is gone), and a truncate whose
+    offset equals the size keeps the stale value (combine of length 0)."""
+    rng = np.random.default_rng(2)
+    cs = 1 << 16
+    chunk = np.zeros(cs, dtype=np.uint8)
+    chunk[:8192] = rng.integers(0, 256, 8192, dtype=np.uint8)
+    good = orc.crc32c(chunk[:8192])
+    err = 0x00400001
+    meta = {"size": 8192, "type": orc.CRC32C, "value": good ^ err}
+    p = rng.integers(0, 256, 100, dtype=np.uint8)
+    res, meta = orc.replica_update(meta, chunk, cs, {"kind": orc.UPD_WRITE, "offset": 8192, "length": 100,
+                                                     "type": orc.CRC32C, "value": orc.crc32c(p)}, p)
+    assert res["ucase"] == orc.CASE_COMBINE
+    assert meta["value"] == orc.crc32c(chunk[:8292]) ^ orc.lib().orc_shift(err, 100, orc.POLY_CRC32C)
+    res, meta2 = orc.replica_update(dict(meta), chunk.copy(), cs, {"kind": orc.UPD_TRUNCATE, "offset": 8292,
+                                                                   "length": 50, "type": 0, "value": 0})
+    assert res["ucase"] == orc.CASE_COMBINE and meta2["size"] == 50 and meta2["value"] == meta["value"]
+    q = rng.integers(0, 256, 10, dtype=np.uint8)
+    res, meta = orc.replica_update(meta, chunk, cs, {"kind": orc.UPD_WRITE, "offset": 20, "length": 10,
+                                                     "type": orc.CRC32C, "value": orc.crc32c(q)}, q)
+    assert res["ucase"] == orc.CASE_READ_CHUNK and meta["value"] == orc.crc32c(chunk[:8292])
+
+
+def test_engine_restatement_relational_pin():
+    """engine.rs's own assertion (test_engine_checksum :1229-1253 and :789-818): after every
+    update the stored std checksum is crc32c of the chunk content; the "etc" + "zzz" at offset
+    3 trace; and the checksum counters add up to the ops that reached copy_on_write /
+    safe_write."""
+    cs = 1 << 16
+    chunk = np.zeros(cs, dtype=np.uint8)
+    meta = {"size": 0, "type": orc.CRC32C, "value": 0}
+    cnt = orc.EngineCounters()
+    for off, data in ((0, b"etc"), (3, b"zzz")):
+        p = np.frombuffer(data, dtype=np.uint8)
+        res, meta = orc.engine_update(meta, chunk, cs, {"kind": orc.UPD_WRITE, "offset": off, "length": 3,
+                                                        "type": orc.CRC32C, "value": orc.crc32c(p)}, p,
+                                      counters=cnt)
+        assert res["status"] == 0
+    assert bytes(chunk[:6]) == b"etczzz" and meta["value"] == _std(orc.crc32c(b"etczzz"))
+    rng = np.random.default_rng(3)
+    host = np.zeros(cs, dtype=np.uint8)
+    size, applied = 6, 2
+    host[:6] = chunk[:6]
+    for _ in range(300):
+        u = rng.random()
+        if u < 0.6:
+            off = int(rng.integers(0, cs))
+            if rng.random() < 0.5:
+                off -= off % 4096
+            ln = int(rng.integers(0, min(cs - off, 9000) + 1))
+            if rng.random() < 0.3:
+                ln -= ln % 4096
+            p = rng.integers(0, 256, ln, dtype=np.uint8)
+            io = {"kind": orc.UPD_WRITE, "offset": off, "length": ln, "type": orc.CRC32C, "value": orc.crc32c(p)}
+            res, meta = orc.engine_update(meta, chunk, cs, io, p, payload_aligned=rng.random() < 0.5, counters=cnt)
+            if off > size:
+                host[size:off] = 0
+            host[off:off + ln] = p
+            size = max(size, off + ln)
+        else:
+            t = int(rng.integers(0, cs + 1))
+            kind = orc.UPD_TRUNCATE if u < 0.85 else orc.UPD_EXTEND
+            res, meta = orc.engine_update(meta, chunk, cs, {"kind": kind, "offset": 0, "length": t, "type": 0,
+                                                            "value": 0}, None, counters=cnt)
+            if t > size:
+                host[size:t] = 0
+            if kind == orc.UPD_TRUNCATE or t > size:
+                size = t
+        assert res["status"] == 0 and res["size"] == size == meta["size"]
+        assert meta["value"] == _std(orc.crc32c(host[:size])), _
+        assert res["type"] == orc.CRC32C and res["value"] == orc.crc32c(host[:size])
+        if res["ucase"] != orc.CASE_KEEP:
+            applied += 1
+    assert cnt.reuse + cnt.recalculate + cnt.combine >= applied - 2
