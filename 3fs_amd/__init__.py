@@ -42,8 +42,13 @@ from .engine import (  # noqa: F401
     UPDATE_IO_DTYPE,
     UPDATE_RESULT_DTYPE,
     UPD_WRITE,
+    UPD_REMOVE,
     UPD_TRUNCATE,
     UPD_EXTEND,
+    UPD_COMMIT,
+    UPD_EXACT,
+    IO_SYNCING,
+    UpdateCounters,
 )
 
 __all__ = [
@@ -77,6 +82,11 @@ __all__ = [
     "UPDATE_IO_DTYPE",
     "UPDATE_RESULT_DTYPE",
     "UPD_WRITE",
+    "UPD_REMOVE",
     "UPD_TRUNCATE",
     "UPD_EXTEND",
+    "UPD_COMMIT",
+    "UPD_EXACT",
+    "IO_SYNCING",
+    "UpdateCounters",
 ]

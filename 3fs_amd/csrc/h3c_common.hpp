@@ -113,6 +113,11 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
                uint32_t max_chunk_segs, uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc,
                const uint32_t *expected, uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind,
                uint32_t small_rows = 0);
+// Payload CRCs of UpdateIOs in 4 KiB pieces (op_piece_crc_kernel): crc0_out[i] ^= init-0 CRC
+// of op i's payload; pbase = exclusive scan of the per-op piece counts, *d_total their sum;
+// *work a zeroed work counter.
+int launch_op_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, const uint32_t *pbase, uint32_t n,
+                        const uint32_t *d_total, uint32_t *crc0_out, uint32_t *work);
 // Rows (1 KiB, absolute alignment) a byte range touches.
 inline uint32_t host_rows(uint64_t ptr, uint64_t len) {
   return len ? (uint32_t)((((ptr + len + 1023) & ~uint64_t(1023)) - (ptr & ~uint64_t(1023))) / 1024) : 0;
@@ -208,6 +213,9 @@ struct PolyConsts {
   uint32_t tabq[4][256];  // tabq[k][b] = (b << 8k) * x^(8*kQuadRowBytes): the small-chunk kernel's rows
   uint32_t tabo[4][256];  // tabo[k][b] = (b << 8k) * x^(8*128): its 8-lane (128-byte row) variant
   uint32_t tabf[4][256];  // tabf[k][b] = (b << 8k) * x^(8*64): its 4-lane (64-byte row) variant
+  // Shift tables for x^(8e), 0 <= e < 2^26 (dxpow8_fast): x^(8*4096*k) and x^(8r), r < 4096.
+  uint32_t x4k[16384];
+  uint32_t xb[4096];
 };
 constexpr int kRedTables = 7;
 constexpr int kRedWords = kRedTables * 4 * 256;  // 7168 dwords = 28 KiB of LDS
@@ -243,6 +251,10 @@ inline void build_consts(PolyConsts &pc, uint32_t poly) {
     for (int k = 0; k < 4; ++k)
       for (uint32_t b = 0; b < 256; ++b) pc.red[m][k][b] = hgf_mul(b << (8 * k), c, poly);
   }
+  const uint32_t x8 = 0x00800000u, x4096 = hxpow8n(4096, poly);
+  pc.xb[0] = pc.x4k[0] = kOne;
+  for (int r = 1; r < 4096; ++r) pc.xb[r] = hgf_mul(pc.xb[r - 1], x8, poly);
+  for (int k = 1; k < 16384; ++k) pc.x4k[k] = hgf_mul(pc.x4k[k - 1], x4096, poly);
 }
 
 using h3c_rt::DevChunk;
@@ -303,6 +315,22 @@ __device__ inline uint32_t dxpow8s(int64_t n, const PolyConsts *__restrict__ pc,
     ++k;
   }
   return r;
+}
+
+// a * b with the common identities short-cut (0 and x^0 = kOne).
+__device__ __forceinline__ uint32_t dgf_mul_fast(uint32_t a, uint32_t b, uint32_t poly) {
+  if (a == 0 || b == 0) return 0;
+  if (a == kOne) return b;
+  if (b == kOne) return a;
+  return dgf_mul(a, b, poly);
+}
+
+// x^(8e) for a signed byte count e: two table lookups and one multiply for 0 <= e < 2^26
+// (chunk offsets: kMaxChunkSize is 64 MiB, src/storage/store/ChunkMetadata.h:22), the
+// square-and-multiply chains otherwise.
+__device__ __forceinline__ uint32_t dxpow8_fast(int64_t e, const PolyConsts *__restrict__ pc, uint32_t poly) {
+  if (e >= 0 && e < (int64_t(1) << 26)) return dgf_mul_fast(pc->x4k[e >> 12], pc->xb[e & 4095], poly);
+  return dxpow8s(e, pc, poly);
 }
 
 #ifndef H3C_PERM_LAYOUT

@@ -430,6 +430,101 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
   }
 }
 
+// Kernel A''': payload CRCs of a batch of UpdateIOs, without host-built descriptors (the
+// device-resident h3c_update_ios pipeline).  Piece k of op i is [4096 j, min(4096 (j+1), len))
+// of op i's payload, where pbase[i] <= k < pbase[i] + pieces(i) and j = k - pbase[i]; the
+// piece count lives in device memory (*d_total).  A group of 4 lanes owns a piece and walks
+// it in 64-byte rows like seg_quad_kernel<4,1>; the piece's init-0 CRC, moved to the end of
+// its payload (x^(8 (len - piece end))), is XORed into crc0_out[i], which the caller zeroes.
+__global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(const h3c_update_io *__restrict__ ios,
+                                                                const uint32_t *__restrict__ pbase, uint32_t n,
+                                                                const uint32_t *__restrict__ d_total,
+                                                                const PolyConsts *__restrict__ pc,
+                                                                uint32_t *__restrict__ crc0_out,
+                                                                uint32_t *__restrict__ work) {
+  constexpr int G = 4, kLevels = 2, NG = 64 / G;
+  constexpr uint64_t kQ = 16u * G;
+  constexpr int kRed = (1 + kLevels) * 1024;
+  __shared__ uint32_t lds[kLdsWords + kRed];
+  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value_of(pc->tabf, i);
+  const uint32_t *red_g = &pc->red[0][0][0];
+  for (int i = threadIdx.x; i < kRed; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  __syncthreads();
+  const uint32_t total = *d_total;
+  const uint32_t *red = lds + kLdsWords;
+  const char *lb = reinterpret_cast<const char *>(lds);
+  const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
+  const uint32_t poly = pc->poly;
+  const LaneLut L = make_lut(lane);
+  // waves take steps of NG pieces from a shared counter (a static split left a third of the
+  // waves with one step more than the rest: a few steps per wave at 100k pieces)
+  for (;;) {
+    uint32_t q0 = 0;
+    if (lane == 0) q0 = atomicAdd(work, (uint32_t)NG);
+    q0 = (uint32_t)__builtin_amdgcn_readfirstlane(q0);
+    if (q0 >= total) break;
+    const uint32_t k = q0 + grp;
+    const bool valid = k < total;
+    uint64_t S = 0, E = 0;
+    uint32_t op = 0, shift = 0;
+    if (valid) {  // op i: the last with pbase[i] <= k (pieces of ops with none are skipped over)
+      uint32_t a = 0, b = n;
+      while (b - a > 1) {
+        const uint32_t m = (a + b) >> 1;
+        if (pbase[m] <= k) a = m; else b = m;
+      }
+      op = a;
+      const uint32_t j = k - pbase[a];
+      const h3c_update_io &io = ios[a];
+      const uint32_t off = j * 4096u, plen = min(4096u, io.length - off);
+      S = io.payload + off;
+      E = S + plen;
+      shift = io.length - off - plen;
+    }
+    const uint64_t base = S & ~(kQ - 1);
+    const uint64_t la = base + 16u * gl;
+    const uint32_t K = valid ? (uint32_t)((E - base + kQ - 1) / kQ) : 0u;
+    uint32_t kmax = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < (uint32_t)NG; ++g) kmax = max(kmax, (uint32_t)__builtin_amdgcn_readlane(K, g * G));
+    Streams st{0, 0, 0, 0};
+    uint4 cur[4], nxt[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) cur[b] = (uint32_t)b < K ? load_row(la + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+    for (uint32_t u0 = 0; u0 < kmax; u0 += 4) {
+      const uint32_t n0 = u0 + 4;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) nxt[b] = n0 + b < K ? load_row(la + (uint64_t)(n0 + b) * kQ) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t u = u0 + b;
+        if (u < K) {
+          uint4 x = cur[b];
+          if ((u == 0 && (S & (kQ - 1))) || (u + 1 == K && (E & (kQ - 1)))) x = mask_row(x, la + (uint64_t)u * kQ, S, E);
+          consume(st, x, lb, L);
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) cur[b] = nxt[b];
+    }
+    uint32_t v = tab_mul(st.s3, red) ^ st.s2;
+    v = tab_mul(v, red) ^ st.s1;
+    v = tab_mul(v, red) ^ st.s0;
+#pragma unroll
+    for (int lv = 0; lv < kLevels; ++lv) {
+      const uint32_t o = (uint32_t)__shfl_down((int)v, 1u << lv, G);
+      if ((gl & ((2u << lv) - 1u)) == 0) v ^= tab_mul(o, red + 1024 * (lv + 1));
+    }
+    if (gl == 0 && valid) {
+      const uint32_t pad = (uint32_t)(((E + kQ - 1) & ~(kQ - 1)) - E);
+      if (pad >> 4) v = dgf_mul(v, pc->fix[4 * (pad >> 4)], poly);
+      if (pad & 15) v = dgf_mul(v, pc->fixz[pad & 15], poly);
+      if (shift) v = dgf_mul_fast(v, dxpow8_fast(shift, pc, poly), poly);
+      atomicXor(&crc0_out[op], v);
+    }
+  }
+}
+
 // Kernel B: per chunk, fold segment CRCs, apply start, optionally compare.
 // Chunks with more segments than this are folded by a whole wave (finalize_big_kernel);
 // one thread folding thousands of segments serially took ~1 ms for a 64 MiB chunk.
@@ -582,11 +677,11 @@ int init_device(int dev) {
       HIP_TRY(hipSetDevice(dev));
       HIP_TRY(hipDeviceGetAttribute(&ctx.num_cu, hipDeviceAttributeMultiprocessorCount, dev));
       const uint32_t polys[2] = {kPolyCrc32c, kPolyCrc32};
+      std::vector<PolyConsts> h(1);  // ~130 KiB: not on the caller's stack
       for (int i = 0; i < 2; ++i) {
-        PolyConsts h;
-        build_consts(h, polys[i]);
+        build_consts(h[0], polys[i]);
         HIP_TRY(hipMalloc(&ctx.d_consts[i], sizeof(PolyConsts)));
-        HIP_TRY(hipMemcpy(ctx.d_consts[i], &h, sizeof(PolyConsts), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(ctx.d_consts[i], h.data(), sizeof(PolyConsts), hipMemcpyHostToDevice));
       }
       return H3C_OK;
     };
@@ -627,12 +722,12 @@ struct ProfRec {
   uint64_t bytes;
   int kind;
 };
-constexpr int kProfKinds = 3;
+constexpr int kProfKinds = 4;
 std::mutex g_prof_mu;
 std::vector<ProfRec> g_prof;
 std::atomic<int> g_prof_on{0};
-double g_prof_ms_done[kProfKinds] = {0, 0, 0};
-uint64_t g_prof_launch_done[kProfKinds] = {0, 0, 0}, g_prof_bytes_done[kProfKinds] = {0, 0, 0};
+double g_prof_ms_done[kProfKinds] = {0, 0, 0, 0};
+uint64_t g_prof_launch_done[kProfKinds] = {0, 0, 0, 0}, g_prof_bytes_done[kProfKinds] = {0, 0, 0, 0};
 
 }  // namespace
 
@@ -784,6 +879,16 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
                        seg_mul, pc, d_segcrc, expected, out_raw, ok, mismatch);
     HIP_TRY(hipGetLastError());
   }
+  return H3C_OK;
+}
+
+int launch_op_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, const uint32_t *pbase, uint32_t n,
+                        const uint32_t *d_total, uint32_t *crc0_out, uint32_t *work) {
+  const DeviceCtx &ctx = g_dev[dev];
+  const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
+  hipLaunchKernelGGL(op_piece_crc_kernel, dim3(std::max(ctx.num_cu, 1)), dim3(kThreads), 0, st, ios, pbase, n,
+                     d_total, pc, crc0_out, work);
+  HIP_TRY(hipGetLastError());
   return H3C_OK;
 }
 

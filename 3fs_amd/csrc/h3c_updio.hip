@@ -1,85 +1,102 @@
-// h3c_updio.hip -- general batched chunk updates on MI355X: every UpdateIO case of
-// ChunkReplica::update (src/storage/store/ChunkReplica.cc:131-317) and its
-// updateChecksum (:319-394), or the Rust chunk engine's Chunk::safe_write /
-// copy_on_write checksum (src/storage/chunk_engine/src/alloc/chunk.rs:89-281).
+// h3c_updio.hip -- general batched chunk updates on MI355X, every per-op step on the device:
+// ChunkReplica::update (src/storage/store/ChunkReplica.cc:131-317) with updateChecksum
+// (:319-394), or the Rust chunk engine's Engine::update_chunk / Chunk::copy_on_write /
+// safe_write (src/storage/chunk_engine/src/core/engine.rs:288-429, alloc/chunk.rs:89-281).
 //
-// The reference handles one UpdateIO at a time: verify the client checksum of the
-// payload (:193-207), zero-fill a gap, write / truncate / extend, and then either
-// reuse, combine (append), or re-read prefix + suffix of the chunk from disk and CRC
-// them (case iv: O(chunk) per write).  Here a batch of ops is applied with O(op bytes)
-// work by linearity of CRC over GF(2).  With r the raw CRC (init ~0) of the chunk's
-// n bytes, every op is an affine map of r:
-//   WRITE [o, o+len), n -> n' = max(n, o+len):
-//       r' = r * x^(8(n'-n)) ^ D * x^(8(n'-o-len)),
-//       D  = crc0(payload) ^ crc0(old[o, e)) * x^(8(o+len-e)),  e = min(o+len, n)
-//       (bytes at or past n read as zero; a gap [n, o) is zero on both sides)
-//   TRUNCATE to t < n:   r' = (r ^ crc0(old[t, n))) * x^(-8(n-t))
-//   grow to t > n (TRUNCATE or EXTEND, zero fill): r' = r * x^(8(t-n))
-//   INIT (the chunk's stored checksum is not of this polynomial): r' = crc of [0, n)
-// Pipeline (one host <-> device round trip per batch):
-//   A. payload CRC jobs of every WRITE (seg_crc_kernel via launch_crc), run on the device
-//      ahead of the update in the same stream.
-//   B. host pass in sequence order: sizes, the reference's case analysis, and byte
-//      jobs (old-range / cut-tail CRCs, payload copies, zero fills).  Jobs that touch
-//      the same 4 KiB block are put in successive epochs (conflict levels); within an
-//      epoch no two ops share a block.  The pass is speculative: it assumes every client
-//      checksum matches (a rejected op changes nothing); the device checks them after A
-//      and, on a mismatch, the copy kernels write nothing and the batch is redone with
-//      the payload CRCs known.
-//   C. per epoch: one launch_crc over the epoch's CRC jobs (reads the chunk before
-//      this epoch's writes), then one copy kernel.
-//   D. per op an affine element (M, E); rocPRIM inclusive_scan_by_key over
-//      (chunk, sequence) order composes them; r_after = r0 * M ^ E.
-//   E. host: per-op results and final chunk states from the case analysis:
-//      case (i) (write type NONE or empty chunk) stores 0; cases (ii)-(iv) store the
-//      CRC of the chunk after the op (reuse and combine equal it given a consistent
-//      stored checksum; the client checksum was verified in A).
-#include <sched.h>
+// Algebra.  With t the raw CRC of a chunk's bytes (init ~0, no final XOR) every op maps t
+// affinely, t' = t*M ^ E (GF(2)[x] mod P, x invertible):
+//   WRITE [o, o+len) (n -> n'):  M = x^(8(n'-n)),  E = crc0(new ^ old over the written range,
+//                                positioned in an n'-byte string; old bytes past n are 0)
+//   full write (o = 0, len >= n, or a syncing write):  M = 0, E = raw(payload)
+//   TRUNCATE to l < n:  M = x^(-8(n-l)), E = crc0(old[l, n)) positioned likewise
+//   grow to l > n (zero fill):  M = x^(8(l-n)), E = 0
+// The stored checksum s follows one of four rules per op, exactly as updateChecksum picks
+// them: case (i) s' = 0; reuse (ii) / prefix+suffix re-read (iv): s' = t'; append (iii):
+// s' = s*M ^ E (the same M, E: combine(~s, w, len) = s*x^(8len) ^ crc0(w)); a combine of
+// length 0 (TRUNCATE / EXTEND at offset == size): s' = s.  So each op is an element
+//   (t, s) -> (t*M ^ E, t*A ^ s*B ^ F)
+// of a monoid, and a segmented scan per chunk in sequence order gives every op's stored
+// checksum from the chunk's (t0, s0).  t0 is s0 when stored checksums are trusted (default),
+// or the CRC of the chunk's bytes (H3C_UPD_EXACT, or a stored type of another polynomial).
+//
+// E needs the old bytes an op overwrites or cuts, and those depend on earlier ops.  Every op
+// is cut into fragments, one per 4 KiB block (absolute addresses) it touches.  The fragments
+// of one block form a chain in sequence order, and one wavefront walks a chain: it loads the
+// block once into registers, applies each fragment in order (CRC of new ^ old, then the new
+// bytes), XORs each fragment's CRC, moved to its op's end, into that op's E, and stores the
+// block once.  A block's traffic is one read, one write and its payload bytes.
+//
+// Pipeline (one stream; one device->host read of the fragment count in the middle):
+//   prep       per op: validation, payload piece count, sort key (chunk)
+//   payload    op_piece_crc_kernel: payload CRCs in 4 KiB pieces -> A6 verify (:193-207)
+//   sort       (chunk, op) pairs, stable (rocPRIM radix sort)
+//   sizes      segmented scan of the size / type maps {n -> max(n, b)} u {n -> c}
+//   classify   per op: size before / after, the reference's case, fragment range
+//   fragments  expansion, chain links (LDS tile grouping + hash of per-tile last links),
+//              chain heads
+//   blocks     one wave per chain: bytes in place, E per op
+//   scan       segmented scan of the (t, s) elements; results, final chunk states, counters
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
-#include <chrono>
-#include <cstdio>
-#include <cstdlib>
 #include <cstdint>
 #include <cstring>
-#include <condition_variable>
-#include <functional>
-#include <memory>
-#include <mutex>
-#include <thread>
 #include <vector>
 
-#include <unistd.h>
-
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_scan_by_key.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "h3c_common.hpp"
 
 namespace {
 
-constexpr uint32_t kNoJob = 0xFFFFFFFFu;
-constexpr uint64_t kConflictBlock = 4096;  // ops touching a common block go to different epochs
-constexpr uint64_t kCopyPiece = 256u << 10;
+constexpr uint32_t kNil = 0xFFFFFFFFu;
+constexpr uint32_t kBlk = 4096;      // fragment granularity: 3FS's IO alignment (kAIOAlignSize)
+constexpr uint32_t kPieceBytes = 4096;
 
-enum : uint32_t { kAffNop = 0, kAffInit = 1, kAffWrite = 2, kAffTrunc = 3, kAffGrow = 4 };
+using h3c_rt::StreamDrain;
 
-struct AffIn {  // every length is below the chunk size (32 bits)
-  uint32_t nb, na; // chunk length before / after the op
-  uint32_t len;    // WRITE: payload bytes; INIT: chunk bytes
-  uint32_t pad;    // WRITE: zero bytes after the old range (o + len - e)
-  uint32_t tail;   // WRITE: bytes after the write in the new chunk (n' - o - len)
-  uint32_t job;    // CRC job (old range / cut tail / whole chunk) or kNoJob
-  uint32_t op;     // WRITE: op index (payload CRC)
-  uint32_t kind;
+// t-map kinds and s-map kinds (see the header comment)
+enum : uint8_t { kT_IDENT = 0, kT_DELTA = 1, kT_FULL = 2 };
+enum : uint8_t { kS_IDENT = 0, kS_ZERO = 1, kS_SET_T = 2, kS_APPEND = 3, kS_KEEP = 4 };
+// counter codes of an applied op
+enum : uint8_t { kC_NONE_ = 0, kC_NONE = 1, kC_REUSE = 2, kC_COMBINE = 3, kC_READ = 4, kC_RECALC = 5 };
+// device counter slots (h3c_update_counters order)
+enum { kCtrNone, kCtrReuse, kCtrCombine, kCtrRead, kCtrRecalc, kCtrMismatch, kCtrInvalid, kCtrStale, kCtrN };
+// device scalars: the payload kernel's work counter, the chain-head counter
+enum { kMiscPieceWork, kMiscHeads, kMiscN = 4 };
+
+// ---------------------------------------------------------------- scan elements
+
+// Size and type maps: n -> cst ? v : max(n, v); type -> tset ? t : type.
+struct SzTy {
+  uint32_t v;
+  uint8_t cst, tset, t, pad;
+};
+struct SzTyOp {
+  __host__ __device__ SzTy operator()(const SzTy &a, const SzTy &b) const {  // a, then b
+    SzTy r;
+    if (b.cst) {
+      r.v = b.v;
+      r.cst = 1;
+    } else {
+      r.v = a.v > b.v ? a.v : b.v;
+      r.cst = a.cst;
+    }
+    r.tset = b.tset ? 1 : a.tset;
+    r.t = b.tset ? b.t : a.t;
+    r.pad = 0;
+    return r;
+  }
 };
 
-struct Aff {
-  uint32_t m, e;  // r -> r * m ^ e
-};
-
-__host__ __device__ inline uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
+__host__ __device__ inline uint32_t hd_gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
+  if (a == 0 || b == 0) return 0;
+  if (a == kOne) return b;
+  if (b == kOne) return a;
   uint32_t p = 0;
   for (int i = 0; i < 32; ++i) {
     p ^= b & (0u - ((a >> (31 - i)) & 1u));
@@ -88,709 +105,842 @@ __host__ __device__ inline uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly
   return p;
 }
 
-struct AffOp {  // apply a, then b
+// An affine map r -> r*m ^ e (GF(2)[x] mod P).  The (t, s) map of an op is two of them:
+// t' = t*M ^ E, and -- once every op's t' is known from the first scan -- s' = s*B ^ c with
+// c = t' (reuse / re-read), E (append, B = M), or 0 (case (i), keep).
+struct Aff {
+  uint32_t m, e;
+};
+struct AffOp {
   uint32_t poly;
-  __host__ __device__ Aff operator()(const Aff &a, const Aff &b) const {
-    // most ops leave the chunk length unchanged (m = 1: overwrites inside the chunk), and
-    // then composing them is a XOR, not two bit-serial GF(2) multiplies
-    if (b.m == kOne) return Aff{a.m, a.e ^ b.e};
-    if (a.m == kOne) return Aff{b.m, gf_mul(a.e, b.m, poly) ^ b.e};
-    return Aff{gf_mul(a.m, b.m, poly), gf_mul(a.e, b.m, poly) ^ b.e};
+  __host__ __device__ Aff operator()(const Aff &x, const Aff &y) const {  // x, then y
+    // most ops keep the chunk length (m = x^0): composing them is a XOR
+    if (y.m == kOne) return Aff{x.m, x.e ^ y.e};
+    return Aff{hd_gf_mul(x.m, y.m, poly), hd_gf_mul(x.e, y.m, poly) ^ y.e};
   }
 };
 
-struct CopyPiece {
-  uint64_t dst, src, len;  // src == 0: zero fill
+// Per op, in (chunk, sequence) order.
+struct OpPos {
+  uint32_t op;      // original index
+  uint32_t nb, na;  // chunk size before / after
+  uint32_t r0, r1;  // chunk-relative byte range its fragments cover
+  uint32_t status;
+  uint8_t tk, sk;   // t-map / s-map kinds
+  uint8_t tb, ta;   // stored type before / after
+  uint8_t ccode;    // counter of an applied op (kC_*)
+  uint8_t ncomb;    // Rust engine: checksum_combine increments (0-2)
+  uint8_t pad[2];
 };
 
-// A client checksum to check against the payload's CRC on the device (speculative pass).
-struct VerifyItem {
-  uint32_t op, want;
+// One block of one op (64 B).  Ranges are block-relative byte offsets in [0, 4096].
+struct FragDesc {
+  uint64_t blk;     // absolute address of the 4 KiB block
+  uint64_t src;     // payload address of block offset 0 (meaningful on [w0, w1) only)
+  uint32_t p;       // the op's position (E accumulator index)
+  uint32_t next;    // next fragment of the same block (kNil: last)
+  uint16_t w0, w1;  // new bytes
+  uint16_t q0, q1;  // old bytes entering the CRC delta
+  uint16_t z0, z1;  // zero fill
+  uint16_t k0, k1;  // the chunk's own bytes in this block (loads / stores)
+  uint32_t mult;    // CRC contribution shift x^(8e), e = the op's size after - block end (chunk-relative)
+  uint32_t flags;
+  uint32_t pad[4];
 };
+static_assert(sizeof(FragDesc) == 64, "FragDesc is one 64-byte record");
+constexpr uint32_t kFragCrc = 1u, kFragWrite = 2u;
 
-// bad[1 + k] = item k's payload CRC differs from the client's; bad[0] = any did.
-__global__ void updio_verify_kernel(const VerifyItem *__restrict__ items, uint32_t nver,
-                                    const uint32_t *__restrict__ payraw, uint32_t std_domain,
-                                    uint32_t *__restrict__ bad) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nver) return;
-  const VerifyItem it = items[k];
-  const uint32_t got = std_domain ? ~payraw[it.op] : payraw[it.op];
-  if (got != it.want) {
-    bad[1 + k] = 1;
-    atomicOr(bad, 1u);
+// counters: a workgroup-aggregated add -- wave sums into LDS, one global atomic per counter
+// and workgroup (call from workgroup-uniform control flow; `sh` holds kCtrN slots)
+__device__ __forceinline__ void ctr_add_block(unsigned int *sh, unsigned long long *ctr, const uint32_t (&v)[8]) {
+  if (threadIdx.x < 8) sh[threadIdx.x] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint32_t x = v[k];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, 64);
+    if ((threadIdx.x & 63) == 0 && x) atomicAdd(&sh[k], x);
   }
+  __syncthreads();
+  if (threadIdx.x < 8 && sh[threadIdx.x]) atomicAdd(&ctr[threadIdx.x], (unsigned long long)sh[threadIdx.x]);
 }
 
-// One workgroup per piece (<= kCopyPiece bytes).  16-byte vector body when source and
-// destination share their alignment (or for zero fill), bytes otherwise.  Nothing is
-// written when `gate` is set (a client checksum failed in the speculative pass).
-__global__ __launch_bounds__(256) void updio_copy_kernel(const CopyPiece *__restrict__ pieces,
-                                                         const uint32_t *__restrict__ gate) {
-  if (gate && *gate) return;
-  const CopyPiece pc = pieces[blockIdx.x];
-  uint8_t *d = reinterpret_cast<uint8_t *>(pc.dst);
-  const uint8_t *s = reinterpret_cast<const uint8_t *>(pc.src);
-  const uint64_t len = pc.len;
-  if (s == nullptr || ((pc.dst ^ pc.src) & 15u) == 0) {
-    const uint64_t head = min<uint64_t>(len, (16u - (pc.dst & 15u)) & 15u);
-    for (uint64_t k = threadIdx.x; k < head; k += blockDim.x) d[k] = s ? s[k] : 0;
-    const uint64_t nvec = (len - head) / 16;
-    uint4 *d4 = reinterpret_cast<uint4 *>(d + head);
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(s ? s + head : nullptr);
-    for (uint64_t k = threadIdx.x; k < nvec; k += blockDim.x) d4[k] = s ? s4[k] : make_uint4(0, 0, 0, 0);
-    for (uint64_t k = head + 16 * nvec + threadIdx.x; k < len; k += blockDim.x) d[k] = s ? s[k] : 0;
-  } else {
-    for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) d[k] = s[k];
+// ---------------------------------------------------------------- kernels
+
+// Validation (ChunkReplica.cc:140-145 range check; the ABI's preconditions), sort keys,
+// payload piece counts.
+__global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t n, const h3c_chunk_state *__restrict__ chunks,
+                                uint32_t nchunks, uint8_t poly_type, uint32_t std_domain, uint32_t *__restrict__ status,
+                                uint32_t *__restrict__ key, uint32_t *__restrict__ idx, uint32_t *__restrict__ npieces,
+                                uint32_t *__restrict__ paycrc0, uint32_t *__restrict__ eacc,
+                                unsigned long long *__restrict__ ctr, uint32_t *__restrict__ misc) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < kCtrN) ctr[i] = 0;
+  if (i < kMiscN) misc[i] = 0;
+  if (i < n) {  // XOR accumulators of the payload and block kernels
+    paycrc0[i] = 0;
+    eacc[i] = 0;
   }
-}
-
-__global__ void updio_aff_kernel(const AffIn *__restrict__ in, uint32_t npos, const uint32_t *__restrict__ payraw,
-                                 const uint32_t *__restrict__ jobcrc, const PolyConsts *__restrict__ pc,
-                                 Aff *__restrict__ out) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= npos) return;
-  const AffIn a = in[p];
-  const uint32_t poly = pc->poly;
-  Aff r{kOne, 0u};
-  switch (a.kind) {
-    case kAffInit:  // reset to the chunk's CRC: shift(~0, n) ^ crc0(bytes)
-      r.m = 0;
-      r.e = dgf_mul(0xFFFFFFFFu, dxpow8n(a.len, pc, poly), poly) ^ jobcrc[a.job];
-      break;
-    case kAffWrite: {
-      uint32_t d = payraw[a.op] ^ dgf_mul(0xFFFFFFFFu, dxpow8n(a.len, pc, poly), poly);  // crc0(payload)
-      if (a.job != kNoJob) d ^= dgf_mul(jobcrc[a.job], dxpow8n(a.pad, pc, poly), poly);
-      r.m = dxpow8s((int64_t)a.na - (int64_t)a.nb, pc, poly);
-      r.e = dgf_mul(d, dxpow8n(a.tail, pc, poly), poly);
-      break;
-    }
-    case kAffTrunc:
-      r.m = dxpow8s((int64_t)a.na - (int64_t)a.nb, pc, poly);
-      r.e = dgf_mul(jobcrc[a.job], r.m, poly);
-      break;
-    case kAffGrow:
-      r.m = dxpow8s((int64_t)a.na - (int64_t)a.nb, pc, poly);
-      break;
-    default:
-      break;
-  }
-  out[p] = r;
-}
-
-__global__ void updio_true_kernel(const Aff *__restrict__ scan, const uint32_t *__restrict__ key, uint32_t npos,
-                                  const uint32_t *__restrict__ raw0, uint32_t poly, uint32_t *__restrict__ out) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= npos) return;
-  const Aff a = scan[p];
-  const uint32_t r0 = raw0[key[p]];
-  out[p] = (a.m == kOne ? r0 : dgf_mul(r0, a.m, poly)) ^ a.e;
-}
-
-using h3c_rt::StreamDrain;
-
-// Device arena for one call: every buffer is carved from one pooled device lease
-// (h3c_rt::DeviceLease; hipMallocAsync pools gave kernels stale bytes under ROCm 7.2).
-struct Arena {
-  char *base = nullptr;
-  size_t off = 0;
-  template <class T>
-  T *take(size_t count) {
-    T *p = reinterpret_cast<T *>(base + off);
-    off += (count * sizeof(T) + 255) & ~size_t(255);
-    return p;
-  }
-};
-
-// Segment layout of a list of CRC jobs for launch_crc.
-struct CrcBatch {
-  std::vector<DevChunk> chunks;
-  uint32_t total_segs = 0, max_segs = 0;
-  uint64_t bytes = 0, max_len = 0;
-};
-
-// set_fold_consts with a one-entry cache per constant: a batch's jobs mostly share one
-// length, and the shared memo behind set_fold_consts is thread_local (a TLS lookup per call
-// in a shared library).  One cache per thread and call (the polynomial is fixed).
-struct FoldCache {
-  uint64_t r = ~0ull, n = ~0ull;
-  uint32_t vr = 0, start = 0, vs = 0;
-  void set(DevChunk &c, uint64_t seg_bytes, uint32_t poly) {
-    const uint64_t m = (c.len + seg_bytes - 1) / seg_bytes;
-    if (!m) {
-      c.xlast = kOne;
-    } else {
-      const uint64_t rem = c.len - (m - 1) * seg_bytes;
-      if (rem != r) {
-        r = rem;
-        vr = hxpow8n_memo(rem, poly);
-      }
-      c.xlast = vr;
-    }
-    if (!c.start) {
-      c.xstart = 0;
-    } else {
-      if (c.len != n || c.start != start) {
-        n = c.len;
-        start = c.start;
-        vs = hstart_shift(c.start, c.len, poly);
-      }
-      c.xstart = vs;
-    }
-  }
-};
-
-void add_job(CrcBatch &b, FoldCache &fc, uint64_t ptr, uint64_t len, uint32_t start, uint32_t out_idx,
-             uint64_t seg_bytes, uint32_t poly) {
-  DevChunk c{};
-  c.ptr = ptr;
-  c.len = len;
-  c.start = start;
-  c.out_idx = out_idx;
-  c.seg_begin = b.total_segs;
-  fc.set(c, seg_bytes, poly);
-  const uint32_t ns = (uint32_t)((len + seg_bytes - 1) / seg_bytes);
-  b.total_segs += ns;
-  b.max_segs = std::max(b.max_segs, ns);
-  b.bytes += len;
-  b.max_len = std::max(b.max_len, len);
-  b.chunks.push_back(c);
-}
-
-enum class Src : uint8_t { kInitial, kZero, kTrue };
-
-struct Track {
-  uint32_t size = 0;
-  uint8_t type = H3C_TYPE_NONE;
-  Src src = Src::kInitial;
-  uint32_t true_pos = 0;   // scan position whose CRC is the stored value (Src::kTrue)
-  bool started = false;    // has a scan segment
-};
-
-// H3C_UPDIO_TIMING=1: per-phase wall times on stderr (tuning aid).
-struct PhaseClock {
-  bool on = std::getenv("H3C_UPDIO_TIMING") != nullptr;
-  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-  void mark(const char *what) {
-    if (!on) return;
-    const auto now = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[updio] %-10s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
-    t = now;
-  }
-};
-
-struct OpOut {
-  Src src = Src::kInitial;
-  uint32_t pos = 0;
-  uint32_t chunk = 0;
-};
-
-// Chunk- and op-indexed state of the host pass.  With T threads, thread t owns a
-// contiguous range of chunks (and their ops), so every write here is to a disjoint entry.
-struct PassShared {
-  std::vector<Track> tr;
-  std::vector<uint32_t> cur;  // next free scan position per chunk
-  std::vector<OpOut> outs;
-  std::vector<uint32_t> raw0;
-};
-
-// One thread's job lists.  Job ids are local until the merge adds the thread's base.
-struct PassLocal {
-  std::vector<CrcBatch> ep_crc;
-  std::vector<std::vector<CopyPiece>> ep_copy;
-  std::vector<VerifyItem> verify;  // speculative attempt: client checksums checked on the device
-  uint32_t njobs = 0;
-  size_t nep = 0;  // epochs in use (ep_crc / ep_copy keep their storage across calls)
-  // last epoch + 1 per 4 KiB block of the chunk being processed, tagged with `gen` (one
-  // generation per chunk, so nothing is cleared between chunks)
-  std::vector<uint64_t> blk;
-  uint32_t gen = 0;
-  void next_chunk(uint64_t blocks) {
-    if (blk.size() < blocks || gen == 0xFFFFFFFFu) {
-      blk.assign(std::max<uint64_t>(blocks, blk.size()), 0);
-      gen = 0;
-    }
-    ++gen;
-  }
-  void clear() {
-    for (size_t e = 0; e < nep; ++e) {
-      ep_crc[e].chunks.clear();
-      ep_crc[e].total_segs = ep_crc[e].max_segs = 0;
-      ep_crc[e].bytes = ep_crc[e].max_len = 0;
-      ep_copy[e].clear();
-    }
-    nep = 0;
-    verify.clear();
-    njobs = 0;
-  }
-};
-
-// A persistent worker pool for the host pass (one per calling thread, so concurrent
-// callers never wait on each other).  run(n, fn) calls fn(0..n-1); the caller runs fn(0).
-class HostPool {
- public:
-  explicit HostPool(unsigned workers) {
-    for (unsigned w = 0; w < workers; ++w) th_.emplace_back([this, w] { loop(w + 1); });
-  }
-  ~HostPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-      ++gen_;
-    }
-    cv_.notify_all();
-    for (std::thread &t : th_) t.join();
-  }
-  unsigned size() const { return (unsigned)th_.size() + 1; }
-  void run(unsigned n, const std::function<void(unsigned)> &fn) {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      fn_ = &fn;
-      n_ = n;
-      pending_ = n - 1;
-      ++gen_;
-    }
-    cv_.notify_all();
-    fn(0);
-    std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [&] { return pending_ == 0; });
-  }
-
- private:
-  void loop(unsigned id) {
-    uint64_t seen = 0;
-    for (;;) {
-      const std::function<void(unsigned)> *fn;
-      unsigned n;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (stop_) return;
-        fn = fn_;
-        n = n_;
-      }
-      if (id < n) {
-        (*fn)(id);
-        std::lock_guard<std::mutex> lk(mu_);
-        if (--pending_ == 0) done_.notify_one();
-      }
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_;
-  const std::function<void(unsigned)> *fn_ = nullptr;
-  unsigned n_ = 0, pending_ = 0;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-};
-
-// Threads for the host pass: 1 below kParallelOps ops, else H3C_HOST_THREADS, by default
-// 16 capped by the CPUs this process may run on (16 threads: 41 M writes/s against 31 M
-// with 8 on the GPU box's 16-core share, profiles/r01d_updio_host_threads_ab.txt).  A
-// service calling from many threads at once should lower it: each calling thread keeps
-// its own pool.
-constexpr uint32_t kParallelOps = 16384;
-unsigned pass_threads(uint32_t n) {
-  if (n < kParallelOps) return 1;
-  static const unsigned t = [] {
-    const char *e = std::getenv("H3C_HOST_THREADS");
-    int v = 16;
-    cpu_set_t cs;
-    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) v = std::min(v, std::max(CPU_COUNT(&cs), 1));
-    if (e) v = std::atoi(e);
-    return (unsigned)std::min(std::max(v, 1), 32);
-  }();
-  return t;
-}
-
-void run_threads(unsigned T, const std::function<void(unsigned)> &fn) {
-  if (T <= 1) {
-    fn(0);
+  if (i >= n) {
+    if (i == n) npieces[n] = 0;  // the scan's extra entry: pbase[n] = total
     return;
   }
-  thread_local std::unique_ptr<HostPool> pool;
-  thread_local pid_t owner = 0;
-  if (pool && owner != getpid()) (void)pool.release();  // forked child: the workers do not exist here
-  if (!pool || pool->size() < T) {
-    pool.reset(new HostPool(T - 1));
-    owner = getpid();
+  const h3c_update_io io = ios[i];
+  uint32_t st = H3C_OK;
+  const uint32_t c = io.chunk;
+  const bool kind_ok = io.kind == H3C_UPD_WRITE || io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND ||
+                       io.kind == H3C_UPD_REMOVE || io.kind == H3C_UPD_COMMIT;
+  if (c >= nchunks || !kind_ok) {
+    st = H3C_ERR_INVALID_ARG;
+  } else if (io.kind != H3C_UPD_COMMIT) {
+    const h3c_chunk_state cs = chunks[c];
+    const bool syncing = (io.flags & H3C_IO_SYNCING) != 0;
+    if (!cs.base || (io.checksum_type != H3C_TYPE_NONE && io.checksum_type != poly_type)) st = H3C_ERR_INVALID_ARG;
+    if (io.kind == H3C_UPD_REMOVE) {  // doRemove's form (StorageOperator.cc:808-815); no range check (:141)
+      if (io.offset || io.length || io.checksum_type != H3C_TYPE_NONE || syncing) st = H3C_ERR_INVALID_ARG;
+    } else {
+      if (io.offset >= cs.chunk_size || (uint64_t)io.offset + io.length > cs.chunk_size) st = H3C_ERR_INVALID_ARG;
+      if (io.kind == H3C_UPD_WRITE && io.length && !io.payload) st = H3C_ERR_INVALID_ARG;
+      if (syncing && (io.kind != H3C_UPD_WRITE || io.offset)) st = H3C_ERR_INVALID_ARG;
+      // A6 on a TRUNCATE / EXTEND: create(type, <no data>, length) is {NONE, 0} (:193-207);
+      // the Rust engine verifies only data (engine.rs:297)
+      if (st == H3C_OK && !std_domain && io.kind != H3C_UPD_WRITE && io.checksum_type != H3C_TYPE_NONE && io.length)
+        st = H3C_ERR_CHECKSUM_MISMATCH;
+    }
   }
-  pool->run(T, fn);
+  status[i] = st;
+  key[i] = c < nchunks ? c : nchunks;
+  idx[i] = i;
+  npieces[i] = (st == H3C_OK && io.kind == H3C_UPD_WRITE && io.length) ? (io.length + kPieceBytes - 1) / kPieceBytes : 0;
 }
 
-// fn(k) for k in [0, ntasks) on T pool threads that pull tasks from a shared counter: a
-// thread the OS runs slowly (the GPU boxes share their cores) takes fewer tasks.
-void run_tasks(unsigned T, unsigned ntasks, const std::function<void(unsigned)> &fn) {
-  std::atomic<unsigned> next{0};
-  run_threads(std::min(T, ntasks), [&](unsigned) {
-    for (unsigned k; (k = next.fetch_add(1, std::memory_order_relaxed)) < ntasks;) fn(k);
-  });
+__device__ __forceinline__ bool applied_kind(uint8_t kind) {
+  return kind == H3C_UPD_WRITE || kind == H3C_UPD_TRUNCATE || kind == H3C_UPD_EXTEND || kind == H3C_UPD_REMOVE;
 }
 
-// Per-thread host scratch, reused across calls: the pass touches tens of MB of host
-// vectors per 100k ops, and fresh allocations each call cost page faults of the same
-// order as the pass itself.
-struct UpdioScratch {
-  PassShared S;
-  std::vector<PassLocal> L;
-  CrcBatch pay;
-  std::vector<CrcBatch> pay_parts;  // payload CRC jobs per op range
-  std::vector<uint32_t> status, payraw, truev, start, opstart, order, cut, hist;
-};
-
-// Scan positions in (chunk, sequence) order, laid out before the pass: chunk c owns
-// [start[c], start[c+1]), one slot per op that passed validation plus one for an INIT
-// reset when the chunk's stored checksum is not of this polynomial.  Slots the pass does
-// not use (rejected ops) stay identity elements.  Returns the slot count.
-uint32_t plan_positions(uint8_t poly_type, const h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
-                        uint32_t n, const std::vector<uint32_t> &status, std::vector<uint32_t> &start) {
-  start.assign(nchunks + 1, 0);
-  for (uint32_t i = 0; i < n; ++i)
-    if (status[i] != H3C_ERR_INVALID_ARG) ++start[ios[i].chunk + 1];
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    if (start[c + 1] && chunks[c].size != 0 && chunks[c].type != poly_type) ++start[c + 1];
-    start[c + 1] += start[c];
+// A6 (:193-207, engine.rs:297-312), the payload's raw CRC against the client's checksum, and
+// the size / type map of each op, in sorted order.
+__global__ void uio_sz_elem_kernel(const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ order, uint32_t n,
+                                   uint32_t *__restrict__ status, const uint32_t *__restrict__ paycrc0,
+                                   const PolyConsts *__restrict__ pc, uint8_t poly_type, uint32_t std_domain,
+                                   uint32_t *__restrict__ payraw, SzTy *__restrict__ el) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t i = order[p];
+  const h3c_update_io io = ios[i];
+  uint32_t st = status[i];
+  if (io.kind == H3C_UPD_WRITE && st == H3C_OK) {
+    const uint32_t poly = pc->poly;
+    const uint32_t raw = io.length ? paycrc0[i] ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(io.length, pc, poly), poly)
+                                   : 0xFFFFFFFFu;
+    payraw[i] = raw;
+    if (io.checksum_type != H3C_TYPE_NONE && io.length && (std_domain ? ~raw : raw) != io.checksum_value) {
+      st = H3C_ERR_CHECKSUM_MISMATCH;
+      status[i] = st;
+    }
   }
-  return start[nchunks];
+  SzTy e{0, 0, 0, 0, 0};
+  if (st == H3C_OK && applied_kind(io.kind)) {
+    switch (io.kind) {
+      case H3C_UPD_WRITE:  // doRealWrite (:122-124); a syncing write sets meta.size = length (:289)
+        if (io.flags & H3C_IO_SYNCING) {
+          e.cst = 1;
+          e.v = io.length;
+        } else {
+          e.v = io.offset + io.length;
+        }
+        e.tset = 1;
+        e.t = std_domain ? poly_type : io.checksum_type;  // :392
+        break;
+      case H3C_UPD_TRUNCATE:  // :261-273: the new length either way
+        e.cst = 1;
+        e.v = io.length;
+        break;
+      case H3C_UPD_EXTEND:
+        e.v = io.length;
+        break;
+      case H3C_UPD_REMOVE:  // case (i) with a NONE checksum (:334-336, :392)
+        e.tset = 1;
+        e.t = H3C_TYPE_NONE;
+        break;
+      default:
+        break;
+    }
+    if (std_domain && io.kind != H3C_UPD_WRITE) {  // the engine reports every result as CRC32C (ChunkEngine.cc:66)
+      e.tset = 1;
+      e.t = poly_type;
+    }
+  }
+  el[p] = e;
 }
 
-// Op indices grouped by chunk, each group in sequence order (a stable counting sort):
-// the ops of chunk c are order[opstart[c] .. opstart[c+1]).  Ops naming no chunk of the
-// batch are left out; other invalid ops stay (their result reports the chunk's size).
-void group_ops(const h3c_update_io *ios, uint32_t n, uint32_t nchunks, std::vector<uint32_t> &opstart,
-               std::vector<uint32_t> &order) {
-  opstart.assign(nchunks + 1, 0);
-  for (uint32_t i = 0; i < n; ++i)
-    if (ios[i].chunk < nchunks) ++opstart[ios[i].chunk + 1];
-  for (uint32_t c = 0; c < nchunks; ++c) opstart[c + 1] += opstart[c];
-  order.resize(opstart[nchunks]);
-  std::vector<uint32_t> fill(opstart.begin(), opstart.end() - 1);
-  for (uint32_t i = 0; i < n; ++i)
-    if (ios[i].chunk < nchunks) order[fill[ios[i].chunk]++] = i;
+__device__ __forceinline__ uint32_t blocks_of(uint64_t base, uint32_t r0, uint32_t r1) {
+  return r1 > r0 ? (uint32_t)(((base + r1 - 1) >> 12) - ((base + r0) >> 12) + 1) : 0u;
 }
 
-// plan_positions + group_ops in one parallel counting sort (per-op-range histograms,
-// prefix, stable scatter) when the per-thread histograms are small against the batch.
-void layout_ops(uint8_t poly_type, const h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
-                uint32_t n, const std::vector<uint32_t> &status, unsigned T, std::vector<uint32_t> &start,
-                std::vector<uint32_t> &opstart, std::vector<uint32_t> &order, std::vector<uint32_t> &hist) {
-  if (T <= 1 || (uint64_t)nchunks * 4 > n) {
-    plan_positions(poly_type, chunks, nchunks, ios, n, status, start);
-    group_ops(ios, n, nchunks, opstart, order);
+// The reference's case analysis per op (ChunkReplica.cc:246, 319-394; engine.rs:375-423 and
+// chunk.rs:89-281 in the std domain), the maps' kinds, and the op's fragment range.
+// `reject_pass`: only mark TRUNCATE / EXTEND of chunks stored under the other polynomial
+// (the caller then rescans sizes).
+__global__ void uio_classify_kernel(const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ order,
+                                    const uint32_t *__restrict__ skey, uint32_t n, const h3c_chunk_state *__restrict__ chunks,
+                                    uint32_t nchunks, const SzTy *__restrict__ scan, uint32_t *__restrict__ status,
+                                    uint8_t poly_type, uint32_t std_domain, uint32_t reject_pass, OpPos *__restrict__ pos,
+                                    uint32_t *__restrict__ nfrag) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) {
+    if (p == n && !reject_pass) nfrag[n] = 0;
     return;
   }
-  // hist[t][c]: ops of range t naming chunk c; hist[T + t][c]: of those, the ones that passed validation
-  hist.resize((size_t)2 * T * nchunks);
-  auto range = [&](unsigned t, uint32_t &i0, uint32_t &i1) {
-    i0 = (uint32_t)((uint64_t)n * t / T);
-    i1 = (uint32_t)((uint64_t)n * (t + 1) / T);
-  };
-  run_threads(T, [&](unsigned t) {
-    uint32_t *all = &hist[(size_t)t * nchunks], *ok = &hist[(size_t)(T + t) * nchunks];
-    std::fill(all, all + nchunks, 0u);
-    std::fill(ok, ok + nchunks, 0u);
-    uint32_t i0, i1;
-    range(t, i0, i1);
-    for (uint32_t i = i0; i < i1; ++i) {
-      const uint32_t c = ios[i].chunk;
-      if (c >= nchunks) continue;
-      ++all[c];
-      ok[c] += status[i] != H3C_ERR_INVALID_ARG;
+  const uint32_t i = order[p], c = skey[p];
+  const h3c_update_io io = ios[i];
+  OpPos r{};
+  r.op = i;
+  r.status = status[i];
+  if (c >= nchunks) {  // names no chunk of the batch
+    if (!reject_pass) {
+      pos[p] = r;
+      nfrag[p] = 0;
     }
-  });
-  start.resize(nchunks + 1);
-  opstart.resize(nchunks + 1);
-  uint32_t pos = 0, op = 0;
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    start[c] = pos;
-    opstart[c] = op;
-    uint32_t nok = 0;
-    for (unsigned t = 0; t < T; ++t) {
-      uint32_t &a = hist[(size_t)t * nchunks + c];
-      const uint32_t na = a;
-      a = op;  // becomes range t's scatter base for chunk c
-      op += na;
-      nok += hist[(size_t)(T + t) * nchunks + c];
-    }
-    pos += nok + (nok && chunks[c].size != 0 && chunks[c].type != poly_type ? 1u : 0u);
+    return;
   }
-  start[nchunks] = pos;
-  opstart[nchunks] = op;
-  order.resize(op);
-  run_threads(T, [&](unsigned t) {
-    uint32_t *base = &hist[(size_t)t * nchunks];
-    uint32_t i0, i1;
-    range(t, i0, i1);
-    for (uint32_t i = i0; i < i1; ++i)
-      if (ios[i].chunk < nchunks) order[base[ios[i].chunk]++] = i;
-  });
-}
-
-// Thread t's chunks [cut[t], cut[t+1]): contiguous ranges of about n/T ops each.
-void cut_chunks(const std::vector<uint32_t> &opstart, uint32_t nchunks, unsigned T, std::vector<uint32_t> &cut) {
-  cut.assign(T + 1, nchunks);
-  cut[0] = 0;
-  const uint64_t total = opstart[nchunks];
-  uint32_t c = 0;
-  for (unsigned t = 1; t < T; ++t) {
-    const uint64_t want = total * t / T;
-    while (c < nchunks && opstart[c] < want) ++c;
-    cut[t] = std::max(c, cut[t - 1]);
+  const h3c_chunk_state cs = chunks[c];
+  uint32_t nb = cs.size, tb = cs.type;
+  if (p > 0 && skey[p - 1] == c) {
+    const SzTy b = scan[p - 1];
+    nb = b.cst ? b.v : (cs.size > b.v ? cs.size : b.v);
+    if (b.tset) tb = b.t;
   }
-}
-
-// B. the host pass over chunks [clo, chi), each chunk's ops in sequence order.
-// `payraw` == nullptr: speculative (every WRITE's client checksum is assumed to match and
-// queued for the device check); otherwise the payload CRCs are known and `status` already
-// carries every mismatch.  S.outs (indexed like `order`, so each thread writes one
-// contiguous range: no false sharing) must hold order.size() entries and S.tr / S.cur /
-// S.raw0 nchunks;
-// this thread fills its own.
-void host_pass(uint8_t poly_type, uint32_t poly, bool std_domain, const h3c_chunk_state *chunks,
-               const h3c_update_io *ios, uint32_t *status, const uint32_t *payraw, uint64_t seg_j,
-               const uint32_t *start, const uint32_t *opstart, const uint32_t *order, AffIn *lay, uint32_t *keys,
-               uint32_t clo, uint32_t chi, PassShared &S, PassLocal &L) {
-  L.clear();
-  // The current chunk's state lives in locals and is stored once per chunk: S.tr / S.cur /
-  // S.raw0 entries of neighbouring chunks share cache lines across threads.
-  Track tk;
-  uint32_t cur = 0, raw0 = 0;
-  FoldCache fc;
-
-  auto epoch_for = [&](uint32_t c, uint64_t a, uint64_t b) -> uint32_t {  // touched [a, b) of chunk c
-    (void)c;
-    if (b <= a) return 0;
-    uint32_t e = 0;
-    const uint64_t b0 = a / kConflictBlock, b1 = (b - 1) / kConflictBlock;
-    const uint64_t tag = (uint64_t)L.gen << 32;
-    for (uint64_t k = b0; k <= b1; ++k)
-      if ((L.blk[k] & ~0xFFFFFFFFull) == tag) e = std::max(e, (uint32_t)L.blk[k]);
-    for (uint64_t k = b0; k <= b1; ++k) L.blk[k] = tag | (e + 1);
-    if (L.nep <= e) {
-      L.nep = e + 1;
-      if (L.ep_crc.size() < L.nep) {
-        L.ep_crc.resize(L.nep);
-        L.ep_copy.resize(L.nep);
+  const SzTy a = scan[p];
+  const uint32_t na_scan = a.cst ? a.v : (cs.size > a.v ? cs.size : a.v);
+  if (reject_pass) {
+    if (r.status == H3C_OK && (io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND) && tb != H3C_TYPE_NONE &&
+        tb != poly_type)
+      status[i] = H3C_ERR_INVALID_ARG;  // documented limit: its stored type cannot be derived here
+    return;
+  }
+  r.nb = nb;
+  r.na = nb;
+  r.tb = (uint8_t)tb;
+  r.ta = (uint8_t)tb;
+  r.tk = kT_IDENT;
+  r.sk = kS_IDENT;
+  const bool applied = r.status == H3C_OK && applied_kind(io.kind);
+  if (applied) {
+    const uint32_t na = na_scan;
+    r.na = na;
+    const uint32_t o = io.offset, len = io.length;
+    const bool syncing = (io.flags & H3C_IO_SYNCING) != 0;
+    if (io.kind == H3C_UPD_WRITE) {
+      const bool full = syncing || (o == 0 && len >= nb);
+      if (full) {
+        r.tk = kT_FULL;
+        r.r0 = 0;
+        r.r1 = len;
+      } else if (len || o > nb) {
+        r.tk = kT_DELTA;
+        r.r0 = o > nb ? nb : o;
+        r.r1 = o + len;
       }
-    }
-    return e;
-  };
-  auto add_copy = [&](uint32_t e, uint64_t dst, uint64_t src, uint64_t len) {
-    for (uint64_t k = 0; k < len; k += kCopyPiece)
-      L.ep_copy[e].push_back(CopyPiece{dst + k, src ? src + k : 0, std::min(kCopyPiece, len - k)});
-  };
-  auto new_elem = [&](const AffIn &a) -> uint32_t {
-    const uint32_t p = cur++;
-    lay[p] = a;
-    return p;
-  };
-
-  const uint32_t kend = opstart[chi];
-  for (uint32_t c = clo; c < chi; ++c) {
-    tk = Track{};
-    tk.size = chunks[c].size;
-    tk.type = chunks[c].type;
-    cur = start[c];
-    raw0 = 0;
-    L.next_chunk(((uint64_t)chunks[c].chunk_size + kConflictBlock - 1) / kConflictBlock);
-    for (uint32_t k = opstart[c]; k < opstart[c + 1]; ++k) {
-      if (k + 16 < kend) {  // ops are visited in chunk order: their records are scattered
-        __builtin_prefetch(&ios[order[k + 16]]);
-        __builtin_prefetch(&status[order[k + 16]]);
-      }
-      const uint32_t i = order[k];
-      const h3c_update_io &io = ios[i];
-      if (status[i] == H3C_ERR_INVALID_ARG) continue;  // (marked by an earlier attempt)
-      const uint64_t base = chunks[c].base;
-      // A6: the client's checksum of the payload (:193-207); TRUNCATE / EXTEND carry NONE.
-      if (status[i] == H3C_OK && io.checksum_type != H3C_TYPE_NONE && io.length != 0) {
-        if (io.kind != H3C_UPD_WRITE) {
-          status[i] = H3C_ERR_CHECKSUM_MISMATCH;
-        } else if (payraw) {
-          const uint32_t got = std_domain ? ~payraw[i] : payraw[i];
-          if (got != io.checksum_value) status[i] = H3C_ERR_CHECKSUM_MISMATCH;
-        } else {
-          L.verify.push_back(VerifyItem{i, io.checksum_value});
+      if (!std_domain) {
+        const uint8_t tw = io.checksum_type;
+        r.ta = tw;
+        if (tw == H3C_TYPE_NONE || na == 0) {  // (i)
+          r.sk = kS_ZERO;
+          r.ccode = kC_NONE;
+        } else if (o == 0 && len == na) {  // (ii): the client's value, verified = raw(payload) = t'
+          r.sk = kS_SET_T;
+          r.ccode = kC_REUSE;
+        } else if (tw == tb && nb > 0 && o == nb) {  // (iii)
+          r.sk = kS_APPEND;
+          r.ccode = kC_COMBINE;
+        } else {  // (iv)
+          r.sk = kS_SET_T;
+          r.ccode = kC_READ;
         }
-      }
-      if (status[i] == H3C_ERR_CHECKSUM_MISMATCH) {  // rejected: nothing changes
-        S.outs[k] = OpOut{tk.src, tk.true_pos, c};
-        continue;
-      }
-      // TRUNCATE / EXTEND store a checksum of the chunk's own type (:328-332); one of the
-      // other polynomial cannot be derived from this batch's CRC state (documented limit).
-      if (io.kind != H3C_UPD_WRITE && !std_domain && tk.type != H3C_TYPE_NONE && tk.type != poly_type) {
-        status[i] = H3C_ERR_INVALID_ARG;
-        continue;
-      }
-      if (!tk.started) {  // the chunk's scan segment starts from a known CRC or an INIT reset
-        tk.started = true;
-        const h3c_chunk_state &cs = chunks[c];
-        if (cs.size == 0) {
-          raw0 = 0xFFFFFFFFu;  // raw CRC of no bytes
-        } else if (cs.type == poly_type) {
-          raw0 = std_domain ? ~cs.value : cs.value;
-        } else {
-          const uint32_t e = epoch_for(c, 0, cs.size);
-          add_job(L.ep_crc[e], fc, base, cs.size, 0u, L.njobs, seg_j, poly);
-          AffIn a{};
-          a.kind = kAffInit;
-          a.len = cs.size;
-          a.job = L.njobs++;
-          new_elem(a);
-        }
-      }
-      const uint64_t nb = tk.size;
-      uint64_t na = nb;
-      AffIn a{};
-      a.job = kNoJob;
-      uint8_t type_after = tk.type;
-      if (io.kind == H3C_UPD_WRITE) {  // :281-291, doRealWrite :124
-        const uint64_t o = io.offset, len = io.length;
-        na = std::max<uint64_t>(nb, o + len);
-        const uint32_t e = epoch_for(c, std::min(o, nb), (o > nb || len) ? o + len : 0);
-        if (o < nb && len) {
-          const uint64_t end = std::min(o + len, nb);
-          add_job(L.ep_crc[e], fc, base + o, end - o, 0u, L.njobs, seg_j, poly);
-          a.job = L.njobs++;
-          a.pad = (uint32_t)(o + len - end);
-        }
-        if (o > nb) add_copy(e, base + nb, 0, o - nb);
-        if (len) add_copy(e, base + o, io.payload, len);
-        a.kind = kAffWrite;
-        a.len = (uint32_t)len;
-        a.tail = (uint32_t)(na - o - len);
-        a.op = i;
-        type_after = io.checksum_type;
-      } else {  // TRUNCATE / EXTEND (:260-273)
-        const uint64_t l = io.length;
-        if (l < nb && io.kind == H3C_UPD_TRUNCATE) {
-          na = l;
-          const uint32_t e = epoch_for(c, l, nb);
-          add_job(L.ep_crc[e], fc, base + l, nb - l, 0u, L.njobs, seg_j, poly);
-          a.kind = kAffTrunc;
-          a.job = L.njobs++;
-        } else if (l > nb) {
-          na = l;
-          const uint32_t e = epoch_for(c, nb, l);
-          add_copy(e, base + nb, 0, l - nb);
-          a.kind = kAffGrow;
-        } else {
-          a.kind = kAffNop;
-        }
-      }
-      a.nb = (uint32_t)nb;
-      a.na = (uint32_t)na;
-      const uint32_t id = new_elem(a);
-      tk.size = (uint32_t)na;
-      tk.type = type_after;
-      // updateChecksum: case (i) stores 0 (:334-336); (ii)-(iv) the chunk's CRC.
-      if (!std_domain && (type_after == H3C_TYPE_NONE || na == 0)) {
-        tk.src = Src::kZero;
       } else {
-        tk.src = Src::kTrue;
-        tk.true_pos = id;  // scan position
+        r.ta = poly_type;
+        if (syncing || (len > 0 && o < nb)) {  // copy_on_write (engine.rs:377-391)
+          r.sk = kS_SET_T;
+          r.ccode = (syncing || (o == 0 && len >= nb)) ? kC_REUSE : kC_RECALC;  // chunk.rs:112,152-158
+        } else if (na > nb) {  // safe_write append / zero pad (chunk.rs:200-276)
+          r.sk = kS_APPEND;
+          r.ccode = kC_COMBINE;
+          const bool aligned = nb % kBlk == 0 && o % kBlk == 0 && (len == 0 || (io.payload % kBlk == 0 && len % kBlk == 0));
+          r.ncomb = aligned ? (uint8_t)((o > nb ? 1 : 0) + (len ? 1 : 0)) : (uint8_t)1;
+        } else {
+          r.sk = kS_KEEP;
+        }
       }
-      S.outs[k] = OpOut{tk.src, tk.true_pos, c};
+    } else if (io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND) {
+      if (na < nb) {
+        r.tk = kT_DELTA;
+        r.r0 = na;
+        r.r1 = nb;
+      } else if (na > nb) {
+        r.tk = kT_DELTA;
+        r.r0 = nb;
+        r.r1 = na;
+      }
+      if (!std_domain) {  // the write checksum is create(meta type, nullptr, 0), offset = size, len 0 (:328-332)
+        if (tb == H3C_TYPE_NONE || na == 0) {
+          r.sk = kS_ZERO;
+          r.ccode = kC_NONE;
+        } else if (nb > 0 && io.offset == nb) {  // isAppendWrite (:246): a combine of length 0 keeps the value
+          r.sk = kS_KEEP;
+          r.ccode = kC_COMBINE;
+        } else {
+          r.sk = kS_SET_T;
+          r.ccode = kC_READ;
+        }
+      } else {
+        r.ta = poly_type;
+        if (io.kind == H3C_UPD_TRUNCATE && na < nb) {  // chunk.rs:184-197
+          r.sk = kS_SET_T;
+          r.ccode = kC_RECALC;
+        } else if (na > nb) {  // zero pad (chunk.rs:205-218, 250-255)
+          r.sk = kS_APPEND;
+          r.ccode = kC_COMBINE;
+          r.ncomb = 1;
+        } else {
+          r.sk = kS_KEEP;
+        }
+      }
+    } else {  // REMOVE
+      if (!std_domain) {
+        r.sk = kS_ZERO;
+        r.ccode = kC_NONE;
+        r.ta = H3C_TYPE_NONE;
+      } else {
+        r.sk = kS_KEEP;  // engine.rs:376
+        r.ta = poly_type;
+      }
     }
-    S.tr[c] = tk;
-    S.cur[c] = cur;
-    S.raw0[c] = raw0;
-    for (uint32_t p = cur; p < start[c + 1]; ++p) lay[p] = AffIn{0, 0, 0, 0, 0, kNoJob, 0, kAffNop};
-    for (uint32_t p = start[c]; p < start[c + 1]; ++p) keys[p] = c;
+  }
+  pos[p] = r;
+  nfrag[p] = r.tk == kT_IDENT ? 0u : blocks_of(cs.base, r.r0, r.r1);
+}
+
+
+__device__ __forceinline__ uint16_t rel_clamp(int64_t a, int64_t rel) {
+  const int64_t x = a - rel;
+  return (uint16_t)(x < 0 ? 0 : (x > (int64_t)kBlk ? (int64_t)kBlk : x));
+}
+
+// Fragment k: the j-th 4 KiB block (absolute) of op position p's range [base + r0, base + r1).
+// The fragment kernels size their grids for a host guess `cap` and read the real count F =
+// fbase[n] on the device: no mid-batch round trip.  F > cap: they do nothing (the block
+// kernel then finds no chains) and the host redoes them with F known.
+__device__ __forceinline__ uint32_t frag_count(const uint32_t *__restrict__ d_F, uint32_t cap) {
+  const uint32_t F = *d_F;
+  return F <= cap ? F : 0u;
+}
+
+__global__ void uio_frag_kernel(const OpPos *__restrict__ pos, const uint32_t *__restrict__ fbase, uint32_t n,
+                                uint32_t cap, const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ skey,
+                                const h3c_chunk_state *__restrict__ chunks, FragDesc *__restrict__ frags,
+                                uint64_t *__restrict__ fkey, const PolyConsts *__restrict__ pc,
+                                uint32_t *__restrict__ hhead, uint32_t hcap) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < hcap) hhead[k] = kNil;  // the link hash's bucket heads (uio_tlink_kernel runs next)
+  const uint32_t F = frag_count(fbase + n, cap);
+  if (k >= F) return;
+  uint32_t a = 0, b = n;  // the last p with fbase[p] <= k
+  while (b - a > 1) {
+    const uint32_t m = (a + b) >> 1;
+    if (fbase[m] <= k) a = m; else b = m;
+  }
+  const uint32_t p = a;
+  const OpPos r = pos[p];
+  const uint32_t c = skey[p];
+  const h3c_chunk_state cs = chunks[c];
+  const h3c_update_io io = ios[r.op];
+  const uint64_t blk = (((cs.base + r.r0) >> 12) + (k - fbase[p])) << 12;
+  const int64_t rel = (int64_t)blk - (int64_t)cs.base;  // chunk offset of the block's first byte
+  FragDesc d{};
+  d.blk = blk;
+  d.p = p;
+  d.next = kNil;
+  d.k0 = rel_clamp(0, rel);
+  d.k1 = rel_clamp(cs.chunk_size, rel);
+  d.mult = dxpow8_fast((int64_t)r.na - (rel + (int64_t)kBlk), pc, pc->poly);
+  auto range = [&](int64_t x0, int64_t x1, uint16_t &o0, uint16_t &o1) {
+    o0 = rel_clamp(x0, rel);
+    o1 = rel_clamp(x1, rel);
+    if (o1 <= o0) o0 = o1 = 0;
+  };
+  if (io.kind == H3C_UPD_WRITE) {
+    const int64_t o = io.offset, e = (int64_t)io.offset + io.length;
+    d.src = io.payload + (uint64_t)rel - (uint64_t)io.offset;
+    range(o, e, d.w0, d.w1);
+    if (r.tk == kT_DELTA) {
+      range(o, e < (int64_t)r.nb ? e : (int64_t)r.nb, d.q0, d.q1);
+      if (o > (int64_t)r.nb) range(r.nb, o, d.z0, d.z1);
+      if (d.w1 > d.w0) d.flags |= kFragCrc;
+    }
+    if (d.w1 > d.w0 || d.z1 > d.z0) d.flags |= kFragWrite;
+  } else if (r.na < r.nb) {  // truncate: the cut bytes leave the CRC
+    range(r.na, r.nb, d.q0, d.q1);
+    if (d.q1 > d.q0) d.flags |= kFragCrc;
+  } else {  // grow: zero fill
+    range(r.nb, r.na, d.z0, d.z1);
+    if (d.z1 > d.z0) d.flags |= kFragWrite;
+  }
+  frags[k] = d;
+  fkey[k] = ((uint64_t)c << 36) | (blk >> 12);
+}
+
+// ---- chain links: each fragment's previous fragment of the same (chunk, block) ----
+// Tiles of kLinkTile consecutive fragments group by key in LDS (open addressing on the
+// 64-bit key, per-key lists of tile positions); a fragment's predecessor inside its tile is
+// the largest earlier listed position.  Each tile's last fragment of a key is pushed (one
+// atomicExch) on its hash bucket's list in HBM; a fragment with no predecessor in its tile
+// takes the largest listed index of its key below its own (h3c_update.hip uses the same
+// scheme for block writes).  Fragments are numbered in (chunk, sequence) order, so index
+// order within a key is sequence order.
+constexpr uint32_t kLinkTile = 256;
+constexpr unsigned long long kNoKey = ~0ull;
+
+__device__ __forceinline__ uint32_t key_hash(uint64_t key) {
+  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32);
+}
+
+__global__ __launch_bounds__(kLinkTile) void uio_tlink_kernel(const uint64_t *__restrict__ fkey,
+                                                              const uint32_t *__restrict__ d_F, uint32_t cap,
+                                                              uint32_t *hhead, uint32_t hmask,
+                                                              uint32_t *__restrict__ gnext, uint32_t *__restrict__ prev) {
+  __shared__ unsigned long long gkey[2 * kLinkTile];
+  __shared__ uint32_t ghead[2 * kLinkTile], gnx[kLinkTile];
+  const uint32_t F = frag_count(d_F, cap);
+  const uint32_t t = threadIdx.x, k0 = blockIdx.x * kLinkTile, k = k0 + t;
+  if (k0 >= F) return;  // (whole workgroup: before any barrier)
+  for (uint32_t e = t; e < 2 * kLinkTile; e += kLinkTile) {
+    gkey[e] = kNoKey;
+    ghead[e] = kNil;
+  }
+  __syncthreads();
+  const unsigned long long key = k < F ? (unsigned long long)fkey[k] : kNoKey;
+  uint32_t h = kNil;
+  if (key != kNoKey) {
+    h = key_hash(key) & (2 * kLinkTile - 1);
+    for (;;) {
+      const unsigned long long old = atomicCAS(&gkey[h], kNoKey, key);
+      if (old == kNoKey || old == key) break;
+      h = (h + 1) & (2 * kLinkTile - 1);
+    }
+    gnx[t] = atomicExch(&ghead[h], t);
+  }
+  __syncthreads();
+  uint32_t pin = kNil;
+  bool last = true;
+  if (h != kNil)
+    for (uint32_t u = ghead[h]; u != kNil; u = gnx[u]) {
+      if (u < t && (pin == kNil || u > pin)) pin = u;
+      if (u > t) last = false;
+    }
+  if (k < F) {
+    prev[k] = pin == kNil ? kNil : k0 + pin;
+    if (last) gnext[k] = atomicExch(&hhead[(key_hash(key) >> 7) & hmask], k);
   }
 }
 
-// Where the threads' lists go in the flattened per-epoch arrays (epoch-major, then thread).
-struct PassMerge {
-  size_t nep = 0, crc_total = 0, copy_total = 0, ver_total = 0;
-  uint32_t njobs = 0, max_segs = 0;
-  std::vector<uint32_t> job_base;             // [t]
-  std::vector<size_t> ver_off;                // [t]
-  std::vector<size_t> crc_off, copy_off;      // [e * T + t]
-  std::vector<uint32_t> seg_base;             // [e * T + t]: segments of earlier threads in epoch e
-  std::vector<CrcBatch> ep;                   // per-epoch totals (chunks unused)
-  std::vector<size_t> ep_crc_begin, ep_copy_begin, ep_copy_count;
+__global__ void uio_resolve_kernel(const uint64_t *__restrict__ fkey, const uint32_t *__restrict__ d_F, uint32_t cap,
+                                   const uint32_t *__restrict__ hhead, uint32_t hmask,
+                                   const uint32_t *__restrict__ gnext, uint32_t *__restrict__ prev) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= frag_count(d_F, cap) || prev[k] != kNil) return;
+  const uint64_t key = fkey[k];
+  uint32_t p = kNil;
+  for (uint32_t j = hhead[(key_hash(key) >> 7) & hmask]; j != kNil; j = gnext[j])
+    if (j < k && fkey[j] == key && (p == kNil || j > p)) p = j;
+  prev[k] = p;
+}
 
-  void build(const std::vector<PassLocal> &L, unsigned T) {
-    nep = 0;
-    for (unsigned t = 0; t < T; ++t) nep = std::max(nep, L[t].nep);
-    job_base.assign(T, 0);
-    ver_off.assign(T, 0);
-    njobs = 0;
-    ver_total = 0;
-    for (unsigned t = 0; t < T; ++t) {
-      job_base[t] = njobs;
-      njobs += L[t].njobs;
-      ver_off[t] = ver_total;
-      ver_total += L[t].verify.size();
-    }
-    crc_off.assign(nep * T, 0);
-    copy_off.assign(nep * T, 0);
-    seg_base.assign(nep * T, 0);
-    ep.assign(nep, CrcBatch{});
-    ep_crc_begin.assign(nep, 0);
-    ep_copy_begin.assign(nep, 0);
-    ep_copy_count.assign(nep, 0);
-    crc_total = copy_total = 0;
-    max_segs = 0;
-    for (size_t e = 0; e < nep; ++e) {
-      ep_crc_begin[e] = crc_total;
-      ep_copy_begin[e] = copy_total;
-      for (unsigned t = 0; t < T; ++t) {
-        crc_off[e * T + t] = crc_total;
-        copy_off[e * T + t] = copy_total;
-        seg_base[e * T + t] = ep[e].total_segs;
-        if (e < L[t].nep) {
-          const CrcBatch &b = L[t].ep_crc[e];
-          crc_total += b.chunks.size();
-          copy_total += L[t].ep_copy[e].size();
-          ep[e].total_segs += b.total_segs;
-          ep[e].max_segs = std::max(ep[e].max_segs, b.max_segs);
-          ep[e].bytes += b.bytes;
-          ep[e].max_len = std::max(ep[e].max_len, b.max_len);
-        }
-      }
-      ep_copy_count[e] = copy_total - ep_copy_begin[e];
-      max_segs = std::max(max_segs, ep[e].total_segs);
-    }
+// next pointers, and the chain heads appended to `heads` (one atomic per wave; the order of
+// the chains is free: they touch disjoint blocks)
+__global__ void uio_heads_kernel(const uint32_t *__restrict__ prev, const uint32_t *__restrict__ d_F, uint32_t cap,
+                                 FragDesc *__restrict__ frags, uint32_t *__restrict__ heads,
+                                 uint32_t *__restrict__ nheads) {
+  const uint32_t F = frag_count(d_F, cap);
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t p = k < F ? prev[k] : 0u;
+  const bool head = k < F && p == kNil;
+  if (k < F && !head) frags[p].next = k;
+  const uint64_t m = __ballot(head);
+  if (!m) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(nheads, (uint32_t)__builtin_popcountll(m));
+  base = (uint32_t)__shfl((int)base, (int)leader, 64);
+  if (head) heads[base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = k;
+}
+
+// ---- the block kernel ----
+__device__ __forceinline__ uint4 mask16(uint32_t rel, uint32_t s, uint32_t e) {
+  return make_uint4(byte_mask(rel, s, e), byte_mask(rel + 4, s, e), byte_mask(rel + 8, s, e), byte_mask(rel + 12, s, e));
+}
+__device__ __forceinline__ uint4 and4(uint4 a, uint4 m) { return make_uint4(a.x & m.x, a.y & m.y, a.z & m.z, a.w & m.w); }
+__device__ __forceinline__ uint4 andn4(uint4 a, uint4 m) {
+  return make_uint4(a.x & ~m.x, a.y & ~m.y, a.z & ~m.z, a.w & ~m.w);
+}
+__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }
+__device__ __forceinline__ uint4 or4(uint4 a, uint4 b) { return make_uint4(a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w); }
+
+__device__ __forceinline__ uint32_t alb(uint32_t hi, uint32_t lo, uint32_t r) {
+  return __builtin_amdgcn_alignbyte(hi, lo, r);
+}
+// bytes [s, s+16) of lo || hi (s in 1..15, wave-uniform)
+__device__ __forceinline__ uint4 funnel16(uint4 lo, uint4 hi, uint32_t s) {
+  const uint32_t r = s & 3u;
+  switch (s >> 2) {
+    case 0: return make_uint4(alb(lo.y, lo.x, r), alb(lo.z, lo.y, r), alb(lo.w, lo.z, r), alb(hi.x, lo.w, r));
+    case 1: return make_uint4(alb(lo.z, lo.y, r), alb(lo.w, lo.z, r), alb(hi.x, lo.w, r), alb(hi.y, hi.x, r));
+    case 2: return make_uint4(alb(lo.w, lo.z, r), alb(hi.x, lo.w, r), alb(hi.y, hi.x, r), alb(hi.z, hi.y, r));
+    default: return make_uint4(alb(hi.x, lo.w, r), alb(hi.y, hi.x, r), alb(hi.z, hi.y, r), alb(hi.w, hi.z, r));
   }
-  size_t ep_crc_count(size_t e) const { return (e + 1 < nep ? ep_crc_begin[e + 1] : crc_total) - ep_crc_begin[e]; }
+}
+
+__device__ __forceinline__ uint4 load_plain(uint64_t a) {
+  const v4u v = *(gv4p)a;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// The byte mask of [s, e) over this lane's 16 bytes at block offset rel, in row `row` (1 KiB
+// at 1024 row).  s, e and row are wave-uniform: a range that misses or covers the whole row is
+// decided by a scalar branch, and only partial rows pay the per-byte compares.
+__device__ __forceinline__ uint4 row_mask(uint32_t row, uint32_t rel, uint32_t s, uint32_t e) {
+  const uint32_t r0 = 1024u * row, r1 = r0 + 1024u;
+  if (e <= s || e <= r0 || s >= r1) return make_uint4(0, 0, 0, 0);
+  if (s <= r0 && e >= r1) return make_uint4(~0u, ~0u, ~0u, ~0u);
+  return mask16(rel, s, e);
+}
+__device__ __forceinline__ bool row_none(uint32_t row, uint32_t s, uint32_t e) {
+  return e <= s || e <= 1024u * row || s >= 1024u * row + 1024u;
+}
+__device__ __forceinline__ bool row_full(uint32_t row, uint32_t s, uint32_t e) {
+  return s <= 1024u * row && e >= 1024u * row + 1024u;
+}
+
+// Block bytes [rel, rel+16) of the new data (payload address src + rel), only those in
+// [w0, w1); granules with no wanted byte are not dereferenced.
+__device__ __forceinline__ uint4 load_new(uint64_t src, uint32_t row, uint32_t rel, uint32_t w0, uint32_t w1) {
+  if (row_none(row, w0, w1)) return make_uint4(0, 0, 0, 0);
+  const uint32_t s = (uint32_t)(src & 15u);
+  const uint64_t a = src + rel;
+  if (row_full(row, w0, w1) && s == 0) return load_row(a);
+  if (rel + 16 <= w0 || rel >= w1) return make_uint4(0, 0, 0, 0);
+  uint4 v;
+  if (s == 0) {
+    v = load_row(a);
+  } else {
+    const uint64_t a0 = a & ~uint64_t(15);
+    const uint64_t wb = src + (rel > w0 ? rel : w0), we = src + (rel + 16 < w1 ? rel + 16 : w1);
+    const uint4 lo = a0 + 16 > wb ? load_row(a0) : make_uint4(0, 0, 0, 0);
+    const uint4 hi = a0 + 16 < we ? load_row(a0 + 16) : make_uint4(0, 0, 0, 0);
+    v = funnel16(lo, hi, s);
+  }
+  return row_full(row, w0, w1) ? v : and4(v, mask16(rel, w0, w1));
+}
+
+__device__ __forceinline__ void store_masked(uint64_t blk, uint32_t rel, uint4 v, uint32_t k0, uint32_t k1) {
+  if (rel >= k0 && rel + 16 <= k1) {
+    v4u w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (v4u __attribute__((address_space(1))) *)(blk + rel));
+  } else if (rel + 16 > k0 && rel < k1) {  // a word shared with a neighbouring chunk: its own bytes only
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint8_t *p = reinterpret_cast<uint8_t *>(blk + rel);
+    for (uint32_t b = 0; b < 16; ++b)
+      if (rel + b >= k0 && rel + b < k1) p[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+  }
+}
+
+// The block rows this lane holds (4 x 16 B at 1024 r + 16 lane) and, for a fragment with new
+// bytes, the matching payload rows.
+struct BlockRows {
+  uint4 img[4], nw[4];
 };
 
-// Phase 2 of the pass, per thread: its lists into the pinned staging with global job ids
-// and epoch-relative segment indices, and its scan elements' job ids made global.
-void pass_publish(const PassLocal &L, const PassMerge &M, unsigned t, unsigned T, uint32_t clo, uint32_t chi,
-                  const uint32_t *start, const PassShared &S, AffIn *lay, DevChunk *crc, CopyPiece *copy,
-                  VerifyItem *ver) {
-  const uint32_t jb = M.job_base[t];
-  for (size_t e = 0; e < L.nep; ++e) {
-    DevChunk *dst = crc + M.crc_off[e * T + t];
-    const uint32_t sb = M.seg_base[e * T + t];
-    for (const DevChunk &d : L.ep_crc[e].chunks) {
-      *dst = d;
-      dst->out_idx += jb;
-      dst->seg_begin += sb;
-      ++dst;
-    }
-    if (!L.ep_copy[e].empty())
-      std::memcpy(copy + M.copy_off[e * T + t], L.ep_copy[e].data(), L.ep_copy[e].size() * sizeof(CopyPiece));
+__device__ __forceinline__ void load_task_rows(uint64_t blk, uint32_t k0, uint32_t k1, uint64_t src, uint32_t w0,
+                                               uint32_t w1, uint32_t lane, BlockRows &b) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t rel = 1024u * r + 16u * lane;
+    b.img[r] = (rel + 16 > k0 && rel < k1) ? load_plain(blk + rel) : make_uint4(0, 0, 0, 0);
+    b.nw[r] = load_new(src, r, rel, w0, w1);
   }
-  if (!L.verify.empty()) std::memcpy(ver + M.ver_off[t], L.verify.data(), L.verify.size() * sizeof(VerifyItem));
-  if (jb)
-    for (uint32_t c = clo; c < chi; ++c)
-      for (uint32_t p = start[c]; p < S.cur[c]; ++p)
-        if (lay[p].job != kNoJob) lay[p].job += jb;
+}
+
+// One fragment on the block rows: its delta CRC (new ^ old) moved to its op's end goes to
+// eacc[p]; then its zero fill and new bytes are applied.  Returns the rows it wrote.
+__device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 (&nw)[4], uint32_t flags, uint32_t w,
+                                                   uint32_t q, uint32_t z, uint32_t mult, uint32_t p, uint32_t lane,
+                                                   const char *lb, const LaneLut &L, const uint32_t *red, uint32_t poly,
+                                                   uint32_t *__restrict__ eacc) {
+  const uint32_t w0 = w & 0xFFFFu, w1 = w >> 16, q0 = q & 0xFFFFu, q1 = q >> 16, z0 = z & 0xFFFFu, z1 = z >> 16;
+  if (flags & kFragCrc) {
+    Streams st{0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t rel = 1024u * r + 16u * lane;
+      const uint4 old = row_full(r, q0, q1) ? img[r] : and4(img[r], row_mask(r, rel, q0, q1));
+      consume(st, xor4(nw[r], old), lb, L);
+    }
+    const uint32_t v = wave_fold_tab(st, lane, red);
+    if (lane == 0) {
+      const uint32_t cv = dgf_mul_fast(v, mult, poly);
+      if (cv) atomicXor(&eacc[p], cv);
+    }
+  }
+  uint32_t dirty = 0;
+  if (flags & kFragWrite) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t rel = 1024u * r + 16u * lane;
+      if (row_full(r, w0, w1)) {
+        img[r] = nw[r];
+      } else {
+        if (!row_none(r, z0, z1)) img[r] = andn4(img[r], row_mask(r, rel, z0, z1));
+        if (!row_none(r, w0, w1)) img[r] = or4(andn4(img[r], row_mask(r, rel, w0, w1)), nw[r]);
+      }
+      if (!row_none(r, w0, w1) || !row_none(r, z0, z1)) dirty |= 1u << r;
+    }
+  }
+  return dirty;
+}
+
+// One wave per chain (a block's fragments in sequence order): the block is loaded once, each
+// fragment's delta CRC goes to its op's E, the new bytes are applied in order, and the rows
+// that changed are stored once.  Per group of 64 chains lane k loads chain k's first fragment
+// record (one vector load round trip instead of a chain of dependent scalar loads per
+// chain); the wave then walks the group with readlane, keeping the next chain's block and
+// payload rows in flight while the current one is folded and stored.  Chains longer than one
+// fragment (blocks written more than once in the batch) continue with uniform loads.
+__global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__restrict__ frags,
+                                                             const uint32_t *__restrict__ heads,
+                                                             const uint32_t *__restrict__ d_ntasks,
+                                                             const PolyConsts *__restrict__ pc,
+                                                             uint32_t *__restrict__ eacc) {
+  __shared__ uint32_t lds[kLdsWords + kRedWords];
+  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
+  const uint32_t *red_g = &pc->red[0][0][0];
+  for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  __syncthreads();
+  const uint32_t ntasks = *d_ntasks;
+  const uint32_t *red = lds + kLdsWords;
+  const char *lb = reinterpret_cast<const char *>(lds);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t lo = (uint32_t)(gw * ntasks / nw), hi = (uint32_t)((gw + 1) * ntasks / nw);
+  if (lo >= hi) return;
+  const uint32_t poly = pc->poly;
+  const LaneLut L = make_lut(lane);
+  auto rl = [](uint32_t v, uint32_t t) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane(v, t); };
+  auto rl64 = [](uint64_t v, uint32_t t) -> uint64_t {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32);
+  };
+  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
+    const uint32_t cnt = min(64u, hi - g0);
+    // lane k: chain g0 + k's first fragment
+    uint64_t m_blk = 0, m_src = 0;
+    uint32_t m_p = 0, m_next = kNil, m_w = 0, m_q = 0, m_z = 0, m_k = 0, m_mult = 0, m_flags = 0;
+    if (lane < cnt) {
+      const FragDesc &d = frags[heads[g0 + lane]];
+      m_blk = d.blk;
+      m_src = d.src;
+      m_p = d.p;
+      m_next = d.next;
+      m_w = (uint32_t)d.w0 | ((uint32_t)d.w1 << 16);
+      m_q = (uint32_t)d.q0 | ((uint32_t)d.q1 << 16);
+      m_z = (uint32_t)d.z0 | ((uint32_t)d.z1 << 16);
+      m_k = (uint32_t)d.k0 | ((uint32_t)d.k1 << 16);
+      m_mult = d.mult;
+      m_flags = d.flags;
+    }
+    BlockRows cur, nxt;
+    {
+      const uint32_t k = rl(m_k, 0), w = rl(m_w, 0);
+      load_task_rows(rl64(m_blk, 0), k & 0xFFFFu, k >> 16, rl64(m_src, 0), w & 0xFFFFu, w >> 16, lane, cur);
+    }
+    for (uint32_t t = 0; t < cnt; ++t) {
+      if (t + 1 < cnt) {  // the next chain's rows in flight while this one is processed
+        const uint32_t k = rl(m_k, t + 1), w = rl(m_w, t + 1);
+        load_task_rows(rl64(m_blk, t + 1), k & 0xFFFFu, k >> 16, rl64(m_src, t + 1), w & 0xFFFFu, w >> 16, lane, nxt);
+      }
+      const uint64_t blk = rl64(m_blk, t);
+      const uint32_t kk = rl(m_k, t), k0 = kk & 0xFFFFu, k1 = kk >> 16;
+      uint32_t dirty = apply_fragment(cur.img, cur.nw, rl(m_flags, t), rl(m_w, t), rl(m_q, t), rl(m_z, t),
+                                      rl(m_mult, t), rl(m_p, t), lane, lb, L, red, poly, eacc);
+      for (uint32_t f = rl(m_next, t); f != kNil;) {  // later fragments of the same block
+        const FragDesc d = frags[f];
+        uint4 nw4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) nw4[r] = load_new(d.src, r, 1024u * r + 16u * lane, d.w0, d.w1);
+        dirty |= apply_fragment(cur.img, nw4, d.flags, (uint32_t)d.w0 | ((uint32_t)d.w1 << 16),
+                                (uint32_t)d.q0 | ((uint32_t)d.q1 << 16), (uint32_t)d.z0 | ((uint32_t)d.z1 << 16),
+                                d.mult, d.p, lane, lb, L, red, poly, eacc);
+        f = d.next;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (dirty & (1u << r)) store_masked(blk, 1024u * r + 16u * lane, cur.img[r], k0, k1);
+      cur = nxt;
+    }
+  }
+}
+
+__device__ __forceinline__ Aff t_map(const OpPos &r, const uint32_t *__restrict__ eacc, const uint32_t *__restrict__ payraw,
+                                     uint32_t p, const PolyConsts *__restrict__ pc) {
+  if (r.tk == kT_DELTA) return Aff{dxpow8_fast((int64_t)r.na - (int64_t)r.nb, pc, pc->poly), eacc[p]};
+  if (r.tk == kT_FULL) return Aff{0u, payraw[r.op]};
+  return Aff{kOne, 0u};
+}
+
+// The scans' inputs, computed as rocPRIM reads them (no element arrays).
+struct TMapFn {
+  const OpPos *pos;
+  const uint32_t *eacc, *payraw;
+  const PolyConsts *pc;
+  __device__ Aff operator()(uint32_t p) const { return t_map(pos[p], eacc, payraw, p, pc); }
+};
+
+// s maps per op position, from each op's t after it (the chunk's t0 through the t scan).
+struct SMapFn {
+  const OpPos *pos;
+  const uint32_t *skey;
+  uint32_t nchunks;
+  const Aff *tscan;
+  const uint32_t *t0v, *eacc, *payraw;
+  const PolyConsts *pc;
+  __device__ Aff operator()(uint32_t p) const {
+    const OpPos r = pos[p];
+    const uint32_t c = skey[p];
+    if (c >= nchunks) return Aff{kOne, 0u};
+    switch (r.sk) {
+      case kS_ZERO:
+        return Aff{0u, 0u};
+      case kS_SET_T: {
+        const Aff t = tscan[p];
+        return Aff{0u, hd_gf_mul(t0v[c], t.m, pc->poly) ^ t.e};
+      }
+      case kS_APPEND:
+        return t_map(r, eacc, payraw, p, pc);
+      default:
+        return Aff{kOne, 0u};
+    }
+  }
+};
+
+// Per op result (IOResult.checksum, ChunkReplica.cc:174,311; ChunkEngine.cc:61-67), each chunk's
+// final state (its last op), and the counters.
+__global__ void uio_result_kernel(const OpPos *__restrict__ pos, const uint32_t *__restrict__ skey, uint32_t n,
+                                  const Aff *__restrict__ sscan, const h3c_chunk_state *__restrict__ chunks,
+                                  h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks,
+                                  const uint32_t *__restrict__ t0v, uint8_t poly_type, uint32_t std_domain,
+                                  uint32_t poly, h3c_update_result *__restrict__ res,
+                                  unsigned long long *__restrict__ ctr) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t c_none = 0, c_reuse = 0, c_comb = 0, c_read = 0, c_recalc = 0, c_mis = 0, c_inv = 0;
+  if (p < n) {
+    const OpPos r = pos[p];
+    const uint32_t c = skey[p];
+    h3c_update_result o{};
+    o.status = r.status;
+    const bool applied = r.status == H3C_OK && r.sk != kS_IDENT;
+    if (r.status == H3C_ERR_INVALID_ARG) c_inv = 1;
+    if (r.status == H3C_ERR_CHECKSUM_MISMATCH) c_mis = 1;
+    if (applied) {
+      c_none = r.ccode == kC_NONE;
+      c_reuse = r.ccode == kC_REUSE;
+      c_read = r.ccode == kC_READ;
+      c_recalc = r.ccode == kC_RECALC;
+      c_comb = r.ccode == kC_COMBINE ? (std_domain ? r.ncomb : 1u) : 0u;
+    }
+    if (c < nchunks) {
+      const h3c_chunk_state cs = chunks[c];
+      const uint32_t t0 = t0v[c];
+      uint32_t s0 = std_domain ? ~cs.value : cs.value;
+      if (std_domain && cs.type != poly_type) s0 = t0;  // the engine's checksum is always crc32c of the bytes
+      const Aff x = sscan[p];
+      const uint32_t s = hd_gf_mul(s0, x.m, poly) ^ x.e;
+      o.size = applied ? r.na : r.nb;
+      if (r.status == H3C_ERR_CHECKSUM_MISMATCH) {
+        o.type = std_domain ? poly_type : r.tb;
+        o.value = std_domain ? 0u : s;  // engine.rs:303 returns before out_checksum is set
+      } else if (applied) {
+        o.type = r.ta;
+        o.value = std_domain ? ~s : s;
+      }
+      if (p + 1 == n || skey[p + 1] != c) {
+        h3c_chunk_state fin = cs;
+        fin.size = o.size;
+        fin.type = r.ta;
+        fin.value = std_domain ? ~s : s;
+        chunks_out[c] = fin;
+      }
+    }
+    res[r.op] = o;
+  }
+  __shared__ unsigned int sh[8];
+  const uint32_t v[8] = {c_none, c_reuse, c_comb, c_read, c_recalc, c_mis, c_inv, 0u};
+  ctr_add_block(sh, ctr, v);
+}
+
+// H3C_UPD_EXACT: chunks whose stored checksum of the batch polynomial disagrees with the bytes.
+__global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks,
+                                 const uint32_t *__restrict__ t0v, uint8_t poly_type, uint32_t std_domain,
+                                 unsigned long long *__restrict__ ctr) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t stale = 0;
+  if (c < nchunks) {
+    const h3c_chunk_state cs = chunks[c];
+    if (cs.size && cs.type == poly_type) stale = t0v[c] != (std_domain ? ~cs.value : cs.value);
+  }
+  __shared__ unsigned int sh[8];
+  const uint32_t v[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, stale};
+  ctr_add_block(sh, ctr, v);
+}
+
+template <class T>
+T *carve(char *&p, size_t count) {
+  T *r = reinterpret_cast<T *>(p);
+  p += (count * sizeof(T) + 255) & ~size_t(255);
+  return r;
+}
+
+uint32_t bits_for(uint64_t v) {  // bits to represent values < v
+  uint32_t b = 0;
+  while (b < 64 && (1ull << b) < v) ++b;
+  return b;
+}
+
+using SortMerge = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                             rocprim::default_config, 1024 * 1024>;
+using SortSweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                             rocprim::default_config, 0>;
+
+// rocPRIM sort of (chunk, op): one onesweep pass for keys of <= 8 bits, the merge-sort path
+// otherwise (faster below 1M items for wider keys, profiles/r02_prim_probe.txt).
+hipError_t sort_pairs(void *tmp, size_t &tmp_bytes, const uint32_t *k, uint32_t *k2, const uint32_t *v, uint32_t *v2,
+                      uint32_t n, uint32_t bits, hipStream_t st) {
+  if (bits <= 8)
+    return rocprim::radix_sort_pairs<SortSweep>(tmp, tmp_bytes, k, k2, v, v2, n, 0, std::max(bits, 1u), st);
+  return rocprim::radix_sort_pairs<SortMerge>(tmp, tmp_bytes, k, k2, v, v2, n, 0, bits, st);
 }
 
 }  // namespace
 
-extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
-                              uint32_t n, h3c_update_result *results, uint32_t flags, void *stream) {
+extern "C" int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
+                                 uint32_t n, h3c_update_result *results, uint32_t flags, h3c_update_counters *counters,
+                                 void *stream) {
+  if (counters) std::memset(counters, 0, sizeof(*counters));
   if (poly_type != H3C_TYPE_CRC32C && poly_type != H3C_TYPE_CRC32) return H3C_ERR_INVALID_ARG;
-  if ((n && (!ios || !results)) || (nchunks && !chunks) || n >= 0x7FFFFFFFu) return H3C_ERR_INVALID_ARG;
+  if ((n && (!ios || !results)) || (nchunks && !chunks) || n >= 0x7FFFFFFFu || nchunks >= (1u << 28))
+    return H3C_ERR_INVALID_ARG;
   for (uint32_t c = 0; c < nchunks; ++c)  // a chunk longer than its capacity is a caller bug
     if (chunks[c].size > chunks[c].chunk_size) {
       h3c_rt::set_error_text("h3c_update_ios: a chunk's size exceeds its chunk_size");
@@ -798,395 +948,288 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
     }
   if (n == 0) return H3C_OK;
   const bool std_domain = (flags & H3C_UPD_STD_DOMAIN) != 0;
+  const bool exact = (flags & H3C_UPD_EXACT) != 0;
   int dev = 0;
   int rc = h3c_rt::current_device(&dev);
   if (rc) return rc;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const PolyConsts *pc = static_cast<const PolyConsts *>(h3c_rt::device_consts(dev, poly_type));
   const uint32_t poly = poly_type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
+  const uint32_t stdf = std_domain ? 1u : 0u;
 
-  PhaseClock clk;
-  thread_local UpdioScratch tls_ws;
-  UpdioScratch &ws = tls_ws;  // a local name: lambdas run on pool threads must not name the thread_local
-  const unsigned T = std::max(1u, std::min<unsigned>(pass_threads(n), nchunks));
-  // ---- per-op validation (range :140-145, kind, client checksum type), by op range ----
-  std::vector<uint32_t> &status = ws.status;
-  status.resize(n);
-  std::vector<uint64_t> part_bytes(T, 0);
-  run_threads(T, [&](unsigned t) {
-    const uint32_t i0 = (uint32_t)((uint64_t)n * t / T), i1 = (uint32_t)((uint64_t)n * (t + 1) / T);
-    uint64_t pb = 0;
-    for (uint32_t i = i0; i < i1; ++i) {
-      const h3c_update_io &io = ios[i];
-      status[i] = H3C_OK;
-      const bool kind_ok = io.kind == H3C_UPD_WRITE || io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND;
-      if (io.chunk >= nchunks || !kind_ok) {
-        status[i] = H3C_ERR_INVALID_ARG;
-        continue;
-      }
-      const h3c_chunk_state &c = chunks[io.chunk];
-      if (io.offset >= c.chunk_size || (uint64_t)io.offset + io.length > c.chunk_size || !c.base ||
-          (io.checksum_type != H3C_TYPE_NONE && io.checksum_type != poly_type) ||
-          (io.kind == H3C_UPD_WRITE && io.length && !io.payload)) {
-        status[i] = H3C_ERR_INVALID_ARG;
-        continue;
-      }
-      if (io.kind == H3C_UPD_WRITE) pb += io.length;
+  // ---- per-chunk host work (O(chunks)): trusted starting CRCs, the chunks to CRC first ----
+  const uint32_t C = std::max(nchunks, 1u);
+  size_t ninit = 0;
+  bool other_poly = false;
+  uint64_t init_bytes = 0;
+  for (uint32_t c = 0; c < nchunks; ++c) {
+    const h3c_chunk_state &cs = chunks[c];
+    if (cs.type != H3C_TYPE_NONE && cs.type != poly_type) other_poly = true;
+    if (cs.size && (exact || cs.type != poly_type)) {
+      ++ninit;
+      init_bytes += cs.size;
     }
-    part_bytes[t] = pb;
-  });
-  uint64_t pay_bytes = 0;
-  for (unsigned t = 0; t < T; ++t) pay_bytes += part_bytes[t];
-  // A. payload CRC jobs (raw, init ~0) of every valid WRITE, built per op range: run on the
-  // device in the same stream as the update itself; the old-range CRC jobs of B use the
-  // same segment size.  `pay` holds the totals; the parts are published into staging.
-  const uint64_t seg = h3c_rt::pick_seg(pay_bytes, dev);
-  if (ws.pay_parts.size() < T) ws.pay_parts.resize(T);
-  run_threads(T, [&](unsigned t) {
-    CrcBatch &b = ws.pay_parts[t];
-    b.chunks.clear();
-    b.total_segs = b.max_segs = 0;
-    b.bytes = b.max_len = 0;
-    FoldCache fc;
-    const uint32_t i0 = (uint32_t)((uint64_t)n * t / T), i1 = (uint32_t)((uint64_t)n * (t + 1) / T);
-    for (uint32_t i = i0; i < i1; ++i)
-      if (status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
-        add_job(b, fc, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg, poly);
-  });
-  CrcBatch &pay = ws.pay;  // totals only (its chunk list stays empty)
-  pay.chunks.clear();
-  pay.total_segs = pay.max_segs = 0;
-  pay.bytes = pay.max_len = 0;
-  std::vector<size_t> pay_off(T + 1, 0);
-  std::vector<uint32_t> pay_seg_base(T, 0);
-  for (unsigned t = 0; t < T; ++t) {
-    const CrcBatch &b = ws.pay_parts[t];
-    pay_off[t + 1] = pay_off[t] + b.chunks.size();
-    pay_seg_base[t] = pay.total_segs;
-    pay.total_segs += b.total_segs;
-    pay.max_segs = std::max(pay.max_segs, b.max_segs);
-    pay.bytes += b.bytes;
-    pay.max_len = std::max(pay.max_len, b.max_len);
   }
-  // The speculative attempt's payload CRCs need nothing from the host pass: they are
-  // uploaded and launched now, so the device works through them while B runs on the host.
-  const size_t npay = pay_off[T];
-  h3c_rt::DeviceLease pay_dev(dev, (npay * sizeof(DevChunk) + 4ull * std::max(pay.total_segs, 1u) + 4ull * n) +
-                                       3 * 256);
-  h3c_rt::PinnedLease pay_pin(npay * sizeof(DevChunk) + 256);
-  if (!pay_dev.ok() || !pay_pin.ok()) return H3C_ERR_HIP;
-  StreamDrain drain{st};  // declared after the leases: every return below waits for the stream first
-  Arena pa;
-  pa.base = pay_dev.data();
-  DevChunk *d_pay = pa.take<DevChunk>(npay);
-  uint32_t *d_payseg = pa.take<uint32_t>(std::max(pay.total_segs, 1u));
-  uint32_t *d_payraw_spec = pa.take<uint32_t>(n);
-  if (npay)
-    run_threads(T, [&](unsigned t) {
-      DevChunk *dst = reinterpret_cast<DevChunk *>(pay_pin.data()) + pay_off[t];
-      for (const DevChunk &d : ws.pay_parts[t].chunks) {
-        *dst = d;
-        dst->seg_begin += pay_seg_base[t];
-        ++dst;
-      }
-    });
-  drain.armed = true;
-  HIP_TRY(hipMemsetAsync(d_payraw_spec, 0xFF, 4ull * n, st));
-  if (npay) {
-    HIP_TRY(hipMemcpyAsync(d_pay, pay_pin.data(), npay * sizeof(DevChunk), hipMemcpyHostToDevice, st));
-    const int r = h3c_rt::launch_crc(st, dev, poly_type, d_pay, (uint32_t)npay, pay.total_segs, pay.max_segs, pay.bytes,
-                                     seg, 0, d_payseg, nullptr, d_payraw_spec, nullptr, nullptr, -1,
-                                     h3c_rt::small_rows_bound(pay.max_len, pay.max_segs));
-    if (r) return r;
-  }
-  clk.mark("A prepare");
+  const bool fused = std_domain || !other_poly;  // else: one extra pass for the other-polynomial limit
+  const uint64_t init_seg = h3c_rt::pick_seg(init_bytes, dev);
 
-  // B + C-D, speculatively first: the host pass assumes every client checksum matches and
-  // the device checks them before any byte is written (the copy kernels are gated on the
-  // check).  A mismatch (rare: a corrupted transfer) costs a second attempt with the
-  // payload CRCs known.  One host <-> device round trip per batch in the common case.
-  PassShared &S = ws.S;
-  // the pass runs as NT chunk-range tasks (4 per thread) pulled by the T threads
-  const unsigned NT = std::max(1u, std::min<unsigned>(T == 1 ? 1u : 4u * T, nchunks));
-  if (ws.L.size() < NT) ws.L.resize(NT);
-  std::vector<uint32_t> &payraw = ws.payraw;  // known payload CRCs (second attempt only)
-  std::vector<uint32_t> &truev = ws.truev;
-  // scan elements and keys are written by the pass straight into pinned staging
-  layout_ops(poly_type, chunks, nchunks, ios, n, status, T, ws.start, ws.opstart, ws.order, ws.hist);
-  const uint32_t npos = ws.start[nchunks];
-  const size_t lay_bytes = ((size_t)npos * sizeof(AffIn) + 255) & ~size_t(255);
-  h3c_rt::PinnedLease pin_el(lay_bytes + 4ull * npos + 256);
-  if (!pin_el.ok()) return H3C_ERR_HIP;
-  AffIn *lay = reinterpret_cast<AffIn *>(pin_el.data());
-  uint32_t *keys = reinterpret_cast<uint32_t *>(pin_el.data() + lay_bytes);
-  truev.resize(npos);  // every entry is filled from the device before it is read
-  S.tr.resize(nchunks);
-  S.cur.resize(nchunks);
-  S.raw0.resize(nchunks);
-  S.outs.resize(ws.order.size());  // written by the pass for every op it accepts, read only for those
-  cut_chunks(ws.opstart, nchunks, NT, ws.cut);
-  clk.mark("B layout");
-  PassMerge M;
+  // ---- device scratch: per op, per chunk, and per fragment for a guessed fragment count ----
+  // (a fragment per 4 KiB block an op touches: one per block-aligned write of <= 4 KiB; the
+  // guess is the larger of 2n and the calling thread's last batch, and a batch that needs more
+  // redoes its fragment stage once with the count known)
+  thread_local uint32_t last_frags = 0;
+  uint32_t cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * n + 1024, last_frags), 0x7FFFFFF0u);
+  size_t sort_tmp = 0, scan_tmp = 0, szscan_tmp = 0, ascan_tmp = 0;
+  const uint32_t bits = bits_for((uint64_t)nchunks + 1);
+  using CountIt = rocprim::counting_iterator<uint32_t>;
+  using TIt = rocprim::transform_iterator<CountIt, TMapFn, Aff>;
+  using SIt = rocprim::transform_iterator<CountIt, SMapFn, Aff>;
+  HIP_TRY(sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, n, bits, st));
+  HIP_TRY(rocprim::exclusive_scan(nullptr, scan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)n + 1,
+                                  rocprim::plus<uint32_t>(), st));
+  HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, szscan_tmp, (uint32_t *)nullptr, (SzTy *)nullptr, (SzTy *)nullptr,
+                                         (size_t)n, SzTyOp(), rocprim::equal_to<uint32_t>(), st));
+  {
+    size_t a = 0, b = 0;
+    HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, a, (uint32_t *)nullptr, TIt(CountIt(0), TMapFn{}), (Aff *)nullptr,
+                                           (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
+    HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, b, (uint32_t *)nullptr, SIt(CountIt(0), SMapFn{}), (Aff *)nullptr,
+                                           (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
+    ascan_tmp = std::max(a, b);
+  }
+  const size_t tmp_bytes = std::max(std::max(sort_tmp, scan_tmp), std::max(szscan_tmp, ascan_tmp));
+  const size_t N1 = (size_t)n + 1;
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  // upload block [chunks | t0 | INIT descriptors] and download block [final chunks | counters | misc]
+  const size_t up_t0 = al(sizeof(h3c_chunk_state) * C), up_init = up_t0 + al(4ull * C);
+  const size_t up_bytes = up_init + al(sizeof(DevChunk) * std::max<size_t>(ninit, 1));
+  const size_t dn_ctr = al(sizeof(h3c_chunk_state) * C), dn_misc = dn_ctr + al(8ull * kCtrN);
+  const size_t dn_bytes = dn_misc + al(4ull * kMiscN) + 256;
+  h3c_update_io *d_ios;
+  uint32_t *d_status, *d_key, *d_idx, *d_skey, *d_order, *d_np, *d_pbase, *d_paycrc0, *d_payraw, *d_nfrag, *d_fbase,
+      *d_eacc, *d_initseg;
+  SzTy *d_sz, *d_szscan;
+  OpPos *d_pos;
+  Aff *d_tscan, *d_sscan;
+  h3c_update_result *d_res;
+  char *d_up, *d_dn;
+  void *d_tmp;
+  // one layout, run twice: with base 0 to size the lease, then on the lease
+  auto layout = [&](char *base) -> size_t {
+    char *c0 = base, *cur = base;
+    d_up = carve<char>(cur, up_bytes);
+    d_dn = carve<char>(cur, dn_bytes);
+    d_ios = carve<h3c_update_io>(cur, n);
+    d_status = carve<uint32_t>(cur, n);
+    d_key = carve<uint32_t>(cur, n);
+    d_idx = carve<uint32_t>(cur, n);
+    d_skey = carve<uint32_t>(cur, n);
+    d_order = carve<uint32_t>(cur, n);
+    d_np = carve<uint32_t>(cur, N1);
+    d_pbase = carve<uint32_t>(cur, N1);
+    d_paycrc0 = carve<uint32_t>(cur, n);
+    d_payraw = carve<uint32_t>(cur, n);
+    d_nfrag = carve<uint32_t>(cur, N1);
+    d_fbase = carve<uint32_t>(cur, N1);
+    d_eacc = carve<uint32_t>(cur, n);
+    d_sz = carve<SzTy>(cur, n);
+    d_szscan = carve<SzTy>(cur, n);
+    d_pos = carve<OpPos>(cur, n);
+    d_tscan = carve<Aff>(cur, n);
+    d_sscan = carve<Aff>(cur, n);
+    d_res = carve<h3c_update_result>(cur, n);
+    d_tmp = carve<char>(cur, tmp_bytes);
+    d_initseg = carve<uint32_t>(cur, init_bytes / init_seg + ninit + 1);
+    return (size_t)(cur - c0);
+  };
+  const size_t bytes1 = layout(nullptr);
+  h3c_rt::DeviceLease lease1(dev, bytes1);
+  if (!lease1.ok()) return H3C_ERR_HIP;
+  h3c_rt::PinnedLease pin(up_bytes + dn_bytes);
+  if (!pin.ok()) return H3C_ERR_HIP;
+  layout(lease1.data());
+  h3c_chunk_state *d_chunks = reinterpret_cast<h3c_chunk_state *>(d_up);
+  uint32_t *d_t0 = reinterpret_cast<uint32_t *>(d_up + up_t0);
+  DevChunk *d_init = reinterpret_cast<DevChunk *>(d_up + up_init);
+  h3c_chunk_state *d_chunks_out = reinterpret_cast<h3c_chunk_state *>(d_dn);
+  unsigned long long *d_ctr = reinterpret_cast<unsigned long long *>(d_dn + dn_ctr);
+  uint32_t *d_misc = reinterpret_cast<uint32_t *>(d_dn + dn_misc);
+
+  // host staging of the upload block: the chunk table, trusted starting CRCs, INIT descriptors
+  char *hp = pin.data();
+  std::memcpy(hp, chunks, sizeof(h3c_chunk_state) * nchunks);
+  uint32_t *h_t0 = reinterpret_cast<uint32_t *>(hp + up_t0);
+  DevChunk *h_init = reinterpret_cast<DevChunk *>(hp + up_init);
+  uint32_t init_segs = 0, init_max = 0;
+  uint64_t init_maxlen = 0;
+  size_t k_init = 0;
+  for (uint32_t c = 0; c < nchunks; ++c) {
+    const h3c_chunk_state &cs = chunks[c];
+    if (cs.size == 0) {
+      h_t0[c] = 0xFFFFFFFFu;  // raw CRC of no bytes
+    } else if (!exact && cs.type == poly_type) {
+      h_t0[c] = std_domain ? ~cs.value : cs.value;  // trusted
+    } else {  // from the bytes (launch_crc below writes t0[c])
+      h_t0[c] = 0;
+      DevChunk d{};
+      d.ptr = cs.base;
+      d.len = cs.size;
+      d.start = 0xFFFFFFFFu;
+      d.out_idx = c;
+      d.seg_begin = init_segs;
+      set_fold_consts(d, init_seg, poly);
+      const uint32_t ns = (uint32_t)((d.len + init_seg - 1) / init_seg);
+      init_segs += ns;
+      init_max = std::max(init_max, ns);
+      init_maxlen = std::max<uint64_t>(init_maxlen, d.len);
+      h_init[k_init++] = d;
+    }
+  }
+  char *hd = hp + up_bytes;  // download staging
+
+  StreamDrain drain{st, true};  // every return below waits for the stream before the leases go back
+  const uint32_t tb = 256, gb = (uint32_t)((n + tb) / tb);  // n + 1 threads (the scans' extra entry)
+  auto scan_excl = [&](const uint32_t *in, uint32_t *out) -> hipError_t {
+    size_t t = tmp_bytes;
+    return rocprim::exclusive_scan(d_tmp, t, in, out, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), st);
+  };
+  HIP_TRY(hipMemcpyAsync(d_up, hp, up_init + (ninit ? al(sizeof(DevChunk) * ninit) : 0), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(d_ios, ios, sizeof(h3c_update_io) * n, hipMemcpyHostToDevice, st));
+  // the chunks whose starting CRC comes from their bytes, before any byte changes
+  if (ninit) {
+    rc = h3c_rt::launch_crc(st, dev, poly_type, d_init, (uint32_t)ninit, init_segs, init_max, init_bytes, init_seg, 0,
+                            d_initseg, nullptr, d_t0, nullptr, nullptr, -1,
+                            h3c_rt::small_rows_bound(init_maxlen, init_max));
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(uio_prep_kernel, dim3(gb), dim3(tb), 0, st, d_ios, n, d_chunks, nchunks, poly_type, stdf,
+                     d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(scan_excl(d_np, d_pbase));
+  rc = h3c_rt::launch_op_piece_crc(st, dev, poly_type, d_ios, d_pbase, n, d_pbase + n, d_paycrc0,
+                                   d_misc + kMiscPieceWork);
+  if (rc) return rc;
+  {
+    size_t t = tmp_bytes;
+    HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, st));
+  }
+  for (int pass = fused ? 1 : 0; pass < 2; ++pass) {  // pass 0: the other-polynomial rejections only
+    hipLaunchKernelGGL(uio_sz_elem_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, n, d_status, d_paycrc0, pc,
+                       poly_type, stdf, d_payraw, d_sz);
+    HIP_TRY(hipGetLastError());
+    size_t t = tmp_bytes;
+    HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_sz, d_szscan, (size_t)n, SzTyOp(),
+                                           rocprim::equal_to<uint32_t>(), st));
+    hipLaunchKernelGGL(uio_classify_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, d_skey, n, d_chunks, nchunks,
+                       d_szscan, d_status, poly_type, stdf, pass == 0 ? 1u : 0u, d_pos, d_nfrag);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(scan_excl(d_nfrag, d_fbase));
+
+  // ---- fragments, blocks, scans, results (redone once if the fragment guess was short) ----
   for (int attempt = 0;; ++attempt) {
-    const bool spec = attempt == 0;
-    run_tasks(T, NT, [&](unsigned k) {
-      host_pass(poly_type, poly, std_domain, chunks, ios, status.data(), spec ? nullptr : payraw.data(), seg,
-                ws.start.data(), ws.opstart.data(), ws.order.data(), lay, keys, ws.cut[k], ws.cut[k + 1], S,
-                ws.L[k]);
-    });
-    M.build(ws.L, NT);
-    clk.mark("B pass");
-    // ---- C-D. device: payload CRCs + check (speculative), epochs, affine scan ----
-    const uint32_t nver = (uint32_t)M.ver_total;
-    size_t scan_tmp = 0;
-    if (npos)
-      HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, scan_tmp, (uint32_t *)nullptr, (Aff *)nullptr, (Aff *)nullptr,
-                                             (size_t)npos, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
-    const size_t crc_chunks = M.crc_total, copy_pieces = M.copy_total;
-    const uint32_t max_segs = M.max_segs;
-    Arena a;
-    const size_t bytes = crc_chunks * sizeof(DevChunk) + copy_pieces * sizeof(CopyPiece) +
-                         nver * sizeof(VerifyItem) + 4ull * max_segs + 4ull * std::max(M.njobs, 1u) + 4ull * n +
-                         npos * (sizeof(AffIn) + 2 * sizeof(Aff) + 8) + 4ull * nchunks + 4ull * nver + scan_tmp +
-                         16 * 256;
-    h3c_rt::DeviceLease scratch(dev, bytes);
-    if (!scratch.ok()) return H3C_ERR_HIP;
-    a.base = scratch.data();
-    DevChunk *d_crc = a.take<DevChunk>(crc_chunks);
-    CopyPiece *d_copy = a.take<CopyPiece>(copy_pieces);
-    VerifyItem *d_ver = a.take<VerifyItem>(nver);
-    uint32_t *d_seg = a.take<uint32_t>(max_segs);
-    uint32_t *d_jobcrc = a.take<uint32_t>(std::max(M.njobs, 1u));
-    uint32_t *d_payraw = spec ? d_payraw_spec : a.take<uint32_t>(n);
-    AffIn *d_in = a.take<AffIn>(npos);
-    Aff *d_aff = a.take<Aff>(npos);
-    Aff *d_scan = a.take<Aff>(npos);
-    uint32_t *d_keys = a.take<uint32_t>(npos);
-    uint32_t *d_true = a.take<uint32_t>(npos);
-    uint32_t *d_raw0 = a.take<uint32_t>(nchunks);
-    uint32_t *d_bad = a.take<uint32_t>(1 + nver);  // [0]: any mismatch (gates the copies); [1+k]: item k
-    void *d_tmp = a.take<char>(scan_tmp);
-
-    // pinned staging: uploads [crc jobs | copies | verify | payraw | raw0] (the scan
-    // elements and keys are already in pin_el), downloads [true values | mismatch flags |
-    // payload CRCs]
-    enum { kCrc, kCopy, kVer, kPayraw, kRaw0, kUp, kTrue = kUp, kBad, kPayBack, kAll };
-    size_t len[kAll] = {crc_chunks * sizeof(DevChunk), copy_pieces * sizeof(CopyPiece),
-                        nver * sizeof(VerifyItem), spec ? 0 : 4ull * n, 4ull * nchunks, 4ull * npos,
-                        spec ? 4ull * (1 + nver) : 0, spec ? 4ull * n : 0};
-    void *dst[kUp] = {d_crc, d_copy, d_ver, d_payraw, d_raw0};
-    size_t off[kAll + 1];
-    off[0] = 0;
-    for (int k = 0; k < kAll; ++k) off[k + 1] = off[k] + ((len[k] + 255) & ~size_t(255));
-    h3c_rt::PinnedLease pin(off[kAll]);
-    if (!pin.ok()) return H3C_ERR_HIP;
-    char *hp = pin.data();
-    run_tasks(T, NT, [&](unsigned k) {
-      pass_publish(ws.L[k], M, k, NT, ws.cut[k], ws.cut[k + 1], ws.start.data(), S, lay,
-                   reinterpret_cast<DevChunk *>(hp + off[kCrc]),
-                   reinterpret_cast<CopyPiece *>(hp + off[kCopy]), reinterpret_cast<VerifyItem *>(hp + off[kVer]));
-    });
-    if (!spec) std::memcpy(hp + off[kPayraw], payraw.data(), len[kPayraw]);
-    std::memcpy(hp + off[kRaw0], S.raw0.data(), len[kRaw0]);
-    const VerifyItem *ver_host = reinterpret_cast<const VerifyItem *>(hp + off[kVer]);
-
-    int err = H3C_OK;
-    auto body = [&]() -> int {
-      for (int k = 0; k < kUp; ++k)
-        if (len[k]) HIP_TRY(hipMemcpyAsync(dst[k], hp + off[k], len[k], hipMemcpyHostToDevice, st));
-      if (npos) {
-        HIP_TRY(hipMemcpyAsync(d_in, lay, npos * sizeof(AffIn), hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(d_keys, keys, 4ull * npos, hipMemcpyHostToDevice, st));
-      }
-      if (spec) {  // the payload CRCs were launched before the host pass
-        HIP_TRY(hipMemsetAsync(d_bad, 0, 4ull * (1 + nver), st));
-        if (nver) {
-          hipLaunchKernelGGL(updio_verify_kernel, dim3((nver + 255) / 256), dim3(256), 0, st, d_ver, nver, d_payraw,
-                             std_domain ? 1u : 0u, d_bad);
-          HIP_TRY(hipGetLastError());
-        }
-      }
-      const uint32_t *gate = spec ? d_bad : nullptr;
-      for (size_t e = 0; e < M.nep; ++e) {
-        const size_t nc = M.ep_crc_count(e);
-        if (nc) {
-          const CrcBatch &b = M.ep[e];
-          const int r = h3c_rt::launch_crc(st, dev, poly_type, d_crc + M.ep_crc_begin[e], (uint32_t)nc, b.total_segs,
-                                           b.max_segs, b.bytes, seg, 0, d_seg, nullptr, d_jobcrc, nullptr, nullptr,
-                                           -1, h3c_rt::small_rows_bound(b.max_len, b.max_segs));
-          if (r) return r;
-        }
-        if (M.ep_copy_count[e]) {
-          hipLaunchKernelGGL(updio_copy_kernel, dim3((uint32_t)M.ep_copy_count[e]), dim3(256), 0, st,
-                             d_copy + M.ep_copy_begin[e], gate);
-          HIP_TRY(hipGetLastError());
-        }
-      }
-      if (npos) {
-        const uint32_t tb = 256, gb = (npos + tb - 1) / tb;
-        hipLaunchKernelGGL(updio_aff_kernel, dim3(gb), dim3(tb), 0, st, d_in, npos, d_payraw, d_jobcrc, pc, d_aff);
-        HIP_TRY(hipGetLastError());
-        size_t tmp = scan_tmp;
-        HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, tmp, d_keys, d_aff, d_scan, (size_t)npos, AffOp{poly},
-                                               rocprim::equal_to<uint32_t>(), st));
-        hipLaunchKernelGGL(updio_true_kernel, dim3(gb), dim3(tb), 0, st, d_scan, d_keys, npos, d_raw0, poly, d_true);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(hp + off[kTrue], d_true, len[kTrue], hipMemcpyDeviceToHost, st));
-      }
-      if (spec) {
-        HIP_TRY(hipMemcpyAsync(hp + off[kBad], d_bad, len[kBad], hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(hp + off[kPayBack], d_payraw, len[kPayBack], hipMemcpyDeviceToHost, st));
-      }
-      return H3C_OK;
+    uint32_t hcap = 256;
+    while (hcap < cap) hcap <<= 1;
+    FragDesc *d_frag;
+    uint64_t *d_fkey;
+    uint32_t *d_prev, *d_gnext, *d_heads, *d_hhead;
+    auto layout2 = [&](char *base) -> size_t {
+      char *c2 = base;
+      d_frag = carve<FragDesc>(c2, cap);
+      d_fkey = carve<uint64_t>(c2, cap);
+      d_prev = carve<uint32_t>(c2, cap);
+      d_gnext = carve<uint32_t>(c2, cap);
+      d_heads = carve<uint32_t>(c2, cap);
+      d_hhead = carve<uint32_t>(c2, hcap);
+      return (size_t)(c2 - base);
     };
-    err = body();
-    const hipError_t e = hipStreamSynchronize(st);  // the leases are reused only after this
-    drain.armed = false;
-    if (err) return err;
-    if (e != hipSuccess) {
-      h3c_rt::set_error("h3c_update_ios", e);
+    h3c_rt::DeviceLease lease2(dev, layout2(nullptr));
+    if (!lease2.ok()) return H3C_ERR_HIP;
+    StreamDrain drain2{st, true};
+    layout2(lease2.data());
+    const uint32_t *d_F = d_fbase + n;
+    const uint32_t fb = (cap + tb - 1) / tb;
+    if (attempt) {  // the first attempt's chain count and counters
+      HIP_TRY(hipMemsetAsync(d_misc + kMiscHeads, 0, 4, st));
+      HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, st));
+    }
+    hipLaunchKernelGGL(uio_frag_kernel, dim3((std::max(cap, hcap) + tb - 1) / tb), dim3(tb), 0, st, d_pos, d_fbase, n,
+                       cap, d_ios, d_skey, d_chunks, d_frag, d_fkey, pc, d_hhead, hcap);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(uio_tlink_kernel, dim3((cap + kLinkTile - 1) / kLinkTile), dim3(kLinkTile), 0, st, d_fkey, d_F,
+                       cap, d_hhead, hcap - 1, d_gnext, d_prev);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(uio_resolve_kernel, dim3(fb), dim3(tb), 0, st, d_fkey, d_F, cap, d_hhead, hcap - 1, d_gnext,
+                       d_prev);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(uio_heads_kernel, dim3(fb), dim3(tb), 0, st, d_prev, d_F, cap, d_frag, d_heads,
+                       d_misc + kMiscHeads);
+    HIP_TRY(hipGetLastError());
+    const uint32_t blocks = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
+    h3c_rt::ProfToken tok;
+    HIP_TRY(h3c_rt::prof_begin(st, tok));
+    hipLaunchKernelGGL(uio_block_kernel, dim3(blocks), dim3(kThreads), 0, st, d_frag, d_heads, d_misc + kMiscHeads,
+                       pc, d_eacc);
+    HIP_TRY(hipGetLastError());
+    // algorithmic bytes, per op: a 4 KiB block read and written once plus 4 KiB of new bytes
+    // (exact for BASELINE config 3's block-aligned 4 KiB writes; bench.py states the unit)
+    HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDIO, 3ull * kBlk * n));
+    // t' per op, then s' per op (two affine scans by chunk; elements computed as they are read)
+    {
+      size_t t = tmp_bytes;
+      HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, TIt(CountIt(0), TMapFn{d_pos, d_eacc, d_payraw, pc}),
+                                             d_tscan, (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
+      t = tmp_bytes;
+      HIP_TRY(rocprim::inclusive_scan_by_key(
+          d_tmp, t, d_skey, SIt(CountIt(0), SMapFn{d_pos, d_skey, nchunks, d_tscan, d_t0, d_eacc, d_payraw, pc}),
+          d_sscan, (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
+    }
+    HIP_TRY(hipMemcpyAsync(d_chunks_out, d_chunks, sizeof(h3c_chunk_state) * nchunks, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(uio_result_kernel, dim3(gb), dim3(tb), 0, st, d_pos, d_skey, n, d_sscan, d_chunks,
+                       d_chunks_out, nchunks, d_t0, poly_type, stdf, poly, d_res, d_ctr);
+    HIP_TRY(hipGetLastError());
+    if (exact) {
+      hipLaunchKernelGGL(uio_stale_kernel, dim3((nchunks + tb - 1) / tb), dim3(tb), 0, st, d_chunks, nchunks, d_t0,
+                         poly_type, stdf, d_ctr);
+      HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipMemcpyAsync(d_misc + 2, d_F, 4, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemcpyAsync(hd, d_dn, dn_misc + 16, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(results, d_res, sizeof(h3c_update_result) * n, hipMemcpyDeviceToHost, st));
+    const hipError_t se = hipStreamSynchronize(st);
+    drain2.armed = false;
+    if (se != hipSuccess) {
+      drain.armed = false;
+      h3c_rt::set_error("h3c_update_ios", se);
       return H3C_ERR_HIP;
     }
-    clk.mark("C-D device");
-    if (spec) {
-      const uint32_t *bad = reinterpret_cast<const uint32_t *>(hp + off[kBad]);
-      if (bad[0]) {  // a client checksum did not match: nothing was written; redo with them known
-        payraw.assign(n, 0xFFFFFFFFu);
-        std::memcpy(payraw.data(), hp + off[kPayBack], 4ull * n);
-        for (uint32_t k = 0; k < nver; ++k)
-          if (bad[1 + k]) status[ver_host[k].op] = H3C_ERR_CHECKSUM_MISMATCH;
-        continue;
-      }
+    const uint32_t F = reinterpret_cast<const uint32_t *>(hd + dn_misc)[2];
+    last_frags = F;
+    if (F <= cap) break;
+    if (attempt) {  // cannot happen: the count is exact on the second attempt
+      drain.armed = false;
+      h3c_rt::set_error_text("h3c_update_ios: fragment count changed between attempts");
+      return H3C_ERR_HIP;
     }
-    if (npos) std::memcpy(truev.data(), hp + off[kTrue], 4ull * npos);
-    break;
+    cap = F;  // nothing was written (no chains ran): redo with the count known
   }
-
-  // ---- E. results and final chunk states, per chunk range on the pass's threads ----
-  for (uint32_t i = 0; i < n; ++i)
-    if (ios[i].chunk >= nchunks) {  // IOResult default {NONE, 0}
-      std::memset(&results[i], 0, sizeof(h3c_update_result));
-      results[i].status = status[i];
-    }
-  run_tasks(T, NT, [&](unsigned k) {
-    for (uint32_t c = ws.cut[k]; c < ws.cut[k + 1]; ++c) {
-      const uint32_t init_value = chunks[c].value;
-      auto value_of = [&](Src src, uint32_t pos) -> uint32_t {
-        if (src == Src::kZero) return 0u;
-        if (src == Src::kInitial) return init_value;
-        return std_domain ? ~truev[pos] : truev[pos];
-      };
-      // replay sizes and types in sequence order for per-op results
-      uint32_t size_now = chunks[c].size;
-      uint8_t type_now = chunks[c].type;
-      for (uint32_t k = ws.opstart[c]; k < ws.opstart[c + 1]; ++k) {
-        const uint32_t i = ws.order[k];
-        const h3c_update_io &io = ios[i];
-        h3c_update_result &r = results[i];
-        std::memset(&r, 0, sizeof(r));
-        r.status = status[i];
-        if (status[i] == H3C_ERR_INVALID_ARG) {  // IOResult default {NONE, 0}
-          r.size = size_now;
-          continue;
-        }
-        if (status[i] == H3C_OK) {  // size after the op (as in the pass)
-          uint64_t na = size_now;
-          if (io.kind == H3C_UPD_WRITE) na = std::max<uint64_t>(size_now, (uint64_t)io.offset + io.length);
-          else if (io.kind == H3C_UPD_TRUNCATE || io.length > size_now) na = io.length;
-          size_now = (uint32_t)na;
-          if (io.kind == H3C_UPD_WRITE) type_now = io.checksum_type;
-        }
-        r.size = size_now;
-        r.type = (std_domain && status[i] == H3C_OK) ? poly_type : type_now;
-        r.value = value_of(S.outs[k].src, S.outs[k].pos);
-      }
-      if (S.tr[c].started) {
-        chunks[c].size = S.tr[c].size;
-        chunks[c].type = std_domain ? poly_type : S.tr[c].type;
-        chunks[c].value = value_of(S.tr[c].src, S.tr[c].true_pos);
-      }
-    }
-  });
-  clk.mark("E results");
-  if (clk.on)
-    std::fprintf(stderr, "[updio] threads %u, tasks %u, epochs %zu, crc jobs %u, elements %u\n", T, NT, M.nep,
-                 M.njobs, npos);
+  drain.armed = false;
+  std::memcpy(chunks, hd, sizeof(h3c_chunk_state) * nchunks);
+  const unsigned long long *h_ctr = reinterpret_cast<const unsigned long long *>(hd + dn_ctr);
+  if (counters) {
+    counters->none = h_ctr[kCtrNone];
+    counters->reuse = h_ctr[kCtrReuse];
+    counters->combine = h_ctr[kCtrCombine];
+    counters->read_chunk = h_ctr[kCtrRead];
+    counters->recalculate = h_ctr[kCtrRecalc];
+    counters->checksum_mismatch = h_ctr[kCtrMismatch];
+    counters->invalid = h_ctr[kCtrInvalid];
+    counters->stale_chunks = h_ctr[kCtrStale];
+  }
   return H3C_OK;
 }
 
-// Diagnostic hook, no device work (the payload-job build here is single-threaded; the
-// call itself builds it per op range on the pool): host time of one speculative h3c_update_ios pass over
-// `ios` (payload-job build, position plan, op grouping, host pass B with its merge and
-// publication into staging), the fastest of `reps`; the phase split goes to stderr with
-// H3C_UPDIO_TIMING.  Used to tune the host pass without a GPU.
-extern "C" double h3c_diag_updio_host_ms(uint8_t poly_type, const h3c_chunk_state *chunks, uint32_t nchunks,
-                                         const h3c_update_io *ios, uint32_t n, int reps) {
-  const uint32_t poly = poly_type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
-  thread_local UpdioScratch tls_ws;
-  UpdioScratch &ws = tls_ws;
-  double total = 0, t_a = 0, t_b = 0, t_c = 0;
-  std::vector<AffIn> lay;
-  std::vector<uint32_t> keys;
-  std::vector<DevChunk> crc;
-  std::vector<CopyPiece> copy;
-  std::vector<VerifyItem> ver;
-  const unsigned T = std::max(1u, std::min<unsigned>(pass_threads(n), nchunks));
-  const unsigned NT = std::max(1u, std::min<unsigned>(T == 1 ? 1u : 4u * T, nchunks));
-  if (ws.L.size() < NT) ws.L.resize(NT);
-  PassMerge M;
-  for (int r = 0; r < reps; ++r) {
-    const auto t0 = std::chrono::steady_clock::now();
-    ws.status.assign(n, H3C_OK);
-    for (uint32_t i = 0; i < n; ++i)
-      if (ios[i].chunk >= nchunks) ws.status[i] = H3C_ERR_INVALID_ARG;
-    const uint64_t seg = 1u << 20;
-    CrcBatch &pay = ws.pay;
-    pay.chunks.clear();
-    pay.total_segs = pay.max_segs = 0;
-    pay.bytes = pay.max_len = 0;
-    FoldCache fc;
-    for (uint32_t i = 0; i < n; ++i)
-      if (ws.status[i] == H3C_OK && ios[i].kind == H3C_UPD_WRITE && ios[i].length)
-        add_job(pay, fc, ios[i].payload, ios[i].length, 0xFFFFFFFFu, i, seg, poly);
-    const uint32_t npos = plan_positions(poly_type, chunks, nchunks, ios, n, ws.status, ws.start);
-    lay.resize(npos);
-    keys.resize(npos);
-    ws.S.tr.resize(nchunks);
-    ws.S.cur.resize(nchunks);
-    ws.S.raw0.resize(nchunks);
-    group_ops(ios, n, nchunks, ws.opstart, ws.order);
-    ws.S.outs.assign(ws.order.size(), OpOut{});
-    cut_chunks(ws.opstart, nchunks, NT, ws.cut);
-    const auto t1 = std::chrono::steady_clock::now();
-    std::vector<double> busy(NT, 0.0);
-    run_tasks(T, NT, [&](unsigned k) {
-      const auto b0 = std::chrono::steady_clock::now();
-      host_pass(poly_type, poly, false, chunks, ios, ws.status.data(), nullptr, seg, ws.start.data(),
-                ws.opstart.data(), ws.order.data(), lay.data(), keys.data(), ws.cut[k], ws.cut[k + 1], ws.S, ws.L[k]);
-      busy[k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b0).count();
-    });
-    if (std::getenv("H3C_UPDIO_BUSY") && r == reps - 1)
-      for (unsigned k = 0; k < NT; ++k) std::fprintf(stderr, "  task %u busy %.3f ms\n", k, busy[k]);
-    M.build(ws.L, NT);
-    const auto t2 = std::chrono::steady_clock::now();
-    crc.resize(M.crc_total);
-    copy.resize(M.copy_total);
-    ver.resize(M.ver_total);
-    run_tasks(T, NT, [&](unsigned k) {
-      pass_publish(ws.L[k], M, k, NT, ws.cut[k], ws.cut[k + 1], ws.start.data(), ws.S, lay.data(), crc.data(),
-                   copy.data(), ver.data());
-    });
-    const auto t3 = std::chrono::steady_clock::now();
-    using ms = std::chrono::duration<double, std::milli>;
-    if (r == 0 || ms(t3 - t0).count() < total) {  // the fastest repetition
-      t_a = ms(t1 - t0).count();
-      t_b = ms(t2 - t1).count();
-      t_c = ms(t3 - t2).count();
-      total = ms(t3 - t0).count();
-    }
-  }
-  if (std::getenv("H3C_UPDIO_TIMING"))
-    std::fprintf(stderr, "[updio host] threads %u: payload jobs + plan + grouping %.3f ms, pass %.3f ms, publish %.3f ms\n",
-                 T, t_a, t_b, t_c);
-  return total;
+extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
+                              uint32_t n, h3c_update_result *results, uint32_t flags, void *stream) {
+  return h3c_update_ios_ex(poly_type, chunks, nchunks, ios, n, results, flags, nullptr, stream);
 }

@@ -83,6 +83,7 @@ _proto("h3c_fill_splitmix", _int, _vp, _u64, _u64, _u64, _u64, _u64, _vp)
 _proto("h3c_update_workspace_bytes", _sz, _u32, _u32, _u64, _u32)
 _proto("h3c_update_blocks", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp)
 _proto("h3c_update_ios", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp)
+_proto("h3c_update_ios_ex", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp)
 _proto("h3c_serde_checksum_mark", _u32, _u32, _int)
 _proto("h3c_batch_serde_checksum", _int, _vp, _sz, _vp, _vp, _vp)
 _proto("h3c_batch_serde_verify", _int, _vp, _sz, _vp, _vp, _vp, _vp)
@@ -103,7 +104,7 @@ _proto("h3c_profile_enable", None, _int)
 _proto("h3c_profile_read", _int, _int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64), ctypes.POINTER(_u64),
        _int)
 
-PROF_SEG, PROF_UPDATE, PROF_HOSTFED = 0, 1, 2
+PROF_SEG, PROF_UPDATE, PROF_HOSTFED, PROF_UPDIO = 0, 1, 2, 3
 
 
 class ChecksumType(enum.IntEnum):
@@ -322,33 +323,57 @@ def update_blocks(chunk_bases, chunk_len: int, raw_in, blk_chunk, blk_index, pay
 
 # ---------------------------------------------------------------- general updates (h3c_update_ios)
 
-UPD_WRITE, UPD_TRUNCATE, UPD_EXTEND = 1, 4, 8  # UpdateType (Common.h:51-58)
+UPD_WRITE, UPD_REMOVE, UPD_TRUNCATE, UPD_EXTEND, UPD_COMMIT = 1, 2, 4, 8, 16  # UpdateType (Common.h:51-58)
 UPD_STD_DOMAIN = 1  # flag: Rust chunk engine semantics (std-domain values)
+UPD_EXACT = 2  # flag: stored checksums are not trusted (each chunk CRC'd once first)
+IO_SYNCING = 1  # per-op flag: UpdateOptions.isSyncing full-chunk replace
 
 CHUNK_STATE_DTYPE = np.dtype([("base", "<u8"), ("chunk_size", "<u4"), ("size", "<u4"), ("value", "<u4"),
                               ("type", "u1"), ("reserved", "u1", 3)])
 UPDATE_IO_DTYPE = np.dtype([("payload", "<u8"), ("chunk", "<u4"), ("offset", "<u4"), ("length", "<u4"),
-                            ("checksum_value", "<u4"), ("checksum_type", "u1"), ("kind", "u1"),
-                            ("reserved", "u1", 6)])
+                            ("checksum_value", "<u4"), ("checksum_type", "u1"), ("kind", "u1"), ("flags", "u1"),
+                            ("reserved", "u1", 5)])
 UPDATE_RESULT_DTYPE = np.dtype([("status", "<u4"), ("size", "<u4"), ("value", "<u4"), ("type", "u1"),
                                 ("reserved", "u1", 3)])
 assert CHUNK_STATE_DTYPE.itemsize == 24 and UPDATE_IO_DTYPE.itemsize == 32 and UPDATE_RESULT_DTYPE.itemsize == 16
 
 
+class UpdateCounters(ctypes.Structure):
+    """h3c_update_counters: the reference's checksum case counters for one batch
+    (ChunkReplica.cc:25-28, StorageTarget.cc:331-332; Rust metrics.rs:12-14)."""
+
+    _fields_ = [(f, _u64) for f in ("none", "reuse", "combine", "read_chunk", "recalculate", "checksum_mismatch",
+                                    "invalid", "stale_chunks")]
+
+    def as_dict(self):
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
 def update_ios(chunks: np.ndarray, ios: np.ndarray, type_: int = ChecksumType.CRC32C, std_domain: bool = False,
-               stream=None) -> np.ndarray:
-    """Batched ChunkReplica::update + updateChecksum for any mix of WRITE / TRUNCATE / EXTEND
-    (h3c_update_ios).  `chunks` (CHUNK_STATE_DTYPE, updated in place: size / type / value)
-    and `ios` (UPDATE_IO_DTYPE) are host arrays whose `base` / `payload` fields are device
-    addresses.  Returns one UPDATE_RESULT_DTYPE record per op: status 0 / 3 kInvalidArg /
-    4080 kChecksumMismatch, chunk size after, and result.checksum (type, value)."""
+               exact: bool = False, counters: Optional[UpdateCounters] = None, stream=None,
+               out: Optional[np.ndarray] = None) -> np.ndarray:
+    """Batched ChunkReplica::update + updateChecksum for any mix of WRITE / REMOVE / TRUNCATE /
+    EXTEND / COMMIT (h3c_update_ios_ex).  `chunks` (CHUNK_STATE_DTYPE, updated in place: size /
+    type / value) and `ios` (UPDATE_IO_DTYPE) are host arrays whose `base` / `payload` fields are
+    device addresses.  Returns one UPDATE_RESULT_DTYPE record per op: status 0 / 3 kInvalidArg /
+    4080 kChecksumMismatch, chunk size after, and result.checksum (type, value).  `exact` does not
+    trust stored checksums (H3C_UPD_EXACT); `counters` receives the batch's case counts; `out`
+    (UPDATE_RESULT_DTYPE, len(ios)) receives the results instead of a new array (pass a pinned
+    one to skip the runtime's staging copy)."""
     if chunks.dtype != CHUNK_STATE_DTYPE or ios.dtype != UPDATE_IO_DTYPE:
         raise TypeError("chunks / ios must use CHUNK_STATE_DTYPE / UPDATE_IO_DTYPE")
     if not (chunks.flags.c_contiguous and ios.flags.c_contiguous):
         raise ValueError("chunks / ios must be contiguous")
-    res = np.zeros(len(ios), dtype=UPDATE_RESULT_DTYPE)
-    _check(lib.h3c_update_ios(int(type_), chunks.ctypes.data, len(chunks), ios.ctypes.data, len(ios),
-                              res.ctypes.data, UPD_STD_DOMAIN if std_domain else 0, _stream_handle(stream)))
+    if out is not None:
+        if out.dtype != UPDATE_RESULT_DTYPE or len(out) != len(ios) or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous UPDATE_RESULT_DTYPE array with one record per op")
+        res = out
+    else:
+        res = np.zeros(len(ios), dtype=UPDATE_RESULT_DTYPE)
+    flags = (UPD_STD_DOMAIN if std_domain else 0) | (UPD_EXACT if exact else 0)
+    _check(lib.h3c_update_ios_ex(int(type_), chunks.ctypes.data, len(chunks), ios.ctypes.data, len(ios),
+                                 res.ctypes.data, flags, ctypes.byref(counters) if counters is not None else None,
+                                 _stream_handle(stream)))
     return res
 
 

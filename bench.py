@@ -216,6 +216,7 @@ PATTERN_CEILING = {
     "seg_crc_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
     "seg_quad_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
     "upd_delta_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
+    "uio_block_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
 }
 
 
@@ -385,10 +386,19 @@ def run_update(args, cx: Ctx) -> dict:
     return res
 
 
+def _pinned_records(torch, n: int, dtype) -> np.ndarray:
+    """A numpy record array in pinned host memory (DMA without a staging copy)."""
+    t = torch.empty(n * dtype.itemsize, dtype=torch.uint8).pin_memory()
+    a = t.numpy().view(dtype)
+    a[...] = 0
+    return a, t
+
+
 def run_updio(args, cx: Ctx) -> dict:
     """BASELINE config 3 through the general path (h3c_update_ios): each 4 KiB write is a full
-    UpdateIO (client checksum verified, updateChecksum case analysis, conflict epochs).  The
-    host metadata pass and both host<->device round trips are inside the timed step."""
+    UpdateIO -- client checksum verified (ChunkReplica.cc:193-207), updateChecksum's case
+    analysis, fragments chained per 4 KiB block.  Op table in, per-op results and chunk states
+    out, all inside the timed step (host arrays in pinned memory); payloads and chunks in HBM."""
     torch, h3c = cx.torch, cx.h3c
     nchunks, clen, nw, G = 64, 64 << 20, args.writes, 4096
     bpc = clen // G
@@ -406,13 +416,13 @@ def run_updio(args, cx: Ctx) -> dict:
     praw = torch.zeros(nw, dtype=torch.int32, device=cx.dev)
     pplan.run(praw, stream=cx.stream)
     torch.cuda.synchronize()
-    state = np.zeros(nchunks, dtype=h3c.CHUNK_STATE_DTYPE)
+    state, _st = _pinned_records(torch, nchunks, h3c.CHUNK_STATE_DTYPE)
     state["base"] = chunks.data_ptr() + np.arange(nchunks, dtype=np.uint64) * np.uint64(clen)
     state["chunk_size"] = clen
     state["size"] = clen
     state["value"] = raw0.cpu().numpy().view(np.uint32)
     state["type"] = 1
-    ios = np.zeros(nw, dtype=h3c.UPDATE_IO_DTYPE)
+    ios, _it = _pinned_records(torch, nw, h3c.UPDATE_IO_DTYPE)
     ios["payload"] = payload.data_ptr() + np.arange(nw, dtype=np.uint64) * np.uint64(G)
     ios["chunk"] = wc
     ios["offset"] = wb * G
@@ -420,25 +430,25 @@ def run_updio(args, cx: Ctx) -> dict:
     ios["checksum_value"] = praw.cpu().numpy().view(np.uint32)
     ios["checksum_type"] = 1
     ios["kind"] = h3c.UPD_WRITE
-    last = {}
+    res, _rt = _pinned_records(torch, nw, h3c.UPDATE_RESULT_DTYPE)
+    counters = h3c.UpdateCounters()
+    exact = bool(getattr(args, "exact", False))
 
     def step():
-        t = time.perf_counter()
-        last["res"] = h3c.update_ios(state, ios, stream=cx.stream)
-        if os.environ.get("H3C_UPDIO_TIMING"):
-            print(f"[bench] update_ios {1e3 * (time.perf_counter() - t):.3f} ms", file=sys.stderr, flush=True)
+        h3c.update_ios(state, ios, stream=cx.stream, out=res, exact=exact, counters=counters)
 
-    elapsed, _ = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDATE)
+    elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDIO)
     fresh = torch.zeros(nchunks, dtype=torch.int32, device=cx.dev)
     plan.run(fresh, stream=cx.stream)
     torch.cuda.synchronize()
-    ok = bool((last["res"]["status"] == 0).all()) and np.array_equal(fresh.cpu().numpy().view(np.uint32),
-                                                                     state["value"])
+    ok = bool((res["status"] == 0).all()) and np.array_equal(fresh.cpu().numpy().view(np.uint32), state["value"])
+    ok = ok and counters.read_chunk == nw
     verified = cx.all_true(ok)
     plan.close()
     pplan.close()
     writes = nw * args.steps * cx.world
-    return {
+    rl = roofline(prof, HBM_PEAK_GBPS, kernel="uio_block_kernel")
+    out = {
         "metric": "partial-update writes/s through the general UpdateIO path (4 KiB writes into 64 MiB chunks)",
         "value": round(writes / elapsed, 1),
         "unit": "writes/s",
@@ -446,11 +456,18 @@ def run_updio(args, cx: Ctx) -> dict:
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (splitmix64 chunks and payloads in HBM, seeded uniform chunk/offset)",
-        "config": {"workload": f"BASELINE config 3 via h3c_update_ios: {nw} random 4 KiB UpdateIOs into "
-                               f"{nchunks} x 64 MiB chunks per GPU", "parallelism": f"shard{cx.world}"},
+        "config": {"workload": f"BASELINE config 3 via h3c_update_ios{' (H3C_UPD_EXACT)' if exact else ''}: {nw} "
+                               f"random 4 KiB UpdateIOs into {nchunks} x 64 MiB chunks per GPU",
+                   "parallelism": f"shard{cx.world}", "exact": exact},
         "verified": verified,
-        "algorithmic_gbps": round(writes * 3 * G / elapsed / 1e9, 1),
+        # per write: payload read twice (A6 verify, then the block kernel), block read + write
+        "algorithmic_gbps": round(writes * 4 * G / elapsed / 1e9, 1),
+        "counters": counters.as_dict(),
+        "roofline": rl,
     }
+    if cx.world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_update()
+    return out
 
 
 def pcie_h2d_peak(torch, dev, nbytes: int = 1 << 30) -> float:
@@ -652,6 +669,7 @@ def main() -> int:
     ap.add_argument("--pass-gib", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exact", action="store_true", help="updio / update: do not trust stored checksums")
     args = ap.parse_args()
     cx = Ctx()
     fn = {"verify": run_verify, "update": run_update, "updio": run_updio, "hostfed": run_hostfed,

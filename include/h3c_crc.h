@@ -147,8 +147,19 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
 
 /* ---- general batched updates: every UpdateIO case of ChunkReplica::update ---- */
 
-/* UpdateType (src/fbs/storage/Common.h:51-58); REMOVE / COMMIT touch no checksum. */
-enum h3c_update_kind { H3C_UPD_WRITE = 1, H3C_UPD_TRUNCATE = 4, H3C_UPD_EXTEND = 8 };
+/* UpdateType (src/fbs/storage/Common.h:51-58).  REMOVE must carry offset 0, length 0 and a
+ * NONE checksum (the form StorageOperator::doRemove builds, StorageOperator.cc:808-815); it
+ * runs updateChecksum's case (i) and stores {NONE, 0} (Rust engine: leaves the checksum).
+ * COMMIT (ChunkReplica::commit, ChunkReplica.cc:397-467) touches no byte and no checksum;
+ * its result is {NONE, 0}.  Both pass through so an UpdateWorker queue can be drained into
+ * one batch without filtering. */
+enum h3c_update_kind {
+  H3C_UPD_WRITE = 1,
+  H3C_UPD_REMOVE = 2,
+  H3C_UPD_TRUNCATE = 4,
+  H3C_UPD_EXTEND = 8,
+  H3C_UPD_COMMIT = 16
+};
 
 /* ChunkMetadata fields on the path (Common.h:662-676) plus where the bytes live. */
 typedef struct h3c_chunk_state {
@@ -160,6 +171,11 @@ typedef struct h3c_chunk_state {
   uint8_t reserved[3];
 } h3c_chunk_state;
 
+/* per-op flags (h3c_update_io.flags) */
+#define H3C_IO_SYNCING 1u /* UpdateOptions.isSyncing: the resync successor's full-chunk replace
+                             (ChunkReplica.cc:211-215, 289; chunk.rs:112, 166-170): WRITE at
+                             offset 0 only (ReliableForwarding.cc:203-207), else kInvalidArg */
+
 /* UpdateIO fields on the path (Common.h:326-345). */
 typedef struct h3c_update_io {
   uint64_t payload;        /* device address of `length` bytes (WRITE) */
@@ -169,37 +185,76 @@ typedef struct h3c_update_io {
   uint32_t checksum_value; /* the client's ChecksumInfo of the payload */
   uint8_t checksum_type;
   uint8_t kind;            /* h3c_update_kind */
-  uint8_t reserved[6];
+  uint8_t flags;           /* H3C_IO_* */
+  uint8_t reserved[5];
 } h3c_update_io;
 
 typedef struct h3c_update_result {
   uint32_t status; /* H3C_OK, H3C_ERR_INVALID_ARG (range, :140-145), H3C_ERR_CHECKSUM_MISMATCH (:193-207) */
   uint32_t size;   /* meta.size after the op */
-  uint32_t value;  /* result.checksum after the op (meta.checksum(), ChunkReplica.cc:313) */
+  uint32_t value;  /* result.checksum after the op (meta.checksum(), ChunkReplica.cc:311; std domain:
+                      the engine's out_checksum, 0 after a checksum mismatch, engine.rs:303,324) */
   uint8_t type;
   uint8_t reserved[3];
 } h3c_update_result;
 
+/* The reference's checksum case counters for one batch.
+ *   ChunkReplica (raw domain): storage.chunk_update.checksum_{none,reuse,combine,read_chunk}
+ *     (ChunkReplica.cc:25-28, incremented at :336,339,355,389) and the update path's
+ *     storage.update.checksum_mismatch (StorageTarget.cc:331-332).
+ *   Rust chunk engine (std domain): checksum_{reuse,combine,recalculate} (metrics.rs:12-14,
+ *     chunk.rs:153,156,188,217,233,273); combine counts the aligned path's zero pad and append
+ *     separately, as chunk.rs does (the pad/append split uses the payload's device address
+ *     for is_aligned_buf, aligned.rs:47-49).
+ *   stale_chunks (H3C_UPD_EXACT only): chunks whose stored checksum of the batch polynomial
+ *     disagreed with their bytes -- the input the trusted mode would have carried forward. */
+typedef struct h3c_update_counters {
+  uint64_t none, reuse, combine, read_chunk; /* raw domain */
+  uint64_t recalculate;                      /* std domain (reuse / combine shared) */
+  uint64_t checksum_mismatch;                /* A6 failures (status 4080) */
+  uint64_t invalid;                          /* status kInvalidArg */
+  uint64_t stale_chunks;                     /* H3C_UPD_EXACT */
+} h3c_update_counters;
+
 /* flags */
 #define H3C_UPD_STD_DOMAIN 1u /* Rust chunk engine (chunk_engine/src/alloc/chunk.rs:89-281): values are
-                                 std-domain crc32c and every applied op leaves crc32c(content) */
+                                 std-domain crc32c, Engine::update_chunk / copy_on_write / safe_write */
+#define H3C_UPD_EXACT 2u      /* do not trust stored checksums: every chunk in the table with bytes is
+                                 CRC'd once before the batch (see below) */
 
 /* Apply `n` UpdateIOs in sequence order to device-resident chunks, replacing
  * ChunkReplica::update's per-op payload verify (ChunkReplica.cc:193-207), zero fill,
- * write / truncate / extend (:256-294) and updateChecksum (:319-394, all four cases)
- * -- or, with H3C_UPD_STD_DOMAIN, Chunk::safe_write / copy_on_write's checksum.
- * Arbitrary offsets and lengths; writes to the same bytes are ordered.  The chunk
- * checksum is maintained by GF(2) deltas: a write costs its own bytes plus the
- * overwritten bytes, a truncate the cut tail; a chunk whose stored checksum is not of
- * `poly_type` (e.g. NONE) is CRC'd once.  A stored checksum of `poly_type` is trusted,
- * as the reference's append case trusts it.  Client checksums must be NONE or
- * `poly_type` (the client's chunk_checksum_type), else the op fails with
- * H3C_ERR_INVALID_ARG; so does a TRUNCATE / EXTEND of a chunk whose stored checksum is
- * of the other polynomial.  `chunks` and `results` are host arrays; chunk bytes are
- * updated in place on device.  Synchronous on `stream`.  A chunk whose size exceeds its
+ * write / truncate / extend / remove (:256-294) and updateChecksum (:319-394, all four cases)
+ * -- or, with H3C_UPD_STD_DOMAIN, Engine::update_chunk's verify and Chunk::copy_on_write /
+ * safe_write's checksum (engine.rs:288-429, chunk.rs:89-281).  Arbitrary offsets and lengths;
+ * writes to the same bytes are ordered.  Every op's result and every chunk's final state equal
+ * the reference's replay of the same ops in sequence order, with one documented exception:
+ *
+ *   Stored checksums.  The reference's prefix / suffix case (iv) re-reads the chunk bytes, so
+ *   its result does not depend on meta.checksumValue; its append case (iii) combines with it
+ *   (and a TRUNCATE / EXTEND at offset == size keeps it).  By default (trusted mode) a stored
+ *   checksum of `poly_type` is taken as the CRC of the chunk's bytes, and every op costs
+ *   O(its own bytes): results are bit-exact whenever stored checksums are consistent with the
+ *   bytes; on a chunk whose stored value is off by e (bit rot, a torn write), the reference
+ *   heals e at its next case-(ii)/(iv) op while the trusted mode carries it, shifted with the
+ *   chunk's length, until a full overwrite.  H3C_UPD_EXACT CRCs each chunk's bytes once
+ *   first (O(chunk) per chunk per batch, not per op) and then reproduces the reference
+ *   exactly, stale values included; counters->stale_chunks reports how many disagreed.
+ *
+ * A chunk whose stored checksum is not of `poly_type` (e.g. NONE) is CRC'd once either way.
+ * Client checksums must be NONE or `poly_type` (the client's chunk_checksum_type), else the
+ * op fails with H3C_ERR_INVALID_ARG; so does a TRUNCATE / EXTEND of a chunk whose stored
+ * checksum is of the other polynomial (raw domain).  `chunks` and `results` are host arrays
+ * (pinned memory avoids a staging copy); chunk bytes are updated in place on device.  All
+ * per-op work runs on the device; the host issues the launches, one mid-batch read of the
+ * work size and the final copy.  Synchronous on `stream`.  A chunk whose size exceeds its
  * chunk_size fails the whole call with H3C_ERR_INVALID_ARG, before any work. */
 int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios, uint32_t n,
                    h3c_update_result *results, uint32_t flags, void *stream);
+/* The same, also returning the batch's case counters (counters may be NULL). */
+int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
+                      uint32_t n, h3c_update_result *results, uint32_t flags, h3c_update_counters *counters,
+                      void *stream);
 
 /* ---- adjacent formats on the same kernels ---- */
 
@@ -287,16 +342,11 @@ int h3c_fill_splitmix(void *base_dev, uint64_t chunk_len, uint64_t nchunks, uint
 enum h3c_prof_kind {
   H3C_PROF_SEG = 0,     /* seg_crc_kernel: payload bytes read */
   H3C_PROF_UPDATE = 1,  /* upd_delta_kernel: 3 x block bytes per block write */
-  H3C_PROF_HOSTFED = 2  /* whole host-fed pipeline (H2D + CRC): payload bytes */
+  H3C_PROF_HOSTFED = 2, /* whole host-fed pipeline (H2D + CRC): payload bytes */
+  H3C_PROF_UPDIO = 3    /* h3c_update_ios's block kernel: 12 KiB per fragment (block in + out + new) */
 };
 void h3c_profile_enable(int on);
 int h3c_profile_read(int kind, double *ms, uint64_t *launches, uint64_t *bytes, int reset);
-
-/* Host time (ms, fastest of `reps`) of h3c_update_ios's host side for these ops with no
- * device work: payload-job build, scan layout, the host pass and its merge.  A tuning aid
- * (scripts/updio_hostbench.py); `base` / `payload` fields are never dereferenced. */
-double h3c_diag_updio_host_ms(uint8_t poly_type, const h3c_chunk_state *chunks, uint32_t nchunks,
-                              const h3c_update_io *ios, uint32_t n, int reps);
 
 #ifdef __cplusplus
 }

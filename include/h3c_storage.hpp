@@ -30,7 +30,7 @@ enum StatusCode : uint32_t {
 };
 
 // UpdateType (Common.h:51-58).
-enum class UpdateType : uint8_t { INVALID = 0, WRITE = 1, REMOVE = 2, TRUNCATE = 4, EXTEND = 8 };
+enum class UpdateType : uint8_t { INVALID = 0, WRITE = 1, REMOVE = 2, TRUNCATE = 4, EXTEND = 8, COMMIT = 16 };
 
 // UpdateIO fields on the path (Common.h:326-345); `chunk` indexes the batch's chunk table
 // (the reference keys by GlobalKey), `data` is the payload's device address.
@@ -41,8 +41,10 @@ struct UpdateIO {
   UpdateType updateType = UpdateType::WRITE;
   ChecksumInfo checksum;
   const uint8_t *data = nullptr;
+  bool isSyncing = false;  // UpdateOptions.isSyncing (ChunkReplica.cc:211-215, 289): WRITE at offset 0
 
   bool isWrite() const { return updateType == UpdateType::WRITE; }
+  bool isRemove() const { return updateType == UpdateType::REMOVE; }
   bool isTruncate() const { return updateType == UpdateType::TRUNCATE; }
   bool isExtend() const { return updateType == UpdateType::EXTEND; }
 };
@@ -72,9 +74,11 @@ struct IOResult {
 struct ChunkReplicaBatch {
   // `metas` are updated in place (size / checksumType / checksumValue), chunk bytes on
   // device.  `checksumType` is the batch's polynomial (the client's chunk_checksum_type).
+  // `flags`: H3C_UPD_EXACT to not trust stored checksums; `counters`: the reference's
+  // storage.chunk_update.checksum_* counts of the batch (ChunkReplica.cc:25-28).
   static int update(std::vector<ChunkMetadata> &metas, const std::vector<UpdateIO> &ios,
                     std::vector<IOResult> &results, ChecksumType checksumType = ChecksumType::CRC32C,
-                    void *stream = nullptr) {
+                    void *stream = nullptr, uint32_t flags = 0, h3c_update_counters *counters = nullptr) {
     std::vector<h3c_chunk_state> cs(metas.size());
     for (size_t c = 0; c < metas.size(); ++c)
       cs[c] = h3c_chunk_state{(uint64_t)(uintptr_t)metas[c].bytes, metas[c].chunkSize, metas[c].size,
@@ -83,10 +87,10 @@ struct ChunkReplicaBatch {
     for (size_t i = 0; i < ios.size(); ++i)
       io[i] = h3c_update_io{(uint64_t)(uintptr_t)ios[i].data, ios[i].chunk, ios[i].offset, ios[i].length,
                             ios[i].checksum.value, (uint8_t)ios[i].checksum.type, (uint8_t)ios[i].updateType,
-                            {0, 0, 0, 0, 0, 0}};
+                            (uint8_t)(ios[i].isSyncing ? H3C_IO_SYNCING : 0u), {0, 0, 0, 0, 0}};
     std::vector<h3c_update_result> res(ios.size());
-    const int rc = h3c_update_ios((uint8_t)checksumType, cs.data(), (uint32_t)cs.size(), io.data(),
-                                  (uint32_t)io.size(), res.data(), 0, stream);
+    const int rc = h3c_update_ios_ex((uint8_t)checksumType, cs.data(), (uint32_t)cs.size(), io.data(),
+                                     (uint32_t)io.size(), res.data(), flags, counters, stream);
     if (rc != H3C_OK) return rc;
     results.resize(ios.size());
     for (size_t i = 0; i < ios.size(); ++i) {

@@ -500,7 +500,11 @@ int orc_chunk_engine_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chunk
   res->type = ORC_CRC32C;
   res->value = ~meta->checksum_value; /* ChunkEngine.cc:66: {CRC32C, ~out_checksum} */
   res->ucase = ORC_CASE_NOT_RUN;
-  if (io->kind == ORC_UPD_COMMIT) return ORC_OK; /* no checksum effect */
+  if (io->kind == ORC_UPD_COMMIT) { /* ChunkEngine::commit sets no checksum on the result */
+    res->type = ORC_NONE;
+    res->value = 0;
+    return ORC_OK;
+  }
   if (io->kind != ORC_UPD_REMOVE && (io->offset >= chunk_size || (uint64_t)io->offset + io->length > chunk_size)) {
     res->status = 3;
     res->type = ORC_NONE;

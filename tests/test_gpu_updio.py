@@ -24,19 +24,28 @@ def torch_dev():
 
 
 class Scenario:
-    """Chunks in one HBM slab, payloads in another, and the oracle's host replica."""
+    """Chunks in one HBM slab, payloads in another, and the oracle's host replica.
 
-    def __init__(self, h3c, torch, dev, nchunks, chunk_size, rng, init="mixed", empty_type=orc.CRC32C):
+    init: "mixed" | "empty" | "crc" | "none"; stale: fraction of CRC chunks whose stored
+    value is off by a random error (bit rot / a torn write) -- the oracle replays the
+    reference literally, so its results are what the engine must return in exact mode."""
+
+    def __init__(self, h3c, torch, dev, nchunks, chunk_size, rng, init="mixed", empty_type=orc.CRC32C, stale=0.0):
         self.h3c, self.torch, self.dev, self.rng = h3c, torch, dev, rng
         self.nchunks, self.chunk_size = nchunks, chunk_size
         self.host = np.zeros((nchunks, chunk_size), dtype=np.uint8)
         self.meta = []
+        self.stale_chunks = 0
         for c in range(nchunks):
             kind = init if init != "mixed" else ["empty", "crc", "none", "crc"][c % 4]
             size = 0 if kind == "empty" else int(rng.integers(1, chunk_size + 1))
             self.host[c, :size] = rng.integers(0, 256, size, dtype=np.uint8)
             if kind == "crc":
-                self.meta.append({"size": size, "type": orc.CRC32C, "value": orc.crc32c(self.host[c, :size])})
+                v = orc.crc32c(self.host[c, :size])
+                if stale and rng.random() < stale:
+                    v ^= int(rng.integers(1, 1 << 32))
+                    self.stale_chunks += 1
+                self.meta.append({"size": size, "type": orc.CRC32C, "value": v})
             elif kind == "none":
                 self.meta.append({"size": size, "type": orc.NONE, "value": 0})
             else:
@@ -45,7 +54,7 @@ class Scenario:
         self.init_meta = [dict(m) for m in self.meta]
         self.ops, self.payloads, self.expect = [], [], []
 
-    def add(self, kind, chunk, offset, length, ctype=orc.CRC32C, good=True, payload=None):
+    def add(self, kind, chunk, offset, length, ctype=orc.CRC32C, good=True, payload=None, syncing=False):
         if payload is None and kind == orc.UPD_WRITE:
             payload = self.rng.integers(0, 256, length, dtype=np.uint8)
         value = 0
@@ -54,20 +63,36 @@ class Scenario:
                 else 0
             if not good:
                 value ^= 0x10
-        io = {"kind": kind, "offset": offset, "length": length, "type": ctype, "value": value}
+        io = {"kind": kind, "offset": offset, "length": length, "type": ctype, "value": value,
+              "syncing": int(syncing)}
         self.ops.append((chunk, io))
         self.payloads.append(payload)
         if chunk < self.nchunks:
             res, self.meta[chunk] = orc.replica_update(self.meta[chunk], self.host[chunk], self.chunk_size, io,
                                                        payload)
         else:
-            res = {"status": 3, "size": 0, "type": 0, "value": 0}
+            res = {"status": 3, "size": 0, "type": 0, "value": 0, "ucase": 0}
         self.expect.append(res)
         return res
 
-    def run(self):
-        torch, h3c = self.torch, self.h3c
-        # payloads packed at odd offsets so payload and chunk alignments differ
+    def expected_counters(self):
+        want = dict.fromkeys(("none", "reuse", "combine", "read_chunk", "recalculate", "checksum_mismatch",
+                              "invalid", "stale_chunks"), 0)
+        names = {orc.CASE_NONE: "none", orc.CASE_REUSE: "reuse", orc.CASE_COMBINE: "combine",
+                 orc.CASE_READ_CHUNK: "read_chunk"}
+        for e in self.expect:
+            if e["status"] == 3:
+                want["invalid"] += 1
+            elif e["status"] == 4080:
+                want["checksum_mismatch"] += 1
+            elif e["ucase"] in names:
+                want[names[e["ucase"]]] += 1
+        return want
+
+    def device_ios(self, type_=None):
+        """(chunks, ios) arrays for the engine; payloads packed at odd offsets so payload and
+        chunk alignments differ."""
+        h3c = self.h3c
         offs, total = [], 0
         for p in self.payloads:
             total += int(self.rng.integers(0, 17))
@@ -77,20 +102,26 @@ class Scenario:
         for o, p in zip(offs, self.payloads):
             if p is not None:
                 pay[o:o + len(p)] = p
-        dpay = torch.from_numpy(pay).to(self.dev)
+        self._dpay = self.torch.from_numpy(pay).to(self.dev)
         chunks = np.zeros(self.nchunks, dtype=h3c.CHUNK_STATE_DTYPE)
         for c, m in enumerate(self.init_meta):
             chunks[c] = (self.slab.data_ptr() + c * self.chunk_size, self.chunk_size, m["size"], m["value"], m["type"],
                          0)
         ios = np.zeros(len(self.ops), dtype=h3c.UPDATE_IO_DTYPE)
         for i, ((c, io), o, p) in enumerate(zip(self.ops, offs, self.payloads)):
-            ios[i] = (dpay.data_ptr() + o if p is not None else 0, c, io["offset"], io["length"], io["value"],
-                      io["type"], io["kind"], 0)
-        res = h3c.update_ios(chunks, ios)
-        torch.cuda.synchronize()
+            ios[i] = (self._dpay.data_ptr() + o if p is not None else 0, c, io["offset"], io["length"], io["value"],
+                      io["type"], io["kind"], h3c.IO_SYNCING if io.get("syncing") else 0, 0)
+        return chunks, ios
+
+    def run(self, exact=False, type_=None):
+        chunks, ios = self.device_ios()
+        self.counters = self.h3c.UpdateCounters()
+        kw = {} if type_ is None else {"type_": type_}
+        res = self.h3c.update_ios(chunks, ios, exact=exact, counters=self.counters, **kw)
+        self.torch.cuda.synchronize()
         return chunks, res
 
-    def check(self, chunks, res):
+    def check(self, chunks, res, counters=True):
         bad = []
         for i, (r, e) in enumerate(zip(res, self.expect)):
             got = (int(r["status"]), int(r["size"]), int(r["type"]), int(r["value"]))
@@ -103,6 +134,11 @@ class Scenario:
             assert (int(chunks[c]["size"]), int(chunks[c]["type"]), int(chunks[c]["value"])) == \
                 (m["size"], m["type"], m["value"] & MASK), c
             assert np.array_equal(dev_bytes[c, :m["size"]], self.host[c, :m["size"]]), f"chunk {c} bytes"
+        if counters:
+            got = self.counters.as_dict()
+            want = self.expected_counters()
+            got["stale_chunks"] = want["stale_chunks"] = 0  # checked by the exact-mode tests
+            assert got == want, (got, want)
 
 
 def random_scenario(h3c, torch, dev, rng, nchunks, chunk_size, nops, align=1, hot=None):
@@ -274,7 +310,7 @@ def test_updio_std_domain_rust_engine(h3c, torch_dev):
     dpay = torch.from_numpy(pay).to(dev)
     ios = np.zeros(len(ops), dtype=h3c.UPDATE_IO_DTYPE)
     for i, ((c, kind, off, ln, val, ty), po, p) in enumerate(zip(ops, offs, pays)):
-        ios[i] = (dpay.data_ptr() + po if p is not None else 0, c, off, ln, val, ty, kind, 0)
+        ios[i] = (dpay.data_ptr() + po if p is not None else 0, c, off, ln, val, ty, kind, 0, 0)
     res = h3c.update_ios(chunks, ios, std_domain=True)
     for i, (r, (st, sz, v)) in enumerate(zip(res, want)):
         assert int(r["status"]) == st and int(r["size"]) == sz, (i, r, st, sz)
@@ -311,7 +347,7 @@ def test_updio_reference_write_patterns_golden(h3c, torch_dev):
                 op = t["ops"][k]
                 p = orc.splitmix_bytes(op["length"], op["seed"], op["widx"])
                 pays.append(torch.from_numpy(p).to(dev))
-                ops.append((pays[-1].data_ptr(), c, op["offset"], op["length"], op["write_crc32c"], 1, h3c.UPD_WRITE, 0))
+                ops.append((pays[-1].data_ptr(), c, op["offset"], op["length"], op["write_crc32c"], 1, h3c.UPD_WRITE, 0, 0))
                 want.append((op["chunk_size_after"], op["chunk_crc32c"]))
     ios = np.zeros(len(ops), dtype=h3c.UPDATE_IO_DTYPE)
     for i, o in enumerate(ops):
@@ -340,25 +376,7 @@ def test_updio_crc32_ieee_polynomial(h3c, torch_dev):
             sc.add(orc.UPD_EXTEND, c, 0, int(rng.integers(0, cs + 1)), orc.NONE)
     torch_, h = sc.torch, sc.h3c
     # run with the CRC32 polynomial
-    offs, total = [], 0
-    for p in sc.payloads:
-        offs.append(total)
-        total += 0 if p is None else len(p)
-    pay = np.zeros(max(total, 1), dtype=np.uint8)
-    for o, p in zip(offs, sc.payloads):
-        if p is not None:
-            pay[o:o + len(p)] = p
-    dpay = torch_.from_numpy(pay).to(dev)
-    chunks = np.zeros(3, dtype=h.CHUNK_STATE_DTYPE)
-    for c, m in enumerate(sc.init_meta):
-        chunks[c] = (sc.slab.data_ptr() + c * cs, cs, m["size"], m["value"], m["type"], 0)
-    ios = np.zeros(len(sc.ops), dtype=h.UPDATE_IO_DTYPE)
-    for i, ((c, io), o, p) in enumerate(zip(sc.ops, offs, sc.payloads)):
-        ios[i] = (dpay.data_ptr() + o if p is not None else 0, c, io["offset"], io["length"], io["value"], io["type"],
-                  io["kind"], 0)
-    res = h.update_ios(chunks, ios, type_=h.ChecksumType.CRC32)
-    torch_.cuda.synchronize()
-    sc.check(chunks, res)
+    sc.check(*sc.run(type_=h.ChecksumType.CRC32))
 
 
 def test_updio_truncate_of_other_polynomial_chunk_is_rejected(h3c, torch_dev):
@@ -369,8 +387,289 @@ def test_updio_truncate_of_other_polynomial_chunk_is_rejected(h3c, torch_dev):
     chunks = np.zeros(1, dtype=h3c.CHUNK_STATE_DTYPE)
     chunks[0] = (slab.data_ptr(), 4096, 100, orc.crc32(np.zeros(100, dtype=np.uint8)), 2, 0)  # stored CRC32
     ios = np.zeros(2, dtype=h3c.UPDATE_IO_DTYPE)
-    ios[0] = (0, 0, 0, 50, 0, 0, h3c.UPD_TRUNCATE, 0)
-    ios[1] = (0, 0, 0, 200, 0, 0, h3c.UPD_EXTEND, 0)
+    ios[0] = (0, 0, 0, 50, 0, 0, h3c.UPD_TRUNCATE, 0, 0)
+    ios[1] = (0, 0, 0, 200, 0, 0, h3c.UPD_EXTEND, 0, 0)
     res = h3c.update_ios(chunks, ios)  # batch polynomial CRC32C
     assert list(res["status"]) == [3, 3]
     assert int(chunks[0]["size"]) == 100 and int(chunks[0]["type"]) == 2
+
+
+def test_updio_remove_commit_and_syncing(h3c, torch_dev):
+    """REMOVE (case (i): {NONE, 0}, size kept), COMMIT (no checksum effect, result {NONE, 0}) and
+    the resync successor's syncing full-chunk replace (size := length, reuse) pass through one
+    batch mixed with ordinary writes, as an UpdateWorker queue would hold them."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(31)
+    cs = 48 << 10
+    sc = Scenario(h3c, torch, dev, 6, cs, rng, init="crc")
+    for _ in range(300):
+        c = int(rng.integers(0, 6))
+        size = sc.meta[c]["size"]
+        u = rng.random()
+        if u < 0.45:
+            off = int(rng.integers(0, cs))
+            sc.add(orc.UPD_WRITE, c, off, int(rng.integers(0, min(cs - off, 6000) + 1)))
+        elif u < 0.55:
+            if size < cs:
+                sc.add(orc.UPD_WRITE, c, size, int(rng.integers(1, min(cs - size, 5000) + 1)))
+        elif u < 0.65:  # resync full-chunk replace, shorter or longer than the chunk
+            sc.add(orc.UPD_WRITE, c, 0, int(rng.integers(0, cs + 1)), syncing=True)
+        elif u < 0.72:
+            sc.add(orc.UPD_REMOVE, c, 0, 0, orc.NONE)
+        elif u < 0.80:
+            sc.add(orc.UPD_COMMIT, c, 0, 0, orc.NONE)
+        elif u < 0.90:
+            sc.add(orc.UPD_TRUNCATE, c, size if rng.random() < 0.3 else 0, int(rng.integers(0, cs + 1)), orc.NONE)
+        else:
+            sc.add(orc.UPD_EXTEND, c, size if rng.random() < 0.3 else 0, int(rng.integers(0, cs + 1)), orc.NONE)
+    sc.check(*sc.run())
+    got = sc.counters.as_dict()
+    assert got["none"] > 0 and got["reuse"] > 0 and got["combine"] > 0 and got["read_chunk"] > 0
+
+
+def test_updio_rejects_malformed_remove_and_syncing(h3c, torch_dev):
+    """ABI preconditions: REMOVE must be doRemove's {offset 0, length 0, NONE}; a syncing op must
+    be a WRITE at offset 0 (ReliableForwarding.cc:203-207).  Others are kInvalidArg and change
+    nothing."""
+    torch, dev = torch_dev
+    slab = torch.zeros(8192, dtype=torch.uint8, device=dev)
+    chunks = np.zeros(1, dtype=h3c.CHUNK_STATE_DTYPE)
+    chunks[0] = (slab.data_ptr(), 8192, 100, orc.crc32c(np.zeros(100, dtype=np.uint8)), 1, 0)
+    pay = torch.zeros(16, dtype=torch.uint8, device=dev)
+    ios = np.zeros(3, dtype=h3c.UPDATE_IO_DTYPE)
+    ios[0] = (0, 0, 0, 5, 0, 0, h3c.UPD_REMOVE, 0, 0)
+    ios[1] = (pay.data_ptr(), 0, 8, 8, 0, 0, h3c.UPD_WRITE, h3c.IO_SYNCING, 0)
+    ios[2] = (0, 0, 0, 50, 0, 0, h3c.UPD_TRUNCATE, h3c.IO_SYNCING, 0)
+    cnt = h3c.UpdateCounters()
+    res = h3c.update_ios(chunks, ios, counters=cnt)
+    assert list(res["status"]) == [3, 3, 3] and cnt.invalid == 3
+    assert int(chunks[0]["size"]) == 100
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_updio_exact_mode_with_stale_stored_checksums(h3c, torch_dev, seed):
+    """H3C_UPD_EXACT on chunks whose stored checksum disagrees with their bytes: every op's result
+    equals the reference's literal replay (ChunkReplica.cc:319-394: appends carry the stale value,
+    case (iv) re-reads the bytes, a TRUNCATE at offset == size keeps it), and stale_chunks counts
+    the disagreeing chunks."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(seed)
+    cs = 64 << 10
+    sc = Scenario(h3c, torch, dev, 10, cs, rng, init="crc", stale=0.6)
+    for _ in range(400):
+        c = int(rng.integers(0, 10))
+        size = sc.meta[c]["size"]
+        u = rng.random()
+        if u < 0.35 and size < cs:  # appends: combine with the stored value
+            sc.add(orc.UPD_WRITE, c, size, int(rng.integers(0, min(cs - size, 3000) + 1)))
+        elif u < 0.6:
+            off = int(rng.integers(0, cs))
+            sc.add(orc.UPD_WRITE, c, off, int(rng.integers(0, min(cs - off, 5000) + 1)))
+        elif u < 0.75:  # at offset == size: the stale value survives the size change
+            sc.add(orc.UPD_TRUNCATE if rng.random() < 0.5 else orc.UPD_EXTEND, c, size,
+                   int(rng.integers(0, cs + 1)), orc.NONE)
+        elif u < 0.85:
+            sc.add(orc.UPD_TRUNCATE, c, 0, int(rng.integers(0, cs + 1)), orc.NONE)
+        else:
+            sc.add(orc.UPD_WRITE, c, 0, int(rng.integers(1, cs + 1)))
+    chunks, res = sc.run(exact=True)
+    sc.check(chunks, res)
+    assert sc.stale_chunks > 0 and sc.counters.stale_chunks == sc.stale_chunks
+
+
+def _xinv8(poly):
+    L = orc.lib()
+    xinv = (((poly ^ 0x80000000) << 1) | 1) & MASK
+    r = 0x80000000
+    for _ in range(8):
+        r = L.orc_gf_mul(r, xinv, poly)
+    return r
+
+
+def _xpow8s(n, poly=orc.POLY_CRC32C):
+    """x^(8n) for a signed n (the inverse shift for n < 0)."""
+    L = orc.lib()
+    if n >= 0:
+        return L.orc_xpow8n(n, poly)
+    base, r, e = _xinv8(poly), 0x80000000, -n
+    while e:
+        if e & 1:
+            r = L.orc_gf_mul(r, base, poly)
+        base = L.orc_gf_mul(base, base, poly)
+        e >>= 1
+    return r
+
+
+def test_updio_trusted_mode_divergence_is_the_propagated_stale_error(h3c, torch_dev):
+    """The default (trusted) mode takes a stored checksum as the CRC of the bytes.  On a chunk
+    whose stored value is off by e0, its results differ from the reference's by exactly e0 carried
+    through the chunk's content CRC: shifted with every size change (x^(8(n'-n))), dropped by a
+    full overwrite, and passed into the stored value wherever the reference re-reads bytes
+    (reuse / case iv).  This pins the documented divergence op by op."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(43)
+    cs = 32 << 10
+    sc = Scenario(h3c, torch, dev, 8, cs, rng, init="crc", stale=1.0)
+    err = {c: sc.init_meta[c]["value"] ^ orc.crc32c(sc.host[c, :sc.init_meta[c]["size"]]) for c in range(8)}
+    for _ in range(250):
+        c = int(rng.integers(0, 8))
+        size = sc.meta[c]["size"]
+        u = rng.random()
+        if u < 0.3 and size < cs:
+            sc.add(orc.UPD_WRITE, c, size, int(rng.integers(1, min(cs - size, 2000) + 1)))
+        elif u < 0.7:
+            off = int(rng.integers(0, cs))
+            sc.add(orc.UPD_WRITE, c, off, int(rng.integers(0, min(cs - off, 3000) + 1)))
+        elif u < 0.8:
+            sc.add(orc.UPD_WRITE, c, 0, int(rng.integers(1, cs + 1)))
+        else:
+            sc.add(orc.UPD_TRUNCATE, c, size if rng.random() < 0.4 else 0, int(rng.integers(0, cs + 1)), orc.NONE)
+    chunks, res = sc.run(exact=False)
+    L = orc.lib()
+    P = orc.POLY_CRC32C
+    dt = dict(err)                 # error in the content CRC (trusted t = true t ^ dt)
+    ds = {c: 0 for c in range(8)}  # error in the stored value
+    size = {c: sc.init_meta[c]["size"] for c in range(8)}
+    for k, ((c, io), e) in enumerate(zip(sc.ops, sc.expect)):
+        if e["status"] == 0:
+            nb, na = size[c], e["size"]
+            full = io["kind"] == orc.UPD_WRITE and io["offset"] == 0 and io["length"] >= nb
+            dt[c] = 0 if full else L.orc_gf_mul(dt[c], _xpow8s(na - nb), P)
+            if e["ucase"] == orc.CASE_NONE:
+                ds[c] = 0
+            elif e["ucase"] in (orc.CASE_REUSE, orc.CASE_READ_CHUNK):
+                ds[c] = dt[c]
+            elif io["kind"] == orc.UPD_WRITE:  # append: combine carries the stored error
+                ds[c] = L.orc_gf_mul(ds[c], _xpow8s(na - nb), P)
+            size[c] = na
+        want = (e["value"] ^ ds[c]) & MASK if e["status"] in (0, 4080) else e["value"]
+        assert int(res[k]["value"]) == want, (k, io, e)
+        assert int(res[k]["status"]) == e["status"] and int(res[k]["size"]) == e["size"]
+    for c in range(8):
+        assert int(chunks[c]["value"]) == (sc.meta[c]["value"] ^ ds[c]) & MASK
+
+
+def _engine_replay(rng, h3c, torch, dev, nchunks, cs, nops, stale=0.0, exact=False):
+    """Random ops through the Rust chunk-engine restatement (std domain) and through
+    h3c_update_ios(H3C_UPD_STD_DOMAIN); payload device addresses are fixed first, so the
+    restatement sees the same is_aligned_buf (aligned.rs:47-49) as the engine."""
+    host = np.zeros((nchunks, cs), dtype=np.uint8)
+    meta, n_stale = [], 0
+    for c in range(nchunks):
+        size = [0, int(rng.integers(1, cs + 1)), 4096 * int(rng.integers(1, cs // 4096 + 1))][c % 3]
+        host[c, :size] = rng.integers(0, 256, size, dtype=np.uint8)
+        std = (~orc.crc32c(host[c, :size])) & MASK
+        if stale and size and rng.random() < stale:
+            std ^= int(rng.integers(1, 1 << 32))
+            n_stale += 1
+        meta.append({"size": size, "type": orc.CRC32C, "value": std})
+    slab = torch.from_numpy(host.copy()).to(dev)
+    ops, pays = [], []
+    for _ in range(nops):
+        c = int(rng.integers(0, nchunks))
+        u = rng.random()
+        if u < 0.65:
+            off = int(rng.integers(0, cs))
+            if rng.random() < 0.5:
+                off -= off % 4096
+            ln = int(rng.integers(0, min(cs - off, 9000) + 1))
+            if rng.random() < 0.4:
+                ln -= ln % 4096
+            p = rng.integers(0, 256, ln, dtype=np.uint8)
+            good = rng.random() > 0.05
+            ops.append({"kind": orc.UPD_WRITE, "offset": off, "length": ln, "type": orc.CRC32C,
+                        "value": orc.crc32c(p) ^ (0 if good else 1), "syncing": int(rng.random() < 0.05 and off == 0)})
+            pays.append(p)
+        else:
+            kind = [orc.UPD_TRUNCATE, orc.UPD_EXTEND, orc.UPD_REMOVE, orc.UPD_COMMIT][int(rng.integers(0, 4))]
+            ln = 4096 * int(rng.integers(0, cs // 4096 + 1)) if rng.random() < 0.5 else int(rng.integers(0, cs + 1))
+            if kind in (orc.UPD_REMOVE, orc.UPD_COMMIT):
+                ln = 0
+            ops.append({"kind": kind, "offset": 0, "length": ln, "type": 0, "value": 0})
+            pays.append(None)
+        ops[-1]["chunk"] = c
+    # payloads: half of them 4 KiB-aligned in HBM, the rest at odd offsets
+    offs, total = [], 0
+    for p in pays:
+        total = (total + 4095) // 4096 * 4096 if rng.random() < 0.5 else total + int(rng.integers(1, 17))
+        offs.append(total)
+        total += 0 if p is None else len(p)
+    buf = np.zeros(max(total, 1), dtype=np.uint8)
+    for o, p in zip(offs, pays):
+        if p is not None:
+            buf[o:o + len(p)] = p
+    dpay = torch.empty(total + 8192, dtype=torch.uint8, device=dev)
+    base = (dpay.data_ptr() + 4095) // 4096 * 4096
+    skew = base - dpay.data_ptr()
+    dpay[skew: skew + buf.size] = torch.from_numpy(buf).to(dev)
+    cnt = orc.EngineCounters()
+    want = []
+    m = [dict(x) for x in meta]
+    for io, o, p in zip(ops, offs, pays):
+        c = io["chunk"]
+        r, m[c] = orc.engine_update(m[c], host[c], cs, io, p, payload_aligned=(base + o) % 4096 == 0, counters=cnt)
+        want.append(r)
+    chunks = np.zeros(nchunks, dtype=h3c.CHUNK_STATE_DTYPE)
+    for c, x in enumerate(meta):
+        chunks[c] = (slab.data_ptr() + c * cs, cs, x["size"], x["value"], x["type"], 0)
+    ios = np.zeros(len(ops), dtype=h3c.UPDATE_IO_DTYPE)
+    for i, (io, o, p) in enumerate(zip(ops, offs, pays)):
+        # the std-domain ABI takes the engine's req.checksum (std); the restatement models the C++
+        # bridge, which passes ~raw (ChunkEngine.cc:41-42)
+        ck = (~io["value"]) & MASK if io["type"] == orc.CRC32C else io["value"]
+        ios[i] = (base + o if p is not None else 0, io["chunk"], io["offset"], io["length"], ck, io["type"],
+                  io["kind"], h3c.IO_SYNCING if io.get("syncing") else 0, 0)
+    counters = h3c.UpdateCounters()
+    res = h3c.update_ios(chunks, ios, std_domain=True, exact=exact, counters=counters)
+    torch.cuda.synchronize()
+    return dict(res=res, want=want, chunks=chunks, m=m, host=host, slab=slab, cnt=cnt, counters=counters,
+                n_stale=n_stale, ops=ops)
+
+
+@pytest.mark.parametrize("exact,stale", [(False, 0.0), (True, 0.0), (True, 0.7)])
+def test_updio_std_domain_matches_engine_restatement(h3c, torch_dev, exact, stale):
+    """H3C_UPD_STD_DOMAIN against the Rust chunk engine restatement (engine.rs:288-429,
+    chunk.rs:89-281): per-op results (std values; {CRC32C, 0} after a checksum mismatch), final
+    chunks, bytes, and the checksum_{reuse,combine,recalculate} counters -- with stale stored
+    values in exact mode (appends and zero pads carry them, copy_on_write recalculates)."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(51 + int(exact) + int(stale * 10))
+    cs = 64 << 10
+    r = _engine_replay(rng, h3c, torch, dev, 9, cs, 350, stale=stale, exact=exact)
+    bad = []
+    for k, (g, w, io) in enumerate(zip(r["res"], r["want"], r["ops"])):
+        got = (int(g["status"]), int(g["size"]), int(g["type"]), int(g["value"]))
+        exp = (w["status"], w["size"], w["type"], (~w["value"]) & MASK if w["type"] else 0)
+        if got != exp:
+            bad.append((k, io, got, exp))
+    assert not bad, bad[:4]
+    dev_bytes = r["slab"].cpu().numpy()
+    for c, mm in enumerate(r["m"]):
+        assert (int(r["chunks"][c]["size"]), int(r["chunks"][c]["value"])) == (mm["size"], mm["value"]), c
+        assert np.array_equal(dev_bytes[c, :mm["size"]], r["host"][c, :mm["size"]])
+    got = r["counters"].as_dict()
+    assert (got["reuse"], got["combine"], got["recalculate"]) == (r["cnt"].reuse, r["cnt"].combine,
+                                                                 r["cnt"].recalculate)
+    if exact:
+        assert got["stale_chunks"] == r["n_stale"]
+
+
+def test_updio_fragment_guess_overflow_redo(h3c, torch_dev):
+    """Ops spanning many 4 KiB blocks (whole-chunk writes, long truncations and extensions):
+    more fragments than the engine's first guess of 2n + 1024, so the fragment stage is redone
+    once with the count known -- results must be identical to the reference's."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(61)
+    cs = 16 << 20
+    sc = Scenario(h3c, torch, dev, 3, cs, rng, init="crc")
+    for _ in range(12):
+        c = int(rng.integers(0, 3))
+        u = rng.random()
+        if u < 0.4:
+            off = int(rng.integers(0, 1 << 20))
+            sc.add(orc.UPD_WRITE, c, off, int(rng.integers(1 << 20, cs - off)))
+        elif u < 0.7:
+            sc.add(orc.UPD_TRUNCATE, c, 0, int(rng.integers(0, cs)), orc.NONE)
+        else:
+            sc.add(orc.UPD_EXTEND, c, 0, int(rng.integers(0, cs + 1)), orc.NONE)
+    sc.check(*sc.run())
