@@ -37,6 +37,7 @@ from .engine import (  # noqa: F401
     read_results,
     update_blocks,
     update_ios,
+    update_ios_dev,
     update_workspace_bytes,
     CHUNK_STATE_DTYPE,
     UPDATE_IO_DTYPE,
@@ -77,6 +78,7 @@ __all__ = [
     "read_results",
     "update_blocks",
     "update_ios",
+    "update_ios_dev",
     "update_workspace_bytes",
     "CHUNK_STATE_DTYPE",
     "UPDATE_IO_DTYPE",

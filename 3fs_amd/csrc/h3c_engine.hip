@@ -430,18 +430,33 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
   }
 }
 
-// Kernel A''': payload CRCs of a batch of UpdateIOs, without host-built descriptors (the
-// device-resident h3c_update_ios pipeline).  Piece k of op i is [4096 j, min(4096 (j+1), len))
-// of op i's payload, where pbase[i] <= k < pbase[i] + pieces(i) and j = k - pbase[i]; the
-// piece count lives in device memory (*d_total).  A group of 4 lanes owns a piece and walks
-// it in 64-byte rows like seg_quad_kernel<4,1>; the piece's init-0 CRC, moved to the end of
-// its payload (x^(8 (len - piece end))), is XORed into crc0_out[i], which the caller zeroes.
-__global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(const h3c_update_io *__restrict__ ios,
-                                                                const uint32_t *__restrict__ pbase, uint32_t n,
+// Kernel A''': CRCs of ranges listed in device memory, without host-built descriptors (the
+// device-resident h3c_update_ios pipeline: UpdateIO payloads, and chunks CRC'd before a batch).
+// Piece k of item i is [4096 j, min(4096 (j+1), len)) of item i's range, where pbase[i] <= k <
+// pbase[i] + pieces(i) and j = k - pbase[i]; the piece count lives in device memory (*d_total).
+// A group of 4 lanes owns a piece and walks it in 64-byte rows like seg_quad_kernel<4,1>; the
+// piece's init-0 CRC, moved to the end of its item (x^(8 (len - piece end))), is XORed into
+// crc0_out[i], which the caller zeroes.  Src::range(i, ptr, len) names item i's bytes.
+struct IoPayloadSrc {  // UpdateIO payloads
+  const h3c_update_io *ios;
+  __device__ void range(uint32_t i, uint64_t &ptr, uint32_t &len) const {
+    ptr = ios[i].payload;
+    len = ios[i].length;
+  }
+};
+struct ChunkBytesSrc {  // chunk contents [0, size)
+  const h3c_chunk_state *chunks;
+  __device__ void range(uint32_t i, uint64_t &ptr, uint32_t &len) const {
+    ptr = chunks[i].base;
+    len = chunks[i].size;
+  }
+};
+
+template <class Src>
+__global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(Src src, const uint32_t *__restrict__ pbase, uint32_t n,
                                                                 const uint32_t *__restrict__ d_total,
                                                                 const PolyConsts *__restrict__ pc,
-                                                                uint32_t *__restrict__ crc0_out,
-                                                                uint32_t *__restrict__ work) {
+                                                                uint32_t *__restrict__ crc0_out) {
   constexpr int G = 4, kLevels = 2, NG = 64 / G;
   constexpr uint64_t kQ = 16u * G;
   constexpr int kRed = (1 + kLevels) * 1024;
@@ -456,15 +471,21 @@ __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(const h3c_update
   const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
   const uint32_t poly = pc->poly;
   const LaneLut L = make_lut(lane);
-  // waves take steps of NG pieces from a shared counter (a static split left a third of the
-  // waves with one step more than the rest: a few steps per wave at 100k pieces)
+  // Each workgroup owns a contiguous range; its waves take steps of NG pieces from an LDS
+  // counter (a static split per wave left a third of the waves with one step more than the
+  // rest at a few steps per wave; one global counter serialised thousands of atomics).
+  __shared__ uint32_t wg_next;
+  const uint32_t wlo = (uint32_t)((uint64_t)blockIdx.x * total / gridDim.x);
+  const uint32_t whi = (uint32_t)((uint64_t)(blockIdx.x + 1) * total / gridDim.x);
+  if (threadIdx.x == 0) wg_next = wlo;
+  __syncthreads();
   for (;;) {
     uint32_t q0 = 0;
-    if (lane == 0) q0 = atomicAdd(work, (uint32_t)NG);
+    if (lane == 0) q0 = atomicAdd(&wg_next, (uint32_t)NG);
     q0 = (uint32_t)__builtin_amdgcn_readfirstlane(q0);
-    if (q0 >= total) break;
+    if (q0 >= whi) break;
     const uint32_t k = q0 + grp;
-    const bool valid = k < total;
+    const bool valid = k < whi;
     uint64_t S = 0, E = 0;
     uint32_t op = 0, shift = 0;
     if (valid) {  // op i: the last with pbase[i] <= k (pieces of ops with none are skipped over)
@@ -475,11 +496,13 @@ __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(const h3c_update
       }
       op = a;
       const uint32_t j = k - pbase[a];
-      const h3c_update_io &io = ios[a];
-      const uint32_t off = j * 4096u, plen = min(4096u, io.length - off);
-      S = io.payload + off;
+      uint64_t base;
+      uint32_t length;
+      src.range(a, base, length);
+      const uint32_t off = j * 4096u, plen = min(4096u, length - off);
+      S = base + off;
       E = S + plen;
-      shift = io.length - off - plen;
+      shift = length - off - plen;
     }
     const uint64_t base = S & ~(kQ - 1);
     const uint64_t la = base + 16u * gl;
@@ -883,11 +906,21 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
 }
 
 int launch_op_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, const uint32_t *pbase, uint32_t n,
-                        const uint32_t *d_total, uint32_t *crc0_out, uint32_t *work) {
+                        const uint32_t *d_total, uint32_t *crc0_out) {
   const DeviceCtx &ctx = g_dev[dev];
   const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
-  hipLaunchKernelGGL(op_piece_crc_kernel, dim3(std::max(ctx.num_cu, 1)), dim3(kThreads), 0, st, ios, pbase, n,
-                     d_total, pc, crc0_out, work);
+  hipLaunchKernelGGL(op_piece_crc_kernel<IoPayloadSrc>, dim3(std::max(ctx.num_cu, 1)), dim3(kThreads), 0, st,
+                     IoPayloadSrc{ios}, pbase, n, d_total, pc, crc0_out);
+  HIP_TRY(hipGetLastError());
+  return H3C_OK;
+}
+
+int launch_chunk_piece_crc(hipStream_t st, int dev, int type, const h3c_chunk_state *chunks, const uint32_t *pbase,
+                           uint32_t n, const uint32_t *d_total, uint32_t *crc0_out) {
+  const DeviceCtx &ctx = g_dev[dev];
+  const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
+  hipLaunchKernelGGL(op_piece_crc_kernel<ChunkBytesSrc>, dim3(std::max(ctx.num_cu, 1)), dim3(kThreads), 0, st,
+                     ChunkBytesSrc{chunks}, pbase, n, d_total, pc, crc0_out);
   HIP_TRY(hipGetLastError());
   return H3C_OK;
 }

@@ -46,8 +46,6 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_scan_by_key.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "h3c_common.hpp"
 
@@ -67,7 +65,7 @@ enum : uint8_t { kC_NONE_ = 0, kC_NONE = 1, kC_REUSE = 2, kC_COMBINE = 3, kC_REA
 // device counter slots (h3c_update_counters order)
 enum { kCtrNone, kCtrReuse, kCtrCombine, kCtrRead, kCtrRecalc, kCtrMismatch, kCtrInvalid, kCtrStale, kCtrN };
 // device scalars: the payload kernel's work counter, the chain-head counter
-enum { kMiscPieceWork, kMiscHeads, kMiscN = 4 };
+enum { kMiscPieceWork, kMiscN = 4 };  // [2]: the fragment count read back
 
 // ---------------------------------------------------------------- scan elements
 
@@ -148,7 +146,7 @@ struct FragDesc {
   uint32_t pad[4];
 };
 static_assert(sizeof(FragDesc) == 64, "FragDesc is one 64-byte record");
-constexpr uint32_t kFragCrc = 1u, kFragWrite = 2u;
+constexpr uint32_t kFragCrc = 1u, kFragWrite = 2u, kFragHead = 4u;
 
 // counters: a workgroup-aggregated add -- wave sums into LDS, one global atomic per counter
 // and workgroup (call from workgroup-uniform control flow; `sh` holds kCtrN slots)
@@ -197,6 +195,12 @@ __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t 
     const h3c_chunk_state cs = chunks[c];
     const bool syncing = (io.flags & H3C_IO_SYNCING) != 0;
     if (!cs.base || (io.checksum_type != H3C_TYPE_NONE && io.checksum_type != poly_type)) st = H3C_ERR_INVALID_ARG;
+    if (cs.size > cs.chunk_size) st = H3C_ERR_INVALID_ARG;  // a corrupt chunk state
+    // documented limit: a TRUNCATE / EXTEND of a chunk stored (at the start of the batch) under the
+    // other polynomial -- its stored type would be kept (:328-332), and this batch CRCs in its own
+    if (!std_domain && (io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND) && cs.type != H3C_TYPE_NONE &&
+        cs.type != poly_type)
+      st = H3C_ERR_INVALID_ARG;
     if (io.kind == H3C_UPD_REMOVE) {  // doRemove's form (StorageOperator.cc:808-815); no range check (:141)
       if (io.offset || io.length || io.checksum_type != H3C_TYPE_NONE || syncing) st = H3C_ERR_INVALID_ARG;
     } else {
@@ -219,29 +223,32 @@ __device__ __forceinline__ bool applied_kind(uint8_t kind) {
   return kind == H3C_UPD_WRITE || kind == H3C_UPD_TRUNCATE || kind == H3C_UPD_EXTEND || kind == H3C_UPD_REMOVE;
 }
 
-// A6 (:193-207, engine.rs:297-312), the payload's raw CRC against the client's checksum, and
-// the size / type map of each op, in sorted order.
+// A6 (:193-207, engine.rs:297-312): the payload's raw CRC against the client's checksum.
+__global__ void uio_verify_kernel(const h3c_update_io *__restrict__ ios, uint32_t n, const uint32_t *__restrict__ paycrc0,
+                                  const PolyConsts *__restrict__ pc, uint32_t std_domain, uint32_t *__restrict__ status,
+                                  uint32_t *__restrict__ payraw) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const h3c_update_io io = ios[i];
+  if (io.kind != H3C_UPD_WRITE || status[i] != H3C_OK) return;
+  const uint32_t poly = pc->poly;
+  const uint32_t raw = io.length ? paycrc0[i] ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(io.length, pc, poly), poly)
+                                 : 0xFFFFFFFFu;
+  payraw[i] = raw;
+  if (io.checksum_type != H3C_TYPE_NONE && io.length && (std_domain ? ~raw : raw) != io.checksum_value)
+    status[i] = H3C_ERR_CHECKSUM_MISMATCH;
+}
+
+// The size / type map of each op, in sorted order.
 __global__ void uio_sz_elem_kernel(const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ order, uint32_t n,
-                                   uint32_t *__restrict__ status, const uint32_t *__restrict__ paycrc0,
-                                   const PolyConsts *__restrict__ pc, uint8_t poly_type, uint32_t std_domain,
-                                   uint32_t *__restrict__ payraw, SzTy *__restrict__ el) {
+                                   const uint32_t *__restrict__ status, uint8_t poly_type, uint32_t std_domain,
+                                   SzTy *__restrict__ el) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   const uint32_t i = order[p];
   const h3c_update_io io = ios[i];
-  uint32_t st = status[i];
-  if (io.kind == H3C_UPD_WRITE && st == H3C_OK) {
-    const uint32_t poly = pc->poly;
-    const uint32_t raw = io.length ? paycrc0[i] ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(io.length, pc, poly), poly)
-                                   : 0xFFFFFFFFu;
-    payraw[i] = raw;
-    if (io.checksum_type != H3C_TYPE_NONE && io.length && (std_domain ? ~raw : raw) != io.checksum_value) {
-      st = H3C_ERR_CHECKSUM_MISMATCH;
-      status[i] = st;
-    }
-  }
   SzTy e{0, 0, 0, 0, 0};
-  if (st == H3C_OK && applied_kind(io.kind)) {
+  if (status[i] == H3C_OK && applied_kind(io.kind)) {
     switch (io.kind) {
       case H3C_UPD_WRITE:  // doRealWrite (:122-124); a syncing write sets meta.size = length (:289)
         if (io.flags & H3C_IO_SYNCING) {
@@ -281,16 +288,14 @@ __device__ __forceinline__ uint32_t blocks_of(uint64_t base, uint32_t r0, uint32
 
 // The reference's case analysis per op (ChunkReplica.cc:246, 319-394; engine.rs:375-423 and
 // chunk.rs:89-281 in the std domain), the maps' kinds, and the op's fragment range.
-// `reject_pass`: only mark TRUNCATE / EXTEND of chunks stored under the other polynomial
-// (the caller then rescans sizes).
 __global__ void uio_classify_kernel(const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ order,
                                     const uint32_t *__restrict__ skey, uint32_t n, const h3c_chunk_state *__restrict__ chunks,
-                                    uint32_t nchunks, const SzTy *__restrict__ scan, uint32_t *__restrict__ status,
-                                    uint8_t poly_type, uint32_t std_domain, uint32_t reject_pass, OpPos *__restrict__ pos,
+                                    uint32_t nchunks, const SzTy *__restrict__ scan, const uint32_t *__restrict__ status,
+                                    uint8_t poly_type, uint32_t std_domain, OpPos *__restrict__ pos,
                                     uint32_t *__restrict__ nfrag) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) {
-    if (p == n && !reject_pass) nfrag[n] = 0;
+    if (p == n) nfrag[n] = 0;
     return;
   }
   const uint32_t i = order[p], c = skey[p];
@@ -299,10 +304,8 @@ __global__ void uio_classify_kernel(const h3c_update_io *__restrict__ ios, const
   r.op = i;
   r.status = status[i];
   if (c >= nchunks) {  // names no chunk of the batch
-    if (!reject_pass) {
-      pos[p] = r;
-      nfrag[p] = 0;
-    }
+    pos[p] = r;
+    nfrag[p] = 0;
     return;
   }
   const h3c_chunk_state cs = chunks[c];
@@ -314,12 +317,6 @@ __global__ void uio_classify_kernel(const h3c_update_io *__restrict__ ios, const
   }
   const SzTy a = scan[p];
   const uint32_t na_scan = a.cst ? a.v : (cs.size > a.v ? cs.size : a.v);
-  if (reject_pass) {
-    if (r.status == H3C_OK && (io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND) && tb != H3C_TYPE_NONE &&
-        tb != poly_type)
-      status[i] = H3C_ERR_INVALID_ARG;  // documented limit: its stored type cannot be derived here
-    return;
-  }
   r.nb = nb;
   r.na = nb;
   r.tb = (uint8_t)tb;
@@ -557,24 +554,16 @@ __global__ void uio_resolve_kernel(const uint64_t *__restrict__ fkey, const uint
   prev[k] = p;
 }
 
-// next pointers, and the chain heads appended to `heads` (one atomic per wave; the order of
-// the chains is free: they touch disjoint blocks)
+// next pointers and chain-head flags (a fragment with no predecessor on its block starts a
+// chain; the block kernel walks the fragments and starts at the flagged ones)
 __global__ void uio_heads_kernel(const uint32_t *__restrict__ prev, const uint32_t *__restrict__ d_F, uint32_t cap,
-                                 FragDesc *__restrict__ frags, uint32_t *__restrict__ heads,
-                                 uint32_t *__restrict__ nheads) {
+                                 FragDesc *__restrict__ frags) {
   const uint32_t F = frag_count(d_F, cap);
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t p = k < F ? prev[k] : 0u;
-  const bool head = k < F && p == kNil;
-  if (k < F && !head) frags[p].next = k;
-  const uint64_t m = __ballot(head);
-  if (!m) return;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(nheads, (uint32_t)__builtin_popcountll(m));
-  base = (uint32_t)__shfl((int)base, (int)leader, 64);
-  if (head) heads[base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = k;
+  if (k >= F) return;
+  const uint32_t p = prev[k];
+  if (p != kNil) frags[p].next = k;
+  else frags[k].flags |= kFragHead;
 }
 
 // ---- the block kernel ----
@@ -712,14 +701,14 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
 
 // One wave per chain (a block's fragments in sequence order): the block is loaded once, each
 // fragment's delta CRC goes to its op's E, the new bytes are applied in order, and the rows
-// that changed are stored once.  Per group of 64 chains lane k loads chain k's first fragment
-// record (one vector load round trip instead of a chain of dependent scalar loads per
-// chain); the wave then walks the group with readlane, keeping the next chain's block and
-// payload rows in flight while the current one is folded and stored.  Chains longer than one
-// fragment (blocks written more than once in the batch) continue with uniform loads.
+// that changed are stored once.  Waves take contiguous fragment ranges; per group of 64 lane
+// k loads fragment g0 + k's record (one vector load round trip instead of a chain of
+// dependent scalar loads per chain) and the wave walks the group's chain heads with readlane,
+// keeping the next head's block and payload rows in flight while the current chain is folded
+// and stored.  Chains longer than one fragment (blocks written more than once in the batch)
+// continue with uniform loads.
 __global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__restrict__ frags,
-                                                             const uint32_t *__restrict__ heads,
-                                                             const uint32_t *__restrict__ d_ntasks,
+                                                             const uint32_t *__restrict__ d_F, uint32_t cap,
                                                              const PolyConsts *__restrict__ pc,
                                                              uint32_t *__restrict__ eacc) {
   __shared__ uint32_t lds[kLdsWords + kRedWords];
@@ -727,14 +716,14 @@ __global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__r
   const uint32_t *red_g = &pc->red[0][0][0];
   for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
   __syncthreads();
-  const uint32_t ntasks = *d_ntasks;
+  const uint32_t F = frag_count(d_F, cap);
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint32_t lo = (uint32_t)(gw * ntasks / nw), hi = (uint32_t)((gw + 1) * ntasks / nw);
+  const uint32_t lo = (uint32_t)(gw * F / nw), hi = (uint32_t)((gw + 1) * F / nw);
   if (lo >= hi) return;
   const uint32_t poly = pc->poly;
   const LaneLut L = make_lut(lane);
@@ -745,11 +734,11 @@ __global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__r
   };
   for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
     const uint32_t cnt = min(64u, hi - g0);
-    // lane k: chain g0 + k's first fragment
+    // lane k: fragment g0 + k
     uint64_t m_blk = 0, m_src = 0;
     uint32_t m_p = 0, m_next = kNil, m_w = 0, m_q = 0, m_z = 0, m_k = 0, m_mult = 0, m_flags = 0;
     if (lane < cnt) {
-      const FragDesc &d = frags[heads[g0 + lane]];
+      const FragDesc &d = frags[g0 + lane];
       m_blk = d.blk;
       m_src = d.src;
       m_p = d.p;
@@ -767,27 +756,32 @@ __global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__r
       load_task_rows(rl64(m_blk, 0), k & 0xFFFFu, k >> 16, rl64(m_src, 0), w & 0xFFFFu, w >> 16, lane, cur);
     }
     for (uint32_t t = 0; t < cnt; ++t) {
-      if (t + 1 < cnt) {  // the next chain's rows in flight while this one is processed
+      // the next fragment's rows in flight while this one is processed (a fragment that is
+      // not a chain head -- a later write to an already written block -- loads them in vain)
+      if (t + 1 < cnt) {
         const uint32_t k = rl(m_k, t + 1), w = rl(m_w, t + 1);
         load_task_rows(rl64(m_blk, t + 1), k & 0xFFFFu, k >> 16, rl64(m_src, t + 1), w & 0xFFFFu, w >> 16, lane, nxt);
       }
-      const uint64_t blk = rl64(m_blk, t);
-      const uint32_t kk = rl(m_k, t), k0 = kk & 0xFFFFu, k1 = kk >> 16;
-      uint32_t dirty = apply_fragment(cur.img, cur.nw, rl(m_flags, t), rl(m_w, t), rl(m_q, t), rl(m_z, t),
-                                      rl(m_mult, t), rl(m_p, t), lane, lb, L, red, poly, eacc);
-      for (uint32_t f = rl(m_next, t); f != kNil;) {  // later fragments of the same block
-        const FragDesc d = frags[f];
-        uint4 nw4[4];
+      const uint32_t flags = rl(m_flags, t);
+      if (flags & kFragHead) {
+        const uint64_t blk = rl64(m_blk, t);
+        const uint32_t kk = rl(m_k, t), k0 = kk & 0xFFFFu, k1 = kk >> 16;
+        uint32_t dirty = apply_fragment(cur.img, cur.nw, flags, rl(m_w, t), rl(m_q, t), rl(m_z, t), rl(m_mult, t),
+                                        rl(m_p, t), lane, lb, L, red, poly, eacc);
+        for (uint32_t f = rl(m_next, t); f != kNil;) {  // later fragments of the same block
+          const FragDesc d = frags[f];
+          uint4 nw4[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) nw4[r] = load_new(d.src, r, 1024u * r + 16u * lane, d.w0, d.w1);
-        dirty |= apply_fragment(cur.img, nw4, d.flags, (uint32_t)d.w0 | ((uint32_t)d.w1 << 16),
-                                (uint32_t)d.q0 | ((uint32_t)d.q1 << 16), (uint32_t)d.z0 | ((uint32_t)d.z1 << 16),
-                                d.mult, d.p, lane, lb, L, red, poly, eacc);
-        f = d.next;
+          for (int r = 0; r < 4; ++r) nw4[r] = load_new(d.src, r, 1024u * r + 16u * lane, d.w0, d.w1);
+          dirty |= apply_fragment(cur.img, nw4, d.flags, (uint32_t)d.w0 | ((uint32_t)d.w1 << 16),
+                                  (uint32_t)d.q0 | ((uint32_t)d.q1 << 16), (uint32_t)d.z0 | ((uint32_t)d.z1 << 16),
+                                  d.mult, d.p, lane, lb, L, red, poly, eacc);
+          f = d.next;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (dirty & (1u << r)) store_masked(blk, 1024u * r + 16u * lane, cur.img[r], k0, k1);
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (dirty & (1u << r)) store_masked(blk, 1024u * r + 16u * lane, cur.img[r], k0, k1);
       cur = nxt;
     }
   }
@@ -800,7 +794,7 @@ __device__ __forceinline__ Aff t_map(const OpPos &r, const uint32_t *__restrict_
   return Aff{kOne, 0u};
 }
 
-// The scans' inputs, computed as rocPRIM reads them (no element arrays).
+// t map per op position.
 struct TMapFn {
   const OpPos *pos;
   const uint32_t *eacc, *payraw;
@@ -808,7 +802,7 @@ struct TMapFn {
   __device__ Aff operator()(uint32_t p) const { return t_map(pos[p], eacc, payraw, p, pc); }
 };
 
-// s maps per op position, from each op's t after it (the chunk's t0 through the t scan).
+// s map per op position, from each op's t after it (the chunk's t0 through the t scan).
 struct SMapFn {
   const OpPos *pos;
   const uint32_t *skey;
@@ -834,6 +828,12 @@ struct SMapFn {
     }
   }
 };
+
+template <class Fn>
+__global__ void uio_elem_kernel(Fn fn, uint32_t n, Aff *__restrict__ out) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n) out[p] = fn(p);
+}
 
 // Per op result (IOResult.checksum, ChunkReplica.cc:174,311; ChunkEngine.cc:61-67), each chunk's
 // final state (its last op), and the counters.
@@ -890,6 +890,41 @@ __global__ void uio_result_kernel(const OpPos *__restrict__ pos, const uint32_t 
   ctr_add_block(sh, ctr, v);
 }
 
+// Chunks whose starting CRC t0 comes from their bytes (H3C_UPD_EXACT, or a stored checksum not
+// of this polynomial): their 4 KiB piece counts, and zeroed CRC accumulators.
+__device__ __forceinline__ bool needs_init(const h3c_chunk_state &cs, uint8_t poly_type, uint32_t exact) {
+  return cs.size && cs.size <= cs.chunk_size && (exact || cs.type != poly_type);
+}
+__global__ void uio_init_count_kernel(const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks, uint8_t poly_type,
+                                      uint32_t exact, uint32_t *__restrict__ npieces, uint32_t *__restrict__ crc0) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > nchunks) return;
+  if (c == nchunks) {
+    npieces[c] = 0;
+    return;
+  }
+  const h3c_chunk_state cs = chunks[c];
+  npieces[c] = needs_init(cs, poly_type, exact) ? (cs.size + kPieceBytes - 1) / kPieceBytes : 0u;
+  crc0[c] = 0;
+}
+// t0 per chunk: the raw CRC of no bytes, the trusted stored value, or the bytes' CRC.
+__global__ void uio_t0_kernel(const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks, uint8_t poly_type,
+                              uint32_t exact, uint32_t std_domain, const uint32_t *__restrict__ crc0,
+                              const PolyConsts *__restrict__ pc, uint32_t *__restrict__ t0v) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  const h3c_chunk_state cs = chunks[c];
+  uint32_t t0;
+  if (cs.size == 0 || cs.size > cs.chunk_size) {
+    t0 = 0xFFFFFFFFu;
+  } else if (needs_init(cs, poly_type, exact)) {
+    t0 = crc0[c] ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(cs.size, pc, pc->poly), pc->poly);
+  } else {
+    t0 = std_domain ? ~cs.value : cs.value;
+  }
+  t0v[c] = t0;
+}
+
 // H3C_UPD_EXACT: chunks whose stored checksum of the batch polynomial disagrees with the bytes.
 __global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks,
                                  const uint32_t *__restrict__ t0v, uint8_t poly_type, uint32_t std_domain,
@@ -903,6 +938,31 @@ __global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uin
   __shared__ unsigned int sh[8];
   const uint32_t v[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, stale};
   ctr_add_block(sh, ctr, v);
+}
+
+// A second stream per calling thread and device: the payload CRCs run on it while the main
+// stream sorts the ops (the sort does not depend on the A6 verdicts).
+struct AuxStream {
+  int dev = -1;
+  hipStream_t st = nullptr;
+  hipEvent_t ready = nullptr, done = nullptr;
+};
+int aux_stream(int dev, AuxStream *&out) {
+  thread_local AuxStream aux[4];
+  thread_local int next = 0;
+  for (AuxStream &a : aux)
+    if (a.dev == dev && a.st) {
+      out = &a;
+      return H3C_OK;
+    }
+  AuxStream &a = aux[next++ & 3];  // a thread using more than 4 devices recycles (leaks) the oldest
+  a = AuxStream{};
+  HIP_TRY(hipStreamCreateWithFlags(&a.st, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&a.ready, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
+  a.dev = dev;
+  out = &a;
+  return H3C_OK;
 }
 
 template <class T>
@@ -932,94 +992,49 @@ hipError_t sort_pairs(void *tmp, size_t &tmp_bytes, const uint32_t *k, uint32_t 
   return rocprim::radix_sort_pairs<SortMerge>(tmp, tmp_bytes, k, k2, v, v2, n, 0, bits, st);
 }
 
-}  // namespace
 
-extern "C" int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
-                                 uint32_t n, h3c_update_result *results, uint32_t flags, h3c_update_counters *counters,
-                                 void *stream) {
-  if (counters) std::memset(counters, 0, sizeof(*counters));
-  if (poly_type != H3C_TYPE_CRC32C && poly_type != H3C_TYPE_CRC32) return H3C_ERR_INVALID_ARG;
-  if ((n && (!ios || !results)) || (nchunks && !chunks) || n >= 0x7FFFFFFFu || nchunks >= (1u << 28))
-    return H3C_ERR_INVALID_ARG;
-  for (uint32_t c = 0; c < nchunks; ++c)  // a chunk longer than its capacity is a caller bug
-    if (chunks[c].size > chunks[c].chunk_size) {
-      h3c_rt::set_error_text("h3c_update_ios: a chunk's size exceeds its chunk_size");
-      return H3C_ERR_INVALID_ARG;
-    }
-  if (n == 0) return H3C_OK;
+
+// The pipeline on device arrays: chunks_in (read), chunks_out (final states; may not alias
+// chunks_in), ios, results, ctr (h3c_update_counters layout, 8 x u64).  `epilogue` enqueues the
+// caller's copies of the outputs before the final synchronisation.  Synchronous.
+template <class Epilogue>
+int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_state *d_chunks_out, uint32_t nchunks,
+                const h3c_update_io *d_ios, uint32_t n, h3c_update_result *d_res, uint32_t flags,
+                unsigned long long *d_ctr, hipStream_t st, int dev, Epilogue epilogue) {
   const bool std_domain = (flags & H3C_UPD_STD_DOMAIN) != 0;
   const bool exact = (flags & H3C_UPD_EXACT) != 0;
-  int dev = 0;
-  int rc = h3c_rt::current_device(&dev);
-  if (rc) return rc;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const PolyConsts *pc = static_cast<const PolyConsts *>(h3c_rt::device_consts(dev, poly_type));
   const uint32_t poly = poly_type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
-  const uint32_t stdf = std_domain ? 1u : 0u;
-
-  // ---- per-chunk host work (O(chunks)): trusted starting CRCs, the chunks to CRC first ----
+  const uint32_t stdf = std_domain ? 1u : 0u, exactf = exact ? 1u : 0u;
   const uint32_t C = std::max(nchunks, 1u);
-  size_t ninit = 0;
-  bool other_poly = false;
-  uint64_t init_bytes = 0;
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    const h3c_chunk_state &cs = chunks[c];
-    if (cs.type != H3C_TYPE_NONE && cs.type != poly_type) other_poly = true;
-    if (cs.size && (exact || cs.type != poly_type)) {
-      ++ninit;
-      init_bytes += cs.size;
-    }
-  }
-  const bool fused = std_domain || !other_poly;  // else: one extra pass for the other-polynomial limit
-  const uint64_t init_seg = h3c_rt::pick_seg(init_bytes, dev);
 
   // ---- device scratch: per op, per chunk, and per fragment for a guessed fragment count ----
   // (a fragment per 4 KiB block an op touches: one per block-aligned write of <= 4 KiB; the
-  // guess is the larger of 2n and the calling thread's last batch, and a batch that needs more
-  // redoes its fragment stage once with the count known)
+  // guess is the larger of 2n + 1024 and the calling thread's last batch, and a batch that
+  // needs more redoes its fragment stage once with the count known)
   thread_local uint32_t last_frags = 0;
   uint32_t cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * n + 1024, last_frags), 0x7FFFFFF0u);
-  size_t sort_tmp = 0, scan_tmp = 0, szscan_tmp = 0, ascan_tmp = 0;
+  size_t sort_tmp = 0, scan_tmp = 0, cscan_tmp = 0, szscan_tmp = 0, ascan_tmp = 0;
   const uint32_t bits = bits_for((uint64_t)nchunks + 1);
-  using CountIt = rocprim::counting_iterator<uint32_t>;
-  using TIt = rocprim::transform_iterator<CountIt, TMapFn, Aff>;
-  using SIt = rocprim::transform_iterator<CountIt, SMapFn, Aff>;
   HIP_TRY(sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, n, bits, st));
   HIP_TRY(rocprim::exclusive_scan(nullptr, scan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)n + 1,
                                   rocprim::plus<uint32_t>(), st));
+  HIP_TRY(rocprim::exclusive_scan(nullptr, cscan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)C + 1,
+                                  rocprim::plus<uint32_t>(), st));
   HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, szscan_tmp, (uint32_t *)nullptr, (SzTy *)nullptr, (SzTy *)nullptr,
                                          (size_t)n, SzTyOp(), rocprim::equal_to<uint32_t>(), st));
-  {
-    size_t a = 0, b = 0;
-    HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, a, (uint32_t *)nullptr, TIt(CountIt(0), TMapFn{}), (Aff *)nullptr,
-                                           (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
-    HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, b, (uint32_t *)nullptr, SIt(CountIt(0), SMapFn{}), (Aff *)nullptr,
-                                           (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
-    ascan_tmp = std::max(a, b);
-  }
+  HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, ascan_tmp, (uint32_t *)nullptr, (Aff *)nullptr, (Aff *)nullptr,
+                                         (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
   const size_t tmp_bytes = std::max(std::max(sort_tmp, scan_tmp), std::max(szscan_tmp, ascan_tmp));
   const size_t N1 = (size_t)n + 1;
-  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-  // upload block [chunks | t0 | INIT descriptors] and download block [final chunks | counters | misc]
-  const size_t up_t0 = al(sizeof(h3c_chunk_state) * C), up_init = up_t0 + al(4ull * C);
-  const size_t up_bytes = up_init + al(sizeof(DevChunk) * std::max<size_t>(ninit, 1));
-  const size_t dn_ctr = al(sizeof(h3c_chunk_state) * C), dn_misc = dn_ctr + al(8ull * kCtrN);
-  const size_t dn_bytes = dn_misc + al(4ull * kMiscN) + 256;
-  h3c_update_io *d_ios;
   uint32_t *d_status, *d_key, *d_idx, *d_skey, *d_order, *d_np, *d_pbase, *d_paycrc0, *d_payraw, *d_nfrag, *d_fbase,
-      *d_eacc, *d_initseg;
+      *d_eacc, *d_t0, *d_cnp, *d_cbase, *d_ccrc, *d_misc;
   SzTy *d_sz, *d_szscan;
   OpPos *d_pos;
-  Aff *d_tscan, *d_sscan;
-  h3c_update_result *d_res;
-  char *d_up, *d_dn;
-  void *d_tmp;
-  // one layout, run twice: with base 0 to size the lease, then on the lease
-  auto layout = [&](char *base) -> size_t {
-    char *c0 = base, *cur = base;
-    d_up = carve<char>(cur, up_bytes);
-    d_dn = carve<char>(cur, dn_bytes);
-    d_ios = carve<h3c_update_io>(cur, n);
+  Aff *d_tel, *d_tscan, *d_sel, *d_sscan;
+  void *d_tmp, *d_ctmp;
+  auto layout = [&](char *base) -> size_t {  // one layout, run with base 0 to size the lease
+    char *cur = base;
     d_status = carve<uint32_t>(cur, n);
     d_key = carve<uint32_t>(cur, n);
     d_idx = carve<uint32_t>(cur, n);
@@ -1032,98 +1047,82 @@ extern "C" int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uin
     d_nfrag = carve<uint32_t>(cur, N1);
     d_fbase = carve<uint32_t>(cur, N1);
     d_eacc = carve<uint32_t>(cur, n);
+    d_t0 = carve<uint32_t>(cur, C);
+    d_cnp = carve<uint32_t>(cur, (size_t)C + 1);
+    d_cbase = carve<uint32_t>(cur, (size_t)C + 1);
+    d_ccrc = carve<uint32_t>(cur, C);
+    d_misc = carve<uint32_t>(cur, kMiscN);
     d_sz = carve<SzTy>(cur, n);
     d_szscan = carve<SzTy>(cur, n);
     d_pos = carve<OpPos>(cur, n);
+    d_tel = carve<Aff>(cur, n);
     d_tscan = carve<Aff>(cur, n);
+    d_sel = carve<Aff>(cur, n);
     d_sscan = carve<Aff>(cur, n);
-    d_res = carve<h3c_update_result>(cur, n);
     d_tmp = carve<char>(cur, tmp_bytes);
-    d_initseg = carve<uint32_t>(cur, init_bytes / init_seg + ninit + 1);
-    return (size_t)(cur - c0);
+    d_ctmp = carve<char>(cur, cscan_tmp);  // the chunk scan runs on the second stream
+    return (size_t)(cur - base);
   };
-  const size_t bytes1 = layout(nullptr);
-  h3c_rt::DeviceLease lease1(dev, bytes1);
+  h3c_rt::DeviceLease lease1(dev, layout(nullptr));
   if (!lease1.ok()) return H3C_ERR_HIP;
-  h3c_rt::PinnedLease pin(up_bytes + dn_bytes);
-  if (!pin.ok()) return H3C_ERR_HIP;
   layout(lease1.data());
-  h3c_chunk_state *d_chunks = reinterpret_cast<h3c_chunk_state *>(d_up);
-  uint32_t *d_t0 = reinterpret_cast<uint32_t *>(d_up + up_t0);
-  DevChunk *d_init = reinterpret_cast<DevChunk *>(d_up + up_init);
-  h3c_chunk_state *d_chunks_out = reinterpret_cast<h3c_chunk_state *>(d_dn);
-  unsigned long long *d_ctr = reinterpret_cast<unsigned long long *>(d_dn + dn_ctr);
-  uint32_t *d_misc = reinterpret_cast<uint32_t *>(d_dn + dn_misc);
+  h3c_rt::PinnedLease pin(4096);
+  if (!pin.ok()) return H3C_ERR_HIP;
+  uint32_t *h_F = reinterpret_cast<uint32_t *>(pin.data());
+  AuxStream *aux = nullptr;
+  int rc = aux_stream(dev, aux);
+  if (rc) return rc;
 
-  // host staging of the upload block: the chunk table, trusted starting CRCs, INIT descriptors
-  char *hp = pin.data();
-  std::memcpy(hp, chunks, sizeof(h3c_chunk_state) * nchunks);
-  uint32_t *h_t0 = reinterpret_cast<uint32_t *>(hp + up_t0);
-  DevChunk *h_init = reinterpret_cast<DevChunk *>(hp + up_init);
-  uint32_t init_segs = 0, init_max = 0;
-  uint64_t init_maxlen = 0;
-  size_t k_init = 0;
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    const h3c_chunk_state &cs = chunks[c];
-    if (cs.size == 0) {
-      h_t0[c] = 0xFFFFFFFFu;  // raw CRC of no bytes
-    } else if (!exact && cs.type == poly_type) {
-      h_t0[c] = std_domain ? ~cs.value : cs.value;  // trusted
-    } else {  // from the bytes (launch_crc below writes t0[c])
-      h_t0[c] = 0;
-      DevChunk d{};
-      d.ptr = cs.base;
-      d.len = cs.size;
-      d.start = 0xFFFFFFFFu;
-      d.out_idx = c;
-      d.seg_begin = init_segs;
-      set_fold_consts(d, init_seg, poly);
-      const uint32_t ns = (uint32_t)((d.len + init_seg - 1) / init_seg);
-      init_segs += ns;
-      init_max = std::max(init_max, ns);
-      init_maxlen = std::max<uint64_t>(init_maxlen, d.len);
-      h_init[k_init++] = d;
-    }
-  }
-  char *hd = hp + up_bytes;  // download staging
-
-  StreamDrain drain{st, true};  // every return below waits for the stream before the leases go back
+  StreamDrain drain{st, true};  // every return below waits for both streams before the leases go back
+  StreamDrain drain_aux{aux->st, true};
   const uint32_t tb = 256, gb = (uint32_t)((n + tb) / tb);  // n + 1 threads (the scans' extra entry)
+  const uint32_t cb = (C + tb) / tb;
   auto scan_excl = [&](const uint32_t *in, uint32_t *out) -> hipError_t {
     size_t t = tmp_bytes;
     return rocprim::exclusive_scan(d_tmp, t, in, out, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), st);
   };
-  HIP_TRY(hipMemcpyAsync(d_up, hp, up_init + (ninit ? al(sizeof(DevChunk) * ninit) : 0), hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(d_ios, ios, sizeof(h3c_update_io) * n, hipMemcpyHostToDevice, st));
-  // the chunks whose starting CRC comes from their bytes, before any byte changes
-  if (ninit) {
-    rc = h3c_rt::launch_crc(st, dev, poly_type, d_init, (uint32_t)ninit, init_segs, init_max, init_bytes, init_seg, 0,
-                            d_initseg, nullptr, d_t0, nullptr, nullptr, -1,
-                            h3c_rt::small_rows_bound(init_maxlen, init_max));
-    if (rc) return rc;
-  }
   hipLaunchKernelGGL(uio_prep_kernel, dim3(gb), dim3(tb), 0, st, d_ios, n, d_chunks, nchunks, poly_type, stdf,
                      d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc);
   HIP_TRY(hipGetLastError());
   HIP_TRY(scan_excl(d_np, d_pbase));
-  rc = h3c_rt::launch_op_piece_crc(st, dev, poly_type, d_ios, d_pbase, n, d_pbase + n, d_paycrc0,
-                                   d_misc + kMiscPieceWork);
+  // second stream: chunks CRC'd from their bytes (t0), payload CRCs and A6; this stream sorts
+  // the ops meanwhile (the sort does not depend on either).  Joined before the sizes.
+  HIP_TRY(hipEventRecord(aux->ready, st));
+  HIP_TRY(hipStreamWaitEvent(aux->st, aux->ready, 0));
+  hipLaunchKernelGGL(uio_init_count_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf,
+                     d_cnp, d_ccrc);
+  HIP_TRY(hipGetLastError());
+  {
+    size_t t = cscan_tmp;
+    HIP_TRY(rocprim::exclusive_scan(d_ctmp, t, d_cnp, d_cbase, 0u, (size_t)nchunks + 1, rocprim::plus<uint32_t>(),
+                                    aux->st));
+  }
+  rc = h3c_rt::launch_chunk_piece_crc(aux->st, dev, poly_type, d_chunks, d_cbase, nchunks, d_cbase + nchunks, d_ccrc);
   if (rc) return rc;
+  hipLaunchKernelGGL(uio_t0_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf, stdf, d_ccrc,
+                     pc, d_t0);
+  HIP_TRY(hipGetLastError());
+  rc = h3c_rt::launch_op_piece_crc(aux->st, dev, poly_type, d_ios, d_pbase, n, d_pbase + n, d_paycrc0);
+  if (rc) return rc;
+  hipLaunchKernelGGL(uio_verify_kernel, dim3(gb), dim3(tb), 0, aux->st, d_ios, n, d_paycrc0, pc, stdf, d_status,
+                     d_payraw);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(aux->done, aux->st));
   {
     size_t t = tmp_bytes;
     HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, st));
   }
-  for (int pass = fused ? 1 : 0; pass < 2; ++pass) {  // pass 0: the other-polynomial rejections only
-    hipLaunchKernelGGL(uio_sz_elem_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, n, d_status, d_paycrc0, pc,
-                       poly_type, stdf, d_payraw, d_sz);
-    HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamWaitEvent(st, aux->done, 0));
+  hipLaunchKernelGGL(uio_sz_elem_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, n, d_status, poly_type, stdf, d_sz);
+  HIP_TRY(hipGetLastError());
+  {
     size_t t = tmp_bytes;
     HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_sz, d_szscan, (size_t)n, SzTyOp(),
                                            rocprim::equal_to<uint32_t>(), st));
-    hipLaunchKernelGGL(uio_classify_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, d_skey, n, d_chunks, nchunks,
-                       d_szscan, d_status, poly_type, stdf, pass == 0 ? 1u : 0u, d_pos, d_nfrag);
-    HIP_TRY(hipGetLastError());
   }
+  hipLaunchKernelGGL(uio_classify_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, d_skey, n, d_chunks, nchunks,
+                     d_szscan, d_status, poly_type, stdf, d_pos, d_nfrag);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(scan_excl(d_nfrag, d_fbase));
 
   // ---- fragments, blocks, scans, results (redone once if the fragment guess was short) ----
@@ -1132,14 +1131,13 @@ extern "C" int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uin
     while (hcap < cap) hcap <<= 1;
     FragDesc *d_frag;
     uint64_t *d_fkey;
-    uint32_t *d_prev, *d_gnext, *d_heads, *d_hhead;
+    uint32_t *d_prev, *d_gnext, *d_hhead;
     auto layout2 = [&](char *base) -> size_t {
       char *c2 = base;
       d_frag = carve<FragDesc>(c2, cap);
       d_fkey = carve<uint64_t>(c2, cap);
       d_prev = carve<uint32_t>(c2, cap);
       d_gnext = carve<uint32_t>(c2, cap);
-      d_heads = carve<uint32_t>(c2, cap);
       d_hhead = carve<uint32_t>(c2, hcap);
       return (size_t)(c2 - base);
     };
@@ -1149,10 +1147,7 @@ extern "C" int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uin
     layout2(lease2.data());
     const uint32_t *d_F = d_fbase + n;
     const uint32_t fb = (cap + tb - 1) / tb;
-    if (attempt) {  // the first attempt's chain count and counters
-      HIP_TRY(hipMemsetAsync(d_misc + kMiscHeads, 0, 4, st));
-      HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, st));
-    }
+    if (attempt) HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, st));  // the first attempt's counters
     hipLaunchKernelGGL(uio_frag_kernel, dim3((std::max(cap, hcap) + tb - 1) / tb), dim3(tb), 0, st, d_pos, d_fbase, n,
                        cap, d_ios, d_skey, d_chunks, d_frag, d_fkey, pc, d_hhead, hcap);
     HIP_TRY(hipGetLastError());
@@ -1162,70 +1157,163 @@ extern "C" int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uin
     hipLaunchKernelGGL(uio_resolve_kernel, dim3(fb), dim3(tb), 0, st, d_fkey, d_F, cap, d_hhead, hcap - 1, d_gnext,
                        d_prev);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(uio_heads_kernel, dim3(fb), dim3(tb), 0, st, d_prev, d_F, cap, d_frag, d_heads,
-                       d_misc + kMiscHeads);
+    hipLaunchKernelGGL(uio_heads_kernel, dim3(fb), dim3(tb), 0, st, d_prev, d_F, cap, d_frag);
     HIP_TRY(hipGetLastError());
     const uint32_t blocks = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
     h3c_rt::ProfToken tok;
     HIP_TRY(h3c_rt::prof_begin(st, tok));
-    hipLaunchKernelGGL(uio_block_kernel, dim3(blocks), dim3(kThreads), 0, st, d_frag, d_heads, d_misc + kMiscHeads,
-                       pc, d_eacc);
+    hipLaunchKernelGGL(uio_block_kernel, dim3(blocks), dim3(kThreads), 0, st, d_frag, d_F, cap, pc, d_eacc);
     HIP_TRY(hipGetLastError());
     // algorithmic bytes, per op: a 4 KiB block read and written once plus 4 KiB of new bytes
     // (exact for BASELINE config 3's block-aligned 4 KiB writes; bench.py states the unit)
     HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDIO, 3ull * kBlk * n));
-    // t' per op, then s' per op (two affine scans by chunk; elements computed as they are read)
+    // t' per op, then s' per op (two affine scans by chunk)
+    hipLaunchKernelGGL(uio_elem_kernel<TMapFn>, dim3(gb), dim3(tb), 0, st, TMapFn{d_pos, d_eacc, d_payraw, pc}, n,
+                       d_tel);
+    HIP_TRY(hipGetLastError());
     {
       size_t t = tmp_bytes;
-      HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, TIt(CountIt(0), TMapFn{d_pos, d_eacc, d_payraw, pc}),
-                                             d_tscan, (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
-      t = tmp_bytes;
-      HIP_TRY(rocprim::inclusive_scan_by_key(
-          d_tmp, t, d_skey, SIt(CountIt(0), SMapFn{d_pos, d_skey, nchunks, d_tscan, d_t0, d_eacc, d_payraw, pc}),
-          d_sscan, (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
+      HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_tel, d_tscan, (size_t)n, AffOp{poly},
+                                             rocprim::equal_to<uint32_t>(), st));
     }
-    HIP_TRY(hipMemcpyAsync(d_chunks_out, d_chunks, sizeof(h3c_chunk_state) * nchunks, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(uio_elem_kernel<SMapFn>, dim3(gb), dim3(tb), 0, st,
+                       SMapFn{d_pos, d_skey, nchunks, d_tscan, d_t0, d_eacc, d_payraw, pc}, n, d_sel);
+    HIP_TRY(hipGetLastError());
+    {
+      size_t t = tmp_bytes;
+      HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_sel, d_sscan, (size_t)n, AffOp{poly},
+                                             rocprim::equal_to<uint32_t>(), st));
+    }
+    if (nchunks)
+      HIP_TRY(hipMemcpyAsync(d_chunks_out, d_chunks, sizeof(h3c_chunk_state) * nchunks, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(uio_result_kernel, dim3(gb), dim3(tb), 0, st, d_pos, d_skey, n, d_sscan, d_chunks,
                        d_chunks_out, nchunks, d_t0, poly_type, stdf, poly, d_res, d_ctr);
     HIP_TRY(hipGetLastError());
-    if (exact) {
+    if (exact && nchunks) {
       hipLaunchKernelGGL(uio_stale_kernel, dim3((nchunks + tb - 1) / tb), dim3(tb), 0, st, d_chunks, nchunks, d_t0,
                          poly_type, stdf, d_ctr);
       HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipMemcpyAsync(d_misc + 2, d_F, 4, hipMemcpyDeviceToDevice, st));
-    HIP_TRY(hipMemcpyAsync(hd, d_dn, dn_misc + 16, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(results, d_res, sizeof(h3c_update_result) * n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h_F, d_F, 4, hipMemcpyDeviceToHost, st));
+    rc = epilogue(st);
+    if (rc) return rc;
     const hipError_t se = hipStreamSynchronize(st);
     drain2.armed = false;
     if (se != hipSuccess) {
-      drain.armed = false;
+      drain.armed = drain_aux.armed = false;
       h3c_rt::set_error("h3c_update_ios", se);
       return H3C_ERR_HIP;
     }
-    const uint32_t F = reinterpret_cast<const uint32_t *>(hd + dn_misc)[2];
+    const uint32_t F = *h_F;
     last_frags = F;
     if (F <= cap) break;
     if (attempt) {  // cannot happen: the count is exact on the second attempt
-      drain.armed = false;
+      drain.armed = drain_aux.armed = false;
       h3c_rt::set_error_text("h3c_update_ios: fragment count changed between attempts");
       return H3C_ERR_HIP;
     }
     cap = F;  // nothing was written (no chains ran): redo with the count known
   }
-  drain.armed = false;
-  std::memcpy(chunks, hd, sizeof(h3c_chunk_state) * nchunks);
-  const unsigned long long *h_ctr = reinterpret_cast<const unsigned long long *>(hd + dn_ctr);
-  if (counters) {
-    counters->none = h_ctr[kCtrNone];
-    counters->reuse = h_ctr[kCtrReuse];
-    counters->combine = h_ctr[kCtrCombine];
-    counters->read_chunk = h_ctr[kCtrRead];
-    counters->recalculate = h_ctr[kCtrRecalc];
-    counters->checksum_mismatch = h_ctr[kCtrMismatch];
-    counters->invalid = h_ctr[kCtrInvalid];
-    counters->stale_chunks = h_ctr[kCtrStale];
+  drain.armed = drain_aux.armed = false;
+  return H3C_OK;
+}
+
+bool valid_update_args(uint8_t poly_type, const void *chunks, uint32_t nchunks, const void *ios, uint32_t n,
+                       const void *results) {
+  if (poly_type != H3C_TYPE_CRC32C && poly_type != H3C_TYPE_CRC32) return false;
+  return !((n && (!ios || !results)) || (nchunks && !chunks) || n >= 0x7FFFFFFFu || nchunks >= (1u << 28));
+}
+
+void counters_from(const unsigned long long *h, h3c_update_counters *c) {
+  c->none = h[kCtrNone];
+  c->reuse = h[kCtrReuse];
+  c->combine = h[kCtrCombine];
+  c->read_chunk = h[kCtrRead];
+  c->recalculate = h[kCtrRecalc];
+  c->checksum_mismatch = h[kCtrMismatch];
+  c->invalid = h[kCtrInvalid];
+  c->stale_chunks = h[kCtrStale];
+}
+
+}  // namespace
+
+extern "C" int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
+                                 uint32_t n, h3c_update_result *results, uint32_t flags, h3c_update_counters *counters,
+                                 void *stream) {
+  if (counters) std::memset(counters, 0, sizeof(*counters));
+  if (!valid_update_args(poly_type, chunks, nchunks, ios, n, results)) return H3C_ERR_INVALID_ARG;
+  for (uint32_t c = 0; c < nchunks; ++c)  // a chunk longer than its capacity is a caller bug
+    if (chunks[c].size > chunks[c].chunk_size) {
+      h3c_rt::set_error_text("h3c_update_ios: a chunk's size exceeds its chunk_size");
+      return H3C_ERR_INVALID_ARG;
+    }
+  if (n == 0) return H3C_OK;
+  int dev = 0;
+  int rc = h3c_rt::current_device(&dev);
+  if (rc) return rc;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const uint32_t C = std::max(nchunks, 1u);
+  // device copies of the caller's arrays; the chunk table and counters through pinned staging
+  const size_t cb = ((sizeof(h3c_chunk_state) * C + 255) & ~size_t(255));
+  h3c_rt::DeviceLease lease(dev, 3 * cb + 256 + ((sizeof(h3c_update_io) * n + 255) & ~size_t(255)) +
+                                     sizeof(h3c_update_result) * n + 256);
+  h3c_rt::PinnedLease pin(2 * cb + 256);
+  if (!lease.ok() || !pin.ok()) return H3C_ERR_HIP;
+  char *cur = lease.data();
+  h3c_chunk_state *d_in = carve<h3c_chunk_state>(cur, C);
+  char *d_outblk = carve<char>(cur, cb + 64);  // [final chunks | counters]
+  h3c_chunk_state *d_out = reinterpret_cast<h3c_chunk_state *>(d_outblk);
+  unsigned long long *d_ctr = reinterpret_cast<unsigned long long *>(d_outblk + cb);
+  h3c_update_io *d_ios = carve<h3c_update_io>(cur, n);
+  h3c_update_result *d_res = carve<h3c_update_result>(cur, n);
+  char *hin = pin.data(), *hout = pin.data() + cb + 256;
+  std::memcpy(hin, chunks, sizeof(h3c_chunk_state) * nchunks);
+  {
+    StreamDrain drain{st, true};
+    HIP_TRY(hipMemcpyAsync(d_in, hin, sizeof(h3c_chunk_state) * nchunks, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_ios, ios, sizeof(h3c_update_io) * n, hipMemcpyHostToDevice, st));
+    rc = update_core(poly_type, d_in, d_out, nchunks, d_ios, n, d_res, flags, d_ctr, st, dev, [&](hipStream_t s) -> int {
+      HIP_TRY(hipMemcpyAsync(results, d_res, sizeof(h3c_update_result) * n, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(hout, d_outblk, cb + 64, hipMemcpyDeviceToHost, s));
+      return H3C_OK;
+    });
+    if (rc) return rc;
+    drain.armed = false;
   }
+  std::memcpy(chunks, hout, sizeof(h3c_chunk_state) * nchunks);
+  if (counters) counters_from(reinterpret_cast<const unsigned long long *>(hout + cb), counters);
+  return H3C_OK;
+}
+
+extern "C" int h3c_update_ios_dev(uint8_t poly_type, h3c_chunk_state *chunks_dev, uint32_t nchunks,
+                                  const h3c_update_io *ios_dev, uint32_t n, h3c_update_result *results_dev,
+                                  uint32_t flags, h3c_update_counters *counters_dev, void *stream) {
+  if (!valid_update_args(poly_type, chunks_dev, nchunks, ios_dev, n, results_dev)) return H3C_ERR_INVALID_ARG;
+  int dev = 0;
+  int rc = h3c_rt::current_device(&dev);
+  if (rc) return rc;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n == 0) {
+    if (counters_dev) HIP_TRY(hipMemsetAsync(counters_dev, 0, sizeof(h3c_update_counters), st));
+    return H3C_OK;
+  }
+  const uint32_t C = std::max(nchunks, 1u);
+  h3c_rt::DeviceLease lease(dev, sizeof(h3c_chunk_state) * C + 256 + sizeof(h3c_update_counters) + 256);
+  if (!lease.ok()) return H3C_ERR_HIP;
+  char *cur = lease.data();
+  h3c_chunk_state *d_out = carve<h3c_chunk_state>(cur, C);
+  unsigned long long *d_ctr = counters_dev ? reinterpret_cast<unsigned long long *>(counters_dev)
+                                           : carve<unsigned long long>(cur, kCtrN);
+  StreamDrain drain{st, true};
+  rc = update_core(poly_type, chunks_dev, d_out, nchunks, ios_dev, n, results_dev, flags, d_ctr, st, dev,
+                   [&](hipStream_t s) -> int {
+                     if (nchunks)
+                       HIP_TRY(hipMemcpyAsync(chunks_dev, d_out, sizeof(h3c_chunk_state) * nchunks,
+                                              hipMemcpyDeviceToDevice, s));
+                     return H3C_OK;
+                   });
+  if (rc) return rc;
+  drain.armed = false;
   return H3C_OK;
 }
 

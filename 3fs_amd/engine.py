@@ -84,6 +84,7 @@ _proto("h3c_update_workspace_bytes", _sz, _u32, _u32, _u64, _u32)
 _proto("h3c_update_blocks", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp)
 _proto("h3c_update_ios", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp)
 _proto("h3c_update_ios_ex", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp)
+_proto("h3c_update_ios_dev", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp)
 _proto("h3c_serde_checksum_mark", _u32, _u32, _int)
 _proto("h3c_batch_serde_checksum", _int, _vp, _sz, _vp, _vp, _vp)
 _proto("h3c_batch_serde_verify", _int, _vp, _sz, _vp, _vp, _vp, _vp)
@@ -375,6 +376,28 @@ def update_ios(chunks: np.ndarray, ios: np.ndarray, type_: int = ChecksumType.CR
                                  res.ctypes.data, flags, ctypes.byref(counters) if counters is not None else None,
                                  _stream_handle(stream)))
     return res
+
+
+def update_ios_dev(chunks, ios, results, type_: int = ChecksumType.CRC32C, std_domain: bool = False,
+                   exact: bool = False, counters=None, stream=None) -> None:
+    """update_ios with every table on the GPU (h3c_update_ios_dev): `chunks` uint8 tensor of
+    nchunks x 24 bytes (CHUNK_STATE_DTYPE records, updated in place), `ios` uint8 tensor of
+    n x 32 bytes (UPDATE_IO_DTYPE), `results` uint8 tensor of n x 16 bytes (UPDATE_RESULT_DTYPE),
+    `counters` an int64 tensor of 8 (UpdateCounters order) or None.  No PCIe traffic; synchronous
+    on `stream`."""
+    for t, rec in ((chunks, CHUNK_STATE_DTYPE), (ios, UPDATE_IO_DTYPE), (results, UPDATE_RESULT_DTYPE)):
+        if not t.is_cuda or not t.is_contiguous() or (t.numel() * t.element_size()) % rec.itemsize:
+            raise ValueError("chunks / ios / results must be contiguous GPU tensors of whole records")
+    nchunks = chunks.numel() * chunks.element_size() // CHUNK_STATE_DTYPE.itemsize
+    n = ios.numel() * ios.element_size() // UPDATE_IO_DTYPE.itemsize
+    if results.numel() * results.element_size() != n * UPDATE_RESULT_DTYPE.itemsize:
+        raise ValueError("results must hold one record per op")
+    if counters is not None and (not counters.is_cuda or counters.numel() * counters.element_size() != 64):
+        raise ValueError("counters must be a GPU tensor of 8 x 64-bit")
+    flags = (UPD_STD_DOMAIN if std_domain else 0) | (UPD_EXACT if exact else 0)
+    _check(lib.h3c_update_ios_dev(int(type_), chunks.data_ptr(), nchunks, ios.data_ptr(), n, results.data_ptr(),
+                                  flags, counters.data_ptr() if counters is not None else None,
+                                  _stream_handle(stream)))
 
 
 READ_JOB_DTYPE = np.dtype([("data", "<u8"), ("length", "<u8"), ("chunk_len", "<u8"), ("offset", "<u4"),

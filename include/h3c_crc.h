@@ -244,17 +244,25 @@ typedef struct h3c_update_counters {
  * A chunk whose stored checksum is not of `poly_type` (e.g. NONE) is CRC'd once either way.
  * Client checksums must be NONE or `poly_type` (the client's chunk_checksum_type), else the
  * op fails with H3C_ERR_INVALID_ARG; so does a TRUNCATE / EXTEND of a chunk whose stored
- * checksum is of the other polynomial (raw domain).  `chunks` and `results` are host arrays
- * (pinned memory avoids a staging copy); chunk bytes are updated in place on device.  All
- * per-op work runs on the device; the host issues the launches, one mid-batch read of the
- * work size and the final copy.  Synchronous on `stream`.  A chunk whose size exceeds its
- * chunk_size fails the whole call with H3C_ERR_INVALID_ARG, before any work. */
+ * checksum at the start of the batch is of the other polynomial (raw domain).  `chunks` and
+ * `results` are host arrays (pinned memory avoids a staging copy); chunk bytes are updated in
+ * place on device.  All per-op and per-chunk work runs on the device; the host issues the
+ * launches and copies and reads one count back at the end.  Synchronous on `stream`.  A chunk
+ * whose size exceeds its chunk_size fails the whole call with H3C_ERR_INVALID_ARG, before any
+ * work. */
 int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios, uint32_t n,
                    h3c_update_result *results, uint32_t flags, void *stream);
 /* The same, also returning the batch's case counters (counters may be NULL). */
 int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
                       uint32_t n, h3c_update_result *results, uint32_t flags, h3c_update_counters *counters,
                       void *stream);
+/* The same with every array in device memory (chunk table in / out, ops, results, counters -- the
+ * latter may be NULL): for callers whose op tables already live in HBM; no PCIe traffic.  A chunk
+ * whose size exceeds its chunk_size fails its ops with H3C_ERR_INVALID_ARG.  Synchronous on
+ * `stream` (the host reads the fragment count back once, at the end). */
+int h3c_update_ios_dev(uint8_t poly_type, h3c_chunk_state *chunks_dev, uint32_t nchunks, const h3c_update_io *ios_dev,
+                       uint32_t n, h3c_update_result *results_dev, uint32_t flags, h3c_update_counters *counters_dev,
+                       void *stream);
 
 /* ---- adjacent formats on the same kernels ---- */
 

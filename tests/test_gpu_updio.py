@@ -113,12 +113,27 @@ class Scenario:
                       io["type"], io["kind"], h3c.IO_SYNCING if io.get("syncing") else 0, 0)
         return chunks, ios
 
-    def run(self, exact=False, type_=None):
+    def run(self, exact=False, type_=None, dev_api=False):
+        """dev_api: drive h3c_update_ios_dev with the chunk / op / result / counter tables in HBM."""
         chunks, ios = self.device_ios()
         self.counters = self.h3c.UpdateCounters()
         kw = {} if type_ is None else {"type_": type_}
-        res = self.h3c.update_ios(chunks, ios, exact=exact, counters=self.counters, **kw)
-        self.torch.cuda.synchronize()
+        if not dev_api:
+            res = self.h3c.update_ios(chunks, ios, exact=exact, counters=self.counters, **kw)
+            self.torch.cuda.synchronize()
+            return chunks, res
+        torch = self.torch
+        d_chunks = torch.from_numpy(chunks.view(np.uint8).copy()).to(self.dev)
+        d_ios = torch.from_numpy(ios.view(np.uint8).copy()).to(self.dev)
+        d_res = torch.full((len(ios) * self.h3c.UPDATE_RESULT_DTYPE.itemsize,), 0xA5, dtype=torch.uint8,
+                           device=self.dev)
+        d_ctr = torch.full((8,), -1, dtype=torch.int64, device=self.dev)
+        self.h3c.update_ios_dev(d_chunks, d_ios, d_res, exact=exact, counters=d_ctr, **kw)
+        torch.cuda.synchronize()
+        chunks = d_chunks.cpu().numpy().view(self.h3c.CHUNK_STATE_DTYPE)
+        res = d_res.cpu().numpy().view(self.h3c.UPDATE_RESULT_DTYPE)
+        for f, v in zip(self.h3c.UpdateCounters._fields_, d_ctr.cpu().tolist()):
+            setattr(self.counters, f[0], v)
         return chunks, res
 
     def check(self, chunks, res, counters=True):
@@ -183,10 +198,47 @@ def test_updio_random_mixed_ops(h3c, torch_dev, seed):
     sc.check(*sc.run())
 
 
-def test_updio_large_batch_parallel_host_pass(h3c, torch_dev):
-    """20000 mixed ops over 24 chunks: past the 16384-op threshold the host pass runs on the
-    worker pool, one contiguous chunk range per thread (and a few client checksums fail, so
-    the speculative attempt is redone)."""
+@pytest.mark.parametrize("exact", [False, True])
+def test_updio_device_resident_tables(h3c, torch_dev, exact):
+    """h3c_update_ios_dev: chunk table, ops, results and counters all in HBM (the bench path),
+    same answers as the host-array entry, including stale chunks in exact mode."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(31 + exact)
+    if not exact:
+        sc = random_scenario(h3c, torch, dev, rng, nchunks=12, chunk_size=64 << 10, nops=3000)
+    else:
+        sc = Scenario(h3c, torch, dev, 12, 64 << 10, rng, stale=0.5)
+        for _ in range(2000):
+            c = int(rng.integers(0, 12))
+            off = int(rng.integers(0, 60 << 10))
+            sc.add(orc.UPD_WRITE, c, off, int(rng.integers(0, 4096)))
+    chunks, res = sc.run(exact=exact, dev_api=True)
+    sc.check(chunks, res)
+    if exact:
+        assert int(sc.counters.stale_chunks) == sc.stale_chunks
+
+
+def test_updio_device_resident_edge_shapes(h3c, torch_dev):
+    """h3c_update_ios_dev with an empty chunk table (every op INVALID) and with no ops."""
+    torch, dev = torch_dev
+    u8 = dict(dtype=torch.uint8, device=dev)
+    ios = np.zeros(3, dtype=h3c.UPDATE_IO_DTYPE)
+    ios["kind"] = orc.UPD_TRUNCATE
+    ios["chunk"] = [0, 1, 7]
+    d_res = torch.zeros(3 * 16, **u8)
+    d_ctr = torch.full((8,), -1, dtype=torch.int64, device=dev)
+    h3c.update_ios_dev(torch.zeros(0, **u8), torch.from_numpy(ios.view(np.uint8).copy()).to(dev), d_res,
+                       counters=d_ctr)
+    res = d_res.cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)
+    assert list(res["status"]) == [3, 3, 3]
+    assert d_ctr.cpu().tolist() == [0, 0, 0, 0, 0, 0, 3, 0]
+    h3c.update_ios_dev(torch.zeros(24, **u8), torch.zeros(0, **u8), torch.zeros(0, **u8), counters=d_ctr)
+    assert d_ctr.cpu().tolist() == [0] * 8
+
+
+def test_updio_large_batch(h3c, torch_dev):
+    """20000 mixed ops over 24 chunks with ops naming no chunk of the batch spread through the
+    sequence (and a few client checksums failing)."""
     torch, dev = torch_dev
     rng = np.random.default_rng(20)
     sc = random_scenario(h3c, torch, dev, rng, nchunks=24, chunk_size=64 << 10, nops=20000)
