@@ -131,6 +131,8 @@ uint32_t small_rows_for(const DevChunk *c, size_t n, uint32_t max_segs);
 uint32_t small_rows_bound(uint64_t max_len, uint32_t max_segs);
 // Segment size the engine picks for a batch of `total_bytes` on device `dev`.
 uint64_t pick_seg(uint64_t total_bytes, int dev);
+// h3c_test_hook values (0 = default; initialised once from the environment).
+uint64_t hook(int key);
 }  // namespace h3c_rt
 
 #define HIP_TRY(expr)               \

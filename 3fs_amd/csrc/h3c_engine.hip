@@ -714,15 +714,40 @@ int init_device(int dev) {
   return ctx.status;
 }
 
+// The device count, queried once per process (the set of visible devices does not change).
+int device_count() {
+  static const int n = [] {
+    int k = 0;
+    return hipGetDeviceCount(&k) == hipSuccess ? k : 0;
+  }();
+  return n;
+}
+
 int current_device(int *dev) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+  if (device_count() <= 0) {
     g_last_error = "no HIP device";
     return H3C_ERR_NO_DEVICE;
   }
   HIP_TRY(hipGetDevice(dev));
   return init_device(*dev);
 }
+
+// h3c_test_hook state: read from the environment once, settable by tests.
+std::atomic<uint64_t> g_hooks[4];
+const bool g_hooks_init = [] {
+  const char *names[4] = {nullptr, "H3C_SEG_BYTES", "H3C_DEBUG_FLAGS", "H3C_UPD_SCAN"};
+  for (int k = 1; k < 4; ++k) {
+    uint64_t v = 0;
+    if (const char *e = std::getenv(names[k])) {
+      if (k == H3C_HOOK_UPD_SCAN)
+        v = std::strcmp(e, "fused") == 0 ? 1 : std::strcmp(e, "tiles") == 0 ? 2 : std::strcmp(e, "sort") == 0 ? 3 : 0;
+      else
+        v = std::strtoull(e, nullptr, 0);
+    }
+    g_hooks[k].store(v);
+  }
+  return true;
+}();
 
 }  // namespace
 
@@ -732,6 +757,7 @@ const void *device_consts(int dev, int type) {
   return g_dev[dev].d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
 }
 int device_num_cu(int dev) { return (dev >= 0 && dev < kMaxDevices) ? g_dev[dev].num_cu : 0; }
+uint64_t hook(int key) { return (key > 0 && key < 4) ? g_hooks[key].load(std::memory_order_relaxed) : 0; }
 int current_device(int *dev) { return ::current_device(dev); }
 void set_error(const char *what, hipError_t e) { ::set_error(what, e); }
 void set_error_text(const char *text) { g_last_error = text; }
@@ -955,10 +981,13 @@ uint64_t pick_seg(uint64_t total_bytes, int dev) { return pick_seg_bytes(total_b
 
 namespace {
 
-// test hook: H3C_DEBUG_FLAGS bit0 disables the pipelined row loop (read per plan)
-uint32_t read_dbg_flags() {
-  const char *e = std::getenv("H3C_DEBUG_FLAGS");
-  return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
+// test hook H3C_HOOK_DEBUG_FLAGS: bit0 disables the pipelined row loop (read per plan)
+uint32_t read_dbg_flags() { return (uint32_t)h3c_rt::hook(H3C_HOOK_DEBUG_FLAGS); }
+
+// test hook H3C_HOOK_SEG_BYTES: force the segment size
+uint64_t forced_seg(uint64_t seg) {
+  const uint64_t v = h3c_rt::hook(H3C_HOOK_SEG_BYTES);
+  return (v >= kRowBytes && v % kRowBytes == 0) ? v : seg;
 }
 
 struct Group {
@@ -1083,10 +1112,12 @@ uint32_t h3c_crc32_combine(uint32_t c1, uint32_t c2, uint64_t len2) {
   return hgf_mul(c1, hxpow8n(len2, kPolyCrc32), kPolyCrc32) ^ c2;
 }
 
-int h3c_device_count(void) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
-  return n;
+int h3c_device_count(void) { return device_count(); }
+
+int h3c_test_hook(int key, uint64_t value) {
+  if (key < 1 || key > 3) return H3C_ERR_INVALID_ARG;
+  g_hooks[key].store(value);
+  return H3C_OK;
 }
 
 int h3c_init(int device) { return init_device(device); }
@@ -1135,10 +1166,7 @@ int h3c_plan_create(const h3c_desc *d, size_t n, int device, h3c_plan **out) {
     if ((d[i].type == H3C_TYPE_CRC32C || d[i].type == H3C_TYPE_CRC32) && d[i].ptr) total += d[i].len;
   p->seg_bytes = pick_seg_for(d, n, g_dev[device].num_cu);
   p->dbg = read_dbg_flags();
-  if (const char *e = std::getenv("H3C_SEG_BYTES")) {  // test hook: force the segment size
-    const uint64_t v = std::strtoull(e, nullptr, 0);
-    if (v >= kRowBytes && v % kRowBytes == 0) p->seg_bytes = v;
-  }
+  p->seg_bytes = forced_seg(p->seg_bytes);
   p->bytes = total;
 
   GroupLayout gl;
@@ -1244,11 +1272,7 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
     const bool crc = x.ptr && x.len && (x.type == H3C_TYPE_CRC32C || x.type == H3C_TYPE_CRC32);
     if (crc && x.mem != H3C_MEM_DEVICE) host_bytes += (x.len + 255) & ~uint64_t(255);
   }
-  uint64_t seg_bytes = pick_seg_for(d, n, g_dev[dev].num_cu);
-  if (const char *e = std::getenv("H3C_SEG_BYTES")) {  // test hook: force the segment size
-    const uint64_t v = std::strtoull(e, nullptr, 0);
-    if (v >= kRowBytes && v % kRowBytes == 0) seg_bytes = v;
-  }
+  const uint64_t seg_bytes = forced_seg(pick_seg_for(d, n, g_dev[dev].num_cu));
   // staging offsets first (descriptor pointers are rewritten to the arena below)
   auto align = [](uint64_t v) { return (v + 255) & ~uint64_t(255); };
   const uint64_t off_stage = 0;

@@ -30,6 +30,16 @@
 //      i.e. the chunk checksum right after write i, which is what updateChecksum stores.
 //      Dense tiles (tile / column / apply kernels) when tiles x chunks is small, else a
 //      rocPRIM stable sort by chunk + inclusive_scan_by_key(XOR) + scatter.
+// Fused path (4 KiB blocks, <= 128 chunks: BASELINE config 3): steps 2, 4 and 5 are one
+// launch.  Each wave resolves its writes' links itself, keeps per-chunk running XORs in
+// its lanes (lane c holds chunk c, c+64), and workgroups chain their per-chunk aggregates
+// in ticket order by decoupled look-back over 8-byte {state, value} granules (one aligned
+// agent-scope store each: the data is the flag, no fences); the last workgroup writes the
+// final checksums and the counters.  One memset (hash heads, ticket, granules) + tlink +
+// the fused kernel: 3 launches instead of 8.
+// H3C_UPD_EXACT: the chunks' checksums are first recomputed from their bytes (one create
+// launch over the chunk set), so results do not depend on the stored values -- what
+// updateChecksum case (iv) computes by re-reading the chunk (ChunkReplica.cc:356-390).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -62,7 +72,8 @@ __device__ __forceinline__ void store_row(uint64_t a, uint4 v) {
 }
 
 #ifndef H3C_UPD_EXPERIMENT
-#define H3C_UPD_EXPERIMENT 0  // timing-only builds: bit0 skips write-back, bit1 skips the CRC math
+#define H3C_UPD_EXPERIMENT 0  // timing-only builds: bit0 skips write-back, bit1 skips the CRC math,
+                              // fused kernel: bit2 skips the hash walk, bit3 stops after the writes
 #endif
 
 // rocPRIM picks merge sort below this many items.  Forcing its onesweep radix passes
@@ -86,13 +97,12 @@ uint32_t bits_for(uint64_t v) {  // number of bits to represent values < v
 // Sort path only: chunk keys and sequence indices for the per-chunk scan.
 __global__ void upd_keys_kernel(const uint32_t *__restrict__ blk_chunk, const uint32_t *__restrict__ blk_index,
                                 uint32_t n, uint32_t nchunks, uint32_t bpc, uint32_t *__restrict__ kchunk,
-                                uint32_t *__restrict__ iota, uint32_t *__restrict__ err) {
+                                uint32_t *__restrict__ iota) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t c = blk_chunk[i], b = blk_index[i];
   iota[i] = i;
   const bool bad = c >= nchunks || b >= bpc;  // invalid entry: parked on the sentinel chunk, no effect
-  if (bad) atomicAdd(err, 1u);
   kchunk[i] = bad ? nchunks : c;
 }
 
@@ -101,7 +111,8 @@ __global__ void upd_keys_kernel(const uint32_t *__restrict__ blk_chunk, const ui
 // each write finds its previous writer of the same slot by an LDS match.  Each tile's last
 // writer of a slot is pushed (one atomicExch) on the list of its hash bucket (key = chunk *
 // bpc + block); a bucket's list may also hold other slots' writers, told apart by their
-// stored key.  A write with no predecessor in its tile then takes the largest listed index
+// stored key (list entries are index + 1, so an all-zero table is empty: one memset per call
+// clears it with the other per-call words).  A write with no predecessor in its tile then takes the largest listed index
 // of its slot below its own: a list holds at most one entry per tile and slot, so the walk
 // stays short even when every write hammers one slot.  (A returning atomicCAS costs about
 // twice an atomicExch here: scripts/atomic_probe.hip.)
@@ -143,14 +154,20 @@ __global__ __launch_bounds__(kLinkTile) void upd_tlink_kernel(const uint32_t *__
                                                               const uint32_t *__restrict__ blk_index, uint32_t n,
                                                               uint32_t nchunks, uint32_t bpc, uint32_t *hhead,
                                                               uint32_t hmask, uint32_t *__restrict__ nkey,
-                                                              uint32_t *__restrict__ next, uint32_t *__restrict__ prev) {
+                                                              uint32_t *__restrict__ next, uint32_t *__restrict__ prev,
+                                                              uint32_t *__restrict__ err, uint32_t *__restrict__ touched) {
   __shared__ TileGroups<kLinkTile> g;
   const uint32_t t = threadIdx.x, i0 = blockIdx.x * kLinkTile, i = i0 + t;
   uint32_t key = kNone;
   if (i < n) {
     const uint32_t c = blk_chunk[i], b = blk_index[i];
-    if (c < nchunks && b < bpc) key = c * bpc + b;
+    if (c < nchunks && b < bpc) {
+      key = c * bpc + b;
+      touched[c] = 1u;  // chunks no write reaches keep their stored checksum
+    }
   }
+  const int ninv = __syncthreads_count(i < n && key == kNone);  // out-of-range entries
+  if (t == 0 && ninv) atomicAdd(err, (uint32_t)ninv);
   const uint32_t head = tile_group(g, t, key);
   uint32_t pin = kNone;
   bool last = true;
@@ -159,9 +176,9 @@ __global__ __launch_bounds__(kLinkTile) void upd_tlink_kernel(const uint32_t *__
     if (u > t) last = false;
   }
   if (i < n) prev[i] = pin == kNone ? kNone : i0 + pin;
-  if (key != kNone && last) {  // push i on its bucket's list
+  if (key != kNone && last) {  // push i on its bucket's list (entries are index + 1; 0 ends a list)
     nkey[i] = key;
-    next[i] = atomicExch(&hhead[slot_hash(key, hmask)], i);
+    next[i] = atomicExch(&hhead[slot_hash(key, hmask)], i + 1);
   }
 }
 
@@ -178,7 +195,8 @@ __global__ void upd_resolve_kernel(const uint32_t *__restrict__ blk_chunk, const
   if (c >= nchunks || b >= bpc) return;
   const uint32_t key = c * bpc + b;
   uint32_t p = kNone, fmax = i;  // i's tile's last writer of the slot is on the list
-  for (uint32_t j = hhead[slot_hash(key, hmask)]; j != kNone; j = next[j]) {
+  for (uint32_t e = hhead[slot_hash(key, hmask)]; e != 0; e = next[e - 1]) {
+    const uint32_t j = e - 1;
     if (nkey[j] != key) continue;
     if (j < i && (p == kNone || j > p)) p = j;
     fmax = max(fmax, j);
@@ -362,6 +380,335 @@ __global__ __launch_bounds__(kThreads) void upd_delta_kernel(
   }
 }
 
+// ---- fused path: links, deltas, write-back and per-chunk prefix in one launch ----
+constexpr uint32_t kFusedCols = 128;    // chunk columns of the look-back: lane c holds chunks c and c + 64
+constexpr uint32_t kFusedMaxWG = 1024;  // granule rows reserved in the workspace
+constexpr uint32_t kGranAgg = 1, kGranIncl = 2;
+constexpr uint32_t kSpinLimit = 1u << 22;  // bounded look-back spins (about a quarter second)
+enum { kCtlTicket = 0, kCtlErr = 1, kCtlTimeout = 2, kCtlWords = 64 };
+typedef unsigned long long __attribute__((address_space(1))) gu64;
+
+__device__ __forceinline__ void gran_store(uint64_t *p, uint32_t state, uint32_t v) {
+  __hip_atomic_store((gu64 *)p, ((unsigned long long)state << 32) | v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
+  return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave w of workgroup L takes writes [lo, hi) of (16 L + w); workgroup L's look-back waits only
+// on workgroups below it.  The grid is at most one workgroup per CU (the tables fill LDS), so all
+// are resident together unless other work holds CUs -- then a waiter only waits longer -- and
+// every spin is bounded.
+// Per group of 64 writes lane k loads write k's metadata -- resolving its previous writer
+// from the tile link or the hash of per-tile last writers -- then the wave walks the group as
+// upd_delta_kernel does.  Afterwards each write's v = delta * sh[b] is folded into the running
+// XOR of its chunk (lane c mod 64), whose value right after the write is kept in inpre[i].
+__global__ __launch_bounds__(kThreads) void upd_fused_kernel(
+    const uint64_t *__restrict__ chunk_base, uint32_t nchunks, uint32_t bpc, const uint32_t *__restrict__ blk_chunk,
+    const uint32_t *__restrict__ blk_index, const uint8_t *payload, uint32_t n, const uint32_t *__restrict__ prev,
+    const uint32_t *__restrict__ hhead, uint32_t hmask, const uint32_t *__restrict__ nkey,
+    const uint32_t *__restrict__ next, const uint32_t *__restrict__ sh, const PolyConsts *__restrict__ pc,
+    const uint32_t *__restrict__ raw_base, const uint32_t *__restrict__ raw_in, uint32_t exact, uint32_t reuse_case,
+    const uint32_t *__restrict__ touched, uint32_t *ctl, uint64_t *gran, uint32_t *__restrict__ inpre,
+    uint32_t *__restrict__ out_raw, uint32_t *__restrict__ raw_out, uint32_t *__restrict__ n_invalid,
+    unsigned long long *__restrict__ counters) {
+  constexpr uint32_t G4 = 4096;
+  __shared__ uint32_t lds[kLdsWords + kRedWords];
+  const uint32_t L = blockIdx.x, nwg = gridDim.x;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)L * kWavesPerBlock + wave;
+  const uint64_t nw = (uint64_t)nwg * kWavesPerBlock;
+  const uint32_t lo = (uint32_t)(gw * n / nw), hi = (uint32_t)((gw + 1) * n / nw);
+  const uint64_t lo16 = 16u * lane;
+  const uint64_t pay = (uint64_t)(uintptr_t)payload;
+  auto rl64 = [](uint64_t v, uint32_t t) -> uint64_t {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32);
+  };
+  // per group of 64 writes: lane k's write (chunk, shift, new / old / destination / final bytes)
+  uint32_t m_c = kNone, m_sh = 0;
+  uint64_t m_new = 0, m_old = 0, m_dst = 0, m_fin = 0;
+  uint4 vn[4], vo[4];
+  bool valid = false;
+  uint64_t pnew = 0, pold = 0;
+  auto start_group = [&](uint32_t g0) {
+    const uint32_t cnt = min(64u, hi - g0);
+    const uint32_t k = g0 + lane;
+    m_c = kNone;
+    m_sh = 0;
+    m_new = m_old = m_dst = m_fin = 0;
+    uint32_t key = kNone;
+    if (lane < cnt) {
+      const uint32_t c = blk_chunk[k], bb = blk_index[k];
+      if (c < nchunks && bb < bpc) {
+        const uint32_t p = prev[k];
+        const uint64_t slot = chunk_base[c] + (uint64_t)bb * G4;
+        m_c = c;
+        m_sh = sh[bb];
+        m_new = pay + (uint64_t)k * G4;
+        // speculate the common case: no earlier writer of the slot anywhere, and no later one
+        m_old = p == kNone ? slot : pay + (uint64_t)p * G4;
+        m_dst = p == kNone ? slot : 0;
+        m_fin = p == kNone ? m_new : 0;
+        if (p == kNone && !(H3C_UPD_EXPERIMENT & 4)) key = c * bpc + bb;
+      }
+    }
+    valid = __builtin_amdgcn_readlane(m_c, 0) != kNone;
+    pnew = rl64(m_new, 0);
+    pold = rl64(m_old, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      vn[u] = valid ? load_row(pnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+      vo[u] = valid ? load_row(pold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+    }
+    // the walk over the slot's listed tile-last writers, while those rows load
+    if (key != kNone) {
+      uint32_t p = kNone, fmax = k;
+      for (uint32_t e = hhead[slot_hash(key, hmask)]; e != 0; e = next[e - 1]) {
+        const uint32_t j = e - 1;
+        if (nkey[j] != key) continue;
+        if (j < k && (p == kNone || j > p)) p = j;
+        fmax = max(fmax, j);
+      }
+      if (p != kNone) {  // an earlier tile wrote the slot: its bytes are the old ones, it writes back
+        m_old = pay + (uint64_t)p * G4;
+        m_dst = 0;
+        m_fin = 0;
+      } else {  // the slot's first writer leaves the slot's last writer's bytes
+        m_fin = pay + (uint64_t)fmax * G4;
+      }
+    }
+    const uint64_t pold2 = rl64(m_old, 0);
+    if (valid && pold2 != pold) {  // write 0 was mis-speculated: reload its old rows
+      pold = pold2;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) vo[u] = load_row(pold + u * kRowBytes + lo16);
+    }
+  };
+  if (lo < hi) start_group(lo);  // the first group's links and rows load while the tables fill
+  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
+  const uint32_t *red_g = &pc->red[0][0][0];
+  for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  __syncthreads();
+  const uint32_t *red = lds + kLdsWords;
+  const char *lb = reinterpret_cast<const char *>(lds);
+  const LaneLut Lt = make_lut(lane);
+  const uint32_t poly = pc->poly;
+  uint32_t acc0 = 0, acc1 = 0;  // running XOR of chunks lane, lane + 64
+  uint32_t my_ip = 0;           // lane t: the chunk XOR right after write t of the group
+  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
+    const uint32_t cnt = min(64u, hi - g0);
+    const uint32_t k = g0 + lane;
+    uint32_t my_d = 0;
+    for (uint32_t t = 0; t < cnt; ++t) {
+      const bool nvalid = t + 1 < cnt && __builtin_amdgcn_readlane(m_c, t + 1) != kNone;
+      uint4 wn[4], wo[4];
+      uint64_t npnew = 0, npold = 0;
+      if (nvalid) {
+        npnew = rl64(m_new, t + 1);
+        npold = rl64(m_old, t + 1);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        wn[u] = nvalid ? load_row(npnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+        wo[u] = nvalid ? load_row(npold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+      }
+      if (valid) {
+        Streams st{0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          consume(st, make_uint4(vn[u].x ^ vo[u].x, vn[u].y ^ vo[u].y, vn[u].z ^ vo[u].z, vn[u].w ^ vo[u].w), lb, Lt);
+        const uint64_t dst = rl64(m_dst, t);
+        if (dst) {  // first writer of the slot: leave the slot's final bytes in the chunk
+          const uint64_t fin = rl64(m_fin, t);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint4 v = fin == pnew ? vn[u] : load_row(fin + u * kRowBytes + lo16);
+            store_row(dst + u * kRowBytes + lo16, v);
+          }
+        }
+        const uint32_t d = __builtin_amdgcn_readlane(wave_fold_tab(st, lane, red), 0);
+        if (lane == t) my_d = d;
+      }
+      valid = nvalid;
+      pnew = npnew;
+      pold = npold;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        vn[u] = wn[u];
+        vo[u] = wo[u];
+      }
+    }
+    // the group's v, all lanes at once; each write's chunk XOR right after it (inclusive, with
+    // the earlier groups' running value), and the running values moved past the group
+    const uint32_t v = m_c != kNone ? dgf_mul(my_d, m_sh, poly) : 0u;
+    const uint32_t src = m_c & 63;
+    const uint32_t r0 = __shfl(acc0, src, 64), r1 = __shfl(acc1, src, 64);
+    my_ip = m_c < 64 ? r0 : r1;
+    for (uint32_t t = 0; t < ((H3C_UPD_EXPERIMENT & 16) ? 0u : cnt); ++t) {
+      const uint32_t ct = __builtin_amdgcn_readlane(m_c, t), vt = __builtin_amdgcn_readlane(v, t);
+      if (lane >= t && m_c == ct) my_ip ^= vt;
+      if (ct == lane) acc0 ^= vt;
+      if (ct == lane + 64) acc1 ^= vt;
+    }
+    if (lane < cnt) inpre[k] = my_ip;
+    if (g0 + 64 < hi) start_group(g0 + 64);
+  }
+  // the chunks' base checksums, one per lane (chunks lane, lane + 64)
+  const uint32_t rb0 = lane < nchunks ? raw_base[lane] : 0u, rb1 = lane + 64 < nchunks ? raw_base[64 + lane] : 0u;
+
+  if (H3C_UPD_EXPERIMENT & 8) return;  // timing experiment: no aggregation / look-back / out_raw
+  // ---- chunk aggregates: waves of the workgroup (LDS), then workgroups (look-back) ----
+  __syncthreads();  // the CRC tables are done with: their LDS holds the aggregates now
+  uint32_t *wagg = lds;                               // [16][128]
+  uint32_t *wexcl = lds + kWavesPerBlock * kFusedCols;  // [128]: the workgroup's exclusive prefix
+  wagg[wave * kFusedCols + lane] = acc0;
+  wagg[wave * kFusedCols + 64 + lane] = acc1;
+  __syncthreads();
+  if (wave == 0) {
+    uint32_t a0 = 0, a1 = 0;
+    for (uint32_t w = 0; w < kWavesPerBlock; ++w) {
+      a0 ^= wagg[w * kFusedCols + lane];
+      a1 ^= wagg[w * kFusedCols + 64 + lane];
+    }
+    const bool two = nchunks > 64;
+    uint64_t *row = gran + (uint64_t)L * kFusedCols;
+    uint32_t x0 = 0, x1 = 0;
+    if (L > 0) {
+      if (lane < nchunks) gran_store(row + lane, kGranAgg, a0);
+      if (two && lane + 64 < nchunks) gran_store(row + 64 + lane, kGranAgg, a1);
+      int j0 = lane < nchunks ? (int)L - 1 : -1, j1 = two && lane + 64 < nchunks ? (int)L - 1 : -1;
+      for (uint32_t spins = 0; __builtin_amdgcn_ballot_w64(j0 >= 0 || j1 >= 0) != 0;) {
+        bool moved = false;
+        if (j0 >= 0) {
+          const uint64_t g = gran_load(gran + (uint64_t)j0 * kFusedCols + lane);
+          const uint32_t state = (uint32_t)(g >> 32);
+          if (state) {
+            x0 ^= (uint32_t)g;
+            j0 = state == kGranIncl ? -1 : j0 - 1;
+            moved = true;
+          }
+        }
+        if (j1 >= 0) {
+          const uint64_t g = gran_load(gran + (uint64_t)j1 * kFusedCols + 64 + lane);
+          const uint32_t state = (uint32_t)(g >> 32);
+          if (state) {
+            x1 ^= (uint32_t)g;
+            j1 = state == kGranIncl ? -1 : j1 - 1;
+            moved = true;
+          }
+        }
+        if (__builtin_amdgcn_ballot_w64(moved) == 0) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > kSpinLimit) {  // a predecessor never published: give up, flag it
+            if (lane == 0) atomicExch(&ctl[kCtlTimeout], 1u);
+            break;
+          }
+        }
+      }
+    }
+    if (lane < nchunks) gran_store(row + lane, kGranIncl, x0 ^ a0);
+    if (two && lane + 64 < nchunks) gran_store(row + 64 + lane, kGranIncl, x1 ^ a1);
+    wexcl[lane] = x0;
+    wexcl[64 + lane] = x1;
+    if (L == nwg - 1) {  // the last workgroup: final checksums, counts
+      const uint32_t t0 = x0 ^ a0, t1 = x1 ^ a1;
+      uint32_t stale = 0;
+      if (lane < nchunks) {
+        raw_out[lane] = touched[lane] ? raw_base[lane] ^ t0 : raw_in[lane];
+        stale += exact && raw_base[lane] != raw_in[lane];
+      }
+      if (lane + 64 < nchunks) {
+        raw_out[64 + lane] = touched[64 + lane] ? raw_base[64 + lane] ^ t1 : raw_in[64 + lane];
+        stale += exact && raw_base[64 + lane] != raw_in[64 + lane];
+      }
+      for (int o = 32; o >= 1; o >>= 1) stale += __shfl_xor(stale, o, 64);
+      if (lane == 0) {
+        const uint32_t inv = __hip_atomic_load(&ctl[kCtlErr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n_invalid) *n_invalid = inv;
+        if (counters) {  // h3c_update_counters: none, reuse, combine, read_chunk, recalculate, mismatch, invalid, stale
+          const unsigned long long ok = n - inv;
+          counters[0] = 0;
+          counters[1] = reuse_case ? ok : 0;
+          counters[2] = 0;
+          counters[3] = reuse_case ? 0 : ok;
+          counters[4] = 0;
+          counters[5] = 0;
+          counters[6] = inv;
+          counters[7] = stale;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t e0 = wexcl[lane], e1 = wexcl[64 + lane];
+  for (uint32_t w = 0; w < wave; ++w) {
+    e0 ^= wagg[w * kFusedCols + lane];
+    e1 ^= wagg[w * kFusedCols + 64 + lane];
+  }
+  const uint32_t be0 = rb0 ^ e0, be1 = rb1 ^ e1;
+  if (hi - lo <= 64) {  // one group (the common case): its chunks and XORs are still in registers
+    const uint32_t x0 = __shfl(be0, m_c & 63, 64), x1 = __shfl(be1, m_c & 63, 64);
+    if (lo + lane < hi) out_raw[lo + lane] = m_c != kNone ? (m_c < 64 ? x0 : x1) ^ my_ip : 0u;
+    return;
+  }
+  for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    uint32_t c = kNone, b = 0;
+    if (i < hi) {
+      c = blk_chunk[i];
+      b = blk_index[i];
+    }
+    const bool ok = i < hi && c < nchunks && b < bpc;
+    const uint32_t x0 = __shfl(be0, c & 63, 64), x1 = __shfl(be1, c & 63, 64);
+    if (i < hi) out_raw[i] = ok ? (c < 64 ? x0 : x1) ^ inpre[i] : 0u;
+  }
+}
+
+// H3C_UPD_EXACT: create descriptors for the chunk set (uniform length, start 0).
+__global__ void upd_exact_desc_kernel(const uint64_t *__restrict__ chunk_base, uint32_t nchunks, uint32_t spc,
+                                      DevChunk tmpl, DevChunk *__restrict__ out) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  DevChunk d = tmpl;
+  d.ptr = chunk_base[c];
+  d.out_idx = c;
+  d.seg_begin = c * spc;
+  out[c] = d;
+}
+
+// Counts for the tile / sort paths (the fused kernel writes them itself).
+__global__ void upd_finish_kernel(const uint32_t *__restrict__ ctl, uint32_t n, uint32_t nchunks,
+                                  const uint32_t *__restrict__ raw_base, const uint32_t *__restrict__ raw_in,
+                                  uint32_t exact, uint32_t reuse_case, uint32_t *__restrict__ n_invalid,
+                                  unsigned long long *__restrict__ counters) {
+  __shared__ unsigned int s_stale;
+  if (threadIdx.x == 0) s_stale = 0;
+  __syncthreads();
+  uint32_t stale = 0;
+  if (exact)
+    for (uint32_t c = threadIdx.x; c < nchunks; c += blockDim.x) stale += raw_base[c] != raw_in[c];
+  if (stale) atomicAdd(&s_stale, stale);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t inv = ctl[kCtlErr];
+    if (n_invalid) *n_invalid = inv;
+    if (counters) {
+      const unsigned long long ok = n - inv;
+      counters[0] = 0;
+      counters[1] = reuse_case ? ok : 0;
+      counters[2] = 0;
+      counters[3] = reuse_case ? 0 : ok;
+      counters[4] = 0;
+      counters[5] = 0;
+      counters[6] = inv;
+      counters[7] = s_stale;
+    }
+  }
+}
+
 // vals[p] = delta of the p-th write in (chunk, sequence) order, moved to its place in
 // the chunk: crc0(new ^ old) * x^(8*(L - (b+1)*G)).  One thread per write.
 __global__ void upd_gather_kernel(const uint32_t *__restrict__ chunk_s, const uint32_t *__restrict__ idx2, uint32_t n,
@@ -403,27 +750,22 @@ __global__ __launch_bounds__(kTile) void upd_tile_kernel(const uint32_t *__restr
                                                          uint32_t nchunks, uint32_t bpc,
                                                          const uint32_t *__restrict__ delta,
                                                          const uint32_t *__restrict__ sh, uint32_t poly,
-                                                         uint32_t *__restrict__ inpre, uint32_t *__restrict__ agg,
-                                                         uint32_t *__restrict__ tile_invalid) {
+                                                         uint32_t *__restrict__ inpre, uint32_t *__restrict__ agg) {
   __shared__ TileGroups<kTile> g;
   __shared__ uint32_t val[kTile];
   const uint32_t t = threadIdx.x, i = blockIdx.x * kTile + t;
   uint32_t c = kNone, v = 0;
-  bool invalid = false;
   if (i < n) {
     const uint32_t cc = blk_chunk[i], b = blk_index[i];
     if (cc < nchunks && b < bpc) {
       c = cc;
       v = dgf_mul(delta[i], sh[b], poly);
-    } else {
-      invalid = true;
     }
   }
   val[t] = v;
   uint32_t *row = agg + (uint64_t)blockIdx.x * nchunks;
   for (uint32_t k = t; k < nchunks; k += kTile) row[k] = 0;
-  const int ninv = __syncthreads_count(invalid);  // also orders val[] and the row zeroing
-  if (t == 0) tile_invalid[blockIdx.x] = (uint32_t)ninv;
+  __syncthreads();  // orders val[] and the row zeroing
   const uint32_t head = tile_group(g, t, c);
   uint32_t acc = 0;
   bool last = true;
@@ -438,23 +780,13 @@ __global__ __launch_bounds__(kTile) void upd_tile_kernel(const uint32_t *__restr
 // One workgroup per chunk: exclusive XOR scan of its agg column over tiles into
 // colpre, and the chunk's final checksum.
 __global__ __launch_bounds__(kTile) void upd_column_kernel(const uint32_t *__restrict__ agg, uint32_t ntiles,
-                                                           uint32_t nchunks, const uint32_t *__restrict__ raw_in,
+                                                           uint32_t nchunks, const uint32_t *__restrict__ raw_base,
+                                                           const uint32_t *__restrict__ raw_in,
+                                                           const uint32_t *__restrict__ touched,
                                                            uint32_t *__restrict__ colpre,
-                                                           uint32_t *__restrict__ raw_out,
-                                                           const uint32_t *__restrict__ tile_invalid,
-                                                           uint32_t *__restrict__ n_invalid) {
+                                                           uint32_t *__restrict__ raw_out) {
   __shared__ uint32_t part[kTile / 64];
   const uint32_t c = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  if (c == 0 && n_invalid) {  // workgroup 0 also totals the invalid entries
-    uint32_t s = 0;
-    for (uint32_t r = t; r < ntiles; r += kTile) s += tile_invalid[r];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (lane == 0) part[wave] = s;
-    __syncthreads();
-    if (t == 0) *n_invalid = part[0] + part[1] + part[2] + part[3];
-    __syncthreads();
-  }
   uint32_t carry = 0;
   for (uint32_t base = 0; base < ntiles; base += kTile) {
     const uint32_t r = base + t;
@@ -475,7 +807,7 @@ __global__ __launch_bounds__(kTile) void upd_column_kernel(const uint32_t *__res
     carry = total;
     __syncthreads();
   }
-  if (t == 0) raw_out[c] = raw_in[c] ^ carry;
+  if (t == 0) raw_out[c] = touched[c] ? raw_base[c] ^ carry : raw_in[c];
 }
 
 // One thread per write: the chunk checksum right after it.
@@ -489,49 +821,71 @@ __global__ void upd_apply_kernel(const uint32_t *__restrict__ blk_chunk, const u
   out_raw[i] = (c < nchunks && b < bpc) ? raw_in[c] ^ colpre[(uint64_t)(i / kTile) * nchunks + c] ^ inpre[i] : 0u;
 }
 
-// Dense tile path unless the aggregate matrix would be large (or a test forces the
-// sort path with H3C_UPD_SCAN=sort).
-bool use_tiles(uint32_t n, uint32_t nchunks) {
-  if (const char *e = std::getenv("H3C_UPD_SCAN"))
-    if (std::strcmp(e, "sort") == 0) return false;
+// Which per-chunk scan: the fused launch for 4 KiB blocks and <= 128 chunks, else dense tiles
+// unless their aggregate matrix would be large, else sort + scan_by_key (test hook
+// H3C_HOOK_UPD_SCAN forces one).
+enum Path { kPathFused = 1, kPathTiles = 2, kPathSort = 3 };
+bool tiles_fit(uint32_t n, uint32_t nchunks) {
   const uint64_t ntiles = (n + kTile - 1) / kTile;
   return ntiles * nchunks <= (1ull << 22);
 }
+int pick_path(uint32_t n, uint32_t nchunks, uint32_t block_bytes) {
+  const bool fused_ok = block_bytes == 4096 && nchunks <= kFusedCols;
+  const uint64_t forced = h3c_rt::hook(H3C_HOOK_UPD_SCAN);
+  if (forced == kPathFused && fused_ok) return kPathFused;
+  if (forced == kPathTiles && tiles_fit(n, nchunks)) return kPathTiles;
+  if (forced == kPathSort) return kPathSort;
+  if (fused_ok) return kPathFused;
+  return tiles_fit(n, nchunks) ? kPathTiles : kPathSort;
+}
 
 struct Workspace {
-  uint32_t *kchunk, *kchunk_s, *iota, *idx2;
-  uint32_t *prev, *final_of, *next, *delta, *vals, *scan, *sh, *err;
-  uint32_t *hhead, *nkey;  // link hash: hcap bucket list heads; per-write slot key of listed writes
+  // zeroed by one memset per call, in this order from the workspace start
+  uint32_t *hhead;    // link hash: hcap bucket list heads
+  uint32_t *ctl;      // ticket, invalid-entry count, look-back timeout
+  uint32_t *touched;  // per chunk: some write reaches it
+  uint64_t *gran;     // fused look-back granules, kFusedCols per workgroup
+  size_t zero_bytes;  // hhead .. gran (all rows; the call zeroes the rows its grid uses)
   uint32_t hcap;
+  uint32_t *kchunk, *kchunk_s, *iota, *idx2;
+  uint32_t *prev, *final_of, *next, *delta, *vals, *scan, *sh, *nkey;
   uint32_t *agg, *colpre;  // dense tile path: ntiles x nchunks each
-  uint32_t *tile_invalid;  // dense tile path: per-tile invalid-entry counts
+  uint32_t *raw_exact;     // H3C_UPD_EXACT: the chunks' checksums from their bytes
+  DevChunk *xdesc;         // ... their create descriptors
+  uint32_t *xseg;          // ... and segment partials
   void *tmp;
   size_t tmp_bytes;
 };
 
 size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
 
-// Lays out (or, with base == nullptr, sizes) the workspace.
-int layout(void *base, uint32_t n, uint32_t nchunks, uint32_t bpc, Workspace &w, size_t &total) {
+// Lays out (or, with base == nullptr, sizes) the workspace; the same layout serves every path.
+int layout(void *base, uint32_t n, uint32_t nchunks, uint64_t chunk_len, uint32_t block_bytes, Workspace &w,
+           size_t &total) {
   size_t off = 0;
   auto take = [&](size_t bytes) -> void * {
     void *p = base ? static_cast<char *>(base) + off : nullptr;
     off += align_up(bytes);
     return p;
   };
-  uint32_t **arrays[] = {&w.kchunk, &w.kchunk_s, &w.iota,  &w.idx2, &w.prev,
-                         &w.final_of, &w.next,    &w.delta, &w.vals, &w.scan};
-  for (uint32_t **a : arrays) *a = (uint32_t *)take(4ull * n);
-  w.nkey = (uint32_t *)take(4ull * n);
+  const uint32_t bpc = (uint32_t)(chunk_len / block_bytes);
   w.hcap = 256;
   while (w.hcap < n) w.hcap <<= 1;
   w.hhead = (uint32_t *)take(4ull * w.hcap);
+  w.ctl = (uint32_t *)take(4ull * kCtlWords);
+  w.touched = (uint32_t *)take(4ull * nchunks);
+  w.gran = (uint64_t *)take(8ull * kFusedCols * kFusedMaxWG);
+  w.zero_bytes = off;
+  uint32_t **arrays[] = {&w.kchunk, &w.kchunk_s, &w.iota, &w.idx2, &w.prev, &w.final_of,
+                         &w.next,   &w.delta,    &w.vals, &w.scan, &w.nkey};
+  for (uint32_t **a : arrays) *a = (uint32_t *)take(4ull * n);
   w.sh = (uint32_t *)take(4ull * bpc);
-  w.err = (uint32_t *)take(4);
-  const uint64_t tiles_cells = use_tiles(n, nchunks) ? (uint64_t)((n + kTile - 1) / kTile) * nchunks : 0;
+  const uint64_t tiles_cells = tiles_fit(n, nchunks) ? (uint64_t)((n + kTile - 1) / kTile) * nchunks : 0;
   w.agg = (uint32_t *)take(4ull * tiles_cells);
   w.colpre = (uint32_t *)take(4ull * tiles_cells);
-  w.tile_invalid = (uint32_t *)take(4ull * ((n + kTile - 1) / kTile));
+  w.raw_exact = (uint32_t *)take(4ull * nchunks);
+  w.xdesc = (DevChunk *)take(sizeof(DevChunk) * nchunks);
+  w.xseg = (uint32_t *)take(4ull * nchunks * ((chunk_len + kMinSegBytes - 1) / kMinSegBytes));
   size_t s1 = 0, s2 = 0;
   if (rocprim::radix_sort_pairs<SortConfig>(nullptr, s1, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                 (uint32_t *)nullptr, n, 0, 32) != hipSuccess)
@@ -584,44 +938,47 @@ int shift_table(int dev, uint8_t type, uint64_t chunk_len, uint32_t block_bytes,
   return H3C_OK;
 }
 
-}  // namespace
 
-extern "C" {
 
-size_t h3c_update_workspace_bytes(uint32_t n_blocks, uint32_t nchunks, uint64_t chunk_len, uint32_t block_bytes) {
-  if (!block_bytes) return 0;
-  Workspace w{};
-  size_t total = 0;
-  if (layout(nullptr, std::max(n_blocks, 1u), nchunks, (uint32_t)(chunk_len / block_bytes), w, total)) return 0;
-  return total;
+// H3C_UPD_EXACT: raw_exact[c] = the raw CRC of chunk c's bytes (one create launch).
+int exact_checksums(hipStream_t st, int dev, uint8_t type, const uint64_t *chunk_base, uint32_t nchunks,
+                    uint64_t chunk_len, const Workspace &w) {
+  const uint32_t poly = type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
+  const uint64_t seg = std::max<uint64_t>(h3c_rt::pick_seg(chunk_len * nchunks, dev), kMinSegBytes);
+  const uint32_t spc = (uint32_t)((chunk_len + seg - 1) / seg);
+  DevChunk tmpl{};
+  tmpl.len = chunk_len;
+  tmpl.start = 0xFFFFFFFFu;  // ChecksumInfo::create's default starting checksum (raw register)
+  set_fold_consts(tmpl, seg, poly);
+  hipLaunchKernelGGL(upd_exact_desc_kernel, dim3((nchunks + 255) / 256), dim3(256), 0, st, chunk_base, nchunks, spc,
+                     tmpl, w.xdesc);
+  HIP_TRY(hipGetLastError());
+  return h3c_rt::launch_crc(st, dev, type, w.xdesc, nchunks, nchunks * spc, spc, chunk_len * nchunks, seg, 0, w.xseg,
+                            nullptr, w.raw_exact, nullptr, nullptr, -1, 0);
 }
 
-int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nchunks, uint64_t chunk_len,
-                      uint32_t block_bytes, const uint32_t *chunk_raw_in_dev, const uint32_t *blk_chunk_dev,
-                      const uint32_t *blk_index_dev, const void *payload_dev, uint32_t n_blocks,
-                      uint32_t *out_raw_dev, uint32_t *chunk_raw_out_dev, void *workspace_dev,
-                      size_t workspace_bytes, uint32_t *n_invalid_dev, void *stream) {
+int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nchunks, uint64_t chunk_len,
+                       uint32_t block_bytes, const uint32_t *chunk_raw_in_dev, const uint32_t *blk_chunk_dev,
+                       const uint32_t *blk_index_dev, const void *payload_dev, uint32_t n_blocks, uint32_t *out_raw_dev,
+                       uint32_t *chunk_raw_out_dev, void *workspace_dev, size_t workspace_bytes,
+                       uint32_t *n_invalid_dev, uint32_t flags, unsigned long long *counters_dev, void *stream) {
   if (type != H3C_TYPE_CRC32C && type != H3C_TYPE_CRC32) return H3C_ERR_INVALID_ARG;
+  if (flags & ~(uint32_t)H3C_UPD_EXACT) return H3C_ERR_INVALID_ARG;  // raw domain only
   if (!block_bytes || block_bytes % kRowBytes || chunk_len % block_bytes || !nchunks) return H3C_ERR_INVALID_ARG;
   if ((uint64_t)nchunks * (chunk_len / block_bytes) >= 0xFFFFFFFFull || n_blocks == 0xFFFFFFFFu)
     return H3C_ERR_INVALID_ARG;
-  if (!chunk_base_dev || !chunk_raw_in_dev || !chunk_raw_out_dev) return H3C_ERR_INVALID_ARG;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (n_blocks == 0) {
-    HIP_TRY(hipMemcpyAsync(chunk_raw_out_dev, chunk_raw_in_dev, 4ull * nchunks, hipMemcpyDeviceToDevice, st));
-    if (n_invalid_dev) HIP_TRY(hipMemsetAsync(n_invalid_dev, 0, 4, st));
-    return H3C_OK;
-  }
-  if (!blk_chunk_dev || !blk_index_dev || !payload_dev || !out_raw_dev || !workspace_dev)
-    return H3C_ERR_INVALID_ARG;
+  if (!chunk_base_dev || !chunk_raw_in_dev || !chunk_raw_out_dev || !workspace_dev) return H3C_ERR_INVALID_ARG;
+  if (n_blocks && (!blk_chunk_dev || !blk_index_dev || !payload_dev || !out_raw_dev)) return H3C_ERR_INVALID_ARG;
   if (((uintptr_t)payload_dev & 15) != 0) return H3C_ERR_INVALID_ARG;
+  const bool exact = (flags & H3C_UPD_EXACT) != 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int dev = 0;
   int rc = h3c_rt::current_device(&dev);
   if (rc) return rc;
   const uint32_t bpc = (uint32_t)(chunk_len / block_bytes);
   Workspace w{};
   size_t need = 0;
-  rc = layout(workspace_dev, n_blocks, nchunks, bpc, w, need);
+  rc = layout(workspace_dev, std::max(n_blocks, 1u), nchunks, chunk_len, block_bytes, w, need);
   if (rc) return rc;
   if (workspace_bytes < need) {
     h3c_rt::set_error_text("h3c_update_blocks: workspace too small (see h3c_update_workspace_bytes)");
@@ -630,25 +987,51 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
   const PolyConsts *pc = static_cast<const PolyConsts *>(h3c_rt::device_consts(dev, type));
   const uint32_t num_cu = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
   const uint32_t tb = 256, gb = (n_blocks + tb - 1) / tb;
-
-  const bool tiles = use_tiles(n_blocks, nchunks);
-  if (!tiles) {  // sort path: chunks without writes keep raw_in; invalid entries counted atomically
+  const uint32_t poly = type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
+  const uint32_t reuse_case = (uint64_t)block_bytes == chunk_len ? 1u : 0u;  // a block write replaces the chunk
+  const int path = pick_path(n_blocks, nchunks, block_bytes);
+  const uint32_t fused_wg = std::min<uint32_t>(std::min(num_cu, kFusedMaxWG), (n_blocks + kWavesPerBlock - 1) / kWavesPerBlock);
+  // one memset: hash heads, control words, touched flags and the granule rows in use
+  const size_t zero = path == kPathFused ? (size_t)((char *)(w.gran + (size_t)fused_wg * kFusedCols) - (char *)w.hhead)
+                                         : (size_t)((char *)w.gran - (char *)w.hhead);
+  HIP_TRY(hipMemsetAsync(w.hhead, 0, zero, st));
+  const uint32_t *raw_base = chunk_raw_in_dev;
+  if (exact) {
+    rc = exact_checksums(st, dev, type, chunk_base_dev, nchunks, chunk_len, w);
+    if (rc) return rc;
+    raw_base = w.raw_exact;
+  }
+  if (n_blocks == 0) {
     HIP_TRY(hipMemcpyAsync(chunk_raw_out_dev, chunk_raw_in_dev, 4ull * nchunks, hipMemcpyDeviceToDevice, st));
-    HIP_TRY(hipMemsetAsync(w.err, 0, 4, st));
+    hipLaunchKernelGGL(upd_finish_kernel, dim3(1), dim3(256), 0, st, w.ctl, 0u, nchunks, raw_base, chunk_raw_in_dev,
+                       exact ? 1u : 0u, reuse_case, n_invalid_dev, counters_dev);
+    HIP_TRY(hipGetLastError());
+    return H3C_OK;
   }
   // previous-writer links: tile match + hash of per-tile last writers (no sort)
-  HIP_TRY(hipMemsetAsync(w.hhead, 0xFF, 4ull * w.hcap, st));
   const uint32_t nlt = (n_blocks + kLinkTile - 1) / kLinkTile;
   hipLaunchKernelGGL(upd_tlink_kernel, dim3(nlt), dim3(kLinkTile), 0, st, blk_chunk_dev, blk_index_dev, n_blocks,
-                     nchunks, bpc, w.hhead, w.hcap - 1, w.nkey, w.next, w.prev);
+                     nchunks, bpc, w.hhead, w.hcap - 1, w.nkey, w.next, w.prev, w.ctl + kCtlErr, w.touched);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(upd_resolve_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks,
-                     bpc, w.hhead, w.hcap - 1, w.nkey, w.next, w.prev, w.final_of);
-  HIP_TRY(hipGetLastError());
-  size_t tmp = w.tmp_bytes;
   const uint32_t *sh = nullptr;
   rc = shift_table(dev, type, chunk_len, block_bytes, pc, w.sh, st, &sh);
   if (rc) return rc;
+  if (path == kPathFused) {
+    h3c_rt::ProfToken tok;
+    HIP_TRY(h3c_rt::prof_begin(st, tok));
+    hipLaunchKernelGGL(upd_fused_kernel, dim3(fused_wg), dim3(kThreads), 0, st, chunk_base_dev, nchunks, bpc,
+                       blk_chunk_dev, blk_index_dev, static_cast<const uint8_t *>(payload_dev), n_blocks, w.prev,
+                       w.hhead, w.hcap - 1, w.nkey, w.next, sh, pc, raw_base, chunk_raw_in_dev, exact ? 1u : 0u,
+                       reuse_case, w.touched, w.ctl, w.gran, w.scan, out_raw_dev, chunk_raw_out_dev, n_invalid_dev,
+                       counters_dev);
+    HIP_TRY(hipGetLastError());
+    // algorithmic bytes: read new + read old + write back, per block write
+    HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDATE, 3ull * block_bytes * n_blocks));
+    return H3C_OK;
+  }
+  hipLaunchKernelGGL(upd_resolve_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks,
+                     bpc, w.hhead, w.hcap - 1, w.nkey, w.next, w.prev, w.final_of);
+  HIP_TRY(hipGetLastError());
   const uint32_t blocks = std::min<uint32_t>(num_cu, (n_blocks + kWavesPerBlock - 1) / kWavesPerBlock);
   h3c_rt::ProfToken tok;
   HIP_TRY(h3c_rt::prof_begin(st, tok));
@@ -656,26 +1039,25 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
                      blk_chunk_dev, blk_index_dev, static_cast<const uint8_t *>(payload_dev), n_blocks, w.prev,
                      w.final_of, pc, w.delta);
   HIP_TRY(hipGetLastError());
-  // algorithmic bytes: read new + read old + write back, per block write
   HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDATE, 3ull * block_bytes * n_blocks));
-  const uint32_t poly = type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
-  if (tiles) {
+  if (path == kPathTiles) {
     const uint32_t ntiles = (n_blocks + kTile - 1) / kTile;
     hipLaunchKernelGGL(upd_tile_kernel, dim3(ntiles), dim3(kTile), 0, st, blk_chunk_dev, blk_index_dev, n_blocks,
-                       nchunks, bpc, w.delta, sh, poly, w.scan, w.agg, w.tile_invalid);
+                       nchunks, bpc, w.delta, sh, poly, w.scan, w.agg);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(upd_column_kernel, dim3(nchunks), dim3(kTile), 0, st, w.agg, ntiles, nchunks, chunk_raw_in_dev,
-                       w.colpre, chunk_raw_out_dev, w.tile_invalid, n_invalid_dev);
+    hipLaunchKernelGGL(upd_column_kernel, dim3(nchunks), dim3(kTile), 0, st, w.agg, ntiles, nchunks, raw_base,
+                       chunk_raw_in_dev, w.touched, w.colpre, chunk_raw_out_dev);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(upd_apply_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks,
-                       bpc, chunk_raw_in_dev, w.colpre, w.scan, out_raw_dev);
+                       bpc, raw_base, w.colpre, w.scan, out_raw_dev);
     HIP_TRY(hipGetLastError());
   } else {
+    HIP_TRY(hipMemcpyAsync(chunk_raw_out_dev, chunk_raw_in_dev, 4ull * nchunks, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(upd_keys_kernel, dim3(gb), dim3(tb), 0, st, blk_chunk_dev, blk_index_dev, n_blocks, nchunks,
-                       bpc, w.kchunk, w.iota, w.err);
+                       bpc, w.kchunk, w.iota);
     HIP_TRY(hipGetLastError());
     // stable radix sort of (chunk, sequence index) for the per-chunk scan
-    tmp = w.tmp_bytes;
+    size_t tmp = w.tmp_bytes;
     HIP_TRY(rocprim::radix_sort_pairs<SortConfig>(w.tmp, tmp, w.kchunk, w.kchunk_s, w.iota, w.idx2, n_blocks, 0,
                                                   bits_for((uint64_t)nchunks + 1), st));
     hipLaunchKernelGGL(upd_gather_kernel, dim3(gb), dim3(tb), 0, st, w.kchunk_s, w.idx2, n_blocks, nchunks,
@@ -685,11 +1067,49 @@ int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nch
     HIP_TRY(rocprim::inclusive_scan_by_key(w.tmp, tmp, w.kchunk_s, w.vals, w.scan, (size_t)n_blocks, XorOp(),
                                            rocprim::equal_to<uint32_t>(), st));
     hipLaunchKernelGGL(upd_scatter_kernel, dim3(gb), dim3(tb), 0, st, w.kchunk_s, w.idx2, n_blocks, nchunks, w.scan,
-                       chunk_raw_in_dev, out_raw_dev, chunk_raw_out_dev);
+                       raw_base, out_raw_dev, chunk_raw_out_dev);
     HIP_TRY(hipGetLastError());
-    if (n_invalid_dev) HIP_TRY(hipMemcpyAsync(n_invalid_dev, w.err, 4, hipMemcpyDeviceToDevice, st));
+  }
+  if (n_invalid_dev || counters_dev) {
+    hipLaunchKernelGGL(upd_finish_kernel, dim3(1), dim3(256), 0, st, w.ctl, n_blocks, nchunks, raw_base,
+                       chunk_raw_in_dev, exact ? 1u : 0u, reuse_case, n_invalid_dev, counters_dev);
+    HIP_TRY(hipGetLastError());
   }
   return H3C_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t h3c_update_workspace_bytes(uint32_t n_blocks, uint32_t nchunks, uint64_t chunk_len, uint32_t block_bytes) {
+  if (!block_bytes) return 0;
+  Workspace w{};
+  size_t total = 0;
+  if (layout(nullptr, std::max(n_blocks, 1u), nchunks, chunk_len, block_bytes, w, total)) return 0;
+  return total;
+}
+
+int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nchunks, uint64_t chunk_len,
+                      uint32_t block_bytes, const uint32_t *chunk_raw_in_dev, const uint32_t *blk_chunk_dev,
+                      const uint32_t *blk_index_dev, const void *payload_dev, uint32_t n_blocks,
+                      uint32_t *out_raw_dev, uint32_t *chunk_raw_out_dev, void *workspace_dev,
+                      size_t workspace_bytes, uint32_t *n_invalid_dev, void *stream) {
+  return update_blocks_impl(type, chunk_base_dev, nchunks, chunk_len, block_bytes, chunk_raw_in_dev, blk_chunk_dev,
+                            blk_index_dev, payload_dev, n_blocks, out_raw_dev, chunk_raw_out_dev, workspace_dev,
+                            workspace_bytes, n_invalid_dev, 0, nullptr, stream);
+}
+
+int h3c_update_blocks_ex(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nchunks, uint64_t chunk_len,
+                         uint32_t block_bytes, const uint32_t *chunk_raw_in_dev, const uint32_t *blk_chunk_dev,
+                         const uint32_t *blk_index_dev, const void *payload_dev, uint32_t n_blocks,
+                         uint32_t *out_raw_dev, uint32_t *chunk_raw_out_dev, void *workspace_dev,
+                         size_t workspace_bytes, uint32_t *n_invalid_dev, uint32_t flags,
+                         h3c_update_counters *counters_dev, void *stream) {
+  return update_blocks_impl(type, chunk_base_dev, nchunks, chunk_len, block_bytes, chunk_raw_in_dev, blk_chunk_dev,
+                            blk_index_dev, payload_dev, n_blocks, out_raw_dev, chunk_raw_out_dev, workspace_dev,
+                            workspace_bytes, n_invalid_dev, flags,
+                            reinterpret_cast<unsigned long long *>(counters_dev), stream);
 }
 
 }  // extern "C"

@@ -84,6 +84,9 @@ _proto("h3c_update_workspace_bytes", _sz, _u32, _u32, _u64, _u32)
 _proto("h3c_update_blocks", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp)
 _proto("h3c_update_ios", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp)
 _proto("h3c_update_ios_ex", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp)
+_proto("h3c_update_blocks_ex", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp,
+       _u32, _vp, _vp)
+_proto("h3c_test_hook", _int, _int, _u64)
 _proto("h3c_update_ios_dev", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp)
 _proto("h3c_serde_checksum_mark", _u32, _u32, _int)
 _proto("h3c_batch_serde_checksum", _int, _vp, _sz, _vp, _vp, _vp)
@@ -303,23 +306,38 @@ def update_workspace_bytes(n_blocks: int, nchunks: int, chunk_len: int, block_by
 
 def update_blocks(chunk_bases, chunk_len: int, raw_in, blk_chunk, blk_index, payload, out_raw, raw_out,
                   block_bytes: int = 4096, workspace=None, n_invalid=None, type_: int = ChecksumType.CRC32C,
-                  stream=None) -> None:
+                  stream=None, exact: bool = False, counters=None) -> None:
     """Batched ChunkReplica::update + updateChecksum for block-aligned overwrites (h3c_update_blocks).
 
     All tensors are on the GPU: chunk_bases int64[nchunks] (device addresses), raw_in /
     raw_out int32[nchunks], blk_chunk / blk_index int32[n], payload uint8[n*block_bytes],
-    out_raw int32[n] (chunk checksum right after each block write)."""
+    out_raw int32[n] (chunk checksum right after each block write).  `exact` recomputes the
+    chunks' checksums from their bytes first (H3C_UPD_EXACT); `counters` (int64[8] on the GPU,
+    UpdateCounters order) receives the batch's case counts (h3c_update_blocks_ex)."""
     import torch
 
     n, nchunks = blk_chunk.numel(), chunk_bases.numel()
     ws_bytes = update_workspace_bytes(n, nchunks, chunk_len, block_bytes)
     if workspace is None:
         workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=payload.device)
-    _check(lib.h3c_update_blocks(int(type_), chunk_bases.data_ptr(), nchunks, chunk_len, block_bytes,
-                                 raw_in.data_ptr(), blk_chunk.data_ptr(), blk_index.data_ptr(), payload.data_ptr(),
-                                 n, out_raw.data_ptr(), raw_out.data_ptr(), workspace.data_ptr(),
-                                 workspace.numel() * workspace.element_size(),
-                                 n_invalid.data_ptr() if n_invalid is not None else None, _stream_handle(stream)))
+    if counters is not None and (not counters.is_cuda or counters.numel() * counters.element_size() != 64):
+        raise ValueError("counters must be a GPU tensor of 8 x 64-bit")
+    _check(lib.h3c_update_blocks_ex(int(type_), chunk_bases.data_ptr(), nchunks, chunk_len, block_bytes,
+                                    raw_in.data_ptr(), blk_chunk.data_ptr(), blk_index.data_ptr(), payload.data_ptr(),
+                                    n, out_raw.data_ptr(), raw_out.data_ptr(), workspace.data_ptr(),
+                                    workspace.numel() * workspace.element_size(),
+                                    n_invalid.data_ptr() if n_invalid is not None else None,
+                                    UPD_EXACT if exact else 0,
+                                    counters.data_ptr() if counters is not None else None, _stream_handle(stream)))
+
+
+HOOK_SEG_BYTES, HOOK_DEBUG_FLAGS, HOOK_UPD_SCAN = 1, 2, 3  # h3c_test_hook keys
+UPD_SCAN_PATHS = {"default": 0, "fused": 1, "tiles": 2, "sort": 3}
+
+
+def set_test_hook(key: int, value: int) -> None:
+    """h3c_test_hook: force an internal path for tests (0 restores the default)."""
+    _check(lib.h3c_test_hook(int(key), int(value)))
 
 
 # ---------------------------------------------------------------- general updates (h3c_update_ios)

@@ -216,6 +216,7 @@ PATTERN_CEILING = {
     "seg_crc_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
     "seg_quad_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
     "upd_delta_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
+    "upd_fused_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
     "uio_block_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
 }
 
@@ -352,19 +353,22 @@ def run_update(args, cx: Ctx) -> dict:
     bases = torch.arange(nchunks, dtype=torch.int64, device=cx.dev) * clen + chunks.data_ptr()
     out = torch.zeros(nw, dtype=torch.int32, device=cx.dev)
     ws = torch.empty(h3c.update_workspace_bytes(nw, nchunks, clen, G), dtype=torch.uint8, device=cx.dev)
+    ctr = torch.zeros(8, dtype=torch.int64, device=cx.dev)
+    exact = bool(getattr(args, "exact", False))
     cur = [0]
 
     def step():  # apply the batch again on top of the previous state: same traffic, new checksums
         i = cur[0]
         h3c.update_blocks(bases, clen, raw[i], wc, wb, payload, out, raw[1 - i], block_bytes=G, workspace=ws,
-                          stream=cx.stream)
+                          stream=cx.stream, exact=exact, counters=ctr)
         cur[0] = 1 - i
 
     elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDATE)
     fresh = torch.zeros(nchunks, dtype=torch.int32, device=cx.dev)
     plan.run(fresh, stream=cx.stream)
     torch.cuda.synchronize()
-    verified = cx.all_true(bool(torch.equal(fresh, raw[cur[0]])))
+    counters = dict(zip((f for f, _ in h3c.UpdateCounters._fields_), ctr.cpu().tolist()))
+    verified = cx.all_true(bool(torch.equal(fresh, raw[cur[0]])) and counters["read_chunk"] == nw)
     plan.close()
     writes = nw * args.steps * cx.world
     res = {
@@ -375,11 +379,13 @@ def run_update(args, cx: Ctx) -> dict:
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (splitmix64 chunks and payloads in HBM, seeded uniform chunk/offset)",
-        "config": {"workload": f"BASELINE config 3: {nw} random 4 KiB writes into {nchunks} x 64 MiB chunks per GPU",
-                   "parallelism": f"shard{cx.world}"},
+        "config": {"workload": f"BASELINE config 3: {nw} random 4 KiB writes into {nchunks} x 64 MiB chunks per GPU"
+                               + (" (H3C_UPD_EXACT: the chunks re-CRC'd from their bytes every step)" if exact else ""),
+                   "parallelism": f"shard{cx.world}", "exact": exact},
         "verified": verified,
+        "counters": counters,
         "algorithmic_gbps": round(writes * 3 * G / elapsed / 1e9, 1),
-        "roofline": roofline(prof, HBM_PEAK_GBPS, kernel="upd_delta_kernel"),
+        "roofline": roofline(prof, HBM_PEAK_GBPS, kernel="upd_fused_kernel"),
     }
     if cx.world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_update()

@@ -136,8 +136,10 @@ int h3c_batch_combine(uint8_t type, const uint32_t *c1_dev, const uint32_t *c2_d
  * block_bytes is a multiple of 1024 (3FS writes are 4 KiB-aligned, kAIOAlignSize).
  * A multi-block write is expanded by the caller into consecutive block writes; its
  * checksum is out_raw of its last block.  Out-of-range entries have no effect,
- * out_raw 0, and are counted in *n_invalid_dev (optional).  The chunk bytes are
- * updated in place.  All arrays are device memory; nothing is synchronised. */
+ * out_raw 0, and are counted in *n_invalid_dev (optional).  Chunks no write reaches keep
+ * chunk_raw_in.  The chunk bytes are updated in place.  All arrays are device memory;
+ * nothing is synchronised.  The stored checksums are trusted; h3c_update_blocks_ex
+ * (below) has the exact mode and the case counters. */
 size_t h3c_update_workspace_bytes(uint32_t n_blocks, uint32_t nchunks, uint64_t chunk_len, uint32_t block_bytes);
 int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nchunks, uint64_t chunk_len,
                       uint32_t block_bytes, const uint32_t *chunk_raw_in_dev, const uint32_t *blk_chunk_dev,
@@ -264,6 +266,23 @@ int h3c_update_ios_dev(uint8_t poly_type, h3c_chunk_state *chunks_dev, uint32_t 
                        uint32_t n, h3c_update_result *results_dev, uint32_t flags, h3c_update_counters *counters_dev,
                        void *stream);
 
+/* h3c_update_blocks with flags and counters.  flags: H3C_UPD_EXACT recomputes each chunk's
+ * checksum from its bytes before the writes (one create pass over the chunk set), so every
+ * out_raw / chunk_raw_out equals what updateChecksum case (iv) computes by re-reading the
+ * chunk (ChunkReplica.cc:356-390) even where chunk_raw_in disagrees with the bytes; chunks no
+ * write reaches keep chunk_raw_in, as the reference leaves their metadata alone.  Without it the
+ * stored checksums are trusted (r' = r ^ delta; a stale r stays stale by its own error).
+ * H3C_UPD_STD_DOMAIN is not accepted (the block path is raw).  counters_dev (device, may be
+ * NULL) receives the batch's case counts: read_chunk per valid block write (reuse when a block
+ * is the whole chunk), invalid entries, and with H3C_UPD_EXACT the stale chunks.
+ * Asynchronous like h3c_update_blocks. */
+int h3c_update_blocks_ex(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nchunks, uint64_t chunk_len,
+                         uint32_t block_bytes, const uint32_t *chunk_raw_in_dev, const uint32_t *blk_chunk_dev,
+                         const uint32_t *blk_index_dev, const void *payload_dev, uint32_t n_blocks,
+                         uint32_t *out_raw_dev, uint32_t *chunk_raw_out_dev, void *workspace_dev,
+                         size_t workspace_bytes, uint32_t *n_invalid_dev, uint32_t flags,
+                         h3c_update_counters *counters_dev, void *stream);
+
 /* ---- adjacent formats on the same kernels ---- */
 
 /* RPC message checksum, Checksum::calcSerde (src/common/net/MessageHeader.h:32-37):
@@ -355,6 +374,16 @@ enum h3c_prof_kind {
 };
 void h3c_profile_enable(int on);
 int h3c_profile_read(int kind, double *ms, uint64_t *launches, uint64_t *bytes, int reset);
+
+/* Test hooks: force internal paths so tests can cover each one.  The environment variables
+ * of the same names set the initial values once, when the library loads; no entry point reads
+ * the environment per call.  value 0 restores the default. */
+enum h3c_hook {
+  H3C_HOOK_SEG_BYTES = 1,   /* segment size of the create / verify kernels (multiple of 1 KiB) */
+  H3C_HOOK_DEBUG_FLAGS = 2, /* bit0: no pipelined row loop; bit1: no small-chunk kernel */
+  H3C_HOOK_UPD_SCAN = 3     /* h3c_update_blocks: 1 fused, 2 dense tiles, 3 sort + scan_by_key */
+};
+int h3c_test_hook(int key, uint64_t value);
 
 #ifdef __cplusplus
 }

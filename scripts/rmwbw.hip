@@ -1,10 +1,14 @@
 // Memory-ceiling probe for the partial-update pattern (upd_delta_kernel): per 4 KiB block
 // write, read the payload (sequential over the batch), read the old slot (random 4 KiB in a
 // 4 GiB chunk set) and write the payload into the slot.  Variants isolate each stream.
+// `ord` (optional) processes the writes in another order: "sorted" walks them in slot address
+// order (payload reads become random), "sorted+seqpay" also lays the payloads out in that order
+// (the ceiling of an address-ordered pass with staged payloads).
 // Build: hipcc --offload-arch=gfx950 -O3 -o scripts/rmwbw scripts/rmwbw.hip
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <random>
 #include <vector>
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -13,7 +17,7 @@ typedef v4u __attribute__((address_space(1))) *gv4p;
 // MODE bit0: read payload, bit1: read slot, bit2: write slot.  INF blocks in flight per wave.
 template <int MODE, int INF>
 __global__ __launch_bounds__(1024) void rmw(const char *pay, char *region, const uint32_t *slot, uint32_t n,
-                                            uint32_t *out) {
+                                            uint32_t *out, const uint32_t *ord) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
@@ -23,7 +27,7 @@ __global__ __launch_bounds__(1024) void rmw(const char *pay, char *region, const
     v4u a[INF][4], b[INF][4];
 #pragma unroll
     for (int f = 0; f < INF; ++f) {
-      const uint32_t k = min(i + f, hi - 1);
+      const uint32_t k0 = min(i + f, hi - 1), k = ord ? ord[k0] : k0;
       const char *p = pay + (uint64_t)k * 4096 + 16 * lane;
       const char *s = region + (uint64_t)slot[k] * 4096 + 16 * lane;
 #pragma unroll
@@ -35,7 +39,7 @@ __global__ __launch_bounds__(1024) void rmw(const char *pay, char *region, const
 #pragma unroll
     for (int f = 0; f < INF; ++f) {
       if (i + f >= hi) break;
-      char *s = region + (uint64_t)slot[i + f] * 4096 + 16 * lane;
+      char *s = region + (uint64_t)slot[ord ? ord[i + f] : i + f] * 4096 + 16 * lane;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (MODE & 2) acc ^= b[f][u];
@@ -65,6 +69,16 @@ int main() {
   std::mt19937 rng(20250629);
   for (auto &x : hs) x = rng() % nslots;
   hipMemcpy(slot, hs.data(), 4ull * n, hipMemcpyHostToDevice);
+  // address order, and the same slots pre-sorted (payload sequential in that order)
+  std::vector<uint32_t> ho(n), hsorted(hs);
+  for (uint32_t i = 0; i < n; ++i) ho[i] = i;
+  std::stable_sort(ho.begin(), ho.end(), [&](uint32_t x, uint32_t y) { return hs[x] < hs[y]; });
+  std::sort(hsorted.begin(), hsorted.end());
+  uint32_t *ord, *slot_sorted;
+  hipMalloc(&ord, 4ull * n);
+  hipMalloc(&slot_sorted, 4ull * n);
+  hipMemcpy(ord, ho.data(), 4ull * n, hipMemcpyHostToDevice);
+  hipMemcpy(slot_sorted, hsorted.data(), 4ull * n, hipMemcpyHostToDevice);
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   hipEvent_t a, b;
@@ -87,9 +101,10 @@ int main() {
     char nm[96];
     snprintf(nm, sizeof nm, "[%2d waves/CU]", wpc);
     printf("%s\n", nm);
-#define R(MODE, INF, BYTES, LABEL)                                                        \
+#define RO(MODE, INF, BYTES, LABEL, SLOT, ORD)                                             \
   snprintf(nm, sizeof nm, "  %-22s inf%d", LABEL, INF);                                    \
-  run(nm, BYTES, [&] { rmw<MODE, INF><<<dim3(cus), dim3(64 * wpc)>>>(pay, region, slot, n, o); });
+  run(nm, BYTES, [&] { rmw<MODE, INF><<<dim3(cus), dim3(64 * wpc)>>>(pay, region, SLOT, n, o, ORD); });
+#define R(MODE, INF, BYTES, LABEL) RO(MODE, INF, BYTES, LABEL, slot, nullptr)
     R(7, 1, 12288, "rmw (pay+old+write)")
     R(7, 2, 12288, "rmw (pay+old+write)")
     R(3, 1, 8192, "read pay+old")
@@ -99,6 +114,12 @@ int main() {
     R(4, 1, 4096, "write slot only")
     R(2, 1, 4096, "read old only")
     R(1, 1, 4096, "read pay only")
+    RO(7, 1, 12288, "rmw sorted", slot, ord)
+    RO(7, 2, 12288, "rmw sorted", slot, ord)
+    RO(7, 1, 12288, "rmw sorted+seqpay", slot_sorted, nullptr)
+    RO(7, 2, 12288, "rmw sorted+seqpay", slot_sorted, nullptr)
+    RO(4, 1, 4096, "write sorted only", slot_sorted, nullptr)
+    RO(6, 1, 8192, "read old+write sorted", slot_sorted, nullptr)
   }
   return 0;
 }

@@ -26,3 +26,18 @@ def orc():
     import oracle_lib
 
     return oracle_lib
+
+
+@pytest.fixture
+def hooks(h3c):
+    """set(key, value) forces an engine path through h3c_test_hook; every key set is reset to
+    its default when the test ends."""
+    used = []
+
+    def set_(key, value):
+        used.append(key)
+        h3c.set_test_hook(key, value)
+
+    yield set_
+    for k in used:
+        h3c.set_test_hook(k, 0)

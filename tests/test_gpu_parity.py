@@ -249,11 +249,11 @@ def test_profile_counters(h3c, torch_dev):
 
 @pytest.mark.parametrize("seg", [1024, 4096, 16384, 65536, 262144])
 @pytest.mark.parametrize("dbg", [0, 1])
-def test_forced_segment_sizes_and_paths(h3c, torch_dev, seg, dbg, monkeypatch):
+def test_forced_segment_sizes_and_paths(h3c, torch_dev, seg, dbg, hooks):
     """Every segment size and both row-loop paths (pipelined / single-row) agree with the oracle."""
     torch, dev = torch_dev
-    monkeypatch.setenv("H3C_SEG_BYTES", str(seg))
-    monkeypatch.setenv("H3C_DEBUG_FLAGS", str(dbg))
+    hooks(h3c.HOOK_SEG_BYTES, seg)
+    hooks(h3c.HOOK_DEBUG_FLAGS, dbg)
     rng = np.random.default_rng(seg + dbg)
     sizes = [1, 17, 1024, 4096, 5120, 6144, 7168, 9216, 12345, 16384, 16385, 65543, 262144 + 1000,
              (1 << 20) + 3, 3 << 20]
@@ -269,11 +269,11 @@ def test_forced_segment_sizes_and_paths(h3c, torch_dev, seg, dbg, monkeypatch):
 
 
 @pytest.mark.parametrize("flags", ["0", "2"])
-def test_small_chunk_batches(h3c, torch_dev, monkeypatch, flags):
+def test_small_chunk_batches(h3c, torch_dev, hooks, flags):
     """Batches whose every chunk is one short segment run seg_small_kernel (flags 0); flags 2
     (H3C_DEBUG_FLAGS bit1) forces the general kernel on the same batches.  Sizes 1 B..7 KiB at
     every alignment, device-resident and host-staged, create and verify."""
-    monkeypatch.setenv("H3C_DEBUG_FLAGS", flags)
+    hooks(h3c.HOOK_DEBUG_FLAGS, int(flags, 0))
     torch, dev = torch_dev
     rng = np.random.default_rng(41)
     host = rng.integers(0, 256, 8 << 20, dtype=np.uint8)

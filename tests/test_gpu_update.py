@@ -31,12 +31,20 @@ def i32(arr, torch, dev):
     return torch.from_numpy(np.ascontiguousarray(np.asarray(arr, dtype=np.uint32)).view(np.int32)).to(dev)
 
 
-def run_case(h3c, torch, dev, nchunks, chunk_len, writes, seed, replay_chunks=None, invalid=()):
-    """writes: list of (chunk, first_block, nblocks).  Returns (ok, details)."""
+def run_case(h3c, torch, dev, nchunks, chunk_len, writes, seed, replay_chunks=None, invalid=(), stale=None,
+             exact=False):
+    """writes: list of (chunk, first_block, nblocks).  stale: {chunk: error} XORed into the
+    stored checksum (bit rot / a torn write): the oracle replays the reference literally, whose
+    case (iv) re-reads the chunk; exact mode must match it, trusted mode must be off by exactly
+    the stored error (a uniform-length chunk's error is never shifted)."""
     rng = np.random.default_rng(seed)
     bpc = chunk_len // G
     chunks = rng.integers(0, 256, (nchunks, chunk_len), dtype=np.uint8)
-    raw0 = np.array([orc.crc32c(chunks[c]) for c in range(nchunks)], dtype=np.uint32)
+    true0 = np.array([orc.crc32c(chunks[c]) for c in range(nchunks)], dtype=np.uint32)
+    err = np.zeros(nchunks, dtype=np.uint32)
+    for c, e in (stale or {}).items():
+        err[c] = e
+    raw0 = true0 ^ err
     # expand writes into block writes (sequence order); last block index of each write
     blk_chunk, blk_index, last_of_write = [], [], []
     for (c, b0, nb) in writes:
@@ -55,10 +63,11 @@ def run_case(h3c, torch, dev, nchunks, chunk_len, writes, seed, replay_chunks=No
     bases = torch.tensor([dchunks[c].data_ptr() for c in range(nchunks)], dtype=torch.int64, device=dev)
     out = torch.zeros(n, dtype=torch.int32, device=dev)
     raw_out = torch.zeros(nchunks, dtype=torch.int32, device=dev)
-    ninv = torch.zeros(1, dtype=torch.int32, device=dev)
+    ninv = torch.full((1,), -1, dtype=torch.int32, device=dev)
+    ctr = torch.full((8,), -1, dtype=torch.int64, device=dev)
     h3c.update_blocks(bases, chunk_len, i32(raw0, torch, dev), i32(blk_chunk, torch, dev),
                       i32(blk_index, torch, dev), torch.from_numpy(payload).to(dev), out, raw_out,
-                      block_bytes=G, n_invalid=ninv)
+                      block_bytes=G, n_invalid=ninv, exact=exact, counters=ctr)
     torch.cuda.synchronize()
     got = u32(out)
     got_final = u32(raw_out)
@@ -87,25 +96,33 @@ def run_case(h3c, torch, dev, nchunks, chunk_len, writes, seed, replay_chunks=No
                                               chunk_len, off == chunk_len, host[c])
             assert rc == 0
             want[idx[-1]] = meta[c]["value"]
-    bad = [(k, hex(int(got[k])), hex(v)) for k, v in want.items() if int(got[k]) != v]
+    off_by = {} if exact else {k: int(err[blk_chunk[k]]) for k in want}  # trusted: the stored error persists
+    bad = [(k, hex(int(got[k])), hex(v)) for k, v in want.items() if int(got[k]) != v ^ off_by.get(k, 0)]
     assert not bad, bad[:10]
     assert np.array_equal(got_chunks, host), "chunk bytes after write-back"
+    touched = {c for c, b in zip(blk_chunk, blk_index) if c < nchunks and b < bpc}
     for c in range(nchunks):
-        assert int(got_final[c]) == orc.crc32c(host[c]), c
+        if c in touched:
+            assert int(got_final[c]) == orc.crc32c(host[c]) ^ (0 if exact else int(err[c])), c
+        else:  # no write reached it: the stored value stays, stale or not
+            assert int(got_final[c]) == int(raw0[c]), c
     for k, v in enumerate(valid):
         if not v:
             assert int(got[k]) == 0
-    assert int(ninv.item()) == sum(1 for v in valid if not v)
+    n_bad = sum(1 for v in valid if not v)
+    assert int(ninv.item()) == n_bad
+    n_ok = len(valid) - n_bad
+    reuse = chunk_len == G
+    assert ctr.cpu().tolist() == [0, n_ok if reuse else 0, 0, 0 if reuse else n_ok, 0, 0, n_bad,
+                                  int((err != 0).sum()) if exact else 0]
 
 
-@pytest.fixture(params=["tiles", "sort"])
-def scan_mode(request, monkeypatch):
-    """Both per-chunk scan paths: dense tiles (default at these sizes) and the rocPRIM
-    sort + scan_by_key fallback for many chunks (forced by H3C_UPD_SCAN=sort)."""
-    if request.param == "sort":
-        monkeypatch.setenv("H3C_UPD_SCAN", "sort")
-    else:
-        monkeypatch.delenv("H3C_UPD_SCAN", raising=False)
+@pytest.fixture(params=["fused", "tiles", "sort"])
+def scan_mode(request, h3c, hooks):
+    """Every per-chunk scan path: the fused launch (default for 4 KiB blocks and <= 128 chunks),
+    dense tiles, and the rocPRIM sort + scan_by_key fallback for many chunks (forced through
+    h3c_test_hook)."""
+    hooks(h3c.HOOK_UPD_SCAN, h3c.UPD_SCAN_PATHS[request.param])
     return request.param
 
 
@@ -137,6 +154,41 @@ def test_update_single_slot_hammer(h3c, torch_dev, scan_mode):
     """Every write hits one slot: the longest possible previous-writer chain."""
     torch, dev = torch_dev
     run_case(h3c, torch, dev, 2, 64 << 10, [(1, 5, 1)] * 700 + [(0, 15, 1)] * 3, seed=5)
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_update_blocks_stale_stored_checksums(h3c, torch_dev, scan_mode, exact):
+    """Stored checksums that disagree with the bytes, through every scan
+    path: H3C_UPD_EXACT reproduces the reference's case (iv) re-read exactly; trusted mode
+    carries each chunk's stored error unchanged; chunks no write reaches keep their value."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(61 + exact)
+    nchunks, chunk_len = 9, 128 << 10
+    writes = [(int(rng.integers(0, nchunks - 1)), int(rng.integers(0, 31)), int(rng.integers(1, 3)))
+              for _ in range(700)]  # chunk 8 gets no write
+    stale = {c: int(rng.integers(1, 1 << 32)) for c in (0, 3, 5, 8)}
+    run_case(h3c, torch, dev, nchunks, chunk_len, writes, seed=62, stale=stale, exact=exact,
+             invalid=[(9, (nchunks, 0)), (400, (2, 32))])
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_update_blocks_whole_chunk_reuse_case(h3c, torch_dev, exact):
+    """block_bytes == chunk_len: every write replaces the chunk, updateChecksum's reuse case
+    (ChunkReplica.cc:337-339) -- the client checksum, i.e. the payload's CRC in exact mode."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(71)
+    writes = [(int(rng.integers(0, 5)), 0, 1) for _ in range(300)]
+    run_case(h3c, torch, dev, 5, G, writes, seed=72, stale={1: 0x1234, 4: 0xFFFF0000}, exact=exact)
+
+
+def test_update_blocks_large_chunk_count_paths(h3c, torch_dev, hooks):
+    """200 chunks (beyond the fused path's 128 columns): tiles by default, sort when forced."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(81)
+    writes = [(int(rng.integers(0, 200)), int(rng.integers(0, 16)), 1) for _ in range(3000)]
+    run_case(h3c, torch, dev, 200, 64 << 10, writes, seed=82, stale={7: 5}, exact=True)
+    hooks(h3c.HOOK_UPD_SCAN, h3c.UPD_SCAN_PATHS["sort"])
+    run_case(h3c, torch, dev, 200, 64 << 10, writes, seed=83, stale={9: 5}, exact=True)
 
 
 def test_update_config3_shape_full_size(h3c, torch_dev):
