@@ -154,6 +154,12 @@ int h3c_combine_fold(const uint8_t *types, const uint32_t *values, const uint64_
 
 int h3c_batch_read_result(uint8_t batch_type, const h3c_read_job *jobs, size_t n, uint8_t *out_type,
                           uint32_t *out_value, uint32_t *status, void *stream) {
+  return h3c_batch_read_result_ex(batch_type, jobs, n, out_type, out_value, status, nullptr, stream);
+}
+
+int h3c_batch_read_result_ex(uint8_t batch_type, const h3c_read_job *jobs, size_t n, uint8_t *out_type,
+                             uint32_t *out_value, uint32_t *status, uint64_t *n_checksum_mismatch, void *stream) {
+  if (n_checksum_mismatch) *n_checksum_mismatch = 0;
   if (n == 0) return H3C_OK;
   if (!jobs || !out_type || !out_value || !status) return H3C_ERR_INVALID_ARG;
   if (batch_type > H3C_TYPE_CRC32) return H3C_ERR_INVALID_ARG;
@@ -192,8 +198,10 @@ int h3c_batch_read_result(uint8_t batch_type, const h3c_read_job *jobs, size_t n
       out_type[i] = t[compute_at[i]];
       out_value[i] = v[compute_at[i]];
     }
-    if (recalc_at[i] >= 0 && (t[recalc_at[i]] != j.chunk_type || v[recalc_at[i]] != j.chunk_value))
+    if (recalc_at[i] >= 0 && (t[recalc_at[i]] != j.chunk_type || v[recalc_at[i]] != j.chunk_value)) {
       status[i] = H3C_ERR_CHECKSUM_MISMATCH;  // :45-53
+      if (n_checksum_mismatch) ++*n_checksum_mismatch;  // storage.aio.checksum_mismatch (:14, :46)
+    }
   }
   return H3C_OK;
 }

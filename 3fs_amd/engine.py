@@ -96,6 +96,7 @@ _proto("h3c_batch_std_crc32c", _int, _vp, _sz, _vp, _vp, _vp)
 _proto("h3c_checksum_combine", _int, ctypes.POINTER(_u8), ctypes.POINTER(_u32), _u8, _u32, _u64)
 _proto("h3c_combine_fold", _int, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp)
 _proto("h3c_batch_read_result", _int, _u8, _vp, _sz, _vp, _vp, _vp, _vp)
+_proto("h3c_batch_read_result_ex", _int, _u8, _vp, _sz, _vp, _vp, _vp, _vp, _vp)
 _proto("h3c_crc32c", _int, _vp, _sz, _u32, ctypes.POINTER(_u32), _vp)
 _proto("h3c_crc32", _int, _vp, _sz, _u32, ctypes.POINTER(_u32), _vp)
 _proto("h3c_hostfed_create", _int, _int, _u64, ctypes.POINTER(_vp))
@@ -424,11 +425,13 @@ READ_JOB_DTYPE = np.dtype([("data", "<u8"), ("length", "<u8"), ("chunk_len", "<u
 assert READ_JOB_DTYPE.itemsize == 40
 
 
-def read_results(batch_type: int, jobs: Sequence, stream=None):
+def read_results(batch_type: int, jobs: Sequence, stream=None, counters: Optional[dict] = None):
     """AioReadJob::setResult (BatchReadJob.cc:24-55) for a batch of completed reads.
 
     jobs[i] = (data, length, chunk_len, offset, stored ChecksumInfo, recalculate).  Returns
-    (list of result ChecksumInfo, status uint32[n]: 0 or 4080 from the recalculate check)."""
+    (list of result ChecksumInfo, status uint32[n]: 0 or 4080 from the recalculate check).
+    `counters` (a dict) receives "checksum_mismatch": the reference's
+    storage.aio.checksum_mismatch count for the batch (BatchReadJob.cc:14)."""
     arr = np.zeros(len(jobs), dtype=READ_JOB_DTYPE)
     keep = []
     for i, (data, length, chunk_len, offset, ck, recalc) in enumerate(jobs):
@@ -441,8 +444,11 @@ def read_results(batch_type: int, jobs: Sequence, stream=None):
     ot = np.zeros(n, dtype=np.uint8)
     ov = np.zeros(n, dtype=np.uint32)
     st = np.zeros(n, dtype=np.uint32)
-    _check(lib.h3c_batch_read_result(int(batch_type), arr.ctypes.data, n, ot.ctypes.data, ov.ctypes.data,
-                                     st.ctypes.data, _stream_handle(stream)))
+    mis = _u64(0)
+    _check(lib.h3c_batch_read_result_ex(int(batch_type), arr.ctypes.data, n, ot.ctypes.data, ov.ctypes.data,
+                                        st.ctypes.data, ctypes.byref(mis), _stream_handle(stream)))
+    if counters is not None:
+        counters["checksum_mismatch"] = int(mis.value)
     del keep
     return [ChecksumInfo(ChecksumType(int(a)), int(b)) for a, b in zip(ot, ov)], st
 

@@ -333,6 +333,11 @@ typedef struct h3c_read_job {
  * difference sets status[i] = H3C_ERR_CHECKSUM_MISMATCH (4080). */
 int h3c_batch_read_result(uint8_t batch_type, const h3c_read_job *jobs, size_t n, uint8_t *out_type,
                           uint32_t *out_value, uint32_t *status, void *stream);
+/* The same, also counting the recalculation mismatches (the reference's
+ * storage.aio.checksum_mismatch counter, BatchReadJob.cc:14, :46) into *n_checksum_mismatch
+ * (may be NULL). */
+int h3c_batch_read_result_ex(uint8_t batch_type, const h3c_read_job *jobs, size_t n, uint8_t *out_type,
+                             uint32_t *out_value, uint32_t *status, uint64_t *n_checksum_mismatch, void *stream);
 
 /* ---- host-fed pipeline (payloads in host memory, BASELINE config 5) ---- */
 

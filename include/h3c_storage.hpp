@@ -118,8 +118,9 @@ struct ReadJob {
 
 // AioReadJob::setResult's checksum selection + recalculate verify for a batch.
 struct BatchReadResults {
+  // checksumMismatch (optional) += the batch's storage.aio.checksum_mismatch count (BatchReadJob.cc:14).
   static int setResults(ChecksumType batchType, bool recalculateChecksum, const std::vector<ReadJob> &jobs,
-                        std::vector<IOResult> &results, void *stream = nullptr) {
+                        std::vector<IOResult> &results, void *stream = nullptr, uint64_t *checksumMismatch = nullptr) {
     std::vector<h3c_read_job> j(jobs.size());
     for (size_t i = 0; i < jobs.size(); ++i)
       j[i] = h3c_read_job{jobs[i].data, jobs[i].length, jobs[i].chunkLen, jobs[i].offset, jobs[i].chunkChecksum.value,
@@ -127,8 +128,11 @@ struct BatchReadResults {
                           (uint8_t)(recalculateChecksum ? 1 : 0), {0, 0, 0, 0, 0}};
     std::vector<uint8_t> t(jobs.size());
     std::vector<uint32_t> v(jobs.size()), st(jobs.size());
-    const int rc = h3c_batch_read_result((uint8_t)batchType, j.data(), j.size(), t.data(), v.data(), st.data(), stream);
+    uint64_t mis = 0;
+    const int rc = h3c_batch_read_result_ex((uint8_t)batchType, j.data(), j.size(), t.data(), v.data(), st.data(), &mis,
+                                            stream);
     if (rc != H3C_OK) return rc;
+    if (checksumMismatch) *checksumMismatch += mis;
     results.resize(jobs.size());
     for (size_t i = 0; i < jobs.size(); ++i)
       results[i] = IOResult{st[i], jobs[i].length, ChecksumInfo{(ChecksumType)t[i], v[i]}, jobs[i].chunkLen};

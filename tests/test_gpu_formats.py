@@ -138,10 +138,14 @@ def test_read_results_match_setresult_oracle(h3c, torch_dev):
         jobs.append((bt, (dd, ln, cl, off, h3c.ChecksumInfo(h3c.ChecksumType(ctype), stored), recalc)))
     for bt in (orc.NONE, orc.CRC32C, orc.CRC32):
         idx = [i for i, (b, _) in enumerate(jobs) if b == bt]
-        infos, st = h3c.read_results(bt, [jobs[i][1] for i in idx])
+        ctr = {}
+        infos, st = h3c.read_results(bt, [jobs[i][1] for i in idx], counters=ctr)
         for k, i in enumerate(idx):
             rc, t, v = want[i]
             assert (int(st[k]), int(infos[k].type), infos[k].value) == (rc, t, v), i
+        # storage.aio.checksum_mismatch (BatchReadJob.cc:14, :46): one per 4080
+        assert ctr["checksum_mismatch"] == sum(1 for i in idx if want[i][0] == 4080)
+    assert any(w[0] == 4080 for w in want)
 
 
 def test_scalar_folly_shaped_entry_points(h3c, torch_dev):

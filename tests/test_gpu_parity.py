@@ -306,3 +306,31 @@ def test_small_chunk_batches(h3c, torch_dev, hooks, flags):
     for k in range(0, 2048, 97):
         assert int(got[k]) == orc.crc32c(host[k * 4096:(k + 1) * 4096])
     plan.close()
+
+
+def test_plan_verify_4mib_chunks_config4_shape(h3c, torch_dev):
+    """BASELINE config 4's chunk size in one process: 64 x 4 MiB splitmix chunks through a
+    device-resident Plan verify, with flips at the first, last and middle bytes; every chunk's
+    raw checksum and ok flag against the oracle."""
+    torch, dev = torch_dev
+    n, clen, seed = 64, 4 << 20, 404
+    buf = torch.empty(n * clen, dtype=torch.uint8, device=dev)
+    h3c.fill_splitmix(buf, clen, n, clen, seed)
+    expected = np.array([orc.crc32c(orc.splitmix_bytes(clen, seed, c)) for c in range(n)], dtype=np.uint32)
+    flips = {0: 0, 9: clen - 1, 33: clen // 2 + 5}
+    want = expected.copy()
+    for c, off in flips.items():
+        buf[c * clen + off] = buf[c * clen + off] ^ 0x40
+        d = orc.splitmix_bytes(clen, seed, c)
+        d[off] ^= 0x40
+        want[c] = orc.crc32c(d)
+    plan = h3c.Plan.uniform(buf.data_ptr(), clen, n)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    mis = torch.zeros(1, dtype=torch.int32, device=dev)
+    plan.run(out, expected=torch.from_numpy(expected.view(np.int32)).to(dev), ok=ok, mismatch=mis)
+    torch.cuda.synchronize()
+    plan.close()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(flips)
+    assert int(mis.item()) == len(flips)
