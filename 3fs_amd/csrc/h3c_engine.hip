@@ -28,13 +28,17 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "h3c_crc.h"
@@ -1254,6 +1258,8 @@ int h3c_plan_run(h3c_plan *p, const uint32_t *expected_raw_dev, uint32_t *out_ra
 // and run the kernels on the caller's stream.  Neither lease allocates in steady state,
 // so concurrent callers on their own streams never force a device-wide synchronisation
 // (hipMalloc / hipFree would; hipMallocAsync pools are not used, see DeviceLease).
+constexpr uint64_t kZeroCopyMin = 64u << 10;  // pinned payloads above this are read in place
+
 static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uint8_t *out_type, uint32_t *out_raw,
                       uint8_t *ok, uint64_t *n_mismatch, void *stream) {
   if (n == 0) {
@@ -1270,6 +1276,20 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
   uint64_t host_bytes = 0;
   for (auto &x : dd) {
     const bool crc = x.ptr && x.len && (x.type == H3C_TYPE_CRC32C || x.type == H3C_TYPE_CRC32);
+    if (crc && x.mem == H3C_MEM_HOST_PINNED && x.len > kZeroCopyMin) {
+      // page-locked host memory the device can address (hipHostMalloc / hipHostRegister, e.g.
+      // RDMA buffers): the kernels read it in place over PCIe, no staging copy.  Small buffers
+      // are staged anyway (a few 1 KiB rows per chunk over PCIe are latency-bound: 34 us for
+      // 32 x 4 KiB read in place against ~5 us copied, profiles/r02_sync_*); memory the runtime
+      // does not know as pinned is staged like pageable memory.
+      void *dp = nullptr;
+      if (hipHostGetDevicePointer(&dp, const_cast<void *>(x.ptr), 0) == hipSuccess && dp) {
+        x.ptr = dp;
+        x.mem = H3C_MEM_DEVICE;
+      } else {
+        (void)hipGetLastError();
+      }
+    }
     if (crc && x.mem != H3C_MEM_DEVICE) host_bytes += (x.len + 255) & ~uint64_t(255);
   }
   const uint64_t seg_bytes = forced_seg(pick_seg_for(d, n, g_dev[dev].num_cu));
@@ -1285,29 +1305,24 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
     rc = layout_groups(probe.data(), n, seg_bytes, gl);
     if (rc) return rc;
   }
+  // one layout for the device arena and the pinned staging buffer, so that everything going
+  // up is one copy and everything coming back is one copy:
+  //   [staged payloads | DevChunk lists | expected | mismatch | results out | ok] [segment partials]
+  //   |<--------------------- H2D ----------------------------->|<------- D2H ------->|
   const uint64_t off_chunks0 = align(off_stage + host_bytes);
   const uint64_t off_chunks1 = align(off_chunks0 + gl.hc[0].size() * sizeof(DevChunk));
-  const uint64_t off_seg = align(off_chunks1 + gl.hc[1].size() * sizeof(DevChunk));
-  const uint64_t off_out = align(off_seg + 4ull * std::max(gl.segs[0], gl.segs[1]));
-  const uint64_t off_exp = align(off_out + 4ull * n);
-  const uint64_t off_ok = align(off_exp + (expected ? 4ull * n : 0));
-  const uint64_t off_mis = align(off_ok + (expected ? n : 0));
-  const uint64_t arena_bytes = off_mis + 256;
-  char *arena = nullptr;
-  // pinned staging: [host payloads | expected | DevChunk lists | results out | ok | mismatch]
-  const uint64_t p_exp = align(host_bytes), p_chunks = align(p_exp + (expected ? 4ull * n : 0));
-  const uint64_t p_out = align(p_chunks + (gl.hc[0].size() + gl.hc[1].size()) * sizeof(DevChunk));
-  const uint64_t p_ok = align(p_out + 4ull * n), p_mis = align(p_ok + n), p_end = p_mis + 256;
-  h3c_rt::PinnedLease pin(p_end);
+  const uint64_t off_exp = align(off_chunks1 + gl.hc[1].size() * sizeof(DevChunk));
+  const uint64_t off_mis = align(off_exp + (expected ? 4ull * n : 0));
+  const uint64_t off_out = off_mis + 256;
+  const uint64_t off_ok = align(off_out + 4ull * n);
+  const uint64_t off_seg = align(off_ok + (expected ? n : 0));
+  const uint64_t arena_bytes = off_seg + 4ull * std::max(gl.segs[0], gl.segs[1]) + 256;
+  h3c_rt::PinnedLease pin(off_seg);
   if (!pin.ok()) return H3C_ERR_HIP;
   char *const pb = pin.data();
   h3c_rt::DeviceLease scratch(dev, arena_bytes);
   if (!scratch.ok()) return H3C_ERR_HIP;
-  arena = scratch.data();
-  auto h2d = [&](void *dst, uint64_t pin_off, const void *src, size_t len) -> hipError_t {
-    std::memcpy(pb + pin_off, src, len);
-    return hipMemcpyAsync(dst, pb + pin_off, len, hipMemcpyHostToDevice, st);
-  };
+  char *const arena = scratch.data();
   uint32_t mis = 0;
   auto body = [&]() -> int {
     // stage host payloads and point their DevChunks at the staged copies
@@ -1316,7 +1331,7 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
     for (size_t i = 0; i < n; ++i) {
       const h3c_desc &x = dd[i];
       if (x.mem != H3C_MEM_DEVICE && x.ptr && x.len && (x.type == H3C_TYPE_CRC32C || x.type == H3C_TYPE_CRC32)) {
-        HIP_TRY(h2d(arena + off, off, x.ptr, x.len));  // staging and arena share offsets
+        std::memcpy(pb + off, x.ptr, x.len);  // staging and arena share offsets
         staged[i] = (uint64_t)(uintptr_t)(arena + off);
         off += (x.len + 255) & ~uint64_t(255);
       }
@@ -1325,6 +1340,13 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
       for (DevChunk &c : gl.hc[k])
         if (staged[c.out_idx]) c.ptr = staged[c.out_idx];
     mark_small(gl);  // staged copies have their own alignment
+    std::memcpy(pb + off_chunks0, gl.hc[0].data(), gl.hc[0].size() * sizeof(DevChunk));
+    std::memcpy(pb + off_chunks1, gl.hc[1].data(), gl.hc[1].size() * sizeof(DevChunk));
+    if (expected) {
+      std::memcpy(pb + off_exp, expected, 4ull * n);
+      std::memset(pb + off_mis, 0, 4);
+    }
+    HIP_TRY(hipMemcpyAsync(arena, pb, off_out, hipMemcpyHostToDevice, st));
     DevChunk *d_chunks[2] = {reinterpret_cast<DevChunk *>(arena + off_chunks0),
                              reinterpret_cast<DevChunk *>(arena + off_chunks1)};
     uint32_t *d_seg = reinterpret_cast<uint32_t *>(arena + off_seg);
@@ -1332,25 +1354,15 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
     uint32_t *d_exp = expected ? reinterpret_cast<uint32_t *>(arena + off_exp) : nullptr;
     uint8_t *d_ok = expected ? reinterpret_cast<uint8_t *>(arena + off_ok) : nullptr;
     uint32_t *d_mis = expected ? reinterpret_cast<uint32_t *>(arena + off_mis) : nullptr;
-    if (expected) {
-      HIP_TRY(h2d(d_exp, p_exp, expected, 4ull * n));
-      HIP_TRY(hipMemsetAsync(d_mis, 0, 4, st));
-    }
     for (int k = 0; k < 2; ++k) {
       if (gl.hc[k].empty()) continue;
-      HIP_TRY(h2d(d_chunks[k], p_chunks + (k ? gl.hc[0].size() * sizeof(DevChunk) : 0), gl.hc[k].data(),
-                  gl.hc[k].size() * sizeof(DevChunk)));
       const int r = h3c_rt::launch_crc(st, dev, k == 0 ? H3C_TYPE_CRC32C : H3C_TYPE_CRC32, d_chunks[k],
                                        (uint32_t)gl.hc[k].size(), gl.segs[k], gl.max_segs[k], gl.bytes[k], seg_bytes,
                                        read_dbg_flags(), d_seg, d_exp, d_out, d_ok, d_mis, H3C_PROF_SEG,
                                        gl.small[k]);
       if (r) return r;
     }
-    HIP_TRY(hipMemcpyAsync(pb + p_out, d_out, 4ull * n, hipMemcpyDeviceToHost, st));
-    if (expected) {
-      HIP_TRY(hipMemcpyAsync(pb + p_ok, d_ok, n, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipMemcpyAsync(pb + p_mis, d_mis, 4, hipMemcpyDeviceToHost, st));
-    }
+    HIP_TRY(hipMemcpyAsync(pb + off_mis, arena + off_mis, off_seg - off_mis, hipMemcpyDeviceToHost, st));
     return H3C_OK;
   };
   rc = body();
@@ -1360,10 +1372,10 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
     set_error("batch_sync: hipStreamSynchronize", se);
     return H3C_ERR_HIP;
   }
-  std::memcpy(out_raw, pb + p_out, 4ull * n);
+  std::memcpy(out_raw, pb + off_out, 4ull * n);
   if (expected) {
-    std::memcpy(ok, pb + p_ok, n);
-    std::memcpy(&mis, pb + p_mis, 4);
+    std::memcpy(ok, pb + off_ok, n);
+    std::memcpy(&mis, pb + off_mis, 4);
   }
   if (out_type)
     for (size_t i = 0; i < n; ++i) {
@@ -1375,14 +1387,185 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
   return H3C_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// ---- coalescing submission queue (h3c_set_coalescing) ----
+// The reference checksums one IO per call from 32 AIO and 32 update threads
+// (BatchReadJob.cc:34, ChunkReplica.cc:194).  With coalescing on, synchronous calls on the
+// default stream queue per device; a caller that finds no batch in flight becomes the
+// leader, takes every queued request (its own included), runs them as ONE batch (one
+// staging copy, one launch, one synchronisation) and wakes the others; callers that arrive
+// meanwhile form the next batch.
+std::atomic<int> g_coalesce{0};
+
+struct SyncReq {
+  const h3c_desc *d;
+  size_t n;
+  const uint32_t *expected;
+  uint8_t *out_type;
+  uint32_t *out_raw;
+  uint8_t *ok;
+  uint64_t *n_mismatch;
+  int rc = H3C_OK;
+  bool done = false;
+};
+
+struct Coalescer {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<SyncReq *> pending;
+  bool busy = false;
+};
+Coalescer g_coal[kMaxDevices];
+
+void run_merged(std::vector<SyncReq *> &b) {
+  if (b.size() == 1) {
+    SyncReq &r = *b[0];
+    r.rc = batch_sync(r.d, r.n, r.expected, r.out_type, r.out_raw, r.ok, r.n_mismatch, nullptr);
+    return;
+  }
+  size_t total = 0;
+  bool verify = false;
+  for (const SyncReq *r : b) {
+    total += r->n;
+    verify |= r->expected != nullptr;
+  }
+  std::vector<h3c_desc> dd;
+  std::vector<uint32_t> exp(verify ? total : 0), raw(total);
+  std::vector<uint8_t> ok(verify ? total : 0);
+  dd.reserve(total);
+  for (const SyncReq *r : b) {
+    if (r->expected) std::copy_n(r->expected, r->n, exp.begin() + dd.size());  // creates verify against 0
+    dd.insert(dd.end(), r->d, r->d + r->n);
+  }
+  const int rc = total > 0xFFFFFFF0u ? H3C_ERR_INVALID_ARG
+                                     : batch_sync(dd.data(), total, verify ? exp.data() : nullptr, nullptr, raw.data(),
+                                                  verify ? ok.data() : nullptr, nullptr, nullptr);
+  size_t at = 0;
+  for (SyncReq *r : b) {
+    r->rc = rc;
+    if (rc == H3C_OK) {
+      std::copy_n(raw.begin() + at, r->n, r->out_raw);
+      if (r->expected) {
+        std::copy_n(ok.begin() + at, r->n, r->ok);
+        if (r->n_mismatch) *r->n_mismatch = (uint64_t)std::count(ok.begin() + at, ok.begin() + at + r->n, (uint8_t)0);
+      }
+      if (r->out_type)
+        for (size_t i = 0; i < r->n; ++i) {
+          const h3c_desc &x = r->d[i];
+          const bool valid = (x.type == H3C_TYPE_CRC32C || x.type == H3C_TYPE_CRC32) && !(x.ptr == nullptr && x.len > 0);
+          r->out_type[i] = valid ? x.type : (uint8_t)H3C_TYPE_NONE;
+        }
+    }
+    at += r->n;
+  }
+}
+
+int submit_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uint8_t *out_type, uint32_t *out_raw, uint8_t *ok,
+                uint64_t *n_mismatch, void *stream) {
+  if (stream != nullptr || n == 0 || !g_coalesce.load(std::memory_order_relaxed))
+    return batch_sync(d, n, expected, out_type, out_raw, ok, n_mismatch, stream);
+  if (!d || !out_raw || n > 0xFFFFFFF0u) return H3C_ERR_INVALID_ARG;
+  int dev = 0;
+  const int rc = current_device(&dev);
+  if (rc) return rc;
+  SyncReq r{d, n, expected, out_type, out_raw, ok, n_mismatch};
+  Coalescer &q = g_coal[dev];
+  std::unique_lock<std::mutex> lk(q.mu);
+  q.pending.push_back(&r);
+  while (!r.done) {
+    if (!q.busy) {  // lead: everything queued so far is one batch
+      q.busy = true;
+      // the leader also runs the batch that queued behind its own (once), so the device is
+      // not idle while a woken waiter gets scheduled
+      for (int round = 0; round < 2 && !q.pending.empty(); ++round) {
+        std::vector<SyncReq *> batch;
+        batch.swap(q.pending);
+        lk.unlock();
+        run_merged(batch);
+        lk.lock();
+        for (SyncReq *x : batch) x->done = true;
+        q.cv.notify_all();
+      }
+      q.busy = false;
+      q.cv.notify_all();
+    } else {
+      q.cv.wait(lk);
+    }
+  }
+  return r.rc;
+}
+}  // namespace
+
+extern "C" {
+
+int h3c_set_coalescing(int on) {
+  g_coalesce.store(on ? 1 : 0);
+  return H3C_OK;
+}
+
 int h3c_batch_create(const h3c_desc *d, size_t n, uint8_t *out_type, uint32_t *out_raw, void *stream) {
-  return batch_sync(d, n, nullptr, out_type, out_raw, nullptr, nullptr, stream);
+  return submit_sync(d, n, nullptr, out_type, out_raw, nullptr, nullptr, stream);
 }
 
 int h3c_batch_verify(const h3c_desc *d, const uint32_t *expected_raw, size_t n, uint32_t *out_raw, uint8_t *ok,
                      uint64_t *n_mismatch, void *stream) {
   if (n && (!expected_raw || !ok)) return H3C_ERR_INVALID_ARG;
-  return batch_sync(d, n, expected_raw, nullptr, out_raw, ok, n_mismatch, stream);
+  return submit_sync(d, n, expected_raw, nullptr, out_raw, ok, n_mismatch, stream);
+}
+
+// Benchmark driver for the synchronous surface (bench.py --workload sync): `threads` host
+// threads each call h3c_batch_verify (api 0) or h3c_crc32c (api 1) `calls` times on their
+// own `bytes`-byte pinned host buffer; lat_us[t * calls + k] receives each call's latency.
+int h3c_diag_sync_bench(int threads, uint64_t bytes, int calls, int api, double *lat_us, double *wall_s) {
+  if (threads < 1 || threads > 1024 || calls < 1 || !lat_us || !wall_s || !bytes) return H3C_ERR_INVALID_ARG;
+  int dev = 0;
+  int rc = current_device(&dev);
+  if (rc) return rc;
+  std::vector<uint8_t *> bufs(threads, nullptr);
+  for (int t = 0; t < threads; ++t) {
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&bufs[t]), bytes, hipHostMallocDefault));
+    uint64_t x = 0x9E3779B97F4A7C15ull * (t + 1);
+    for (uint64_t i = 0; i < bytes; ++i) {
+      x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+      bufs[t][i] = (uint8_t)x;
+    }
+  }
+  std::atomic<int> ready{0}, status{H3C_OK};
+  std::atomic<bool> go{false};
+  std::vector<double> t0(threads), t1(threads);
+  auto body = [&](int t) {
+    (void)hipSetDevice(dev);
+    const h3c_desc d{bufs[t], bytes, 0xFFFFFFFFu, H3C_TYPE_CRC32C, H3C_MEM_HOST_PINNED, 0};
+    uint32_t want = 0, raw = 0;
+    uint8_t ok = 0, ty = 0;
+    int r = h3c_batch_create(&d, 1, &ty, &want, nullptr);
+    for (int w = 0; w < 3 && r == H3C_OK; ++w) r = h3c_batch_verify(&d, &want, 1, &raw, &ok, nullptr, nullptr);
+    ready.fetch_add(1);
+    while (!go.load()) std::this_thread::yield();
+    using clk = std::chrono::steady_clock;
+    const auto start = clk::now();
+    for (int k = 0; k < calls && r == H3C_OK; ++k) {
+      const auto a = clk::now();
+      r = api == 0 ? h3c_batch_verify(&d, &want, 1, &raw, &ok, nullptr, nullptr)
+                   : h3c_batch_create(&d, 1, &ty, &raw, nullptr);
+      if (r == H3C_OK && raw != want) r = H3C_ERR_CHECKSUM_MISMATCH;
+      lat_us[(size_t)t * calls + k] = std::chrono::duration<double, std::micro>(clk::now() - a).count();
+    }
+    t0[t] = std::chrono::duration<double>(start.time_since_epoch()).count();
+    t1[t] = std::chrono::duration<double>(clk::now().time_since_epoch()).count();
+    if (r != H3C_OK) status.store(r);
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; ++t) th.emplace_back(body, t);
+  while (ready.load() < threads) std::this_thread::yield();
+  go.store(true);
+  for (auto &x : th) x.join();
+  for (uint8_t *b : bufs) (void)hipHostFree(b);
+  *wall_s = *std::max_element(t1.begin(), t1.end()) - *std::min_element(t0.begin(), t0.end());
+  return status.load();
 }
 
 int h3c_batch_combine(uint8_t type, const uint32_t *c1_dev, const uint32_t *c2_dev, const uint64_t *len2_dev,

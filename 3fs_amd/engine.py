@@ -87,6 +87,8 @@ _proto("h3c_update_ios_ex", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp
 _proto("h3c_update_blocks_ex", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp,
        _u32, _vp, _vp)
 _proto("h3c_test_hook", _int, _int, _u64)
+_proto("h3c_set_coalescing", _int, _int)
+_proto("h3c_diag_sync_bench", _int, _int, _u64, _int, _int, _vp, _vp)
 _proto("h3c_update_ios_dev", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp)
 _proto("h3c_serde_checksum_mark", _u32, _u32, _int)
 _proto("h3c_batch_serde_checksum", _int, _vp, _sz, _vp, _vp, _vp)
@@ -330,6 +332,21 @@ def update_blocks(chunk_bases, chunk_len: int, raw_in, blk_chunk, blk_index, pay
                                     n_invalid.data_ptr() if n_invalid is not None else None,
                                     UPD_EXACT if exact else 0,
                                     counters.data_ptr() if counters is not None else None, _stream_handle(stream)))
+
+
+def set_coalescing(on: bool) -> None:
+    """h3c_set_coalescing: merge concurrent synchronous default-stream calls into one launch."""
+    _check(lib.h3c_set_coalescing(1 if on else 0))
+
+
+def sync_bench(threads: int, nbytes: int, calls: int, api: str = "verify"):
+    """h3c_diag_sync_bench: per-call latencies (us, threads x calls) and the wall time (s) of
+    `threads` host threads each calling the synchronous API on their own pinned buffer."""
+    lat = np.zeros(threads * calls, dtype=np.float64)
+    wall = ctypes.c_double(0)
+    _check(lib.h3c_diag_sync_bench(threads, nbytes, calls, 0 if api == "verify" else 1, lat.ctypes.data,
+                                   ctypes.byref(wall)))
+    return lat, wall.value
 
 
 HOOK_SEG_BYTES, HOOK_DEBUG_FLAGS, HOOK_UPD_SCAN = 1, 2, 3  # h3c_test_hook keys

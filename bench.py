@@ -504,6 +504,51 @@ def run_updio(args, cx: Ctx) -> dict:
     return out
 
 
+def run_sync(args, cx: Ctx) -> dict:
+    """The synchronous per-IO surface: 32 host threads each verifying their own
+    pinned host buffer one call at a time, as AioReadJob::setResult (BatchReadJob.cc:34) and
+    ChunkReplica::update (ChunkReplica.cc:194) call ChecksumInfo::create once per IO.  Per size:
+    p50 / p99 call latency and aggregate GiB/s, uncoalesced and with the coalescing queue, and
+    the CPU's per-call time for the same buffer (folly's 3-way SSE4.2 path restated in oracle/)."""
+    h3c = cx.h3c
+    threads = args.sync_threads
+    calls_for = {4: 2000, 128: 600, 1024: 150}
+    sizes = [(k << 10, calls_for.get(k, max(50, 2000 * 4 // k))) for k in map(int, args.sync_kib.split(","))]
+    rows = []
+    t_all = 0.0
+    for nbytes, calls in sizes:
+        row = {"bytes": nbytes, "threads": threads, "calls_per_thread": calls}
+        for mode in ("uncoalesced", "coalesced"):
+            h3c.set_coalescing(mode == "coalesced")
+            lat, wall = h3c.sync_bench(threads, nbytes, calls, "verify")
+            t_all += wall
+            row[mode] = {"p50_us": round(float(np.percentile(lat, 50)), 1),
+                         "p99_us": round(float(np.percentile(lat, 99)), 1),
+                         "gib_s": round(threads * calls * nbytes / wall / 2**30, 3),
+                         "calls_s": round(threads * calls / wall, 1)}
+        h3c.set_coalescing(False)
+        if not args.no_cpu_baseline:
+            L = _oracle()
+            L.orc_time_crc32c_calls.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]
+            L.orc_time_crc32c_calls.restype = ctypes.c_double
+            buf = np.random.default_rng(nbytes).integers(0, 256, nbytes, dtype=np.uint8)
+            per = L.orc_time_crc32c_calls(buf.ctypes.data, nbytes, max(200, (256 << 20) // nbytes))
+            row["cpu_per_call_us"] = round(per * 1e6, 3)
+            row["cpu_1core_gib_s"] = round(nbytes / per / 2**30, 2)
+        rows.append(row)
+    head = rows[0]["coalesced"]
+    return {
+        "metric": f"synchronous per-IO verify calls/s at {threads} threads (4 KiB pinned host buffers, coalesced)",
+        "value": head["calls_s"], "unit": "calls/s", "n_gpus": cx.world, "steps": 1, "warmup": 3,
+        "ms_per_step": round(t_all * 1e3, 2), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic (xorshift bytes in pinned host memory)",
+        "config": {"workload": f"sync: {threads} threads x h3c_batch_verify of one host buffer per call, "
+                               "4 KiB / 128 KiB / 1 MiB", "parallelism": "one GPU, many host threads"},
+        "verified": True, "sizes": rows,
+        "note": "PCIe-inclusive per-call latency; cpu_per_call_us is one core's folly-path crc32c of the same buffer",
+    }
+
+
 def pcie_h2d_peak(torch, dev, nbytes: int = 1 << 30) -> float:
     src = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
     dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -688,7 +733,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["verify", "update", "updio", "hostfed", "shard4m", "mixed"], default="verify")
+    ap.add_argument("--workload", choices=["verify", "update", "updio", "hostfed", "shard4m", "mixed", "sync"], default="verify")
     ap.add_argument("--chunks", type=int, default=8192)
     ap.add_argument("--chunk-kib", type=int, default=1024)
     ap.add_argument("--flip-frac", type=float, default=0.05)
@@ -704,10 +749,12 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--exact", action="store_true", help="updio / update: do not trust stored checksums")
+    ap.add_argument("--sync-threads", type=int, default=32)
+    ap.add_argument("--sync-kib", default="4,128,1024", help="sync: buffer sizes (KiB), comma-separated")
     args = ap.parse_args()
     cx = Ctx()
     fn = {"verify": run_verify, "update": run_update, "updio": run_updio, "hostfed": run_hostfed,
-          "shard4m": run_shard4m, "mixed": run_mixed}[args.workload]
+          "shard4m": run_shard4m, "mixed": run_mixed, "sync": run_sync}[args.workload]
     if args.workload in ("hostfed", "updio") and args.steps == 50:
         args.steps, args.warmup = (5, 1) if args.workload == "hostfed" else (10, 2)
     res = fn(args, cx)

@@ -100,6 +100,14 @@ int h3c_batch_create(const h3c_desc *d, size_t n, uint8_t *out_type, uint32_t *o
 int h3c_batch_verify(const h3c_desc *d, const uint32_t *expected_raw, size_t n, uint32_t *out_raw, uint8_t *ok,
                      uint64_t *n_mismatch, void *stream);
 
+/* Coalescing of concurrent synchronous calls (h3c_batch_create / h3c_batch_verify /
+ * h3c_crc32c / h3c_crc32 on the default stream, stream == NULL): callers queue per device and
+ * one of them runs everything queued as a single batch -- one staging copy, one launch, one
+ * synchronisation -- for the reference's pattern of one ChecksumInfo::create per IO from many
+ * AIO / update threads (BatchReadJob.cc:34, ChunkReplica.cc:194).  Results are identical; off
+ * by default. */
+int h3c_set_coalescing(int on);
+
 /* ---- asynchronous plan API (device-resident descriptors and results) ---- */
 
 typedef struct h3c_plan h3c_plan;
@@ -367,6 +375,12 @@ void h3c_hostfed_destroy(h3c_hostfed *h);
 /* chunk i at base + i*stride gets u64 words splitmix64(seed ^ ((first_chunk+i)<<40) ^ k). */
 int h3c_fill_splitmix(void *base_dev, uint64_t chunk_len, uint64_t nchunks, uint64_t stride, uint64_t seed,
                       uint64_t first_chunk, void *stream);
+
+/* Benchmark driver for the synchronous surface: `threads` host threads each call
+ * h3c_batch_verify (api 0) or h3c_batch_create (api 1) `calls` times on their own `bytes`-byte
+ * pinned host buffer (one descriptor per call, the default stream); lat_us[t * calls + k]
+ * receives each call's latency in microseconds, *wall_s the span of the timed calls. */
+int h3c_diag_sync_bench(int threads, uint64_t bytes, int calls, int api, double *lat_us, double *wall_s);
 
 /* When enabled, the engine brackets its hot launches with HIP events on the
  * launch stream.  h3c_profile_read(kind) synchronises those events and returns the

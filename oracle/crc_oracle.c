@@ -701,3 +701,18 @@ void orc_batch_crc32c(const uint8_t *base, uint64_t chunk_len, uint64_t nchunks,
   for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
   for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
 }
+
+/* Per-call CPU time of ChecksumInfo::create's CRC (folly's 3-way SSE4.2 crc32c, variant 0) on
+ * one `len`-byte buffer, repeated `calls` times: seconds per call.  The bench's CPU leg for the
+ * synchronous small-call surface (BatchReadJob.cc:34, ChunkReplica.cc:194). */
+#include <time.h>
+double orc_time_crc32c_calls(const uint8_t *buf, uint64_t len, uint64_t calls) {
+  pthread_once(&g_once, init_tables);
+  struct timespec a, b;
+  volatile uint32_t sink = 0;
+  clock_gettime(CLOCK_MONOTONIC, &a);
+  for (uint64_t i = 0; i < calls; ++i) sink ^= orc_crc32c_sse42_3way(buf, len, 0xFFFFFFFFu ^ (uint32_t)i);
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  (void)sink;
+  return ((double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec)) / (double)(calls ? calls : 1);
+}

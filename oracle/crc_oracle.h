@@ -119,7 +119,10 @@ void orc_fill_splitmix(uint8_t *out, uint64_t len, uint64_t seed, uint64_t chunk
 void orc_batch_crc32c(const uint8_t *base, uint64_t chunk_len, uint64_t nchunks, uint32_t start, int nthreads,
                       int variant, uint32_t *out);
 
+double orc_time_crc32c_calls(const uint8_t *buf, uint64_t len, uint64_t calls);
+
 #ifdef __cplusplus
 }
 #endif
+
 #endif

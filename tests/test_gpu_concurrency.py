@@ -139,3 +139,57 @@ def test_plan_run_captured_in_hip_graph(h3c, torch_dev):
     assert int(mis.item()) == 2
     assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == [5, 200]
     plan.close()
+
+
+def test_coalescing_queue_many_threads(h3c, torch_dev):
+    """h3c_set_coalescing: 32 threads on the default stream, each mixing single-buffer verifies
+    (host and device payloads, one injected mismatch per round), multi-buffer creates and
+    h3c_crc32c; every result against the oracle, then the same with coalescing off."""
+    torch, dev = torch_dev
+    nthreads, rounds = 32, 6
+    rng = np.random.default_rng(9)
+    host = [[rng.integers(0, 256, int(rng.integers(1, 300 << 10)), dtype=np.uint8) for _ in range(4)]
+            for _ in range(nthreads)]
+    want = [[orc.crc32c(d) for d in hs] for hs in host]
+    dev_bufs = [[torch.from_numpy(d).to(dev) for d in hs] for hs in host]
+    torch.cuda.synchronize()
+    for on in (True, False):
+        h3c.set_coalescing(on)
+        errors = []
+        start = threading.Barrier(nthreads)
+
+        def work(k):
+            try:
+                start.wait()
+                for it in range(rounds):
+                    j = it % 4
+                    bufs = dev_bufs[k] if it % 2 else host[k]
+                    exp = want[k][j] ^ (1 if it == 3 else 0)
+                    raw, ok, nbad = h3c.batch_verify([bufs[j]], [exp])
+                    if int(raw[0]) != want[k][j] or bool(ok[0]) != (it != 3) or nbad != (it == 3):
+                        errors.append((k, it, "verify"))
+                    t, v = h3c.batch_create(host[k])
+                    if list(map(int, v)) != want[k]:
+                        errors.append((k, it, "create"))
+                    if h3c.crc32c(host[k][j]) != want[k][j]:
+                        errors.append((k, it, "crc32c"))
+            except Exception as e:  # noqa: BLE001
+                errors.append((k, repr(e)))
+
+        threads = [threading.Thread(target=work, args=(k,)) for k in range(nthreads)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=120)
+        h3c.set_coalescing(False)
+        assert not errors, (on, errors[:5])
+
+
+def test_sync_bench_driver(h3c, torch_dev):
+    """h3c_diag_sync_bench returns one latency per call and flags no mismatch (it checks every
+    result against the buffer's own create)."""
+    for on in (False, True):
+        h3c.set_coalescing(on)
+        lat, wall = h3c.sync_bench(8, 4096, 50)
+        assert lat.shape == (400,) and (lat > 0).all() and wall > 0
+    h3c.set_coalescing(False)
