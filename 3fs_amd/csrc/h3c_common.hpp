@@ -109,10 +109,20 @@ constexpr uint32_t kFlagNone = 1u;
 // small_rows != 0: every chunk is exactly one segment of at most small_rows 1 KiB rows
 // (see small_rows_for) and none is NONE-flagged -- the small-chunk kernel then computes
 // and stores the results.
+// A small-path batch whose chunks share one length (a multiple of the small kernel's row), one
+// start and row-aligned addresses (uniform_for): seg_uni_kernel.  contiguous: chunk i at
+// base + i * stride with result i, no descriptor reads.
+struct UniformBatch {
+  uint32_t lanes = 0;  // 4 or 16 lanes per chunk; 0: not uniform
+  uint32_t rows = 0;   // rows of 16 * lanes bytes per chunk
+  uint32_t xs = 0;     // the shared start's share of the raw CRC
+  bool contiguous = false;
+  uint64_t base = 0, stride = 0;
+};
 int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint32_t nchunks, uint32_t total_segs,
                uint32_t max_chunk_segs, uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc,
                const uint32_t *expected, uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind,
-               uint32_t small_rows = 0);
+               uint32_t small_rows = 0, const UniformBatch *uni = nullptr);
 // Payload CRCs of UpdateIOs in 4 KiB pieces (op_piece_crc_kernel): crc0_out[i] ^= init-0 CRC
 // of op i's payload; pbase = exclusive scan of the per-op piece counts, *d_total their sum.
 int launch_op_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, const uint32_t *pbase, uint32_t n,
@@ -127,6 +137,8 @@ inline uint32_t host_rows(uint64_t ptr, uint64_t len) {
 // launch_crc's small_rows for host descriptors `c` (laid out with max_segs segments per
 // chunk at most): their largest row count when all qualify for the small-chunk kernel, else 0.
 uint32_t small_rows_for(const DevChunk *c, size_t n, uint32_t max_segs);
+// uniform_for: fills `u` when host descriptors `c` (with small_rows != 0) form a UniformBatch.
+void uniform_for(const DevChunk *c, size_t n, uint32_t small_rows, UniformBatch &u);
 // The same from bounds alone: chunks of at most max_len bytes in at most max_segs segments.
 uint32_t small_rows_bound(uint64_t max_len, uint32_t max_segs);
 // Segment size the engine picks for a batch of `total_bytes` on device `dev`.
@@ -217,6 +229,8 @@ struct PolyConsts {
   uint32_t tabq[4][256];  // tabq[k][b] = (b << 8k) * x^(8*kQuadRowBytes): the small-chunk kernel's rows
   uint32_t tabo[4][256];  // tabo[k][b] = (b << 8k) * x^(8*128): its 8-lane (128-byte row) variant
   uint32_t tabf[4][256];  // tabf[k][b] = (b << 8k) * x^(8*64): its 4-lane (64-byte row) variant
+  uint32_t tab2[4][256];  // (b << 8k) * x^(8*32): the uniform kernel's 2-lane (32-byte row) variant
+  uint32_t tab1[4][256];  // (b << 8k) * x^(8*16): its 1-lane (16-byte row) variant
   // Shift tables for x^(8e), 0 <= e < 2^26 (dxpow8_fast): x^(8*4096*k) and x^(8r), r < 4096.
   uint32_t x4k[16384];
   uint32_t xb[4096];
@@ -239,6 +253,12 @@ inline void build_consts(PolyConsts &pc, uint32_t poly) {
   const uint32_t frow = hxpow8n(64, poly);
   for (int k = 0; k < 4; ++k)
     for (uint32_t b = 0; b < 256; ++b) pc.tabf[k][b] = hgf_mul(b << (8 * k), frow, poly);
+  const uint32_t row2 = hxpow8n(32, poly), row1 = hxpow8n(16, poly);
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t b = 0; b < 256; ++b) {
+      pc.tab2[k][b] = hgf_mul(b << (8 * k), row2, poly);
+      pc.tab1[k][b] = hgf_mul(b << (8 * k), row1, poly);
+    }
   const uint32_t xinv8 = hgf_pow(hx_inverse(poly), 8, poly);
   for (int l = 0; l < 64; ++l)
     for (int j = 0; j < 4; ++j) pc.fix[4 * l + j] = hgf_pow(xinv8, 16u * l + 4u * j, poly);

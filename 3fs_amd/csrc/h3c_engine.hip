@@ -265,6 +265,16 @@ __global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__r
 #define H3C_QUAD_BATCH 4
 #endif
 constexpr int kQuadBatch = H3C_QUAD_BATCH;  // rows per load batch (two batches in flight)
+#ifndef H3C_UNI_BATCH
+#define H3C_UNI_BATCH 4
+#endif
+constexpr int kUniBatch = H3C_UNI_BATCH;  // the same for seg_uni_kernel
+#ifndef H3C_UNI_LANES_LO
+#define H3C_UNI_LANES_LO 4  // seg_uni_kernel's lanes per chunk up to 6 rows of 1 KiB
+#endif
+#ifndef H3C_UNI_LANES_HI
+#define H3C_UNI_LANES_HI 16
+#endif
 
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
 
@@ -431,6 +441,112 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
       src = src1;
     }
     m = n;
+  }
+}
+
+// Kernel A4: seg_quad_kernel<G, 1> for a batch whose chunks all have one length, a multiple of
+// the 16*G-byte row, at row-aligned addresses, with one start value -- a plan or verify of
+// uniform IO buffers / chunk pieces.  Every row is whole (no edge masks, no tail fix), the row
+// count K is the same for every chunk (loop control stays scalar) and the start's share xs is
+// one value.  With chunks == nullptr the batch is contiguous (chunk i at base + i * stride,
+// result i): no descriptor at all.
+template <int G>
+__global__ __launch_bounds__(kThreads) void seg_uni_kernel(const DevChunk *__restrict__ chunks, uint64_t base,
+                                                          uint64_t stride, uint32_t nchunks, uint32_t K, uint32_t xs,
+                                                          const PolyConsts *__restrict__ pc,
+                                                          const uint32_t *__restrict__ expected,
+                                                          uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                                          uint32_t *__restrict__ mismatch) {
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "1, 2, 4, 8 or 16 lanes per chunk");
+  constexpr int kLevels = G == 16 ? 4 : G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
+  constexpr uint32_t NG = 64 / G;
+  constexpr int kRed = (1 + kLevels) * 1024;
+  constexpr uint64_t kQ = 16u * G;
+  __shared__ uint32_t lds[kLdsWords + kRed];
+  for (int i = threadIdx.x; i < kLdsWords; i += kThreads)
+    lds[i] = fill_value_of(kQ == 256 ? pc->tabq : kQ == 128 ? pc->tabo : kQ == 64 ? pc->tabf : kQ == 32 ? pc->tab2 : pc->tab1, i);
+  const uint32_t *red_g = &pc->red[0][0][0];
+  for (int i = threadIdx.x; i < kRed; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  __syncthreads();
+  const uint32_t *red = lds + kLdsWords;
+  const char *lb = reinterpret_cast<const char *>(lds);
+  const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t lo = (uint32_t)(gw * nchunks / nw), hi = (uint32_t)((gw + 1) * nchunks / nw);
+  if (lo >= hi) return;
+  const LaneLut L = make_lut(lane);
+  // quad q (chunks q .. q + NG - 1; this group's is q + grp): its first row address for this
+  // lane, its result index and expected value
+  auto quad = [&](uint32_t q, uint64_t &la, uint32_t &o, uint32_t &want, bool &valid) {
+    const uint32_t t = q + grp;
+    valid = t < hi;
+    uint64_t p = 0;
+    o = t;
+    if (valid) {
+      if (chunks) {
+        p = chunks[t].ptr;
+        o = chunks[t].out_idx;
+      } else {
+        p = base + (uint64_t)t * stride;
+      }
+    }
+    la = p + 16u * gl;
+    want = valid && expected ? expected[o] : 0u;
+  };
+  uint64_t la;
+  uint32_t o, want;
+  bool valid;
+  quad(lo, la, o, want, valid);
+  uint4 cur[kUniBatch], nxt[kUniBatch];
+#pragma unroll
+  for (int b = 0; b < kUniBatch; ++b)
+    cur[b] = valid && (uint32_t)b < K ? load_row(la + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+  for (uint32_t q0 = lo; q0 < hi; q0 += NG) {
+    uint64_t la1 = la;
+    uint32_t o1 = o, want1 = want;
+    bool valid1 = false;
+    if (q0 + NG < hi) quad(q0 + NG, la1, o1, want1, valid1);  // its rows load during this quad's last batch
+    Streams st{0, 0, 0, 0};
+    for (uint32_t u0 = 0; u0 < K; u0 += kUniBatch) {
+      const uint32_t n0 = u0 + kUniBatch;
+      if (n0 < K) {
+#pragma unroll
+        for (int b = 0; b < kUniBatch; ++b)
+          nxt[b] = valid && n0 + b < K ? load_row(la + (uint64_t)(n0 + b) * kQ) : make_uint4(0, 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int b = 0; b < kUniBatch; ++b)
+          nxt[b] = valid1 && (uint32_t)b < K ? load_row(la1 + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int b = 0; b < kUniBatch; ++b)
+        if (u0 + b < K) consume(st, cur[b], lb, L);
+#pragma unroll
+      for (int b = 0; b < kUniBatch; ++b) cur[b] = nxt[b];
+    }
+    uint32_t p = tab_mul(st.s3, red) ^ st.s2;
+    p = tab_mul(p, red) ^ st.s1;
+    uint32_t v = tab_mul(p, red) ^ st.s0;
+#pragma unroll
+    for (int k = 0; k < kLevels; ++k) {
+      const uint32_t x = (uint32_t)__shfl_down((int)v, 1u << k, G);
+      if ((gl & ((2u << k) - 1u)) == 0) v ^= tab_mul(x, red + 1024 * (k + 1));
+    }
+    if (gl == 0 && valid) {
+      const uint32_t raw = v ^ xs;
+      out_raw[o] = raw;
+      if (expected) {
+        const bool good = raw == want;
+        ok[o] = good ? 1 : 0;
+        if (!good && mismatch) atomicAdd(mismatch, 1u);
+      }
+    }
+    la = la1;
+    o = o1;
+    want = want1;
+    valid = valid1;
   }
 }
 
@@ -885,7 +1001,7 @@ hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes
 int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint32_t nchunks, uint32_t total_segs,
                uint32_t max_chunk_segs, uint64_t payload_bytes, uint64_t seg_bytes, uint32_t dbg, uint32_t *d_segcrc,
                const uint32_t *expected, uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind,
-               uint32_t small_rows) {
+               uint32_t small_rows, const UniformBatch *uni) {
   const DeviceCtx &ctx = g_dev[dev];
   const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
   const uint32_t poly = type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
@@ -893,7 +1009,24 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
     const uint32_t blocks = std::min<uint32_t>(ctx.num_cu, (nchunks + kWavesPerBlock - 1) / kWavesPerBlock);
     ProfToken tok;
     if (prof_kind >= 0) HIP_TRY(prof_begin(st, tok));
-    if (H3C_SMALL_QUAD)
+    if (H3C_SMALL_QUAD && uni && uni->lanes && !(dbg & 4u)) {  // test hook: H3C_DEBUG_FLAGS bit2 disables it
+      const DevChunk *dc = uni->contiguous ? nullptr : d_chunks;
+      if (uni->lanes == 1)
+        hipLaunchKernelGGL(seg_uni_kernel<1>, dim3(blocks), dim3(kThreads), 0, st, dc, uni->base, uni->stride,
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+      else if (uni->lanes == 2)
+        hipLaunchKernelGGL(seg_uni_kernel<2>, dim3(blocks), dim3(kThreads), 0, st, dc, uni->base, uni->stride,
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+      else if (uni->lanes == 4)
+        hipLaunchKernelGGL(seg_uni_kernel<4>, dim3(blocks), dim3(kThreads), 0, st, dc, uni->base, uni->stride,
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+      else if (uni->lanes == 8)
+        hipLaunchKernelGGL(seg_uni_kernel<8>, dim3(blocks), dim3(kThreads), 0, st, dc, uni->base, uni->stride,
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+      else
+        hipLaunchKernelGGL(seg_uni_kernel<16>, dim3(blocks), dim3(kThreads), 0, st, dc, uni->base, uni->stride,
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+    } else if (H3C_SMALL_QUAD)
       // up to ~5 KiB chunks 4 lanes per chunk (4 KiB: +8 % over 8 lanes, +13 % over 16);
       // 16 lanes above (4 lanes lose 10 % at 8 and 16 KiB): profiles/r01d_small_lanes_ab.txt
       if (small_rows <= 6)
@@ -981,6 +1114,27 @@ uint32_t small_rows_for(const DevChunk *c, size_t n, uint32_t max_segs) {
 }
 
 uint64_t pick_seg(uint64_t total_bytes, int dev) { return pick_seg_bytes(total_bytes, device_num_cu(dev)); }
+
+void uniform_for(const DevChunk *c, size_t n, uint32_t small_rows, UniformBatch &u) {
+  u = UniformBatch{};
+  if (!n || !small_rows) return;
+  const uint32_t lanes = small_rows <= 6 ? H3C_UNI_LANES_LO : H3C_UNI_LANES_HI;
+  if (lanes != 1 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16) return;
+  const uint64_t row = 16u * lanes, len = c[0].len;
+  if (!len || len % row) return;
+  const uint64_t stride = n > 1 ? c[1].ptr - c[0].ptr : len;
+  bool contiguous = stride >= len && stride % row == 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (c[i].len != len || (c[i].ptr % row) || (c[i].flags & kFlagNone) || c[i].xstart != c[0].xstart) return;
+    contiguous = contiguous && c[i].out_idx == i && c[i].ptr == c[0].ptr + i * stride;
+  }
+  u.lanes = lanes;
+  u.rows = (uint32_t)(len / row);
+  u.xs = c[0].xstart;
+  u.contiguous = contiguous;
+  u.base = c[0].ptr;
+  u.stride = stride;
+}
 }  // namespace h3c_rt
 
 namespace {
@@ -1001,6 +1155,7 @@ struct Group {
   uint32_t max_chunk_segs = 0;
   uint64_t bytes = 0;
   uint32_t small = 0;  // seg_small_kernel rows (0: general kernels)
+  h3c_rt::UniformBatch uni;
   DevChunk *d_chunks = nullptr;
 };
 
@@ -1052,11 +1207,15 @@ struct GroupLayout {
   uint64_t bytes[2] = {0, 0};
   // every chunk one short segment: its largest row count (seg_small_kernel), else 0
   uint32_t small[2] = {0, 0};
+  h3c_rt::UniformBatch uni[2];
 };
 
 // Recomputes GroupLayout::small from the final device pointers.
 void mark_small(GroupLayout &g) {
-  for (int k = 0; k < 2; ++k) g.small[k] = h3c_rt::small_rows_for(g.hc[k].data(), g.hc[k].size(), g.max_segs[k]);
+  for (int k = 0; k < 2; ++k) {
+    g.small[k] = h3c_rt::small_rows_for(g.hc[k].data(), g.hc[k].size(), g.max_segs[k]);
+    h3c_rt::uniform_for(g.hc[k].data(), g.hc[k].size(), g.small[k], g.uni[k]);
+  }
 }
 
 int layout_groups(const h3c_desc *d, size_t n, uint64_t seg_bytes, GroupLayout &g) {
@@ -1193,6 +1352,7 @@ int h3c_plan_create(const h3c_desc *d, size_t n, int device, h3c_plan **out) {
     gr.max_chunk_segs = max_segs_chunk[g];
     gr.bytes = bytes[g];
     gr.small = gl.small[g];
+    gr.uni = gl.uni[g];
     hipError_t e = hipMalloc(&gr.d_chunks, hc[g].size() * sizeof(DevChunk));
     if (e == hipSuccess)
       e = hipMemcpy(gr.d_chunks, hc[g].data(), hc[g].size() * sizeof(DevChunk), hipMemcpyHostToDevice);
@@ -1247,7 +1407,7 @@ int h3c_plan_run(h3c_plan *p, const uint32_t *expected_raw_dev, uint32_t *out_ra
   for (const Group &g : p->groups) {
     rc = h3c_rt::launch_crc(st, p->device, g.type, g.d_chunks, g.nchunks, g.total_segs, g.max_chunk_segs, g.bytes,
                             p->seg_bytes, p->dbg, p->d_segcrc, expected_raw_dev, out_raw_dev, ok_dev, mismatch_dev,
-                            H3C_PROF_SEG, g.small);
+                            H3C_PROF_SEG, g.small, &g.uni);
     if (rc) break;
   }
   if (prev != p->device) HIP_TRY(hipSetDevice(prev));
@@ -1359,7 +1519,7 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
       const int r = h3c_rt::launch_crc(st, dev, k == 0 ? H3C_TYPE_CRC32C : H3C_TYPE_CRC32, d_chunks[k],
                                        (uint32_t)gl.hc[k].size(), gl.segs[k], gl.max_segs[k], gl.bytes[k], seg_bytes,
                                        read_dbg_flags(), d_seg, d_exp, d_out, d_ok, d_mis, H3C_PROF_SEG,
-                                       gl.small[k]);
+                                       gl.small[k], &gl.uni[k]);
       if (r) return r;
     }
     HIP_TRY(hipMemcpyAsync(pb + off_mis, arena + off_mis, off_seg - off_mis, hipMemcpyDeviceToHost, st));

@@ -399,7 +399,7 @@ int h3c_profile_read(int kind, double *ms, uint64_t *launches, uint64_t *bytes, 
  * the environment per call.  value 0 restores the default. */
 enum h3c_hook {
   H3C_HOOK_SEG_BYTES = 1,   /* segment size of the create / verify kernels (multiple of 1 KiB) */
-  H3C_HOOK_DEBUG_FLAGS = 2, /* bit0: no pipelined row loop; bit1: no small-chunk kernel */
+  H3C_HOOK_DEBUG_FLAGS = 2, /* bit0: no pipelined row loop; bit1: no small-chunk kernel; bit2: no uniform kernel */
   H3C_HOOK_UPD_SCAN = 3     /* h3c_update_blocks: 1 fused, 2 dense tiles, 3 sort + scan_by_key */
 };
 int h3c_test_hook(int key, uint64_t value);

@@ -334,3 +334,43 @@ def test_plan_verify_4mib_chunks_config4_shape(h3c, torch_dev):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
     assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(flips)
     assert int(mis.item()) == len(flips)
+
+
+@pytest.mark.parametrize("flags", ["0", "4"])
+@pytest.mark.parametrize("clen", [64, 1024, 4096, 6144, 8192, 12288])
+def test_uniform_small_chunk_batches(h3c, torch_dev, hooks, flags, clen):
+    """Uniform batches (one length, row-aligned, one start) run seg_uni_kernel (flags 0); flags 4
+    (H3C_DEBUG_FLAGS bit2) forces seg_quad_kernel on the same batches.  Contiguous plans (no
+    descriptors), strided plans, scattered aligned buffers and a verify with flips; a batch
+    that is almost uniform (one odd length) must take the general small kernel correctly."""
+    hooks(h3c.HOOK_DEBUG_FLAGS, int(flags, 0))
+    torch, dev = torch_dev
+    rng = np.random.default_rng(clen)
+    n = 3001
+    size = max(16 << 20, n * (clen + 4096))  # room for the strided plan below
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    buf = to_dev(torch, dev, host)
+    for stride in (clen, clen + 4096):
+        assert (n - 1) * stride + clen <= size
+        plan = h3c.Plan.uniform(buf.data_ptr(), clen, n, stride=stride)
+        out = torch.zeros(n, dtype=torch.int32, device=dev)
+        exp = np.array([orc.crc32c(host[k * stride: k * stride + clen]) for k in range(n)], dtype=np.uint32)
+        flips = sorted(set(int(x) for x in rng.integers(0, n, 20)))
+        bad = exp.copy()
+        bad[flips] ^= 0x80
+        ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+        plan.run(out, expected=torch.from_numpy(bad.view(np.int32)).to(dev), ok=ok)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), exp)
+        assert np.nonzero(ok.cpu().numpy() == 0)[0].tolist() == flips
+        plan.close()
+    # scattered row-aligned buffers (descriptors, not contiguous), then one odd length
+    offs = sorted(int(x) * 256 for x in rng.choice((16 << 20) // 256 - 64, 700, replace=False))
+    items = [(buf[o: o + clen], clen) for o in offs]
+    want = [orc.crc32c(host[o: o + clen]) for o in offs]
+    t, v = h3c.batch_create(items)
+    assert [int(x) for x in v] == want
+    items[5] = (buf[offs[5]: offs[5] + clen - 1], clen - 1)
+    want[5] = orc.crc32c(host[offs[5]: offs[5] + clen - 1])
+    t, v = h3c.batch_create(items)
+    assert [int(x) for x in v] == want
