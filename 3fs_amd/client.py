@@ -9,11 +9,17 @@
 * split reads (StorageClientImpl.cc:1607-1633): a large read split into pieces gets the
   first piece's checksum, combined with every further piece's (``ChecksumInfo::combine``).
 
+The checksum switches are the reference's (src/client/storage/StorageClient.h:161-221, 418):
+``ReadOptions.enableChecksum`` (default off) and ``WriteOptions.enableChecksum`` (default on),
+both forced on in debug builds (``#ifndef NDEBUG``) and off under the ``bypass_disk_io`` /
+``bypass_rdma_xmit`` debug options; ``IoOptions::Config.chunk_checksum_type`` (CRC32C).
+
 Payloads may be torch CUDA tensors (read in place) or host buffers (staged by the engine).
 """
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -22,16 +28,70 @@ from .engine import ChecksumInfo, ChecksumType, _check, batch_create, lib
 kChecksumMismatch = 7015  # StorageClientCode::kChecksumMismatch
 
 
-def write_checksums(payloads: Sequence, checksum_type: int = ChecksumType.CRC32C, stream=None) -> List[ChecksumInfo]:
-    """One ChecksumInfo per write IO payload (the client's chunk_checksum_type)."""
-    t, v = batch_create(payloads, int(checksum_type), stream=stream)
+@dataclass
+class DebugOptions:
+    """StorageClient.h:161-163."""
+    bypass_disk_io: bool = False
+    bypass_rdma_xmit: bool = False
+
+
+@dataclass
+class _ChecksumOptions:
+    enable_checksum: bool
+    debug: DebugOptions = field(default_factory=DebugOptions)
+    ndebug: bool = True  # a release build (NDEBUG); debug builds always checksum
+
+    def verify_checksum(self) -> bool:
+        """StorageClient.h:196-204 / 214-222."""
+        enabled = self.enable_checksum if self.ndebug else True
+        return enabled and not self.debug.bypass_disk_io and not self.debug.bypass_rdma_xmit
+
+
+@dataclass
+class ReadOptions(_ChecksumOptions):
+    enable_checksum: bool = False  # CONFIG_HOT_UPDATED_ITEM(enableChecksum, false), StorageClient.h:192
+
+
+@dataclass
+class WriteOptions(_ChecksumOptions):
+    enable_checksum: bool = True  # CONFIG_HOT_UPDATED_ITEM(enableChecksum, true), StorageClient.h:211
+
+
+@dataclass
+class ClientConfig:
+    chunk_checksum_type: int = ChecksumType.CRC32C  # CONFIG_ITEM(chunk_checksum_type, CRC32C), StorageClient.h:418
+
+
+def read_checksum_type(config: Optional[ClientConfig] = None, options: Optional[ReadOptions] = None) -> int:
+    """The checksum type a read request asks the server for (StorageClientImpl.cc:703):
+    chunk_checksum_type when the read verifies, else NONE."""
+    config = config or ClientConfig()
+    options = options or ReadOptions()
+    return int(config.chunk_checksum_type) if options.verify_checksum() else int(ChecksumType.NONE)
+
+
+def write_checksums(payloads: Sequence, checksum_type: Optional[int] = None, stream=None,
+                    config: Optional[ClientConfig] = None, options: Optional[WriteOptions] = None) -> List[ChecksumInfo]:
+    """One ChecksumInfo per write IO payload (StorageClientImpl.cc:1878-1883): created with the
+    client's chunk_checksum_type when ``options.verify_checksum()``, else the default {NONE, 0}.
+    ``checksum_type`` (if given) overrides ``config.chunk_checksum_type``."""
+    options = options or WriteOptions()
+    if not options.verify_checksum():
+        return [ChecksumInfo(ChecksumType.NONE, 0) for _ in payloads]
+    ctype = checksum_type if checksum_type is not None else (config or ClientConfig()).chunk_checksum_type
+    t, v = batch_create(payloads, int(ctype), stream=stream)
     return [ChecksumInfo(ChecksumType(int(a)), int(b)) for a, b in zip(t, v)]
 
 
-def verify_read_checksums(results: Sequence[Tuple[object, int, ChecksumInfo]], stream=None) -> np.ndarray:
+def verify_read_checksums(results: Sequence[Tuple[object, int, ChecksumInfo]], stream=None,
+                          options: Optional[ReadOptions] = None) -> np.ndarray:
     """results[i] = (data, result length, server checksum).  Returns per-IO status:
-    0, or kChecksumMismatch when the local checksum differs (IOs of length 0 are skipped)."""
+    0, or kChecksumMismatch when the local checksum differs (IOs of length 0 are skipped).
+    With ``options`` given, nothing is checked unless ``options.verify_checksum()``
+    (StorageClientImpl.cc:1720); without, every IO is checked."""
     status = np.zeros(len(results), dtype=np.uint32)
+    if options is not None and not options.verify_checksum():
+        return status
     idx = [i for i, (_, n, _) in enumerate(results) if n > 0]
     if not idx:
         return status

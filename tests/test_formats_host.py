@@ -91,3 +91,22 @@ def test_checksum_info_serde_roundtrip(h3c):
     for bad in (b"", b"\x80", b"\x05\x02\xff", b"\x03\x01\x00\x00"):
         with pytest.raises(h3c.EngineError):
             CI.deserialize(bad)
+
+
+def test_client_checksum_switches(h3c, client):
+    """ReadOptions / WriteOptions.verifyChecksum() (StorageClient.h:188-222) and the read
+    request's checksum type (StorageClientImpl.cc:703): defaults, debug builds, bypass options;
+    a write with checksums off carries the default {NONE, 0} (no engine call)."""
+    R, W, D = client.ReadOptions, client.WriteOptions, client.DebugOptions
+    assert not R().verify_checksum() and W().verify_checksum()
+    assert R(ndebug=False).verify_checksum()  # debug builds always checksum
+    assert R(enable_checksum=True).verify_checksum()
+    assert not W(debug=D(bypass_disk_io=True)).verify_checksum()
+    assert not W(ndebug=False, debug=D(bypass_rdma_xmit=True)).verify_checksum()
+    cfg = client.ClientConfig(chunk_checksum_type=h3c.ChecksumType.CRC32)
+    assert client.read_checksum_type(cfg, R(enable_checksum=True)) == int(h3c.ChecksumType.CRC32)
+    assert client.read_checksum_type(cfg, R()) == int(h3c.ChecksumType.NONE)
+    infos = client.write_checksums([b"abc", b"defg"], options=W(enable_checksum=False))
+    assert [(int(i.type), i.value) for i in infos] == [(0, 0), (0, 0)]
+    st = client.verify_read_checksums([(b"abc", 3, h3c.ChecksumInfo(h3c.ChecksumType.CRC32C, 1))], options=R())
+    assert list(st) == [0]  # reads not verified by default
