@@ -900,9 +900,12 @@ int layout(void *base, uint32_t n, uint32_t nchunks, uint64_t chunk_len, uint32_
 }
 
 // Per-(device, polynomial, chunk_len, block_bytes) block-shift tables sh[b] =
-// x^(8*(L-(b+1)*G)), built once and kept for the process ("precomputed per chunk
-// size").  Entries are never freed, so a table handed out stays valid; the cache is
-// bounded, and a miss past the bound computes into the caller's workspace instead.
+// x^(8*(L-(b+1)*G)), built once and kept for the process ("precomputed per chunk size").
+// Entries are never freed, so a table handed out stays valid; the cache is bounded.  A miss
+// builds the table on a private stream with no lock held (other threads' calls are not held
+// up), then publishes it; a miss past the bound, or while `st` is being captured into a graph
+// (no allocation or synchronisation allowed then), computes into the caller's workspace on
+// `st` instead.
 struct ShiftEntry {
   int dev;
   int type;
@@ -918,27 +921,53 @@ int shift_table(int dev, uint8_t type, uint64_t chunk_len, uint32_t block_bytes,
                 uint32_t *scratch, hipStream_t st, const uint32_t **out) {
   const uint32_t bpc = (uint32_t)(chunk_len / block_bytes);
   const uint32_t tb = 256;
-  std::lock_guard<std::mutex> lk(g_shift_mu);
-  for (const ShiftEntry &e : g_shift_cache)
-    if (e.dev == dev && e.type == type && e.chunk_len == chunk_len && e.block_bytes == block_bytes) {
-      *out = e.table;
+  auto find = [&]() -> const uint32_t * {
+    for (const ShiftEntry &e : g_shift_cache)
+      if (e.dev == dev && e.type == type && e.chunk_len == chunk_len && e.block_bytes == block_bytes) return e.table;
+    return nullptr;
+  };
+  bool room = false;
+  {
+    std::lock_guard<std::mutex> lk(g_shift_mu);
+    if (const uint32_t *t = find()) {
+      *out = t;
       return H3C_OK;
     }
-  uint32_t *table = scratch;
-  const bool keep = g_shift_cache.size() < kShiftCacheMax;
-  if (keep) HIP_TRY(hipMalloc(&table, 4ull * bpc));
-  hipLaunchKernelGGL(upd_shift_kernel, dim3((bpc + tb - 1) / tb), dim3(tb), 0, st, bpc, chunk_len, block_bytes, pc,
-                     table);
-  HIP_TRY(hipGetLastError());
-  if (keep) {  // publish only once the table is complete: other threads use it on other streams
-    HIP_TRY(hipStreamSynchronize(st));
-    g_shift_cache.push_back({dev, type, chunk_len, block_bytes, table});
+    room = g_shift_cache.size() < kShiftCacheMax;
   }
-  *out = table;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cap) != hipSuccess) cap = hipStreamCaptureStatusNone;
+  if (room && cap == hipStreamCaptureStatusNone) {
+    uint32_t *table = nullptr;
+    hipStream_t priv = nullptr;
+    bool built = hipMalloc(&table, 4ull * bpc) == hipSuccess &&
+                 hipStreamCreateWithFlags(&priv, hipStreamNonBlocking) == hipSuccess;
+    if (built) {
+      hipLaunchKernelGGL(upd_shift_kernel, dim3((bpc + tb - 1) / tb), dim3(tb), 0, priv, bpc, chunk_len, block_bytes,
+                         pc, table);
+      built = hipGetLastError() == hipSuccess && hipStreamSynchronize(priv) == hipSuccess;
+    }
+    if (priv) (void)hipStreamDestroy(priv);
+    if (built) {
+      std::lock_guard<std::mutex> lk(g_shift_mu);
+      if (const uint32_t *t = find()) {  // another thread published the same geometry meanwhile
+        (void)hipFree(table);
+        *out = t;
+      } else {
+        g_shift_cache.push_back({dev, type, chunk_len, block_bytes, table});
+        *out = table;
+      }
+      return H3C_OK;
+    }
+    if (table) (void)hipFree(table);
+    (void)hipGetLastError();
+  }
+  hipLaunchKernelGGL(upd_shift_kernel, dim3((bpc + tb - 1) / tb), dim3(tb), 0, st, bpc, chunk_len, block_bytes, pc,
+                     scratch);
+  HIP_TRY(hipGetLastError());
+  *out = scratch;
   return H3C_OK;
 }
-
-
 
 // H3C_UPD_EXACT: raw_exact[c] = the raw CRC of chunk c's bytes (one create launch).
 int exact_checksums(hipStream_t st, int dev, uint8_t type, const uint64_t *chunk_base, uint32_t nchunks,

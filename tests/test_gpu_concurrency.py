@@ -193,3 +193,45 @@ def test_sync_bench_driver(h3c, torch_dev):
         lat, wall = h3c.sync_bench(8, 4096, 50)
         assert lat.shape == (400,) and (lat > 0).all() and wall > 0
     h3c.set_coalescing(False)
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_update_blocks_captured_in_hip_graph_cold_cache(h3c, torch_dev, exact):
+    """h3c_update_blocks(_ex) captured into a HIP graph on its first call for a chunk geometry
+    (the shift-table cache is cold, so the table is computed on the capturing stream instead of
+    being built and published), then replayed: the chunk checksums equal a fresh create of the
+    bytes, and the counters are written by the graph."""
+    torch, dev = torch_dev
+    nchunks, cl, G = 5, (7 << 16) + (1 << 12) * (3 if exact else 5), 4096  # geometries no other test uses
+    bpc = cl // G
+    slab = torch.empty(nchunks * cl, dtype=torch.uint8, device=dev)
+    h3c.fill_splitmix(slab, cl, nchunks, cl, 11)
+    plan = h3c.Plan.uniform(slab.data_ptr(), cl, nchunks)
+    raw_in = torch.zeros(nchunks, dtype=torch.int32, device=dev)
+    plan.run(raw_in)
+    rng = np.random.default_rng(3)
+    nw = 300
+    wc = torch.from_numpy(rng.integers(0, nchunks, nw).astype(np.int32)).to(dev)
+    wb = torch.from_numpy(rng.integers(0, bpc, nw).astype(np.int32)).to(dev)
+    pay = torch.empty(nw * G, dtype=torch.uint8, device=dev)
+    h3c.fill_splitmix(pay, G, nw, G, 12)
+    bases = torch.arange(nchunks, dtype=torch.int64, device=dev) * cl + slab.data_ptr()
+    out = torch.zeros(nw, dtype=torch.int32, device=dev)
+    raw_out = torch.zeros(nchunks, dtype=torch.int32, device=dev)
+    ctr = torch.zeros(8, dtype=torch.int64, device=dev)
+    ws = torch.empty(h3c.update_workspace_bytes(nw, nchunks, cl, G), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            h3c.update_blocks(bases, cl, raw_in, wc, wb, pay, out, raw_out, block_bytes=G, workspace=ws, stream=s,
+                              exact=exact, counters=ctr)
+    g.replay()
+    torch.cuda.synchronize()
+    fresh = torch.zeros(nchunks, dtype=torch.int32, device=dev)
+    plan.run(fresh)
+    torch.cuda.synchronize()
+    assert torch.equal(fresh, raw_out)
+    assert ctr.cpu().tolist() == [0, 0, 0, nw, 0, 0, 0, 0]
+    plan.close()
