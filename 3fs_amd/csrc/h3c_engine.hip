@@ -609,10 +609,16 @@ __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(Src src, const u
     uint64_t S = 0, E = 0;
     uint32_t op = 0, shift = 0;
     if (valid) {  // op i: the last with pbase[i] <= k (pieces of ops with none are skipped over)
-      uint32_t a = 0, b = n;
-      while (b - a > 1) {
-        const uint32_t m = (a + b) >> 1;
-        if (pbase[m] <= k) a = m; else b = m;
+      // first guess: one piece per op (payloads of at most 4 KiB, BASELINE config 3), two
+      // independent loads; otherwise a binary search (pbase[n] is the total, > k)
+      uint32_t a = min(k, n - 1);
+      if (!(pbase[a] <= k && pbase[a + 1] > k)) {
+        a = 0;
+        uint32_t b = n;
+        while (b - a > 1) {
+          const uint32_t m = (a + b) >> 1;
+          if (pbase[m] <= k) a = m; else b = m;
+        }
       }
       op = a;
       const uint32_t j = k - pbase[a];

@@ -945,7 +945,7 @@ __global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uin
 struct AuxStream {
   int dev = -1;
   hipStream_t st = nullptr;
-  hipEvent_t ready = nullptr, done = nullptr;
+  hipEvent_t ready = nullptr, done = nullptr, init_done = nullptr;
 };
 int aux_stream(int dev, AuxStream *&out) {
   thread_local AuxStream aux[4];
@@ -960,6 +960,7 @@ int aux_stream(int dev, AuxStream *&out) {
   HIP_TRY(hipStreamCreateWithFlags(&a.st, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&a.ready, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&a.init_done, hipEventDisableTiming));
   a.dev = dev;
   out = &a;
   return H3C_OK;
@@ -1085,10 +1086,17 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                      d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc);
   HIP_TRY(hipGetLastError());
   HIP_TRY(scan_excl(d_np, d_pbase));
-  // second stream: chunks CRC'd from their bytes (t0), payload CRCs and A6; this stream sorts
-  // the ops meanwhile (the sort does not depend on either).  Joined before the sizes.
+  // second stream: payload CRCs and A6 first (the sizes wait for them), then the chunks CRC'd
+  // from their bytes (t0, needed only by the s-scan after the block kernel); this stream sorts
+  // the ops meanwhile (the sort depends on neither).
   HIP_TRY(hipEventRecord(aux->ready, st));
   HIP_TRY(hipStreamWaitEvent(aux->st, aux->ready, 0));
+  rc = h3c_rt::launch_op_piece_crc(aux->st, dev, poly_type, d_ios, d_pbase, n, d_pbase + n, d_paycrc0);
+  if (rc) return rc;
+  hipLaunchKernelGGL(uio_verify_kernel, dim3(gb), dim3(tb), 0, aux->st, d_ios, n, d_paycrc0, pc, stdf, d_status,
+                     d_payraw);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(aux->done, aux->st));
   hipLaunchKernelGGL(uio_init_count_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf,
                      d_cnp, d_ccrc);
   HIP_TRY(hipGetLastError());
@@ -1102,12 +1110,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   hipLaunchKernelGGL(uio_t0_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf, stdf, d_ccrc,
                      pc, d_t0);
   HIP_TRY(hipGetLastError());
-  rc = h3c_rt::launch_op_piece_crc(aux->st, dev, poly_type, d_ios, d_pbase, n, d_pbase + n, d_paycrc0);
-  if (rc) return rc;
-  hipLaunchKernelGGL(uio_verify_kernel, dim3(gb), dim3(tb), 0, aux->st, d_ios, n, d_paycrc0, pc, stdf, d_status,
-                     d_payraw);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(aux->done, aux->st));
+  HIP_TRY(hipEventRecord(aux->init_done, aux->st));
   {
     size_t t = tmp_bytes;
     HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, st));
@@ -1167,7 +1170,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     // algorithmic bytes, per op: a 4 KiB block read and written once plus 4 KiB of new bytes
     // (exact for BASELINE config 3's block-aligned 4 KiB writes; bench.py states the unit)
     HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDIO, 3ull * kBlk * n));
-    // t' per op, then s' per op (two affine scans by chunk)
+    // t' per op, then s' per op (two affine scans by chunk); the s-scan reads t0
+    if (attempt == 0) HIP_TRY(hipStreamWaitEvent(st, aux->init_done, 0));
     hipLaunchKernelGGL(uio_elem_kernel<TMapFn>, dim3(gb), dim3(tb), 0, st, TMapFn{d_pos, d_eacc, d_payraw, pc}, n,
                        d_tel);
     HIP_TRY(hipGetLastError());
