@@ -859,10 +859,11 @@ int current_device(int *dev) {
 }
 
 // h3c_test_hook state: read from the environment once, settable by tests.
-std::atomic<uint64_t> g_hooks[4];
+constexpr int kHooks = 5;
+std::atomic<uint64_t> g_hooks[kHooks];
 const bool g_hooks_init = [] {
-  const char *names[4] = {nullptr, "H3C_SEG_BYTES", "H3C_DEBUG_FLAGS", "H3C_UPD_SCAN"};
-  for (int k = 1; k < 4; ++k) {
+  const char *names[kHooks] = {nullptr, "H3C_SEG_BYTES", "H3C_DEBUG_FLAGS", "H3C_UPD_SCAN", "H3C_UPD_GRAPHS"};
+  for (int k = 1; k < kHooks; ++k) {
     uint64_t v = 0;
     if (const char *e = std::getenv(names[k])) {
       if (k == H3C_HOOK_UPD_SCAN)
@@ -883,7 +884,7 @@ const void *device_consts(int dev, int type) {
   return g_dev[dev].d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
 }
 int device_num_cu(int dev) { return (dev >= 0 && dev < kMaxDevices) ? g_dev[dev].num_cu : 0; }
-uint64_t hook(int key) { return (key > 0 && key < 4) ? g_hooks[key].load(std::memory_order_relaxed) : 0; }
+uint64_t hook(int key) { return (key > 0 && key < kHooks) ? g_hooks[key].load(std::memory_order_relaxed) : 0; }
 int current_device(int *dev) { return ::current_device(dev); }
 void set_error(const char *what, hipError_t e) { ::set_error(what, e); }
 void set_error_text(const char *text) { g_last_error = text; }
@@ -1284,7 +1285,7 @@ uint32_t h3c_crc32_combine(uint32_t c1, uint32_t c2, uint64_t len2) {
 int h3c_device_count(void) { return device_count(); }
 
 int h3c_test_hook(int key, uint64_t value) {
-  if (key < 1 || key > 3) return H3C_ERR_INVALID_ARG;
+  if (key < 1 || key >= kHooks) return H3C_ERR_INVALID_ARG;
   g_hooks[key].store(value);
   return H3C_OK;
 }

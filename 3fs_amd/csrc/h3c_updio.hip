@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -925,6 +926,14 @@ __global__ void uio_t0_kernel(const h3c_chunk_state *__restrict__ chunks, uint32
   t0v[c] = t0;
 }
 
+// h3c_update_ios_dev: the final chunk states over the input table, unless the fragment
+// guess was short (the host then redoes the fragment stage from the original states).
+__global__ void uio_commit_kernel(const h3c_chunk_state *__restrict__ fin, h3c_chunk_state *__restrict__ chunks,
+                                  uint32_t nchunks, const uint32_t *__restrict__ d_F, uint32_t cap) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < nchunks && *d_F <= cap) chunks[c] = fin[c];
+}
+
 // H3C_UPD_EXACT: chunks whose stored checksum of the batch polynomial disagrees with the bytes.
 __global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks,
                                  const uint32_t *__restrict__ t0v, uint8_t poly_type, uint32_t std_domain,
@@ -994,6 +1003,93 @@ hipError_t sort_pairs(void *tmp, size_t &tmp_bytes, const uint32_t *k, uint32_t 
 }
 
 
+
+// ---- per-thread cache of captured pipeline graphs (update_core) ----
+std::atomic<uint64_t> g_graph_stats[3];  // replays, captures, capture failures (h3c_diag_counter)
+struct UpdGraphKey {
+  int dev;
+  uint8_t poly;
+  uint32_t flags, n, nchunks, cap, hcap;
+  const void *chunks, *chunks_out, *ios, *res, *ctr, *lease1, *lease2;
+  hipStream_t aux;
+  bool operator==(const UpdGraphKey &o) const { return std::memcmp(this, &o, sizeof(*this)) == 0; }
+};
+struct UpdGraphs {
+  UpdGraphKey key{};
+  hipGraphExec_t a = nullptr, b = nullptr;
+  bool failed = false;
+  uint64_t used = 0;
+};
+// The graphs of `key`, or nullptr when this call should launch plainly: the first sight of a
+// shape launches plainly (a caller whose buffers move every call never pays a capture); the
+// second sight returns an empty entry to capture into; later sights replay.  Graphs are not
+// used while `st` itself is being captured, or with h3c_test_hook(H3C_HOOK_UPD_GRAPHS, 1).
+UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st) {
+  thread_local UpdGraphs cache[4];
+  thread_local UpdGraphKey last{};
+  thread_local uint64_t tick = 0;
+  if (h3c_rt::hook(H3C_HOOK_UPD_GRAPHS) == 1) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  UpdGraphKey key;
+  std::memset(&key, 0, sizeof(key));  // padding compared by memcmp
+  key.dev = key_in.dev;
+  key.poly = key_in.poly;
+  key.flags = key_in.flags;
+  key.n = key_in.n;
+  key.nchunks = key_in.nchunks;
+  key.cap = key_in.cap;
+  key.hcap = key_in.hcap;
+  key.chunks = key_in.chunks;
+  key.chunks_out = key_in.chunks_out;
+  key.ios = key_in.ios;
+  key.res = key_in.res;
+  key.ctr = key_in.ctr;
+  key.lease1 = key_in.lease1;
+  key.lease2 = key_in.lease2;
+  key.aux = key_in.aux;
+  ++tick;
+  for (UpdGraphs &g : cache)
+    if (g.used && g.key == key) {
+      g.used = tick;
+      return g.failed ? nullptr : &g;
+    }
+  const bool seen = last == key;
+  last = key;
+  if (!seen) return nullptr;
+  UpdGraphs *victim = &cache[0];
+  for (UpdGraphs &g : cache)
+    if (g.used < victim->used) victim = &g;
+  if (victim->a) (void)hipGraphExecDestroy(victim->a);
+  if (victim->b) (void)hipGraphExecDestroy(victim->b);
+  *victim = UpdGraphs{};
+  victim->key = key;
+  victim->used = tick;
+  return victim;
+}
+
+// Captures what `body` enqueues on `st` (and the streams it forks) into an executable graph.
+template <class Body>
+int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out) {
+  if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) return H3C_ERR_HIP;
+  const int r = body();
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(st, &g);
+  if (r || e != hipSuccess || !g) {
+    if (g) (void)hipGraphDestroy(g);
+    return r ? r : H3C_ERR_HIP;
+  }
+  const hipError_t ie = hipGraphInstantiate(&out, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (ie != hipSuccess) {
+    out = nullptr;
+    return H3C_ERR_HIP;
+  }
+  return H3C_OK;
+}
 
 // The pipeline on device arrays: chunks_in (read), chunks_out (final states; may not alias
 // chunks_in), ios, results, ctr (h3c_update_counters layout, 8 x u64).  `epilogue` enqueues the
@@ -1082,51 +1178,57 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     size_t t = tmp_bytes;
     return rocprim::exclusive_scan(d_tmp, t, in, out, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), st);
   };
-  hipLaunchKernelGGL(uio_prep_kernel, dim3(gb), dim3(tb), 0, st, d_ios, n, d_chunks, nchunks, poly_type, stdf,
-                     d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(scan_excl(d_np, d_pbase));
-  // second stream: payload CRCs and A6 first (the sizes wait for them), then the chunks CRC'd
-  // from their bytes (t0, needed only by the s-scan after the block kernel); this stream sorts
-  // the ops meanwhile (the sort depends on neither).
-  HIP_TRY(hipEventRecord(aux->ready, st));
-  HIP_TRY(hipStreamWaitEvent(aux->st, aux->ready, 0));
-  rc = h3c_rt::launch_op_piece_crc(aux->st, dev, poly_type, d_ios, d_pbase, n, d_pbase + n, d_paycrc0);
-  if (rc) return rc;
-  hipLaunchKernelGGL(uio_verify_kernel, dim3(gb), dim3(tb), 0, aux->st, d_ios, n, d_paycrc0, pc, stdf, d_status,
-                     d_payraw);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(aux->done, aux->st));
-  hipLaunchKernelGGL(uio_init_count_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf,
-                     d_cnp, d_ccrc);
-  HIP_TRY(hipGetLastError());
-  {
-    size_t t = cscan_tmp;
-    HIP_TRY(rocprim::exclusive_scan(d_ctmp, t, d_cnp, d_cbase, 0u, (size_t)nchunks + 1, rocprim::plus<uint32_t>(),
-                                    aux->st));
-  }
-  rc = h3c_rt::launch_chunk_piece_crc(aux->st, dev, poly_type, d_chunks, d_cbase, nchunks, d_cbase + nchunks, d_ccrc);
-  if (rc) return rc;
-  hipLaunchKernelGGL(uio_t0_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf, stdf, d_ccrc,
-                     pc, d_t0);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(aux->init_done, aux->st));
-  {
-    size_t t = tmp_bytes;
-    HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, st));
-  }
-  HIP_TRY(hipStreamWaitEvent(st, aux->done, 0));
-  hipLaunchKernelGGL(uio_sz_elem_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, n, d_status, poly_type, stdf, d_sz);
-  HIP_TRY(hipGetLastError());
-  {
-    size_t t = tmp_bytes;
-    HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_sz, d_szscan, (size_t)n, SzTyOp(),
-                                           rocprim::equal_to<uint32_t>(), st));
-  }
-  hipLaunchKernelGGL(uio_classify_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, d_skey, n, d_chunks, nchunks,
-                     d_szscan, d_status, poly_type, stdf, d_pos, d_nfrag);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(scan_excl(d_nfrag, d_fbase));
+  // phase A: validation, payload CRCs + A6 and the INIT CRCs (second stream), sort, sizes,
+  // cases and fragment counts; joined back into `st` at its end
+  auto phase_a = [&]() -> int {
+    hipLaunchKernelGGL(uio_prep_kernel, dim3(gb), dim3(tb), 0, st, d_ios, n, d_chunks, nchunks, poly_type, stdf,
+                       d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(scan_excl(d_np, d_pbase));
+    // second stream: payload CRCs and A6 first (the sizes wait for them), then the chunks CRC'd
+    // from their bytes (t0); this stream sorts the ops meanwhile (the sort depends on neither)
+    HIP_TRY(hipEventRecord(aux->ready, st));
+    HIP_TRY(hipStreamWaitEvent(aux->st, aux->ready, 0));
+    int r = h3c_rt::launch_op_piece_crc(aux->st, dev, poly_type, d_ios, d_pbase, n, d_pbase + n, d_paycrc0);
+    if (r) return r;
+    hipLaunchKernelGGL(uio_verify_kernel, dim3(gb), dim3(tb), 0, aux->st, d_ios, n, d_paycrc0, pc, stdf, d_status,
+                       d_payraw);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(aux->done, aux->st));
+    hipLaunchKernelGGL(uio_init_count_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf,
+                       d_cnp, d_ccrc);
+    HIP_TRY(hipGetLastError());
+    {
+      size_t t = cscan_tmp;
+      HIP_TRY(rocprim::exclusive_scan(d_ctmp, t, d_cnp, d_cbase, 0u, (size_t)nchunks + 1, rocprim::plus<uint32_t>(),
+                                      aux->st));
+    }
+    r = h3c_rt::launch_chunk_piece_crc(aux->st, dev, poly_type, d_chunks, d_cbase, nchunks, d_cbase + nchunks, d_ccrc);
+    if (r) return r;
+    hipLaunchKernelGGL(uio_t0_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf, stdf,
+                       d_ccrc, pc, d_t0);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(aux->init_done, aux->st));
+    {
+      size_t t = tmp_bytes;
+      HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, st));
+    }
+    HIP_TRY(hipStreamWaitEvent(st, aux->done, 0));
+    hipLaunchKernelGGL(uio_sz_elem_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, n, d_status, poly_type, stdf,
+                       d_sz);
+    HIP_TRY(hipGetLastError());
+    {
+      size_t t = tmp_bytes;
+      HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_sz, d_szscan, (size_t)n, SzTyOp(),
+                                             rocprim::equal_to<uint32_t>(), st));
+    }
+    hipLaunchKernelGGL(uio_classify_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, d_skey, n, d_chunks, nchunks,
+                       d_szscan, d_status, poly_type, stdf, d_pos, d_nfrag);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(scan_excl(d_nfrag, d_fbase));
+    HIP_TRY(hipStreamWaitEvent(st, aux->init_done, 0));
+    return H3C_OK;
+  };
 
   // ---- fragments, blocks, scans, results (redone once if the fragment guess was short) ----
   for (int attempt = 0;; ++attempt) {
@@ -1150,18 +1252,88 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     layout2(lease2.data());
     const uint32_t *d_F = d_fbase + n;
     const uint32_t fb = (cap + tb - 1) / tb;
-    if (attempt) HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, st));  // the first attempt's counters
-    hipLaunchKernelGGL(uio_frag_kernel, dim3((std::max(cap, hcap) + tb - 1) / tb), dim3(tb), 0, st, d_pos, d_fbase, n,
-                       cap, d_ios, d_skey, d_chunks, d_frag, d_fkey, pc, d_hhead, hcap);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(uio_tlink_kernel, dim3((cap + kLinkTile - 1) / kLinkTile), dim3(kLinkTile), 0, st, d_fkey, d_F,
-                       cap, d_hhead, hcap - 1, d_gnext, d_prev);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(uio_resolve_kernel, dim3(fb), dim3(tb), 0, st, d_fkey, d_F, cap, d_hhead, hcap - 1, d_gnext,
-                       d_prev);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(uio_heads_kernel, dim3(fb), dim3(tb), 0, st, d_prev, d_F, cap, d_frag);
-    HIP_TRY(hipGetLastError());
+    auto phase_frag = [&]() -> int {  // fragments and their chains
+      if (attempt) HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, st));  // the first attempt's counters
+      hipLaunchKernelGGL(uio_frag_kernel, dim3((std::max(cap, hcap) + tb - 1) / tb), dim3(tb), 0, st, d_pos, d_fbase,
+                         n, cap, d_ios, d_skey, d_chunks, d_frag, d_fkey, pc, d_hhead, hcap);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(uio_tlink_kernel, dim3((cap + kLinkTile - 1) / kLinkTile), dim3(kLinkTile), 0, st, d_fkey,
+                         d_F, cap, d_hhead, hcap - 1, d_gnext, d_prev);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(uio_resolve_kernel, dim3(fb), dim3(tb), 0, st, d_fkey, d_F, cap, d_hhead, hcap - 1, d_gnext,
+                         d_prev);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(uio_heads_kernel, dim3(fb), dim3(tb), 0, st, d_prev, d_F, cap, d_frag);
+      HIP_TRY(hipGetLastError());
+      return H3C_OK;
+    };
+    auto phase_b = [&]() -> int {  // t' per op, then s' per op (two affine scans by chunk), results
+      hipLaunchKernelGGL(uio_elem_kernel<TMapFn>, dim3(gb), dim3(tb), 0, st, TMapFn{d_pos, d_eacc, d_payraw, pc}, n,
+                         d_tel);
+      HIP_TRY(hipGetLastError());
+      {
+        size_t t = tmp_bytes;
+        HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_tel, d_tscan, (size_t)n, AffOp{poly},
+                                               rocprim::equal_to<uint32_t>(), st));
+      }
+      hipLaunchKernelGGL(uio_elem_kernel<SMapFn>, dim3(gb), dim3(tb), 0, st,
+                         SMapFn{d_pos, d_skey, nchunks, d_tscan, d_t0, d_eacc, d_payraw, pc}, n, d_sel);
+      HIP_TRY(hipGetLastError());
+      {
+        size_t t = tmp_bytes;
+        HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_sel, d_sscan, (size_t)n, AffOp{poly},
+                                               rocprim::equal_to<uint32_t>(), st));
+      }
+      if (nchunks)
+        HIP_TRY(
+            hipMemcpyAsync(d_chunks_out, d_chunks, sizeof(h3c_chunk_state) * nchunks, hipMemcpyDeviceToDevice, st));
+      hipLaunchKernelGGL(uio_result_kernel, dim3(gb), dim3(tb), 0, st, d_pos, d_skey, n, d_sscan, d_chunks,
+                         d_chunks_out, nchunks, d_t0, poly_type, stdf, poly, d_res, d_ctr);
+      HIP_TRY(hipGetLastError());
+      if (exact && nchunks) {
+        hipLaunchKernelGGL(uio_stale_kernel, dim3((nchunks + tb - 1) / tb), dim3(tb), 0, st, d_chunks, nchunks, d_t0,
+                           poly_type, stdf, d_ctr);
+        HIP_TRY(hipGetLastError());
+      }
+      return H3C_OK;
+    };
+    // The first attempt's phases run as two HIP graphs when this thread has seen the same
+    // batch shape and buffers before (the lease pools hand a steady caller the same ones):
+    // ~30 launches become two, so the short kernels run back to back instead of at the host's
+    // launch rate.  The block kernel stays a plain launch between them (profiled).
+    UpdGraphs *gr = nullptr;
+    if (attempt == 0) {
+      const UpdGraphKey key{dev, poly_type, flags, n, nchunks, cap, hcap, d_chunks, d_chunks_out, d_ios, d_res,
+                            d_ctr, lease1.data(), lease2.data(), aux->st};
+      gr = upd_graphs(key, st);
+    }
+    if (gr && !gr->a) {  // capture both phases once
+      rc = capture_graph(st, [&] {
+        const int r = phase_a();
+        return r ? r : phase_frag();
+      }, gr->a);
+      if (!rc) rc = capture_graph(st, phase_b, gr->b);
+      if (rc) {  // not capturable here: plain launches from now on for this shape
+        gr->failed = true;
+        (void)hipGetLastError();
+        g_graph_stats[2].fetch_add(1);
+      } else {
+        g_graph_stats[1].fetch_add(1);
+      }
+      rc = H3C_OK;
+    }
+    const bool use_graphs = gr && gr->a && gr->b && !gr->failed;
+    if (use_graphs) {
+      HIP_TRY(hipGraphLaunch(gr->a, st));
+      g_graph_stats[0].fetch_add(1);
+    } else {
+      if (attempt == 0) {
+        rc = phase_a();
+        if (rc) return rc;
+      }
+      rc = phase_frag();
+      if (rc) return rc;
+    }
     const uint32_t blocks = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
     h3c_rt::ProfToken tok;
     HIP_TRY(h3c_rt::prof_begin(st, tok));
@@ -1170,36 +1342,14 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     // algorithmic bytes, per op: a 4 KiB block read and written once plus 4 KiB of new bytes
     // (exact for BASELINE config 3's block-aligned 4 KiB writes; bench.py states the unit)
     HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDIO, 3ull * kBlk * n));
-    // t' per op, then s' per op (two affine scans by chunk); the s-scan reads t0
-    if (attempt == 0) HIP_TRY(hipStreamWaitEvent(st, aux->init_done, 0));
-    hipLaunchKernelGGL(uio_elem_kernel<TMapFn>, dim3(gb), dim3(tb), 0, st, TMapFn{d_pos, d_eacc, d_payraw, pc}, n,
-                       d_tel);
-    HIP_TRY(hipGetLastError());
-    {
-      size_t t = tmp_bytes;
-      HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_tel, d_tscan, (size_t)n, AffOp{poly},
-                                             rocprim::equal_to<uint32_t>(), st));
-    }
-    hipLaunchKernelGGL(uio_elem_kernel<SMapFn>, dim3(gb), dim3(tb), 0, st,
-                       SMapFn{d_pos, d_skey, nchunks, d_tscan, d_t0, d_eacc, d_payraw, pc}, n, d_sel);
-    HIP_TRY(hipGetLastError());
-    {
-      size_t t = tmp_bytes;
-      HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_sel, d_sscan, (size_t)n, AffOp{poly},
-                                             rocprim::equal_to<uint32_t>(), st));
-    }
-    if (nchunks)
-      HIP_TRY(hipMemcpyAsync(d_chunks_out, d_chunks, sizeof(h3c_chunk_state) * nchunks, hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(uio_result_kernel, dim3(gb), dim3(tb), 0, st, d_pos, d_skey, n, d_sscan, d_chunks,
-                       d_chunks_out, nchunks, d_t0, poly_type, stdf, poly, d_res, d_ctr);
-    HIP_TRY(hipGetLastError());
-    if (exact && nchunks) {
-      hipLaunchKernelGGL(uio_stale_kernel, dim3((nchunks + tb - 1) / tb), dim3(tb), 0, st, d_chunks, nchunks, d_t0,
-                         poly_type, stdf, d_ctr);
-      HIP_TRY(hipGetLastError());
+    if (use_graphs) {
+      HIP_TRY(hipGraphLaunch(gr->b, st));
+    } else {
+      rc = phase_b();
+      if (rc) return rc;
     }
     HIP_TRY(hipMemcpyAsync(h_F, d_F, 4, hipMemcpyDeviceToHost, st));
-    rc = epilogue(st);
+    rc = epilogue(st, d_F, cap);  // (outputs of an attempt whose fragment guess was short are redone)
     if (rc) return rc;
     const hipError_t se = hipStreamSynchronize(st);
     drain2.armed = false;
@@ -1241,6 +1391,10 @@ void counters_from(const unsigned long long *h, h3c_update_counters *c) {
 
 }  // namespace
 
+extern "C" uint64_t h3c_diag_counter(int which) {
+  return which >= 0 && which < 3 ? g_graph_stats[which].load() : 0;
+}
+
 extern "C" int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,
                                  uint32_t n, h3c_update_result *results, uint32_t flags, h3c_update_counters *counters,
                                  void *stream) {
@@ -1276,7 +1430,8 @@ extern "C" int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uin
     StreamDrain drain{st, true};
     HIP_TRY(hipMemcpyAsync(d_in, hin, sizeof(h3c_chunk_state) * nchunks, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(d_ios, ios, sizeof(h3c_update_io) * n, hipMemcpyHostToDevice, st));
-    rc = update_core(poly_type, d_in, d_out, nchunks, d_ios, n, d_res, flags, d_ctr, st, dev, [&](hipStream_t s) -> int {
+    rc = update_core(poly_type, d_in, d_out, nchunks, d_ios, n, d_res, flags, d_ctr, st, dev,
+                     [&](hipStream_t s, const uint32_t *, uint32_t) -> int {
       HIP_TRY(hipMemcpyAsync(results, d_res, sizeof(h3c_update_result) * n, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipMemcpyAsync(hout, d_outblk, cb + 64, hipMemcpyDeviceToHost, s));
       return H3C_OK;
@@ -1310,10 +1465,14 @@ extern "C" int h3c_update_ios_dev(uint8_t poly_type, h3c_chunk_state *chunks_dev
                                            : carve<unsigned long long>(cur, kCtrN);
   StreamDrain drain{st, true};
   rc = update_core(poly_type, chunks_dev, d_out, nchunks, ios_dev, n, results_dev, flags, d_ctr, st, dev,
-                   [&](hipStream_t s) -> int {
-                     if (nchunks)
-                       HIP_TRY(hipMemcpyAsync(chunks_dev, d_out, sizeof(h3c_chunk_state) * nchunks,
-                                              hipMemcpyDeviceToDevice, s));
+                   [&](hipStream_t s, const uint32_t *d_F, uint32_t cap) -> int {
+                     // the final states replace the input table only once the fragment guess
+                     // held: a redo must start from the batch's original states
+                     if (nchunks) {
+                       hipLaunchKernelGGL(uio_commit_kernel, dim3((nchunks + 255) / 256), dim3(256), 0, s, d_out,
+                                          chunks_dev, nchunks, d_F, cap);
+                       HIP_TRY(hipGetLastError());
+                     }
                      return H3C_OK;
                    });
   if (rc) return rc;

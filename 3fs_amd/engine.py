@@ -88,6 +88,7 @@ _proto("h3c_update_blocks_ex", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, 
        _u32, _vp, _vp)
 _proto("h3c_test_hook", _int, _int, _u64)
 _proto("h3c_set_coalescing", _int, _int)
+_proto("h3c_diag_counter", _u64, _int)
 _proto("h3c_diag_sync_bench", _int, _int, _u64, _int, _int, _vp, _vp)
 _proto("h3c_update_ios_dev", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp)
 _proto("h3c_serde_checksum_mark", _u32, _u32, _int)
@@ -349,8 +350,13 @@ def sync_bench(threads: int, nbytes: int, calls: int, api: str = "verify"):
     return lat, wall.value
 
 
-HOOK_SEG_BYTES, HOOK_DEBUG_FLAGS, HOOK_UPD_SCAN = 1, 2, 3  # h3c_test_hook keys
+HOOK_SEG_BYTES, HOOK_DEBUG_FLAGS, HOOK_UPD_SCAN, HOOK_UPD_GRAPHS = 1, 2, 3, 4  # h3c_test_hook keys
 UPD_SCAN_PATHS = {"default": 0, "fused": 1, "tiles": 2, "sort": 3}
+
+
+def diag_counter(which: int) -> int:
+    """h3c_diag_counter: 0 UpdateIO graph replays, 1 captures, 2 capture failures."""
+    return int(lib.h3c_diag_counter(int(which)))
 
 
 def set_test_hook(key: int, value: int) -> None:

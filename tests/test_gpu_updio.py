@@ -725,3 +725,65 @@ def test_updio_fragment_guess_overflow_redo(h3c, torch_dev):
         else:
             sc.add(orc.UPD_EXTEND, c, 0, int(rng.integers(0, cs + 1)), orc.NONE)
     sc.check(*sc.run())
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_updio_repeated_batches_replay_graphs(h3c, torch_dev, hooks, graphs):
+    """The same device-resident batch run 4 times on the same buffers (state restored between
+    runs): the first call launches plainly, the second captures the pipeline into HIP graphs,
+    the later ones replay them.  Every run must equal the ChunkReplica::update replay."""
+    torch, dev = torch_dev
+    if not graphs:
+        hooks(h3c.HOOK_UPD_GRAPHS, 1)
+    rng = np.random.default_rng(91)
+    sc = random_scenario(h3c, torch, dev, rng, nchunks=10, chunk_size=64 << 10, nops=2500)
+    chunks, ios = sc.device_ios()
+    d_chunks0 = torch.from_numpy(chunks.view(np.uint8).copy()).to(dev)
+    d_chunks = d_chunks0.clone()
+    d_ios = torch.from_numpy(ios.view(np.uint8).copy()).to(dev)
+    d_res = torch.zeros(len(ios) * h3c.UPDATE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    d_ctr = torch.zeros(8, dtype=torch.int64, device=dev)
+    slab0 = sc.slab.clone()
+    for it in range(4):
+        sc.slab.copy_(slab0)
+        d_chunks.copy_(d_chunks0)
+        d_res.fill_(0xA5)
+        torch.cuda.synchronize()
+        h3c.update_ios_dev(d_chunks, d_ios, d_res, counters=d_ctr)
+        torch.cuda.synchronize()
+        got_chunks = d_chunks.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)
+        res = d_res.cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)
+        sc.counters = h3c.UpdateCounters()
+        for f, v in zip(h3c.UpdateCounters._fields_, d_ctr.cpu().tolist()):
+            setattr(sc.counters, f[0], v)
+        sc.check(got_chunks, res)
+
+
+def test_updio_device_resident_redo_from_original_states(h3c, torch_dev):
+    """h3c_update_ios_dev on a fresh thread (no fragment-count history) with a batch of many
+    multi-block truncates / extends: the first attempt's fragment guess is short, so the
+    fragment stage is redone -- and it must start from the batch's original chunk states (the
+    device table is only overwritten once the guess held).  Appends make results depend on the
+    stored values."""
+    import threading
+
+    torch, dev = torch_dev
+    rng = np.random.default_rng(97)
+    cs = 64 << 10
+    sc = Scenario(h3c, torch, dev, 8, cs, rng, init="crc")
+    for r in range(40):
+        for c in range(8):
+            sc.add(orc.UPD_TRUNCATE, c, 0, int(rng.integers(0, 4096)), orc.NONE)
+            sc.add(orc.UPD_EXTEND, c, 0, cs, orc.NONE)  # 16 zero-fill fragments
+            size = sc.meta[c]["size"]
+            sc.add(orc.UPD_WRITE, c, int(rng.integers(0, size)), int(rng.integers(1, 3000)))
+    assert len(sc.ops) * 2 + 1024 < 40 * 8 * 17  # more fragments than the first guess
+    out = {}
+
+    def run():
+        out["r"] = sc.run(dev_api=True)
+
+    t = threading.Thread(target=run)
+    t.start()
+    t.join(timeout=120)
+    sc.check(*out["r"])
