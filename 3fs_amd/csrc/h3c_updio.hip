@@ -66,7 +66,9 @@ enum : uint8_t { kC_NONE_ = 0, kC_NONE = 1, kC_REUSE = 2, kC_COMBINE = 3, kC_REA
 // device counter slots (h3c_update_counters order)
 enum { kCtrNone, kCtrReuse, kCtrCombine, kCtrRead, kCtrRecalc, kCtrMismatch, kCtrInvalid, kCtrStale, kCtrN };
 // device scalars: the payload kernel's work counter, the chain-head counter
-enum { kMiscPieceWork, kMiscN = 4 };  // [2]: the fragment count read back
+// misc words: [kMiscA6] some client checksum failed A6 (the speculative pass is void);
+// [kMiscOutF], [kMiscOutA6]: the fragment count and that flag, copied for the one read-back
+enum { kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscN = 4 };
 
 // ---------------------------------------------------------------- scan elements
 
@@ -225,19 +227,34 @@ __device__ __forceinline__ bool applied_kind(uint8_t kind) {
 }
 
 // A6 (:193-207, engine.rs:297-312): the payload's raw CRC against the client's checksum.
+// The verdicts go to a6[] and one flag: the sizes, cases and fragments are computed meanwhile
+// assuming every check passes (a corrupted transfer is rare), and a failed check voids that
+// speculative pass (the block kernel writes nothing; the host redoes from the sizes on).
 __global__ void uio_verify_kernel(const h3c_update_io *__restrict__ ios, uint32_t n, const uint32_t *__restrict__ paycrc0,
-                                  const PolyConsts *__restrict__ pc, uint32_t std_domain, uint32_t *__restrict__ status,
-                                  uint32_t *__restrict__ payraw) {
+                                  const PolyConsts *__restrict__ pc, uint32_t std_domain,
+                                  const uint32_t *__restrict__ status, uint32_t *__restrict__ payraw,
+                                  uint32_t *__restrict__ a6, uint32_t *__restrict__ misc) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const h3c_update_io io = ios[i];
-  if (io.kind != H3C_UPD_WRITE || status[i] != H3C_OK) return;
-  const uint32_t poly = pc->poly;
-  const uint32_t raw = io.length ? paycrc0[i] ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(io.length, pc, poly), poly)
-                                 : 0xFFFFFFFFu;
-  payraw[i] = raw;
-  if (io.checksum_type != H3C_TYPE_NONE && io.length && (std_domain ? ~raw : raw) != io.checksum_value)
-    status[i] = H3C_ERR_CHECKSUM_MISMATCH;
+  uint32_t bad = 0;
+  if (io.kind == H3C_UPD_WRITE && status[i] == H3C_OK) {
+    const uint32_t poly = pc->poly;
+    const uint32_t raw = io.length ? paycrc0[i] ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(io.length, pc, poly), poly)
+                                   : 0xFFFFFFFFu;
+    payraw[i] = raw;
+    bad = io.checksum_type != H3C_TYPE_NONE && io.length && (std_domain ? ~raw : raw) != io.checksum_value;
+  }
+  a6[i] = bad;
+  if (bad) atomicOr(&misc[kMiscA6], 1u);
+}
+
+// After a failed A6: the verdicts into the statuses, and the flag cleared for the redo.
+__global__ void uio_merge_a6_kernel(const uint32_t *__restrict__ a6, uint32_t n, uint32_t *__restrict__ status,
+                                    uint32_t *__restrict__ misc) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) misc[kMiscA6] = 0;
+  if (i < n && a6[i] && status[i] == H3C_OK) status[i] = H3C_ERR_CHECKSUM_MISMATCH;
 }
 
 // The size / type map of each op, in sorted order.
@@ -711,13 +728,14 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
 __global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__restrict__ frags,
                                                              const uint32_t *__restrict__ d_F, uint32_t cap,
                                                              const PolyConsts *__restrict__ pc,
-                                                             uint32_t *__restrict__ eacc) {
+                                                             uint32_t *__restrict__ eacc,
+                                                             const uint32_t *__restrict__ misc) {
   __shared__ uint32_t lds[kLdsWords + kRedWords];
   for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
   const uint32_t *red_g = &pc->red[0][0][0];
   for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
   __syncthreads();
-  const uint32_t F = frag_count(d_F, cap);
+  const uint32_t F = misc[kMiscA6] ? 0u : frag_count(d_F, cap);  // a failed A6: this pass writes nothing
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
   const uint32_t lane = threadIdx.x & 63;
@@ -843,8 +861,13 @@ __global__ void uio_result_kernel(const OpPos *__restrict__ pos, const uint32_t 
                                   h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks,
                                   const uint32_t *__restrict__ t0v, uint8_t poly_type, uint32_t std_domain,
                                   uint32_t poly, h3c_update_result *__restrict__ res,
-                                  unsigned long long *__restrict__ ctr) {
+                                  unsigned long long *__restrict__ ctr, const uint32_t *__restrict__ d_F,
+                                  uint32_t *__restrict__ misc) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p == 0) {  // the pass's outcome, for the host's one read-back
+    misc[kMiscOutF] = *d_F;
+    misc[kMiscOutA6] = misc[kMiscA6];
+  }
   uint32_t c_none = 0, c_reuse = 0, c_comb = 0, c_read = 0, c_recalc = 0, c_mis = 0, c_inv = 0;
   if (p < n) {
     const OpPos r = pos[p];
@@ -926,12 +949,12 @@ __global__ void uio_t0_kernel(const h3c_chunk_state *__restrict__ chunks, uint32
   t0v[c] = t0;
 }
 
-// h3c_update_ios_dev: the final chunk states over the input table, unless the fragment
-// guess was short (the host then redoes the fragment stage from the original states).
+// h3c_update_ios_dev: the final chunk states over the input table, unless the pass is redone
+// (a short fragment guess or a failed A6): the redo starts from the original states.
 __global__ void uio_commit_kernel(const h3c_chunk_state *__restrict__ fin, h3c_chunk_state *__restrict__ chunks,
-                                  uint32_t nchunks, const uint32_t *__restrict__ d_F, uint32_t cap) {
+                                  uint32_t nchunks, const uint32_t *__restrict__ out, uint32_t cap) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < nchunks && *d_F <= cap) chunks[c] = fin[c];
+  if (c < nchunks && out[0] <= cap && !out[1]) chunks[c] = fin[c];  // out: kMiscOutF, kMiscOutA6
 }
 
 // H3C_UPD_EXACT: chunks whose stored checksum of the batch polynomial disagrees with the bytes.
@@ -1021,12 +1044,14 @@ struct UpdGraphs {
   uint64_t used = 0;
 };
 // The graphs of `key`, or nullptr when this call should launch plainly: the first sight of a
-// shape launches plainly (a caller whose buffers move every call never pays a capture); the
-// second sight returns an empty entry to capture into; later sights replay.  Graphs are not
+// shape launches plainly (a caller whose buffers move every call never pays a capture); a
+// shape seen among the last four plain calls returns an empty entry to capture into; later
+// sights replay.  Graphs are not
 // used while `st` itself is being captured, or with h3c_test_hook(H3C_HOOK_UPD_GRAPHS, 1).
 UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st) {
   thread_local UpdGraphs cache[4];
-  thread_local UpdGraphKey last{};
+  thread_local UpdGraphKey recent[4] = {};  // keys of the last plain calls (lease pools may alternate buffers)
+  thread_local uint32_t recent_next = 0;
   thread_local uint64_t tick = 0;
   if (h3c_rt::hook(H3C_HOOK_UPD_GRAPHS) == 1) return nullptr;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1057,9 +1082,12 @@ UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st) {
       g.used = tick;
       return g.failed ? nullptr : &g;
     }
-  const bool seen = last == key;
-  last = key;
-  if (!seen) return nullptr;
+  bool seen = false;
+  for (const UpdGraphKey &r : recent) seen = seen || r == key;
+  if (!seen) {
+    recent[recent_next++ & 3] = key;
+    return nullptr;
+  }
   UpdGraphs *victim = &cache[0];
   for (UpdGraphs &g : cache)
     if (g.used < victim->used) victim = &g;
@@ -1071,20 +1099,45 @@ UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st) {
   return victim;
 }
 
+// A per-thread, per-device stream to capture on: the caller's stream may be the legacy
+// default stream, which cannot be captured (a graph then launches on it all the same).
+hipStream_t capture_stream(int dev) {
+  thread_local hipStream_t cs[8] = {};
+  thread_local int cs_dev[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  for (int i = 0; i < 8; ++i)
+    if (cs_dev[i] == dev && cs[i]) return cs[i];
+  for (int i = 0; i < 8; ++i)
+    if (!cs[i]) {
+      if (hipStreamCreateWithFlags(&cs[i], hipStreamNonBlocking) != hipSuccess) {
+        cs[i] = nullptr;
+        return nullptr;
+      }
+      cs_dev[i] = dev;
+      return cs[i];
+    }
+  return nullptr;
+}
+
 // Captures what `body` enqueues on `st` (and the streams it forks) into an executable graph.
 template <class Body>
 int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out) {
-  if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) return H3C_ERR_HIP;
+  const hipError_t be = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+  if (be != hipSuccess) {
+    h3c_rt::set_error("graph capture: hipStreamBeginCapture", be);
+    return H3C_ERR_HIP;
+  }
   const int r = body();
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(st, &g);
   if (r || e != hipSuccess || !g) {
     if (g) (void)hipGraphDestroy(g);
+    if (!r) h3c_rt::set_error("graph capture: hipStreamEndCapture", e);  // (else the body's error stays)
     return r ? r : H3C_ERR_HIP;
   }
   const hipError_t ie = hipGraphInstantiate(&out, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   if (ie != hipSuccess) {
+    h3c_rt::set_error("graph capture: hipGraphInstantiate", ie);
     out = nullptr;
     return H3C_ERR_HIP;
   }
@@ -1125,7 +1178,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   const size_t tmp_bytes = std::max(std::max(sort_tmp, scan_tmp), std::max(szscan_tmp, ascan_tmp));
   const size_t N1 = (size_t)n + 1;
   uint32_t *d_status, *d_key, *d_idx, *d_skey, *d_order, *d_np, *d_pbase, *d_paycrc0, *d_payraw, *d_nfrag, *d_fbase,
-      *d_eacc, *d_t0, *d_cnp, *d_cbase, *d_ccrc, *d_misc;
+      *d_eacc, *d_t0, *d_cnp, *d_cbase, *d_ccrc, *d_misc, *d_a6;
   SzTy *d_sz, *d_szscan;
   OpPos *d_pos;
   Aff *d_tel, *d_tscan, *d_sel, *d_sscan;
@@ -1141,6 +1194,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     d_pbase = carve<uint32_t>(cur, N1);
     d_paycrc0 = carve<uint32_t>(cur, n);
     d_payraw = carve<uint32_t>(cur, n);
+    d_a6 = carve<uint32_t>(cur, n);
     d_nfrag = carve<uint32_t>(cur, N1);
     d_fbase = carve<uint32_t>(cur, N1);
     d_eacc = carve<uint32_t>(cur, n);
@@ -1174,25 +1228,41 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   StreamDrain drain_aux{aux->st, true};
   const uint32_t tb = 256, gb = (uint32_t)((n + tb) / tb);  // n + 1 threads (the scans' extra entry)
   const uint32_t cb = (C + tb) / tb;
-  auto scan_excl = [&](const uint32_t *in, uint32_t *out) -> hipError_t {
+  auto scan_excl = [&](const uint32_t *in, uint32_t *out, hipStream_t q) -> hipError_t {
     size_t t = tmp_bytes;
-    return rocprim::exclusive_scan(d_tmp, t, in, out, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), st);
+    return rocprim::exclusive_scan(d_tmp, t, in, out, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), q);
   };
-  // phase A: validation, payload CRCs + A6 and the INIT CRCs (second stream), sort, sizes,
-  // cases and fragment counts; joined back into `st` at its end
-  auto phase_a = [&]() -> int {
-    hipLaunchKernelGGL(uio_prep_kernel, dim3(gb), dim3(tb), 0, st, d_ios, n, d_chunks, nchunks, poly_type, stdf,
+  // sizes and types per op (a segmented scan), the reference's cases, fragment counts
+  auto phase_sizes = [&](hipStream_t q) -> int {
+    hipLaunchKernelGGL(uio_sz_elem_kernel, dim3(gb), dim3(tb), 0, q, d_ios, d_order, n, d_status, poly_type, stdf,
+                       d_sz);
+    HIP_TRY(hipGetLastError());
+    {
+      size_t t = tmp_bytes;
+      HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_sz, d_szscan, (size_t)n, SzTyOp(),
+                                             rocprim::equal_to<uint32_t>(), q));
+    }
+    hipLaunchKernelGGL(uio_classify_kernel, dim3(gb), dim3(tb), 0, q, d_ios, d_order, d_skey, n, d_chunks, nchunks,
+                       d_szscan, d_status, poly_type, stdf, d_pos, d_nfrag);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(scan_excl(d_nfrag, d_fbase, q));
+    return H3C_OK;
+  };
+  // phase A: validation, payload CRCs + A6 and the INIT CRCs (second stream), sort, and the
+  // speculative sizes / cases / fragment counts
+  auto phase_a = [&](hipStream_t q) -> int {
+    hipLaunchKernelGGL(uio_prep_kernel, dim3(gb), dim3(tb), 0, q, d_ios, n, d_chunks, nchunks, poly_type, stdf,
                        d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(scan_excl(d_np, d_pbase));
+    HIP_TRY(scan_excl(d_np, d_pbase, q));
     // second stream: payload CRCs and A6 first (the sizes wait for them), then the chunks CRC'd
     // from their bytes (t0); this stream sorts the ops meanwhile (the sort depends on neither)
-    HIP_TRY(hipEventRecord(aux->ready, st));
+    HIP_TRY(hipEventRecord(aux->ready, q));
     HIP_TRY(hipStreamWaitEvent(aux->st, aux->ready, 0));
     int r = h3c_rt::launch_op_piece_crc(aux->st, dev, poly_type, d_ios, d_pbase, n, d_pbase + n, d_paycrc0);
     if (r) return r;
     hipLaunchKernelGGL(uio_verify_kernel, dim3(gb), dim3(tb), 0, aux->st, d_ios, n, d_paycrc0, pc, stdf, d_status,
-                       d_payraw);
+                       d_payraw, d_a6, d_misc);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(aux->done, aux->st));
     hipLaunchKernelGGL(uio_init_count_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf,
@@ -1211,23 +1281,9 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     HIP_TRY(hipEventRecord(aux->init_done, aux->st));
     {
       size_t t = tmp_bytes;
-      HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, st));
+      HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, q));
     }
-    HIP_TRY(hipStreamWaitEvent(st, aux->done, 0));
-    hipLaunchKernelGGL(uio_sz_elem_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, n, d_status, poly_type, stdf,
-                       d_sz);
-    HIP_TRY(hipGetLastError());
-    {
-      size_t t = tmp_bytes;
-      HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_sz, d_szscan, (size_t)n, SzTyOp(),
-                                             rocprim::equal_to<uint32_t>(), st));
-    }
-    hipLaunchKernelGGL(uio_classify_kernel, dim3(gb), dim3(tb), 0, st, d_ios, d_order, d_skey, n, d_chunks, nchunks,
-                       d_szscan, d_status, poly_type, stdf, d_pos, d_nfrag);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(scan_excl(d_nfrag, d_fbase));
-    HIP_TRY(hipStreamWaitEvent(st, aux->init_done, 0));
-    return H3C_OK;
+    return phase_sizes(q);  // speculative: every A6 check passes (joined before the block kernel)
   };
 
   // ---- fragments, blocks, scans, results (redone once if the fragment guess was short) ----
@@ -1252,46 +1308,50 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     layout2(lease2.data());
     const uint32_t *d_F = d_fbase + n;
     const uint32_t fb = (cap + tb - 1) / tb;
-    auto phase_frag = [&]() -> int {  // fragments and their chains
-      if (attempt) HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, st));  // the first attempt's counters
-      hipLaunchKernelGGL(uio_frag_kernel, dim3((std::max(cap, hcap) + tb - 1) / tb), dim3(tb), 0, st, d_pos, d_fbase,
+    auto phase_frag = [&](hipStream_t q) -> int {  // fragments and their chains
+      if (attempt) HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, q));  // the first attempt's counters
+      hipLaunchKernelGGL(uio_frag_kernel, dim3((std::max(cap, hcap) + tb - 1) / tb), dim3(tb), 0, q, d_pos, d_fbase,
                          n, cap, d_ios, d_skey, d_chunks, d_frag, d_fkey, pc, d_hhead, hcap);
       HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(uio_tlink_kernel, dim3((cap + kLinkTile - 1) / kLinkTile), dim3(kLinkTile), 0, st, d_fkey,
+      hipLaunchKernelGGL(uio_tlink_kernel, dim3((cap + kLinkTile - 1) / kLinkTile), dim3(kLinkTile), 0, q, d_fkey,
                          d_F, cap, d_hhead, hcap - 1, d_gnext, d_prev);
       HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(uio_resolve_kernel, dim3(fb), dim3(tb), 0, st, d_fkey, d_F, cap, d_hhead, hcap - 1, d_gnext,
+      hipLaunchKernelGGL(uio_resolve_kernel, dim3(fb), dim3(tb), 0, q, d_fkey, d_F, cap, d_hhead, hcap - 1, d_gnext,
                          d_prev);
       HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(uio_heads_kernel, dim3(fb), dim3(tb), 0, st, d_prev, d_F, cap, d_frag);
+      hipLaunchKernelGGL(uio_heads_kernel, dim3(fb), dim3(tb), 0, q, d_prev, d_F, cap, d_frag);
       HIP_TRY(hipGetLastError());
+      if (attempt == 0) {  // the A6 verdicts (the block kernel reads the flag) and t0
+        HIP_TRY(hipStreamWaitEvent(q, aux->done, 0));
+        HIP_TRY(hipStreamWaitEvent(q, aux->init_done, 0));
+      }
       return H3C_OK;
     };
-    auto phase_b = [&]() -> int {  // t' per op, then s' per op (two affine scans by chunk), results
-      hipLaunchKernelGGL(uio_elem_kernel<TMapFn>, dim3(gb), dim3(tb), 0, st, TMapFn{d_pos, d_eacc, d_payraw, pc}, n,
+    auto phase_b = [&](hipStream_t q) -> int {  // t' per op, then s' per op (two affine scans by chunk), results
+      hipLaunchKernelGGL(uio_elem_kernel<TMapFn>, dim3(gb), dim3(tb), 0, q, TMapFn{d_pos, d_eacc, d_payraw, pc}, n,
                          d_tel);
       HIP_TRY(hipGetLastError());
       {
         size_t t = tmp_bytes;
         HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_tel, d_tscan, (size_t)n, AffOp{poly},
-                                               rocprim::equal_to<uint32_t>(), st));
+                                               rocprim::equal_to<uint32_t>(), q));
       }
-      hipLaunchKernelGGL(uio_elem_kernel<SMapFn>, dim3(gb), dim3(tb), 0, st,
+      hipLaunchKernelGGL(uio_elem_kernel<SMapFn>, dim3(gb), dim3(tb), 0, q,
                          SMapFn{d_pos, d_skey, nchunks, d_tscan, d_t0, d_eacc, d_payraw, pc}, n, d_sel);
       HIP_TRY(hipGetLastError());
       {
         size_t t = tmp_bytes;
         HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_sel, d_sscan, (size_t)n, AffOp{poly},
-                                               rocprim::equal_to<uint32_t>(), st));
+                                               rocprim::equal_to<uint32_t>(), q));
       }
       if (nchunks)
         HIP_TRY(
-            hipMemcpyAsync(d_chunks_out, d_chunks, sizeof(h3c_chunk_state) * nchunks, hipMemcpyDeviceToDevice, st));
-      hipLaunchKernelGGL(uio_result_kernel, dim3(gb), dim3(tb), 0, st, d_pos, d_skey, n, d_sscan, d_chunks,
-                         d_chunks_out, nchunks, d_t0, poly_type, stdf, poly, d_res, d_ctr);
+            hipMemcpyAsync(d_chunks_out, d_chunks, sizeof(h3c_chunk_state) * nchunks, hipMemcpyDeviceToDevice, q));
+      hipLaunchKernelGGL(uio_result_kernel, dim3(gb), dim3(tb), 0, q, d_pos, d_skey, n, d_sscan, d_chunks,
+                         d_chunks_out, nchunks, d_t0, poly_type, stdf, poly, d_res, d_ctr, d_F, d_misc);
       HIP_TRY(hipGetLastError());
       if (exact && nchunks) {
-        hipLaunchKernelGGL(uio_stale_kernel, dim3((nchunks + tb - 1) / tb), dim3(tb), 0, st, d_chunks, nchunks, d_t0,
+        hipLaunchKernelGGL(uio_stale_kernel, dim3((nchunks + tb - 1) / tb), dim3(tb), 0, q, d_chunks, nchunks, d_t0,
                            poly_type, stdf, d_ctr);
         HIP_TRY(hipGetLastError());
       }
@@ -1307,12 +1367,13 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                             d_ctr, lease1.data(), lease2.data(), aux->st};
       gr = upd_graphs(key, st);
     }
-    if (gr && !gr->a) {  // capture both phases once
-      rc = capture_graph(st, [&] {
-        const int r = phase_a();
-        return r ? r : phase_frag();
-      }, gr->a);
-      if (!rc) rc = capture_graph(st, phase_b, gr->b);
+    if (gr && !gr->a) {  // capture both phases once, on a capture stream of this thread
+      hipStream_t cst = capture_stream(dev);
+      rc = cst ? capture_graph(cst, [&] {
+        const int r = phase_a(cst);
+        return r ? r : phase_frag(cst);
+      }, gr->a) : H3C_ERR_HIP;
+      if (!rc) rc = capture_graph(cst, [&] { return phase_b(cst); }, gr->b);
       if (rc) {  // not capturable here: plain launches from now on for this shape
         gr->failed = true;
         (void)hipGetLastError();
@@ -1328,16 +1389,16 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       g_graph_stats[0].fetch_add(1);
     } else {
       if (attempt == 0) {
-        rc = phase_a();
+        rc = phase_a(st);
         if (rc) return rc;
       }
-      rc = phase_frag();
+      rc = phase_frag(st);
       if (rc) return rc;
     }
     const uint32_t blocks = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
     h3c_rt::ProfToken tok;
     HIP_TRY(h3c_rt::prof_begin(st, tok));
-    hipLaunchKernelGGL(uio_block_kernel, dim3(blocks), dim3(kThreads), 0, st, d_frag, d_F, cap, pc, d_eacc);
+    hipLaunchKernelGGL(uio_block_kernel, dim3(blocks), dim3(kThreads), 0, st, d_frag, d_F, cap, pc, d_eacc, d_misc);
     HIP_TRY(hipGetLastError());
     // algorithmic bytes, per op: a 4 KiB block read and written once plus 4 KiB of new bytes
     // (exact for BASELINE config 3's block-aligned 4 KiB writes; bench.py states the unit)
@@ -1345,11 +1406,11 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     if (use_graphs) {
       HIP_TRY(hipGraphLaunch(gr->b, st));
     } else {
-      rc = phase_b();
+      rc = phase_b(st);
       if (rc) return rc;
     }
-    HIP_TRY(hipMemcpyAsync(h_F, d_F, 4, hipMemcpyDeviceToHost, st));
-    rc = epilogue(st, d_F, cap);  // (outputs of an attempt whose fragment guess was short are redone)
+    HIP_TRY(hipMemcpyAsync(h_F, d_misc + kMiscOutF, 8, hipMemcpyDeviceToHost, st));
+    rc = epilogue(st, d_misc + kMiscOutF, cap);  // (a redone attempt's outputs are replaced)
     if (rc) return rc;
     const hipError_t se = hipStreamSynchronize(st);
     drain2.armed = false;
@@ -1358,15 +1419,23 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       h3c_rt::set_error("h3c_update_ios", se);
       return H3C_ERR_HIP;
     }
-    const uint32_t F = *h_F;
+    const uint32_t F = h_F[0], a6_failed = h_F[1];
     last_frags = F;
-    if (F <= cap) break;
-    if (attempt) {  // cannot happen: the count is exact on the second attempt
+    if (F <= cap && !a6_failed) break;
+    if (attempt) {  // cannot happen: the second attempt knows the count and the verdicts
       drain.armed = drain_aux.armed = false;
       h3c_rt::set_error_text("h3c_update_ios: fragment count changed between attempts");
       return H3C_ERR_HIP;
     }
-    cap = F;  // nothing was written (no chains ran): redo with the count known
+    // nothing was written (no chain ran): redo, with the count known and, after a failed A6,
+    // the sizes / cases / fragment counts recomputed from the real verdicts (F can only shrink)
+    cap = std::max(cap, F);
+    if (a6_failed) {
+      hipLaunchKernelGGL(uio_merge_a6_kernel, dim3(gb), dim3(tb), 0, st, d_a6, n, d_status, d_misc);
+      HIP_TRY(hipGetLastError());
+      rc = phase_sizes(st);
+      if (rc) return rc;
+    }
   }
   drain.armed = drain_aux.armed = false;
   return H3C_OK;
@@ -1465,12 +1534,12 @@ extern "C" int h3c_update_ios_dev(uint8_t poly_type, h3c_chunk_state *chunks_dev
                                            : carve<unsigned long long>(cur, kCtrN);
   StreamDrain drain{st, true};
   rc = update_core(poly_type, chunks_dev, d_out, nchunks, ios_dev, n, results_dev, flags, d_ctr, st, dev,
-                   [&](hipStream_t s, const uint32_t *d_F, uint32_t cap) -> int {
-                     // the final states replace the input table only once the fragment guess
-                     // held: a redo must start from the batch's original states
+                   [&](hipStream_t s, const uint32_t *outcome, uint32_t cap) -> int {
+                     // the final states replace the input table only if this pass is not
+                     // redone: a redo must start from the batch's original states
                      if (nchunks) {
                        hipLaunchKernelGGL(uio_commit_kernel, dim3((nchunks + 255) / 256), dim3(256), 0, s, d_out,
-                                          chunks_dev, nchunks, d_F, cap);
+                                          chunks_dev, nchunks, outcome, cap);
                        HIP_TRY(hipGetLastError());
                      }
                      return H3C_OK;

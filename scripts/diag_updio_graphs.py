@@ -46,4 +46,4 @@ for it in range(5):
     diff_fields = {f: int((res[f] != ref[0][f]).sum()) for f in ("status", "size", "value", "type")}
     print(f"run {it}: vs oracle {bad_oracle} ops wrong; vs run 0: {diff_fields}, chunks differ "
           f"{int((ch != ref[1]).sum())}, counters {d_ctr.cpu().tolist()}, graphs (replays, captures, failures) "
-          f"{[h3c.diag_counter(k) for k in range(3)]}", flush=True)
+          f"{[h3c.diag_counter(k) for k in range(3)]}; last error: {h3c.engine.lib.h3c_last_error()}", flush=True)
