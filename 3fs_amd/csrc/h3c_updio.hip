@@ -112,12 +112,19 @@ __host__ __device__ inline uint32_t hd_gf_mul(uint32_t a, uint32_t b, uint32_t p
 struct Aff {
   uint32_t m, e;
 };
+// The general composition is a real call, so a scan whose elements take the two short cuts
+// below never executes the bit-serial multiplies (inlined, they were if-converted and ran for
+// every element: 28 us per 100k-op scan on config 3, where every element is x^0 or 0).
+__host__ __device__ __attribute__((noinline)) Aff aff_general(Aff x, Aff y, uint32_t poly) {
+  return Aff{hd_gf_mul(x.m, y.m, poly), hd_gf_mul(x.e, y.m, poly) ^ y.e};
+}
 struct AffOp {
   uint32_t poly;
   __host__ __device__ Aff operator()(const Aff &x, const Aff &y) const {  // x, then y
     // most ops keep the chunk length (m = x^0): composing them is a XOR
     if (y.m == kOne) return Aff{x.m, x.e ^ y.e};
-    return Aff{hd_gf_mul(x.m, y.m, poly), hd_gf_mul(x.e, y.m, poly) ^ y.e};
+    if (y.m == 0u) return y;  // y forgets its input (case iv / full rewrite: s' = t')
+    return aff_general(x, y, poly);
   }
 };
 
@@ -932,12 +939,16 @@ __global__ void uio_init_count_kernel(const h3c_chunk_state *__restrict__ chunks
   crc0[c] = 0;
 }
 // t0 per chunk: the raw CRC of no bytes, the trusted stored value, or the bytes' CRC.
+// Also copies the chunk table to the output table, whose entries of chunks with ops the result
+// kernel replaces (the same chunks on a redone pass, so the copy is made once).
 __global__ void uio_t0_kernel(const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks, uint8_t poly_type,
                               uint32_t exact, uint32_t std_domain, const uint32_t *__restrict__ crc0,
-                              const PolyConsts *__restrict__ pc, uint32_t *__restrict__ t0v) {
+                              const PolyConsts *__restrict__ pc, uint32_t *__restrict__ t0v,
+                              h3c_chunk_state *__restrict__ chunks_out) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= nchunks) return;
   const h3c_chunk_state cs = chunks[c];
+  chunks_out[c] = cs;
   uint32_t t0;
   if (cs.size == 0 || cs.size > cs.chunk_size) {
     t0 = 0xFFFFFFFFu;
@@ -1013,16 +1024,147 @@ uint32_t bits_for(uint64_t v) {  // bits to represent values < v
 
 using SortMerge = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                              rocprim::default_config, 1024 * 1024>;
-using SortSweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                             rocprim::default_config, 0>;
 
-// rocPRIM sort of (chunk, op): one onesweep pass for keys of <= 8 bits, the merge-sort path
-// otherwise (faster below 1M items for wider keys, profiles/r02_prim_probe.txt).
+// ---- stable counting sort of (chunk, op) by 8-bit digits, for batches of <= 256 tiles ----
+// A pass is two launches with no initialised state: per-tile digit histograms, then a scatter
+// in which every tile sums the histograms of the tiles before it (and all of them, for the
+// digit bases) and ranks its items stably -- wave ranks from 8 ballots (lanes with the same
+// digit), wave offsets from a per-digit prefix over the 16 waves.  Keys of <= 8 bits take one
+// pass, <= 16 bits two (least significant digit first).  rocPRIM's onesweep pass measured
+// 33 us for 100k keys of 7 bits, its merge path ~50 us for wider keys (r02_prim_probe.txt).
+constexpr uint32_t kSortTile = 1024, kSortDigits = 256, kSortMaxTiles = 256;
+
+__global__ __launch_bounds__(kSortTile) void csort_count_kernel(const uint32_t *__restrict__ keys, uint32_t n,
+                                                                 uint32_t shift, uint32_t *__restrict__ counts) {
+  __shared__ uint32_t h[kSortDigits];
+  const uint32_t t = threadIdx.x, i = blockIdx.x * kSortTile + t;
+  if (t < kSortDigits) h[t] = 0;
+  __syncthreads();
+  if (i < n) atomicAdd(&h[(keys[i] >> shift) & (kSortDigits - 1)], 1u);
+  __syncthreads();
+  if (t < kSortDigits) counts[blockIdx.x * kSortDigits + t] = h[t];
+}
+
+__global__ __launch_bounds__(kSortTile) void csort_scatter_kernel(const uint32_t *__restrict__ keys,
+                                                                   const uint32_t *__restrict__ vals, uint32_t n,
+                                                                   uint32_t shift, uint32_t ntiles,
+                                                                   const uint32_t *__restrict__ counts,
+                                                                   uint32_t *__restrict__ okeys,
+                                                                   uint32_t *__restrict__ ovals) {
+  constexpr uint32_t kW = kSortTile / 64, kQ = kSortTile / kSortDigits, kU = 8;
+  // 17 KiB of LDS, so a scatter tile fits beside the payload-CRC kernel (140 KiB) on a CU
+  __shared__ uint32_t off[kSortDigits];  // where this tile's items of digit b start
+  __shared__ uint32_t wsum[kSortDigits / 64];
+  __shared__ uint32_t wc[kW][kSortDigits];  // per-wave digit counts, then their prefix over waves
+  uint32_t(*part)[kQ][kSortDigits] = reinterpret_cast<uint32_t(*)[kQ][kSortDigits]>(&wc[0][0]);  // first 8 KiB
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, tile = blockIdx.x;
+  {  // every tile's histogram, summed by 4 threads per digit with 8 loads in flight each
+    const uint32_t dg = t % kSortDigits, q = t / kSortDigits;
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t u0 = q; u0 < ntiles; u0 += kQ * kU) {
+      uint32_t c[kU];
+#pragma unroll
+      for (uint32_t j = 0; j < kU; ++j) {
+        const uint32_t u = u0 + j * kQ;
+        c[j] = u < ntiles ? counts[u * kSortDigits + dg] : 0u;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kU; ++j) {
+        tot += c[j];
+        pre += u0 + j * kQ < tile ? c[j] : 0u;
+      }
+    }
+    part[0][q][dg] = pre;
+    part[1][q][dg] = tot;
+  }
+  // this item's digit, and its rank among the wave's lanes with the same digit
+  const uint32_t i = tile * kSortTile + t;
+  const bool valid = i < n;
+  const uint32_t key = valid ? keys[i] : 0u, d = (key >> shift) & (kSortDigits - 1);
+  uint64_t m = __builtin_amdgcn_ballot_w64(valid);
+#pragma unroll
+  for (uint32_t b = 0; b < 8; ++b) {
+    const uint64_t s = __builtin_amdgcn_ballot_w64((d >> b) & 1u);
+    m &= ((d >> b) & 1u) ? s : ~s;
+  }
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint32_t rank = (uint32_t)__popcll(m & below);
+  __syncthreads();
+  if (t < kSortDigits) {
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q) {
+      pre += part[0][q][t];
+      tot += part[1][q][t];
+    }
+    uint32_t inc = tot;  // inclusive scan of the digit totals: in the wave, then across 4 waves
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t x = (uint32_t)__shfl_up((int)inc, o, 64);
+      if (lane >= o) inc += x;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    off[t] = inc - tot + pre;
+  }
+  __syncthreads();  // part is consumed: its LDS becomes the per-wave counts
+  for (uint32_t e = t; e < kW * kSortDigits; e += kSortTile) wc[e / kSortDigits][e % kSortDigits] = 0;
+  if (t < kSortDigits) {
+    uint32_t add = 0;
+    for (uint32_t w = 0; w < wave; ++w) add += wsum[w];
+    off[t] += add;
+  }
+  __syncthreads();
+  if (valid && rank == 0) wc[wave][d] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (t < kSortDigits) {
+    uint32_t run = 0;
+    for (uint32_t w = 0; w < kW; ++w) {
+      const uint32_t x = wc[w][t];
+      wc[w][t] = run;
+      run += x;
+    }
+  }
+  __syncthreads();
+  if (valid) {
+    const uint32_t dst = off[d] + wc[wave][d] + rank;
+    okeys[dst] = key;
+    ovals[dst] = vals[i];
+  }
+}
+
+size_t csort_tmp_bytes(uint32_t n) {  // counts, and the keys / values between two passes
+  const size_t ntiles = (n + kSortTile - 1) / kSortTile;
+  return 4 * ntiles * kSortDigits + 256 + 8ull * n + 512;
+}
+bool csort_fits(uint32_t n, uint32_t bits) { return bits <= 16 && (n + kSortTile - 1) / kSortTile <= kSortMaxTiles; }
+
+// Sort of (chunk, op), stable: the counting sort when it fits, else rocPRIM's merge-sort path
+// (faster below 1M items than its onesweep passes for wide keys, profiles/r02_prim_probe.txt).
 hipError_t sort_pairs(void *tmp, size_t &tmp_bytes, const uint32_t *k, uint32_t *k2, const uint32_t *v, uint32_t *v2,
                       uint32_t n, uint32_t bits, hipStream_t st) {
-  if (bits <= 8)
-    return rocprim::radix_sort_pairs<SortSweep>(tmp, tmp_bytes, k, k2, v, v2, n, 0, std::max(bits, 1u), st);
-  return rocprim::radix_sort_pairs<SortMerge>(tmp, tmp_bytes, k, k2, v, v2, n, 0, bits, st);
+  if (!csort_fits(n, bits))
+    return rocprim::radix_sort_pairs<SortMerge>(tmp, tmp_bytes, k, k2, v, v2, n, 0, bits, st);
+  if (!tmp) {
+    tmp_bytes = csort_tmp_bytes(n);
+    return hipSuccess;
+  }
+  if (tmp_bytes < csort_tmp_bytes(n)) return hipErrorInvalidValue;
+  const uint32_t ntiles = std::max(1u, (n + kSortTile - 1) / kSortTile);
+  char *p = static_cast<char *>(tmp);
+  uint32_t *counts = reinterpret_cast<uint32_t *>(p);
+  p += (4ull * ntiles * kSortDigits + 255) & ~size_t(255);
+  uint32_t *mk = reinterpret_cast<uint32_t *>(p), *mv = mk + n;
+  const bool two = bits > 8;
+  const uint32_t *ik = k, *iv = v;
+  for (uint32_t pass = 0; pass < (two ? 2u : 1u); ++pass) {
+    uint32_t *ok = two && pass == 0 ? mk : k2, *ov = two && pass == 0 ? mv : v2;
+    hipLaunchKernelGGL(csort_count_kernel, dim3(ntiles), dim3(kSortTile), 0, st, ik, n, 8 * pass, counts);
+    hipLaunchKernelGGL(csort_scatter_kernel, dim3(ntiles), dim3(kSortTile), 0, st, ik, iv, n, 8 * pass, ntiles,
+                       counts, ok, ov);
+    ik = ok;
+    iv = ov;
+  }
+  return hipGetLastError();
 }
 
 
@@ -1276,7 +1418,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     r = h3c_rt::launch_chunk_piece_crc(aux->st, dev, poly_type, d_chunks, d_cbase, nchunks, d_cbase + nchunks, d_ccrc);
     if (r) return r;
     hipLaunchKernelGGL(uio_t0_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf, stdf,
-                       d_ccrc, pc, d_t0);
+                       d_ccrc, pc, d_t0, d_chunks_out);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(aux->init_done, aux->st));
     {
@@ -1344,9 +1486,6 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         HIP_TRY(rocprim::inclusive_scan_by_key(d_tmp, t, d_skey, d_sel, d_sscan, (size_t)n, AffOp{poly},
                                                rocprim::equal_to<uint32_t>(), q));
       }
-      if (nchunks)
-        HIP_TRY(
-            hipMemcpyAsync(d_chunks_out, d_chunks, sizeof(h3c_chunk_state) * nchunks, hipMemcpyDeviceToDevice, q));
       hipLaunchKernelGGL(uio_result_kernel, dim3(gb), dim3(tb), 0, q, d_pos, d_skey, n, d_sscan, d_chunks,
                          d_chunks_out, nchunks, d_t0, poly_type, stdf, poly, d_res, d_ctr, d_F, d_misc);
       HIP_TRY(hipGetLastError());

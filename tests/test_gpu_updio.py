@@ -250,6 +250,19 @@ def test_updio_large_batch(h3c, torch_dev):
     sc.check(*sc.run())
 
 
+@pytest.mark.parametrize("nchunks,chunk_kib,nops", [(300, 8, 6000), (3000, 4, 4000), (70000, 4, 3000)])
+def test_updio_many_chunks_sort_paths(h3c, torch_dev, nchunks, chunk_kib, nops):
+    """The ops' sort by chunk: keys of <= 8 bits take one counting-sort pass (every test above),
+    9-16 bits two passes (300 and 3000 chunks), wider keys rocPRIM's merge sort (70000)."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(nchunks)
+    sc = random_scenario(h3c, torch, dev, rng, nchunks=nchunks, chunk_size=chunk_kib << 10, nops=nops)
+    sc.check(*sc.run())
+    sc2 = random_scenario(h3c, torch, dev, np.random.default_rng(nchunks + 1), nchunks=nchunks,
+                          chunk_size=chunk_kib << 10, nops=nops)
+    sc2.check(*sc2.run(dev_api=True))
+
+
 def test_updio_hot_region_conflicts(h3c, torch_dev):
     """Many overlapping writes into the first 16 KiB of two chunks: long epoch chains."""
     torch, dev = torch_dev
