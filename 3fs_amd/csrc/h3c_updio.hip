@@ -658,10 +658,17 @@ __device__ __forceinline__ uint4 load_new(uint64_t src, uint32_t row, uint32_t r
   return row_full(row, w0, w1) ? v : and4(v, mask16(rel, w0, w1));
 }
 
+#ifndef H3C_UIO_NT_STORES
+#define H3C_UIO_NT_STORES 1
+#endif
 __device__ __forceinline__ void store_masked(uint64_t blk, uint32_t rel, uint4 v, uint32_t k0, uint32_t k1) {
   if (rel >= k0 && rel + 16 <= k1) {
     v4u w = {v.x, v.y, v.z, v.w};
+#if H3C_UIO_NT_STORES
     __builtin_nontemporal_store(w, (v4u __attribute__((address_space(1))) *)(blk + rel));
+#else
+    *(v4u __attribute__((address_space(1))) *)(blk + rel) = w;
+#endif
   } else if (rel + 16 > k0 && rel < k1) {  // a word shared with a neighbouring chunk: its own bytes only
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint8_t *p = reinterpret_cast<uint8_t *>(blk + rel);
