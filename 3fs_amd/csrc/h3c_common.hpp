@@ -16,6 +16,7 @@ namespace h3c_rt {
 // Per-device constant block for `type` (H3C_TYPE_CRC32C / H3C_TYPE_CRC32), built on first use.
 const void *device_consts(int dev, int type);
 int device_num_cu(int dev);
+int device_wall_clock_khz(int dev);  // the rate of the device's wall_clock64() counter
 // hipGetDevice + lazy init; returns H3C_OK or an h3c_status.
 int current_device(int *dev);
 void set_error(const char *what, hipError_t e);
@@ -27,6 +28,10 @@ struct ProfToken {
 };
 hipError_t prof_begin(hipStream_t st, ProfToken &t);
 hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes);
+// For launches timed by hipEvents recorded inside a replayed graph: whether profiling is on, and
+// one launch's measured time added to the totals.
+bool prof_enabled();
+void prof_add(int kind, float ms, uint64_t bytes);
 
 // Pinned host staging for the synchronous entry points.  Every host<->device transfer
 // of host-side metadata or pageable payloads goes through one of these: a pageable

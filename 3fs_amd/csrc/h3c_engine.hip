@@ -813,6 +813,7 @@ struct DeviceCtx {
   int status = H3C_ERR_NO_DEVICE;
   PolyConsts *d_consts[2] = {nullptr, nullptr};  // [0] CRC32C, [1] CRC32
   int num_cu = 0;
+  int wall_khz = 0;  // wall_clock64() rate
 };
 DeviceCtx g_dev[kMaxDevices];
 
@@ -825,6 +826,10 @@ int init_device(int dev) {
     auto body = [&]() -> int {
       HIP_TRY(hipSetDevice(dev));
       HIP_TRY(hipDeviceGetAttribute(&ctx.num_cu, hipDeviceAttributeMultiprocessorCount, dev));
+      if (hipDeviceGetAttribute(&ctx.wall_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) {
+        ctx.wall_khz = 0;  // the in-graph UpdateIO block kernel then goes untimed
+        (void)hipGetLastError();
+      }
       const uint32_t polys[2] = {kPolyCrc32c, kPolyCrc32};
       std::vector<PolyConsts> h(1);  // ~130 KiB: not on the caller's stack
       for (int i = 0; i < 2; ++i) {
@@ -884,6 +889,7 @@ const void *device_consts(int dev, int type) {
   return g_dev[dev].d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
 }
 int device_num_cu(int dev) { return (dev >= 0 && dev < kMaxDevices) ? g_dev[dev].num_cu : 0; }
+int device_wall_clock_khz(int dev) { return (dev >= 0 && dev < kMaxDevices) ? g_dev[dev].wall_khz : 0; }
 uint64_t hook(int key) { return (key > 0 && key < kHooks) ? g_hooks[key].load(std::memory_order_relaxed) : 0; }
 int current_device(int *dev) { return ::current_device(dev); }
 void set_error(const char *what, hipError_t e) { ::set_error(what, e); }
@@ -1003,6 +1009,15 @@ hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes
   std::lock_guard<std::mutex> lk(g_prof_mu);
   g_prof.push_back(ProfRec{t.a, t.b, bytes, kind});
   return e;
+}
+
+bool prof_enabled() { return g_prof_on.load() != 0; }
+void prof_add(int kind, float ms, uint64_t bytes) {
+  if (kind < 0 || kind >= kProfKinds) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof_ms_done[kind] += ms;
+  g_prof_launch_done[kind] += 1;
+  g_prof_bytes_done[kind] += bytes;
 }
 
 int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint32_t nchunks, uint32_t total_segs,

@@ -67,8 +67,10 @@ enum : uint8_t { kC_NONE_ = 0, kC_NONE = 1, kC_REUSE = 2, kC_COMBINE = 3, kC_REA
 enum { kCtrNone, kCtrReuse, kCtrCombine, kCtrRead, kCtrRecalc, kCtrMismatch, kCtrInvalid, kCtrStale, kCtrN };
 // device scalars: the payload kernel's work counter, the chain-head counter
 // misc words: [kMiscA6] some client checksum failed A6 (the speculative pass is void);
-// [kMiscOutF], [kMiscOutA6]: the fragment count and that flag, copied for the one read-back
-enum { kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscN = 4 };
+// [kMiscOutF], [kMiscOutA6]: the fragment count and that flag, copied for the one read-back;
+// [kMiscT0], [kMiscT1]: the block kernel's first start and last end (wall clock, u64 each), its
+// timing when it runs inside a replayed graph (read back with the two words before them)
+enum { kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscT0 = 4, kMiscT1 = 6, kMiscN = 8 };
 
 // ---------------------------------------------------------------- scan elements
 
@@ -185,7 +187,7 @@ __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t 
                                 unsigned long long *__restrict__ ctr, uint32_t *__restrict__ misc) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < kCtrN) ctr[i] = 0;
-  if (i < kMiscN) misc[i] = 0;
+  if (i < kMiscN) misc[i] = i == kMiscT0 || i == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;
   if (i < n) {  // XOR accumulators of the payload and block kernels
     paycrc0[i] = 0;
     eacc[i] = 0;
@@ -739,12 +741,10 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
 // keeping the next head's block and payload rows in flight while the current chain is folded
 // and stored.  Chains longer than one fragment (blocks written more than once in the batch)
 // continue with uniform loads.
-__global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__restrict__ frags,
-                                                             const uint32_t *__restrict__ d_F, uint32_t cap,
-                                                             const PolyConsts *__restrict__ pc,
-                                                             uint32_t *__restrict__ eacc,
-                                                             const uint32_t *__restrict__ misc) {
-  __shared__ uint32_t lds[kLdsWords + kRedWords];
+__device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frags, const uint32_t *__restrict__ d_F,
+                                               uint32_t cap, const PolyConsts *__restrict__ pc,
+                                               uint32_t *__restrict__ eacc, const uint32_t *__restrict__ misc,
+                                               uint32_t *lds) {
   for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
   const uint32_t *red_g = &pc->red[0][0][0];
   for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
@@ -818,6 +818,19 @@ __global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__r
       cur = nxt;
     }
   }
+}
+
+// ts (nullable): [0] the earliest workgroup start, [1] the latest wave end (wall clock).
+__global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__restrict__ frags,
+                                                             const uint32_t *__restrict__ d_F, uint32_t cap,
+                                                             const PolyConsts *__restrict__ pc,
+                                                             uint32_t *__restrict__ eacc,
+                                                             const uint32_t *__restrict__ misc,
+                                                             unsigned long long *ts) {
+  __shared__ uint32_t lds[kLdsWords + kRedWords];
+  if (ts && threadIdx.x == 0) atomicMin(&ts[0], (unsigned long long)wall_clock64());
+  uio_block_body(frags, d_F, cap, pc, eacc, misc, lds);
+  if (ts && (threadIdx.x & 63) == 0) atomicMax(&ts[1], (unsigned long long)wall_clock64());
 }
 
 __device__ __forceinline__ Aff t_map(const OpPos &r, const uint32_t *__restrict__ eacc, const uint32_t *__restrict__ payraw,
@@ -1188,7 +1201,7 @@ struct UpdGraphKey {
 };
 struct UpdGraphs {
   UpdGraphKey key{};
-  hipGraphExec_t a = nullptr, b = nullptr;
+  hipGraphExec_t g = nullptr;
   bool failed = false;
   uint64_t used = 0;
 };
@@ -1240,8 +1253,7 @@ UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st) {
   UpdGraphs *victim = &cache[0];
   for (UpdGraphs &g : cache)
     if (g.used < victim->used) victim = &g;
-  if (victim->a) (void)hipGraphExecDestroy(victim->a);
-  if (victim->b) (void)hipGraphExecDestroy(victim->b);
+  if (victim->g) (void)hipGraphExecDestroy(victim->g);
   *victim = UpdGraphs{};
   victim->key = key;
   victim->used = tick;
@@ -1503,23 +1515,38 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       }
       return H3C_OK;
     };
-    // The first attempt's phases run as two HIP graphs when this thread has seen the same
-    // batch shape and buffers before (the lease pools hand a steady caller the same ones):
-    // ~30 launches become two, so the short kernels run back to back instead of at the host's
-    // launch rate.  The block kernel stays a plain launch between them (profiled).
+    // The first attempt runs as one HIP graph when this thread has seen the same batch shape and
+    // buffers before (the lease pools hand a steady caller the same ones): ~30 launches and the
+    // block kernel become one launch, and the short kernels run back to back instead of at the
+    // host's launch rate.  The block kernel times itself there (wall clock).  (Two
+    // graphs with the block kernel launched between them cost ~30 us more per config-3 batch:
+    // the kernel after a multi-stream graph started ~24 us after the graph's last node,
+    // profiles/r02_updio_one_graph_ab.txt.)
+    const uint32_t blocks = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
+    auto block_kernel = [&](hipStream_t q, bool timed) -> int {
+      hipLaunchKernelGGL(uio_block_kernel, dim3(blocks), dim3(kThreads), 0, q, d_frag, d_F, cap, pc, d_eacc, d_misc,
+                         timed ? reinterpret_cast<unsigned long long *>(d_misc + kMiscT0) : nullptr);
+      HIP_TRY(hipGetLastError());
+      return H3C_OK;
+    };
+    // algorithmic bytes, per op: a 4 KiB block read and written once plus 4 KiB of new bytes
+    // (exact for BASELINE config 3's block-aligned 4 KiB writes; bench.py states the unit)
+    const uint64_t alg_bytes = 3ull * kBlk * n;
     UpdGraphs *gr = nullptr;
     if (attempt == 0) {
       const UpdGraphKey key{dev, poly_type, flags, n, nchunks, cap, hcap, d_chunks, d_chunks_out, d_ios, d_res,
                             d_ctr, lease1.data(), lease2.data(), aux->st};
       gr = upd_graphs(key, st);
     }
-    if (gr && !gr->a) {  // capture both phases once, on a capture stream of this thread
+    if (gr && !gr->g && !gr->failed) {  // capture the attempt once, on a capture stream of this thread
       hipStream_t cst = capture_stream(dev);
       rc = cst ? capture_graph(cst, [&] {
-        const int r = phase_a(cst);
-        return r ? r : phase_frag(cst);
-      }, gr->a) : H3C_ERR_HIP;
-      if (!rc) rc = capture_graph(cst, [&] { return phase_b(cst); }, gr->b);
+        int r = phase_a(cst);
+        if (!r) r = phase_frag(cst);
+        if (!r) r = block_kernel(cst, true);
+        if (!r) r = phase_b(cst);
+        return r;
+      }, gr->g) : H3C_ERR_HIP;
       if (rc) {  // not capturable here: plain launches from now on for this shape
         gr->failed = true;
         (void)hipGetLastError();
@@ -1529,9 +1556,9 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       }
       rc = H3C_OK;
     }
-    const bool use_graphs = gr && gr->a && gr->b && !gr->failed;
-    if (use_graphs) {
-      HIP_TRY(hipGraphLaunch(gr->a, st));
+    const bool use_graph = gr && gr->g && !gr->failed;
+    if (use_graph) {
+      HIP_TRY(hipGraphLaunch(gr->g, st));
       g_graph_stats[0].fetch_add(1);
     } else {
       if (attempt == 0) {
@@ -1540,22 +1567,16 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       }
       rc = phase_frag(st);
       if (rc) return rc;
-    }
-    const uint32_t blocks = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
-    h3c_rt::ProfToken tok;
-    HIP_TRY(h3c_rt::prof_begin(st, tok));
-    hipLaunchKernelGGL(uio_block_kernel, dim3(blocks), dim3(kThreads), 0, st, d_frag, d_F, cap, pc, d_eacc, d_misc);
-    HIP_TRY(hipGetLastError());
-    // algorithmic bytes, per op: a 4 KiB block read and written once plus 4 KiB of new bytes
-    // (exact for BASELINE config 3's block-aligned 4 KiB writes; bench.py states the unit)
-    HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDIO, 3ull * kBlk * n));
-    if (use_graphs) {
-      HIP_TRY(hipGraphLaunch(gr->b, st));
-    } else {
+      h3c_rt::ProfToken tok;
+      HIP_TRY(h3c_rt::prof_begin(st, tok));
+      rc = block_kernel(st, false);
+      if (rc) return rc;
+      HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDIO, alg_bytes));
       rc = phase_b(st);
       if (rc) return rc;
     }
-    HIP_TRY(hipMemcpyAsync(h_F, d_misc + kMiscOutF, 8, hipMemcpyDeviceToHost, st));
+    const bool prof_graph = use_graph && h3c_rt::prof_enabled();
+    HIP_TRY(hipMemcpyAsync(h_F, d_misc + kMiscOutF, 4 * (kMiscN - kMiscOutF), hipMemcpyDeviceToHost, st));
     rc = epilogue(st, d_misc + kMiscOutF, cap);  // (a redone attempt's outputs are replaced)
     if (rc) return rc;
     const hipError_t se = hipStreamSynchronize(st);
@@ -1564,6 +1585,13 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       drain.armed = drain_aux.armed = false;
       h3c_rt::set_error("h3c_update_ios", se);
       return H3C_ERR_HIP;
+    }
+    if (prof_graph) {  // the in-graph block kernel's own wall-clock span (hipEvents are not timed in a graph)
+      uint64_t t0, t1;
+      std::memcpy(&t0, h_F + (kMiscT0 - kMiscOutF), 8);
+      std::memcpy(&t1, h_F + (kMiscT1 - kMiscOutF), 8);
+      const int khz = h3c_rt::device_wall_clock_khz(dev);
+      if (t1 > t0 && khz > 0) h3c_rt::prof_add(H3C_PROF_UPDIO, (float)((double)(t1 - t0) / khz), alg_bytes);
     }
     const uint32_t F = h_F[0], a6_failed = h_F[1];
     last_frags = F;
