@@ -820,7 +820,7 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
   }
 }
 
-// ts (nullable): [0] the earliest workgroup start, [1] the latest wave end (wall clock).
+// ts (nullable): [0] the earliest workgroup start, [1] the latest workgroup end (wall clock).
 __global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__restrict__ frags,
                                                              const uint32_t *__restrict__ d_F, uint32_t cap,
                                                              const PolyConsts *__restrict__ pc,
@@ -830,7 +830,10 @@ __global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__r
   __shared__ uint32_t lds[kLdsWords + kRedWords];
   if (ts && threadIdx.x == 0) atomicMin(&ts[0], (unsigned long long)wall_clock64());
   uio_block_body(frags, d_F, cap, pc, eacc, misc, lds);
-  if (ts && (threadIdx.x & 63) == 0) atomicMax(&ts[1], (unsigned long long)wall_clock64());
+  if (ts) {  // one stamp per workgroup, once all its waves are done
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(&ts[1], (unsigned long long)wall_clock64());
+  }
 }
 
 __device__ __forceinline__ Aff t_map(const OpPos &r, const uint32_t *__restrict__ eacc, const uint32_t *__restrict__ payraw,
