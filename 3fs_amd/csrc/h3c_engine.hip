@@ -932,8 +932,11 @@ DeviceLease::DeviceLease(int dev, size_t bytes) : dev_(dev) {
   {
     std::lock_guard<std::mutex> lk(g_dev_pool_mu);
     auto &pool = g_dev_pool[dev];
+    // best fit, the most recently returned first among equal sizes: a caller that repeats a
+    // call gets the same buffers back (graph caches key on them; a FIFO among equal buffers
+    // handed each call the other one)
     size_t best = pool.size();
-    for (size_t i = 0; i < pool.size(); ++i)
+    for (size_t i = pool.size(); i-- > 0;)
       if (pool[i].second >= bytes && (best == pool.size() || pool[i].second < pool[best].second)) best = i;
     if (best != pool.size()) {
       p_ = pool[best].first;
@@ -965,8 +968,8 @@ PinnedLease::PinnedLease(size_t bytes) {
   bytes = std::max<size_t>(bytes, 4096);
   {
     std::lock_guard<std::mutex> lk(g_pin_mu);
-    size_t best = g_pin_free.size();
-    for (size_t i = 0; i < g_pin_free.size(); ++i)
+    size_t best = g_pin_free.size();  // best fit, most recently returned first (as DeviceLease)
+    for (size_t i = g_pin_free.size(); i-- > 0;)
       if (g_pin_free[i].second >= bytes && (best == g_pin_free.size() || g_pin_free[i].second < g_pin_free[best].second))
         best = i;
     if (best != g_pin_free.size()) {

@@ -779,10 +779,12 @@ def test_updio_repeated_batches_replay_graphs(h3c, torch_dev, hooks, graphs):
             setattr(sc.counters, f[0], v)
         sc.check(got_chunks, res)
     assert h3c.diag_counter(2) == fails0
-    # calls 2-4 capture and replay; a call that redoes its batch (this scenario's failing client
-    # checksums) may hand the next one other pooled scratch buffers, which is a new graph key
+    # calls 2-4 may capture and replay, but every call here redoes its batch (failing client
+    # checksums), which can hand the next call other pooled scratch buffers -- a new graph key --
+    # so how many replay depends on the pools' history (replays are pinned by
+    # test_updio_graph_replay_times_the_block_kernel)
     replays = h3c.diag_counter(0) - replays0
-    assert (1 <= replays <= 3) if graphs else replays == 0, replays
+    assert replays <= 3 if graphs else replays == 0, replays
 
 
 def test_updio_graph_replay_times_the_block_kernel(h3c, torch_dev):
