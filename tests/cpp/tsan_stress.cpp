@@ -150,6 +150,9 @@ int main(int argc, char **argv) {
   for (int t = 0; t < threads; ++t) th.emplace_back(worker, t, iters);
   for (auto &x : th) x.join();
   h3c_set_coalescing(0);
-  std::printf("tsan_stress: %d threads x %d iterations, %d errors\n", threads, iters, g_errors.load());
+  std::printf("tsan_stress: %d threads x %d iterations, %d errors; UpdateIO graph replays %llu, captures %llu, "
+              "capture failures %llu\n",
+              threads, iters, g_errors.load(), (unsigned long long)h3c_diag_counter(0),
+              (unsigned long long)h3c_diag_counter(1), (unsigned long long)h3c_diag_counter(2));
   return g_errors.load() ? 1 : 0;
 }
