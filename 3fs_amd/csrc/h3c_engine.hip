@@ -854,7 +854,13 @@ int device_count() {
   return n;
 }
 
+std::atomic<int> g_engine_threads{0};
 int current_device(int *dev) {
+  thread_local bool registered = false;
+  if (!registered) {
+    registered = true;
+    g_engine_threads.fetch_add(1, std::memory_order_relaxed);
+  }
   if (device_count() <= 0) {
     g_last_error = "no HIP device";
     return H3C_ERR_NO_DEVICE;
@@ -892,6 +898,7 @@ int device_num_cu(int dev) { return (dev >= 0 && dev < kMaxDevices) ? g_dev[dev]
 int device_wall_clock_khz(int dev) { return (dev >= 0 && dev < kMaxDevices) ? g_dev[dev].wall_khz : 0; }
 uint64_t hook(int key) { return (key > 0 && key < kHooks) ? g_hooks[key].load(std::memory_order_relaxed) : 0; }
 int current_device(int *dev) { return ::current_device(dev); }
+int engine_threads() { return g_engine_threads.load(std::memory_order_relaxed); }
 void set_error(const char *what, hipError_t e) { ::set_error(what, e); }
 void set_error_text(const char *text) { g_last_error = text; }
 }  // namespace h3c_rt
@@ -933,8 +940,7 @@ DeviceLease::DeviceLease(int dev, size_t bytes) : dev_(dev) {
     std::lock_guard<std::mutex> lk(g_dev_pool_mu);
     auto &pool = g_dev_pool[dev];
     // best fit, the most recently returned first among equal sizes: a caller that repeats a
-    // call gets the same buffers back (graph caches key on them; a FIFO among equal buffers
-    // handed each call the other one)
+    // call gets the same buffers back when nothing else leased meanwhile
     size_t best = pool.size();
     for (size_t i = pool.size(); i-- > 0;)
       if (pool[i].second >= bytes && (best == pool.size() || pool[i].second < pool[best].second)) best = i;

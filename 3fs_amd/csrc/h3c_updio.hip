@@ -42,6 +42,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -1219,6 +1220,13 @@ UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st) {
   thread_local uint32_t recent_next = 0;
   thread_local uint64_t tick = 0;
   if (h3c_rt::hook(H3C_HOOK_UPD_GRAPHS) == 1) return nullptr;
+  // Only while one thread uses the engine: a launch into the legacy default stream while any
+  // stream of the process is capturing fails in HIP ("operation not permitted when stream is
+  // capturing") and invalidates the capture, whatever the capture mode or the capture
+  // stream's flags -- a 16-thread stress with captures in flight saw hundreds of such failures
+  // (profiles/r02b_tsan.txt).  Replays (no capture) stay safe; a multi-threaded caller simply
+  // runs the plain launches.
+  if (h3c_rt::engine_threads() > 1 && h3c_rt::hook(H3C_HOOK_UPD_GRAPHS) != 2) return nullptr;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
     (void)hipGetLastError();
@@ -1283,9 +1291,19 @@ hipStream_t capture_stream(int dev) {
 }
 
 // Captures what `body` enqueues on `st` (and the streams it forks) into an executable graph.
+// One capture at a time in the process: under concurrent captures from several threads the
+// runtime failed captures and then other threads' launches ("operation failed due to a previous
+// error during capture", profiles/r02b_tsan.txt).  Captures are rare (once per batch shape
+// and thread), so the lock costs nothing in steady state.
+std::mutex g_capture_mu;
+
 template <class Body>
 int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out) {
-  const hipError_t be = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+  std::lock_guard<std::mutex> lk(g_capture_mu);
+  // Relaxed: the capture makes no synchronous or allocating call itself, and it should not make
+  // other threads' calls fail (under the thread-local mode a 16-thread stress saw another
+  // thread's hipMemcpy fail; see upd_graphs for the legacy-stream limit that remains).
+  const hipError_t be = hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed);
   if (be != hipSuccess) {
     h3c_rt::set_error("graph capture: hipStreamBeginCapture", be);
     return H3C_ERR_HIP;

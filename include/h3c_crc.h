@@ -401,7 +401,10 @@ enum h3c_hook {
   H3C_HOOK_SEG_BYTES = 1,   /* segment size of the create / verify kernels (multiple of 1 KiB) */
   H3C_HOOK_DEBUG_FLAGS = 2, /* bit0: no pipelined row loop; bit1: no small-chunk kernel; bit2: no uniform kernel */
   H3C_HOOK_UPD_SCAN = 3,    /* h3c_update_blocks: 1 fused, 2 dense tiles, 3 sort + scan_by_key */
-  H3C_HOOK_UPD_GRAPHS = 4   /* h3c_update_ios: 1 never replays its pipeline as HIP graphs */
+  H3C_HOOK_UPD_GRAPHS = 4   /* h3c_update_ios: 1 never replays its pipeline as HIP graphs; 2 captures
+                               them even after several threads have called the engine (by default
+                               only a single-threaded caller does: HIP fails legacy-stream launches
+                               made while any stream captures) */
 };
 int h3c_test_hook(int key, uint64_t value);
 /* Engine-internal counters for tests: 0 = h3c_update_ios pipeline graph replays, 1 = graph

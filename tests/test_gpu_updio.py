@@ -746,8 +746,7 @@ def test_updio_repeated_batches_replay_graphs(h3c, torch_dev, hooks, graphs):
     runs): the first call launches plainly, the second captures the pipeline into HIP graphs,
     the later ones replay them.  Every run must equal the ChunkReplica::update replay."""
     torch, dev = torch_dev
-    if not graphs:
-        hooks(h3c.HOOK_UPD_GRAPHS, 1)
+    hooks(h3c.HOOK_UPD_GRAPHS, 2 if graphs else 1)
     rng = np.random.default_rng(91)
     sc = random_scenario(h3c, torch, dev, rng, nchunks=10, chunk_size=64 << 10, nops=2500)
     chunks, ios = sc.device_ios()
@@ -787,12 +786,13 @@ def test_updio_repeated_batches_replay_graphs(h3c, torch_dev, hooks, graphs):
     assert replays <= 3 if graphs else replays == 0, replays
 
 
-def test_updio_graph_replay_times_the_block_kernel(h3c, torch_dev):
+def test_updio_graph_replay_times_the_block_kernel(h3c, torch_dev, hooks):
     """Block-aligned writes with good client checksums (no redo), one batch run 5 times: the later
     calls run the pipeline as one captured graph, the block kernel inside it timed by its own wall-clock
     stamps (the bench's roofline) -- one timed launch per call with a plausible duration -- and
     every run equal to the ChunkReplica::update replay."""
     torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_GRAPHS, 2)  # capture although other tests' threads have used the engine
     rng = np.random.default_rng(93)
     sc = Scenario(h3c, torch, dev, 6, 256 << 10, rng, init="crc")
     for _ in range(3000):
@@ -827,6 +827,36 @@ def test_updio_graph_replay_times_the_block_kernel(h3c, torch_dev):
     # the first sight of a shape launches plainly, a repeat captures, later ones replay (the
     # fragment-count guess carried over from an earlier test can make the first two shapes differ)
     assert replays[0] == 0 and replays[-2:] == [1, 1], replays
+
+
+def test_updio_graphs_only_single_threaded_by_default(h3c, torch_dev):
+    """Once several threads have called the engine, a repeated batch shape is not captured (HIP
+    fails legacy-stream launches made while any stream captures): the calls run plainly and
+    stay correct."""
+    import threading
+
+    torch, dev = torch_dev
+    t = threading.Thread(target=lambda: h3c.device_count() and h3c.crc32c(b"x" * 64))
+    t.start()
+    t.join()  # a second thread has used the engine (the module's own tests use more)
+    rng = np.random.default_rng(95)
+    sc = Scenario(h3c, torch, dev, 4, 64 << 10, rng, init="crc")
+    for _ in range(500):
+        sc.add(orc.UPD_WRITE, int(rng.integers(0, 4)), 4096 * int(rng.integers(0, 16)), 4096)
+    chunks, ios = sc.device_ios()
+    d_chunks0 = torch.from_numpy(chunks.view(np.uint8).copy()).to(dev)
+    d_ios = torch.from_numpy(ios.view(np.uint8).copy()).to(dev)
+    d_res = torch.zeros(len(ios) * h3c.UPDATE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    slab0 = sc.slab.clone()
+    r0, c0 = h3c.diag_counter(0), h3c.diag_counter(1)
+    for _ in range(4):
+        sc.slab.copy_(slab0)
+        d_chunks = d_chunks0.clone()
+        h3c.update_ios_dev(d_chunks, d_ios, d_res)
+        torch.cuda.synchronize()
+        sc.check(d_chunks.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE),
+                 d_res.cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE), counters=False)
+    assert (h3c.diag_counter(0), h3c.diag_counter(1)) == (r0, c0)
 
 
 def test_updio_device_resident_redo_from_original_states(h3c, torch_dev):
