@@ -1103,7 +1103,11 @@ int launch_op_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *
                         const uint32_t *d_total, uint32_t *crc0_out) {
   const DeviceCtx &ctx = g_dev[dev];
   const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
-  hipLaunchKernelGGL(op_piece_crc_kernel<IoPayloadSrc>, dim3(std::max(ctx.num_cu, 1)), dim3(kThreads), 0, st,
+#ifndef H3C_PIECE_CU_PCT
+#define H3C_PIECE_CU_PCT 100  // share of the CUs the UpdateIO payload-CRC kernel takes (A/B switch)
+#endif
+  hipLaunchKernelGGL(op_piece_crc_kernel<IoPayloadSrc>, dim3(std::max(ctx.num_cu * H3C_PIECE_CU_PCT / 100, 1)),
+                     dim3(kThreads), 0, st,
                      IoPayloadSrc{ios}, pbase, n, d_total, pc, crc0_out);
   HIP_TRY(hipGetLastError());
   return H3C_OK;
