@@ -272,6 +272,9 @@ constexpr int kUniBatch = H3C_UNI_BATCH;  // the same for seg_uni_kernel
 #ifndef H3C_UNI_LANES_LO
 #define H3C_UNI_LANES_LO 4  // seg_uni_kernel's lanes per chunk up to 6 rows of 1 KiB
 #endif
+#ifndef H3C_UNI_DYNAMIC
+#define H3C_UNI_DYNAMIC 1  // seg_uni_kernel: waves take steps from a per-workgroup counter (0: static split)
+#endif
 #ifndef H3C_UNI_LANES_HI
 #define H3C_UNI_LANES_HI 16
 #endif
@@ -463,19 +466,36 @@ __global__ __launch_bounds__(kThreads) void seg_uni_kernel(const DevChunk *__res
   constexpr int kRed = (1 + kLevels) * 1024;
   constexpr uint64_t kQ = 16u * G;
   __shared__ uint32_t lds[kLdsWords + kRed];
+  __shared__ uint32_t wg_next;
   for (int i = threadIdx.x; i < kLdsWords; i += kThreads)
     lds[i] = fill_value_of(kQ == 256 ? pc->tabq : kQ == 128 ? pc->tabo : kQ == 64 ? pc->tabf : kQ == 32 ? pc->tab2 : pc->tab1, i);
   const uint32_t *red_g = &pc->red[0][0][0];
   for (int i = threadIdx.x; i < kRed; i += kThreads) lds[kLdsWords + i] = red_g[i];
-  __syncthreads();
-  const uint32_t *red = lds + kLdsWords;
-  const char *lb = reinterpret_cast<const char *>(lds);
   const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if H3C_UNI_DYNAMIC
+  // The workgroup owns a contiguous range; its waves take steps of NG chunks from an LDS
+  // counter, so a wave slowed by its neighbours does not leave the others idle at the end
+  // (a static split per wave kept waves alive 81 % of the kernel at 8 lanes per chunk).
+  const uint32_t wlo = (uint32_t)((uint64_t)blockIdx.x * nchunks / gridDim.x);
+  const uint32_t hi = (uint32_t)((uint64_t)(blockIdx.x + 1) * nchunks / gridDim.x);
+  if (threadIdx.x == 0) wg_next = wlo;
+  __syncthreads();
+  auto grab = [&]() -> uint32_t {
+    uint32_t q = 0;
+    if (lane == 0) q = atomicAdd(&wg_next, NG);
+    return (uint32_t)__builtin_amdgcn_readfirstlane(q);
+  };
+  const uint32_t lo = grab();
+#else
+  __syncthreads();
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint32_t lo = (uint32_t)(gw * nchunks / nw), hi = (uint32_t)((gw + 1) * nchunks / nw);
+#endif
   if (lo >= hi) return;
+  const uint32_t *red = lds + kLdsWords;
+  const char *lb = reinterpret_cast<const char *>(lds);
   const LaneLut L = make_lut(lane);
   // quad q (chunks q .. q + NG - 1; this group's is q + grp): its first row address for this
   // lane, its result index and expected value
@@ -503,11 +523,17 @@ __global__ __launch_bounds__(kThreads) void seg_uni_kernel(const DevChunk *__res
 #pragma unroll
   for (int b = 0; b < kUniBatch; ++b)
     cur[b] = valid && (uint32_t)b < K ? load_row(la + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+#if H3C_UNI_DYNAMIC
+  for (uint32_t q0 = lo; q0 < hi;) {
+    const uint32_t qn = grab();  // the next step, taken now so its rows load during this one's last batch
+#else
   for (uint32_t q0 = lo; q0 < hi; q0 += NG) {
+    const uint32_t qn = q0 + NG;
+#endif
     uint64_t la1 = la;
     uint32_t o1 = o, want1 = want;
     bool valid1 = false;
-    if (q0 + NG < hi) quad(q0 + NG, la1, o1, want1, valid1);  // its rows load during this quad's last batch
+    if (qn < hi) quad(qn, la1, o1, want1, valid1);  // its rows load during this quad's last batch
     Streams st{0, 0, 0, 0};
     for (uint32_t u0 = 0; u0 < K; u0 += kUniBatch) {
       const uint32_t n0 = u0 + kUniBatch;
@@ -547,6 +573,9 @@ __global__ __launch_bounds__(kThreads) void seg_uni_kernel(const DevChunk *__res
     o = o1;
     want = want1;
     valid = valid1;
+#if H3C_UNI_DYNAMIC
+    q0 = qn;
+#endif
   }
 }
 
