@@ -374,3 +374,22 @@ def test_uniform_small_chunk_batches(h3c, torch_dev, hooks, flags, clen):
     want[5] = orc.crc32c(host[offs[5]: offs[5] + clen - 1])
     t, v = h3c.batch_create(items)
     assert [int(x) for x in v] == want
+
+
+@pytest.mark.parametrize("n", [1, 7, 17, 63, 300, 4097])
+def test_uniform_small_chunk_counts(h3c, torch_dev, n):
+    """seg_uni_kernel's waves take steps from a per-workgroup counter: batches smaller than a
+    step, than a wave's worth of groups and than the grid, and one just past a grid multiple."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(n)
+    for clen in (4096, 1024):
+        host = rng.integers(0, 256, n * clen, dtype=np.uint8)
+        buf = to_dev(torch, dev, host)
+        plan = h3c.Plan.uniform(buf.data_ptr(), clen, n)
+        out = torch.zeros(n, dtype=torch.int32, device=dev)
+        plan.run(out)
+        torch.cuda.synchronize()
+        exp = np.array([orc.crc32c(host[k * clen:(k + 1) * clen]) for k in range(n)], dtype=np.uint32)
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), exp), (n, clen)
+        plan.close()
+
