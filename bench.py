@@ -447,7 +447,9 @@ def run_updio(args, cx: Ctx) -> dict:
     def step():
         h3c.update_ios_dev(d_state, d_ios, d_res, stream=cx.stream, exact=exact, counters=d_ctr)
 
+    g0 = [h3c.diag_counter(k) for k in range(3)]
     elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDIO)
+    graphs = dict(zip(("replays", "captures", "capture_failures"), (h3c.diag_counter(k) - g0[k] for k in range(3))))
     torch.cuda.synchronize()
     fin = d_state.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)
     res = d_res.cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)
@@ -494,6 +496,7 @@ def run_updio(args, cx: Ctx) -> dict:
         # per write: payload read twice (A6 verify, then the block kernel), block read + write
         "algorithmic_gbps": round(writes * 4 * G / elapsed / 1e9, 1),
         "counters": counters,
+        "graphs": graphs,  # UpdateIO pipeline graph use over warmup + timed steps (one thread: replays)
         "pcie_inclusive": {"entry": "h3c_update_ios_ex (host tables in pinned memory)",
                            "value": round(nw * hsteps * cx.world / helapsed, 1), "unit": "writes/s",
                            "ms_per_step": round(helapsed / hsteps * 1e3, 4), "steps": hsteps},
