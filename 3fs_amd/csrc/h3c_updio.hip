@@ -1437,8 +1437,14 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                        d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc);
     HIP_TRY(hipGetLastError());
     HIP_TRY(scan_excl(d_np, d_pbase, q));
+    // The ops' sort first, alone: its latency-bound passes took ~70 us beside the bandwidth-bound
+    // payload-CRC kernel and ~12 us before it (profiles/r02_updio_sort_first_ab.txt)
+    {
+      size_t t = tmp_bytes;
+      HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, q));
+    }
     // second stream: payload CRCs and A6 first (the sizes wait for them), then the chunks CRC'd
-    // from their bytes (t0); this stream sorts the ops meanwhile (the sort depends on neither)
+    // from their bytes (t0); this stream runs the sizes and fragment stages meanwhile
     HIP_TRY(hipEventRecord(aux->ready, q));
     HIP_TRY(hipStreamWaitEvent(aux->st, aux->ready, 0));
     int r = h3c_rt::launch_op_piece_crc(aux->st, dev, poly_type, d_ios, d_pbase, n, d_pbase + n, d_paycrc0);
@@ -1461,10 +1467,6 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                        d_ccrc, pc, d_t0, d_chunks_out);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(aux->init_done, aux->st));
-    {
-      size_t t = tmp_bytes;
-      HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, q));
-    }
     return phase_sizes(q);  // speculative: every A6 check passes (joined before the block kernel)
   };
 
