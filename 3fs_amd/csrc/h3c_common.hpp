@@ -416,6 +416,32 @@ __device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const L
 __device__ __forceinline__ uint32_t fill_value_of(const uint32_t (*tab)[256], int i) {
   return tab[((i >> 14) << 1) | ((i >> 5) & 1)][(i >> 6) & 255];
 }
+// A 16-copy image of the same tables (64 KiB), for a kernel that runs two workgroups per CU:
+// table t, entry b, copy c at byte address b*256 + t*64 + c*4 (the v_perm address keeps b in
+// byte 1; byte 0 = t<<6 | c<<2).  Lanes l and l+16 share a copy: ds_read_b32 banks on
+// (addr/4)%32 = (t&1)*16 + c, a 2-way conflict inside each 32-lane half-wave.
+constexpr int kLdsWords16 = 4 * 256 * 16;  // 16384 dwords = 64 KiB
+__device__ __forceinline__ LaneLut make_lut16(uint32_t lane) {
+  LaneLut L;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) L.off[t] = ((uint32_t)t << 6) | ((lane & 15u) * 4u);
+  return L;
+}
+__device__ __forceinline__ uint32_t row_step16(uint32_t r, const char *lb, const LaneLut &L) {
+  const uint32_t a0 = __builtin_amdgcn_perm(r, L.off[0], 0x0C0C0400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(r, L.off[1], 0x0C0C0500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(r, L.off[2], 0x0C0C0600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(r, L.off[3], 0x0C0C0700u);
+  const uint32_t t0 = *reinterpret_cast<const uint32_t *>(lb + a0);
+  const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1);
+  const uint32_t t2 = *reinterpret_cast<const uint32_t *>(lb + a2);
+  const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3);
+  return xor3(t0, t1, t2) ^ t3;
+}
+// LDS dword i of the 16-copy image holds table (i>>4)&3, entry (i>>6)&255.
+__device__ __forceinline__ uint32_t fill_value16_of(const uint32_t (*tab)[256], int i) {
+  return tab[(i >> 4) & 3][(i >> 6) & 255];
+}
 #else
 // Layout: table k, entry b, copy c at byte address k*32 KiB + b*128 + c*4.
 __device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
@@ -497,6 +523,14 @@ __device__ __forceinline__ void consume(Streams &st, uint4 v, const char *lb, co
   st.s2 = row_step(st.s2 ^ v.z, lb, L);
   st.s3 = row_step(st.s3 ^ v.w, lb, L);
 }
+#if H3C_PERM_LAYOUT
+__device__ __forceinline__ void consume16(Streams &st, uint4 v, const char *lb, const LaneLut &L) {
+  st.s0 = row_step16(st.s0 ^ v.x, lb, L);
+  st.s1 = row_step16(st.s1 ^ v.y, lb, L);
+  st.s2 = row_step16(st.s2 ^ v.z, lb, L);
+  st.s3 = row_step16(st.s3 ^ v.w, lb, L);
+}
+#endif
 
 // a * C for the constant whose byte tables start at `t` (4 x 256 dwords in LDS).
 __device__ __forceinline__ uint32_t tab_mul(uint32_t a, const uint32_t *t) {

@@ -272,6 +272,13 @@ constexpr int kUniBatch = H3C_UNI_BATCH;  // the same for seg_uni_kernel
 #ifndef H3C_UNI_LANES_LO
 #define H3C_UNI_LANES_LO 4  // seg_uni_kernel's lanes per chunk up to 6 rows of 1 KiB
 #endif
+#ifndef H3C_UNI_COPIES
+#define H3C_UNI_COPIES 32  // seg_uni_kernel's LDS table copies: 32 (1 x 1024 threads per CU) or 16 (2 x 768)
+#endif
+constexpr int kUniCopies = H3C_UNI_COPIES;
+constexpr int kUniThreads = kUniCopies == 16 ? 768 : kThreads;
+constexpr int kUniWaves = kUniThreads / 64;
+constexpr int kUniLdsWords = kUniCopies == 16 ? kLdsWords16 : kLdsWords;
 #ifndef H3C_UNI_DYNAMIC
 #define H3C_UNI_DYNAMIC 1  // seg_uni_kernel: waves take steps from a per-workgroup counter (0: static split)
 #endif
@@ -454,7 +461,7 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
 // one value.  With chunks == nullptr the batch is contiguous (chunk i at base + i * stride,
 // result i): no descriptor at all.
 template <int G>
-__global__ __launch_bounds__(kThreads) void seg_uni_kernel(const DevChunk *__restrict__ chunks, uint64_t base,
+__global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni_kernel(const DevChunk *__restrict__ chunks, uint64_t base,
                                                           uint64_t stride, uint32_t nchunks, uint32_t K, uint32_t xs,
                                                           const PolyConsts *__restrict__ pc,
                                                           const uint32_t *__restrict__ expected,
@@ -465,14 +472,16 @@ __global__ __launch_bounds__(kThreads) void seg_uni_kernel(const DevChunk *__res
   constexpr uint32_t NG = 64 / G;
   constexpr int kRed = (1 + kLevels) * 1024;
   constexpr uint64_t kQ = 16u * G;
-  __shared__ uint32_t lds[kLdsWords + kRed];
+  __shared__ uint32_t lds[kUniLdsWords + kRed];
   __shared__ uint32_t wg_next;
-  for (int i = threadIdx.x; i < kLdsWords; i += kThreads)
-    lds[i] = fill_value_of(kQ == 256 ? pc->tabq : kQ == 128 ? pc->tabo : kQ == 64 ? pc->tabf : kQ == 32 ? pc->tab2 : pc->tab1, i);
+  {
+    const uint32_t(*tab)[256] = kQ == 256 ? pc->tabq : kQ == 128 ? pc->tabo : kQ == 64 ? pc->tabf : kQ == 32 ? pc->tab2 : pc->tab1;
+    for (int i = threadIdx.x; i < kUniLdsWords; i += kUniThreads)
+      lds[i] = kUniCopies == 16 ? fill_value16_of(tab, i) : fill_value_of(tab, i);
+  }
   const uint32_t *red_g = &pc->red[0][0][0];
-  for (int i = threadIdx.x; i < kRed; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  for (int i = threadIdx.x; i < kRed; i += kUniThreads) lds[kUniLdsWords + i] = red_g[i];
   const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #if H3C_UNI_DYNAMIC
   // The workgroup owns a contiguous range; its waves take steps of NG chunks from an LDS
   // counter, so a wave slowed by its neighbours does not leave the others idle at the end
@@ -489,14 +498,15 @@ __global__ __launch_bounds__(kThreads) void seg_uni_kernel(const DevChunk *__res
   const uint32_t lo = grab();
 #else
   __syncthreads();
-  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kUniWaves + wave;
+  const uint64_t nw = (uint64_t)gridDim.x * kUniWaves;
   const uint32_t lo = (uint32_t)(gw * nchunks / nw), hi = (uint32_t)((gw + 1) * nchunks / nw);
 #endif
   if (lo >= hi) return;
-  const uint32_t *red = lds + kLdsWords;
+  const uint32_t *red = lds + kUniLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
-  const LaneLut L = make_lut(lane);
+  const LaneLut L = kUniCopies == 16 ? make_lut16(lane) : make_lut(lane);
   // quad q (chunks q .. q + NG - 1; this group's is q + grp): its first row address for this
   // lane, its result index and expected value
   auto quad = [&](uint32_t q, uint64_t &la, uint32_t &o, uint32_t &want, bool &valid) {
@@ -548,7 +558,12 @@ __global__ __launch_bounds__(kThreads) void seg_uni_kernel(const DevChunk *__res
       }
 #pragma unroll
       for (int b = 0; b < kUniBatch; ++b)
-        if (u0 + b < K) consume(st, cur[b], lb, L);
+        if (u0 + b < K) {
+          if constexpr (kUniCopies == 16)
+            consume16(st, cur[b], lb, L);
+          else
+            consume(st, cur[b], lb, L);
+        }
 #pragma unroll
       for (int b = 0; b < kUniBatch; ++b) cur[b] = nxt[b];
     }
@@ -1071,20 +1086,22 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
     if (prof_kind >= 0) HIP_TRY(prof_begin(st, tok));
     if (H3C_SMALL_QUAD && uni && uni->lanes && !(dbg & 4u)) {  // test hook: H3C_DEBUG_FLAGS bit2 disables it
       const DevChunk *dc = uni->contiguous ? nullptr : d_chunks;
+      const uint32_t ublocks = std::min<uint32_t>(ctx.num_cu * (kUniCopies == 16 ? 2 : 1),
+                                                  (nchunks + kUniWaves - 1) / kUniWaves);
       if (uni->lanes == 1)
-        hipLaunchKernelGGL(seg_uni_kernel<1>, dim3(blocks), dim3(kThreads), 0, st, dc, uni->base, uni->stride,
+        hipLaunchKernelGGL(seg_uni_kernel<1>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
                            nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
       else if (uni->lanes == 2)
-        hipLaunchKernelGGL(seg_uni_kernel<2>, dim3(blocks), dim3(kThreads), 0, st, dc, uni->base, uni->stride,
+        hipLaunchKernelGGL(seg_uni_kernel<2>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
                            nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
       else if (uni->lanes == 4)
-        hipLaunchKernelGGL(seg_uni_kernel<4>, dim3(blocks), dim3(kThreads), 0, st, dc, uni->base, uni->stride,
+        hipLaunchKernelGGL(seg_uni_kernel<4>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
                            nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
       else if (uni->lanes == 8)
-        hipLaunchKernelGGL(seg_uni_kernel<8>, dim3(blocks), dim3(kThreads), 0, st, dc, uni->base, uni->stride,
+        hipLaunchKernelGGL(seg_uni_kernel<8>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
                            nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
       else
-        hipLaunchKernelGGL(seg_uni_kernel<16>, dim3(blocks), dim3(kThreads), 0, st, dc, uni->base, uni->stride,
+        hipLaunchKernelGGL(seg_uni_kernel<16>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
                            nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
     } else if (H3C_SMALL_QUAD)
       // up to ~5 KiB chunks 4 lanes per chunk (4 KiB: +8 % over 8 lanes, +13 % over 16);
