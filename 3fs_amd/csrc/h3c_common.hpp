@@ -666,13 +666,37 @@ __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, c
 #endif
       return make_uint4(v.x, v.y, v.z, v.w);
     };
-    // NOTE: an explicit two-buffer ping-pong form of this loop (no copy) miscompiled
-    // under ROCm 7.2 hipcc -O3 at kUnroll=4 (wrong CRCs from the first pipelined
-    // row; correct at -O1 and at kUnroll=2); this copy form is correct at every
-    // setting tried and the copies are register renames.
+    // NOTE: an explicit two-buffer ping-pong form of this loop (no copy) gave wrong CRCs
+    // under ROCm 7.2 hipcc -O3 at kUnroll=4 in round 1 (correct at -O1 and kUnroll=2).
+    // Rebuilt against the current source (H3C_PINGPONG=1 below) it is correct at -O3 and
+    // -O1 but 4 % slower (profiles/r02_pingpong_repro.txt), so the copy form stays; the
+    // copies are register renames.
     uint4 a[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) a[u] = ld(r + u);
+#if H3C_PINGPONG
+    // The two-buffer ping-pong form of the note above, kept as the miscompile reproducer
+    // (scripts/pingpong_repro.sh builds it at -O3 and -O1; profiles/r02_pingpong_repro.txt).
+    for (;;) {
+      uint4 b[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) b[u] = ld(r + kUnroll + u);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) consume(st, a[u], lb, L);
+      r += kUnroll;
+      if (r + kUnroll > plain_end) {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) a[u] = b[u];
+        break;
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) a[u] = ld(r + kUnroll + u);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) consume(st, b[u], lb, L);
+      r += kUnroll;
+      if (r + kUnroll > plain_end) break;
+    }
+#else
     for (;;) {
       uint4 b[kUnroll];
 #pragma unroll
@@ -684,6 +708,7 @@ __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, c
       for (int u = 0; u < kUnroll; ++u) a[u] = b[u];
       if (r + kUnroll > plain_end) break;
     }
+#endif
     // a[] holds rows r .. r+kUnroll-1; fewer than kUnroll plain rows remain.
 #pragma unroll
     for (int u = 0; u < kUnroll - 1; ++u)
