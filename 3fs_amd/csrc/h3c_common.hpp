@@ -132,12 +132,12 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
                const uint32_t *expected, uint32_t *out_raw, uint8_t *ok, uint32_t *mismatch, int prof_kind,
                uint32_t small_rows = 0, const UniformBatch *uni = nullptr);
 // Payload CRCs of UpdateIOs in 4 KiB pieces (op_piece_crc_kernel): crc0_out[i] ^= init-0 CRC
-// of op i's payload; pbase = exclusive scan of the per-op piece counts, *d_total their sum.
-int launch_op_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, const uint32_t *pbase, uint32_t n,
-                        const uint32_t *d_total, uint32_t *crc0_out);
-// The same over chunk contents [0, size) (pbase from per-chunk piece counts; 0 pieces skips a chunk).
-int launch_chunk_piece_crc(hipStream_t st, int dev, int type, const h3c_chunk_state *chunks, const uint32_t *pbase,
-                           uint32_t n, const uint32_t *d_total, uint32_t *crc0_out);
+// of item i; pbase = exclusive scan of the per-item piece counts, *d_total their sum.  Items:
+// the n op payloads followed by the contents [0, size) of nchunks chunks (item
+// n + c; 0 pieces skips an item): one launch for both, pbase over n + nchunks items.
+int launch_uio_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, uint32_t n,
+                         const h3c_chunk_state *chunks, uint32_t nchunks, const uint32_t *pbase,
+                         const uint32_t *d_total, uint32_t *crc0_out);
 // Rows (1 KiB, absolute alignment) a byte range touches.
 inline uint32_t host_rows(uint64_t ptr, uint64_t len) {
   return len ? (uint32_t)((((ptr + len + 1023) & ~uint64_t(1023)) - (ptr & ~uint64_t(1023))) / 1024) : 0;

@@ -601,18 +601,18 @@ __global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni
 // A group of 4 lanes owns a piece and walks it in 64-byte rows like seg_quad_kernel<4,1>; the
 // piece's init-0 CRC, moved to the end of its item (x^(8 (len - piece end))), is XORed into
 // crc0_out[i], which the caller zeroes.  Src::range(i, ptr, len) names item i's bytes.
-struct IoPayloadSrc {  // UpdateIO payloads
+struct UioPieceSrc {  // UpdateIO payloads (items < n), then chunk contents [0, size) (item n + c)
   const h3c_update_io *ios;
-  __device__ void range(uint32_t i, uint64_t &ptr, uint32_t &len) const {
-    ptr = ios[i].payload;
-    len = ios[i].length;
-  }
-};
-struct ChunkBytesSrc {  // chunk contents [0, size)
   const h3c_chunk_state *chunks;
+  uint32_t n;
   __device__ void range(uint32_t i, uint64_t &ptr, uint32_t &len) const {
-    ptr = chunks[i].base;
-    len = chunks[i].size;
+    if (i < n) {
+      ptr = ios[i].payload;
+      len = ios[i].length;
+    } else {
+      ptr = chunks[i - n].base;
+      len = chunks[i - n].size;
+    }
   }
 };
 
@@ -1145,26 +1145,16 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
   return H3C_OK;
 }
 
-int launch_op_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, const uint32_t *pbase, uint32_t n,
-                        const uint32_t *d_total, uint32_t *crc0_out) {
-  const DeviceCtx &ctx = g_dev[dev];
-  const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
 #ifndef H3C_PIECE_CU_PCT
 #define H3C_PIECE_CU_PCT 100  // share of the CUs the UpdateIO payload-CRC kernel takes (A/B switch)
 #endif
-  hipLaunchKernelGGL(op_piece_crc_kernel<IoPayloadSrc>, dim3(std::max(ctx.num_cu * H3C_PIECE_CU_PCT / 100, 1)),
-                     dim3(kThreads), 0, st,
-                     IoPayloadSrc{ios}, pbase, n, d_total, pc, crc0_out);
-  HIP_TRY(hipGetLastError());
-  return H3C_OK;
-}
-
-int launch_chunk_piece_crc(hipStream_t st, int dev, int type, const h3c_chunk_state *chunks, const uint32_t *pbase,
-                           uint32_t n, const uint32_t *d_total, uint32_t *crc0_out) {
+int launch_uio_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, uint32_t n,
+                         const h3c_chunk_state *chunks, uint32_t nchunks, const uint32_t *pbase,
+                         const uint32_t *d_total, uint32_t *crc0_out) {
   const DeviceCtx &ctx = g_dev[dev];
   const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
-  hipLaunchKernelGGL(op_piece_crc_kernel<ChunkBytesSrc>, dim3(std::max(ctx.num_cu, 1)), dim3(kThreads), 0, st,
-                     ChunkBytesSrc{chunks}, pbase, n, d_total, pc, crc0_out);
+  hipLaunchKernelGGL(op_piece_crc_kernel<UioPieceSrc>, dim3(std::max(ctx.num_cu * H3C_PIECE_CU_PCT / 100, 1)),
+                     dim3(kThreads), 0, st, UioPieceSrc{ios, chunks, n}, pbase, n + nchunks, d_total, pc, crc0_out);
   HIP_TRY(hipGetLastError());
   return H3C_OK;
 }

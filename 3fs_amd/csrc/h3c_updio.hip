@@ -26,10 +26,12 @@
 // bytes), XORs each fragment's CRC, moved to its op's end, into that op's E, and stores the
 // block once.  A block's traffic is one read, one write and its payload bytes.
 //
-// Pipeline (one stream; one device->host read of the fragment count in the middle):
-//   prep       per op: validation, payload piece count, sort key (chunk)
-//   payload    op_piece_crc_kernel: payload CRCs in 4 KiB pieces -> A6 verify (:193-207)
-//   sort       (chunk, op) pairs, stable (rocPRIM radix sort)
+// Pipeline (two streams, one graph per repeated batch; one device->host read at the end):
+//   prep       per op: validation, payload piece count, sort key (chunk); per chunk: the piece
+//              count of its bytes when t0 comes from them
+//   pieces     op_piece_crc_kernel: payload and chunk CRCs in 4 KiB pieces (second stream), one
+//              launch -> A6 verify (:193-207) and t0 per chunk, one launch
+//   sort       (chunk, op) pairs, stable (counting sort; rocPRIM merge sort past 16 key bits)
 //   sizes      segmented scan of the size / type maps {n -> max(n, b)} u {n -> c}
 //   classify   per op: size before / after, the reference's case, fragment range
 //   fragments  expansion, chain links (LDS tile grouping + hash of per-tile last links),
@@ -179,24 +181,33 @@ __device__ __forceinline__ void ctr_add_block(unsigned int *sh, unsigned long lo
 
 // ---------------------------------------------------------------- kernels
 
-// Validation (ChunkReplica.cc:140-145 range check; the ABI's preconditions), sort keys,
-// payload piece counts.
+// Chunks whose starting CRC t0 comes from their bytes (H3C_UPD_EXACT, or a stored checksum not
+// of this polynomial).
+__device__ __forceinline__ bool needs_init(const h3c_chunk_state &cs, uint8_t poly_type, uint32_t exact) {
+  return cs.size && cs.size <= cs.chunk_size && (exact || cs.type != poly_type);
+}
+
+// Validation (ChunkReplica.cc:140-145 range check; the ABI's preconditions), sort keys, and
+// the piece counts of the one piece-CRC pass: op i's payload is item i, chunk c's bytes (when
+// t0 comes from them) item n + c.  max(n, nchunks) + 1 threads.
 __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t n, const h3c_chunk_state *__restrict__ chunks,
-                                uint32_t nchunks, uint8_t poly_type, uint32_t std_domain, uint32_t *__restrict__ status,
-                                uint32_t *__restrict__ key, uint32_t *__restrict__ idx, uint32_t *__restrict__ npieces,
-                                uint32_t *__restrict__ paycrc0, uint32_t *__restrict__ eacc,
-                                unsigned long long *__restrict__ ctr, uint32_t *__restrict__ misc) {
+                                uint32_t nchunks, uint8_t poly_type, uint32_t std_domain, uint32_t exact,
+                                uint32_t *__restrict__ status, uint32_t *__restrict__ key, uint32_t *__restrict__ idx,
+                                uint32_t *__restrict__ npieces, uint32_t *__restrict__ paycrc0,
+                                uint32_t *__restrict__ eacc, unsigned long long *__restrict__ ctr,
+                                uint32_t *__restrict__ misc) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < kCtrN) ctr[i] = 0;
   if (i < kMiscN) misc[i] = i == kMiscT0 || i == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;
-  if (i < n) {  // XOR accumulators of the payload and block kernels
-    paycrc0[i] = 0;
-    eacc[i] = 0;
+  if (i < nchunks) {
+    const h3c_chunk_state cs = chunks[i];
+    npieces[n + i] = needs_init(cs, poly_type, exact) ? (cs.size + kPieceBytes - 1) / kPieceBytes : 0u;
+    paycrc0[n + i] = 0;
   }
-  if (i >= n) {
-    if (i == n) npieces[n] = 0;  // the scan's extra entry: pbase[n] = total
-    return;
-  }
+  if (i == nchunks) npieces[n + nchunks] = 0;  // the scan's extra entry: pbase[n + nchunks] = total
+  if (i >= n) return;
+  paycrc0[i] = 0;  // XOR accumulators of the piece and block kernels
+  eacc[i] = 0;
   const h3c_update_io io = ios[i];
   uint32_t st = H3C_OK;
   const uint32_t c = io.chunk;
@@ -240,12 +251,11 @@ __device__ __forceinline__ bool applied_kind(uint8_t kind) {
 // The verdicts go to a6[] and one flag: the sizes, cases and fragments are computed meanwhile
 // assuming every check passes (a corrupted transfer is rare), and a failed check voids that
 // speculative pass (the block kernel writes nothing; the host redoes from the sizes on).
-__global__ void uio_verify_kernel(const h3c_update_io *__restrict__ ios, uint32_t n, const uint32_t *__restrict__ paycrc0,
-                                  const PolyConsts *__restrict__ pc, uint32_t std_domain,
-                                  const uint32_t *__restrict__ status, uint32_t *__restrict__ payraw,
-                                  uint32_t *__restrict__ a6, uint32_t *__restrict__ misc) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__device__ __forceinline__ void verify_op(uint32_t i, const h3c_update_io *__restrict__ ios,
+                                          const uint32_t *__restrict__ paycrc0, const PolyConsts *__restrict__ pc,
+                                          uint32_t std_domain, const uint32_t *__restrict__ status,
+                                          uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6,
+                                          uint32_t *__restrict__ misc) {
   const h3c_update_io io = ios[i];
   uint32_t bad = 0;
   if (io.kind == H3C_UPD_WRITE && status[i] == H3C_OK) {
@@ -945,32 +955,13 @@ __global__ void uio_result_kernel(const OpPos *__restrict__ pos, const uint32_t 
   ctr_add_block(sh, ctr, v);
 }
 
-// Chunks whose starting CRC t0 comes from their bytes (H3C_UPD_EXACT, or a stored checksum not
-// of this polynomial): their 4 KiB piece counts, and zeroed CRC accumulators.
-__device__ __forceinline__ bool needs_init(const h3c_chunk_state &cs, uint8_t poly_type, uint32_t exact) {
-  return cs.size && cs.size <= cs.chunk_size && (exact || cs.type != poly_type);
-}
-__global__ void uio_init_count_kernel(const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks, uint8_t poly_type,
-                                      uint32_t exact, uint32_t *__restrict__ npieces, uint32_t *__restrict__ crc0) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c > nchunks) return;
-  if (c == nchunks) {
-    npieces[c] = 0;
-    return;
-  }
-  const h3c_chunk_state cs = chunks[c];
-  npieces[c] = needs_init(cs, poly_type, exact) ? (cs.size + kPieceBytes - 1) / kPieceBytes : 0u;
-  crc0[c] = 0;
-}
 // t0 per chunk: the raw CRC of no bytes, the trusted stored value, or the bytes' CRC.
 // Also copies the chunk table to the output table, whose entries of chunks with ops the result
 // kernel replaces (the same chunks on a redone pass, so the copy is made once).
-__global__ void uio_t0_kernel(const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks, uint8_t poly_type,
-                              uint32_t exact, uint32_t std_domain, const uint32_t *__restrict__ crc0,
-                              const PolyConsts *__restrict__ pc, uint32_t *__restrict__ t0v,
-                              h3c_chunk_state *__restrict__ chunks_out) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nchunks) return;
+__device__ __forceinline__ void t0_chunk(uint32_t c, const h3c_chunk_state *__restrict__ chunks, uint8_t poly_type,
+                                         uint32_t exact, uint32_t std_domain, const uint32_t *__restrict__ crc0,
+                                         const PolyConsts *__restrict__ pc, uint32_t *__restrict__ t0v,
+                                         h3c_chunk_state *__restrict__ chunks_out) {
   const h3c_chunk_state cs = chunks[c];
   chunks_out[c] = cs;
   uint32_t t0;
@@ -982,6 +973,20 @@ __global__ void uio_t0_kernel(const h3c_chunk_state *__restrict__ chunks, uint32
     t0 = std_domain ? ~cs.value : cs.value;
   }
   t0v[c] = t0;
+}
+
+// After the piece pass: A6 per op and t0 per chunk (the chunk CRCs are items n + c), one launch
+// of max(n, nchunks) threads.
+__global__ void uio_verify_t0_kernel(const h3c_update_io *__restrict__ ios, uint32_t n,
+                                     const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks, uint8_t poly_type,
+                                     uint32_t exact, uint32_t std_domain, const uint32_t *__restrict__ crc0,
+                                     const PolyConsts *__restrict__ pc, const uint32_t *__restrict__ status,
+                                     uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6,
+                                     uint32_t *__restrict__ misc, uint32_t *__restrict__ t0v,
+                                     h3c_chunk_state *__restrict__ chunks_out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) verify_op(i, ios, crc0, pc, std_domain, status, payraw, a6, misc);
+  if (i < nchunks) t0_chunk(i, chunks, poly_type, exact, std_domain, crc0 + n, pc, t0v, chunks_out);
 }
 
 // h3c_update_ios_dev: the final chunk states over the input table, unless the pass is redone
@@ -1012,7 +1017,7 @@ __global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uin
 struct AuxStream {
   int dev = -1;
   hipStream_t st = nullptr;
-  hipEvent_t ready = nullptr, done = nullptr, init_done = nullptr;
+  hipEvent_t ready = nullptr, done = nullptr;
 };
 int aux_stream(int dev, AuxStream *&out) {
   thread_local AuxStream aux[4];
@@ -1027,7 +1032,6 @@ int aux_stream(int dev, AuxStream *&out) {
   HIP_TRY(hipStreamCreateWithFlags(&a.st, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&a.ready, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&a.init_done, hipEventDisableTiming));
   a.dev = dev;
   out = &a;
   return H3C_OK;
@@ -1346,25 +1350,26 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   // needs more redoes its fragment stage once with the count known)
   thread_local uint32_t last_frags = 0;
   uint32_t cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * n + 1024, last_frags), 0x7FFFFFF0u);
-  size_t sort_tmp = 0, scan_tmp = 0, cscan_tmp = 0, szscan_tmp = 0, ascan_tmp = 0;
+  size_t sort_tmp = 0, scan_tmp = 0, pscan_tmp = 0, szscan_tmp = 0, ascan_tmp = 0;
   const uint32_t bits = bits_for((uint64_t)nchunks + 1);
   HIP_TRY(sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, n, bits, st));
   HIP_TRY(rocprim::exclusive_scan(nullptr, scan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)n + 1,
                                   rocprim::plus<uint32_t>(), st));
-  HIP_TRY(rocprim::exclusive_scan(nullptr, cscan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)C + 1,
-                                  rocprim::plus<uint32_t>(), st));
+  HIP_TRY(rocprim::exclusive_scan(nullptr, pscan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
+                                  (size_t)n + C + 1, rocprim::plus<uint32_t>(), st));
   HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, szscan_tmp, (uint32_t *)nullptr, (SzTy *)nullptr, (SzTy *)nullptr,
                                          (size_t)n, SzTyOp(), rocprim::equal_to<uint32_t>(), st));
   HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, ascan_tmp, (uint32_t *)nullptr, (Aff *)nullptr, (Aff *)nullptr,
                                          (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
-  const size_t tmp_bytes = std::max(std::max(sort_tmp, scan_tmp), std::max(szscan_tmp, ascan_tmp));
-  const size_t N1 = (size_t)n + 1;
+  const size_t tmp_bytes =
+      std::max(std::max(std::max(sort_tmp, scan_tmp), std::max(szscan_tmp, ascan_tmp)), pscan_tmp);
+  const size_t N1 = (size_t)n + 1, NP = (size_t)n + C;  // NP: piece-pass items (ops, then chunks)
   uint32_t *d_status, *d_key, *d_idx, *d_skey, *d_order, *d_np, *d_pbase, *d_paycrc0, *d_payraw, *d_nfrag, *d_fbase,
-      *d_eacc, *d_t0, *d_cnp, *d_cbase, *d_ccrc, *d_misc, *d_a6;
+      *d_eacc, *d_t0, *d_misc, *d_a6;
   SzTy *d_sz, *d_szscan;
   OpPos *d_pos;
   Aff *d_tel, *d_tscan, *d_sel, *d_sscan;
-  void *d_tmp, *d_ctmp;
+  void *d_tmp;
   auto layout = [&](char *base) -> size_t {  // one layout, run with base 0 to size the lease
     char *cur = base;
     d_status = carve<uint32_t>(cur, n);
@@ -1372,18 +1377,15 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     d_idx = carve<uint32_t>(cur, n);
     d_skey = carve<uint32_t>(cur, n);
     d_order = carve<uint32_t>(cur, n);
-    d_np = carve<uint32_t>(cur, N1);
-    d_pbase = carve<uint32_t>(cur, N1);
-    d_paycrc0 = carve<uint32_t>(cur, n);
+    d_np = carve<uint32_t>(cur, NP + 1);
+    d_pbase = carve<uint32_t>(cur, NP + 1);
+    d_paycrc0 = carve<uint32_t>(cur, NP);
     d_payraw = carve<uint32_t>(cur, n);
     d_a6 = carve<uint32_t>(cur, n);
     d_nfrag = carve<uint32_t>(cur, N1);
     d_fbase = carve<uint32_t>(cur, N1);
     d_eacc = carve<uint32_t>(cur, n);
     d_t0 = carve<uint32_t>(cur, C);
-    d_cnp = carve<uint32_t>(cur, (size_t)C + 1);
-    d_cbase = carve<uint32_t>(cur, (size_t)C + 1);
-    d_ccrc = carve<uint32_t>(cur, C);
     d_misc = carve<uint32_t>(cur, kMiscN);
     d_sz = carve<SzTy>(cur, n);
     d_szscan = carve<SzTy>(cur, n);
@@ -1393,7 +1395,6 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     d_sel = carve<Aff>(cur, n);
     d_sscan = carve<Aff>(cur, n);
     d_tmp = carve<char>(cur, tmp_bytes);
-    d_ctmp = carve<char>(cur, cscan_tmp);  // the chunk scan runs on the second stream
     return (size_t)(cur - base);
   };
   h3c_rt::DeviceLease lease1(dev, layout(nullptr));
@@ -1409,7 +1410,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   StreamDrain drain{st, true};  // every return below waits for both streams before the leases go back
   StreamDrain drain_aux{aux->st, true};
   const uint32_t tb = 256, gb = (uint32_t)((n + tb) / tb);  // n + 1 threads (the scans' extra entry)
-  const uint32_t cb = (C + tb) / tb;
+  const uint32_t pb = (uint32_t)((std::max<size_t>(n, C) + tb) / tb);  // max(n, nchunks) + 1 threads
+  const uint32_t vb = (uint32_t)((std::max<size_t>(n, C) + tb - 1) / tb);
   auto scan_excl = [&](const uint32_t *in, uint32_t *out, hipStream_t q) -> hipError_t {
     size_t t = tmp_bytes;
     return rocprim::exclusive_scan(d_tmp, t, in, out, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), q);
@@ -1433,40 +1435,31 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   // phase A: validation, payload CRCs + A6 and the INIT CRCs (second stream), sort, and the
   // speculative sizes / cases / fragment counts
   auto phase_a = [&](hipStream_t q) -> int {
-    hipLaunchKernelGGL(uio_prep_kernel, dim3(gb), dim3(tb), 0, q, d_ios, n, d_chunks, nchunks, poly_type, stdf,
-                       d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc);
+    hipLaunchKernelGGL(uio_prep_kernel, dim3(pb), dim3(tb), 0, q, d_ios, n, d_chunks, nchunks, poly_type, stdf,
+                       exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(scan_excl(d_np, d_pbase, q));
+    {
+      size_t t = tmp_bytes;
+      HIP_TRY(rocprim::exclusive_scan(d_tmp, t, d_np, d_pbase, 0u, NP + 1, rocprim::plus<uint32_t>(), q));
+    }
     // The ops' sort first, alone: its latency-bound passes took ~70 us beside the bandwidth-bound
     // payload-CRC kernel and ~12 us before it (profiles/r02_updio_sort_first_ab.txt)
     {
       size_t t = tmp_bytes;
       HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, q));
     }
-    // second stream: payload CRCs and A6 first (the sizes wait for them), then the chunks CRC'd
-    // from their bytes (t0); this stream runs the sizes and fragment stages meanwhile
+    // second stream: one piece-CRC pass over the payloads and the chunks CRC'd from their bytes
+    // (before the block kernel overwrites them), then A6 and t0; this stream runs the sizes and
+    // fragment stages meanwhile
     HIP_TRY(hipEventRecord(aux->ready, q));
     HIP_TRY(hipStreamWaitEvent(aux->st, aux->ready, 0));
-    int r = h3c_rt::launch_op_piece_crc(aux->st, dev, poly_type, d_ios, d_pbase, n, d_pbase + n, d_paycrc0);
+    int r = h3c_rt::launch_uio_piece_crc(aux->st, dev, poly_type, d_ios, n, d_chunks, nchunks, d_pbase, d_pbase + NP,
+                                         d_paycrc0);
     if (r) return r;
-    hipLaunchKernelGGL(uio_verify_kernel, dim3(gb), dim3(tb), 0, aux->st, d_ios, n, d_paycrc0, pc, stdf, d_status,
-                       d_payraw, d_a6, d_misc);
+    hipLaunchKernelGGL(uio_verify_t0_kernel, dim3(vb), dim3(tb), 0, aux->st, d_ios, n, d_chunks, nchunks, poly_type,
+                       exactf, stdf, d_paycrc0, pc, d_status, d_payraw, d_a6, d_misc, d_t0, d_chunks_out);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(aux->done, aux->st));
-    hipLaunchKernelGGL(uio_init_count_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf,
-                       d_cnp, d_ccrc);
-    HIP_TRY(hipGetLastError());
-    {
-      size_t t = cscan_tmp;
-      HIP_TRY(rocprim::exclusive_scan(d_ctmp, t, d_cnp, d_cbase, 0u, (size_t)nchunks + 1, rocprim::plus<uint32_t>(),
-                                      aux->st));
-    }
-    r = h3c_rt::launch_chunk_piece_crc(aux->st, dev, poly_type, d_chunks, d_cbase, nchunks, d_cbase + nchunks, d_ccrc);
-    if (r) return r;
-    hipLaunchKernelGGL(uio_t0_kernel, dim3(cb), dim3(tb), 0, aux->st, d_chunks, nchunks, poly_type, exactf, stdf,
-                       d_ccrc, pc, d_t0, d_chunks_out);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(aux->init_done, aux->st));
     return phase_sizes(q);  // speculative: every A6 check passes (joined before the block kernel)
   };
 
@@ -1507,7 +1500,6 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       HIP_TRY(hipGetLastError());
       if (attempt == 0) {  // the A6 verdicts (the block kernel reads the flag) and t0
         HIP_TRY(hipStreamWaitEvent(q, aux->done, 0));
-        HIP_TRY(hipStreamWaitEvent(q, aux->init_done, 0));
       }
       return H3C_OK;
     };
