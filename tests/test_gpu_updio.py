@@ -263,6 +263,21 @@ def test_updio_many_chunks_sort_paths(h3c, torch_dev, nchunks, chunk_kib, nops):
     sc2.check(*sc2.run(dev_api=True))
 
 
+@pytest.mark.parametrize("dev_api", [False, True])
+def test_updio_exact_mode_more_chunks_than_ops(h3c, torch_dev, dev_api):
+    """The one piece pass holds the payloads (items 0..n-1) and the chunks CRC'd from their bytes
+    (items n + c): with 2000 chunks and 300 ops, exact mode CRCs every chunk past the ops' range."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(77 + dev_api)
+    sc = Scenario(h3c, torch, dev, 2000, 8 << 10, rng, stale=0.3)
+    for _ in range(300):
+        c = int(rng.integers(0, 2000))
+        sc.add(orc.UPD_WRITE, c, int(rng.integers(0, 6 << 10)), int(rng.integers(0, 2048)))
+    chunks, res = sc.run(exact=True, dev_api=dev_api)
+    sc.check(chunks, res)
+    assert int(sc.counters.stale_chunks) == sc.stale_chunks
+
+
 def test_updio_hot_region_conflicts(h3c, torch_dev):
     """Many overlapping writes into the first 16 KiB of two chunks: long epoch chains."""
     torch, dev = torch_dev
