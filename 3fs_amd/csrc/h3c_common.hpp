@@ -19,9 +19,6 @@ int device_num_cu(int dev);
 int device_wall_clock_khz(int dev);  // the rate of the device's wall_clock64() counter
 // hipGetDevice + lazy init; returns H3C_OK or an h3c_status.
 int current_device(int *dev);
-// How many threads have called into the engine (through current_device): the UpdateIO graph
-// cache only captures while this is 1.
-int engine_threads();
 void set_error(const char *what, hipError_t e);
 void set_error_text(const char *text);
 // Profiling hooks (h3c_profile_enable): event pair around a launch, per kind.

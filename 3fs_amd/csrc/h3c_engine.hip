@@ -898,13 +898,7 @@ int device_count() {
   return n;
 }
 
-std::atomic<int> g_engine_threads{0};
 int current_device(int *dev) {
-  thread_local bool registered = false;
-  if (!registered) {
-    registered = true;
-    g_engine_threads.fetch_add(1, std::memory_order_relaxed);
-  }
   if (device_count() <= 0) {
     g_last_error = "no HIP device";
     return H3C_ERR_NO_DEVICE;
@@ -914,10 +908,11 @@ int current_device(int *dev) {
 }
 
 // h3c_test_hook state: read from the environment once, settable by tests.
-constexpr int kHooks = 5;
+constexpr int kHooks = 6;
 std::atomic<uint64_t> g_hooks[kHooks];
 const bool g_hooks_init = [] {
-  const char *names[kHooks] = {nullptr, "H3C_SEG_BYTES", "H3C_DEBUG_FLAGS", "H3C_UPD_SCAN", "H3C_UPD_GRAPHS"};
+  const char *names[kHooks] = {nullptr, "H3C_SEG_BYTES", "H3C_DEBUG_FLAGS", "H3C_UPD_SCAN", "H3C_UPD_GRAPHS",
+                                "H3C_UPD_LOOKBACK"};
   for (int k = 1; k < kHooks; ++k) {
     uint64_t v = 0;
     if (const char *e = std::getenv(names[k])) {
@@ -942,7 +937,6 @@ int device_num_cu(int dev) { return (dev >= 0 && dev < kMaxDevices) ? g_dev[dev]
 int device_wall_clock_khz(int dev) { return (dev >= 0 && dev < kMaxDevices) ? g_dev[dev].wall_khz : 0; }
 uint64_t hook(int key) { return (key > 0 && key < kHooks) ? g_hooks[key].load(std::memory_order_relaxed) : 0; }
 int current_device(int *dev) { return ::current_device(dev); }
-int engine_threads() { return g_engine_threads.load(std::memory_order_relaxed); }
 void set_error(const char *what, hipError_t e) { ::set_error(what, e); }
 void set_error_text(const char *text) { g_last_error = text; }
 }  // namespace h3c_rt
@@ -1289,7 +1283,30 @@ void mark_small(GroupLayout &g) {
   }
 }
 
-int layout_groups(const h3c_desc *d, size_t n, uint64_t seg_bytes, GroupLayout &g) {
+// Extent check for device payloads: a descriptor whose bytes start inside a HIP allocation the
+// runtime knows (hipMalloc'd memory, torch's caching-allocator segments) must end inside it, or
+// the kernels would read unmapped memory and fault the device (round 2: a test plan's stride
+// walked 8 MiB past its buffer).  Rejected with kInvalidArg before any launch.  Pointers the
+// runtime cannot place (e.g. device addresses of registered host memory) are not checked.  The
+// last allocation found is cached, so a batch inside one buffer costs one runtime query.
+struct ExtentCheck {
+  uint64_t lo = 1, hi = 0;  // empty
+  bool ok(uint64_t p, uint64_t len) {
+    if (p >= lo && p < hi) return len <= hi - p;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(p)) != hipSuccess || !base || !size) {
+      (void)hipGetLastError();
+      return true;  // unknown to the runtime: cannot check
+    }
+    lo = (uint64_t)(uintptr_t)base;
+    hi = lo + size;
+    return p >= lo && len <= hi - p;
+  }
+};
+
+int layout_groups(const h3c_desc *d, size_t n, uint64_t seg_bytes, GroupLayout &g, bool check_extent = true) {
+  ExtentCheck ext;
   for (size_t i = 0; i < n; ++i) {
     const h3c_desc &x = d[i];
     DevChunk c{};
@@ -1299,6 +1316,11 @@ int layout_groups(const h3c_desc *d, size_t n, uint64_t seg_bytes, GroupLayout &
     const bool none = !(x.type == H3C_TYPE_CRC32C || x.type == H3C_TYPE_CRC32) || (x.ptr == nullptr && x.len > 0);
     if (!none && x.len > 0 && x.mem != H3C_MEM_DEVICE) {
       g_last_error = "descriptors must be device-resident";
+      return H3C_ERR_INVALID_ARG;
+    }
+    if (!none && x.len > 0 && check_extent && !ext.ok((uint64_t)(uintptr_t)x.ptr, x.len)) {
+      g_last_error = "descriptor " + std::to_string(i) + " (" + std::to_string(x.len) +
+                     " bytes) runs past the end of its device allocation";
       return H3C_ERR_INVALID_ARG;
     }
     c.seg_begin = g.segs[k];
@@ -1529,11 +1551,19 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
   const uint64_t off_stage = 0;
   GroupLayout gl;
   {
+    ExtentCheck ext;  // the caller's device payloads only (staged copies are ours)
+    for (size_t i = 0; i < n; ++i)
+      if (d[i].mem == H3C_MEM_DEVICE && d[i].ptr && d[i].len &&
+          (d[i].type == H3C_TYPE_CRC32C || d[i].type == H3C_TYPE_CRC32) &&
+          !ext.ok((uint64_t)(uintptr_t)d[i].ptr, d[i].len)) {
+        g_last_error = "descriptor " + std::to_string(i) + " runs past the end of its device allocation";
+        return H3C_ERR_INVALID_ARG;
+      }
     // layout with placeholder pointers for staged payloads (device-ness is all that matters)
     std::vector<h3c_desc> probe(dd);
     for (auto &x : probe)
       if (x.mem != H3C_MEM_DEVICE) x.mem = H3C_MEM_DEVICE;
-    rc = layout_groups(probe.data(), n, seg_bytes, gl);
+    rc = layout_groups(probe.data(), n, seg_bytes, gl, /*check_extent=*/false);
     if (rc) return rc;
   }
   // one layout for the device arena and the pinned staging buffer, so that everything going

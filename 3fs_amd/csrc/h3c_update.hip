@@ -397,9 +397,12 @@ __device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
 }
 
 // Wave w of workgroup L takes writes [lo, hi) of (16 L + w); workgroup L's look-back waits only
-// on workgroups below it.  The grid is at most one workgroup per CU (the tables fill LDS), so all
-// are resident together unless other work holds CUs -- then a waiter only waits longer -- and
-// every spin is bounded.
+// on workgroups below it.  L is a ticket taken when the workgroup starts (not blockIdx.x), so a
+// workgroup only ever waits on workgroups that are already running, whatever order the hardware
+// dispatches them in or however many CUs other work holds.  Every spin is still bounded: a
+// workgroup that gives up publishes what it has and flags the batch, and the last workgroup
+// reports the flag as *n_invalid = counters.invalid = all ones (the chunk bytes are right; the
+// checksums of that call are void -- a create pass over the chunks recovers them).
 // Per group of 64 writes lane k loads write k's metadata -- resolving its previous writer
 // from the tile link or the hash of per-tile last writers -- then the wave walks the group as
 // upd_delta_kernel does.  Afterwards each write's v = delta * sh[b] is folded into the running
@@ -412,10 +415,13 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
     const uint32_t *__restrict__ raw_base, const uint32_t *__restrict__ raw_in, uint32_t exact, uint32_t reuse_case,
     const uint32_t *__restrict__ touched, uint32_t *ctl, uint64_t *gran, uint32_t *__restrict__ inpre,
     uint32_t *__restrict__ out_raw, uint32_t *__restrict__ raw_out, uint32_t *__restrict__ n_invalid,
-    unsigned long long *__restrict__ counters) {
+    unsigned long long *__restrict__ counters, uint32_t force_timeout) {
   constexpr uint32_t G4 = 4096;
   __shared__ uint32_t lds[kLdsWords + kRedWords];
-  const uint32_t L = blockIdx.x, nwg = gridDim.x;
+  __shared__ uint32_t s_ticket;
+  if (threadIdx.x == 0) s_ticket = atomicAdd(&ctl[kCtlTicket], 1u);
+  __syncthreads();
+  const uint32_t L = s_ticket, nwg = gridDim.x;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)L * kWavesPerBlock + wave;
@@ -580,6 +586,8 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
       if (lane < nchunks) gran_store(row + lane, kGranAgg, a0);
       if (two && lane + 64 < nchunks) gran_store(row + 64 + lane, kGranAgg, a1);
       int j0 = lane < nchunks ? (int)L - 1 : -1, j1 = two && lane + 64 < nchunks ? (int)L - 1 : -1;
+      // test hook (H3C_HOOK_UPD_LOOKBACK): ticket 1 gives up at once, as a starved wait would
+      const uint32_t limit = force_timeout && L == 1 ? 0u : kSpinLimit;
       for (uint32_t spins = 0; __builtin_amdgcn_ballot_w64(j0 >= 0 || j1 >= 0) != 0;) {
         bool moved = false;
         if (j0 >= 0) {
@@ -600,10 +608,11 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
             moved = true;
           }
         }
-        if (__builtin_amdgcn_ballot_w64(moved) == 0) {
+        if (__builtin_amdgcn_ballot_w64(moved) == 0 || limit == 0) {
           __builtin_amdgcn_s_sleep(2);
-          if (++spins > kSpinLimit) {  // a predecessor never published: give up, flag it
+          if (++spins > limit) {  // a predecessor never published: give up, flag the batch
             if (lane == 0) atomicExch(&ctl[kCtlTimeout], 1u);
+            __threadfence();  // the flag before this workgroup's inclusive granules
             break;
           }
         }
@@ -626,8 +635,12 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
       }
       for (int o = 32; o >= 1; o >>= 1) stale += __shfl_xor(stale, o, 64);
       if (lane == 0) {
+        __threadfence();
         const uint32_t inv = __hip_atomic_load(&ctl[kCtlErr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (n_invalid) *n_invalid = inv;
+        // every workgroup's inclusive granule was read (directly or through a later one's) before
+        // this: a workgroup that gave up had raised the flag first
+        const bool void_batch = __hip_atomic_load(&ctl[kCtlTimeout], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n_invalid) *n_invalid = void_batch ? 0xFFFFFFFFu : inv;
         if (counters) {  // h3c_update_counters: none, reuse, combine, read_chunk, recalculate, mismatch, invalid, stale
           const unsigned long long ok = n - inv;
           counters[0] = 0;
@@ -636,7 +649,7 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
           counters[3] = reuse_case ? 0 : ok;
           counters[4] = 0;
           counters[5] = 0;
-          counters[6] = inv;
+          counters[6] = void_batch ? ~0ull : inv;
           counters[7] = stale;
         }
       }
@@ -1052,7 +1065,7 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
                        blk_chunk_dev, blk_index_dev, static_cast<const uint8_t *>(payload_dev), n_blocks, w.prev,
                        w.hhead, w.hcap - 1, w.nkey, w.next, sh, pc, raw_base, chunk_raw_in_dev, exact ? 1u : 0u,
                        reuse_case, w.touched, w.ctl, w.gran, w.scan, out_raw_dev, chunk_raw_out_dev, n_invalid_dev,
-                       counters_dev);
+                       counters_dev, (uint32_t)(h3c_rt::hook(H3C_HOOK_UPD_LOOKBACK) == 1));
     HIP_TRY(hipGetLastError());
     // algorithmic bytes: read new + read old + write back, per block write
     HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDATE, 3ull * block_bytes * n_blocks));

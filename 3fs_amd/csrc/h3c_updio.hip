@@ -228,9 +228,13 @@ __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t 
     if (io.kind == H3C_UPD_REMOVE) {  // doRemove's form (StorageOperator.cc:808-815); no range check (:141)
       if (io.offset || io.length || io.checksum_type != H3C_TYPE_NONE || syncing) st = H3C_ERR_INVALID_ARG;
     } else {
-      if (io.offset >= cs.chunk_size || (uint64_t)io.offset + io.length > cs.chunk_size) st = H3C_ERR_INVALID_ARG;
+      // :141-145 against writeIO.chunkSize (H3C_IO_CHUNK_SIZE; else the chunk's own), then :171-180
+      const bool own = !std_domain && (io.flags & H3C_IO_CHUNK_SIZE);
+      const uint32_t wcs = own ? io.chunk_size : cs.chunk_size;
+      if (io.offset >= wcs || (uint64_t)io.offset + io.length > wcs) st = H3C_ERR_INVALID_ARG;
       if (io.kind == H3C_UPD_WRITE && io.length && !io.payload) st = H3C_ERR_INVALID_ARG;
       if (syncing && (io.kind != H3C_UPD_WRITE || io.offset)) st = H3C_ERR_INVALID_ARG;
+      if (st == H3C_OK && wcs != cs.chunk_size) st = H3C_ERR_CHUNK_SIZE_MISMATCH;
       // A6 on a TRUNCATE / EXTEND: create(type, <no data>, length) is {NONE, 0} (:193-207);
       // the Rust engine verifies only data (engine.rs:297)
       if (st == H3C_OK && !std_domain && io.kind != H3C_UPD_WRITE && io.checksum_type != H3C_TYPE_NONE && io.length)
@@ -933,7 +937,8 @@ __global__ void uio_result_kernel(const OpPos *__restrict__ pos, const uint32_t 
       const Aff x = sscan[p];
       const uint32_t s = hd_gf_mul(s0, x.m, poly) ^ x.e;
       o.size = applied ? r.na : r.nb;
-      if (r.status == H3C_ERR_CHECKSUM_MISMATCH) {
+      if (r.status == H3C_ERR_CHECKSUM_MISMATCH || r.status == H3C_ERR_CHUNK_SIZE_MISMATCH) {
+        // both fail after :174 set result.checksum = meta.checksum()
         o.type = std_domain ? poly_type : r.tb;
         o.value = std_domain ? 0u : s;  // engine.rs:303 returns before out_checksum is set
       } else if (applied) {
@@ -1218,19 +1223,20 @@ struct UpdGraphs {
 // shape seen among the last four plain calls returns an empty entry to capture into; later
 // sights replay.  Graphs are not
 // used while `st` itself is being captured, or with h3c_test_hook(H3C_HOOK_UPD_GRAPHS, 1).
-UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st) {
+UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st, bool asked) {
   thread_local UpdGraphs cache[4];
   thread_local UpdGraphKey recent[4] = {};  // keys of the last plain calls (lease pools may alternate buffers)
   thread_local uint32_t recent_next = 0;
   thread_local uint64_t tick = 0;
-  if (h3c_rt::hook(H3C_HOOK_UPD_GRAPHS) == 1) return nullptr;
-  // Only while one thread uses the engine: a launch into the legacy default stream while any
-  // stream of the process is capturing fails in HIP ("operation not permitted when stream is
-  // capturing") and invalidates the capture, whatever the capture mode or the capture
-  // stream's flags -- a 16-thread stress with captures in flight saw hundreds of such failures
-  // (profiles/r02b_tsan.txt).  Replays (no capture) stay safe; a multi-threaded caller simply
-  // runs the plain launches.
-  if (h3c_rt::engine_threads() > 1 && h3c_rt::hook(H3C_HOOK_UPD_GRAPHS) != 2) return nullptr;
+  // Only when the caller asks (H3C_UPD_GRAPHS): a launch into the legacy default stream made by
+  // ANY thread of the process while a stream is capturing fails in HIP ("operation not permitted
+  // when stream is capturing") and invalidates the capture, whatever the capture mode or the
+  // capture stream's flags -- a 16-thread stress with captures in flight saw hundreds of such
+  // failures (profiles/r02b_tsan.txt).  The engine cannot see other users of the GPU (PyTorch,
+  // the caller's own threads), so only the caller can promise that none launches meanwhile.
+  // Test hook: 1 never captures, 2 captures without the flag.
+  const uint64_t hk = h3c_rt::hook(H3C_HOOK_UPD_GRAPHS);
+  if (hk == 1 || (!asked && hk != 2)) return nullptr;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
     (void)hipGetLastError();
@@ -1339,6 +1345,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                 unsigned long long *d_ctr, hipStream_t st, int dev, Epilogue epilogue) {
   const bool std_domain = (flags & H3C_UPD_STD_DOMAIN) != 0;
   const bool exact = (flags & H3C_UPD_EXACT) != 0;
+  flags &= H3C_UPD_STD_DOMAIN | H3C_UPD_EXACT | H3C_UPD_GRAPHS;
   const PolyConsts *pc = static_cast<const PolyConsts *>(h3c_rt::device_consts(dev, poly_type));
   const uint32_t poly = poly_type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
   const uint32_t stdf = std_domain ? 1u : 0u, exactf = exact ? 1u : 0u;
@@ -1551,7 +1558,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     if (attempt == 0) {
       const UpdGraphKey key{dev, poly_type, flags, n, nchunks, cap, hcap, d_chunks, d_chunks_out, d_ios, d_res,
                             d_ctr, lease1.data(), lease2.data(), aux->st};
-      gr = upd_graphs(key, st);
+      gr = upd_graphs(key, st, (flags & H3C_UPD_GRAPHS) != 0);
     }
     if (gr && !gr->g && !gr->failed) {  // capture the attempt once, on a capture stream of this thread
       hipStream_t cst = capture_stream(dev);

@@ -127,6 +127,7 @@ class StatusCode(enum.IntEnum):
     OK = 0
     kInvalidArg = 3
     kChunkReadFailed = 4010  # StatusCodeDetails.h:160
+    kChunkSizeMismatch = 4015  # StatusCodeDetails.h:165
     kChecksumMismatch = 4080  # StatusCodeDetails.h:186
     kHipError = 9001
     kNoDevice = 9002
@@ -350,7 +351,7 @@ def sync_bench(threads: int, nbytes: int, calls: int, api: str = "verify"):
     return lat, wall.value
 
 
-HOOK_SEG_BYTES, HOOK_DEBUG_FLAGS, HOOK_UPD_SCAN, HOOK_UPD_GRAPHS = 1, 2, 3, 4  # h3c_test_hook keys
+HOOK_SEG_BYTES, HOOK_DEBUG_FLAGS, HOOK_UPD_SCAN, HOOK_UPD_GRAPHS, HOOK_UPD_LOOKBACK = 1, 2, 3, 4, 5  # h3c_test_hook keys
 UPD_SCAN_PATHS = {"default": 0, "fused": 1, "tiles": 2, "sort": 3}
 
 
@@ -369,13 +370,16 @@ def set_test_hook(key: int, value: int) -> None:
 UPD_WRITE, UPD_REMOVE, UPD_TRUNCATE, UPD_EXTEND, UPD_COMMIT = 1, 2, 4, 8, 16  # UpdateType (Common.h:51-58)
 UPD_STD_DOMAIN = 1  # flag: Rust chunk engine semantics (std-domain values)
 UPD_EXACT = 2  # flag: stored checksums are not trusted (each chunk CRC'd once first)
+UPD_GRAPHS = 4  # flag: a repeated batch shape may run as one captured HIP graph (caller: no concurrent
+#                 legacy-default-stream launches in the process during the call)
 IO_SYNCING = 1  # per-op flag: UpdateOptions.isSyncing full-chunk replace
+IO_CHUNK_SIZE = 2  # per-op flag: `chunk_size` carries UpdateIO.chunkSize (range check, kChunkSizeMismatch)
 
 CHUNK_STATE_DTYPE = np.dtype([("base", "<u8"), ("chunk_size", "<u4"), ("size", "<u4"), ("value", "<u4"),
                               ("type", "u1"), ("reserved", "u1", 3)])
 UPDATE_IO_DTYPE = np.dtype([("payload", "<u8"), ("chunk", "<u4"), ("offset", "<u4"), ("length", "<u4"),
                             ("checksum_value", "<u4"), ("checksum_type", "u1"), ("kind", "u1"), ("flags", "u1"),
-                            ("reserved", "u1", 5)])
+                            ("reserved", "u1"), ("chunk_size", "<u4")])
 UPDATE_RESULT_DTYPE = np.dtype([("status", "<u4"), ("size", "<u4"), ("value", "<u4"), ("type", "u1"),
                                 ("reserved", "u1", 3)])
 assert CHUNK_STATE_DTYPE.itemsize == 24 and UPDATE_IO_DTYPE.itemsize == 32 and UPDATE_RESULT_DTYPE.itemsize == 16
@@ -394,7 +398,7 @@ class UpdateCounters(ctypes.Structure):
 
 def update_ios(chunks: np.ndarray, ios: np.ndarray, type_: int = ChecksumType.CRC32C, std_domain: bool = False,
                exact: bool = False, counters: Optional[UpdateCounters] = None, stream=None,
-               out: Optional[np.ndarray] = None) -> np.ndarray:
+               out: Optional[np.ndarray] = None, graphs: bool = False) -> np.ndarray:
     """Batched ChunkReplica::update + updateChecksum for any mix of WRITE / REMOVE / TRUNCATE /
     EXTEND / COMMIT (h3c_update_ios_ex).  `chunks` (CHUNK_STATE_DTYPE, updated in place: size /
     type / value) and `ios` (UPDATE_IO_DTYPE) are host arrays whose `base` / `payload` fields are
@@ -402,7 +406,9 @@ def update_ios(chunks: np.ndarray, ios: np.ndarray, type_: int = ChecksumType.CR
     4080 kChecksumMismatch, chunk size after, and result.checksum (type, value).  `exact` does not
     trust stored checksums (H3C_UPD_EXACT); `counters` receives the batch's case counts; `out`
     (UPDATE_RESULT_DTYPE, len(ios)) receives the results instead of a new array (pass a pinned
-    one to skip the runtime's staging copy)."""
+    one to skip the runtime's staging copy).  `graphs` (H3C_UPD_GRAPHS): a repeated batch shape
+    may replay as one HIP graph -- only when no other thread launches on the legacy default
+    stream meanwhile."""
     if chunks.dtype != CHUNK_STATE_DTYPE or ios.dtype != UPDATE_IO_DTYPE:
         raise TypeError("chunks / ios must use CHUNK_STATE_DTYPE / UPDATE_IO_DTYPE")
     if not (chunks.flags.c_contiguous and ios.flags.c_contiguous):
@@ -413,7 +419,7 @@ def update_ios(chunks: np.ndarray, ios: np.ndarray, type_: int = ChecksumType.CR
         res = out
     else:
         res = np.zeros(len(ios), dtype=UPDATE_RESULT_DTYPE)
-    flags = (UPD_STD_DOMAIN if std_domain else 0) | (UPD_EXACT if exact else 0)
+    flags = (UPD_STD_DOMAIN if std_domain else 0) | (UPD_EXACT if exact else 0) | (UPD_GRAPHS if graphs else 0)
     _check(lib.h3c_update_ios_ex(int(type_), chunks.ctypes.data, len(chunks), ios.ctypes.data, len(ios),
                                  res.ctypes.data, flags, ctypes.byref(counters) if counters is not None else None,
                                  _stream_handle(stream)))
@@ -421,7 +427,7 @@ def update_ios(chunks: np.ndarray, ios: np.ndarray, type_: int = ChecksumType.CR
 
 
 def update_ios_dev(chunks, ios, results, type_: int = ChecksumType.CRC32C, std_domain: bool = False,
-                   exact: bool = False, counters=None, stream=None) -> None:
+                   exact: bool = False, counters=None, stream=None, graphs: bool = False) -> None:
     """update_ios with every table on the GPU (h3c_update_ios_dev): `chunks` uint8 tensor of
     nchunks x 24 bytes (CHUNK_STATE_DTYPE records, updated in place), `ios` uint8 tensor of
     n x 32 bytes (UPDATE_IO_DTYPE), `results` uint8 tensor of n x 16 bytes (UPDATE_RESULT_DTYPE),
@@ -436,7 +442,7 @@ def update_ios_dev(chunks, ios, results, type_: int = ChecksumType.CRC32C, std_d
         raise ValueError("results must hold one record per op")
     if counters is not None and (not counters.is_cuda or counters.numel() * counters.element_size() != 64):
         raise ValueError("counters must be a GPU tensor of 8 x 64-bit")
-    flags = (UPD_STD_DOMAIN if std_domain else 0) | (UPD_EXACT if exact else 0)
+    flags = (UPD_STD_DOMAIN if std_domain else 0) | (UPD_EXACT if exact else 0) | (UPD_GRAPHS if graphs else 0)
     _check(lib.h3c_update_ios_dev(int(type_), chunks.data_ptr(), nchunks, ios.data_ptr(), n, results.data_ptr(),
                                   flags, counters.data_ptr() if counters is not None else None,
                                   _stream_handle(stream)))
@@ -500,9 +506,26 @@ class Plan:
         self.bytes = int(lib.h3c_plan_bytes(self._h))
 
     @classmethod
-    def uniform(cls, base_ptr: int, chunk_len: int, nchunks: int, stride: Optional[int] = None,
-                start: int = 0xFFFFFFFF, type_: int = ChecksumType.CRC32C, device: int = 0) -> "Plan":
+    def uniform(cls, base_ptr, chunk_len: int, nchunks: int, stride: Optional[int] = None,
+                start: int = 0xFFFFFFFF, type_: int = ChecksumType.CRC32C, device: int = 0,
+                extent: Optional[int] = None) -> "Plan":
+        """Chunk i = [base + i*stride, + chunk_len).  `base_ptr` is a device address or a GPU
+        tensor; the bytes the plan may read end at base + `extent` (default: the tensor's size
+        when a tensor is given).  A layout that runs past it, stride*(n-1) + chunk_len > extent,
+        is rejected with kInvalidArg before anything is uploaded or launched; the library also
+        rejects descriptors that run past their HIP allocation (h3c_plan_create)."""
+        if not isinstance(base_ptr, int):  # a tensor: its own extent bounds the plan
+            if extent is None:
+                extent = base_ptr.numel() * base_ptr.element_size()
+            base_ptr = base_ptr.data_ptr()
         stride = chunk_len if stride is None else stride
+        if chunk_len < 0 or stride < 0 or nchunks < 0:
+            raise EngineError(StatusCode.kInvalidArg, "negative plan geometry")
+        need = stride * (nchunks - 1) + chunk_len if nchunks else 0
+        if extent is not None and need > extent:
+            raise EngineError(StatusCode.kInvalidArg,
+                              f"uniform plan reads {need} bytes (stride {stride} x {nchunks - 1} + {chunk_len}) "
+                              f"past an extent of {extent}")
         d = np.zeros(nchunks, dtype=DESC_DTYPE)
         d["ptr"] = base_ptr + np.arange(nchunks, dtype=np.uint64) * np.uint64(stride)
         d["len"] = chunk_len

@@ -158,7 +158,8 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         # one process per GPU; modulo only matters for single-GPU rehearsals of N>1
-        self.local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+        self.ndev = torch.cuda.device_count()
+        self.local = int(os.environ.get("LOCAL_RANK", "0")) % max(self.ndev, 1)
         if self.world > 1:
             # Control plane only (barrier, max-over-ranks time, verified flag): no data
             # path collective exists, so gloo on CPU tensors is enough; set
@@ -445,7 +446,7 @@ def run_updio(args, cx: Ctx) -> dict:
     d_ctr = torch.zeros(8, dtype=torch.int64, device=cx.dev)
 
     def step():
-        h3c.update_ios_dev(d_state, d_ios, d_res, stream=cx.stream, exact=exact, counters=d_ctr)
+        h3c.update_ios_dev(d_state, d_ios, d_res, stream=cx.stream, exact=exact, counters=d_ctr, graphs=True)
 
     g0 = [h3c.diag_counter(k) for k in range(3)]
     elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDIO)
@@ -468,7 +469,7 @@ def run_updio(args, cx: Ctx) -> dict:
     hsteps = max(1, min(args.steps, 20))
 
     def hstep():
-        h3c.update_ios(state, ios, stream=cx.stream, out=hres, exact=exact, counters=hctr)
+        h3c.update_ios(state, ios, stream=cx.stream, out=hres, exact=exact, counters=hctr, graphs=True)
 
     helapsed, _ = cx.timed(hstep, hsteps, min(args.warmup, 2), h3c.engine.PROF_UPDIO)
     plan.run(fresh, stream=cx.stream)
@@ -552,16 +553,25 @@ def run_sync(args, cx: Ctx) -> dict:
     }
 
 
-def pcie_h2d_peak(torch, dev, nbytes: int = 1 << 30) -> float:
-    src = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
-    dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+def pcie_h2d_peak(cx: "Ctx", nbytes: int = 1 << 30, hb=None) -> float:
+    """Pinned H2D GB/s per rank with EVERY rank copying at once (the ranks of one node share
+    host DRAM and PCIe switches, so a rank measured alone would overstate its share): barrier,
+    5 copies of `nbytes` per rank, barrier; per-rank rate = 5 * nbytes / the slowest rank's
+    time.  The source is the rank's NUMA-local HostBuffer when given (the memory the host-fed
+    pass read), else torch pinned memory."""
+    torch = cx.torch
+    src = torch.from_numpy(hb.array[:nbytes]) if hb is not None and hb.nbytes >= nbytes \
+        else torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(nbytes, dtype=torch.uint8, device=cx.dev)
     dst.copy_(src, non_blocking=True)
-    torch.cuda.synchronize()
+    cx.barrier()
     t0 = time.perf_counter()
     for _ in range(5):
         dst.copy_(src, non_blocking=True)
     torch.cuda.synchronize()
-    return 5 * nbytes / (time.perf_counter() - t0) / 1e9
+    el = time.perf_counter() - t0
+    cx.barrier()
+    return 5 * nbytes / cx.max_over_ranks(el) / 1e9
 
 
 def run_hostfed(args, cx: Ctx) -> dict:
@@ -602,9 +612,9 @@ def run_hostfed(args, cx: Ctx) -> dict:
     hf.close()
     items = host = None
     node = hb.node if hb is not None else -1
+    peak = pcie_h2d_peak(cx, hb=hb)
     if hb is not None:
         hb.close()
-    peak = pcie_h2d_peak(torch, cx.dev)
     value = total * args.steps * cx.world / elapsed / 2**30
     rl = roofline(prof, round(peak, 1), bound="pcie", kernel="hostfed pipeline (H2D + CRC)")
     rl["pcie_spec_gbps"] = PCIE_SPEC_GBPS
@@ -619,6 +629,7 @@ def run_hostfed(args, cx: Ctx) -> dict:
                    "host_numa_node": node},
         "verified": verified,
         "measured_h2d_gbps": round(peak, 1),
+        "measured_h2d_note": f"per rank, all {cx.world} rank(s) copying pinned -> HBM at once",
         "roofline": rl,
     }
 
@@ -731,8 +742,110 @@ def run_shard4m(args, cx: Ctx) -> dict:
     }
 
 
+def _set_pdeathsig() -> None:  # pragma: no cover - runs in the child between fork and exec
+    """Children die with the launcher (a driver timeout that kills it must not leave ranks on
+    the GPU): prctl(PR_SET_PDEATHSIG, SIGTERM)."""
+    import signal
+
+    try:
+        ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGTERM), 0, 0, 0)
+    except (OSError, AttributeError):
+        pass
+
+
+def rank_env(rank: int, world: int, port: int, base: dict | None = None) -> dict:
+    """The environment torch.distributed.run gives rank `rank` of a one-node job."""
+    env = dict(os.environ if base is None else base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), H3C_BENCH_LAUNCHED="1")
+    return env
+
+
+def check_world(gpus: int, env=os.environ) -> str | None:
+    """The --gpus / WORLD_SIZE contract: under a launcher (WORLD_SIZE set) the two must agree.
+    Returns an error message, or None."""
+    if gpus < 1:
+        return f"--gpus must be >= 1 (got {gpus})"
+    ws = env.get("WORLD_SIZE")
+    if ws is not None and int(ws) != gpus:
+        return f"WORLD_SIZE={ws} from the launcher disagrees with --gpus {gpus}"
+    return None
+
+
+def spawn_ranks(gpus: int, argv: list, grace_s: float = 60.0) -> int:
+    """`bench.py --gpus N` run without a launcher (WORLD_SIZE unset): start N child processes of
+    this script, one per GPU, with the env torchrun would give them (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free MASTER_PORT).  The parent never imports torch
+    or touches HIP -- it only waits.  Rank 0 prints the JSON line on the inherited stdout.
+    Returns 0 only when every rank exits 0, else the exit code of the first rank to fail; then the
+    others get `grace_s` to finish before they are terminated (they would otherwise wait in a
+    barrier for gloo's 30-minute timeout)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=rank_env(r, gpus, port),
+                              preexec_fn=_set_pdeathsig) for r in range(gpus)]
+    first_fail, cause = None, 0
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs):
+            break
+        if first_fail is None and any(rc not in (None, 0) for rc in rcs):
+            first_fail = time.monotonic()
+            cause = next(rc for rc in rcs if rc not in (None, 0))
+        if first_fail is not None and time.monotonic() - first_fail > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        time.sleep(0.2)
+    rcs = [p.returncode for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        print(f"bench.py: rank exit codes {rcs}", file=sys.stderr, flush=True)
+        # the first rank to fail is the cause (ranks terminated after the grace period are not);
+        # a signal death (-N) becomes 128 + N, as a shell reports it
+        rc = cause if first_fail is not None else bad[0]
+        return 128 - rc if rc < 0 else rc
+    return 0
+
+
+def dry_run_launch(args) -> int:
+    """CPU-only rehearsal of the launch contract (tests/test_bench_contract.py): every rank joins
+    a gloo group from the env it was given and rank 0 prints the ranks it saw; rank
+    `--dry-run-launch K` (K >= 0) exits 3 before joining, to exercise failure propagation."""
+    world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+    if args.dry_run_launch == rank:
+        return 3
+    seen = [rank]
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+        t = torch.zeros(world, dtype=torch.int64)
+        t[rank] = int(os.environ["LOCAL_RANK"]) + 1
+        dist.all_reduce(t)
+        seen = [int(v) - 1 for v in t.tolist()]
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "local_ranks": seen,
+                          "launched": bool(os.environ.get("H3C_BENCH_LAUNCHED"))}), flush=True)
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
+    ap.add_argument("--dry-run-launch", type=int, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
@@ -755,6 +868,14 @@ def main() -> int:
     ap.add_argument("--sync-threads", type=int, default=32)
     ap.add_argument("--sync-kib", default="4,128,1024", help="sync: buffer sizes (KiB), comma-separated")
     args = ap.parse_args()
+    err = check_world(args.gpus)
+    if err:
+        print(f"bench.py: {err}", file=sys.stderr, flush=True)
+        return 2
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus, sys.argv[1:], float(os.environ.get("H3C_BENCH_GRACE_S", "60")))
+    if args.dry_run_launch is not None:
+        return dry_run_launch(args)
     cx = Ctx()
     fn = {"verify": run_verify, "update": run_update, "updio": run_updio, "hostfed": run_hostfed,
           "shard4m": run_shard4m, "mixed": run_mixed, "sync": run_sync}[args.workload]
@@ -774,6 +895,10 @@ def main() -> int:
             "host_numa_node_rank0": hf["config"]["host_numa_node"], "verified": hf["verified"],
             "note": "PCIe-inclusive (payloads in NUMA-local pinned host memory); not the headline value",
         }
+    # N ranks on fewer devices is a rehearsal (ranks share a GPU); the line says so
+    res.setdefault("config", {})["devices_visible"] = cx.ndev
+    res["config"]["launcher"] = "bench.py --gpus (spawned ranks)" if os.environ.get("H3C_BENCH_LAUNCHED") \
+        else ("torchrun" if cx.world > 1 else "single process")
     if cx.rank == 0:
         print(json.dumps(res), flush=True)
     if cx.world > 1:

@@ -45,6 +45,7 @@ enum h3c_status {
   H3C_OK = 0,
   H3C_ERR_INVALID_ARG = 3,            /* StatusCode::kInvalidArg */
   H3C_ERR_CHUNK_READ_FAILED = 4010,   /* StorageCode::kChunkReadFailed, StatusCodeDetails.h:160 */
+  H3C_ERR_CHUNK_SIZE_MISMATCH = 4015, /* StorageCode::kChunkSizeMismatch, StatusCodeDetails.h:165 */
   H3C_ERR_CHECKSUM_MISMATCH = 4080,   /* StorageCode::kChecksumMismatch, StatusCodeDetails.h:186 */
   H3C_ERR_HIP = 9001,                 /* HIP runtime failure (h3c_last_error() has text) */
   H3C_ERR_NO_DEVICE = 9002
@@ -147,7 +148,11 @@ int h3c_batch_combine(uint8_t type, const uint32_t *c1_dev, const uint32_t *c2_d
  * out_raw 0, and are counted in *n_invalid_dev (optional).  Chunks no write reaches keep
  * chunk_raw_in.  The chunk bytes are updated in place.  All arrays are device memory;
  * nothing is synchronised.  The stored checksums are trusted; h3c_update_blocks_ex
- * (below) has the exact mode and the case counters. */
+ * (below) has the exact mode and the case counters.
+ * *n_invalid_dev == UINT32_MAX (counters.invalid == UINT64_MAX) reports a void batch: the
+ * one-launch path chains its workgroups' per-chunk sums, and a workgroup that waited past its
+ * bound (> 0.25 s, i.e. starved of its CU by other work) gave up.  The chunk bytes are right;
+ * out_raw / chunk_raw_out of that call are not -- recompute them (h3c_plan_run over the chunks). */
 size_t h3c_update_workspace_bytes(uint32_t n_blocks, uint32_t nchunks, uint64_t chunk_len, uint32_t block_bytes);
 int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nchunks, uint64_t chunk_len,
                       uint32_t block_bytes, const uint32_t *chunk_raw_in_dev, const uint32_t *blk_chunk_dev,
@@ -186,6 +191,13 @@ typedef struct h3c_chunk_state {
                              (ChunkReplica.cc:211-215, 289; chunk.rs:112, 166-170): WRITE at
                              offset 0 only (ReliableForwarding.cc:203-207), else kInvalidArg */
 
+#define H3C_IO_CHUNK_SIZE 2u /* `chunk_size` carries UpdateIO.chunkSize (raw domain): the range check uses it
+                                (ChunkReplica.cc:141-145, kInvalidArg) and a value other than the chunk's
+                                innerFileId.chunkSize (the table's chunk_size) fails the op with
+                                H3C_ERR_CHUNK_SIZE_MISMATCH (:171-180).  Without the flag the table's
+                                chunk_size stands in for it.  The Rust engine path (H3C_UPD_STD_DOMAIN) has
+                                no such check (ChunkEngine.cc:32-52) and ignores it. */
+
 /* UpdateIO fields on the path (Common.h:326-345). */
 typedef struct h3c_update_io {
   uint64_t payload;        /* device address of `length` bytes (WRITE) */
@@ -196,11 +208,13 @@ typedef struct h3c_update_io {
   uint8_t checksum_type;
   uint8_t kind;            /* h3c_update_kind */
   uint8_t flags;           /* H3C_IO_* */
-  uint8_t reserved[5];
+  uint8_t reserved;
+  uint32_t chunk_size;     /* UpdateIO.chunkSize, read with H3C_IO_CHUNK_SIZE */
 } h3c_update_io;
 
 typedef struct h3c_update_result {
-  uint32_t status; /* H3C_OK, H3C_ERR_INVALID_ARG (range, :140-145), H3C_ERR_CHECKSUM_MISMATCH (:193-207) */
+  uint32_t status; /* H3C_OK, H3C_ERR_INVALID_ARG (range, :140-145), H3C_ERR_CHUNK_SIZE_MISMATCH (:176-180),
+                      H3C_ERR_CHECKSUM_MISMATCH (:193-207) */
   uint32_t size;   /* meta.size after the op */
   uint32_t value;  /* result.checksum after the op (meta.checksum(), ChunkReplica.cc:311; std domain:
                       the engine's out_checksum, 0 after a checksum mismatch, engine.rs:303,324) */
@@ -231,6 +245,11 @@ typedef struct h3c_update_counters {
                                  std-domain crc32c, Engine::update_chunk / copy_on_write / safe_write */
 #define H3C_UPD_EXACT 2u      /* do not trust stored checksums: every chunk in the table with bytes is
                                  CRC'd once before the batch (see below) */
+#define H3C_UPD_GRAPHS 4u     /* h3c_update_ios*: a batch shape this thread repeats on the same buffers
+                                 runs its ~30-launch pipeline as one captured HIP graph.  The caller
+                                 promises that no thread of the process launches onto the legacy
+                                 default stream while the call runs (HIP fails such launches during
+                                 a capture and voids the capture).  Off: plain launches. */
 
 /* Apply `n` UpdateIOs in sequence order to device-resident chunks, replacing
  * ChunkReplica::update's per-op payload verify (ChunkReplica.cc:193-207), zero fill,
@@ -401,10 +420,11 @@ enum h3c_hook {
   H3C_HOOK_SEG_BYTES = 1,   /* segment size of the create / verify kernels (multiple of 1 KiB) */
   H3C_HOOK_DEBUG_FLAGS = 2, /* bit0: no pipelined row loop; bit1: no small-chunk kernel; bit2: no uniform kernel */
   H3C_HOOK_UPD_SCAN = 3,    /* h3c_update_blocks: 1 fused, 2 dense tiles, 3 sort + scan_by_key */
-  H3C_HOOK_UPD_GRAPHS = 4   /* h3c_update_ios: 1 never replays its pipeline as HIP graphs; 2 captures
-                               them even after several threads have called the engine (by default
-                               only a single-threaded caller does: HIP fails legacy-stream launches
-                               made while any stream captures) */
+  H3C_HOOK_UPD_GRAPHS = 4,  /* h3c_update_ios: 1 never replays its pipeline as HIP graphs, even with
+                               H3C_UPD_GRAPHS; 2 captures them without the flag */
+  H3C_HOOK_UPD_LOOKBACK = 5 /* h3c_update_blocks fused path: 1 makes the workgroup with ticket 1 give up
+                               its look-back at once, as a starved wait would (the void-batch report:
+                               *n_invalid = UINT32_MAX, counters.invalid = UINT64_MAX) */
 };
 int h3c_test_hook(int key, uint64_t value);
 /* Engine-internal counters for tests: 0 = h3c_update_ios pipeline graph replays, 1 = graph

@@ -26,6 +26,7 @@ enum StatusCode : uint32_t {
   kOK = 0,
   kInvalidArg = 3,
   kChunkReadFailed = 4010,
+  kChunkSizeMismatch = 4015,
   kChecksumMismatch = 4080,
 };
 
@@ -42,6 +43,7 @@ struct UpdateIO {
   ChecksumInfo checksum;
   const uint8_t *data = nullptr;
   bool isSyncing = false;  // UpdateOptions.isSyncing (ChunkReplica.cc:211-215, 289): WRITE at offset 0
+  uint32_t chunkSize = 0;  // UpdateIO.chunkSize; 0: not carried (the chunk's own innerFileId.chunkSize is used)
 
   bool isWrite() const { return updateType == UpdateType::WRITE; }
   bool isRemove() const { return updateType == UpdateType::REMOVE; }
@@ -87,7 +89,9 @@ struct ChunkReplicaBatch {
     for (size_t i = 0; i < ios.size(); ++i)
       io[i] = h3c_update_io{(uint64_t)(uintptr_t)ios[i].data, ios[i].chunk, ios[i].offset, ios[i].length,
                             ios[i].checksum.value, (uint8_t)ios[i].checksum.type, (uint8_t)ios[i].updateType,
-                            (uint8_t)(ios[i].isSyncing ? H3C_IO_SYNCING : 0u), {0, 0, 0, 0, 0}};
+                            (uint8_t)((ios[i].isSyncing ? H3C_IO_SYNCING : 0u) |
+                                      (ios[i].chunkSize ? H3C_IO_CHUNK_SIZE : 0u)),
+                            0, ios[i].chunkSize};
     std::vector<h3c_update_result> res(ios.size());
     const int rc = h3c_update_ios_ex((uint8_t)checksumType, cs.data(), (uint32_t)cs.size(), io.data(),
                                      (uint32_t)io.size(), res.data(), flags, counters, stream);

@@ -414,6 +414,15 @@ int orc_update_checksum(orc_chunk_meta *meta, orc_write_io wio, uint32_t chunk_s
 /* ------------------------------------------------------------------ */
 int orc_chunk_replica_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chunk_size, const orc_update_io *io,
                              const uint8_t *payload, orc_update_result *res) {
+  return orc_chunk_replica_update_cs(meta, chunk, chunk_size, chunk_size, io, payload, res);
+}
+
+/* The same with the op's own UpdateIO.chunkSize (`io_chunk_size`) beside the chunk's
+ * innerFileId.chunkSize (`chunk_size`, also the capacity of `chunk`): the range check of
+ * :141-145 uses the op's, and :171-180 fails a non-REMOVE op whose chunkSize differs from the
+ * chunk's with kChunkSizeMismatch -- after :174 has set result.checksum = meta.checksum(). */
+int orc_chunk_replica_update_cs(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chunk_size, uint32_t io_chunk_size,
+                                const orc_update_io *io, const uint8_t *payload, orc_update_result *res) {
   res->status = ORC_OK;
   res->size = meta->size;
   res->type = ORC_NONE; /* IOResult default until :174 */
@@ -423,13 +432,18 @@ int orc_chunk_replica_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chun
     return ORC_OK;
   }
   const int is_remove = io->kind == ORC_UPD_REMOVE;
-  /* :140-145 range check (not for REMOVE) */
-  if (!is_remove && (io->offset >= chunk_size || (uint64_t)io->offset + io->length > chunk_size)) {
+  /* :140-145 range check against writeIO.chunkSize (not for REMOVE) */
+  if (!is_remove && (io->offset >= io_chunk_size || (uint64_t)io->offset + io->length > io_chunk_size)) {
     res->status = 3; /* StatusCode::kInvalidArg */
     return res->status;
   }
   res->type = meta->checksum_type; /* :174 result.checksum = meta.checksum() */
   res->value = meta->checksum_value;
+  /* :171 chunkSize = isRemove ? meta.innerFileId.chunkSize : writeIO.chunkSize; :176-180 */
+  if (!is_remove && io_chunk_size != chunk_size) {
+    res->status = ORC_ERR_CHUNK_SIZE_MISMATCH;
+    return res->status;
+  }
   /* :193-207 verify the client's checksum of the payload */
   if (io->checksum_type != ORC_NONE && io->length != 0) {
     uint8_t t;

@@ -24,7 +24,8 @@ extern "C" {
 #define ORC_POLY_CRC32 0xEDB88320u  /* reflected IEEE 802.3 */
 
 enum { ORC_NONE = 0, ORC_CRC32C = 1, ORC_CRC32 = 2 };
-enum { ORC_OK = 0, ORC_ERR_CHECKSUM_MISMATCH = 4080, ORC_ERR_CHUNK_READ_FAILED = 4010 };
+enum { ORC_OK = 0, ORC_ERR_CHECKSUM_MISMATCH = 4080, ORC_ERR_CHUNK_READ_FAILED = 4010,
+       ORC_ERR_CHUNK_SIZE_MISMATCH = 4015 };
 
 /* --- A1: folly::crc32c / folly::crc32, three independent mechanisms --- */
 uint32_t orc_crc32c_bitwise(const uint8_t *d, size_t n, uint32_t start);
@@ -89,7 +90,7 @@ typedef struct {
   uint8_t syncing; /* UpdateOptions.isSyncing (ChunkReplica.cc:211-215, 289) */
 } orc_update_io;
 typedef struct {
-  int status;    /* 0, 3 kInvalidArg, 4080 kChecksumMismatch */
+  int status;    /* 0, 3 kInvalidArg, 4015 kChunkSizeMismatch, 4080 kChecksumMismatch */
   uint32_t size; /* meta.size after */
   uint8_t type;  /* result.checksum */
   uint32_t value;
@@ -97,6 +98,9 @@ typedef struct {
 } orc_update_result;
 int orc_chunk_replica_update(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chunk_size, const orc_update_io *io,
                              const uint8_t *payload, orc_update_result *res);
+/* with UpdateIO.chunkSize (io_chunk_size) distinct from the chunk's (chunk_size): :141-145, :171-180 */
+int orc_chunk_replica_update_cs(orc_chunk_meta *meta, uint8_t *chunk, uint32_t chunk_size, uint32_t io_chunk_size,
+                                const orc_update_io *io, const uint8_t *payload, orc_update_result *res);
 
 /* --- A10 + A11: Rust chunk engine update (std domain; meta->checksum_value is std) --- */
 typedef struct {

@@ -115,7 +115,7 @@ static void gpu_tests() {
       const uint32_t o = (k % 3 == 0 || size == 0) ? size : (uint32_t)(rng() % size);
       const uint8_t *p = hp.data() + k * 8192;
       ios.push_back(h3c_update_io{(uint64_t)(uintptr_t)(pay + k * 8192), 0, o, len, orc_crc32c_sse42(p, len, ~0U), 1,
-                                  H3C_UPD_WRITE, 0, {0, 0, 0, 0, 0}});
+                                  H3C_UPD_WRITE, 0, 0, 0});
       std::memcpy(model.data() + o, p, len);
       size = std::max(size, o + len);
     }

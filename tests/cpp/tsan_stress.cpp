@@ -102,7 +102,7 @@ void worker(int t, int iters) {
       const uint32_t off = (uint32_t)(rnd() % (len - pay.size()));
       ios[i] = h3c_update_io{(uint64_t)(uintptr_t)d_pay, (uint32_t)i, off, (uint32_t)pay.size(),
                              crc_bitwise(pay.data(), pay.size(), 0xFFFFFFFFu), H3C_TYPE_CRC32C, H3C_UPD_WRITE, 0,
-                             {0, 0, 0, 0, 0}};
+                             0, 0};
       std::memcpy(host.data() + i * len + off, pay.data(), pay.size());
     }
     std::vector<h3c_update_result> res(nb);

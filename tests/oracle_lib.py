@@ -144,6 +144,10 @@ def _bind_update(L):
         L.orc_chunk_replica_update.argtypes = [ctypes.POINTER(ChunkMeta), ctypes.c_void_p, ctypes.c_uint32,
                                                ctypes.POINTER(UpdateIO), ctypes.c_void_p,
                                                ctypes.POINTER(UpdateResult)]
+        L.orc_chunk_replica_update_cs.restype = ctypes.c_int
+        L.orc_chunk_replica_update_cs.argtypes = [ctypes.POINTER(ChunkMeta), ctypes.c_void_p, ctypes.c_uint32,
+                                                  ctypes.c_uint32, ctypes.POINTER(UpdateIO), ctypes.c_void_p,
+                                                  ctypes.POINTER(UpdateResult)]
         L.orc_chunk_engine_update.restype = ctypes.c_int
         L.orc_chunk_engine_update.argtypes = [ctypes.POINTER(ChunkMeta), ctypes.c_void_p, ctypes.c_uint32,
                                               ctypes.POINTER(UpdateIO), ctypes.c_void_p, ctypes.c_int,
@@ -164,14 +168,15 @@ def _update_args(meta, io, payload):
 def replica_update(meta: dict, chunk: np.ndarray, chunk_size: int, io: dict, payload=None):
     """ChunkReplica::update restatement (A6 + A8): applies one UpdateIO to `chunk` in place.
 
-    io = {kind, offset, length, type, value[, syncing]}.  Returns (result dict with the
-    updateChecksum branch in "ucase", new meta dict)."""
+    io = {kind, offset, length, type, value[, syncing][, chunk_size]}: `chunk_size` is the op's
+    UpdateIO.chunkSize (default: the chunk's own, `chunk_size` here).  Returns (result dict with
+    the updateChecksum branch in "ucase", new meta dict)."""
     L = lib()
     _bind_update(L)
     m, u, pay = _update_args(meta, io, payload)
     r = UpdateResult()
-    L.orc_chunk_replica_update(ctypes.byref(m), chunk.ctypes.data, chunk_size, ctypes.byref(u),
-                               pay.ctypes.data if pay is not None else None, ctypes.byref(r))
+    L.orc_chunk_replica_update_cs(ctypes.byref(m), chunk.ctypes.data, chunk_size, io.get("chunk_size", chunk_size),
+                                  ctypes.byref(u), pay.ctypes.data if pay is not None else None, ctypes.byref(r))
     return ({"status": r.status, "size": r.size, "type": r.type, "value": r.value, "ucase": r.ucase},
             {"size": m.size, "type": m.checksum_type, "value": m.checksum_value})
 

@@ -37,3 +37,43 @@ def test_roofline_update_workload_and_unmatched_sizes():
     # no PMC summary for another per-launch size: traffic stays null rather than borrowed
     r = b.roofline((1.0, 1, per + 4096), b.HBM_PEAK_GBPS, kernel="upd_delta_kernel")
     assert r["traffic"] is None
+
+
+def _bench(args, env_extra=None, timeout=120):
+    import json
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    return p.returncode, lines, p.stderr
+
+
+def test_gpus_n_spawns_n_ranks_without_a_launcher():
+    """`bench.py --gpus N` with WORLD_SIZE unset starts N ranks itself (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* as torchrun sets them); rank 0 prints the one line."""
+    rc, lines, err = _bench(["--gpus", "3", "--dry-run-launch", "-1"])
+    assert rc == 0, err
+    assert len(lines) == 1
+    assert lines[0]["n_gpus"] == 3 and lines[0]["local_ranks"] == [0, 1, 2] and lines[0]["launched"]
+
+
+def test_gpus_one_runs_in_process():
+    rc, lines, err = _bench(["--gpus", "1", "--dry-run-launch", "-1"])
+    assert rc == 0, err
+    assert lines == [{"dry_run": True, "n_gpus": 1, "local_ranks": [0], "launched": False}]
+
+
+def test_world_size_mismatch_fails():
+    rc, lines, err = _bench(["--gpus", "2", "--dry-run-launch", "-1"], {"WORLD_SIZE": "4", "RANK": "0"})
+    assert rc != 0 and not lines and "disagrees" in err
+
+
+def test_failed_rank_fails_the_launch():
+    """A rank that dies makes the launcher exit non-zero (the worst code) after a grace period
+    that ends the ranks left waiting in the rendezvous."""
+    rc, lines, err = _bench(["--gpus", "2", "--dry-run-launch", "1"], {"H3C_BENCH_GRACE_S": "3"})
+    assert rc == 3 and not lines

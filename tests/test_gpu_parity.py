@@ -393,3 +393,32 @@ def test_uniform_small_chunk_counts(h3c, torch_dev, n):
         assert np.array_equal(out.cpu().numpy().view(np.uint32), exp), (n, clen)
         plan.close()
 
+
+
+def test_plan_extent_is_checked_before_launch(h3c, torch_dev):
+    """a plan whose layout runs past its buffer is rejected with kInvalidArg
+    before any upload or launch -- by Plan.uniform against the tensor's (or a given) extent, and
+    by h3c_plan_create against the HIP allocation holding each descriptor.  Nothing here is ever
+    run: only plan creation is attempted."""
+    torch, dev = torch_dev
+    buf = torch.zeros(16 << 20, dtype=torch.uint8, device=dev)
+    with pytest.raises(h3c.EngineError) as e:
+        h3c.Plan.uniform(buf, 4096, 3001, stride=8192)  # 24 MiB > 16 MiB
+    assert e.value.code == h3c.StatusCode.kInvalidArg
+    with pytest.raises(h3c.EngineError):
+        h3c.Plan.uniform(buf.data_ptr(), 4096, 2049, extent=8 << 20)
+    h3c.Plan.uniform(buf, 4096, 4096).close()  # exactly the buffer: fine
+    # library level: a descriptor ending 400 GiB past its allocation (beyond any HBM)
+    d = np.zeros(2, dtype=h3c.engine.DESC_DTYPE)
+    d["ptr"] = [buf.data_ptr(), buf.data_ptr() + (8 << 20)]
+    d["len"] = [4096, 400 << 30]
+    d["start_raw"] = 0xFFFFFFFF
+    d["type"] = 1
+    with pytest.raises(h3c.EngineError) as e:
+        h3c.Plan(d, dev.index or 0)
+    assert e.value.code == h3c.StatusCode.kInvalidArg and "past the end" in str(e.value)
+    # the synchronous batch path checks device payloads the same way (and launches nothing)
+    d["mem"] = 0
+    out_t, out_v = np.zeros(2, dtype=np.uint8), np.zeros(2, dtype=np.uint32)
+    rc = h3c.engine.lib.h3c_batch_create(d.ctypes.data, 2, out_t.ctypes.data, out_v.ctypes.data, None)
+    assert rc == h3c.StatusCode.kInvalidArg

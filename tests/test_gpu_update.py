@@ -194,9 +194,8 @@ def test_update_blocks_large_chunk_count_paths(h3c, torch_dev, hooks):
 def test_update_config3_shape_full_size(h3c, torch_dev):
     """BASELINE config 3: 100k random 4 KiB writes into 64 x 64 MiB chunks.
 
-    Size-independent checks: every chunk's final checksum equals a fresh GPU create of
-    its final bytes, the bytes equal the host replay, and chunk 0 is replayed write by
-    write through the oracle's updateChecksum."""
+    Every chunk's final checksum equals the oracle's CRC of its final bytes (and a fresh GPU
+    create), and chunk 0 is replayed write by write through the oracle's updateChecksum."""
     torch, dev = torch_dev
     nchunks, chunk_len, nw = 64, 64 << 20, 100_000
     bpc = chunk_len // G
@@ -219,6 +218,11 @@ def test_update_config3_shape_full_size(h3c, torch_dev):
     plan.run(fresh)
     torch.cuda.synchronize()
     assert torch.equal(fresh, raw_out)
+    final_bytes = dchunks.cpu().numpy()
+    want_final = np.zeros(nchunks, dtype=np.uint32)
+    orc.lib().orc_batch_crc32c(final_bytes.ctypes.data, chunk_len, nchunks, 0xFFFFFFFF, 16, 0, want_final.ctypes.data)
+    assert np.array_equal(u32(raw_out), want_final)  # all 64 chunks against the oracle
+    del final_bytes
     got = u32(out)
     # chunk 0, write by write, through the oracle's updateChecksum (case iv over 64 MiB)
     pay = payload.cpu().numpy().reshape(nw, G)
@@ -267,3 +271,37 @@ def test_update_blocks_crc32_ieee(h3c, torch_dev):
         host[c, b * G:(b + 1) * G] = pay[k]
         assert int(got[k]) == orc.crc32(host[c]), k
     assert np.array_equal(d.cpu().numpy(), host)
+
+
+def test_update_fused_lookback_gives_up_and_reports_void_batch(h3c, torch_dev, hooks):
+    """a fused-path workgroup that gives up its look-back wait (forced for ticket 1
+    through H3C_HOOK_UPD_LOOKBACK) must not pass as a good batch: *n_invalid = UINT32_MAX and
+    counters.invalid = UINT64_MAX; the chunk bytes are still right.  Without the hook the same
+    batch is exact (run_case)."""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_SCAN, h3c.UPD_SCAN_PATHS["fused"])
+    rng = np.random.default_rng(99)
+    nchunks, chunk_len, nw = 8, 256 << 10, 20000  # many workgroups: ticket 1 has a predecessor
+    wc = rng.integers(0, nchunks, nw).astype(np.uint32)
+    wb = rng.integers(0, chunk_len // G, nw).astype(np.uint32)
+    chunks = rng.integers(0, 256, (nchunks, chunk_len), dtype=np.uint8)
+    raw0 = np.array([orc.crc32c(chunks[c]) for c in range(nchunks)], dtype=np.uint32)
+    pay = rng.integers(0, 256, (nw, G), dtype=np.uint8)
+    d = torch.from_numpy(chunks.copy()).to(dev)
+    bases = torch.tensor([d[c].data_ptr() for c in range(nchunks)], dtype=torch.int64, device=dev)
+    out = torch.zeros(nw, dtype=torch.int32, device=dev)
+    raw_out = torch.zeros(nchunks, dtype=torch.int32, device=dev)
+    ninv = torch.zeros(1, dtype=torch.int32, device=dev)
+    ctr = torch.zeros(8, dtype=torch.int64, device=dev)
+    hooks(h3c.HOOK_UPD_LOOKBACK, 1)
+    h3c.update_blocks(bases, chunk_len, i32(raw0, torch, dev), i32(wc, torch, dev), i32(wb, torch, dev),
+                      torch.from_numpy(pay).to(dev), out, raw_out, n_invalid=ninv, counters=ctr)
+    torch.cuda.synchronize()
+    assert int(ninv.item()) == -1 and int(ctr[6].item()) == -1
+    host = chunks.copy()
+    for k in range(nw):
+        host[wc[k], wb[k] * G:(wb[k] + 1) * G] = pay[k]
+    assert np.array_equal(d.cpu().numpy(), host)
+    hooks(h3c.HOOK_UPD_LOOKBACK, 0)
+    writes = [(int(c), int(b), 1) for c, b in zip(wc[:3000], wb[:3000])]
+    run_case(h3c, torch, dev, nchunks, chunk_len, writes, seed=100)

@@ -54,7 +54,9 @@ class Scenario:
         self.init_meta = [dict(m) for m in self.meta]
         self.ops, self.payloads, self.expect = [], [], []
 
-    def add(self, kind, chunk, offset, length, ctype=orc.CRC32C, good=True, payload=None, syncing=False):
+    def add(self, kind, chunk, offset, length, ctype=orc.CRC32C, good=True, payload=None, syncing=False,
+            io_chunk_size=None):
+        """io_chunk_size: the op carries UpdateIO.chunkSize (H3C_IO_CHUNK_SIZE) with this value."""
         if payload is None and kind == orc.UPD_WRITE:
             payload = self.rng.integers(0, 256, length, dtype=np.uint8)
         value = 0
@@ -65,6 +67,8 @@ class Scenario:
                 value ^= 0x10
         io = {"kind": kind, "offset": offset, "length": length, "type": ctype, "value": value,
               "syncing": int(syncing)}
+        if io_chunk_size is not None:
+            io["chunk_size"] = io_chunk_size
         self.ops.append((chunk, io))
         self.payloads.append(payload)
         if chunk < self.nchunks:
@@ -83,6 +87,8 @@ class Scenario:
         for e in self.expect:
             if e["status"] == 3:
                 want["invalid"] += 1
+            elif e["status"] == 4015:
+                pass  # kChunkSizeMismatch has no counter on the path
             elif e["status"] == 4080:
                 want["checksum_mismatch"] += 1
             elif e["ucase"] in names:
@@ -109,8 +115,9 @@ class Scenario:
                          0)
         ios = np.zeros(len(self.ops), dtype=h3c.UPDATE_IO_DTYPE)
         for i, ((c, io), o, p) in enumerate(zip(self.ops, offs, self.payloads)):
+            flags = (h3c.IO_SYNCING if io.get("syncing") else 0) | (h3c.IO_CHUNK_SIZE if "chunk_size" in io else 0)
             ios[i] = (self._dpay.data_ptr() + o if p is not None else 0, c, io["offset"], io["length"], io["value"],
-                      io["type"], io["kind"], h3c.IO_SYNCING if io.get("syncing") else 0, 0)
+                      io["type"], io["kind"], flags, 0, io.get("chunk_size", 0))
         return chunks, ios
 
     def run(self, exact=False, type_=None, dev_api=False):
@@ -325,6 +332,39 @@ def test_updio_edge_cases(h3c, torch_dev):
     sc.check(*sc.run())
 
 
+@pytest.mark.parametrize("dev_api", [False, True])
+def test_updio_chunk_size_of_the_update_io(h3c, torch_dev, dev_api):
+    """UpdateIO.chunkSize (H3C_IO_CHUNK_SIZE).  The range check of
+    ChunkReplica.cc:141-145 uses the op's chunkSize; an op whose chunkSize differs from the
+    chunk's innerFileId.chunkSize fails with kChunkSizeMismatch (4015, :171-180) and reports
+    meta.checksum() (:174); REMOVE uses the chunk's own (:171).  Mixed with ops that carry no
+    chunkSize, replayed through the oracle."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(4015)
+    cs = 64 << 10
+    sc = Scenario(h3c, torch, dev, 6, cs, rng, init="mixed")
+    for k in range(600):
+        c = int(rng.integers(0, 6))
+        u = rng.random()
+        ocs = cs if u < 0.5 else (None if u < 0.7 else int(rng.choice([cs // 2, cs * 2, 1 << 20, 4096])))
+        off = int(rng.integers(0, cs))
+        kind = orc.UPD_WRITE if rng.random() < 0.85 else orc.UPD_TRUNCATE
+        if kind == orc.UPD_WRITE:
+            sc.add(kind, c, off, int(rng.integers(0, min(cs - off, 6000) + 1)), io_chunk_size=ocs,
+                   good=rng.random() > 0.05)
+        else:
+            sc.add(kind, c, 0, int(rng.integers(0, cs + 1)), orc.NONE, io_chunk_size=ocs)
+    # explicit corners: offset inside the chunk but past the op's chunkSize -> kInvalidArg first;
+    # a smaller op chunkSize that admits the range -> 4015; REMOVE with a wrong chunkSize -> fine
+    sc.add(orc.UPD_WRITE, 1, 5000, 10, io_chunk_size=4096)
+    sc.add(orc.UPD_WRITE, 1, 100, 10, io_chunk_size=4096)
+    sc.add(orc.UPD_WRITE, 1, 100, 10, io_chunk_size=cs * 2)
+    sc.add(orc.UPD_WRITE, 1, cs, 10, io_chunk_size=cs * 2)
+    sc.add(orc.UPD_REMOVE, 2, 0, 0, orc.NONE, io_chunk_size=7)
+    assert sum(e["status"] == 4015 for e in sc.expect) > 50
+    sc.check(*sc.run(dev_api=dev_api))
+
+
 def test_updio_invalid_chunk_index(h3c, torch_dev):
     torch, dev = torch_dev
     rng = np.random.default_rng(8)
@@ -518,8 +558,8 @@ def test_updio_rejects_malformed_remove_and_syncing(h3c, torch_dev):
     pay = torch.zeros(16, dtype=torch.uint8, device=dev)
     ios = np.zeros(3, dtype=h3c.UPDATE_IO_DTYPE)
     ios[0] = (0, 0, 0, 5, 0, 0, h3c.UPD_REMOVE, 0, 0)
-    ios[1] = (pay.data_ptr(), 0, 8, 8, 0, 0, h3c.UPD_WRITE, h3c.IO_SYNCING, 0)
-    ios[2] = (0, 0, 0, 50, 0, 0, h3c.UPD_TRUNCATE, h3c.IO_SYNCING, 0)
+    ios[1] = (pay.data_ptr(), 0, 8, 8, 0, 0, h3c.UPD_WRITE, h3c.IO_SYNCING, 0, 0)
+    ios[2] = (0, 0, 0, 50, 0, 0, h3c.UPD_TRUNCATE, h3c.IO_SYNCING, 0, 0)
     cnt = h3c.UpdateCounters()
     res = h3c.update_ios(chunks, ios, counters=cnt)
     assert list(res["status"]) == [3, 3, 3] and cnt.invalid == 3
@@ -698,7 +738,7 @@ def _engine_replay(rng, h3c, torch, dev, nchunks, cs, nops, stale=0.0, exact=Fal
         # bridge, which passes ~raw (ChunkEngine.cc:41-42)
         ck = (~io["value"]) & MASK if io["type"] == orc.CRC32C else io["value"]
         ios[i] = (base + o if p is not None else 0, io["chunk"], io["offset"], io["length"], ck, io["type"],
-                  io["kind"], h3c.IO_SYNCING if io.get("syncing") else 0, 0)
+                  io["kind"], h3c.IO_SYNCING if io.get("syncing") else 0, 0, 0)
     counters = h3c.UpdateCounters()
     res = h3c.update_ios(chunks, ios, std_domain=True, exact=exact, counters=counters)
     torch.cuda.synchronize()
@@ -844,16 +884,13 @@ def test_updio_graph_replay_times_the_block_kernel(h3c, torch_dev, hooks):
     assert replays[0] == 0 and replays[-2:] == [1, 1], replays
 
 
-def test_updio_graphs_only_single_threaded_by_default(h3c, torch_dev):
-    """Once several threads have called the engine, a repeated batch shape is not captured (HIP
-    fails legacy-stream launches made while any stream captures): the calls run plainly and
+@pytest.mark.parametrize("asked", [False, True])
+def test_updio_graphs_only_when_the_caller_asks(h3c, torch_dev, asked):
+    """A repeated batch shape is captured only with H3C_UPD_GRAPHS (HIP fails legacy-stream
+    launches that any thread makes while a stream captures, so only the caller can vouch for
+    the process): without the flag the calls run plainly, with it the later calls replay; both
     stay correct."""
-    import threading
-
     torch, dev = torch_dev
-    t = threading.Thread(target=lambda: h3c.device_count() and h3c.crc32c(b"x" * 64))
-    t.start()
-    t.join()  # a second thread has used the engine (the module's own tests use more)
     rng = np.random.default_rng(95)
     sc = Scenario(h3c, torch, dev, 4, 64 << 10, rng, init="crc")
     for _ in range(500):
@@ -864,14 +901,18 @@ def test_updio_graphs_only_single_threaded_by_default(h3c, torch_dev):
     d_res = torch.zeros(len(ios) * h3c.UPDATE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
     slab0 = sc.slab.clone()
     r0, c0 = h3c.diag_counter(0), h3c.diag_counter(1)
+    d_chunks = d_chunks0.clone()
     for _ in range(4):
         sc.slab.copy_(slab0)
-        d_chunks = d_chunks0.clone()
-        h3c.update_ios_dev(d_chunks, d_ios, d_res)
+        d_chunks.copy_(d_chunks0)
+        h3c.update_ios_dev(d_chunks, d_ios, d_res, graphs=asked)
         torch.cuda.synchronize()
         sc.check(d_chunks.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE),
                  d_res.cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE), counters=False)
-    assert (h3c.diag_counter(0), h3c.diag_counter(1)) == (r0, c0)
+    if asked:
+        assert h3c.diag_counter(0) > r0 and h3c.diag_counter(1) > c0
+    else:
+        assert (h3c.diag_counter(0), h3c.diag_counter(1)) == (r0, c0)
 
 
 def test_updio_device_resident_redo_from_original_states(h3c, torch_dev):

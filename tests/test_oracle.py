@@ -332,3 +332,33 @@ def test_engine_restatement_relational_pin():
         if res["ucase"] != orc.CASE_KEEP:
             applied += 1
     assert cnt.reuse + cnt.recalculate + cnt.combine >= applied - 2
+
+
+def test_replica_update_chunk_size_semantics():
+    """UpdateIO.chunkSize restated (ChunkReplica.cc:141-145, 171-180): the range check uses the
+    op's chunkSize (kInvalidArg, before result.checksum is set); a WRITE / TRUNCATE whose chunkSize
+    differs from the chunk's fails with kChunkSizeMismatch (4015) after :174 set result.checksum =
+    meta.checksum(), leaving bytes and metadata alone; REMOVE takes the chunk's own chunkSize."""
+    cs = 8192
+    rng = np.random.default_rng(15)
+    chunk = rng.integers(0, 256, cs, dtype=np.uint8)
+    meta = {"size": 6000, "type": orc.CRC32C, "value": orc.crc32c(chunk[:6000])}
+    before = chunk.copy()
+    pay = rng.integers(0, 256, 10, dtype=np.uint8)
+    w = {"kind": orc.UPD_WRITE, "offset": 100, "length": 10, "type": orc.CRC32C,
+         "value": orc.create(orc.CRC32C, pay, 10)[1]}
+    res, m2 = orc.replica_update(dict(meta), chunk, cs, dict(w, chunk_size=4096), pay)
+    assert res["status"] == 4015 and (res["type"], res["value"]) == (orc.CRC32C, meta["value"])
+    assert m2 == meta and np.array_equal(chunk, before)
+    res, m2 = orc.replica_update(dict(meta), chunk, cs, dict(w, offset=5000, chunk_size=4096), pay)
+    assert res["status"] == 3 and res["type"] == 0 and res["value"] == 0  # range check first
+    res, m2 = orc.replica_update(dict(meta), chunk, cs, dict(w, offset=8190, chunk_size=16384), pay)
+    assert res["status"] == 4015
+    res, _ = orc.replica_update(dict(meta), chunk, cs, {"kind": orc.UPD_TRUNCATE, "offset": 0, "length": 10,
+                                                        "type": 0, "value": 0, "chunk_size": 4096})
+    assert res["status"] == 4015
+    res, m2 = orc.replica_update(dict(meta), chunk, cs, {"kind": orc.UPD_REMOVE, "offset": 0, "length": 0,
+                                                         "type": 0, "value": 0, "chunk_size": 7})
+    assert res["status"] == 0 and m2["type"] == orc.NONE
+    res, m2 = orc.replica_update(dict(meta), chunk, cs, dict(w, chunk_size=cs), pay)  # equal: applied
+    assert res["status"] == 0 and m2["value"] == orc.crc32c(chunk[:6000])
