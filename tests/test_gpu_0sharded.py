@@ -110,7 +110,7 @@ def _worker(rank, world, port, q, expected):
                     keep.append(t)
                     ptr = t.data_ptr() if ln else 0
                     ctype, value = orc.CRC32C, orc.create(orc.CRC32C, p, ln)[1]
-                ios[k] = (ptr, local, off, ln, value, ctype, kind, 0, 0)
+                ios[k] = (ptr, local, off, ln, value, ctype, kind, 0, 0, 0)
             return h3c.update_ios(table, ios)
 
         res = shard.run_sharded_updates([o[1] for o in ops], chunk_bytes, apply, rank, world)

@@ -82,7 +82,7 @@ def test_concurrent_update_batches_distinct_chunks(h3c, torch_dev):
         dpay = torch.from_numpy(pay.reshape(-1)).to(dev)
         for i in range(nw):
             c, b = int(rng.integers(0, nchunks)), int(rng.integers(0, cl // G))
-            io[i] = (dpay.data_ptr() + i * G, c, b * G, G, orc.crc32c(pay[i]), 1, h3c.UPD_WRITE, 0, 0)
+            io[i] = (dpay.data_ptr() + i * G, c, b * G, G, orc.crc32c(pay[i]), 1, h3c.UPD_WRITE, 0, 0, 0)
             host[c, b * G:(b + 1) * G] = pay[i]
         slabs.append(slab)
         states.append(st)

@@ -50,7 +50,7 @@ class Engine:
                 t = self.torch.from_numpy(np.frombuffer(bytes(data), dtype=np.uint8).copy()).to(self.dev)
                 self.keep.append(t)
                 ptr = t.data_ptr()
-            ios[i] = (ptr, c, off, length, 0 if ck is None else ck, 0 if ck is None else 1, kind, 0, 0)
+            ios[i] = (ptr, c, off, length, 0 if ck is None else ck, 0 if ck is None else 1, kind, 0, 0, 0)
         res = self.h3c.update_ios(self.state, ios, std_domain=True)
         self.torch.cuda.synchronize()
         return res

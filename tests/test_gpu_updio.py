@@ -430,7 +430,7 @@ def test_updio_std_domain_rust_engine(h3c, torch_dev):
     dpay = torch.from_numpy(pay).to(dev)
     ios = np.zeros(len(ops), dtype=h3c.UPDATE_IO_DTYPE)
     for i, ((c, kind, off, ln, val, ty), po, p) in enumerate(zip(ops, offs, pays)):
-        ios[i] = (dpay.data_ptr() + po if p is not None else 0, c, off, ln, val, ty, kind, 0, 0)
+        ios[i] = (dpay.data_ptr() + po if p is not None else 0, c, off, ln, val, ty, kind, 0, 0, 0)
     res = h3c.update_ios(chunks, ios, std_domain=True)
     for i, (r, (st, sz, v)) in enumerate(zip(res, want)):
         assert int(r["status"]) == st and int(r["size"]) == sz, (i, r, st, sz)
@@ -507,8 +507,8 @@ def test_updio_truncate_of_other_polynomial_chunk_is_rejected(h3c, torch_dev):
     chunks = np.zeros(1, dtype=h3c.CHUNK_STATE_DTYPE)
     chunks[0] = (slab.data_ptr(), 4096, 100, orc.crc32(np.zeros(100, dtype=np.uint8)), 2, 0)  # stored CRC32
     ios = np.zeros(2, dtype=h3c.UPDATE_IO_DTYPE)
-    ios[0] = (0, 0, 0, 50, 0, 0, h3c.UPD_TRUNCATE, 0, 0)
-    ios[1] = (0, 0, 0, 200, 0, 0, h3c.UPD_EXTEND, 0, 0)
+    ios[0] = (0, 0, 0, 50, 0, 0, h3c.UPD_TRUNCATE, 0, 0, 0)
+    ios[1] = (0, 0, 0, 200, 0, 0, h3c.UPD_EXTEND, 0, 0, 0)
     res = h3c.update_ios(chunks, ios)  # batch polynomial CRC32C
     assert list(res["status"]) == [3, 3]
     assert int(chunks[0]["size"]) == 100 and int(chunks[0]["type"]) == 2
@@ -557,7 +557,7 @@ def test_updio_rejects_malformed_remove_and_syncing(h3c, torch_dev):
     chunks[0] = (slab.data_ptr(), 8192, 100, orc.crc32c(np.zeros(100, dtype=np.uint8)), 1, 0)
     pay = torch.zeros(16, dtype=torch.uint8, device=dev)
     ios = np.zeros(3, dtype=h3c.UPDATE_IO_DTYPE)
-    ios[0] = (0, 0, 0, 5, 0, 0, h3c.UPD_REMOVE, 0, 0)
+    ios[0] = (0, 0, 0, 5, 0, 0, h3c.UPD_REMOVE, 0, 0, 0)
     ios[1] = (pay.data_ptr(), 0, 8, 8, 0, 0, h3c.UPD_WRITE, h3c.IO_SYNCING, 0, 0)
     ios[2] = (0, 0, 0, 50, 0, 0, h3c.UPD_TRUNCATE, h3c.IO_SYNCING, 0, 0)
     cnt = h3c.UpdateCounters()
