@@ -625,22 +625,25 @@ __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(Src src, const u
   constexpr uint64_t kQ = 16u * G;
   constexpr int kRed = (1 + kLevels) * 1024;
   __shared__ uint32_t lds[kLdsWords + kRed];
+  const uint32_t total = *d_total;
+  // Each workgroup owns a contiguous range; one with none returns before filling its tables (a
+  // pass with few or no pieces -- the UpdateIO late pass, usually empty -- costs a launch only).
+  const uint32_t wlo = (uint32_t)((uint64_t)blockIdx.x * total / gridDim.x);
+  const uint32_t whi = (uint32_t)((uint64_t)(blockIdx.x + 1) * total / gridDim.x);
+  if (wlo >= whi) return;
   for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value_of(pc->tabf, i);
   const uint32_t *red_g = &pc->red[0][0][0];
   for (int i = threadIdx.x; i < kRed; i += kThreads) lds[kLdsWords + i] = red_g[i];
   __syncthreads();
-  const uint32_t total = *d_total;
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
   const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
   const uint32_t poly = pc->poly;
   const LaneLut L = make_lut(lane);
-  // Each workgroup owns a contiguous range; its waves take steps of NG pieces from an LDS
-  // counter (a static split per wave left a third of the waves with one step more than the
-  // rest at a few steps per wave; one global counter serialised thousands of atomics).
+  // Its waves take steps of NG pieces from an LDS counter (a static split per wave left a third
+  // of the waves with one step more than the rest at a few steps per wave; one global counter
+  // serialised thousands of atomics).
   __shared__ uint32_t wg_next;
-  const uint32_t wlo = (uint32_t)((uint64_t)blockIdx.x * total / gridDim.x);
-  const uint32_t whi = (uint32_t)((uint64_t)(blockIdx.x + 1) * total / gridDim.x);
   if (threadIdx.x == 0) wg_next = wlo;
   __syncthreads();
   for (;;) {

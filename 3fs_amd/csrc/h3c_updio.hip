@@ -143,8 +143,17 @@ struct OpPos {
   uint8_t tb, ta;   // stored type before / after
   uint8_t ccode;    // counter of an applied op (kC_*)
   uint8_t ncomb;    // Rust engine: checksum_combine increments (0-2)
-  uint8_t pad[2];
+  uint8_t pf;       // kPos* flags
+  uint8_t pad;
 };
+// A "fold" op's client checksum (A6) is checked by the block kernel as it reads the payload --
+// the payload is read once -- instead of by the piece pass before it.  That is sound only for
+// an op whose failure changes nothing but its own bytes and checksum: a typed WRITE whose bytes
+// lie in one 4 KiB block and which keeps the chunk's size and stored type (its failure then
+// leaves every later op's case, size and fragments as speculated; the block kernel skips its
+// bytes and phase B treats it as the identity).  Other candidates are checked by a late piece
+// pass before the block kernel, beside the fragment stage.
+constexpr uint8_t kPosFold = 1;
 
 // One block of one op (64 B).  Ranges are block-relative byte offsets in [0, 4096].
 struct FragDesc {
@@ -158,10 +167,13 @@ struct FragDesc {
   uint16_t k0, k1;  // the chunk's own bytes in this block (loads / stores)
   uint32_t mult;    // CRC contribution shift x^(8e), e = the op's size after - block end (chunk-relative)
   uint32_t flags;
-  uint32_t pad[4];
+  uint32_t op;      // kFragA6: the op, its client checksum and payload length
+  uint32_t expect;
+  uint32_t len;
+  uint32_t pad;
 };
 static_assert(sizeof(FragDesc) == 64, "FragDesc is one 64-byte record");
-constexpr uint32_t kFragCrc = 1u, kFragWrite = 2u, kFragHead = 4u;
+constexpr uint32_t kFragCrc = 1u, kFragWrite = 2u, kFragHead = 4u, kFragA6 = 8u;
 
 // counters: a workgroup-aggregated add -- wave sums into LDS, one global atomic per counter
 // and workgroup (call from workgroup-uniform control flow; `sh` holds kCtrN slots)
@@ -187,9 +199,21 @@ __device__ __forceinline__ bool needs_init(const h3c_chunk_state &cs, uint8_t po
   return cs.size && cs.size <= cs.chunk_size && (exact || cs.type != poly_type);
 }
 
+// A typed, non-empty, non-syncing WRITE whose payload lands in one 4 KiB block of its chunk
+// (absolute addresses): its A6 check may move into the block kernel (kPosFold, decided by
+// classify).  `st` is the op's status so far.
+__device__ __forceinline__ bool fold_candidate(const h3c_update_io &io, const h3c_chunk_state &cs, uint32_t st) {
+  if (st != H3C_OK || io.kind != H3C_UPD_WRITE || io.checksum_type == H3C_TYPE_NONE || !io.length ||
+      (io.flags & H3C_IO_SYNCING))
+    return false;
+  const uint64_t a = cs.base + io.offset;
+  return (a >> 12) == ((a + io.length - 1) >> 12);
+}
+
 // Validation (ChunkReplica.cc:140-145 range check; the ABI's preconditions), sort keys, and
-// the piece counts of the one piece-CRC pass: op i's payload is item i, chunk c's bytes (when
-// t0 comes from them) item n + c.  max(n, nchunks) + 1 threads.
+// the piece counts of the early piece-CRC pass: op i's payload is item i (fold candidates have
+// none: the block kernel or the late pass checks them), chunk c's bytes (when t0 comes from
+// them) item n + c.  max(n, nchunks) + 1 threads.
 __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t n, const h3c_chunk_state *__restrict__ chunks,
                                 uint32_t nchunks, uint8_t poly_type, uint32_t std_domain, uint32_t exact,
                                 uint32_t *__restrict__ status, uint32_t *__restrict__ key, uint32_t *__restrict__ idx,
@@ -199,12 +223,18 @@ __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t 
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < kCtrN) ctr[i] = 0;
   if (i < kMiscN) misc[i] = i == kMiscT0 || i == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;
-  if (i < nchunks) {
-    const h3c_chunk_state cs = chunks[i];
-    npieces[n + i] = needs_init(cs, poly_type, exact) ? (cs.size + kPieceBytes - 1) / kPieceBytes : 0u;
+  // chunk items n + c for c < C = max(nchunks, 1) (the piece pass's NP = n + C items), then the
+  // scan's extra entry: pbase[n + C] = total
+  const uint32_t C = nchunks ? nchunks : 1u;
+  if (i < C) {
+    npieces[n + i] = 0;
+    if (i < nchunks) {
+      const h3c_chunk_state cs = chunks[i];
+      npieces[n + i] = needs_init(cs, poly_type, exact) ? (cs.size + kPieceBytes - 1) / kPieceBytes : 0u;
+    }
     paycrc0[n + i] = 0;
   }
-  if (i == nchunks) npieces[n + nchunks] = 0;  // the scan's extra entry: pbase[n + nchunks] = total
+  if (i == C) npieces[n + C] = 0;
   if (i >= n) return;
   paycrc0[i] = 0;  // XOR accumulators of the piece and block kernels
   eacc[i] = 0;
@@ -244,7 +274,9 @@ __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t 
   status[i] = st;
   key[i] = c < nchunks ? c : nchunks;
   idx[i] = i;
-  npieces[i] = (st == H3C_OK && io.kind == H3C_UPD_WRITE && io.length) ? (io.length + kPieceBytes - 1) / kPieceBytes : 0;
+  const bool cand = st == H3C_OK && fold_candidate(io, chunks[c], st);
+  npieces[i] = (st == H3C_OK && io.kind == H3C_UPD_WRITE && io.length && !cand)
+                   ? (io.length + kPieceBytes - 1) / kPieceBytes : 0;
 }
 
 __device__ __forceinline__ bool applied_kind(uint8_t kind) {
@@ -259,10 +291,11 @@ __device__ __forceinline__ void verify_op(uint32_t i, const h3c_update_io *__res
                                           const uint32_t *__restrict__ paycrc0, const PolyConsts *__restrict__ pc,
                                           uint32_t std_domain, const uint32_t *__restrict__ status,
                                           uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6,
-                                          uint32_t *__restrict__ misc) {
+                                          uint32_t *__restrict__ misc, const h3c_chunk_state *__restrict__ skip_cand) {
   const h3c_update_io io = ios[i];
   uint32_t bad = 0;
-  if (io.kind == H3C_UPD_WRITE && status[i] == H3C_OK) {
+  // skip_cand: the early pass, which carries no fold candidate's payload
+  if (io.kind == H3C_UPD_WRITE && status[i] == H3C_OK && !(skip_cand && fold_candidate(io, skip_cand[io.chunk], H3C_OK))) {
     const uint32_t poly = pc->poly;
     const uint32_t raw = io.length ? paycrc0[i] ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(io.length, pc, poly), poly)
                                    : 0xFFFFFFFFu;
@@ -333,11 +366,11 @@ __device__ __forceinline__ uint32_t blocks_of(uint64_t base, uint32_t r0, uint32
 __global__ void uio_classify_kernel(const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ order,
                                     const uint32_t *__restrict__ skey, uint32_t n, const h3c_chunk_state *__restrict__ chunks,
                                     uint32_t nchunks, const SzTy *__restrict__ scan, const uint32_t *__restrict__ status,
-                                    uint8_t poly_type, uint32_t std_domain, OpPos *__restrict__ pos,
-                                    uint32_t *__restrict__ nfrag) {
+                                    uint8_t poly_type, uint32_t std_domain, uint32_t nofold, OpPos *__restrict__ pos,
+                                    uint32_t *__restrict__ nfrag, uint32_t *__restrict__ late) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) {
-    if (p == n) nfrag[n] = 0;
+    if (p == n) nfrag[n] = late[n] = 0;
     return;
   }
   const uint32_t i = order[p], c = skey[p];
@@ -348,6 +381,7 @@ __global__ void uio_classify_kernel(const h3c_update_io *__restrict__ ios, const
   if (c >= nchunks) {  // names no chunk of the batch
     pos[p] = r;
     nfrag[p] = 0;
+    late[i] = 0;
     return;
   }
   const h3c_chunk_state cs = chunks[c];
@@ -457,8 +491,41 @@ __global__ void uio_classify_kernel(const h3c_update_io *__restrict__ ios, const
       }
     }
   }
+  // A6 of a fold candidate: in the block kernel when the op is local (keeps size and stored type),
+  // else in the late piece pass (late[op] = its one piece); nofold: every verdict is known already
+  const bool cand = !nofold && fold_candidate(io, cs, r.status);
+  const bool fold = cand && r.na == r.nb && r.ta == r.tb && r.tk != kT_IDENT;
+  r.pf = fold ? kPosFold : 0;
+  late[i] = cand && !fold ? 1u : 0u;
   pos[p] = r;
   nfrag[p] = r.tk == kT_IDENT ? 0u : blocks_of(cs.base, r.r0, r.r1);
+}
+
+// The late pass's verdicts: A6 of the fold candidates that were not folded (late[i] == 1).  Their
+// payload CRCs were zeroed by the prep kernel and accumulated by the late piece pass.
+__global__ void uio_late_verify_kernel(const h3c_update_io *__restrict__ ios, uint32_t n,
+                                       const uint32_t *__restrict__ late, const uint32_t *__restrict__ paycrc0,
+                                       const PolyConsts *__restrict__ pc, uint32_t std_domain,
+                                       const uint32_t *__restrict__ status, uint32_t *__restrict__ payraw,
+                                       uint32_t *__restrict__ a6, uint32_t *__restrict__ misc) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && late[i]) verify_op(i, ios, paycrc0, pc, std_domain, status, payraw, a6, misc, nullptr);
+}
+
+// Before a redo after a failed A6: every typed WRITE's payload is CRC'd again, fold candidates
+// included (n items; chunk items keep their t0), so that the redo runs with every verdict known.
+__global__ void uio_redo_pieces_kernel(const h3c_update_io *__restrict__ ios, uint32_t n, uint32_t np_items,
+                                       const uint32_t *__restrict__ status, uint32_t *__restrict__ npieces,
+                                       uint32_t *__restrict__ paycrc0) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const h3c_update_io io = ios[i];
+    npieces[i] = (status[i] == H3C_OK && io.kind == H3C_UPD_WRITE && io.length)
+                     ? (io.length + kPieceBytes - 1) / kPieceBytes : 0u;
+    paycrc0[i] = 0;
+  } else if (i <= np_items) {  // chunk items (their t0 is known) and the scan's extra entry
+    npieces[i] = 0;
+  }
 }
 
 
@@ -519,6 +586,12 @@ __global__ void uio_frag_kernel(const OpPos *__restrict__ pos, const uint32_t *_
       if (d.w1 > d.w0) d.flags |= kFragCrc;
     }
     if (d.w1 > d.w0 || d.z1 > d.z0) d.flags |= kFragWrite;
+    if (r.pf & kPosFold) {  // the op's only fragment: its A6 check happens here
+      d.flags |= kFragA6;
+      d.op = r.op;
+      d.expect = io.checksum_value;
+      d.len = io.length;
+    }
   } else if (r.na < r.nb) {  // truncate: the cut bytes leave the CRC
     range(r.na, r.nb, d.q0, d.q1);
     if (d.q1 > d.q0) d.flags |= kFragCrc;
@@ -710,13 +783,41 @@ __device__ __forceinline__ void load_task_rows(uint64_t blk, uint32_t k0, uint32
   }
 }
 
+// The fold check's per-fragment inputs (kFragA6) and outputs.
+struct FoldIo {
+  uint32_t op, expect, len;
+  uint32_t std_domain;
+  const PolyConsts *pc;
+  uint32_t *payraw, *a6;
+};
+
 // One fragment on the block rows: its delta CRC (new ^ old) moved to its op's end goes to
 // eacc[p]; then its zero fill and new bytes are applied.  Returns the rows it wrote.
+// kFragA6 (a fold op): the payload's own CRC is folded beside the old bytes' (crc0 is linear:
+// crc0(new ^ old) = crc0(new) ^ crc0(old)), its raw value checked against the client's checksum
+// (ChunkReplica.cc:193-207, engine.rs:297-308); a failed op contributes nothing and writes nothing.
 __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 (&nw)[4], uint32_t flags, uint32_t w,
                                                    uint32_t q, uint32_t z, uint32_t mult, uint32_t p, uint32_t lane,
                                                    const char *lb, const LaneLut &L, const uint32_t *red, uint32_t poly,
-                                                   uint32_t *__restrict__ eacc) {
+                                                   uint32_t *__restrict__ eacc, const FoldIo &fx) {
   const uint32_t w0 = w & 0xFFFFu, w1 = w >> 16, q0 = q & 0xFFFFu, q1 = q >> 16, z0 = z & 0xFFFFu, z1 = z >> 16;
+  uint32_t vnew = 0;
+  if (flags & kFragA6) {
+    Streams sn{0, 0, 0, 0};  // the new bytes alone (one stream set at a time: registers are short)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) consume(sn, nw[r], lb, L);
+    vnew = wave_fold_tab(sn, lane, red);
+    // crc0(payload) = crc0(block image) * x^-(8 (4096 - w1)); raw = crc0 ^ ~0 * x^(8 len)
+    const uint32_t c0 = dgf_mul_fast(vnew, dxpow8_fast(-(int64_t)(kBlk - w1), fx.pc, poly), poly);
+    const uint32_t raw = c0 ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(fx.len, fx.pc, poly), poly);
+    const bool bad = (fx.std_domain ? ~raw : raw) != fx.expect;  // wave-uniform (lane 0's value)
+    const bool bad_u = __builtin_amdgcn_readfirstlane(bad ? 1 : 0) != 0;
+    if (lane == 0) {
+      fx.payraw[fx.op] = raw;
+      if (bad) fx.a6[fx.op] = 1u;
+    }
+    if (bad_u) return 0u;
+  }
   if (flags & kFragCrc) {
     Streams st{0, 0, 0, 0};
 #pragma unroll
@@ -759,7 +860,8 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
 __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frags, const uint32_t *__restrict__ d_F,
                                                uint32_t cap, const PolyConsts *__restrict__ pc,
                                                uint32_t *__restrict__ eacc, const uint32_t *__restrict__ misc,
-                                               uint32_t *lds) {
+                                               uint32_t *lds, uint32_t std_domain, uint32_t *__restrict__ payraw,
+                                               uint32_t *__restrict__ a6) {
   for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
   const uint32_t *red_g = &pc->red[0][0][0];
   for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
@@ -814,16 +916,25 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
       if (flags & kFragHead) {
         const uint64_t blk = rl64(m_blk, t);
         const uint32_t kk = rl(m_k, t), k0 = kk & 0xFFFFu, k1 = kk >> 16;
+        // a fold fragment's op / checksum / length: scalar loads of the record the lanes just read
+        FoldIo fx{0, 0, 0, std_domain, pc, payraw, a6};
+        if (flags & kFragA6) {
+          const FragDesc *dh = frags + (g0 + t);
+          fx.op = dh->op;
+          fx.expect = dh->expect;
+          fx.len = dh->len;
+        }
         uint32_t dirty = apply_fragment(cur.img, cur.nw, flags, rl(m_w, t), rl(m_q, t), rl(m_z, t), rl(m_mult, t),
-                                        rl(m_p, t), lane, lb, L, red, poly, eacc);
+                                        rl(m_p, t), lane, lb, L, red, poly, eacc, fx);
         for (uint32_t f = rl(m_next, t); f != kNil;) {  // later fragments of the same block
           const FragDesc d = frags[f];
           uint4 nw4[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) nw4[r] = load_new(d.src, r, 1024u * r + 16u * lane, d.w0, d.w1);
+          const FoldIo fd{d.op, d.expect, d.len, std_domain, pc, payraw, a6};
           dirty |= apply_fragment(cur.img, nw4, d.flags, (uint32_t)d.w0 | ((uint32_t)d.w1 << 16),
                                   (uint32_t)d.q0 | ((uint32_t)d.q1 << 16), (uint32_t)d.z0 | ((uint32_t)d.z1 << 16),
-                                  d.mult, d.p, lane, lb, L, red, poly, eacc);
+                                  d.mult, d.p, lane, lb, L, red, poly, eacc, fd);
           f = d.next;
         }
 #pragma unroll
@@ -841,18 +952,25 @@ __global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__r
                                                              const PolyConsts *__restrict__ pc,
                                                              uint32_t *__restrict__ eacc,
                                                              const uint32_t *__restrict__ misc,
-                                                             unsigned long long *ts) {
+                                                             unsigned long long *ts, uint32_t std_domain,
+                                                             uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6) {
   __shared__ uint32_t lds[kLdsWords + kRedWords];
   if (ts && threadIdx.x == 0) atomicMin(&ts[0], (unsigned long long)wall_clock64());
-  uio_block_body(frags, d_F, cap, pc, eacc, misc, lds);
+  uio_block_body(frags, d_F, cap, pc, eacc, misc, lds, std_domain, payraw, a6);
   if (ts) {  // one stamp per workgroup, once all its waves are done
     __syncthreads();
     if (threadIdx.x == 0) atomicMax(&ts[1], (unsigned long long)wall_clock64());
   }
 }
 
+// A fold op whose A6 check failed in the block kernel (it changed nothing).
+__device__ __forceinline__ bool fold_failed(const OpPos &r, const uint32_t *__restrict__ a6) {
+  return (r.pf & kPosFold) && a6[r.op];
+}
+
 __device__ __forceinline__ Aff t_map(const OpPos &r, const uint32_t *__restrict__ eacc, const uint32_t *__restrict__ payraw,
-                                     uint32_t p, const PolyConsts *__restrict__ pc) {
+                                     uint32_t p, const PolyConsts *__restrict__ pc, const uint32_t *__restrict__ a6) {
+  if (fold_failed(r, a6)) return Aff{kOne, 0u};
   if (r.tk == kT_DELTA) return Aff{dxpow8_fast((int64_t)r.na - (int64_t)r.nb, pc, pc->poly), eacc[p]};
   if (r.tk == kT_FULL) return Aff{0u, payraw[r.op]};
   return Aff{kOne, 0u};
@@ -863,7 +981,8 @@ struct TMapFn {
   const OpPos *pos;
   const uint32_t *eacc, *payraw;
   const PolyConsts *pc;
-  __device__ Aff operator()(uint32_t p) const { return t_map(pos[p], eacc, payraw, p, pc); }
+  const uint32_t *a6;
+  __device__ Aff operator()(uint32_t p) const { return t_map(pos[p], eacc, payraw, p, pc, a6); }
 };
 
 // s map per op position, from each op's t after it (the chunk's t0 through the t scan).
@@ -874,10 +993,11 @@ struct SMapFn {
   const Aff *tscan;
   const uint32_t *t0v, *eacc, *payraw;
   const PolyConsts *pc;
+  const uint32_t *a6;
   __device__ Aff operator()(uint32_t p) const {
     const OpPos r = pos[p];
     const uint32_t c = skey[p];
-    if (c >= nchunks) return Aff{kOne, 0u};
+    if (c >= nchunks || fold_failed(r, a6)) return Aff{kOne, 0u};
     switch (r.sk) {
       case kS_ZERO:
         return Aff{0u, 0u};
@@ -886,7 +1006,7 @@ struct SMapFn {
         return Aff{0u, hd_gf_mul(t0v[c], t.m, pc->poly) ^ t.e};
       }
       case kS_APPEND:
-        return t_map(r, eacc, payraw, p, pc);
+        return t_map(r, eacc, payraw, p, pc, a6);
       default:
         return Aff{kOne, 0u};
     }
@@ -907,7 +1027,7 @@ __global__ void uio_result_kernel(const OpPos *__restrict__ pos, const uint32_t 
                                   const uint32_t *__restrict__ t0v, uint8_t poly_type, uint32_t std_domain,
                                   uint32_t poly, h3c_update_result *__restrict__ res,
                                   unsigned long long *__restrict__ ctr, const uint32_t *__restrict__ d_F,
-                                  uint32_t *__restrict__ misc) {
+                                  uint32_t *__restrict__ misc, const uint32_t *__restrict__ a6) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p == 0) {  // the pass's outcome, for the host's one read-back
     misc[kMiscOutF] = *d_F;
@@ -915,8 +1035,9 @@ __global__ void uio_result_kernel(const OpPos *__restrict__ pos, const uint32_t 
   }
   uint32_t c_none = 0, c_reuse = 0, c_comb = 0, c_read = 0, c_recalc = 0, c_mis = 0, c_inv = 0;
   if (p < n) {
-    const OpPos r = pos[p];
+    OpPos r = pos[p];
     const uint32_t c = skey[p];
+    if (fold_failed(r, a6)) r.status = H3C_ERR_CHECKSUM_MISMATCH;  // checked in the block kernel
     h3c_update_result o{};
     o.status = r.status;
     const bool applied = r.status == H3C_OK && r.sk != kS_IDENT;
@@ -988,9 +1109,9 @@ __global__ void uio_verify_t0_kernel(const h3c_update_io *__restrict__ ios, uint
                                      const PolyConsts *__restrict__ pc, const uint32_t *__restrict__ status,
                                      uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6,
                                      uint32_t *__restrict__ misc, uint32_t *__restrict__ t0v,
-                                     h3c_chunk_state *__restrict__ chunks_out) {
+                                     h3c_chunk_state *__restrict__ chunks_out, uint32_t skip_cand) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) verify_op(i, ios, crc0, pc, std_domain, status, payraw, a6, misc);
+  if (i < n) verify_op(i, ios, crc0, pc, std_domain, status, payraw, a6, misc, skip_cand ? chunks : nullptr);
   if (i < nchunks) t0_chunk(i, chunks, poly_type, exact, std_domain, crc0 + n, pc, t0v, chunks_out);
 }
 
@@ -1372,7 +1493,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       std::max(std::max(std::max(sort_tmp, scan_tmp), std::max(szscan_tmp, ascan_tmp)), pscan_tmp);
   const size_t N1 = (size_t)n + 1, NP = (size_t)n + C;  // NP: piece-pass items (ops, then chunks)
   uint32_t *d_status, *d_key, *d_idx, *d_skey, *d_order, *d_np, *d_pbase, *d_paycrc0, *d_payraw, *d_nfrag, *d_fbase,
-      *d_eacc, *d_t0, *d_misc, *d_a6;
+      *d_eacc, *d_t0, *d_misc, *d_a6, *d_late, *d_lbase;
   SzTy *d_sz, *d_szscan;
   OpPos *d_pos;
   Aff *d_tel, *d_tscan, *d_sel, *d_sscan;
@@ -1391,6 +1512,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     d_a6 = carve<uint32_t>(cur, n);
     d_nfrag = carve<uint32_t>(cur, N1);
     d_fbase = carve<uint32_t>(cur, N1);
+    d_late = carve<uint32_t>(cur, N1);
+    d_lbase = carve<uint32_t>(cur, N1);
     d_eacc = carve<uint32_t>(cur, n);
     d_t0 = carve<uint32_t>(cur, C);
     d_misc = carve<uint32_t>(cur, kMiscN);
@@ -1423,6 +1546,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     size_t t = tmp_bytes;
     return rocprim::exclusive_scan(d_tmp, t, in, out, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), q);
   };
+  uint32_t nofold = 0;  // a redo after a failed A6 knows every verdict: no check moves into the block kernel
   // sizes and types per op (a segmented scan), the reference's cases, fragment counts
   auto phase_sizes = [&](hipStream_t q) -> int {
     hipLaunchKernelGGL(uio_sz_elem_kernel, dim3(gb), dim3(tb), 0, q, d_ios, d_order, n, d_status, poly_type, stdf,
@@ -1434,7 +1558,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                                              rocprim::equal_to<uint32_t>(), q));
     }
     hipLaunchKernelGGL(uio_classify_kernel, dim3(gb), dim3(tb), 0, q, d_ios, d_order, d_skey, n, d_chunks, nchunks,
-                       d_szscan, d_status, poly_type, stdf, d_pos, d_nfrag);
+                       d_szscan, d_status, poly_type, stdf, nofold, d_pos, d_nfrag, d_late);
     HIP_TRY(hipGetLastError());
     HIP_TRY(scan_excl(d_nfrag, d_fbase, q));
     return H3C_OK;
@@ -1464,10 +1588,27 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                                          d_paycrc0);
     if (r) return r;
     hipLaunchKernelGGL(uio_verify_t0_kernel, dim3(vb), dim3(tb), 0, aux->st, d_ios, n, d_chunks, nchunks, poly_type,
-                       exactf, stdf, d_paycrc0, pc, d_status, d_payraw, d_a6, d_misc, d_t0, d_chunks_out);
+                       exactf, stdf, d_paycrc0, pc, d_status, d_payraw, d_a6, d_misc, d_t0, d_chunks_out, 1u);
+    HIP_TRY(hipGetLastError());
+    r = phase_sizes(q);  // speculative: every A6 check passes (joined before the block kernel)
+    if (r) return r;
+    // second stream, after the cases are known: the late pass over the fold candidates that
+    // were not folded (each one piece), beside the fragment stage
+    HIP_TRY(hipEventRecord(aux->ready, q));
+    HIP_TRY(hipStreamWaitEvent(aux->st, aux->ready, 0));
+    {
+      size_t t = tmp_bytes;
+      HIP_TRY(rocprim::exclusive_scan(d_tmp, t, d_late, d_lbase, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(),
+                                      aux->st));
+    }
+    r = h3c_rt::launch_uio_piece_crc(aux->st, dev, poly_type, d_ios, n, d_chunks, 0, d_lbase, d_lbase + n,
+                                     d_paycrc0);
+    if (r) return r;
+    hipLaunchKernelGGL(uio_late_verify_kernel, dim3(gb), dim3(tb), 0, aux->st, d_ios, n, d_late, d_paycrc0, pc, stdf,
+                       d_status, d_payraw, d_a6, d_misc);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(aux->done, aux->st));
-    return phase_sizes(q);  // speculative: every A6 check passes (joined before the block kernel)
+    return H3C_OK;
   };
 
   // ---- fragments, blocks, scans, results (redone once if the fragment guess was short) ----
@@ -1511,8 +1652,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       return H3C_OK;
     };
     auto phase_b = [&](hipStream_t q) -> int {  // t' per op, then s' per op (two affine scans by chunk), results
-      hipLaunchKernelGGL(uio_elem_kernel<TMapFn>, dim3(gb), dim3(tb), 0, q, TMapFn{d_pos, d_eacc, d_payraw, pc}, n,
-                         d_tel);
+      hipLaunchKernelGGL(uio_elem_kernel<TMapFn>, dim3(gb), dim3(tb), 0, q, TMapFn{d_pos, d_eacc, d_payraw, pc, d_a6},
+                         n, d_tel);
       HIP_TRY(hipGetLastError());
       {
         size_t t = tmp_bytes;
@@ -1520,7 +1661,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                                                rocprim::equal_to<uint32_t>(), q));
       }
       hipLaunchKernelGGL(uio_elem_kernel<SMapFn>, dim3(gb), dim3(tb), 0, q,
-                         SMapFn{d_pos, d_skey, nchunks, d_tscan, d_t0, d_eacc, d_payraw, pc}, n, d_sel);
+                         SMapFn{d_pos, d_skey, nchunks, d_tscan, d_t0, d_eacc, d_payraw, pc, d_a6}, n, d_sel);
       HIP_TRY(hipGetLastError());
       {
         size_t t = tmp_bytes;
@@ -1528,7 +1669,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                                                rocprim::equal_to<uint32_t>(), q));
       }
       hipLaunchKernelGGL(uio_result_kernel, dim3(gb), dim3(tb), 0, q, d_pos, d_skey, n, d_sscan, d_chunks,
-                         d_chunks_out, nchunks, d_t0, poly_type, stdf, poly, d_res, d_ctr, d_F, d_misc);
+                         d_chunks_out, nchunks, d_t0, poly_type, stdf, poly, d_res, d_ctr, d_F, d_misc, d_a6);
       HIP_TRY(hipGetLastError());
       if (exact && nchunks) {
         hipLaunchKernelGGL(uio_stale_kernel, dim3((nchunks + tb - 1) / tb), dim3(tb), 0, q, d_chunks, nchunks, d_t0,
@@ -1547,7 +1688,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     const uint32_t blocks = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
     auto block_kernel = [&](hipStream_t q, bool timed) -> int {
       hipLaunchKernelGGL(uio_block_kernel, dim3(blocks), dim3(kThreads), 0, q, d_frag, d_F, cap, pc, d_eacc, d_misc,
-                         timed ? reinterpret_cast<unsigned long long *>(d_misc + kMiscT0) : nullptr);
+                         timed ? reinterpret_cast<unsigned long long *>(d_misc + kMiscT0) : nullptr, stdf, d_payraw,
+                         d_a6);
       HIP_TRY(hipGetLastError());
       return H3C_OK;
     };
@@ -1624,11 +1766,27 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       return H3C_ERR_HIP;
     }
     // nothing was written (no chain ran): redo, with the count known and, after a failed A6,
-    // the sizes / cases / fragment counts recomputed from the real verdicts (F can only shrink)
+    // the sizes / cases / fragment counts recomputed from the real verdicts (F can only shrink).
+    // A failed A6 came from the piece passes; the fold candidates' own checks never ran, so every
+    // typed WRITE is checked again first and the redo moves no check into the block kernel.
     cap = std::max(cap, F);
     if (a6_failed) {
+      hipLaunchKernelGGL(uio_redo_pieces_kernel, dim3((uint32_t)((NP + 1 + tb - 1) / tb)), dim3(tb), 0, st, d_ios, n,
+                         (uint32_t)NP, d_status, d_np, d_paycrc0);
+      HIP_TRY(hipGetLastError());
+      {
+        size_t t = tmp_bytes;
+        HIP_TRY(rocprim::exclusive_scan(d_tmp, t, d_np, d_pbase, 0u, NP + 1, rocprim::plus<uint32_t>(), st));
+      }
+      rc = h3c_rt::launch_uio_piece_crc(st, dev, poly_type, d_ios, n, d_chunks, nchunks, d_pbase, d_pbase + NP,
+                                        d_paycrc0);
+      if (rc) return rc;
+      hipLaunchKernelGGL(uio_verify_t0_kernel, dim3(vb), dim3(tb), 0, st, d_ios, n, d_chunks, nchunks, poly_type,
+                         exactf, stdf, d_paycrc0, pc, d_status, d_payraw, d_a6, d_misc, d_t0, d_chunks_out, 0u);
+      HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(uio_merge_a6_kernel, dim3(gb), dim3(tb), 0, st, d_a6, n, d_status, d_misc);
       HIP_TRY(hipGetLastError());
+      nofold = 1;
       rc = phase_sizes(st);
       if (rc) return rc;
     }
