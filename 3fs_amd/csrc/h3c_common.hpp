@@ -118,7 +118,8 @@ constexpr uint32_t kFlagNone = 1u;
 // start and row-aligned addresses (uniform_for): seg_uni_kernel.  contiguous: chunk i at
 // base + i * stride with result i, no descriptor reads.
 struct UniformBatch {
-  uint32_t lanes = 0;  // 4 or 16 lanes per chunk; 0: not uniform
+  uint32_t lanes = 0;  // 4, 8 or 16 lanes per chunk; 0: not uniform
+  bool pair = false;   // 8 lanes walk two chunks each (seg_uni_kernel<8, 2>)
   uint32_t rows = 0;   // rows of 16 * lanes bytes per chunk
   uint32_t xs = 0;     // the shared start's share of the raw CRC
   bool contiguous = false;

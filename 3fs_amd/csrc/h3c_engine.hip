@@ -285,6 +285,9 @@ constexpr int kUniLdsWords = kUniCopies == 16 ? kLdsWords16 : kLdsWords;
 #ifndef H3C_UNI_LANES_HI
 #define H3C_UNI_LANES_HI 16
 #endif
+#ifndef H3C_UNI_PAIR
+#define H3C_UNI_PAIR 1  // uniform chunks of <= 6 rows, 128-byte multiples: 8 lanes x 2 chunks (0: 4 lanes x 1)
+#endif
 
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
 
@@ -460,7 +463,11 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
 // count K is the same for every chunk (loop control stays scalar) and the start's share xs is
 // one value.  With chunks == nullptr the batch is contiguous (chunk i at base + i * stride,
 // result i): no descriptor at all.
-template <int G>
+// C chunks per group of G lanes: with C = 2 an 8-lane group walks two chunks in interleaved
+// rows, so every load instruction reads whole 128-byte lines (the 8-lane access pattern alone
+// reads at ~7.0 TB/s against ~6.1 TB/s for 4 lanes' 64-byte rows) while a wave step still
+// covers 16 chunks and their folds overlap (profiles/r02_small_pattern_ceiling.txt).
+template <int G, int C = 1>
 __global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni_kernel(const DevChunk *__restrict__ chunks, uint64_t base,
                                                           uint64_t stride, uint32_t nchunks, uint32_t K, uint32_t xs,
                                                           const PolyConsts *__restrict__ pc,
@@ -468,8 +475,10 @@ __global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni
                                                           uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
                                                           uint32_t *__restrict__ mismatch) {
   static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "1, 2, 4, 8 or 16 lanes per chunk");
+  static_assert(C == 1 || C == 2, "one or two chunks per group");
   constexpr int kLevels = G == 16 ? 4 : G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
   constexpr uint32_t NG = 64 / G;
+  constexpr uint32_t kStep = NG * C;  // chunks per wave step
   constexpr int kRed = (1 + kLevels) * 1024;
   constexpr uint64_t kQ = 16u * G;
   __shared__ uint32_t lds[kUniLdsWords + kRed];
@@ -483,7 +492,7 @@ __global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni
   for (int i = threadIdx.x; i < kRed; i += kUniThreads) lds[kUniLdsWords + i] = red_g[i];
   const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
 #if H3C_UNI_DYNAMIC
-  // The workgroup owns a contiguous range; its waves take steps of NG chunks from an LDS
+  // The workgroup owns a contiguous range; its waves take steps of kStep chunks from an LDS
   // counter, so a wave slowed by its neighbours does not leave the others idle at the end
   // (a static split per wave kept waves alive 81 % of the kernel at 8 lanes per chunk).
   const uint32_t wlo = (uint32_t)((uint64_t)blockIdx.x * nchunks / gridDim.x);
@@ -492,7 +501,7 @@ __global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni
   __syncthreads();
   auto grab = [&]() -> uint32_t {
     uint32_t q = 0;
-    if (lane == 0) q = atomicAdd(&wg_next, NG);
+    if (lane == 0) q = atomicAdd(&wg_next, kStep);
     return (uint32_t)__builtin_amdgcn_readfirstlane(q);
   };
   const uint32_t lo = grab();
@@ -507,10 +516,10 @@ __global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni
   const uint32_t *red = lds + kUniLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
   const LaneLut L = kUniCopies == 16 ? make_lut16(lane) : make_lut(lane);
-  // quad q (chunks q .. q + NG - 1; this group's is q + grp): its first row address for this
-  // lane, its result index and expected value
-  auto quad = [&](uint32_t q, uint64_t &la, uint32_t &o, uint32_t &want, bool &valid) {
-    const uint32_t t = q + grp;
+  // step q (chunks q .. q + kStep - 1; this group's j-th is q + grp + j * NG): its first row
+  // address for this lane, its result index and expected value
+  auto quad = [&](uint32_t q, uint32_t j, uint64_t &la, uint32_t &o, uint32_t &want, bool &valid) {
+    const uint32_t t = q + grp + j * NG;
     valid = t < hi;
     uint64_t p = 0;
     o = t;
@@ -525,69 +534,102 @@ __global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni
     la = p + 16u * gl;
     want = valid && expected ? expected[o] : 0u;
   };
-  uint64_t la;
-  uint32_t o, want;
-  bool valid;
-  quad(lo, la, o, want, valid);
-  uint4 cur[kUniBatch], nxt[kUniBatch];
+  uint64_t la[C];
+  uint32_t o[C], want[C];
+  bool valid[C];
 #pragma unroll
-  for (int b = 0; b < kUniBatch; ++b)
-    cur[b] = valid && (uint32_t)b < K ? load_row(la + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+  for (int j = 0; j < C; ++j) quad(lo, j, la[j], o[j], want[j], valid[j]);
+  uint4 cur[C][kUniBatch], nxt[C][kUniBatch];
+#pragma unroll
+  for (int j = 0; j < C; ++j)
+#pragma unroll
+    for (int b = 0; b < kUniBatch; ++b)
+      cur[j][b] = valid[j] && (uint32_t)b < K ? load_row(la[j] + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
 #if H3C_UNI_DYNAMIC
   for (uint32_t q0 = lo; q0 < hi;) {
     const uint32_t qn = grab();  // the next step, taken now so its rows load during this one's last batch
 #else
-  for (uint32_t q0 = lo; q0 < hi; q0 += NG) {
-    const uint32_t qn = q0 + NG;
+  for (uint32_t q0 = lo; q0 < hi; q0 += kStep) {
+    const uint32_t qn = q0 + kStep;
 #endif
-    uint64_t la1 = la;
-    uint32_t o1 = o, want1 = want;
-    bool valid1 = false;
-    if (qn < hi) quad(qn, la1, o1, want1, valid1);  // its rows load during this quad's last batch
-    Streams st{0, 0, 0, 0};
+    uint64_t la1[C];
+    uint32_t o1[C], want1[C];
+    bool valid1[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      la1[j] = la[j];
+      o1[j] = o[j];
+      want1[j] = want[j];
+      valid1[j] = false;
+      if (qn < hi) quad(qn, j, la1[j], o1[j], want1[j], valid1[j]);  // its rows load during this step's last batch
+    }
+    Streams st[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) st[j] = Streams{0, 0, 0, 0};
     for (uint32_t u0 = 0; u0 < K; u0 += kUniBatch) {
       const uint32_t n0 = u0 + kUniBatch;
       if (n0 < K) {
 #pragma unroll
         for (int b = 0; b < kUniBatch; ++b)
-          nxt[b] = valid && n0 + b < K ? load_row(la + (uint64_t)(n0 + b) * kQ) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < C; ++j)
+            nxt[j][b] = valid[j] && n0 + b < K ? load_row(la[j] + (uint64_t)(n0 + b) * kQ) : make_uint4(0, 0, 0, 0);
       } else {
 #pragma unroll
         for (int b = 0; b < kUniBatch; ++b)
-          nxt[b] = valid1 && (uint32_t)b < K ? load_row(la1 + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < C; ++j)
+            nxt[j][b] = valid1[j] && (uint32_t)b < K ? load_row(la1[j] + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int b = 0; b < kUniBatch; ++b)
         if (u0 + b < K) {
-          if constexpr (kUniCopies == 16)
-            consume16(st, cur[b], lb, L);
-          else
-            consume(st, cur[b], lb, L);
+#pragma unroll
+          for (int j = 0; j < C; ++j) {
+            if constexpr (kUniCopies == 16)
+              consume16(st[j], cur[j][b], lb, L);
+            else
+              consume(st[j], cur[j][b], lb, L);
+          }
         }
 #pragma unroll
-      for (int b = 0; b < kUniBatch; ++b) cur[b] = nxt[b];
+      for (int j = 0; j < C; ++j)
+#pragma unroll
+        for (int b = 0; b < kUniBatch; ++b) cur[j][b] = nxt[j][b];
     }
-    uint32_t p = tab_mul(st.s3, red) ^ st.s2;
-    p = tab_mul(p, red) ^ st.s1;
-    uint32_t v = tab_mul(p, red) ^ st.s0;
+    uint32_t v[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) v[j] = tab_mul(st[j].s3, red) ^ st[j].s2;
+#pragma unroll
+    for (int j = 0; j < C; ++j) v[j] = tab_mul(v[j], red) ^ st[j].s1;
+#pragma unroll
+    for (int j = 0; j < C; ++j) v[j] = tab_mul(v[j], red) ^ st[j].s0;
 #pragma unroll
     for (int k = 0; k < kLevels; ++k) {
-      const uint32_t x = (uint32_t)__shfl_down((int)v, 1u << k, G);
-      if ((gl & ((2u << k) - 1u)) == 0) v ^= tab_mul(x, red + 1024 * (k + 1));
-    }
-    if (gl == 0 && valid) {
-      const uint32_t raw = v ^ xs;
-      out_raw[o] = raw;
-      if (expected) {
-        const bool good = raw == want;
-        ok[o] = good ? 1 : 0;
-        if (!good && mismatch) atomicAdd(mismatch, 1u);
+      uint32_t x[C];
+#pragma unroll
+      for (int j = 0; j < C; ++j) x[j] = (uint32_t)__shfl_down((int)v[j], 1u << k, G);
+      if ((gl & ((2u << k) - 1u)) == 0) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) v[j] ^= tab_mul(x[j], red + 1024 * (k + 1));
       }
     }
-    la = la1;
-    o = o1;
-    want = want1;
-    valid = valid1;
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      if (gl == 0 && valid[j]) {
+        const uint32_t raw = v[j] ^ xs;
+        out_raw[o[j]] = raw;
+        if (expected) {
+          const bool good = raw == want[j];
+          ok[o[j]] = good ? 1 : 0;
+          if (!good && mismatch) atomicAdd(mismatch, 1u);
+        }
+      }
+      la[j] = la1[j];
+      o[j] = o1[j];
+      want[j] = want1[j];
+      valid[j] = valid1[j];
+    }
 #if H3C_UNI_DYNAMIC
     q0 = qn;
 #endif
@@ -1094,6 +1136,9 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
       else if (uni->lanes == 4)
         hipLaunchKernelGGL(seg_uni_kernel<4>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
                            nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+      else if (uni->lanes == 8 && uni->pair)
+        hipLaunchKernelGGL((seg_uni_kernel<8, 2>), dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
       else if (uni->lanes == 8)
         hipLaunchKernelGGL(seg_uni_kernel<8>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
                            nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
@@ -1186,8 +1231,15 @@ uint64_t pick_seg(uint64_t total_bytes, int dev) { return pick_seg_bytes(total_b
 void uniform_for(const DevChunk *c, size_t n, uint32_t small_rows, UniformBatch &u) {
   u = UniformBatch{};
   if (!n || !small_rows) return;
-  const uint32_t lanes = small_rows <= 6 ? H3C_UNI_LANES_LO : H3C_UNI_LANES_HI;
+  uint32_t lanes = small_rows <= 6 ? H3C_UNI_LANES_LO : H3C_UNI_LANES_HI;
   if (lanes != 1 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16) return;
+  // short chunks whose rows are whole 128-byte lines: 8 lanes, two chunks per group
+  bool pair = false;
+  if (H3C_UNI_PAIR && lanes == 4 && c[0].len && c[0].len % 128 == 0) {
+    pair = true;
+    for (size_t i = 0; i < n && pair; ++i) pair = c[i].ptr % 128 == 0;
+    if (pair) lanes = 8;
+  }
   const uint64_t row = 16u * lanes, len = c[0].len;
   if (!len || len % row) return;
   const uint64_t stride = n > 1 ? c[1].ptr - c[0].ptr : len;
@@ -1197,6 +1249,7 @@ void uniform_for(const DevChunk *c, size_t n, uint32_t small_rows, UniformBatch 
     contiguous = contiguous && c[i].out_idx == i && c[i].ptr == c[0].ptr + i * stride;
   }
   u.lanes = lanes;
+  u.pair = pair;
   u.rows = (uint32_t)(len / row);
   u.xs = c[0].xstart;
   u.contiguous = contiguous;
