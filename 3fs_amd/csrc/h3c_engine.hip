@@ -1737,6 +1737,8 @@ struct Coalescer {
 };
 Coalescer g_coal[kMaxDevices];
 
+constexpr size_t kMergeMax = 1u << 20;  // descriptors per merged batch
+
 void run_merged(std::vector<SyncReq *> &b) {
   if (b.size() == 1) {
     SyncReq &r = *b[0];
@@ -1757,9 +1759,13 @@ void run_merged(std::vector<SyncReq *> &b) {
     if (r->expected) std::copy_n(r->expected, r->n, exp.begin() + dd.size());  // creates verify against 0
     dd.insert(dd.end(), r->d, r->d + r->n);
   }
-  const int rc = total > 0xFFFFFFF0u ? H3C_ERR_INVALID_ARG
-                                     : batch_sync(dd.data(), total, verify ? exp.data() : nullptr, nullptr, raw.data(),
-                                                  verify ? ok.data() : nullptr, nullptr, nullptr);
+  const int rc = batch_sync(dd.data(), total, verify ? exp.data() : nullptr, nullptr, raw.data(),
+                            verify ? ok.data() : nullptr, nullptr, nullptr);
+  if (rc != H3C_OK) {  // one caller's bad descriptor (or a HIP error) must not fail the others:
+    for (SyncReq *r : b)  // each request again on its own, with its own status
+      r->rc = batch_sync(r->d, r->n, r->expected, r->out_type, r->out_raw, r->ok, r->n_mismatch, nullptr);
+    return;
+  }
   size_t at = 0;
   for (SyncReq *r : b) {
     r->rc = rc;
@@ -1798,8 +1804,14 @@ int submit_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uint8_t *
       // the leader also runs the batch that queued behind its own (once), so the device is
       // not idle while a woken waiter gets scheduled
       for (int round = 0; round < 2 && !q.pending.empty(); ++round) {
+        // at most kMergeMax descriptors per merged batch (the rest waits for the next one), so a
+        // merged batch stays within the per-call limits every request met on its own
         std::vector<SyncReq *> batch;
-        batch.swap(q.pending);
+        size_t taken = 0, total = 0;
+        while (taken < q.pending.size() && (taken == 0 || total + q.pending[taken]->n <= kMergeMax))
+          total += q.pending[taken++]->n;
+        batch.assign(q.pending.begin(), q.pending.begin() + (long)taken);
+        q.pending.erase(q.pending.begin(), q.pending.begin() + (long)taken);
         lk.unlock();
         run_merged(batch);
         lk.lock();

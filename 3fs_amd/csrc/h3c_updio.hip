@@ -1145,24 +1145,6 @@ struct AuxStream {
   hipStream_t st = nullptr;
   hipEvent_t ready = nullptr, done = nullptr;
 };
-int aux_stream(int dev, AuxStream *&out) {
-  thread_local AuxStream aux[4];
-  thread_local int next = 0;
-  for (AuxStream &a : aux)
-    if (a.dev == dev && a.st) {
-      out = &a;
-      return H3C_OK;
-    }
-  AuxStream &a = aux[next++ & 3];  // a thread using more than 4 devices recycles (leaks) the oldest
-  a = AuxStream{};
-  HIP_TRY(hipStreamCreateWithFlags(&a.st, hipStreamNonBlocking));
-  HIP_TRY(hipEventCreateWithFlags(&a.ready, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
-  a.dev = dev;
-  out = &a;
-  return H3C_OK;
-}
-
 template <class T>
 T *carve(char *&p, size_t count) {
   T *r = reinterpret_cast<T *>(p);
@@ -1344,11 +1326,88 @@ struct UpdGraphs {
 // shape seen among the last four plain calls returns an empty entry to capture into; later
 // sights replay.  Graphs are not
 // used while `st` itself is being captured, or with h3c_test_hook(H3C_HOOK_UPD_GRAPHS, 1).
+// Per-thread HIP resources -- the aux stream sets, the capture streams, the graph cache.  When a
+// thread ends they go back to process-wide pools (no HIP call in a thread-exit destructor) and the
+// next thread that needs one on the same device takes it from there; graph execs of ended threads
+// are destroyed by the next update call.  A caller that spawns short-lived threads therefore
+// reuses a bounded set of streams instead of leaking them.
+struct ResPool {
+  std::mutex mu;
+  std::vector<AuxStream> aux;
+  std::vector<std::pair<int, hipStream_t>> cap;
+  std::vector<hipGraphExec_t> dead;
+};
+ResPool g_res;
+
+struct ThreadRes {
+  AuxStream aux[4];
+  int aux_next = 0;
+  hipStream_t cs[8] = {};
+  int cs_dev[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  UpdGraphs cache[4];
+  UpdGraphKey recent[4] = {};  // keys of the last plain calls (lease pools may alternate buffers)
+  uint32_t recent_next = 0;
+  uint64_t tick = 0;
+  ~ThreadRes() {
+    std::lock_guard<std::mutex> lk(g_res.mu);
+    for (AuxStream &a : aux)
+      if (a.st) g_res.aux.push_back(a);
+    for (int i = 0; i < 8; ++i)
+      if (cs[i]) g_res.cap.emplace_back(cs_dev[i], cs[i]);
+    for (UpdGraphs &g : cache)
+      if (g.g) g_res.dead.push_back(g.g);
+  }
+};
+ThreadRes &tres() {
+  thread_local ThreadRes r;
+  return r;
+}
+
+void drain_dead_graphs() {
+  std::vector<hipGraphExec_t> dead;
+  {
+    std::lock_guard<std::mutex> lk(g_res.mu);
+    dead.swap(g_res.dead);
+  }
+  for (hipGraphExec_t g : dead) (void)hipGraphExecDestroy(g);
+}
+
+// A second stream per calling thread and device (and its fork / join events).
+int aux_stream(int dev, AuxStream *&out) {
+  ThreadRes &tr = tres();
+  for (AuxStream &a : tr.aux)
+    if (a.dev == dev && a.st) {
+      out = &a;
+      return H3C_OK;
+    }
+  AuxStream &a = tr.aux[tr.aux_next++ & 3];
+  {
+    std::lock_guard<std::mutex> lk(g_res.mu);
+    if (a.st) g_res.aux.push_back(a);  // a thread using more than 4 devices hands the oldest back
+    a = AuxStream{};
+    for (size_t i = 0; i < g_res.aux.size(); ++i)
+      if (g_res.aux[i].dev == dev) {
+        a = g_res.aux[i];
+        g_res.aux.erase(g_res.aux.begin() + (long)i);
+        break;
+      }
+  }
+  if (!a.st) {
+    HIP_TRY(hipStreamCreateWithFlags(&a.st, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&a.ready, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
+    a.dev = dev;
+  }
+  out = &a;
+  return H3C_OK;
+}
+
 UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st, bool asked) {
-  thread_local UpdGraphs cache[4];
-  thread_local UpdGraphKey recent[4] = {};  // keys of the last plain calls (lease pools may alternate buffers)
-  thread_local uint32_t recent_next = 0;
-  thread_local uint64_t tick = 0;
+  ThreadRes &tr = tres();
+  UpdGraphs(&cache)[4] = tr.cache;
+  UpdGraphKey(&recent)[4] = tr.recent;
+  uint32_t &recent_next = tr.recent_next;
+  uint64_t &tick = tr.tick;
   // Only when the caller asks (H3C_UPD_GRAPHS): a launch into the legacy default stream made by
   // ANY thread of the process while a stream is capturing fails in HIP ("operation not permitted
   // when stream is capturing") and invalidates the capture, whatever the capture mode or the
@@ -1405,18 +1464,26 @@ UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st, bool asked) {
 // A per-thread, per-device stream to capture on: the caller's stream may be the legacy
 // default stream, which cannot be captured (a graph then launches on it all the same).
 hipStream_t capture_stream(int dev) {
-  thread_local hipStream_t cs[8] = {};
-  thread_local int cs_dev[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  ThreadRes &tr = tres();
   for (int i = 0; i < 8; ++i)
-    if (cs_dev[i] == dev && cs[i]) return cs[i];
+    if (tr.cs_dev[i] == dev && tr.cs[i]) return tr.cs[i];
   for (int i = 0; i < 8; ++i)
-    if (!cs[i]) {
-      if (hipStreamCreateWithFlags(&cs[i], hipStreamNonBlocking) != hipSuccess) {
-        cs[i] = nullptr;
+    if (!tr.cs[i]) {
+      {
+        std::lock_guard<std::mutex> lk(g_res.mu);
+        for (size_t k = 0; k < g_res.cap.size(); ++k)
+          if (g_res.cap[k].first == dev) {
+            tr.cs[i] = g_res.cap[k].second;
+            g_res.cap.erase(g_res.cap.begin() + (long)k);
+            break;
+          }
+      }
+      if (!tr.cs[i] && hipStreamCreateWithFlags(&tr.cs[i], hipStreamNonBlocking) != hipSuccess) {
+        tr.cs[i] = nullptr;
         return nullptr;
       }
-      cs_dev[i] = dev;
-      return cs[i];
+      tr.cs_dev[i] = dev;
+      return tr.cs[i];
     }
   return nullptr;
 }
@@ -1467,6 +1534,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   const bool std_domain = (flags & H3C_UPD_STD_DOMAIN) != 0;
   const bool exact = (flags & H3C_UPD_EXACT) != 0;
   flags &= H3C_UPD_STD_DOMAIN | H3C_UPD_EXACT | H3C_UPD_GRAPHS;
+  drain_dead_graphs();
   const PolyConsts *pc = static_cast<const PolyConsts *>(h3c_rt::device_consts(dev, poly_type));
   const uint32_t poly = poly_type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
   const uint32_t stdf = std_domain ? 1u : 0u, exactf = exact ? 1u : 0u;

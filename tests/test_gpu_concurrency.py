@@ -185,6 +185,52 @@ def test_coalescing_queue_many_threads(h3c, torch_dev):
         assert not errors, (on, errors[:5])
 
 
+def test_coalescing_isolates_a_failing_caller(h3c, torch_dev):
+    """with coalescing on, one caller's bad request (a device descriptor that runs past
+    its allocation -> kInvalidArg) fails that caller only; the requests merged with it still get
+    their own correct results."""
+    import ctypes
+
+    torch, dev = torch_dev
+    nthreads, rounds = 24, 8
+    rng = np.random.default_rng(19)
+    host = [rng.integers(0, 256, int(rng.integers(1, 64 << 10)), dtype=np.uint8) for _ in range(nthreads)]
+    want = [orc.crc32c(d) for d in host]
+    big = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
+    bad = np.zeros(1, dtype=h3c.engine.DESC_DTYPE)
+    bad["ptr"] = big.data_ptr() + (1 << 19)
+    bad["len"] = 400 << 30  # beyond any HBM: rejected before launch
+    bad["start_raw"] = 0xFFFFFFFF
+    bad["type"] = 1
+    h3c.set_coalescing(True)
+    errors = []
+    start = threading.Barrier(nthreads)
+
+    def work(k):
+        try:
+            start.wait()
+            for it in range(rounds):
+                if k % 6 == 0 and it % 2 == 0:
+                    out_t, out_v = np.zeros(1, dtype=np.uint8), np.zeros(1, dtype=np.uint32)
+                    rc = h3c.engine.lib.h3c_batch_create(bad.ctypes.data, 1, out_t.ctypes.data, out_v.ctypes.data, None)
+                    if rc != h3c.StatusCode.kInvalidArg:
+                        errors.append((k, it, "bad request rc", rc))
+                else:
+                    t, v = h3c.batch_create([host[k]])
+                    if int(v[0]) != want[k]:
+                        errors.append((k, it, "create"))
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    threads = [threading.Thread(target=work, args=(k,)) for k in range(nthreads)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    h3c.set_coalescing(False)
+    assert not errors, errors[:5]
+
+
 def test_sync_bench_driver(h3c, torch_dev):
     """h3c_diag_sync_bench returns one latency per call and flags no mismatch (it checks every
     result against the buffer's own create)."""
