@@ -314,16 +314,11 @@ __global__ void uio_merge_a6_kernel(const uint32_t *__restrict__ a6, uint32_t n,
   if (i < n && a6[i] && status[i] == H3C_OK) status[i] = H3C_ERR_CHECKSUM_MISMATCH;
 }
 
-// The size / type map of each op, in sorted order.
-__global__ void uio_sz_elem_kernel(const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ order, uint32_t n,
-                                   const uint32_t *__restrict__ status, uint8_t poly_type, uint32_t std_domain,
-                                   SzTy *__restrict__ el) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const uint32_t i = order[p];
-  const h3c_update_io io = ios[i];
+// The size / type map of one op.
+__device__ __forceinline__ SzTy sz_elem_of(const h3c_update_io &io, uint32_t st, uint8_t poly_type,
+                                           uint32_t std_domain) {
   SzTy e{0, 0, 0, 0, 0};
-  if (status[i] == H3C_OK && applied_kind(io.kind)) {
+  if (st == H3C_OK && applied_kind(io.kind)) {
     switch (io.kind) {
       case H3C_UPD_WRITE:  // doRealWrite (:122-124); a syncing write sets meta.size = length (:289)
         if (io.flags & H3C_IO_SYNCING) {
@@ -354,45 +349,40 @@ __global__ void uio_sz_elem_kernel(const h3c_update_io *__restrict__ ios, const 
       e.t = poly_type;
     }
   }
-  el[p] = e;
+  return e;
+}
+
+// The size / type map of each op, in sorted order.
+__global__ void uio_sz_elem_kernel(const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ order, uint32_t n,
+                                   const uint32_t *__restrict__ status, uint8_t poly_type, uint32_t std_domain,
+                                   SzTy *__restrict__ el) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t i = order[p];
+  el[p] = sz_elem_of(ios[i], status[i], poly_type, std_domain);
 }
 
 __device__ __forceinline__ uint32_t blocks_of(uint64_t base, uint32_t r0, uint32_t r1) {
   return r1 > r0 ? (uint32_t)(((base + r1 - 1) >> 12) - ((base + r0) >> 12) + 1) : 0u;
 }
 
-// The reference's case analysis per op (ChunkReplica.cc:246, 319-394; engine.rs:375-423 and
-// chunk.rs:89-281 in the std domain), the maps' kinds, and the op's fragment range.
-__global__ void uio_classify_kernel(const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ order,
-                                    const uint32_t *__restrict__ skey, uint32_t n, const h3c_chunk_state *__restrict__ chunks,
-                                    uint32_t nchunks, const SzTy *__restrict__ scan, const uint32_t *__restrict__ status,
-                                    uint8_t poly_type, uint32_t std_domain, uint32_t nofold, OpPos *__restrict__ pos,
-                                    uint32_t *__restrict__ nfrag, uint32_t *__restrict__ late) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) {
-    if (p == n) nfrag[n] = late[n] = 0;
-    return;
-  }
-  const uint32_t i = order[p], c = skey[p];
-  const h3c_update_io io = ios[i];
-  OpPos r{};
+// The reference's case analysis for op i at sorted position p of chunk c (ChunkReplica.cc:246,
+// 319-394; engine.rs:375-423 and chunk.rs:89-281 in the std domain), the maps' kinds, and the
+// op's fragment range.  `ex` / `in` are the size / type maps of the chunk's ops before it and
+// through it (identity: SzTy{}).  Returns the op's fragment count; *late: a fold candidate whose
+// A6 check must happen before the block kernel.
+__device__ __forceinline__ uint32_t classify_op(const h3c_update_io &io, uint32_t i, uint32_t st, uint32_t c,
+                                                uint32_t nchunks, const h3c_chunk_state &cs, const SzTy &ex,
+                                                const SzTy &in, uint8_t poly_type, uint32_t std_domain,
+                                                uint32_t nofold, OpPos &r, bool &late) {
+  r = OpPos{};
   r.op = i;
-  r.status = status[i];
-  if (c >= nchunks) {  // names no chunk of the batch
-    pos[p] = r;
-    nfrag[p] = 0;
-    late[i] = 0;
-    return;
-  }
-  const h3c_chunk_state cs = chunks[c];
-  uint32_t nb = cs.size, tb = cs.type;
-  if (p > 0 && skey[p - 1] == c) {
-    const SzTy b = scan[p - 1];
-    nb = b.cst ? b.v : (cs.size > b.v ? cs.size : b.v);
-    if (b.tset) tb = b.t;
-  }
-  const SzTy a = scan[p];
-  const uint32_t na_scan = a.cst ? a.v : (cs.size > a.v ? cs.size : a.v);
+  r.status = st;
+  late = false;
+  if (c >= nchunks) return 0;  // names no chunk of the batch
+  const uint32_t nb = ex.cst ? ex.v : (cs.size > ex.v ? cs.size : ex.v);
+  const uint32_t tb = ex.tset ? ex.t : cs.type;
+  const uint32_t na_scan = in.cst ? in.v : (cs.size > in.v ? cs.size : in.v);
   r.nb = nb;
   r.na = nb;
   r.tb = (uint8_t)tb;
@@ -492,13 +482,34 @@ __global__ void uio_classify_kernel(const h3c_update_io *__restrict__ ios, const
     }
   }
   // A6 of a fold candidate: in the block kernel when the op is local (keeps size and stored type),
-  // else in the late piece pass (late[op] = its one piece); nofold: every verdict is known already
+  // else before it (late); nofold: every verdict is known already
   const bool cand = !nofold && fold_candidate(io, cs, r.status);
   const bool fold = cand && r.na == r.nb && r.ta == r.tb && r.tk != kT_IDENT;
   r.pf = fold ? kPosFold : 0;
-  late[i] = cand && !fold ? 1u : 0u;
+  late = cand && !fold;
+  return r.tk == kT_IDENT ? 0u : blocks_of(cs.base, r.r0, r.r1);
+}
+
+// classify_op over the sorted positions, from the segmented scan of the size / type maps.
+__global__ void uio_classify_kernel(const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ order,
+                                    const uint32_t *__restrict__ skey, uint32_t n, const h3c_chunk_state *__restrict__ chunks,
+                                    uint32_t nchunks, const SzTy *__restrict__ scan, const uint32_t *__restrict__ status,
+                                    uint8_t poly_type, uint32_t std_domain, uint32_t nofold, OpPos *__restrict__ pos,
+                                    uint32_t *__restrict__ nfrag, uint32_t *__restrict__ late) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) {
+    if (p == n) nfrag[n] = late[n] = 0;
+    return;
+  }
+  const uint32_t i = order[p], c = skey[p];
+  const SzTy id{0, 0, 0, 0, 0};
+  const h3c_chunk_state cs = c < nchunks ? chunks[c] : h3c_chunk_state{};
+  OpPos r;
+  bool lt;
+  nfrag[p] = classify_op(ios[i], i, status[i], c, nchunks, cs, (p > 0 && skey[p - 1] == c) ? scan[p - 1] : id,
+                         scan[p], poly_type, std_domain, nofold, r, lt);
+  late[i] = lt ? 1u : 0u;
   pos[p] = r;
-  nfrag[p] = r.tk == kT_IDENT ? 0u : blocks_of(cs.base, r.r0, r.r1);
 }
 
 // The late pass's verdicts: A6 of the fold candidates that were not folded (late[i] == 1).  Their
