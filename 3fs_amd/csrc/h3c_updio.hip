@@ -73,7 +73,7 @@ enum { kCtrNone, kCtrReuse, kCtrCombine, kCtrRead, kCtrRecalc, kCtrMismatch, kCt
 // [kMiscOutF], [kMiscOutA6]: the fragment count and that flag, copied for the one read-back;
 // [kMiscT0], [kMiscT1]: the block kernel's first start and last end (wall clock, u64 each), its
 // timing when it runs inside a replayed graph (read back with the two words before them)
-enum { kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscT0 = 4, kMiscT1 = 6, kMiscN = 8 };
+enum { kMiscTicket = 0, kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscT0 = 4, kMiscT1 = 6, kMiscN = 8 };
 
 // ---------------------------------------------------------------- scan elements
 
@@ -219,8 +219,11 @@ __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t 
                                 uint32_t *__restrict__ status, uint32_t *__restrict__ key, uint32_t *__restrict__ idx,
                                 uint32_t *__restrict__ npieces, uint32_t *__restrict__ paycrc0,
                                 uint32_t *__restrict__ eacc, unsigned long long *__restrict__ ctr,
-                                uint32_t *__restrict__ misc) {
+                                uint32_t *__restrict__ misc, uint32_t *__restrict__ fz, uint32_t fz_words,
+                                uint32_t *__restrict__ hhead, uint32_t hcap) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < fz_words) fz[i] = 0;        // the one-pass front's tile states (uio_front_kernel)
+  if (i < hcap) hhead[i] = 0xFFFFFFFFu;  // ... and its link hash's bucket heads
   if (i < kCtrN) ctr[i] = 0;
   if (i < kMiscN) misc[i] = i == kMiscT0 || i == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;
   // chunk items n + c for c < C = max(nchunks, 1) (the piece pass's NP = n + C items), then the
@@ -554,26 +557,11 @@ __device__ __forceinline__ uint32_t frag_count(const uint32_t *__restrict__ d_F,
   return F <= cap ? F : 0u;
 }
 
-__global__ void uio_frag_kernel(const OpPos *__restrict__ pos, const uint32_t *__restrict__ fbase, uint32_t n,
-                                uint32_t cap, const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ skey,
-                                const h3c_chunk_state *__restrict__ chunks, FragDesc *__restrict__ frags,
-                                uint64_t *__restrict__ fkey, const PolyConsts *__restrict__ pc,
-                                uint32_t *__restrict__ hhead, uint32_t hcap) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < hcap) hhead[k] = kNil;  // the link hash's bucket heads (uio_tlink_kernel runs next)
-  const uint32_t F = frag_count(fbase + n, cap);
-  if (k >= F) return;
-  uint32_t a = 0, b = n;  // the last p with fbase[p] <= k
-  while (b - a > 1) {
-    const uint32_t m = (a + b) >> 1;
-    if (fbase[m] <= k) a = m; else b = m;
-  }
-  const uint32_t p = a;
-  const OpPos r = pos[p];
-  const uint32_t c = skey[p];
-  const h3c_chunk_state cs = chunks[c];
-  const h3c_update_io io = ios[r.op];
-  const uint64_t blk = (((cs.base + r.r0) >> 12) + (k - fbase[p])) << 12;
+// Fragment j of op position p (its j-th 4 KiB block) and the fragment's chain key.
+__device__ __forceinline__ FragDesc make_frag(const OpPos &r, uint32_t p, uint32_t j, uint32_t c,
+                                              const h3c_chunk_state &cs, const h3c_update_io &io,
+                                              const PolyConsts *__restrict__ pc, uint64_t &key) {
+  const uint64_t blk = (((cs.base + r.r0) >> 12) + j) << 12;
   const int64_t rel = (int64_t)blk - (int64_t)cs.base;  // chunk offset of the block's first byte
   FragDesc d{};
   d.blk = blk;
@@ -610,8 +598,30 @@ __global__ void uio_frag_kernel(const OpPos *__restrict__ pos, const uint32_t *_
     range(r.nb, r.na, d.z0, d.z1);
     if (d.z1 > d.z0) d.flags |= kFragWrite;
   }
-  frags[k] = d;
-  fkey[k] = ((uint64_t)c << 36) | (blk >> 12);
+  key = ((uint64_t)c << 36) | (blk >> 12);
+  return d;
+}
+
+__global__ void uio_frag_kernel(const OpPos *__restrict__ pos, const uint32_t *__restrict__ fbase, uint32_t n,
+                                uint32_t cap, const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ skey,
+                                const h3c_chunk_state *__restrict__ chunks, FragDesc *__restrict__ frags,
+                                uint64_t *__restrict__ fkey, const PolyConsts *__restrict__ pc,
+                                uint32_t *__restrict__ hhead, uint32_t hcap) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < hcap) hhead[k] = kNil;  // the link hash's bucket heads (uio_tlink_kernel runs next)
+  const uint32_t F = frag_count(fbase + n, cap);
+  if (k >= F) return;
+  uint32_t a = 0, b = n;  // the last p with fbase[p] <= k
+  while (b - a > 1) {
+    const uint32_t m = (a + b) >> 1;
+    if (fbase[m] <= k) a = m; else b = m;
+  }
+  const uint32_t p = a;
+  const OpPos r = pos[p];
+  const uint32_t c = skey[p];
+  uint64_t key;
+  frags[k] = make_frag(r, p, k - fbase[p], c, chunks[c], ios[r.op], pc, key);
+  fkey[k] = key;
 }
 
 // ---- chain links: each fragment's previous fragment of the same (chunk, block) ----
@@ -690,6 +700,404 @@ __global__ void uio_heads_kernel(const uint32_t *__restrict__ prev, const uint32
   const uint32_t p = prev[k];
   if (p != kNil) frags[p].next = k;
   else frags[k].flags |= kFragHead;
+}
+
+// ---- one-pass front: sizes, cases, fragment numbering, fragments and chain links ----
+// uio_front_kernel does in one launch what the scan-based stage does in ~10 (size-map scan,
+// classify, fragment-count scan, fragments, tile links, link resolution, chain heads).  A
+// workgroup takes a ticket k and owns sorted op positions [k T, (k+1) T); tiles are chained by
+// decoupled look-back over per-tile states in HBM (ticket order: a tile only waits on tiles that
+// are already running, so the chain cannot deadlock whatever the dispatch order):
+//   1. the size / type maps of the tile's ops, a segmented scan in LDS; the tile's last run is
+//      published (aggregate), the carry into its first run read back from earlier tiles, the
+//      inclusive state published;
+//   2. each op's case (classify_op), its fragment count; a fold candidate that is not local gets
+//      its A6 check here (one thread per op, a table-driven CRC of <= 4 KiB);
+//   3. fragment numbering: the tile's count published, its base read back the same way;
+//   4. the tile's fragments, grouped by (chunk, block) in LDS for the links inside the tile; each
+//      group's last fragment pushed on its hash bucket's list (next pointer first, then a CAS on
+//      the head, so a list read concurrently is always well formed); the tile's links flag set;
+//   5. once every earlier tile has set its flag, the fragments with no predecessor in their tile
+//      walk their bucket's list for the largest earlier fragment of their key.
+// Waits are bounded: a tile that gives up sets bit 1 of misc[kMiscA6] -- the pass is void, the
+// block kernel writes nothing and the host redoes the batch on the scan-based stage.
+constexpr uint32_t kFrontTile = 1024;
+constexpr uint32_t kFrontSpin = 1u << 21;
+constexpr uint32_t kMiscVoid = 2;  // misc[kMiscA6] bit: a front tile gave up waiting
+struct FrontSlot {
+  uint32_t sz_flag, nf_flag, ln_flag, whole;  // 0: nothing yet, 1: aggregate, 2: inclusive (ln: 1 = published)
+  uint32_t key, nf_agg, nf_incl, pad;         // the tile's last chunk key; fragment counts
+  SzTy sz_agg, sz_incl;                       // the tile's last run of `key`: alone / with everything before
+};
+static_assert(sizeof(FrontSlot) == 48, "FrontSlot is 48 bytes");
+
+__device__ __forceinline__ void pub_flag(uint32_t *f, uint32_t v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t get_flag(uint32_t *f) {
+  return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T ld_agent(T *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// spin until *f != 0; 0 after kFrontSpin polls (the caller voids the pass)
+__device__ __forceinline__ uint32_t wait_flag(uint32_t *f) {
+  uint32_t v;
+  for (uint32_t spins = 0; (v = get_flag(f)) == 0;) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > kFrontSpin) return 0;
+  }
+  return v;
+}
+
+// SzTy <-> two dwords (v; cst | tset << 8 | t << 16 | segment-head flag << 24) for shuffles
+__device__ __forceinline__ uint32_t sz_pack(const SzTy &a, uint32_t head) {
+  return (uint32_t)a.cst | ((uint32_t)a.tset << 8) | ((uint32_t)a.t << 16) | (head << 24);
+}
+__device__ __forceinline__ SzTy sz_unpack(uint32_t v, uint32_t w) {
+  return SzTy{v, (uint8_t)(w & 1u), (uint8_t)((w >> 8) & 1u), (uint8_t)((w >> 16) & 255u), 0};
+}
+// (head, map) pairs of a segmented scan: a, then b
+__device__ __forceinline__ void seg_combine(uint32_t av, uint32_t aw, uint32_t &bv, uint32_t &bw) {
+  if (bw >> 24) return;  // b starts a segment
+  const SzTy r = SzTyOp()(sz_unpack(av, aw), sz_unpack(bv, bw));
+  bv = r.v;
+  bw = sz_pack(r, aw >> 24);
+}
+
+// The raw CRC of a payload of at most a few KiB by one thread: 16-byte granules (edges masked)
+// into four dword streams stepped by x^(8*16) (PolyConsts::tab1), folded with x^-32 (red[0]); the
+// zero pad past the end removed with x^-(8 pad); the ~0 start's share added (init ~0, no final
+// XOR).  For the rare fold candidates that are not local (appends, first writes); tables read
+// from HBM through the caches.
+__device__ uint32_t thread_raw_crc(uint64_t S, uint32_t len, const PolyConsts *__restrict__ pc, uint32_t poly) {
+  const uint64_t E = S + len;
+  auto tstep = [&](uint32_t x) {
+    return pc->tab1[0][x & 255u] ^ pc->tab1[1][(x >> 8) & 255u] ^ pc->tab1[2][(x >> 16) & 255u] ^ pc->tab1[3][x >> 24];
+  };
+  auto tred = [&](uint32_t x) {
+    return pc->red[0][0][x & 255u] ^ pc->red[0][1][(x >> 8) & 255u] ^ pc->red[0][2][(x >> 16) & 255u] ^
+           pc->red[0][3][x >> 24];
+  };
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  for (uint64_t a = S & ~uint64_t(15); a < E; a += 16) {
+    const uint4 v = load_masked(a, S, E);
+    s0 = tstep(s0 ^ v.x);
+    s1 = tstep(s1 ^ v.y);
+    s2 = tstep(s2 ^ v.z);
+    s3 = tstep(s3 ^ v.w);
+  }
+  uint32_t v = tred(s3) ^ s2;
+  v = tred(v) ^ s1;
+  v = tred(v) ^ s0;
+  const uint32_t pad = (uint32_t)(((E + 15) & ~uint64_t(15)) - E);
+  if (pad) v = dgf_mul(v, pc->fixz[pad], poly);
+  return v ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(len, pc, poly), poly);
+}
+
+__global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
+    const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ order, const uint32_t *__restrict__ skey,
+    uint32_t n, const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks, const uint32_t *__restrict__ status,
+    uint8_t poly_type, uint32_t std_domain, const PolyConsts *__restrict__ pc, OpPos *__restrict__ pos,
+    uint32_t *__restrict__ nfrag, uint32_t *__restrict__ fbase, uint32_t *__restrict__ late,
+    uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6, uint32_t *misc, FragDesc *frags, uint64_t *fkey,
+    uint32_t cap, uint32_t *hhead, uint32_t hmask, uint32_t *gnext, uint32_t *prev, FrontSlot *slots) {
+  constexpr uint32_t T = kFrontTile, NW = T / 64;
+  __shared__ uint32_t s_key[T], s_v[T], s_w[T];         // keys; the inclusive maps (v, packed)
+  __shared__ uint32_t s_fex[T + 1];                     // exclusive fragment counts of the tile
+  __shared__ uint32_t s_op[T], s_nb[T], s_na[T], s_r0[T], s_r1[T], s_kind[T];
+  __shared__ uint32_t s_wv[NW], s_ww[NW], s_wn[NW];
+  __shared__ unsigned long long s_gkey[2 * T];          // link grouping of a fragment sub-tile
+  __shared__ uint32_t s_ghead[2 * T], s_gnx[T];
+  __shared__ uint32_t s_tile, s_cv, s_cw, s_cnf, s_void;
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t == 0) {
+    s_tile = atomicAdd(&misc[kMiscTicket], 1u);
+    s_void = 0;
+  }
+  __syncthreads();
+  const uint32_t k = s_tile;
+  const uint32_t p0 = k * T;
+  if (p0 >= n) return;  // (whole workgroup)
+  const uint32_t cnt = min(T, n - p0), tlast = cnt - 1;
+  const uint32_t poly = pc->poly;
+  const bool valid = t < cnt;
+  const uint32_t p = p0 + t;
+  const uint32_t c = valid ? skey[p] : 0xFFFFFFFFu;
+  const uint32_t i = valid ? order[p] : 0u;
+  h3c_update_io io{};
+  uint32_t st = H3C_ERR_INVALID_ARG;
+  if (valid) {
+    io = ios[i];
+    st = status[i];
+  }
+  const SzTy id{0, 0, 0, 0, 0};
+  const SzTy e = valid ? sz_elem_of(io, st, poly_type, std_domain) : id;
+  s_key[t] = c;
+  __syncthreads();
+  const uint32_t c0 = s_key[0];
+
+  // 1. segmented inclusive scan of the maps over the tile (a head where the key changes)
+  uint32_t xv = e.v, xw = sz_pack(e, (t == 0 || c != s_key[t - 1]) ? 1u : 0u);
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t yv = (uint32_t)__shfl_up((int)xv, o, 64), yw = (uint32_t)__shfl_up((int)xw, o, 64);
+    if (lane >= o) seg_combine(yv, yw, xv, xw);
+  }
+  if (lane == 63) {
+    s_wv[wave] = xv;
+    s_ww[wave] = xw;
+  }
+  __syncthreads();
+  {  // the earlier waves' totals combined in order, then into this lane
+
+    uint32_t pv = 0, pw = 0;  // identity, no head
+    for (uint32_t w = 0; w < wave; ++w) {
+      uint32_t bv = s_wv[w], bw = s_ww[w];
+      seg_combine(pv, pw, bv, bw);
+      pv = bv;
+      pw = bw;
+    }
+    if (wave) seg_combine(pv, pw, xv, xw);
+  }
+  // the tile's last run, published as its aggregate
+  if (t == tlast) {
+    FrontSlot &sl = slots[k];
+    sl.key = c;
+    sl.whole = c == c0;
+    sl.sz_agg = sz_unpack(xv, xw);
+    pub_flag(&sl.sz_flag, 1u);
+  }
+  // the carry into the tile's first run: the maps of the positions before it with key c0
+  if (wave == 0) {
+    SzTy carry = id;
+    bool done = k == 0;
+    for (int64_t j0 = (int64_t)k - 1; !done; j0 -= 64) {
+      const int64_t j = j0 - (int64_t)lane;
+      uint32_t fl = 3, key = 0xFFFFFFFFu, whole = 0, v = 0, w = 0;
+      if (j >= 0) {
+        FrontSlot &sl = slots[j];
+        fl = wait_flag(&sl.sz_flag);
+        key = sl.key;
+        whole = sl.whole;
+        const SzTy a = fl == 2 ? sl.sz_incl : sl.sz_agg;
+        v = a.v;
+        w = sz_pack(a, 0);
+      }
+      for (uint32_t l = 0; l < 64; ++l) {
+        const uint32_t fl_l = (uint32_t)__builtin_amdgcn_readlane((int)fl, (int)l);
+        if (fl_l == 3) {  // before tile 0
+          done = true;
+          break;
+        }
+        if (fl_l == 0) {  // gave up waiting
+          if (lane == 0) s_void = 1;
+          done = true;
+          break;
+        }
+        if ((uint32_t)__builtin_amdgcn_readlane((int)key, (int)l) != c0) {
+          done = true;
+          break;
+        }
+        carry = SzTyOp()(sz_unpack((uint32_t)__builtin_amdgcn_readlane((int)v, (int)l),
+                                   (uint32_t)__builtin_amdgcn_readlane((int)w, (int)l)), carry);
+        if (fl_l == 2 || !__builtin_amdgcn_readlane((int)whole, (int)l)) {
+          done = true;
+          break;
+        }
+      }
+    }
+    if (lane == 0) {
+      s_cv = carry.v;
+      s_cw = sz_pack(carry, 0);
+    }
+  }
+  __syncthreads();
+  const SzTy carry = sz_unpack(s_cv, s_cw);
+  SzTy in = sz_unpack(xv, xw);
+  if (c == c0) in = SzTyOp()(carry, in);
+  s_v[t] = in.v;
+  s_w[t] = sz_pack(in, 0);
+  if (t == tlast) {
+    slots[k].sz_incl = in;
+    pub_flag(&slots[k].sz_flag, 2u);
+  }
+  __syncthreads();
+
+  // 2. each op's case and fragment count
+  const SzTy ex = (t > 0 && s_key[t - 1] == c) ? sz_unpack(s_v[t - 1], s_w[t - 1]) : (c == c0 ? carry : id);
+  OpPos r{};
+  bool lt = false;
+  uint32_t f = 0;
+  h3c_chunk_state cs{};
+  if (valid) {
+    if (c < nchunks) cs = chunks[c];
+    f = classify_op(io, i, st, c, nchunks, cs, ex, in, poly_type, std_domain, 0u, r, lt);
+    if (lt) {  // A6 before the block kernel (a failure voids the speculative pass: the host redoes it)
+      const uint32_t raw = thread_raw_crc(io.payload, io.length, pc, poly);
+      payraw[i] = raw;
+      const bool bad = (std_domain ? ~raw : raw) != io.checksum_value;
+      a6[i] = bad ? 1u : 0u;
+      if (bad) atomicOr(&misc[kMiscA6], 1u);
+    }
+    late[i] = 0;
+  }
+
+  // 3. fragment numbering: exclusive counts in the tile, the tile's base from the tiles before
+  uint32_t fx = f;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)fx, o, 64);
+    if (lane >= o) fx += y;
+  }
+  if (lane == 63) s_wn[wave] = fx;
+  __syncthreads();
+  uint32_t wpre = 0, tot = 0;
+  for (uint32_t w = 0; w < NW; ++w) {
+    if (w < wave) wpre += s_wn[w];
+    tot += s_wn[w];
+  }
+  const uint32_t fex = wpre + fx - f;
+  s_fex[t] = fex;
+  if (t == 0) {
+    s_fex[T] = tot;
+    slots[k].nf_agg = tot;
+    pub_flag(&slots[k].nf_flag, 1u);
+  }
+  if (wave == 0) {
+    uint32_t base = 0;
+    bool done = k == 0;
+    for (int64_t j0 = (int64_t)k - 1; !done; j0 -= 64) {
+      const int64_t j = j0 - (int64_t)lane;
+      uint32_t fl = 3, v = 0;
+      if (j >= 0) {
+        FrontSlot &sl = slots[j];
+        fl = wait_flag(&sl.nf_flag);
+        v = fl == 2 ? sl.nf_incl : sl.nf_agg;
+      }
+      const uint64_t stop = __builtin_amdgcn_ballot_w64(fl != 1);  // inclusive, before tile 0, or gave up
+      const uint32_t first = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
+      uint32_t x = lane <= first && fl != 3 && fl != 0 ? v : 0u;
+#pragma unroll
+      for (uint32_t o = 32; o >= 1; o >>= 1) x += (uint32_t)__shfl_xor((int)x, (int)o, 64);
+      base += x;
+      if (stop) {
+        done = true;
+        if (first < 64 && (uint32_t)__builtin_amdgcn_readlane((int)fl, (int)first) == 0 && lane == 0) s_void = 1;
+      }
+    }
+    if (lane == 0) s_cnf = base;
+  }
+  __syncthreads();
+  const uint32_t F0 = s_cnf, FT = s_fex[T];
+  if (t == 0) {
+    slots[k].nf_incl = F0 + tot;
+    pub_flag(&slots[k].nf_flag, 2u);
+  }
+  if (valid) {
+    pos[p] = r;
+    nfrag[p] = f;
+    fbase[p] = F0 + fex;
+    if (p == n - 1) fbase[n] = F0 + tot;  // F: read by the block kernel and the host
+  }
+  s_op[t] = r.op;
+  s_nb[t] = r.nb;
+  s_na[t] = r.na;
+  s_r0[t] = r.r0;
+  s_r1[t] = r.r1;
+  s_kind[t] = (uint32_t)r.tk | ((uint32_t)r.pf << 8) | ((uint32_t)r.sk << 16);
+  __syncthreads();
+
+  // 4. the tile's fragments and the links inside it, in sub-tiles of T fragments
+  for (uint32_t s0 = 0; s0 < FT; s0 += T) {
+    for (uint32_t q = t; q < 2 * T; q += T) {
+      s_gkey[q] = kNoKey;
+      s_ghead[q] = kNil;
+    }
+    __syncthreads();
+    const uint32_t kk = s0 + t, g = F0 + kk;
+    const bool fv = kk < FT && g < cap;
+    unsigned long long key = kNoKey;
+    uint32_t h = kNil;
+    if (fv) {
+      uint32_t a = 0, b = cnt;  // the last position q of the tile with s_fex[q] <= kk
+      while (b - a > 1) {
+        const uint32_t m = (a + b) >> 1;
+        if (s_fex[m] <= kk) a = m; else b = m;
+      }
+      OpPos rq{};
+      rq.op = s_op[a];
+      rq.nb = s_nb[a];
+      rq.na = s_na[a];
+      rq.r0 = s_r0[a];
+      rq.r1 = s_r1[a];
+      rq.tk = (uint8_t)(s_kind[a] & 255u);
+      rq.pf = (uint8_t)((s_kind[a] >> 8) & 255u);
+      const uint32_t cq = s_key[a];
+      uint64_t k64;
+      frags[g] = make_frag(rq, p0 + a, kk - s_fex[a], cq, chunks[cq], ios[rq.op], pc, k64);
+      fkey[g] = k64;
+      key = k64;
+      h = key_hash(key) & (2 * T - 1);
+      for (;;) {
+        const unsigned long long old = atomicCAS(&s_gkey[h], kNoKey, key);
+        if (old == kNoKey || old == key) break;
+        h = (h + 1) & (2 * T - 1);
+      }
+      s_gnx[t] = atomicExch(&s_ghead[h], t);
+    }
+    __syncthreads();
+    uint32_t pin = kNil;
+    bool lastk = true;
+    if (h != kNil)
+      for (uint32_t u = s_ghead[h]; u != kNil; u = s_gnx[u]) {
+        if (u < t && (pin == kNil || u > pin)) pin = u;
+        if (u > t) lastk = false;
+      }
+    if (fv) {
+      prev[g] = pin == kNil ? kNil : F0 + s0 + pin;
+      if (lastk) {  // publish: the next pointer before the head, so a concurrent reader never sees a gap
+        uint32_t *bucket = &hhead[(key_hash(key) >> 7) & hmask];
+        uint32_t old = ld_agent(bucket);
+        do {
+          __hip_atomic_store(&gnext[g], old, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } while (!__hip_atomic_compare_exchange_strong(bucket, &old, g, __ATOMIC_RELEASE, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT));
+      }
+    }
+    __syncthreads();  // the sub-tile's records are written before their next pointers
+    if (fv && pin != kNil) frags[F0 + s0 + pin].next = g;
+    __syncthreads();
+  }
+  __threadfence();
+  __syncthreads();
+  if (t == 0) pub_flag(&slots[k].ln_flag, 1u);
+
+  // 5. predecessors in earlier tiles, once every earlier tile has published its links
+  if (wave == 0) {
+    for (int64_t j0 = (int64_t)k - 1; j0 >= 0; j0 -= 64) {
+      const int64_t j = j0 - (int64_t)lane;
+      const uint32_t fl = j >= 0 ? wait_flag(&slots[j].ln_flag) : 1u;
+      if (__builtin_amdgcn_ballot_w64(fl == 0) && lane == 0) s_void = 1;
+    }
+  }
+  __syncthreads();
+  if (s_void) {  // the pass is void: no chain is run, the host redoes the batch
+    if (t == 0) atomicOr(&misc[kMiscA6], kMiscVoid);
+    return;
+  }
+  for (uint32_t s0 = 0; s0 < FT; s0 += T) {
+    const uint32_t kk = s0 + t, g = F0 + kk;
+    if (kk >= FT || g >= cap || prev[g] != kNil) continue;
+    const uint64_t key = fkey[g];
+    uint32_t pr = kNil;
+    auto acq = [](uint32_t *q) { return __hip_atomic_load(q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); };
+    for (uint32_t j = acq(&hhead[(key_hash(key) >> 7) & hmask]); j != kNil; j = acq(&gnext[j]))
+      if (j < g && ld_agent(&fkey[j]) == key && (pr == kNil || j > pr)) pr = j;
+    if (pr != kNil) frags[pr].next = g;
+    else frags[g].flags |= kFragHead;
+  }
 }
 
 // ---- the block kernel ----
@@ -1555,6 +1963,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   // (a fragment per 4 KiB block an op touches: one per block-aligned write of <= 4 KiB; the
   // guess is the larger of 2n + 1024 and the calling thread's last batch, and a batch that
   // needs more redoes its fragment stage once with the count known)
+  const uint32_t ntiles_front = (uint32_t)((n + kFrontTile - 1) / kFrontTile);
   thread_local uint32_t last_frags = 0;
   uint32_t cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * n + 1024, last_frags), 0x7FFFFFF0u);
   size_t sort_tmp = 0, scan_tmp = 0, pscan_tmp = 0, szscan_tmp = 0, ascan_tmp = 0;
@@ -1574,6 +1983,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   uint32_t *d_status, *d_key, *d_idx, *d_skey, *d_order, *d_np, *d_pbase, *d_paycrc0, *d_payraw, *d_nfrag, *d_fbase,
       *d_eacc, *d_t0, *d_misc, *d_a6, *d_late, *d_lbase;
   SzTy *d_sz, *d_szscan;
+  FrontSlot *d_fslot;
   OpPos *d_pos;
   Aff *d_tel, *d_tscan, *d_sel, *d_sscan;
   void *d_tmp;
@@ -1596,6 +2006,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     d_eacc = carve<uint32_t>(cur, n);
     d_t0 = carve<uint32_t>(cur, C);
     d_misc = carve<uint32_t>(cur, kMiscN);
+    d_fslot = carve<FrontSlot>(cur, std::max(ntiles_front, 1u));
     d_sz = carve<SzTy>(cur, n);
     d_szscan = carve<SzTy>(cur, n);
     d_pos = carve<OpPos>(cur, n);
@@ -1619,13 +2030,20 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   StreamDrain drain{st, true};  // every return below waits for both streams before the leases go back
   StreamDrain drain_aux{aux->st, true};
   const uint32_t tb = 256, gb = (uint32_t)((n + tb) / tb);  // n + 1 threads (the scans' extra entry)
-  const uint32_t pb = (uint32_t)((std::max<size_t>(n, C) + tb) / tb);  // max(n, nchunks) + 1 threads
   const uint32_t vb = (uint32_t)((std::max<size_t>(n, C) + tb - 1) / tb);
   auto scan_excl = [&](const uint32_t *in, uint32_t *out, hipStream_t q) -> hipError_t {
     size_t t = tmp_bytes;
     return rocprim::exclusive_scan(d_tmp, t, in, out, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), q);
   };
   uint32_t nofold = 0;  // a redo after a failed A6 knows every verdict: no check moves into the block kernel
+  // the one-pass front (uio_front_kernel) on the first attempt; test hook H3C_HOOK_UPD_FRONT = 1: the
+  // scan-based stage (redone attempts always take that one)
+  const bool front = h3c_rt::hook(H3C_HOOK_UPD_FRONT) != 1;
+  // per attempt (fragment arrays for a guessed count, see below)
+  uint32_t hcap = 256;
+  FragDesc *d_frag = nullptr;
+  uint64_t *d_fkey = nullptr;
+  uint32_t *d_prev = nullptr, *d_gnext = nullptr, *d_hhead = nullptr;
   // sizes and types per op (a segmented scan), the reference's cases, fragment counts
   auto phase_sizes = [&](hipStream_t q) -> int {
     hipLaunchKernelGGL(uio_sz_elem_kernel, dim3(gb), dim3(tb), 0, q, d_ios, d_order, n, d_status, poly_type, stdf,
@@ -1645,8 +2063,11 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   // phase A: validation, payload CRCs + A6 and the INIT CRCs (second stream), sort, and the
   // speculative sizes / cases / fragment counts
   auto phase_a = [&](hipStream_t q) -> int {
-    hipLaunchKernelGGL(uio_prep_kernel, dim3(pb), dim3(tb), 0, q, d_ios, n, d_chunks, nchunks, poly_type, stdf,
-                       exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc);
+    const uint32_t fz_words = front ? ntiles_front * (uint32_t)(sizeof(FrontSlot) / 4) : 0u;
+    const uint32_t prep_threads = std::max<uint32_t>(std::max<uint32_t>(n, nchunks), std::max(fz_words, front ? hcap : 0u));
+    hipLaunchKernelGGL(uio_prep_kernel, dim3((prep_threads + tb) / tb), dim3(tb), 0, q, d_ios, n, d_chunks, nchunks,
+                       poly_type, stdf, exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc,
+                       reinterpret_cast<uint32_t *>(d_fslot), fz_words, d_hhead, front ? hcap : 0u);
     HIP_TRY(hipGetLastError());
     {
       size_t t = tmp_bytes;
@@ -1669,6 +2090,10 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     hipLaunchKernelGGL(uio_verify_t0_kernel, dim3(vb), dim3(tb), 0, aux->st, d_ios, n, d_chunks, nchunks, poly_type,
                        exactf, stdf, d_paycrc0, pc, d_status, d_payraw, d_a6, d_misc, d_t0, d_chunks_out, 1u);
     HIP_TRY(hipGetLastError());
+    if (front) {  // the sizes, cases, late A6 checks and fragments come in one launch (phase_frag)
+      HIP_TRY(hipEventRecord(aux->done, aux->st));
+      return H3C_OK;
+    }
     r = phase_sizes(q);  // speculative: every A6 check passes (joined before the block kernel)
     if (r) return r;
     // second stream, after the cases are known: the late pass over the fold candidates that
@@ -1692,11 +2117,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
 
   // ---- fragments, blocks, scans, results (redone once if the fragment guess was short) ----
   for (int attempt = 0;; ++attempt) {
-    uint32_t hcap = 256;
+    hcap = 256;
     while (hcap < cap) hcap <<= 1;
-    FragDesc *d_frag;
-    uint64_t *d_fkey;
-    uint32_t *d_prev, *d_gnext, *d_hhead;
     auto layout2 = [&](char *base) -> size_t {
       char *c2 = base;
       d_frag = carve<FragDesc>(c2, cap);
@@ -1713,6 +2135,15 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     const uint32_t *d_F = d_fbase + n;
     const uint32_t fb = (cap + tb - 1) / tb;
     auto phase_frag = [&](hipStream_t q) -> int {  // fragments and their chains
+      if (front && attempt == 0) {
+        hipLaunchKernelGGL(uio_front_kernel, dim3(std::max(ntiles_front, 1u)), dim3(kFrontTile), 0, q, d_ios, d_order,
+                           d_skey, n, d_chunks, nchunks, d_status, poly_type, stdf, pc, d_pos, d_nfrag, d_fbase,
+                           d_late, d_payraw, d_a6, d_misc, d_frag, d_fkey, cap, d_hhead, hcap - 1, d_gnext, d_prev,
+                           d_fslot);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamWaitEvent(q, aux->done, 0));  // the early A6 verdicts and t0
+        return H3C_OK;
+      }
       if (attempt) HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, q));  // the first attempt's counters
       hipLaunchKernelGGL(uio_frag_kernel, dim3((std::max(cap, hcap) + tb - 1) / tb), dim3(tb), 0, q, d_pos, d_fbase,
                          n, cap, d_ios, d_skey, d_chunks, d_frag, d_fkey, pc, d_hhead, hcap);
@@ -1837,18 +2268,20 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       if (t1 > t0 && khz > 0) h3c_rt::prof_add(H3C_PROF_UPDIO, (float)((double)(t1 - t0) / khz), alg_bytes);
     }
     const uint32_t F = h_F[0], a6_failed = h_F[1];
-    last_frags = F;
+    const bool void_pass = (a6_failed & kMiscVoid) != 0;  // a front tile gave up waiting: F means nothing
+    if (!void_pass) last_frags = F;
     if (F <= cap && !a6_failed) break;
-    if (attempt) {  // cannot happen: the second attempt knows the count and the verdicts
+    if (attempt >= 2) {  // cannot happen: a redo knows the verdicts, and the count after the first redo
       drain.armed = drain_aux.armed = false;
       h3c_rt::set_error_text("h3c_update_ios: fragment count changed between attempts");
       return H3C_ERR_HIP;
     }
-    // nothing was written (no chain ran): redo, with the count known and, after a failed A6,
-    // the sizes / cases / fragment counts recomputed from the real verdicts (F can only shrink).
-    // A failed A6 came from the piece passes; the fold candidates' own checks never ran, so every
-    // typed WRITE is checked again first and the redo moves no check into the block kernel.
-    cap = std::max(cap, F);
+    // nothing was written (no chain ran): redo on the scan-based stage, with the count known and,
+    // after a failed A6 (or a void front pass), the sizes / cases / fragment counts recomputed from
+    // the real verdicts (F can only shrink).  A failed A6 came from the piece passes or the late
+    // checks; the fold candidates' own checks never ran, so every typed WRITE is checked again
+    // first and the redo moves no check into the block kernel.
+    if (!void_pass) cap = std::max(cap, F);
     if (a6_failed) {
       hipLaunchKernelGGL(uio_redo_pieces_kernel, dim3((uint32_t)((NP + 1 + tb - 1) / tb)), dim3(tb), 0, st, d_ios, n,
                          (uint32_t)NP, d_status, d_np, d_paycrc0);

@@ -351,7 +351,7 @@ def sync_bench(threads: int, nbytes: int, calls: int, api: str = "verify"):
     return lat, wall.value
 
 
-HOOK_SEG_BYTES, HOOK_DEBUG_FLAGS, HOOK_UPD_SCAN, HOOK_UPD_GRAPHS, HOOK_UPD_LOOKBACK = 1, 2, 3, 4, 5  # h3c_test_hook keys
+HOOK_SEG_BYTES, HOOK_DEBUG_FLAGS, HOOK_UPD_SCAN, HOOK_UPD_GRAPHS, HOOK_UPD_LOOKBACK, HOOK_UPD_FRONT = 1, 2, 3, 4, 5, 6
 UPD_SCAN_PATHS = {"default": 0, "fused": 1, "tiles": 2, "sort": 3}
 
 

@@ -422,9 +422,11 @@ enum h3c_hook {
   H3C_HOOK_UPD_SCAN = 3,    /* h3c_update_blocks: 1 fused, 2 dense tiles, 3 sort + scan_by_key */
   H3C_HOOK_UPD_GRAPHS = 4,  /* h3c_update_ios: 1 never replays its pipeline as HIP graphs, even with
                                H3C_UPD_GRAPHS; 2 captures them without the flag */
-  H3C_HOOK_UPD_LOOKBACK = 5 /* h3c_update_blocks fused path: 1 makes the workgroup with ticket 1 give up
+  H3C_HOOK_UPD_LOOKBACK = 5, /* h3c_update_blocks fused path: 1 makes the workgroup with ticket 1 give up
                                its look-back at once, as a starved wait would (the void-batch report:
                                *n_invalid = UINT32_MAX, counters.invalid = UINT64_MAX) */
+  H3C_HOOK_UPD_FRONT = 6     /* h3c_update_ios: 1 runs the sizes / cases / fragments as the scan-based
+                               stage (~10 launches) instead of the one-pass front kernel */
 };
 int h3c_test_hook(int key, uint64_t value);
 /* Engine-internal counters for tests: 0 = h3c_update_ios pipeline graph replays, 1 = graph

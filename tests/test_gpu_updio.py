@@ -197,8 +197,16 @@ def random_scenario(h3c, torch, dev, rng, nchunks, chunk_size, nops, align=1, ho
     return sc
 
 
+@pytest.fixture(params=["front", "scan"])
+def front_mode(request, h3c, hooks):
+    """The sizes / cases / fragments stage both ways: the one-pass front kernel (default) and the
+    scan-based stage (h3c_test_hook(H3C_HOOK_UPD_FRONT, 1), also what every redo runs)."""
+    hooks(h3c.HOOK_UPD_FRONT, 1 if request.param == "scan" else 0)
+    return request.param
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_updio_random_mixed_ops(h3c, torch_dev, seed):
+def test_updio_random_mixed_ops(h3c, torch_dev, seed, front_mode):
     torch, dev = torch_dev
     rng = np.random.default_rng(seed)
     sc = random_scenario(h3c, torch, dev, rng, nchunks=8, chunk_size=64 << 10, nops=400)
@@ -243,7 +251,7 @@ def test_updio_device_resident_edge_shapes(h3c, torch_dev):
     assert d_ctr.cpu().tolist() == [0] * 8
 
 
-def test_updio_large_batch(h3c, torch_dev):
+def test_updio_large_batch(h3c, torch_dev, front_mode):
     """20000 mixed ops over 24 chunks with ops naming no chunk of the batch spread through the
     sequence (and a few client checksums failing)."""
     torch, dev = torch_dev
@@ -258,7 +266,7 @@ def test_updio_large_batch(h3c, torch_dev):
 
 
 @pytest.mark.parametrize("nchunks,chunk_kib,nops", [(300, 8, 6000), (3000, 4, 4000), (70000, 4, 3000)])
-def test_updio_many_chunks_sort_paths(h3c, torch_dev, nchunks, chunk_kib, nops):
+def test_updio_many_chunks_sort_paths(h3c, torch_dev, nchunks, chunk_kib, nops, front_mode):
     """The ops' sort by chunk: keys of <= 8 bits take one counting-sort pass (every test above),
     9-16 bits two passes (300 and 3000 chunks), wider keys rocPRIM's merge sort (70000)."""
     torch, dev = torch_dev
@@ -285,7 +293,7 @@ def test_updio_exact_mode_more_chunks_than_ops(h3c, torch_dev, dev_api):
     assert int(sc.counters.stale_chunks) == sc.stale_chunks
 
 
-def test_updio_hot_region_conflicts(h3c, torch_dev):
+def test_updio_hot_region_conflicts(h3c, torch_dev, front_mode):
     """Many overlapping writes into the first 16 KiB of two chunks: long epoch chains."""
     torch, dev = torch_dev
     rng = np.random.default_rng(11)
