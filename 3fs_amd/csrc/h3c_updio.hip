@@ -219,7 +219,8 @@ __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t 
                                 uint32_t *__restrict__ status, uint32_t *__restrict__ key, uint32_t *__restrict__ idx,
                                 uint32_t *__restrict__ npieces, uint32_t *__restrict__ paycrc0,
                                 uint32_t *__restrict__ eacc, unsigned long long *__restrict__ ctr,
-                                uint32_t *__restrict__ misc, uint32_t *__restrict__ fz, uint32_t fz_words,
+                                uint32_t *__restrict__ misc, uint32_t *__restrict__ a6, uint32_t *__restrict__ fz,
+                                uint32_t fz_words,
                                 uint32_t *__restrict__ hhead, uint32_t hcap) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < fz_words) fz[i] = 0;        // the one-pass front's tile states (uio_front_kernel)
@@ -241,6 +242,7 @@ __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t 
   if (i >= n) return;
   paycrc0[i] = 0;  // XOR accumulators of the piece and block kernels
   eacc[i] = 0;
+  a6[i] = 0;       // A6 verdicts (the early pass, the front / late checks, the block kernel)
   const h3c_update_io io = ios[i];
   uint32_t st = H3C_OK;
   const uint32_t c = io.chunk;
@@ -296,17 +298,18 @@ __device__ __forceinline__ void verify_op(uint32_t i, const h3c_update_io *__res
                                           uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6,
                                           uint32_t *__restrict__ misc, const h3c_chunk_state *__restrict__ skip_cand) {
   const h3c_update_io io = ios[i];
-  uint32_t bad = 0;
-  // skip_cand: the early pass, which carries no fold candidate's payload
+  // skip_cand: the early pass, which carries no fold candidate's payload (their verdicts come from
+  // the block kernel or the front kernel, concurrently: a6[] of a skipped op is not written here;
+  // the prep kernel zeroed it)
   if (io.kind == H3C_UPD_WRITE && status[i] == H3C_OK && !(skip_cand && fold_candidate(io, skip_cand[io.chunk], H3C_OK))) {
     const uint32_t poly = pc->poly;
     const uint32_t raw = io.length ? paycrc0[i] ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(io.length, pc, poly), poly)
                                    : 0xFFFFFFFFu;
     payraw[i] = raw;
-    bad = io.checksum_type != H3C_TYPE_NONE && io.length && (std_domain ? ~raw : raw) != io.checksum_value;
+    const bool bad = io.checksum_type != H3C_TYPE_NONE && io.length && (std_domain ? ~raw : raw) != io.checksum_value;
+    a6[i] = bad ? 1u : 0u;
+    if (bad) atomicOr(&misc[kMiscA6], 1u);
   }
-  a6[i] = bad;
-  if (bad) atomicOr(&misc[kMiscA6], 1u);
 }
 
 // After a failed A6: the verdicts into the statuses, and the flag cleared for the redo.
@@ -2066,7 +2069,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     const uint32_t fz_words = front ? ntiles_front * (uint32_t)(sizeof(FrontSlot) / 4) : 0u;
     const uint32_t prep_threads = std::max<uint32_t>(std::max<uint32_t>(n, nchunks), std::max(fz_words, front ? hcap : 0u));
     hipLaunchKernelGGL(uio_prep_kernel, dim3((prep_threads + tb) / tb), dim3(tb), 0, q, d_ios, n, d_chunks, nchunks,
-                       poly_type, stdf, exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc,
+                       poly_type, stdf, exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc, d_a6,
                        reinterpret_cast<uint32_t *>(d_fslot), fz_words, d_hhead, front ? hcap : 0u);
     HIP_TRY(hipGetLastError());
     {
