@@ -475,7 +475,7 @@ def test_updio_reference_write_patterns_golden(h3c, torch_dev):
                 op = t["ops"][k]
                 p = orc.splitmix_bytes(op["length"], op["seed"], op["widx"])
                 pays.append(torch.from_numpy(p).to(dev))
-                ops.append((pays[-1].data_ptr(), c, op["offset"], op["length"], op["write_crc32c"], 1, h3c.UPD_WRITE, 0, 0))
+                ops.append((pays[-1].data_ptr(), c, op["offset"], op["length"], op["write_crc32c"], 1, h3c.UPD_WRITE, 0, 0, 0))
                 want.append((op["chunk_size_after"], op["chunk_crc32c"]))
     ios = np.zeros(len(ops), dtype=h3c.UPDATE_IO_DTYPE)
     for i, o in enumerate(ops):
