@@ -286,7 +286,8 @@ constexpr int kUniLdsWords = kUniCopies == 16 ? kLdsWords16 : kLdsWords;
 #define H3C_UNI_LANES_HI 16
 #endif
 #ifndef H3C_UNI_PAIR
-#define H3C_UNI_PAIR 1  // uniform chunks of <= 6 rows, 128-byte multiples: 8 lanes x 2 chunks (0: 4 lanes x 1)
+#define H3C_UNI_PAIR 0  // 1: uniform chunks of <= 6 rows, 128-byte multiples take 8 lanes x 2 chunks instead of
+                        // 4 lanes x 1 -- measured 10 % slower at 4 KiB (profiles/r03_small_pair_ab.txt)
 #endif
 
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }

@@ -202,7 +202,11 @@ __device__ __forceinline__ bool needs_init(const h3c_chunk_state &cs, uint8_t po
 // A typed, non-empty, non-syncing WRITE whose payload lands in one 4 KiB block of its chunk
 // (absolute addresses): its A6 check may move into the block kernel (kPosFold, decided by
 // classify).  `st` is the op's status so far.
+#ifndef H3C_UIO_FOLD
+#define H3C_UIO_FOLD 1  // A6 checks of local one-block writes in the block kernel (0: all in the piece pass)
+#endif
 __device__ __forceinline__ bool fold_candidate(const h3c_update_io &io, const h3c_chunk_state &cs, uint32_t st) {
+  if (!H3C_UIO_FOLD) return false;
   if (st != H3C_OK || io.kind != H3C_UPD_WRITE || io.checksum_type == H3C_TYPE_NONE || !io.length ||
       (io.flags & H3C_IO_SYNCING))
     return false;
