@@ -565,9 +565,13 @@ __device__ __forceinline__ uint32_t frag_count(const uint32_t *__restrict__ d_F,
 }
 
 // Fragment j of op position p (its j-th 4 KiB block) and the fragment's chain key.
+// A fold fragment carries the client's checksum as the init-0 CRC its block image must have
+// (payload bytes at [w0, w1), zeros elsewhere): the block kernel compares without a multiply.
+// *praw receives the raw payload CRC the op has when its check passes (its t-map needs it).
 __device__ __forceinline__ FragDesc make_frag(const OpPos &r, uint32_t p, uint32_t j, uint32_t c,
                                               const h3c_chunk_state &cs, const h3c_update_io &io,
-                                              const PolyConsts *__restrict__ pc, uint64_t &key) {
+                                              const PolyConsts *__restrict__ pc, uint32_t std_domain,
+                                              uint64_t &key, uint32_t &praw) {
   const uint64_t blk = (((cs.base + r.r0) >> 12) + j) << 12;
   const int64_t rel = (int64_t)blk - (int64_t)cs.base;  // chunk offset of the block's first byte
   FragDesc d{};
@@ -592,10 +596,13 @@ __device__ __forceinline__ FragDesc make_frag(const OpPos &r, uint32_t p, uint32
       if (d.w1 > d.w0) d.flags |= kFragCrc;
     }
     if (d.w1 > d.w0 || d.z1 > d.z0) d.flags |= kFragWrite;
-    if (r.pf & kPosFold) {  // the op's only fragment: its A6 check happens here
+    if (r.pf & kPosFold) {  // the op's only fragment: its A6 check happens in the block kernel
+      const uint32_t poly = pc->poly;
+      praw = std_domain ? ~io.checksum_value : io.checksum_value;
+      const uint32_t c0 = praw ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(io.length, pc, poly), poly);
       d.flags |= kFragA6;
       d.op = r.op;
-      d.expect = io.checksum_value;
+      d.expect = dgf_mul_fast(c0, dxpow8_fast((int64_t)kBlk - d.w1, pc, poly), poly);
       d.len = io.length;
     }
   } else if (r.na < r.nb) {  // truncate: the cut bytes leave the CRC
@@ -613,7 +620,8 @@ __global__ void uio_frag_kernel(const OpPos *__restrict__ pos, const uint32_t *_
                                 uint32_t cap, const h3c_update_io *__restrict__ ios, const uint32_t *__restrict__ skey,
                                 const h3c_chunk_state *__restrict__ chunks, FragDesc *__restrict__ frags,
                                 uint64_t *__restrict__ fkey, const PolyConsts *__restrict__ pc,
-                                uint32_t *__restrict__ hhead, uint32_t hcap) {
+                                uint32_t *__restrict__ hhead, uint32_t hcap, uint32_t std_domain,
+                                uint32_t *__restrict__ payraw) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < hcap) hhead[k] = kNil;  // the link hash's bucket heads (uio_tlink_kernel runs next)
   const uint32_t F = frag_count(fbase + n, cap);
@@ -627,8 +635,11 @@ __global__ void uio_frag_kernel(const OpPos *__restrict__ pos, const uint32_t *_
   const OpPos r = pos[p];
   const uint32_t c = skey[p];
   uint64_t key;
-  frags[k] = make_frag(r, p, k - fbase[p], c, chunks[c], ios[r.op], pc, key);
+  uint32_t praw = 0;
+  const FragDesc d = make_frag(r, p, k - fbase[p], c, chunks[c], ios[r.op], pc, std_domain, key, praw);
+  frags[k] = d;
   fkey[k] = key;
+  if (d.flags & kFragA6) payraw[r.op] = praw;
 }
 
 // ---- chain links: each fragment's previous fragment of the same (chunk, block) ----
@@ -741,20 +752,19 @@ static_assert(sizeof(FrontSlot) == 48, "FrontSlot is 48 bytes");
 __device__ __forceinline__ void pub_flag(uint32_t *f, uint32_t v) {
   __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint32_t get_flag(uint32_t *f) {
-  return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-}
 template <class T>
-__device__ __forceinline__ T ld_agent(T *p) {
+__device__ __forceinline__ T ld_agent(T *p) {  // a relaxed load at the coherence point (L2)
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// spin until *f != 0; 0 after kFrontSpin polls (the caller voids the pass)
+// spin until *f != 0 (relaxed polls through L2, then one acquire fence: an acquire load per poll
+// would invalidate the CU's L1 each time); 0 after kFrontSpin polls (the caller voids the pass)
 __device__ __forceinline__ uint32_t wait_flag(uint32_t *f) {
   uint32_t v;
-  for (uint32_t spins = 0; (v = get_flag(f)) == 0;) {
+  for (uint32_t spins = 0; (v = ld_agent(f)) == 0;) {
     __builtin_amdgcn_s_sleep(1);
     if (++spins > kFrontSpin) return 0;
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return v;
 }
 
@@ -1043,8 +1053,11 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
       rq.pf = (uint8_t)((s_kind[a] >> 8) & 255u);
       const uint32_t cq = s_key[a];
       uint64_t k64;
-      frags[g] = make_frag(rq, p0 + a, kk - s_fex[a], cq, chunks[cq], ios[rq.op], pc, k64);
+      uint32_t praw = 0;
+      const FragDesc d = make_frag(rq, p0 + a, kk - s_fex[a], cq, chunks[cq], ios[rq.op], pc, std_domain, k64, praw);
+      frags[g] = d;
       fkey[g] = k64;
+      if (d.flags & kFragA6) payraw[rq.op] = praw;
       key = k64;
       h = key_hash(key) & (2 * T - 1);
       for (;;) {
@@ -1099,8 +1112,9 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
     if (kk >= FT || g >= cap || prev[g] != kNil) continue;
     const uint64_t key = fkey[g];
     uint32_t pr = kNil;
-    auto acq = [](uint32_t *q) { return __hip_atomic_load(q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); };
-    for (uint32_t j = acq(&hhead[(key_hash(key) >> 7) & hmask]); j != kNil; j = acq(&gnext[j]))
+    // relaxed loads through L2: a published entry's next pointer reached L2 before the CAS that
+    // made the entry reachable (release), and each load here depends on the one before
+    for (uint32_t j = ld_agent(&hhead[(key_hash(key) >> 7) & hmask]); j != kNil; j = ld_agent(&gnext[j]))
       if (j < g && ld_agent(&fkey[j]) == key && (pr == kNil || j > pr)) pr = j;
     if (pr != kNil) frags[pr].next = g;
     else frags[g].flags |= kFragHead;
@@ -1227,22 +1241,16 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
                                                    const char *lb, const LaneLut &L, const uint32_t *red, uint32_t poly,
                                                    uint32_t *__restrict__ eacc, const FoldIo &fx) {
   const uint32_t w0 = w & 0xFFFFu, w1 = w >> 16, q0 = q & 0xFFFFu, q1 = q >> 16, z0 = z & 0xFFFFu, z1 = z >> 16;
-  uint32_t vnew = 0;
   if (flags & kFragA6) {
-    Streams sn{0, 0, 0, 0};  // the new bytes alone (one stream set at a time: registers are short)
+    Streams sn{0, 0, 0, 0};  // the new bytes alone (one stream set at a time: the registers are full)
 #pragma unroll
     for (int r = 0; r < 4; ++r) consume(sn, nw[r], lb, L);
-    vnew = wave_fold_tab(sn, lane, red);
-    // crc0(payload) = crc0(block image) * x^-(8 (4096 - w1)); raw = crc0 ^ ~0 * x^(8 len)
-    const uint32_t c0 = dgf_mul_fast(vnew, dxpow8_fast(-(int64_t)(kBlk - w1), fx.pc, poly), poly);
-    const uint32_t raw = c0 ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(fx.len, fx.pc, poly), poly);
-    const bool bad = (fx.std_domain ? ~raw : raw) != fx.expect;  // wave-uniform (lane 0's value)
-    const bool bad_u = __builtin_amdgcn_readfirstlane(bad ? 1 : 0) != 0;
-    if (lane == 0) {
-      fx.payraw[fx.op] = raw;
-      if (bad) fx.a6[fx.op] = 1u;
+    // the payload's init-0 CRC in its block image against the client's, precomputed (make_frag)
+    const bool bad = __builtin_amdgcn_readfirstlane(wave_fold_tab(sn, lane, red)) != fx.expect;
+    if (bad) {
+      if (lane == 0) fx.a6[fx.op] = 1u;
+      return 0u;
     }
-    if (bad_u) return 0u;
   }
   if (flags & kFragCrc) {
     Streams st{0, 0, 0, 0};
@@ -2153,7 +2161,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       }
       if (attempt) HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, q));  // the first attempt's counters
       hipLaunchKernelGGL(uio_frag_kernel, dim3((std::max(cap, hcap) + tb - 1) / tb), dim3(tb), 0, q, d_pos, d_fbase,
-                         n, cap, d_ios, d_skey, d_chunks, d_frag, d_fkey, pc, d_hhead, hcap);
+                         n, cap, d_ios, d_skey, d_chunks, d_frag, d_fkey, pc, d_hhead, hcap, stdf, d_payraw);
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(uio_tlink_kernel, dim3((cap + kLinkTile - 1) / kLinkTile), dim3(kLinkTile), 0, q, d_fkey,
                          d_F, cap, d_hhead, hcap - 1, d_gnext, d_prev);
