@@ -749,22 +749,50 @@ struct FrontSlot {
 };
 static_assert(sizeof(FrontSlot) == 48, "FrontSlot is 48 bytes");
 
-__device__ __forceinline__ void pub_flag(uint32_t *f, uint32_t v) {
-  __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
+// Cross-workgroup traffic inside the kernel uses relaxed agent-scope atomics only (sc1 loads and
+// stores, coherent across the XCDs' L2s) and a vmcnt wait before a flag store: a release / acquire
+// at agent scope would write back / invalidate the whole L2 (buffer_wbl2 / buffer_inv sc1) every
+// time -- with one per published hash entry, the first version of this kernel took 117-170 us.
 template <class T>
-__device__ __forceinline__ T ld_agent(T *p) {  // a relaxed load at the coherence point (L2)
+__device__ __forceinline__ T ld_agent(T *p) {  // a relaxed load at the coherence point
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// spin until *f != 0 (relaxed polls through L2, then one acquire fence: an acquire load per poll
-// would invalidate the CU's L1 each time); 0 after kFrontSpin polls (the caller voids the pass)
+template <class T>
+__device__ __forceinline__ void st_agent(T *p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void pub_flag(uint32_t *f, uint32_t v) {
+  stores_done();  // this thread's payload stores are at the coherence point before the flag
+  st_agent(f, v);
+}
+// A fragment record written through to the coherence point: another tile may set its next
+// pointer later (a plain store would leave a dirty L2 line on this XCD whose write-back at the
+// kernel's end could land after that tile's store).
+__device__ __forceinline__ void store_frag(FragDesc *dst, const FragDesc &d) {
+  uint64_t w[8];
+  __builtin_memcpy(w, &d, 64);
+  unsigned long long *q = reinterpret_cast<unsigned long long *>(dst);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) st_agent(q + k, (unsigned long long)w[k]);
+}
+__device__ __forceinline__ uint64_t sz_bits(const SzTy &a) {
+  uint64_t b;
+  __builtin_memcpy(&b, &a, 8);
+  return b;
+}
+__device__ __forceinline__ SzTy sz_from_bits(uint64_t b) {
+  SzTy a;
+  __builtin_memcpy(&a, &b, 8);
+  return a;
+}
+// spin until *f != 0; 0 after kFrontSpin polls (the caller voids the pass)
 __device__ __forceinline__ uint32_t wait_flag(uint32_t *f) {
   uint32_t v;
   for (uint32_t spins = 0; (v = ld_agent(f)) == 0;) {
     __builtin_amdgcn_s_sleep(1);
     if (++spins > kFrontSpin) return 0;
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return v;
 }
 
@@ -881,9 +909,9 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
   // the tile's last run, published as its aggregate
   if (t == tlast) {
     FrontSlot &sl = slots[k];
-    sl.key = c;
-    sl.whole = c == c0;
-    sl.sz_agg = sz_unpack(xv, xw);
+    st_agent(&sl.key, c);
+    st_agent(&sl.whole, c == c0 ? 1u : 0u);
+    st_agent(reinterpret_cast<uint64_t *>(&sl.sz_agg), sz_bits(sz_unpack(xv, xw)));
     pub_flag(&sl.sz_flag, 1u);
   }
   // the carry into the tile's first run: the maps of the positions before it with key c0
@@ -896,9 +924,9 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
       if (j >= 0) {
         FrontSlot &sl = slots[j];
         fl = wait_flag(&sl.sz_flag);
-        key = sl.key;
-        whole = sl.whole;
-        const SzTy a = fl == 2 ? sl.sz_incl : sl.sz_agg;
+        key = ld_agent(&sl.key);
+        whole = ld_agent(&sl.whole);
+        const SzTy a = sz_from_bits(ld_agent(reinterpret_cast<uint64_t *>(fl == 2 ? &sl.sz_incl : &sl.sz_agg)));
         v = a.v;
         w = sz_pack(a, 0);
       }
@@ -937,7 +965,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
   s_v[t] = in.v;
   s_w[t] = sz_pack(in, 0);
   if (t == tlast) {
-    slots[k].sz_incl = in;
+    st_agent(reinterpret_cast<uint64_t *>(&slots[k].sz_incl), sz_bits(in));
     pub_flag(&slots[k].sz_flag, 2u);
   }
   __syncthreads();
@@ -979,7 +1007,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
   s_fex[t] = fex;
   if (t == 0) {
     s_fex[T] = tot;
-    slots[k].nf_agg = tot;
+    st_agent(&slots[k].nf_agg, tot);
     pub_flag(&slots[k].nf_flag, 1u);
   }
   if (wave == 0) {
@@ -991,7 +1019,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
       if (j >= 0) {
         FrontSlot &sl = slots[j];
         fl = wait_flag(&sl.nf_flag);
-        v = fl == 2 ? sl.nf_incl : sl.nf_agg;
+        v = ld_agent(fl == 2 ? &sl.nf_incl : &sl.nf_agg);
       }
       const uint64_t stop = __builtin_amdgcn_ballot_w64(fl != 1);  // inclusive, before tile 0, or gave up
       const uint32_t first = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
@@ -1009,7 +1037,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
   __syncthreads();
   const uint32_t F0 = s_cnf, FT = s_fex[T];
   if (t == 0) {
-    slots[k].nf_incl = F0 + tot;
+    st_agent(&slots[k].nf_incl, F0 + tot);
     pub_flag(&slots[k].nf_flag, 2u);
   }
   if (valid) {
@@ -1055,8 +1083,8 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
       uint64_t k64;
       uint32_t praw = 0;
       const FragDesc d = make_frag(rq, p0 + a, kk - s_fex[a], cq, chunks[cq], ios[rq.op], pc, std_domain, k64, praw);
-      frags[g] = d;
-      fkey[g] = k64;
+      store_frag(&frags[g], d);
+      st_agent(reinterpret_cast<unsigned long long *>(&fkey[g]), (unsigned long long)k64);  // read by later tiles
       if (d.flags & kFragA6) payraw[rq.op] = praw;
       key = k64;
       h = key_hash(key) & (2 * T - 1);
@@ -1081,16 +1109,18 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
         uint32_t *bucket = &hhead[(key_hash(key) >> 7) & hmask];
         uint32_t old = ld_agent(bucket);
         do {
-          __hip_atomic_store(&gnext[g], old, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } while (!__hip_atomic_compare_exchange_strong(bucket, &old, g, __ATOMIC_RELEASE, __ATOMIC_RELAXED,
+          st_agent(&gnext[g], old);
+          stores_done();
+        } while (!__hip_atomic_compare_exchange_strong(bucket, &old, g, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT));
       }
     }
+    stores_done();
     __syncthreads();  // the sub-tile's records are written before their next pointers
-    if (fv && pin != kNil) frags[F0 + s0 + pin].next = g;
+    if (fv && pin != kNil) st_agent(&frags[F0 + s0 + pin].next, g);
     __syncthreads();
   }
-  __threadfence();
+  stores_done();  // every thread's fkey / gnext / CAS traffic is out before the flag
   __syncthreads();
   if (t == 0) pub_flag(&slots[k].ln_flag, 1u);
 
@@ -1110,14 +1140,14 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
   for (uint32_t s0 = 0; s0 < FT; s0 += T) {
     const uint32_t kk = s0 + t, g = F0 + kk;
     if (kk >= FT || g >= cap || prev[g] != kNil) continue;
-    const uint64_t key = fkey[g];
+    const unsigned long long key = ld_agent(reinterpret_cast<unsigned long long *>(&fkey[g]));
     uint32_t pr = kNil;
-    // relaxed loads through L2: a published entry's next pointer reached L2 before the CAS that
-    // made the entry reachable (release), and each load here depends on the one before
+    // a published entry's next pointer reached the coherence point before the CAS that made the
+    // entry reachable (stores_done), and each load here depends on the one before
     for (uint32_t j = ld_agent(&hhead[(key_hash(key) >> 7) & hmask]); j != kNil; j = ld_agent(&gnext[j]))
-      if (j < g && ld_agent(&fkey[j]) == key && (pr == kNil || j > pr)) pr = j;
-    if (pr != kNil) frags[pr].next = g;
-    else frags[g].flags |= kFragHead;
+      if (j < g && ld_agent(reinterpret_cast<unsigned long long *>(&fkey[j])) == key && (pr == kNil || j > pr)) pr = j;
+    if (pr != kNil) st_agent(&frags[pr].next, g);
+    else st_agent(&frags[g].flags, ld_agent(&frags[g].flags) | kFragHead);
   }
 }
 
