@@ -73,7 +73,8 @@ enum { kCtrNone, kCtrReuse, kCtrCombine, kCtrRead, kCtrRecalc, kCtrMismatch, kCt
 // [kMiscOutF], [kMiscOutA6]: the fragment count and that flag, copied for the one read-back;
 // [kMiscT0], [kMiscT1]: the block kernel's first start and last end (wall clock, u64 each), its
 // timing when it runs inside a replayed graph (read back with the two words before them)
-enum { kMiscTicket = 0, kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscT0 = 4, kMiscT1 = 6, kMiscN = 8 };
+// [kMiscTicket]: uio_front_kernel's tile ticket; [kMiscPBVoid]: a uio_phaseb_kernel tile gave up waiting
+enum { kMiscTicket = 0, kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscT0 = 4, kMiscT1 = 6, kMiscPBVoid = 8, kMiscN = 10 };
 
 // ---------------------------------------------------------------- scan elements
 
@@ -1417,9 +1418,15 @@ __global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__r
                                                              uint32_t *__restrict__ eacc,
                                                              const uint32_t *__restrict__ misc,
                                                              unsigned long long *ts, uint32_t std_domain,
-                                                             uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6) {
+                                                             uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6,
+                                                             uint32_t *__restrict__ pbz, uint32_t pbz_words,
+                                                             uint32_t *__restrict__ misc_w) {
   __shared__ uint32_t lds[kLdsWords + kRedWords];
   if (ts && threadIdx.x == 0) atomicMin(&ts[0], (unsigned long long)wall_clock64());
+  if (blockIdx.x == 0) {  // uio_phaseb_kernel's tile states and ticket, fresh for every attempt
+    for (uint32_t i = threadIdx.x; i < pbz_words; i += blockDim.x) pbz[i] = 0;
+    if (threadIdx.x == 0) misc_w[kMiscPBVoid] = 0;
+  }
   uio_block_body(frags, d_F, cap, pc, eacc, misc, lds, std_domain, payraw, a6);
   if (ts) {  // one stamp per workgroup, once all its waves are done
     __syncthreads();
@@ -1485,6 +1492,54 @@ __global__ void uio_elem_kernel(Fn fn, uint32_t n, Aff *__restrict__ out) {
 
 // Per op result (IOResult.checksum, ChunkReplica.cc:174,311; ChunkEngine.cc:61-67), each chunk's
 // final state (its last op), and the counters.
+// Position p's result (IOResult.checksum, ChunkReplica.cc:174,311; ChunkEngine.cc:61-67) from its
+// s-scan value, the chunk's final state when p is the chunk's last op, and the counter increments.
+__device__ __forceinline__ void result_at(uint32_t p, OpPos r, uint32_t c, bool last_of_chunk, const Aff &x,
+                                          const h3c_chunk_state *__restrict__ chunks,
+                                          h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks,
+                                          const uint32_t *__restrict__ t0v, uint8_t poly_type, uint32_t std_domain,
+                                          uint32_t poly, h3c_update_result *__restrict__ res,
+                                          const uint32_t *__restrict__ a6, uint32_t (&v)[8]) {
+  if (fold_failed(r, a6)) r.status = H3C_ERR_CHECKSUM_MISMATCH;  // checked in the block kernel
+  h3c_update_result o{};
+  o.status = r.status;
+  const bool applied = r.status == H3C_OK && r.sk != kS_IDENT;
+  if (r.status == H3C_ERR_INVALID_ARG) v[6] = 1;
+  if (r.status == H3C_ERR_CHECKSUM_MISMATCH) v[5] = 1;
+  if (applied) {
+    v[0] = r.ccode == kC_NONE;
+    v[1] = r.ccode == kC_REUSE;
+    v[3] = r.ccode == kC_READ;
+    v[4] = r.ccode == kC_RECALC;
+    v[2] = r.ccode == kC_COMBINE ? (std_domain ? r.ncomb : 1u) : 0u;
+  }
+  if (c < nchunks) {
+    const h3c_chunk_state cs = chunks[c];
+    const uint32_t t0 = t0v[c];
+    uint32_t s0 = std_domain ? ~cs.value : cs.value;
+    if (std_domain && cs.type != poly_type) s0 = t0;  // the engine's checksum is always crc32c of the bytes
+    const uint32_t s = hd_gf_mul(s0, x.m, poly) ^ x.e;
+    o.size = applied ? r.na : r.nb;
+    if (r.status == H3C_ERR_CHECKSUM_MISMATCH || r.status == H3C_ERR_CHUNK_SIZE_MISMATCH) {
+      // both fail after :174 set result.checksum = meta.checksum()
+      o.type = std_domain ? poly_type : r.tb;
+      o.value = std_domain ? 0u : s;  // engine.rs:303 returns before out_checksum is set
+    } else if (applied) {
+      o.type = r.ta;
+      o.value = std_domain ? ~s : s;
+    }
+    if (last_of_chunk) {
+      h3c_chunk_state fin = cs;
+      fin.size = o.size;
+      fin.type = r.ta;
+      fin.value = std_domain ? ~s : s;
+      chunks_out[c] = fin;
+    }
+  }
+  res[r.op] = o;
+}
+
+// Per op result, each chunk's final state (its last op), and the counters.
 __global__ void uio_result_kernel(const OpPos *__restrict__ pos, const uint32_t *__restrict__ skey, uint32_t n,
                                   const Aff *__restrict__ sscan, const h3c_chunk_state *__restrict__ chunks,
                                   h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks,
@@ -1497,52 +1552,220 @@ __global__ void uio_result_kernel(const OpPos *__restrict__ pos, const uint32_t 
     misc[kMiscOutF] = *d_F;
     misc[kMiscOutA6] = misc[kMiscA6];
   }
-  uint32_t c_none = 0, c_reuse = 0, c_comb = 0, c_read = 0, c_recalc = 0, c_mis = 0, c_inv = 0;
+  uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (p < n) {
-    OpPos r = pos[p];
     const uint32_t c = skey[p];
-    if (fold_failed(r, a6)) r.status = H3C_ERR_CHECKSUM_MISMATCH;  // checked in the block kernel
-    h3c_update_result o{};
-    o.status = r.status;
-    const bool applied = r.status == H3C_OK && r.sk != kS_IDENT;
-    if (r.status == H3C_ERR_INVALID_ARG) c_inv = 1;
-    if (r.status == H3C_ERR_CHECKSUM_MISMATCH) c_mis = 1;
-    if (applied) {
-      c_none = r.ccode == kC_NONE;
-      c_reuse = r.ccode == kC_REUSE;
-      c_read = r.ccode == kC_READ;
-      c_recalc = r.ccode == kC_RECALC;
-      c_comb = r.ccode == kC_COMBINE ? (std_domain ? r.ncomb : 1u) : 0u;
-    }
-    if (c < nchunks) {
-      const h3c_chunk_state cs = chunks[c];
-      const uint32_t t0 = t0v[c];
-      uint32_t s0 = std_domain ? ~cs.value : cs.value;
-      if (std_domain && cs.type != poly_type) s0 = t0;  // the engine's checksum is always crc32c of the bytes
-      const Aff x = sscan[p];
-      const uint32_t s = hd_gf_mul(s0, x.m, poly) ^ x.e;
-      o.size = applied ? r.na : r.nb;
-      if (r.status == H3C_ERR_CHECKSUM_MISMATCH || r.status == H3C_ERR_CHUNK_SIZE_MISMATCH) {
-        // both fail after :174 set result.checksum = meta.checksum()
-        o.type = std_domain ? poly_type : r.tb;
-        o.value = std_domain ? 0u : s;  // engine.rs:303 returns before out_checksum is set
-      } else if (applied) {
-        o.type = r.ta;
-        o.value = std_domain ? ~s : s;
-      }
-      if (p + 1 == n || skey[p + 1] != c) {
-        h3c_chunk_state fin = cs;
-        fin.size = o.size;
-        fin.type = r.ta;
-        fin.value = std_domain ? ~s : s;
-        chunks_out[c] = fin;
-      }
-    }
-    res[r.op] = o;
+    result_at(p, pos[p], c, p + 1 == n || skey[p + 1] != c, sscan[p], chunks, chunks_out, nchunks, t0v, poly_type,
+              std_domain, poly, res, a6, v);
   }
   __shared__ unsigned int sh[8];
-  const uint32_t v[8] = {c_none, c_reuse, c_comb, c_read, c_recalc, c_mis, c_inv, 0u};
   ctr_add_block(sh, ctr, v);
+}
+
+// ---- one-pass phase B: the t-scan, the s-scan and the results in one launch ----
+// uio_phaseb_kernel replaces the elem / scan_by_key / elem / scan_by_key / result launches: per
+// ticket-ordered tile of sorted positions, a segmented scan of the t maps in LDS, the carry from
+// earlier tiles by decoupled look-back (as in uio_front_kernel), the s maps from each op's t, a
+// second scan and look-back, then each position's result.  Its tile states and ticket are zeroed by
+// the block kernel that runs just before it, on every attempt.
+struct PhaseBSlot {
+  uint32_t flag[2];  // [0] t-scan, [1] s-scan: 0 nothing yet, 1 aggregate, 2 inclusive
+  uint32_t whole, key;
+  unsigned long long agg[2], incl[2];
+};
+static_assert(sizeof(PhaseBSlot) == 48, "PhaseBSlot is 48 bytes");
+constexpr uint32_t kPhaseBTile = 1024;
+
+__device__ __forceinline__ unsigned long long aff_bits(const Aff &a) {
+  return (unsigned long long)a.m | ((unsigned long long)a.e << 32);
+}
+__device__ __forceinline__ Aff aff_from(unsigned long long b) { return Aff{(uint32_t)b, (uint32_t)(b >> 32)}; }
+
+// Segmented inclusive scan of (head, map) over a 1024-thread tile; `sw` holds 3 x 16 words of LDS.
+__device__ __forceinline__ Aff aff_tile_scan(Aff x, uint32_t head, uint32_t poly, uint32_t lane, uint32_t wave,
+                                             uint32_t *sw) {
+  const AffOp op{poly};
+  uint32_t h = head;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const Aff y{(uint32_t)__shfl_up((int)x.m, o, 64), (uint32_t)__shfl_up((int)x.e, o, 64)};
+    const uint32_t yh = (uint32_t)__shfl_up((int)h, o, 64);
+    if (lane >= o && !h) {
+      x = op(y, x);
+      h = yh;
+    }
+  }
+  if (lane == 63) {
+    sw[wave] = x.m;
+    sw[16 + wave] = x.e;
+    sw[32 + wave] = h;
+  }
+  __syncthreads();
+  if (!h) {  // no head at or before this lane in its wave: the earlier waves' run continues into it
+    Aff pre{kOne, 0u};
+    uint32_t ph = 0;
+    for (uint32_t w = 0; w < wave; ++w) {
+      const Aff y{sw[w], sw[16 + w]};
+      if (sw[32 + w]) {
+        pre = y;
+        ph = 1;
+      } else {
+        pre = op(pre, y);
+      }
+    }
+    (void)ph;
+    x = op(pre, x);
+  }
+  __syncthreads();
+  return x;
+}
+
+// The carry into the tile's first run (key c0) of scan `which`, from earlier tiles (wave 0).
+__device__ Aff aff_carry(PhaseBSlot *slots, uint32_t k, uint32_t c0, int which, uint32_t poly, uint32_t lane,
+                         uint32_t *gave_up) {
+  const AffOp op{poly};
+  Aff carry{kOne, 0u};
+  bool done = k == 0;
+  for (int64_t j0 = (int64_t)k - 1; !done; j0 -= 64) {
+    const int64_t j = j0 - (int64_t)lane;
+    uint32_t fl = 3, key = 0xFFFFFFFFu, whole = 0;
+    unsigned long long a = 0;
+    if (j >= 0) {
+      PhaseBSlot &sl = slots[j];
+      fl = wait_flag(&sl.flag[which]);
+      key = ld_agent(&sl.key);
+      whole = ld_agent(&sl.whole);
+      a = ld_agent(fl == 2 ? &sl.incl[which] : &sl.agg[which]);
+    }
+    for (uint32_t l = 0; l < 64; ++l) {
+      const uint32_t fl_l = (uint32_t)__builtin_amdgcn_readlane((int)fl, (int)l);
+      if (fl_l == 3) {
+        done = true;
+        break;
+      }
+      if (fl_l == 0) {
+        if (lane == 0) *gave_up = 1;
+        done = true;
+        break;
+      }
+      if ((uint32_t)__builtin_amdgcn_readlane((int)key, (int)l) != c0) {
+        done = true;
+        break;
+      }
+      const Aff al{(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a, (int)l),
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a >> 32), (int)l)};
+      carry = op(al, carry);
+      if (fl_l == 2 || !__builtin_amdgcn_readlane((int)whole, (int)l)) {
+        done = true;
+        break;
+      }
+    }
+  }
+  return carry;
+}
+
+// s map of position p (SMapFn) given its t-scan value.
+__device__ __forceinline__ Aff s_map_at(const OpPos &r, uint32_t c, uint32_t nchunks, const Aff &t,
+                                        const uint32_t *__restrict__ t0v, const uint32_t *__restrict__ eacc,
+                                        const uint32_t *__restrict__ payraw, uint32_t p,
+                                        const PolyConsts *__restrict__ pc, const uint32_t *__restrict__ a6) {
+  if (c >= nchunks || fold_failed(r, a6)) return Aff{kOne, 0u};
+  switch (r.sk) {
+    case kS_ZERO:
+      return Aff{0u, 0u};
+    case kS_SET_T:
+      return Aff{0u, hd_gf_mul(t0v[c], t.m, pc->poly) ^ t.e};
+    case kS_APPEND:
+      return t_map(r, eacc, payraw, p, pc, a6);
+    default:
+      return Aff{kOne, 0u};
+  }
+}
+
+__global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
+    const OpPos *__restrict__ pos, const uint32_t *__restrict__ skey, uint32_t n, const uint32_t *__restrict__ eacc,
+    const uint32_t *__restrict__ payraw, const PolyConsts *__restrict__ pc, const uint32_t *__restrict__ a6,
+    const uint32_t *__restrict__ t0v, const h3c_chunk_state *__restrict__ chunks,
+    h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks, uint8_t poly_type, uint32_t std_domain,
+    h3c_update_result *__restrict__ res, unsigned long long *__restrict__ ctr, const uint32_t *__restrict__ d_F,
+    uint32_t *misc, PhaseBSlot *slots, uint32_t *ticket) {
+  constexpr uint32_t T = kPhaseBTile;
+  __shared__ uint32_t s_key[T + 1], sw[48], s_c[2], s_tile, s_void;
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const uint32_t poly = pc->poly;
+  const AffOp op{poly};
+  if (t == 0) {
+    s_tile = atomicAdd(ticket, 1u);
+    s_void = 0;
+  }
+  __syncthreads();
+  const uint32_t k = s_tile, p0 = k * T;
+  if (p0 >= n) return;  // (whole workgroup)
+  const uint32_t cnt = min(T, n - p0), tlast = cnt - 1;
+  const bool valid = t < cnt;
+  const uint32_t p = p0 + t;
+  const uint32_t c = valid ? skey[p] : 0xFFFFFFFFu;
+  OpPos r{};
+  if (valid) r = pos[p];
+  s_key[t] = c;
+  if (t == 0) s_key[T] = p0 + T < n ? skey[p0 + T] : 0xFFFFFFFFu;  // the next tile's first key
+  __syncthreads();
+  const uint32_t c0 = s_key[0];
+  const uint32_t head = (t == 0 || c != s_key[t - 1]) ? 1u : 0u;
+  PhaseBSlot &me = slots[k];
+  // t-scan
+  Aff tin = aff_tile_scan(valid ? t_map(r, eacc, payraw, p, pc, a6) : Aff{kOne, 0u}, head, poly, lane, wave, sw);
+  if (t == tlast) {
+    st_agent(&me.key, c);
+    st_agent(&me.whole, c == c0 ? 1u : 0u);
+    st_agent(&me.agg[0], aff_bits(tin));
+    pub_flag(&me.flag[0], 1u);
+  }
+  if (wave == 0) {
+    const Aff cy = aff_carry(slots, k, c0, 0, poly, lane, &s_void);
+    if (lane == 0) {
+      s_c[0] = cy.m;
+      s_c[1] = cy.e;
+    }
+  }
+  __syncthreads();
+  if (c == c0) tin = op(Aff{s_c[0], s_c[1]}, tin);
+  if (t == tlast) {
+    st_agent(&me.incl[0], aff_bits(tin));
+    pub_flag(&me.flag[0], 2u);
+  }
+  __syncthreads();  // (s_c is reused below)
+  // s-scan, from each op's t
+  Aff sin = aff_tile_scan(valid ? s_map_at(r, c, nchunks, tin, t0v, eacc, payraw, p, pc, a6) : Aff{kOne, 0u}, head,
+                          poly, lane, wave, sw);
+  if (t == tlast) {
+    st_agent(&me.agg[1], aff_bits(sin));
+    pub_flag(&me.flag[1], 1u);
+  }
+  if (wave == 0) {
+    const Aff cy = aff_carry(slots, k, c0, 1, poly, lane, &s_void);
+    if (lane == 0) {
+      s_c[0] = cy.m;
+      s_c[1] = cy.e;
+    }
+  }
+  __syncthreads();
+  if (c == c0) sin = op(Aff{s_c[0], s_c[1]}, sin);
+  if (t == tlast) {
+    st_agent(&me.incl[1], aff_bits(sin));
+    pub_flag(&me.flag[1], 2u);
+  }
+  // results
+  if (p == 0) {  // the pass's outcome, for the host's one read-back
+    misc[kMiscOutF] = *d_F;
+    misc[kMiscOutA6] = misc[kMiscA6];
+  }
+  uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (valid) result_at(p, r, c, s_key[t + 1] != c, sin, chunks, chunks_out, nchunks, t0v, poly_type, std_domain, poly,
+                       res, a6, v);
+  __shared__ unsigned int sh[8];
+  ctr_add_block(sh, ctr, v);
+  if (s_void && t == 0) atomicOr(&misc[kMiscPBVoid], 1u);  // the host reruns phase B the scan-based way
 }
 
 // t0 per chunk: the raw CRC of no bytes, the trusted stored value, or the bytes' CRC.
@@ -2009,6 +2232,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   // guess is the larger of 2n + 1024 and the calling thread's last batch, and a batch that
   // needs more redoes its fragment stage once with the count known)
   const uint32_t ntiles_front = (uint32_t)((n + kFrontTile - 1) / kFrontTile);
+  const uint32_t ntiles_pb = (uint32_t)((n + kPhaseBTile - 1) / kPhaseBTile);
+  const uint32_t pbz_words = ntiles_pb * (uint32_t)(sizeof(PhaseBSlot) / 4) + 1;
   thread_local uint32_t last_frags = 0;
   uint32_t cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * n + 1024, last_frags), 0x7FFFFFF0u);
   size_t sort_tmp = 0, scan_tmp = 0, pscan_tmp = 0, szscan_tmp = 0, ascan_tmp = 0;
@@ -2029,6 +2254,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       *d_eacc, *d_t0, *d_misc, *d_a6, *d_late, *d_lbase;
   SzTy *d_sz, *d_szscan;
   FrontSlot *d_fslot;
+  uint32_t *d_pbz;  // uio_phaseb_kernel: tile states, then its ticket
   OpPos *d_pos;
   Aff *d_tel, *d_tscan, *d_sel, *d_sscan;
   void *d_tmp;
@@ -2052,6 +2278,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     d_t0 = carve<uint32_t>(cur, C);
     d_misc = carve<uint32_t>(cur, kMiscN);
     d_fslot = carve<FrontSlot>(cur, std::max(ntiles_front, 1u));
+    d_pbz = carve<uint32_t>(cur, pbz_words);
     d_sz = carve<SzTy>(cur, n);
     d_szscan = carve<SzTy>(cur, n);
     d_pos = carve<OpPos>(cur, n);
@@ -2083,7 +2310,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   uint32_t nofold = 0;  // a redo after a failed A6 knows every verdict: no check moves into the block kernel
   // the one-pass front (uio_front_kernel) on the first attempt; test hook H3C_HOOK_UPD_FRONT = 1: the
   // scan-based stage (redone attempts always take that one)
-  const bool front = h3c_rt::hook(H3C_HOOK_UPD_FRONT) != 1;
+  const bool front = (h3c_rt::hook(H3C_HOOK_UPD_FRONT) & 1) == 0;
+  const bool pb1 = (h3c_rt::hook(H3C_HOOK_UPD_FRONT) & 2) == 0;  // phase B in one launch (uio_phaseb_kernel)
   // per attempt (fragment arrays for a guessed count, see below)
   uint32_t hcap = 256;
   FragDesc *d_frag = nullptr;
@@ -2206,7 +2434,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       }
       return H3C_OK;
     };
-    auto phase_b = [&](hipStream_t q) -> int {  // t' per op, then s' per op (two affine scans by chunk), results
+    auto phase_b_scans = [&](hipStream_t q) -> int {  // t' per op, then s' per op (two affine scans by chunk), results
       hipLaunchKernelGGL(uio_elem_kernel<TMapFn>, dim3(gb), dim3(tb), 0, q, TMapFn{d_pos, d_eacc, d_payraw, pc, d_a6},
                          n, d_tel);
       HIP_TRY(hipGetLastError());
@@ -2226,6 +2454,18 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       hipLaunchKernelGGL(uio_result_kernel, dim3(gb), dim3(tb), 0, q, d_pos, d_skey, n, d_sscan, d_chunks,
                          d_chunks_out, nchunks, d_t0, poly_type, stdf, poly, d_res, d_ctr, d_F, d_misc, d_a6);
       HIP_TRY(hipGetLastError());
+      return H3C_OK;
+    };
+    auto phase_b = [&](hipStream_t q) -> int {
+      if (pb1) {
+        hipLaunchKernelGGL(uio_phaseb_kernel, dim3(std::max(ntiles_pb, 1u)), dim3(kPhaseBTile), 0, q, d_pos, d_skey, n,
+                           d_eacc, d_payraw, pc, d_a6, d_t0, d_chunks, d_chunks_out, nchunks, poly_type, stdf, d_res,
+                           d_ctr, d_F, d_misc, reinterpret_cast<PhaseBSlot *>(d_pbz), d_pbz + pbz_words - 1);
+        HIP_TRY(hipGetLastError());
+      } else {
+        const int r = phase_b_scans(q);
+        if (r) return r;
+      }
       if (exact && nchunks) {
         hipLaunchKernelGGL(uio_stale_kernel, dim3((nchunks + tb - 1) / tb), dim3(tb), 0, q, d_chunks, nchunks, d_t0,
                            poly_type, stdf, d_ctr);
@@ -2244,7 +2484,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     auto block_kernel = [&](hipStream_t q, bool timed) -> int {
       hipLaunchKernelGGL(uio_block_kernel, dim3(blocks), dim3(kThreads), 0, q, d_frag, d_F, cap, pc, d_eacc, d_misc,
                          timed ? reinterpret_cast<unsigned long long *>(d_misc + kMiscT0) : nullptr, stdf, d_payraw,
-                         d_a6);
+                         d_a6, d_pbz, pbz_words, d_misc);
       HIP_TRY(hipGetLastError());
       return H3C_OK;
     };
@@ -2311,6 +2551,27 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       std::memcpy(&t1, h_F + (kMiscT1 - kMiscOutF), 8);
       const int khz = h3c_rt::device_wall_clock_khz(dev);
       if (t1 > t0 && khz > 0) h3c_rt::prof_add(H3C_PROF_UPDIO, (float)((double)(t1 - t0) / khz), alg_bytes);
+    }
+    if (h_F[kMiscPBVoid - kMiscOutF] && h_F[0] <= cap && !h_F[1]) {
+      // a phase-B tile gave up waiting (its CU starved by other work): the chunk bytes are
+      // written and right; redo phase B the scan-based way over the same state, then the epilogue
+      HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, st));
+      rc = phase_b_scans(st);
+      if (rc) return rc;
+      if (exact && nchunks) {
+        hipLaunchKernelGGL(uio_stale_kernel, dim3((nchunks + tb - 1) / tb), dim3(tb), 0, st, d_chunks, nchunks, d_t0,
+                           poly_type, stdf, d_ctr);
+        HIP_TRY(hipGetLastError());
+      }
+      HIP_TRY(hipMemcpyAsync(h_F, d_misc + kMiscOutF, 4 * (kMiscN - kMiscOutF), hipMemcpyDeviceToHost, st));
+      rc = epilogue(st, d_misc + kMiscOutF, cap);
+      if (rc) return rc;
+      const hipError_t se2 = hipStreamSynchronize(st);
+      if (se2 != hipSuccess) {
+        drain.armed = drain_aux.armed = false;
+        h3c_rt::set_error("h3c_update_ios", se2);
+        return H3C_ERR_HIP;
+      }
     }
     const uint32_t F = h_F[0], a6_failed = h_F[1];
     const bool void_pass = (a6_failed & kMiscVoid) != 0;  // a front tile gave up waiting: F means nothing

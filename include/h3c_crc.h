@@ -425,8 +425,9 @@ enum h3c_hook {
   H3C_HOOK_UPD_LOOKBACK = 5, /* h3c_update_blocks fused path: 1 makes the workgroup with ticket 1 give up
                                its look-back at once, as a starved wait would (the void-batch report:
                                *n_invalid = UINT32_MAX, counters.invalid = UINT64_MAX) */
-  H3C_HOOK_UPD_FRONT = 6     /* h3c_update_ios: 1 runs the sizes / cases / fragments as the scan-based
-                               stage (~10 launches) instead of the one-pass front kernel */
+  H3C_HOOK_UPD_FRONT = 6     /* h3c_update_ios, bit mask: 1 runs the sizes / cases / fragments as the
+                               scan-based stage (~10 launches) instead of the one-pass front kernel; 2 runs
+                               phase B (t / s scans, results) as 5 launches instead of one */
 };
 int h3c_test_hook(int key, uint64_t value);
 /* Engine-internal counters for tests: 0 = h3c_update_ios pipeline graph replays, 1 = graph

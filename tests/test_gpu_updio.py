@@ -197,11 +197,13 @@ def random_scenario(h3c, torch, dev, rng, nchunks, chunk_size, nops, align=1, ho
     return sc
 
 
-@pytest.fixture(params=["front", "scan"])
+@pytest.fixture(params=["onepass", "scan", "front_only"])
 def front_mode(request, h3c, hooks):
-    """The sizes / cases / fragments stage both ways: the one-pass front kernel (default) and the
-    scan-based stage (h3c_test_hook(H3C_HOOK_UPD_FRONT, 1), also what every redo runs)."""
-    hooks(h3c.HOOK_UPD_FRONT, 1 if request.param == "scan" else 0)
+    """The pipeline's two one-pass kernels against their scan-based forms: the front kernel
+    (sizes / cases / fragments / links) and the phase-B kernel (t / s scans, results) by default;
+    both scan-based (h3c_test_hook(H3C_HOOK_UPD_FRONT, 3), also what every redo's front runs); the
+    front kernel with the scan-based phase B (2)."""
+    hooks(h3c.HOOK_UPD_FRONT, {"onepass": 0, "scan": 3, "front_only": 2}[request.param])
     return request.param
 
 
