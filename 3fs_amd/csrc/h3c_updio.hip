@@ -1579,7 +1579,6 @@ constexpr uint32_t kPhaseBTile = 1024;
 __device__ __forceinline__ unsigned long long aff_bits(const Aff &a) {
   return (unsigned long long)a.m | ((unsigned long long)a.e << 32);
 }
-__device__ __forceinline__ Aff aff_from(unsigned long long b) { return Aff{(uint32_t)b, (uint32_t)(b >> 32)}; }
 
 // Segmented inclusive scan of (head, map) over a 1024-thread tile; `sw` holds 3 x 16 words of LDS.
 __device__ __forceinline__ Aff aff_tile_scan(Aff x, uint32_t head, uint32_t poly, uint32_t lane, uint32_t wave,
