@@ -740,6 +740,9 @@ __global__ void uio_heads_kernel(const uint32_t *__restrict__ prev, const uint32
 //      walk their bucket's list for the largest earlier fragment of their key.
 // Waits are bounded: a tile that gives up sets bit 1 of misc[kMiscA6] -- the pass is void, the
 // block kernel writes nothing and the host redoes the batch on the scan-based stage.
+#ifndef H3C_FRONT_TRACE
+#define H3C_FRONT_TRACE 0  // 1: tiles 0, 1, the middle one and the last print their step times (diagnostics)
+#endif
 constexpr uint32_t kFrontTile = 1024;
 constexpr uint32_t kFrontSpin = 1u << 21;
 constexpr uint32_t kMiscVoid = 2;  // misc[kMiscA6] bit: a front tile gave up waiting
@@ -868,6 +871,13 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
   if (p0 >= n) return;  // (whole workgroup)
   const uint32_t cnt = min(T, n - p0), tlast = cnt - 1;
   const uint32_t poly = pc->poly;
+#if H3C_FRONT_TRACE
+  uint64_t tr[8];
+  tr[0] = wall_clock64();
+#define FRONT_MARK(i) (tr[i] = wall_clock64())
+#else
+#define FRONT_MARK(i) ((void)0)
+#endif
   const bool valid = t < cnt;
   const uint32_t p = p0 + t;
   const uint32_t c = valid ? skey[p] : 0xFFFFFFFFu;
@@ -960,6 +970,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
     }
   }
   __syncthreads();
+  FRONT_MARK(1);
   const SzTy carry = sz_unpack(s_cv, s_cw);
   SzTy in = sz_unpack(xv, xw);
   if (c == c0) in = SzTyOp()(carry, in);
@@ -1036,6 +1047,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
     if (lane == 0) s_cnf = base;
   }
   __syncthreads();
+  FRONT_MARK(2);
   const uint32_t F0 = s_cnf, FT = s_fex[T];
   if (t == 0) {
     st_agent(&slots[k].nf_incl, F0 + tot);
@@ -1124,6 +1136,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
   stores_done();  // every thread's fkey / gnext / CAS traffic is out before the flag
   __syncthreads();
   if (t == 0) pub_flag(&slots[k].ln_flag, 1u);
+  FRONT_MARK(3);
 
   // 5. predecessors in earlier tiles, once every earlier tile has published its links
   if (wave == 0) {
@@ -1134,6 +1147,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
     }
   }
   __syncthreads();
+  FRONT_MARK(4);
   if (s_void) {  // the pass is void: no chain is run, the host redoes the batch
     if (t == 0) atomicOr(&misc[kMiscA6], kMiscVoid);
     return;
@@ -1150,6 +1164,15 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
     if (pr != kNil) st_agent(&frags[pr].next, g);
     else st_agent(&frags[g].flags, ld_agent(&frags[g].flags) | kFragHead);
   }
+#if H3C_FRONT_TRACE
+  __syncthreads();
+  FRONT_MARK(5);
+  const uint32_t ntl = (n + T - 1) / T;
+  if (t == 0 && (k < 2 || k == ntl / 2 || k + 1 == ntl))
+    printf("front tile %u start %llu sz %llu nf %llu links %llu wait %llu end %llu (ticks)\n", k,
+           (unsigned long long)tr[0], (unsigned long long)(tr[1] - tr[0]), (unsigned long long)(tr[2] - tr[0]),
+           (unsigned long long)(tr[3] - tr[0]), (unsigned long long)(tr[4] - tr[0]), (unsigned long long)(tr[5] - tr[0]));
+#endif
 }
 
 // ---- the block kernel ----
