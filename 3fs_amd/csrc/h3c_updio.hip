@@ -161,7 +161,7 @@ struct FragDesc {
   uint64_t blk;     // absolute address of the 4 KiB block
   uint64_t src;     // payload address of block offset 0 (meaningful on [w0, w1) only)
   uint32_t p;       // the op's position (E accumulator index)
-  uint32_t next;    // next fragment of the same block (kNil: last)
+  uint32_t rsv;     // (the next fragment of the same block is in its own array, fnext[])
   uint16_t w0, w1;  // new bytes
   uint16_t q0, q1;  // old bytes entering the CRC delta
   uint16_t z0, z1;  // zero fill
@@ -175,6 +175,14 @@ struct FragDesc {
 };
 static_assert(sizeof(FragDesc) == 64, "FragDesc is one 64-byte record");
 constexpr uint32_t kFragCrc = 1u, kFragWrite = 2u, kFragHead = 4u, kFragA6 = 8u;
+// kFragSolo: the op's only fragment.  The block kernel stores its delta CRC unshifted with the
+// shift beside it (eacc[2p], eacc[2p+1]) and phase B multiplies, one op per thread, instead of a
+// bit-serial GF(2) multiply issued by the whole wave for lane 0.  Other fragments XOR their
+// shifted contributions into eacc[2p] (eacc[2p+1] stays 0: nothing left to multiply).
+constexpr uint32_t kFragSolo = 16u;
+#ifndef H3C_UIO_SOLO
+#define H3C_UIO_SOLO 1  // 0: every fragment's contribution shifted in the block kernel (A/B)
+#endif
 
 // counters: a workgroup-aggregated add -- wave sums into LDS, one global atomic per counter
 // and workgroup (call from workgroup-uniform control flow; `sh` holds kCtrN slots)
@@ -226,10 +234,15 @@ __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t 
                                 uint32_t *__restrict__ eacc, unsigned long long *__restrict__ ctr,
                                 uint32_t *__restrict__ misc, uint32_t *__restrict__ a6, uint32_t *__restrict__ fz,
                                 uint32_t fz_words,
-                                uint32_t *__restrict__ hhead, uint32_t hcap) {
+                                uint32_t *__restrict__ hhead, uint32_t hcap, uint32_t *__restrict__ gnext,
+                                uint32_t *__restrict__ fnext, uint32_t fcap) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < fz_words) fz[i] = 0;        // the one-pass front's tile states (uio_front_kernel)
-  if (i < hcap) hhead[i] = 0xFFFFFFFFu;  // ... and its link hash's bucket heads
+  if (i < hcap) hhead[i] = 0xFFFFFFFFu;  // ... its link hash's bucket heads
+  if (i < fcap) {                     // ... its bucket lists' next pointers and the chains'
+    gnext[i] = 0xFFFFFFFEu;           // (kPending)
+    fnext[i] = 0xFFFFFFFFu;           // (kNil)
+  }
   if (i < kCtrN) ctr[i] = 0;
   if (i < kMiscN) misc[i] = i == kMiscT0 || i == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;
   // chunk items n + c for c < C = max(nchunks, 1) (the piece pass's NP = n + C items), then the
@@ -246,7 +259,8 @@ __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t 
   if (i == C) npieces[n + C] = 0;
   if (i >= n) return;
   paycrc0[i] = 0;  // XOR accumulators of the piece and block kernels
-  eacc[i] = 0;
+  eacc[2 * i] = 0;
+  eacc[2 * i + 1] = 0;
   a6[i] = 0;       // A6 verdicts (the early pass, the front / late checks, the block kernel)
   const h3c_update_io io = ios[i];
   uint32_t st = H3C_OK;
@@ -571,14 +585,13 @@ __device__ __forceinline__ uint32_t frag_count(const uint32_t *__restrict__ d_F,
 // *praw receives the raw payload CRC the op has when its check passes (its t-map needs it).
 __device__ __forceinline__ FragDesc make_frag(const OpPos &r, uint32_t p, uint32_t j, uint32_t c,
                                               const h3c_chunk_state &cs, const h3c_update_io &io,
-                                              const PolyConsts *__restrict__ pc, uint32_t std_domain,
+                                              const PolyConsts *__restrict__ pc, uint32_t std_domain, bool solo,
                                               uint64_t &key, uint32_t &praw) {
   const uint64_t blk = (((cs.base + r.r0) >> 12) + j) << 12;
   const int64_t rel = (int64_t)blk - (int64_t)cs.base;  // chunk offset of the block's first byte
   FragDesc d{};
   d.blk = blk;
   d.p = p;
-  d.next = kNil;
   d.k0 = rel_clamp(0, rel);
   d.k1 = rel_clamp(cs.chunk_size, rel);
   d.mult = dxpow8_fast((int64_t)r.na - (rel + (int64_t)kBlk), pc, pc->poly);
@@ -594,7 +607,7 @@ __device__ __forceinline__ FragDesc make_frag(const OpPos &r, uint32_t p, uint32
     if (r.tk == kT_DELTA) {
       range(o, e < (int64_t)r.nb ? e : (int64_t)r.nb, d.q0, d.q1);
       if (o > (int64_t)r.nb) range(r.nb, o, d.z0, d.z1);
-      if (d.w1 > d.w0) d.flags |= kFragCrc;
+      if (d.w1 > d.w0) d.flags |= kFragCrc | (solo ? kFragSolo : 0u);
     }
     if (d.w1 > d.w0 || d.z1 > d.z0) d.flags |= kFragWrite;
     if (r.pf & kPosFold) {  // the op's only fragment: its A6 check happens in the block kernel
@@ -608,7 +621,7 @@ __device__ __forceinline__ FragDesc make_frag(const OpPos &r, uint32_t p, uint32
     }
   } else if (r.na < r.nb) {  // truncate: the cut bytes leave the CRC
     range(r.na, r.nb, d.q0, d.q1);
-    if (d.q1 > d.q0) d.flags |= kFragCrc;
+    if (d.q1 > d.q0) d.flags |= kFragCrc | (solo ? kFragSolo : 0u);
   } else {  // grow: zero fill
     range(r.nb, r.na, d.z0, d.z1);
     if (d.z1 > d.z0) d.flags |= kFragWrite;
@@ -622,9 +635,10 @@ __global__ void uio_frag_kernel(const OpPos *__restrict__ pos, const uint32_t *_
                                 const h3c_chunk_state *__restrict__ chunks, FragDesc *__restrict__ frags,
                                 uint64_t *__restrict__ fkey, const PolyConsts *__restrict__ pc,
                                 uint32_t *__restrict__ hhead, uint32_t hcap, uint32_t std_domain,
-                                uint32_t *__restrict__ payraw) {
+                                uint32_t *__restrict__ payraw, uint32_t *__restrict__ fnext) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < hcap) hhead[k] = kNil;  // the link hash's bucket heads (uio_tlink_kernel runs next)
+  if (k < cap) fnext[k] = kNil;   // chain next pointers (uio_heads_kernel)
   const uint32_t F = frag_count(fbase + n, cap);
   if (k >= F) return;
   uint32_t a = 0, b = n;  // the last p with fbase[p] <= k
@@ -637,7 +651,9 @@ __global__ void uio_frag_kernel(const OpPos *__restrict__ pos, const uint32_t *_
   const uint32_t c = skey[p];
   uint64_t key;
   uint32_t praw = 0;
-  const FragDesc d = make_frag(r, p, k - fbase[p], c, chunks[c], ios[r.op], pc, std_domain, key, praw);
+  const FragDesc d = make_frag(r, p, k - fbase[p], c, chunks[c], ios[r.op], pc, std_domain,
+                               H3C_UIO_SOLO && fbase[p + 1] - fbase[p] == 1,
+                               key, praw);
   frags[k] = d;
   fkey[k] = key;
   if (d.flags & kFragA6) payraw[r.op] = praw;
@@ -712,12 +728,12 @@ __global__ void uio_resolve_kernel(const uint64_t *__restrict__ fkey, const uint
 // next pointers and chain-head flags (a fragment with no predecessor on its block starts a
 // chain; the block kernel walks the fragments and starts at the flagged ones)
 __global__ void uio_heads_kernel(const uint32_t *__restrict__ prev, const uint32_t *__restrict__ d_F, uint32_t cap,
-                                 FragDesc *__restrict__ frags) {
+                                 FragDesc *__restrict__ frags, uint32_t *__restrict__ fnext) {
   const uint32_t F = frag_count(d_F, cap);
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= F) return;
   const uint32_t p = prev[k];
-  if (p != kNil) frags[p].next = k;
+  if (p != kNil) fnext[p] = k;
   else frags[k].flags |= kFragHead;
 }
 
@@ -745,6 +761,7 @@ __global__ void uio_heads_kernel(const uint32_t *__restrict__ prev, const uint32
 #endif
 constexpr uint32_t kFrontTile = 1024;
 constexpr uint32_t kFrontSpin = 1u << 21;
+constexpr uint32_t kPending = 0xFFFFFFFEu;  // gnext[] entry pushed, its next pointer not yet stored
 constexpr uint32_t kMiscVoid = 2;  // misc[kMiscA6] bit: a front tile gave up waiting
 struct FrontSlot {
   uint32_t sz_flag, nf_flag, ln_flag, whole;  // 0: nothing yet, 1: aggregate, 2: inclusive (ln: 1 = published)
@@ -769,16 +786,6 @@ __device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)
 __device__ __forceinline__ void pub_flag(uint32_t *f, uint32_t v) {
   stores_done();  // this thread's payload stores are at the coherence point before the flag
   st_agent(f, v);
-}
-// A fragment record written through to the coherence point: another tile may set its next
-// pointer later (a plain store would leave a dirty L2 line on this XCD whose write-back at the
-// kernel's end could land after that tile's store).
-__device__ __forceinline__ void store_frag(FragDesc *dst, const FragDesc &d) {
-  uint64_t w[8];
-  __builtin_memcpy(w, &d, 64);
-  unsigned long long *q = reinterpret_cast<unsigned long long *>(dst);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) st_agent(q + k, (unsigned long long)w[k]);
 }
 __device__ __forceinline__ uint64_t sz_bits(const SzTy &a) {
   uint64_t b;
@@ -851,7 +858,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
     uint8_t poly_type, uint32_t std_domain, const PolyConsts *__restrict__ pc, OpPos *__restrict__ pos,
     uint32_t *__restrict__ nfrag, uint32_t *__restrict__ fbase, uint32_t *__restrict__ late,
     uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6, uint32_t *misc, FragDesc *frags, uint64_t *fkey,
-    uint32_t cap, uint32_t *hhead, uint32_t hmask, uint32_t *gnext, uint32_t *prev, FrontSlot *slots) {
+    uint32_t cap, uint32_t *hhead, uint32_t hmask, uint32_t *gnext, uint32_t *prev, uint32_t *fnext, FrontSlot *slots) {
   constexpr uint32_t T = kFrontTile, NW = T / 64;
   __shared__ uint32_t s_key[T], s_v[T], s_w[T];         // keys; the inclusive maps (v, packed)
   __shared__ uint32_t s_fex[T + 1];                     // exclusive fragment counts of the tile
@@ -1095,8 +1102,9 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
       const uint32_t cq = s_key[a];
       uint64_t k64;
       uint32_t praw = 0;
-      const FragDesc d = make_frag(rq, p0 + a, kk - s_fex[a], cq, chunks[cq], ios[rq.op], pc, std_domain, k64, praw);
-      store_frag(&frags[g], d);
+      const FragDesc d = make_frag(rq, p0 + a, kk - s_fex[a], cq, chunks[cq], ios[rq.op], pc, std_domain,
+                                   H3C_UIO_SOLO && s_fex[a + 1] - s_fex[a] == 1, k64, praw);
+      frags[g] = d;  // plain stores: only this thread writes the record (its head flag below)
       st_agent(reinterpret_cast<unsigned long long *>(&fkey[g]), (unsigned long long)k64);  // read by later tiles
       if (d.flags & kFragA6) payraw[rq.op] = praw;
       key = k64;
@@ -1118,20 +1126,19 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
       }
     if (fv) {
       prev[g] = pin == kNil ? kNil : F0 + s0 + pin;
-      if (lastk) {  // publish: the next pointer before the head, so a concurrent reader never sees a gap
+      // next pointers are written through: a later tile may set this tile's last ones (step 5)
+      if (pin != kNil) st_agent(&fnext[F0 + s0 + pin], g);
+      if (lastk) {
+        // publish on the bucket: this entry's key at the coherence point first, then one exchange
+        // for the old head, then the next pointer (gnext[] starts as kPending, prep kernel: a
+        // reader that reaches this entry before its next pointer lands waits for it)
         uint32_t *bucket = &hhead[(key_hash(key) >> 7) & hmask];
-        uint32_t old = ld_agent(bucket);
-        do {
-          st_agent(&gnext[g], old);
-          stores_done();
-        } while (!__hip_atomic_compare_exchange_strong(bucket, &old, g, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT));
+        stores_done();
+        const uint32_t old = __hip_atomic_exchange(bucket, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st_agent(&gnext[g], old);
       }
     }
-    stores_done();
-    __syncthreads();  // the sub-tile's records are written before their next pointers
-    if (fv && pin != kNil) st_agent(&frags[F0 + s0 + pin].next, g);
-    __syncthreads();
+    __syncthreads();  // (the sub-tile's LDS groups are reused)
   }
   stores_done();  // every thread's fkey / gnext / CAS traffic is out before the flag
   __syncthreads();
@@ -1157,12 +1164,29 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
     if (kk >= FT || g >= cap || prev[g] != kNil) continue;
     const unsigned long long key = ld_agent(reinterpret_cast<unsigned long long *>(&fkey[g]));
     uint32_t pr = kNil;
-    // a published entry's next pointer reached the coherence point before the CAS that made the
-    // entry reachable (stores_done), and each load here depends on the one before
-    for (uint32_t j = ld_agent(&hhead[(key_hash(key) >> 7) & hmask]); j != kNil; j = ld_agent(&gnext[j]))
+    bool gave_up = false;
+    // an entry's key reached the coherence point before the exchange that made it reachable, and
+    // each load here depends on the one before; a next pointer still kPending is waited for
+    for (uint32_t j = ld_agent(&hhead[(key_hash(key) >> 7) & hmask]); j != kNil;) {
       if (j < g && ld_agent(reinterpret_cast<unsigned long long *>(&fkey[j])) == key && (pr == kNil || j > pr)) pr = j;
-    if (pr != kNil) st_agent(&frags[pr].next, g);
-    else st_agent(&frags[g].flags, ld_agent(&frags[g].flags) | kFragHead);
+      uint32_t nx = ld_agent(&gnext[j]);
+      for (uint32_t spins = 0; nx == kPending && !gave_up; nx = ld_agent(&gnext[j])) {
+        __builtin_amdgcn_s_sleep(1);
+        gave_up = ++spins > kFrontSpin;
+      }
+      if (gave_up) break;
+      j = nx;
+    }
+    if (gave_up) {
+      atomicOr(&misc[kMiscA6], kMiscVoid);  // the pass is void (the block kernel skips it)
+      continue;
+    }
+    if (pr != kNil) {
+      prev[g] = pr;
+      st_agent(&fnext[pr], g);
+    } else {
+      frags[g].flags |= kFragHead;  // this thread wrote the record (step 4)
+    }
   }
 #if H3C_FRONT_TRACE
   __syncthreads();
@@ -1242,6 +1266,18 @@ __device__ __forceinline__ uint4 load_new(uint64_t src, uint32_t row, uint32_t r
   return row_full(row, w0, w1) ? v : and4(v, mask16(rel, w0, w1));
 }
 
+// Waves per block-kernel workgroup (one per CU: the LDS tables take 156 KiB).  16 waves leave
+// 128 registers a lane; 12 leave 168.
+#ifndef H3C_UIO_BLOCK_WAVES
+#define H3C_UIO_BLOCK_WAVES 16
+#endif
+constexpr uint32_t kBlkWaves = H3C_UIO_BLOCK_WAVES, kBlkThreads = 64 * kBlkWaves;
+#ifndef H3C_UIO_SFIELDS
+#define H3C_UIO_SFIELDS 1  // block kernel: per-fragment fields by scalar loads (0: all in the lanes)
+#endif
+#ifndef H3C_UIO_FOLD_ILP
+#define H3C_UIO_FOLD_ILP 0  // 1: the fold check's CRC and the delta's interleaved (spills: 362 vs 288 us, r03c_updio_ab)
+#endif
 #ifndef H3C_UIO_NT_STORES
 #define H3C_UIO_NT_STORES 1
 #endif
@@ -1295,6 +1331,35 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
                                                    const char *lb, const LaneLut &L, const uint32_t *red, uint32_t poly,
                                                    uint32_t *__restrict__ eacc, const FoldIo &fx) {
   const uint32_t w0 = w & 0xFFFFu, w1 = w >> 16, q0 = q & 0xFFFFu, q1 = q >> 16, z0 = z & 0xFFFFu, z1 = z >> 16;
+#if H3C_UIO_FOLD_ILP
+  if ((flags & (kFragA6 | kFragCrc)) == (kFragA6 | kFragCrc)) {
+    // the check and the delta side by side: two independent stream sets per row and one
+    // two-way fold, so the LDS round trips of the two folds' Horner / tree chains overlap
+    Streams s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t rel = 1024u * r + 16u * lane;
+      const uint4 old = row_full(r, q0, q1) ? img[r] : and4(img[r], row_mask(r, rel, q0, q1));
+      consume(s2[0], nw[r], lb, L);
+      consume(s2[1], xor4(nw[r], old), lb, L);
+    }
+    uint32_t fv[2];
+    wave_fold_tab_n<2>(s2, lane, red, fv);
+    if (__builtin_amdgcn_readfirstlane(fv[0]) != fx.expect) {
+      if (lane == 0) fx.a6[fx.op] = 1u;
+      return 0u;
+    }
+    if (lane == 0) {
+      if (H3C_UIO_SOLO && (flags & kFragSolo)) {
+        *reinterpret_cast<uint2 *>(eacc + 2 * p) = make_uint2(fv[1], mult);
+      } else {
+        const uint32_t cv = dgf_mul_fast(fv[1], mult, poly);
+        if (cv) atomicXor(&eacc[2 * p], cv);
+      }
+    }
+    flags &= ~(kFragA6 | kFragCrc);
+  }
+#endif
   if (flags & kFragA6) {
     Streams sn{0, 0, 0, 0};  // the new bytes alone (one stream set at a time: the registers are full)
 #pragma unroll
@@ -1316,8 +1381,12 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
     }
     const uint32_t v = wave_fold_tab(st, lane, red);
     if (lane == 0) {
-      const uint32_t cv = dgf_mul_fast(v, mult, poly);
-      if (cv) atomicXor(&eacc[p], cv);
+      if (H3C_UIO_SOLO && (flags & kFragSolo)) {
+        *reinterpret_cast<uint2 *>(eacc + 2 * p) = make_uint2(v, mult);
+      } else {
+        const uint32_t cv = dgf_mul_fast(v, mult, poly);
+        if (cv) atomicXor(&eacc[2 * p], cv);
+      }
     }
   }
   uint32_t dirty = 0;
@@ -1345,26 +1414,88 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
 // keeping the next head's block and payload rows in flight while the current chain is folded
 // and stored.  Chains longer than one fragment (blocks written more than once in the batch)
 // continue with uniform loads.
-__device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frags, const uint32_t *__restrict__ d_F,
+__device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frags, const uint32_t *__restrict__ fnext,
+                                               const uint32_t *__restrict__ d_F,
                                                uint32_t cap, const PolyConsts *__restrict__ pc,
                                                uint32_t *__restrict__ eacc, const uint32_t *__restrict__ misc,
                                                uint32_t *lds, uint32_t std_domain, uint32_t *__restrict__ payraw,
                                                uint32_t *__restrict__ a6) {
-  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
+  for (int i = threadIdx.x; i < kLdsWords; i += kBlkThreads) lds[i] = fill_value(pc, i);
   const uint32_t *red_g = &pc->red[0][0][0];
-  for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  for (int i = threadIdx.x; i < kRedWords; i += kBlkThreads) lds[kLdsWords + i] = red_g[i];
   __syncthreads();
   const uint32_t F = misc[kMiscA6] ? 0u : frag_count(d_F, cap);  // a failed A6: this pass writes nothing
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint64_t gw = (uint64_t)blockIdx.x * kBlkWaves + wave;
+  const uint64_t nw = (uint64_t)gridDim.x * kBlkWaves;
   const uint32_t lo = (uint32_t)(gw * F / nw), hi = (uint32_t)((gw + 1) * F / nw);
   if (lo >= hi) return;
   const uint32_t poly = pc->poly;
   const LaneLut L = make_lut(lane);
+#if H3C_UIO_SFIELDS
+  // Every field comes from uniform (scalar) loads: the wave walks its fragments in order, the
+  // rows of fragment g + 1 in flight while g is processed and the addresses of g + 2 loaded
+  // meanwhile.  No per-lane copies of the records: 128 VGPRs hold the rows with no spill (a
+  // spill's reload at the loop top waits, in vmcnt order, for the previous stores' acks).
+  const uint4 *rec = reinterpret_cast<const uint4 *>(frags);  // 4 x 16 bytes per record
+  auto addr_of = [&](uint32_t g, uint64_t &blk, uint64_t &src, uint32_t &w, uint32_t &k) {
+    const uint4 a = rec[4 * (size_t)g], b = rec[4 * (size_t)g + 1], c = rec[4 * (size_t)g + 2];
+    blk = (uint64_t)a.x | ((uint64_t)a.y << 32);
+    src = (uint64_t)a.z | ((uint64_t)a.w << 32);
+    w = b.z;
+    k = c.y;
+  };
+  uint64_t c_blk, c_src, n_blk = 0, n_src = 0;
+  uint32_t c_w, c_k, n_w = 0, n_k = 0;
+  addr_of(lo, c_blk, c_src, c_w, c_k);
+  BlockRows cur, nxt;
+  load_task_rows(c_blk, c_k & 0xFFFFu, c_k >> 16, c_src, c_w & 0xFFFFu, c_w >> 16, lane, cur);
+  if (lo + 1 < hi) addr_of(lo + 1, n_blk, n_src, n_w, n_k);
+  for (uint32_t g = lo; g < hi; ++g) {
+    const uint4 f1 = rec[4 * (size_t)g + 1], f2 = rec[4 * (size_t)g + 2];  // {p, rsv, w, q}, {z, k, mult, flags}
+    const uint64_t blk = c_blk;
+    const uint32_t kk = c_k;
+    if (g + 1 < hi) {
+      // the next fragment's rows in flight while this one is processed (a fragment that is not a
+      // chain head -- a later write to an already written block -- loads them in vain)
+      load_task_rows(n_blk, n_k & 0xFFFFu, n_k >> 16, n_src, n_w & 0xFFFFu, n_w >> 16, lane, nxt);
+      c_blk = n_blk;
+      c_k = n_k;
+      if (g + 2 < hi) addr_of(g + 2, n_blk, n_src, n_w, n_k);
+    }
+    const uint32_t flags = f2.w;
+    if (flags & kFragHead) {
+      const uint32_t k0 = kk & 0xFFFFu, k1 = kk >> 16;
+      FoldIo fx{0, 0, 0, std_domain, pc, payraw, a6};
+      if (flags & kFragA6) {  // a fold fragment's op / checksum / length
+        const uint4 f3 = rec[4 * (size_t)g + 3];
+        fx.op = f3.x;
+        fx.expect = f3.y;
+        fx.len = f3.z;
+      }
+      uint32_t dirty = apply_fragment(cur.img, cur.nw, flags, f1.z, f1.w, f2.x, f2.z, f1.x, lane, lb, L, red, poly, eacc,
+                                      fx);
+      for (uint32_t f = fnext[g]; f != kNil;) {  // later fragments of the same block
+        const FragDesc d = frags[f];
+        uint4 nw4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) nw4[r] = load_new(d.src, r, 1024u * r + 16u * lane, d.w0, d.w1);
+        const FoldIo fd{d.op, d.expect, d.len, std_domain, pc, payraw, a6};
+        dirty |= apply_fragment(cur.img, nw4, d.flags, (uint32_t)d.w0 | ((uint32_t)d.w1 << 16),
+                                (uint32_t)d.q0 | ((uint32_t)d.q1 << 16), (uint32_t)d.z0 | ((uint32_t)d.z1 << 16),
+                                d.mult, d.p, lane, lb, L, red, poly, eacc, fd);
+        f = fnext[f];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (dirty & (1u << r)) store_masked(blk, 1024u * r + 16u * lane, cur.img[r], k0, k1);
+    }
+    cur = nxt;
+  }
+#else
   auto rl = [](uint32_t v, uint32_t t) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane(v, t); };
   auto rl64 = [](uint64_t v, uint32_t t) -> uint64_t {
     return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t) |
@@ -1380,7 +1511,7 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
       m_blk = d.blk;
       m_src = d.src;
       m_p = d.p;
-      m_next = d.next;
+      m_next = fnext[g0 + lane];
       m_w = (uint32_t)d.w0 | ((uint32_t)d.w1 << 16);
       m_q = (uint32_t)d.q0 | ((uint32_t)d.q1 << 16);
       m_z = (uint32_t)d.z0 | ((uint32_t)d.z1 << 16);
@@ -1423,7 +1554,7 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
           dirty |= apply_fragment(cur.img, nw4, d.flags, (uint32_t)d.w0 | ((uint32_t)d.w1 << 16),
                                   (uint32_t)d.q0 | ((uint32_t)d.q1 << 16), (uint32_t)d.z0 | ((uint32_t)d.z1 << 16),
                                   d.mult, d.p, lane, lb, L, red, poly, eacc, fd);
-          f = d.next;
+          f = fnext[f];
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -1432,10 +1563,11 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
       cur = nxt;
     }
   }
+#endif
 }
 
 // ts (nullable): [0] the earliest workgroup start, [1] the latest workgroup end (wall clock).
-__global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__restrict__ frags,
+__global__ __launch_bounds__(kBlkThreads) void uio_block_kernel(const FragDesc *__restrict__ frags, const uint32_t *__restrict__ fnext,
                                                              const uint32_t *__restrict__ d_F, uint32_t cap,
                                                              const PolyConsts *__restrict__ pc,
                                                              uint32_t *__restrict__ eacc,
@@ -1450,7 +1582,7 @@ __global__ __launch_bounds__(kThreads) void uio_block_kernel(const FragDesc *__r
     for (uint32_t i = threadIdx.x; i < pbz_words; i += blockDim.x) pbz[i] = 0;
     if (threadIdx.x == 0) misc_w[kMiscPBVoid] = 0;
   }
-  uio_block_body(frags, d_F, cap, pc, eacc, misc, lds, std_domain, payraw, a6);
+  uio_block_body(frags, fnext, d_F, cap, pc, eacc, misc, lds, std_domain, payraw, a6);
   if (ts) {  // one stamp per workgroup, once all its waves are done
     __syncthreads();
     if (threadIdx.x == 0) atomicMax(&ts[1], (unsigned long long)wall_clock64());
@@ -1465,7 +1597,10 @@ __device__ __forceinline__ bool fold_failed(const OpPos &r, const uint32_t *__re
 __device__ __forceinline__ Aff t_map(const OpPos &r, const uint32_t *__restrict__ eacc, const uint32_t *__restrict__ payraw,
                                      uint32_t p, const PolyConsts *__restrict__ pc, const uint32_t *__restrict__ a6) {
   if (fold_failed(r, a6)) return Aff{kOne, 0u};
-  if (r.tk == kT_DELTA) return Aff{dxpow8_fast((int64_t)r.na - (int64_t)r.nb, pc, pc->poly), eacc[p]};
+  if (r.tk == kT_DELTA) {
+    const uint2 w = *reinterpret_cast<const uint2 *>(eacc + 2 * p);  // (a solo fragment's shift: kFragSolo)
+    return Aff{dxpow8_fast((int64_t)r.na - (int64_t)r.nb, pc, pc->poly), w.y ? dgf_mul_fast(w.x, w.y, pc->poly) : w.x};
+  }
   if (r.tk == kT_FULL) return Aff{0u, payraw[r.op]};
   return Aff{kOne, 0u};
 }
@@ -2279,7 +2414,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   uint32_t *d_pbz;  // uio_phaseb_kernel: tile states, then its ticket
   OpPos *d_pos;
   Aff *d_tel, *d_tscan, *d_sel, *d_sscan;
-  void *d_tmp;
+  void *d_tmp, *d_ptmp;
   auto layout = [&](char *base) -> size_t {  // one layout, run with base 0 to size the lease
     char *cur = base;
     d_status = carve<uint32_t>(cur, n);
@@ -2296,7 +2431,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     d_fbase = carve<uint32_t>(cur, N1);
     d_late = carve<uint32_t>(cur, N1);
     d_lbase = carve<uint32_t>(cur, N1);
-    d_eacc = carve<uint32_t>(cur, n);
+    d_eacc = carve<uint32_t>(cur, 2 * (size_t)n);
     d_t0 = carve<uint32_t>(cur, C);
     d_misc = carve<uint32_t>(cur, kMiscN);
     d_fslot = carve<FrontSlot>(cur, std::max(ntiles_front, 1u));
@@ -2309,6 +2444,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     d_sel = carve<Aff>(cur, n);
     d_sscan = carve<Aff>(cur, n);
     d_tmp = carve<char>(cur, tmp_bytes);
+    d_ptmp = carve<char>(cur, pscan_tmp);
     return (size_t)(cur - base);
   };
   h3c_rt::DeviceLease lease1(dev, layout(nullptr));
@@ -2338,7 +2474,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   uint32_t hcap = 256;
   FragDesc *d_frag = nullptr;
   uint64_t *d_fkey = nullptr;
-  uint32_t *d_prev = nullptr, *d_gnext = nullptr, *d_hhead = nullptr;
+  uint32_t *d_prev = nullptr, *d_gnext = nullptr, *d_hhead = nullptr, *d_fnext = nullptr;
   // sizes and types per op (a segmented scan), the reference's cases, fragment counts
   auto phase_sizes = [&](hipStream_t q) -> int {
     hipLaunchKernelGGL(uio_sz_elem_kernel, dim3(gb), dim3(tb), 0, q, d_ios, d_order, n, d_status, poly_type, stdf,
@@ -2362,23 +2498,26 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     const uint32_t prep_threads = std::max<uint32_t>(std::max<uint32_t>(n, nchunks), std::max(fz_words, front ? hcap : 0u));
     hipLaunchKernelGGL(uio_prep_kernel, dim3((prep_threads + tb) / tb), dim3(tb), 0, q, d_ios, n, d_chunks, nchunks,
                        poly_type, stdf, exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc, d_a6,
-                       reinterpret_cast<uint32_t *>(d_fslot), fz_words, d_hhead, front ? hcap : 0u);
+                       reinterpret_cast<uint32_t *>(d_fslot), fz_words, d_hhead, front ? hcap : 0u, d_gnext, d_fnext,
+                       front ? cap : 0u);
     HIP_TRY(hipGetLastError());
+    // second stream, forked here: the piece counts' scan (its own scratch), one piece-CRC pass over
+    // the payloads that are not fold candidates and the chunks CRC'd from their bytes (before the
+    // block kernel overwrites them), then A6 and t0; this stream sorts the ops and runs the sizes
+    // and fragment stages meanwhile.  (With the fold checks in the block kernel the piece pass is
+    // short; in round 2, when it carried every payload, the scan ran before the fork.)
+    HIP_TRY(hipEventRecord(aux->ready, q));
+    HIP_TRY(hipStreamWaitEvent(aux->st, aux->ready, 0));
     {
-      size_t t = tmp_bytes;
-      HIP_TRY(rocprim::exclusive_scan(d_tmp, t, d_np, d_pbase, 0u, NP + 1, rocprim::plus<uint32_t>(), q));
+      size_t t = pscan_tmp;
+      HIP_TRY(rocprim::exclusive_scan(d_ptmp, t, d_np, d_pbase, 0u, NP + 1, rocprim::plus<uint32_t>(), aux->st));
     }
-    // The ops' sort first, alone: its latency-bound passes took ~70 us beside the bandwidth-bound
-    // payload-CRC kernel and ~12 us before it (profiles/r02_updio_sort_first_ab.txt)
+    // The ops' sort alone on this stream: its latency-bound passes took ~70 us beside the
+    // bandwidth-bound payload-CRC kernel and ~12 us before it (profiles/r02_updio_sort_first_ab.txt)
     {
       size_t t = tmp_bytes;
       HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, q));
     }
-    // second stream: one piece-CRC pass over the payloads and the chunks CRC'd from their bytes
-    // (before the block kernel overwrites them), then A6 and t0; this stream runs the sizes and
-    // fragment stages meanwhile
-    HIP_TRY(hipEventRecord(aux->ready, q));
-    HIP_TRY(hipStreamWaitEvent(aux->st, aux->ready, 0));
     int r = h3c_rt::launch_uio_piece_crc(aux->st, dev, poly_type, d_ios, n, d_chunks, nchunks, d_pbase, d_pbase + NP,
                                          d_paycrc0);
     if (r) return r;
@@ -2420,6 +2559,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       d_fkey = carve<uint64_t>(c2, cap);
       d_prev = carve<uint32_t>(c2, cap);
       d_gnext = carve<uint32_t>(c2, cap);
+      d_fnext = carve<uint32_t>(c2, cap);
       d_hhead = carve<uint32_t>(c2, hcap);
       return (size_t)(c2 - base);
     };
@@ -2434,14 +2574,14 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         hipLaunchKernelGGL(uio_front_kernel, dim3(std::max(ntiles_front, 1u)), dim3(kFrontTile), 0, q, d_ios, d_order,
                            d_skey, n, d_chunks, nchunks, d_status, poly_type, stdf, pc, d_pos, d_nfrag, d_fbase,
                            d_late, d_payraw, d_a6, d_misc, d_frag, d_fkey, cap, d_hhead, hcap - 1, d_gnext, d_prev,
-                           d_fslot);
+                           d_fnext, d_fslot);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipStreamWaitEvent(q, aux->done, 0));  // the early A6 verdicts and t0
         return H3C_OK;
       }
       if (attempt) HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, q));  // the first attempt's counters
       hipLaunchKernelGGL(uio_frag_kernel, dim3((std::max(cap, hcap) + tb - 1) / tb), dim3(tb), 0, q, d_pos, d_fbase,
-                         n, cap, d_ios, d_skey, d_chunks, d_frag, d_fkey, pc, d_hhead, hcap, stdf, d_payraw);
+                         n, cap, d_ios, d_skey, d_chunks, d_frag, d_fkey, pc, d_hhead, hcap, stdf, d_payraw, d_fnext);
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(uio_tlink_kernel, dim3((cap + kLinkTile - 1) / kLinkTile), dim3(kLinkTile), 0, q, d_fkey,
                          d_F, cap, d_hhead, hcap - 1, d_gnext, d_prev);
@@ -2449,7 +2589,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       hipLaunchKernelGGL(uio_resolve_kernel, dim3(fb), dim3(tb), 0, q, d_fkey, d_F, cap, d_hhead, hcap - 1, d_gnext,
                          d_prev);
       HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(uio_heads_kernel, dim3(fb), dim3(tb), 0, q, d_prev, d_F, cap, d_frag);
+      hipLaunchKernelGGL(uio_heads_kernel, dim3(fb), dim3(tb), 0, q, d_prev, d_F, cap, d_frag, d_fnext);
       HIP_TRY(hipGetLastError());
       if (attempt == 0) {  // the A6 verdicts (the block kernel reads the flag) and t0
         HIP_TRY(hipStreamWaitEvent(q, aux->done, 0));
@@ -2504,7 +2644,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     // profiles/r02_updio_one_graph_ab.txt.)
     const uint32_t blocks = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
     auto block_kernel = [&](hipStream_t q, bool timed) -> int {
-      hipLaunchKernelGGL(uio_block_kernel, dim3(blocks), dim3(kThreads), 0, q, d_frag, d_F, cap, pc, d_eacc, d_misc,
+      hipLaunchKernelGGL(uio_block_kernel, dim3(blocks), dim3(kBlkThreads), 0, q, d_frag, d_fnext, d_F, cap, pc, d_eacc, d_misc,
                          timed ? reinterpret_cast<unsigned long long *>(d_misc + kMiscT0) : nullptr, stdf, d_payraw,
                          d_a6, d_pbz, pbz_words, d_misc);
       HIP_TRY(hipGetLastError());
