@@ -370,9 +370,10 @@ __device__ __forceinline__ uint32_t dxpow8_fast(int64_t e, const PolyConsts *__r
 #define H3C_XOR3_ASM 1
 #endif
 
-// Per-lane LDS addressing of the replicated tables (see kernel header comment).
+// Per-lane LDS addressing of the replicated tables (see kernel header comment): two registers;
+// the tables' remaining offsets ride in the ds_read immediate.
 struct LaneLut {
-  uint32_t off[4];
+  uint32_t off[2];
 };
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -391,23 +392,24 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // i.e. each 256-byte LDS row holds entry b of two tables x 32 copies.  ds_read_b32
 // banks on (addr/4)%32 = c, so lane l reading copy l%32 never conflicts.  The
 // address is one v_perm_b32: byte1 <- byte k of r, bytes 0 and 2 <- the lane's
-// per-table offset (byte0 = (t&1)<<7 | c<<2, byte2 = t>>1), byte3 <- 0.
+// lane offset (byte0 = c<<2, byte2 = t>>1: off[t>>1]), byte3 <- 0; the (t&1)<<7 of tables 1 and 3
+// is the ds_read's immediate offset (two offset registers a lane instead of four).
 __device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
   LaneLut L;
   const uint32_t c4 = (lane & 31u) * 4u;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) L.off[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) << 7) | c4;
+  L.off[0] = c4;
+  L.off[1] = c4 | 0x10000u;
   return L;
 }
 __device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const LaneLut &L) {
   const uint32_t a0 = __builtin_amdgcn_perm(r, L.off[0], 0x0C020400u);
-  const uint32_t a1 = __builtin_amdgcn_perm(r, L.off[1], 0x0C020500u);
-  const uint32_t a2 = __builtin_amdgcn_perm(r, L.off[2], 0x0C020600u);
-  const uint32_t a3 = __builtin_amdgcn_perm(r, L.off[3], 0x0C020700u);
+  const uint32_t a1 = __builtin_amdgcn_perm(r, L.off[0], 0x0C020500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(r, L.off[1], 0x0C020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(r, L.off[1], 0x0C020700u);
   const uint32_t t0 = *reinterpret_cast<const uint32_t *>(lb + a0);
-  const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1);
+  const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1 + 128);
   const uint32_t t2 = *reinterpret_cast<const uint32_t *>(lb + a2);
-  const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3);
+  const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3 + 128);
   return xor3(t0, t1, t2) ^ t3;
 }
 // LDS dword i holds table ((i>>14)<<1 | (i>>5)&1), entry (i>>6)&255.
@@ -421,19 +423,19 @@ __device__ __forceinline__ uint32_t fill_value_of(const uint32_t (*tab)[256], in
 constexpr int kLdsWords16 = 4 * 256 * 16;  // 16384 dwords = 64 KiB
 __device__ __forceinline__ LaneLut make_lut16(uint32_t lane) {
   LaneLut L;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) L.off[t] = ((uint32_t)t << 6) | ((lane & 15u) * 4u);
+  L.off[0] = (lane & 15u) * 4u;  // (t << 6: the immediate offset)
+  L.off[1] = 0;
   return L;
 }
 __device__ __forceinline__ uint32_t row_step16(uint32_t r, const char *lb, const LaneLut &L) {
   const uint32_t a0 = __builtin_amdgcn_perm(r, L.off[0], 0x0C0C0400u);
-  const uint32_t a1 = __builtin_amdgcn_perm(r, L.off[1], 0x0C0C0500u);
-  const uint32_t a2 = __builtin_amdgcn_perm(r, L.off[2], 0x0C0C0600u);
-  const uint32_t a3 = __builtin_amdgcn_perm(r, L.off[3], 0x0C0C0700u);
+  const uint32_t a1 = __builtin_amdgcn_perm(r, L.off[0], 0x0C0C0500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(r, L.off[0], 0x0C0C0600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(r, L.off[0], 0x0C0C0700u);
   const uint32_t t0 = *reinterpret_cast<const uint32_t *>(lb + a0);
-  const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1);
-  const uint32_t t2 = *reinterpret_cast<const uint32_t *>(lb + a2);
-  const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3);
+  const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1 + 64);
+  const uint32_t t2 = *reinterpret_cast<const uint32_t *>(lb + a2 + 128);
+  const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3 + 192);
   return xor3(t0, t1, t2) ^ t3;
 }
 // LDS dword i of the 16-copy image holds table (i>>4)&3, entry (i>>6)&255.
@@ -446,7 +448,6 @@ __device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
   LaneLut L;
   L.off[0] = (lane & 31u) * 4u;
   L.off[1] = L.off[0] + 65536u;
-  L.off[2] = L.off[3] = 0;
   return L;
 }
 __device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const LaneLut &L) {

@@ -73,8 +73,9 @@ enum { kCtrNone, kCtrReuse, kCtrCombine, kCtrRead, kCtrRecalc, kCtrMismatch, kCt
 // [kMiscOutF], [kMiscOutA6]: the fragment count and that flag, copied for the one read-back;
 // [kMiscT0], [kMiscT1]: the block kernel's first start and last end (wall clock, u64 each), its
 // timing when it runs inside a replayed graph (read back with the two words before them)
-// [kMiscTicket]: uio_front_kernel's tile ticket; [kMiscPBVoid]: a uio_phaseb_kernel tile gave up waiting
-enum { kMiscTicket = 0, kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscT0 = 4, kMiscT1 = 6, kMiscPBVoid = 8, kMiscN = 10 };
+// [kMiscTicket]: uio_front_kernel's tile ticket; [kMiscPBVoid]: a uio_phaseb_kernel tile gave up waiting;
+// [kMiscPBDone]: uio_phaseb_kernel's finished tiles (the last one copies [kMiscOutF, kMiscN) to the host)
+enum { kMiscTicket = 0, kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscT0 = 4, kMiscT1 = 6, kMiscPBVoid = 8, kMiscPBDone = 9, kMiscN = 10 };
 
 // ---------------------------------------------------------------- scan elements
 
@@ -1272,6 +1273,15 @@ __device__ __forceinline__ uint4 load_new(uint64_t src, uint32_t row, uint32_t r
 #define H3C_UIO_BLOCK_WAVES 16
 #endif
 constexpr uint32_t kBlkWaves = H3C_UIO_BLOCK_WAVES, kBlkThreads = 64 * kBlkWaves;
+#ifndef H3C_UIO_GRAB
+#define H3C_UIO_GRAB 0  // block kernel: fragments a wave takes per grab from an LDS counter (0: one fixed range per wave; 2 spills, 353 vs 282 us: r03i)
+#endif
+#ifndef H3C_UIO_IMG_NT
+#define H3C_UIO_IMG_NT 0  // 1: the old block rows by nontemporal loads (A/B)
+#endif
+#ifndef H3C_BLOCK_TRACE
+#define H3C_BLOCK_TRACE 0  // 1: every block-kernel wave prints its start / end (diagnostics)
+#endif
 #ifndef H3C_UIO_SFIELDS
 #define H3C_UIO_SFIELDS 1  // block kernel: per-fragment fields by scalar loads (0: all in the lanes)
 #endif
@@ -1308,7 +1318,11 @@ __device__ __forceinline__ void load_task_rows(uint64_t blk, uint32_t k0, uint32
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const uint32_t rel = 1024u * r + 16u * lane;
+#if H3C_UIO_IMG_NT
+    b.img[r] = (rel + 16 > k0 && rel < k1) ? load_row(blk + rel) : make_uint4(0, 0, 0, 0);
+#else
     b.img[r] = (rel + 16 > k0 && rel < k1) ? load_plain(blk + rel) : make_uint4(0, 0, 0, 0);
+#endif
     b.nw[r] = load_new(src, r, rel, w0, w1);
   }
 }
@@ -1419,10 +1433,11 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
                                                uint32_t cap, const PolyConsts *__restrict__ pc,
                                                uint32_t *__restrict__ eacc, const uint32_t *__restrict__ misc,
                                                uint32_t *lds, uint32_t std_domain, uint32_t *__restrict__ payraw,
-                                               uint32_t *__restrict__ a6) {
+                                               uint32_t *__restrict__ a6, uint32_t *misc_w) {
   for (int i = threadIdx.x; i < kLdsWords; i += kBlkThreads) lds[i] = fill_value(pc, i);
   const uint32_t *red_g = &pc->red[0][0][0];
   for (int i = threadIdx.x; i < kRedWords; i += kBlkThreads) lds[kLdsWords + i] = red_g[i];
+  if (threadIdx.x == 0) lds[kLdsWords + kRedWords] = 0;  // the waves' range counter (H3C_UIO_GRAB)
   __syncthreads();
   const uint32_t F = misc[kMiscA6] ? 0u : frag_count(d_F, cap);  // a failed A6: this pass writes nothing
   const uint32_t *red = lds + kLdsWords;
@@ -1431,8 +1446,17 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kBlkWaves + wave;
   const uint64_t nw = (uint64_t)gridDim.x * kBlkWaves;
+#if H3C_UIO_SFIELDS && H3C_UIO_GRAB
+  (void)gw;
+  (void)nw;
+  // this workgroup's share; its waves take it in ranges from the LDS counter (lds[kLdsWords + kRedWords])
+  uint32_t *grab = lds + kLdsWords + kRedWords;
+  const uint32_t wg_lo = (uint32_t)((uint64_t)blockIdx.x * F / gridDim.x);
+  const uint32_t wg_hi = (uint32_t)((uint64_t)(blockIdx.x + 1) * F / gridDim.x);
+#else
   const uint32_t lo = (uint32_t)(gw * F / nw), hi = (uint32_t)((gw + 1) * F / nw);
   if (lo >= hi) return;
+#endif
   const uint32_t poly = pc->poly;
   const LaneLut L = make_lut(lane);
 #if H3C_UIO_SFIELDS
@@ -1448,24 +1472,9 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
     w = b.z;
     k = c.y;
   };
-  uint64_t c_blk, c_src, n_blk = 0, n_src = 0;
-  uint32_t c_w, c_k, n_w = 0, n_k = 0;
-  addr_of(lo, c_blk, c_src, c_w, c_k);
-  BlockRows cur, nxt;
-  load_task_rows(c_blk, c_k & 0xFFFFu, c_k >> 16, c_src, c_w & 0xFFFFu, c_w >> 16, lane, cur);
-  if (lo + 1 < hi) addr_of(lo + 1, n_blk, n_src, n_w, n_k);
-  for (uint32_t g = lo; g < hi; ++g) {
+  // fragment g's chain on the block rows in `cb` (its fields by scalar loads)
+  auto process = [&](uint32_t g, uint64_t blk, uint32_t kk, BlockRows &cb) {
     const uint4 f1 = rec[4 * (size_t)g + 1], f2 = rec[4 * (size_t)g + 2];  // {p, rsv, w, q}, {z, k, mult, flags}
-    const uint64_t blk = c_blk;
-    const uint32_t kk = c_k;
-    if (g + 1 < hi) {
-      // the next fragment's rows in flight while this one is processed (a fragment that is not a
-      // chain head -- a later write to an already written block -- loads them in vain)
-      load_task_rows(n_blk, n_k & 0xFFFFu, n_k >> 16, n_src, n_w & 0xFFFFu, n_w >> 16, lane, nxt);
-      c_blk = n_blk;
-      c_k = n_k;
-      if (g + 2 < hi) addr_of(g + 2, n_blk, n_src, n_w, n_k);
-    }
     const uint32_t flags = f2.w;
     if (flags & kFragHead) {
       const uint32_t k0 = kk & 0xFFFFu, k1 = kk >> 16;
@@ -1476,7 +1485,7 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
         fx.expect = f3.y;
         fx.len = f3.z;
       }
-      uint32_t dirty = apply_fragment(cur.img, cur.nw, flags, f1.z, f1.w, f2.x, f2.z, f1.x, lane, lb, L, red, poly, eacc,
+      uint32_t dirty = apply_fragment(cb.img, cb.nw, flags, f1.z, f1.w, f2.x, f2.z, f1.x, lane, lb, L, red, poly, eacc,
                                       fx);
       for (uint32_t f = fnext[g]; f != kNil;) {  // later fragments of the same block
         const FragDesc d = frags[f];
@@ -1484,17 +1493,87 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
 #pragma unroll
         for (int r = 0; r < 4; ++r) nw4[r] = load_new(d.src, r, 1024u * r + 16u * lane, d.w0, d.w1);
         const FoldIo fd{d.op, d.expect, d.len, std_domain, pc, payraw, a6};
-        dirty |= apply_fragment(cur.img, nw4, d.flags, (uint32_t)d.w0 | ((uint32_t)d.w1 << 16),
+        dirty |= apply_fragment(cb.img, nw4, d.flags, (uint32_t)d.w0 | ((uint32_t)d.w1 << 16),
                                 (uint32_t)d.q0 | ((uint32_t)d.q1 << 16), (uint32_t)d.z0 | ((uint32_t)d.z1 << 16),
                                 d.mult, d.p, lane, lb, L, red, poly, eacc, fd);
         f = fnext[f];
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (dirty & (1u << r)) store_masked(blk, 1024u * r + 16u * lane, cur.img[r], k0, k1);
+        if (dirty & (1u << r)) store_masked(blk, 1024u * r + 16u * lane, cb.img[r], k0, k1);
+    }
+  };
+  uint64_t c_blk, c_src, n_blk = 0, n_src = 0;
+  uint32_t c_w, c_k, n_w = 0, n_k = 0;
+  BlockRows cur, nxt;
+#if H3C_UIO_GRAB
+  // Dynamic ranges: the workgroup's share of the fragments is handed to its waves
+  // H3C_UIO_GRAB at a time from an LDS counter (an LDS atomic: ~100 cycles, counted in lgkmcnt,
+  // so it never waits behind the wave's row loads) instead of a fixed share per wave, so a wave
+  // that meets slow blocks does not set the kernel's end.  A range is asked for two fragments
+  // before it is needed.
+  constexpr uint32_t G = H3C_UIO_GRAB;
+  static_assert(G >= 2, "a range holds at least two fragments (the addresses run two ahead)");
+  const uint32_t whi = wg_hi;
+  auto ask = [&]() -> uint32_t {
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(grab, G);
+    return wg_lo + (uint32_t)__builtin_amdgcn_readfirstlane(v);
+  };
+  uint32_t xb = ask();  // this range: [xb, xb + G)
+  if (xb >= whi) return;
+  uint32_t nb = 0, j = 0;  // the next range's base (asked for when first needed); x = xb + j
+  bool nb_read = false;
+  auto at = [&](uint32_t k) -> uint32_t {  // the k-th fragment from xb in this wave's order (k < 2G)
+    if (k < G) return xb + k;
+    if (!nb_read) {
+      nb = ask();
+      nb_read = true;
+    }
+    return nb + (k - G);
+  };
+  addr_of(xb, c_blk, c_src, c_w, c_k);
+  load_task_rows(c_blk, c_k & 0xFFFFu, c_k >> 16, c_src, c_w & 0xFFFFu, c_w >> 16, lane, cur);
+  if (at(1) < whi) addr_of(at(1), n_blk, n_src, n_w, n_k);
+  for (;;) {
+    const uint32_t x = xb + j, s1 = at(j + 1);  // (indices past whi: none, the ranges come in order)
+    const uint64_t blk = c_blk;
+    const uint32_t kk = c_k;
+    if (s1 < whi) {
+      load_task_rows(n_blk, n_k & 0xFFFFu, n_k >> 16, n_src, n_w & 0xFFFFu, n_w >> 16, lane, nxt);
+      c_blk = n_blk;
+      c_k = n_k;
+      const uint32_t s2 = at(j + 2);
+      if (s2 < whi) addr_of(s2, n_blk, n_src, n_w, n_k);
+    }
+    process(x, blk, kk, cur);
+    if (s1 >= whi) break;
+    if (++j == G) {  // into the next range
+      xb = nb;
+      j = 0;
+      nb_read = false;
     }
     cur = nxt;
   }
+#else
+  addr_of(lo, c_blk, c_src, c_w, c_k);
+  load_task_rows(c_blk, c_k & 0xFFFFu, c_k >> 16, c_src, c_w & 0xFFFFu, c_w >> 16, lane, cur);
+  if (lo + 1 < hi) addr_of(lo + 1, n_blk, n_src, n_w, n_k);
+  for (uint32_t g = lo; g < hi; ++g) {
+    const uint64_t blk = c_blk;
+    const uint32_t kk = c_k;
+    if (g + 1 < hi) {
+      // the next fragment's rows in flight while this one is processed (a fragment that is not a
+      // chain head -- a later write to an already written block -- loads them in vain)
+      load_task_rows(n_blk, n_k & 0xFFFFu, n_k >> 16, n_src, n_w & 0xFFFFu, n_w >> 16, lane, nxt);
+      c_blk = n_blk;
+      c_k = n_k;
+      if (g + 2 < hi) addr_of(g + 2, n_blk, n_src, n_w, n_k);
+    }
+    process(g, blk, kk, cur);
+    cur = nxt;
+  }
+#endif
 #else
   auto rl = [](uint32_t v, uint32_t t) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane(v, t); };
   auto rl64 = [](uint64_t v, uint32_t t) -> uint64_t {
@@ -1566,6 +1645,11 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
 #endif
 }
 
+#if H3C_BLOCK_TRACE
+__device__ unsigned int g_btr[67] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                     0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                     0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x7FFFFFFFu};
+#endif
 // ts (nullable): [0] the earliest workgroup start, [1] the latest workgroup end (wall clock).
 __global__ __launch_bounds__(kBlkThreads) void uio_block_kernel(const FragDesc *__restrict__ frags, const uint32_t *__restrict__ fnext,
                                                              const uint32_t *__restrict__ d_F, uint32_t cap,
@@ -1576,13 +1660,35 @@ __global__ __launch_bounds__(kBlkThreads) void uio_block_kernel(const FragDesc *
                                                              uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6,
                                                              uint32_t *__restrict__ pbz, uint32_t pbz_words,
                                                              uint32_t *__restrict__ misc_w) {
-  __shared__ uint32_t lds[kLdsWords + kRedWords];
+  __shared__ uint32_t lds[kLdsWords + kRedWords + 1];
   if (ts && threadIdx.x == 0) atomicMin(&ts[0], (unsigned long long)wall_clock64());
   if (blockIdx.x == 0) {  // uio_phaseb_kernel's tile states and ticket, fresh for every attempt
     for (uint32_t i = threadIdx.x; i < pbz_words; i += blockDim.x) pbz[i] = 0;
-    if (threadIdx.x == 0) misc_w[kMiscPBVoid] = 0;
+    if (threadIdx.x == 0) misc_w[kMiscPBVoid] = misc_w[kMiscPBDone] = 0;
   }
-  uio_block_body(frags, fnext, d_F, cap, pc, eacc, misc, lds, std_domain, payraw, a6);
+#if H3C_BLOCK_TRACE
+  const uint64_t tb0 = wall_clock64();
+  if ((threadIdx.x & 63) == 0) atomicMin(&g_btr[66], (unsigned int)(tb0 & 0x7FFFFFFFu));
+#endif
+  uio_block_body(frags, fnext, d_F, cap, pc, eacc, misc, lds, std_domain, payraw, a6, misc_w);
+#if H3C_BLOCK_TRACE  // diagnostics: a histogram of the waves' end times (5 us bins from the earliest start)
+  if ((threadIdx.x & 63) == 0) {
+    const uint64_t te = wall_clock64();
+    __builtin_amdgcn_s_sleep(100);  // every workgroup has stamped its start by now (one per CU)
+    const uint32_t rel = (uint32_t)((te & 0x7FFFFFFFu) - __hip_atomic_load(&g_btr[66], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    atomicAdd(&g_btr[min(rel / 500u, 63u)], 1u);
+    if (atomicAdd(&g_btr[64], 1u) + 1 == gridDim.x * (blockDim.x / 64)) {
+      printf("btrace waves by end time (5 us bins):");
+      for (int b = 0; b < 64; ++b) {
+        const unsigned int v = atomicExch(&g_btr[b], 0u);
+        if (v) printf(" %d:%u", b * 5, v);
+      }
+      printf("\n");
+      g_btr[64] = 0;
+      g_btr[66] = 0x7FFFFFFFu;
+    }
+  }
+#endif
   if (ts) {  // one stamp per workgroup, once all its waves are done
     __syncthreads();
     if (threadIdx.x == 0) atomicMax(&ts[1], (unsigned long long)wall_clock64());
@@ -1845,7 +1951,7 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
     const uint32_t *__restrict__ t0v, const h3c_chunk_state *__restrict__ chunks,
     h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks, uint8_t poly_type, uint32_t std_domain,
     h3c_update_result *__restrict__ res, unsigned long long *__restrict__ ctr, const uint32_t *__restrict__ d_F,
-    uint32_t *misc, PhaseBSlot *slots, uint32_t *ticket) {
+    uint32_t *misc, PhaseBSlot *slots, uint32_t *ticket, uint32_t *hout) {
   constexpr uint32_t T = kPhaseBTile;
   __shared__ uint32_t s_key[T + 1], sw[48], s_c[2], s_tile, s_void;
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -1913,9 +2019,9 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
     pub_flag(&me.flag[1], 2u);
   }
   // results
-  if (p == 0) {  // the pass's outcome, for the host's one read-back
-    misc[kMiscOutF] = *d_F;
-    misc[kMiscOutA6] = misc[kMiscA6];
+  if (p == 0) {  // the pass's outcome, for the host's one read-back (written through: the last tile copies it)
+    st_agent(&misc[kMiscOutF], *d_F);
+    st_agent(&misc[kMiscOutA6], ld_agent(&misc[kMiscA6]));
   }
   uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (valid) result_at(p, r, c, s_key[t + 1] != c, sin, chunks, chunks_out, nchunks, t0v, poly_type, std_domain, poly,
@@ -1923,6 +2029,16 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
   __shared__ unsigned int sh[8];
   ctr_add_block(sh, ctr, v);
   if (s_void && t == 0) atomicOr(&misc[kMiscPBVoid], 1u);  // the host reruns phase B the scan-based way
+  if (hout && t == 0) {
+    // the last tile to finish hands the outcome words straight to the caller's pinned host buffer
+    // (no device-to-host copy after the kernel); every tile's misc traffic is at the coherence
+    // point before its count (write-through stores and device atomics, then the vmcnt wait)
+    stores_done();
+    if (atomicAdd(&misc[kMiscPBDone], 1u) + 1 == (n + T - 1) / T) {
+#pragma unroll
+      for (uint32_t w = kMiscOutF; w < kMiscN; ++w) hout[w - kMiscOutF] = ld_agent(&misc[w]);
+    }
+  }
 }
 
 // t0 per chunk: the raw CRC of no bytes, the trusted stored value, or the bytes' CRC.
@@ -1964,7 +2080,8 @@ __global__ void uio_verify_t0_kernel(const h3c_update_io *__restrict__ ios, uint
 __global__ void uio_commit_kernel(const h3c_chunk_state *__restrict__ fin, h3c_chunk_state *__restrict__ chunks,
                                   uint32_t nchunks, const uint32_t *__restrict__ out, uint32_t cap) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < nchunks && out[0] <= cap && !out[1]) chunks[c] = fin[c];  // out: kMiscOutF, kMiscOutA6
+  // out: kMiscOutF, kMiscOutA6, ... kMiscPBVoid (a void phase B is redone before its outputs count)
+  if (c < nchunks && out[0] <= cap && !out[1] && !out[kMiscPBVoid - kMiscOutF]) chunks[c] = fin[c];
 }
 
 // H3C_UPD_EXACT: chunks whose stored checksum of the batch polynomial disagrees with the bytes.
@@ -2155,7 +2272,7 @@ struct UpdGraphKey {
   int dev;
   uint8_t poly;
   uint32_t flags, n, nchunks, cap, hcap;
-  const void *chunks, *chunks_out, *ios, *res, *ctr, *lease1, *lease2;
+  const void *chunks, *chunks_out, *ios, *res, *ctr, *lease1, *lease2, *hout;
   hipStream_t aux;
   bool operator==(const UpdGraphKey &o) const { return std::memcmp(this, &o, sizeof(*this)) == 0; }
 };
@@ -2370,11 +2487,13 @@ int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out) {
 
 // The pipeline on device arrays: chunks_in (read), chunks_out (final states; may not alias
 // chunks_in), ios, results, ctr (h3c_update_counters layout, 8 x u64).  `epilogue` enqueues the
-// caller's copies of the outputs before the final synchronisation.  Synchronous.
+// caller's copies of the outputs before the final synchronisation; with `epi_graph` (its work is
+// device-only and its arguments are part of the graph key) it is captured into the batch's graph.
+// Synchronous.
 template <class Epilogue>
 int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_state *d_chunks_out, uint32_t nchunks,
                 const h3c_update_io *d_ios, uint32_t n, h3c_update_result *d_res, uint32_t flags,
-                unsigned long long *d_ctr, hipStream_t st, int dev, Epilogue epilogue) {
+                unsigned long long *d_ctr, hipStream_t st, int dev, Epilogue epilogue, bool epi_graph = false) {
   const bool std_domain = (flags & H3C_UPD_STD_DOMAIN) != 0;
   const bool exact = (flags & H3C_UPD_EXACT) != 0;
   flags &= H3C_UPD_STD_DOMAIN | H3C_UPD_EXACT | H3C_UPD_GRAPHS;
@@ -2453,6 +2572,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   h3c_rt::PinnedLease pin(4096);
   if (!pin.ok()) return H3C_ERR_HIP;
   uint32_t *h_F = reinterpret_cast<uint32_t *>(pin.data());
+  uint32_t *d_hF = nullptr;  // the same words as the device addresses them (uio_phaseb_kernel writes them)
+  HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_hF), h_F, 0));
   AuxStream *aux = nullptr;
   int rc = aux_stream(dev, aux);
   if (rc) return rc;
@@ -2622,7 +2743,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       if (pb1) {
         hipLaunchKernelGGL(uio_phaseb_kernel, dim3(std::max(ntiles_pb, 1u)), dim3(kPhaseBTile), 0, q, d_pos, d_skey, n,
                            d_eacc, d_payraw, pc, d_a6, d_t0, d_chunks, d_chunks_out, nchunks, poly_type, stdf, d_res,
-                           d_ctr, d_F, d_misc, reinterpret_cast<PhaseBSlot *>(d_pbz), d_pbz + pbz_words - 1);
+                           d_ctr, d_F, d_misc, reinterpret_cast<PhaseBSlot *>(d_pbz), d_pbz + pbz_words - 1,
+                           d_hF);
         HIP_TRY(hipGetLastError());
       } else {
         const int r = phase_b_scans(q);
@@ -2656,7 +2778,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     UpdGraphs *gr = nullptr;
     if (attempt == 0) {
       const UpdGraphKey key{dev, poly_type, flags, n, nchunks, cap, hcap, d_chunks, d_chunks_out, d_ios, d_res,
-                            d_ctr, lease1.data(), lease2.data(), aux->st};
+                            d_ctr, lease1.data(), lease2.data(), d_hF, aux->st};
       gr = upd_graphs(key, st, (flags & H3C_UPD_GRAPHS) != 0);
     }
     if (gr && !gr->g && !gr->failed) {  // capture the attempt once, on a capture stream of this thread
@@ -2666,6 +2788,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         if (!r) r = phase_frag(cst);
         if (!r) r = block_kernel(cst, true);
         if (!r) r = phase_b(cst);
+        if (!r && epi_graph) r = epilogue(cst, d_misc + kMiscOutF, cap);
         return r;
       }, gr->g) : H3C_ERR_HIP;
       if (rc) {  // not capturable here: plain launches from now on for this shape
@@ -2697,9 +2820,12 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       if (rc) return rc;
     }
     const bool prof_graph = use_graph && h3c_rt::prof_enabled();
-    HIP_TRY(hipMemcpyAsync(h_F, d_misc + kMiscOutF, 4 * (kMiscN - kMiscOutF), hipMemcpyDeviceToHost, st));
-    rc = epilogue(st, d_misc + kMiscOutF, cap);  // (a redone attempt's outputs are replaced)
-    if (rc) return rc;
+    if (!pb1)  // (uio_phaseb_kernel's last tile writes the outcome words to h_F itself)
+      HIP_TRY(hipMemcpyAsync(h_F, d_misc + kMiscOutF, 4 * (kMiscN - kMiscOutF), hipMemcpyDeviceToHost, st));
+    if (!(use_graph && epi_graph)) {
+      rc = epilogue(st, d_misc + kMiscOutF, cap);  // (a redone attempt's outputs are replaced)
+      if (rc) return rc;
+    }
     const hipError_t se = hipStreamSynchronize(st);
     drain2.armed = false;
     if (se != hipSuccess) {
@@ -2718,6 +2844,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       // a phase-B tile gave up waiting (its CU starved by other work): the chunk bytes are
       // written and right; redo phase B the scan-based way over the same state, then the epilogue
       HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, st));
+      HIP_TRY(hipMemsetAsync(d_misc + kMiscPBVoid, 0, 4, st));  // (the epilogue below commits)
       rc = phase_b_scans(st);
       if (rc) return rc;
       if (exact && nchunks) {
@@ -2877,7 +3004,7 @@ extern "C" int h3c_update_ios_dev(uint8_t poly_type, h3c_chunk_state *chunks_dev
                        HIP_TRY(hipGetLastError());
                      }
                      return H3C_OK;
-                   });
+                   }, true);
   if (rc) return rc;
   drain.armed = false;
   return H3C_OK;
