@@ -135,7 +135,8 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
 // n + c; 0 pieces skips an item): one launch for both, pbase over n + nchunks items.
 int launch_uio_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, uint32_t n,
                          const h3c_chunk_state *chunks, uint32_t nchunks, const uint32_t *pbase,
-                         const uint32_t *d_total, uint32_t *crc0_out);
+                         const uint32_t *d_total, uint32_t *crc0_out, const uint32_t *tbase = nullptr,
+                         uint32_t tile = 0);  // tbase: item i's offset is pbase[i] + tbase[i / tile]
 // Rows (1 KiB, absolute alignment) a byte range touches.
 inline uint32_t host_rows(uint64_t ptr, uint64_t len) {
   return len ? (uint32_t)((((ptr + len + 1023) & ~uint64_t(1023)) - (ptr & ~uint64_t(1023))) / 1024) : 0;

@@ -663,7 +663,8 @@ template <class Src>
 __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(Src src, const uint32_t *__restrict__ pbase, uint32_t n,
                                                                 const uint32_t *__restrict__ d_total,
                                                                 const PolyConsts *__restrict__ pc,
-                                                                uint32_t *__restrict__ crc0_out) {
+                                                                uint32_t *__restrict__ crc0_out,
+                                                                const uint32_t *__restrict__ tbase, uint32_t tshift) {
   constexpr int G = 4, kLevels = 2, NG = 64 / G;
   constexpr uint64_t kQ = 16u * G;
   constexpr int kRed = (1 + kLevels) * 1024;
@@ -695,30 +696,36 @@ __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(Src src, const u
     q0 = (uint32_t)__builtin_amdgcn_readfirstlane(q0);
     if (q0 >= whi) break;
     const uint32_t k = q0 + grp;
-    const bool valid = k < whi;
+    bool valid = k < whi;
     uint64_t S = 0, E = 0;
     uint32_t op = 0, shift = 0;
     if (valid) {  // op i: the last with pbase[i] <= k (pieces of ops with none are skipped over)
       // first guess: one piece per op (payloads of at most 4 KiB, BASELINE config 3), two
       // independent loads; otherwise a binary search (pbase[n] is the total, > k)
+      // (with `tbase`, item i's offset is pbase[i] + tbase[i >> tshift]: the prep kernel's two-level scan)
+      auto at = [&](uint32_t m) -> uint32_t { return pbase[m] + (tbase ? tbase[m >> tshift] : 0u); };
       uint32_t a = min(k, n - 1);
-      if (!(pbase[a] <= k && pbase[a + 1] > k)) {
+      if (!(at(a) <= k && at(a + 1) > k)) {
         a = 0;
         uint32_t b = n;
         while (b - a > 1) {
           const uint32_t m = (a + b) >> 1;
-          if (pbase[m] <= k) a = m; else b = m;
+          if (at(m) <= k) a = m; else b = m;
         }
       }
       op = a;
-      const uint32_t j = k - pbase[a];
+      const uint32_t j = k - at(a);
       uint64_t base;
       uint32_t length;
       src.range(a, base, length);
-      const uint32_t off = j * 4096u, plen = min(4096u, length - off);
-      S = base + off;
-      E = S + plen;
-      shift = length - off - plen;
+      if ((uint64_t)j * 4096u < length) {
+        const uint32_t off = j * 4096u, plen = min(4096u, length - off);
+        S = base + off;
+        E = S + plen;
+        shift = length - off - plen;
+      } else {  // (a piece table that disagrees with the items: read nothing)
+        valid = false;
+      }
     }
     const uint64_t base = S & ~(kQ - 1);
     const uint64_t la = base + 16u * gl;
@@ -1193,11 +1200,12 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
 #endif
 int launch_uio_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, uint32_t n,
                          const h3c_chunk_state *chunks, uint32_t nchunks, const uint32_t *pbase,
-                         const uint32_t *d_total, uint32_t *crc0_out) {
+                         const uint32_t *d_total, uint32_t *crc0_out, const uint32_t *tbase, uint32_t tile) {
   const DeviceCtx &ctx = g_dev[dev];
   const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
   hipLaunchKernelGGL(op_piece_crc_kernel<UioPieceSrc>, dim3(std::max(ctx.num_cu * H3C_PIECE_CU_PCT / 100, 1)),
-                     dim3(kThreads), 0, st, UioPieceSrc{ios, chunks, n}, pbase, n + nchunks, d_total, pc, crc0_out);
+                     dim3(kThreads), 0, st, UioPieceSrc{ios, chunks, n}, pbase, n + nchunks, d_total, pc, crc0_out, tbase,
+                     tbase ? (uint32_t)__builtin_ctz(tile) : 0u);
   HIP_TRY(hipGetLastError());
   return H3C_OK;
 }

@@ -74,7 +74,7 @@ enum { kCtrNone, kCtrReuse, kCtrCombine, kCtrRead, kCtrRecalc, kCtrMismatch, kCt
 // [kMiscT0], [kMiscT1]: the block kernel's first start and last end (wall clock, u64 each), its
 // timing when it runs inside a replayed graph (read back with the two words before them)
 // [kMiscTicket]: uio_front_kernel's tile ticket; [kMiscPBVoid]: a uio_phaseb_kernel tile gave up waiting;
-// [kMiscPBDone]: uio_phaseb_kernel's finished tiles (the last one copies [kMiscOutF, kMiscN) to the host)
+// [kMiscPBDone]: uio_phaseb_kernel's finished tiles (the last one copies [kMiscOutF, kMiscN) to the host);
 enum { kMiscTicket = 0, kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscT0 = 4, kMiscT1 = 6, kMiscPBVoid = 8, kMiscPBDone = 9, kMiscN = 10 };
 
 // ---------------------------------------------------------------- scan elements
@@ -224,20 +224,51 @@ __device__ __forceinline__ bool fold_candidate(const h3c_update_io &io, const h3
   return (a >> 12) == ((a + io.length - 1) >> 12);
 }
 
+// Cross-workgroup traffic inside a kernel (the prep kernel's scan, uio_front_kernel, uio_phaseb_kernel) uses relaxed agent-scope atomics only (sc1 loads and
+// stores, coherent across the XCDs' L2s) and a vmcnt wait before a flag store: a release / acquire
+// at agent scope would write back / invalidate the whole L2 (buffer_wbl2 / buffer_inv sc1) every
+// time -- with one per published hash entry, the first version of this kernel took 117-170 us.
+template <class T>
+__device__ __forceinline__ T ld_agent(T *p) {  // a relaxed load at the coherence point
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void st_agent(T *p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void pub_flag(uint32_t *f, uint32_t v) {
+  stores_done();  // this thread's payload stores are at the coherence point before the flag
+  st_agent(f, v);
+}
 // Validation (ChunkReplica.cc:140-145 range check; the ABI's preconditions), sort keys, and
 // the piece counts of the early piece-CRC pass: op i's payload is item i (fold candidates have
 // none: the block kernel or the late pass checks them), chunk c's bytes (when t0 comes from
-// them) item n + c.  max(n, nchunks) + 1 threads.
-__global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t n, const h3c_chunk_state *__restrict__ chunks,
-                                uint32_t nchunks, uint8_t poly_type, uint32_t std_domain, uint32_t exact,
-                                uint32_t *__restrict__ status, uint32_t *__restrict__ key, uint32_t *__restrict__ idx,
-                                uint32_t *__restrict__ npieces, uint32_t *__restrict__ paycrc0,
-                                uint32_t *__restrict__ eacc, unsigned long long *__restrict__ ctr,
-                                uint32_t *__restrict__ misc, uint32_t *__restrict__ a6, uint32_t *__restrict__ fz,
-                                uint32_t fz_words,
-                                uint32_t *__restrict__ hhead, uint32_t hcap, uint32_t *__restrict__ gnext,
-                                uint32_t *__restrict__ fnext, uint32_t fcap) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// them) item n + c; thread j handles item j (n + max(nchunks, 1) + 1 threads at least).
+// With `pbase`, the kernel also scans the piece counts, in two levels and with no waiting: each
+// tile of kPrepTile items writes its items' exclusive offsets within the tile to pbase[] and its
+// total to tbase[k]; the last tile to finish turns tbase[] into the tiles' exclusive bases (item
+// i's offset is pbase[i] + tbase[i / kPrepTile]; op_piece_crc_kernel adds them).  `sstate`
+// (zeroed by the caller): [0] the ticket, [1] finished tiles, [2] the total, [3 + k] tbase[k].
+__global__ void uio_zero_kernel(uint32_t *__restrict__ p, uint32_t n) {
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0;
+}
+constexpr uint32_t kPrepTile = 256;
+__global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
+    const h3c_update_io *__restrict__ ios, uint32_t n, const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks,
+    uint8_t poly_type, uint32_t std_domain, uint32_t exact, uint32_t *__restrict__ status, uint32_t *__restrict__ key,
+    uint32_t *__restrict__ idx, uint32_t *__restrict__ npieces, uint32_t *__restrict__ paycrc0,
+    uint32_t *__restrict__ eacc, unsigned long long *__restrict__ ctr, uint32_t *__restrict__ misc,
+    uint32_t *__restrict__ a6, uint32_t *__restrict__ fz, uint32_t fz_words, uint32_t *__restrict__ hhead,
+    uint32_t hcap, uint32_t *__restrict__ gnext, uint32_t *__restrict__ fnext, uint32_t fcap,
+    uint32_t *__restrict__ pbase, uint32_t *sstate) {
+  __shared__ uint32_t s_tile, s_w[kPrepTile / 64], s_last;
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pbase) {  // ticket order for the look-back (tile k waits only on tiles already running)
+    if (threadIdx.x == 0) s_tile = atomicAdd(&sstate[0], 1u);
+    __syncthreads();
+    i = s_tile * blockDim.x + threadIdx.x;
+  }
   if (i < fz_words) fz[i] = 0;        // the one-pass front's tile states (uio_front_kernel)
   if (i < hcap) hhead[i] = 0xFFFFFFFFu;  // ... its link hash's bucket heads
   if (i < fcap) {                     // ... its bucket lists' next pointers and the chains'
@@ -249,59 +280,113 @@ __global__ void uio_prep_kernel(const h3c_update_io *__restrict__ ios, uint32_t 
   // chunk items n + c for c < C = max(nchunks, 1) (the piece pass's NP = n + C items), then the
   // scan's extra entry: pbase[n + C] = total
   const uint32_t C = nchunks ? nchunks : 1u;
-  if (i < C) {
-    npieces[n + i] = 0;
-    if (i < nchunks) {
-      const h3c_chunk_state cs = chunks[i];
-      npieces[n + i] = needs_init(cs, poly_type, exact) ? (cs.size + kPieceBytes - 1) / kPieceBytes : 0u;
+  uint32_t np = 0;
+  if (i >= n && i < n + C) {
+    const uint32_t c = i - n;
+    if (c < nchunks) {
+      const h3c_chunk_state cs = chunks[c];
+      np = needs_init(cs, poly_type, exact) ? (cs.size + kPieceBytes - 1) / kPieceBytes : 0u;
     }
-    paycrc0[n + i] = 0;
+    npieces[i] = np;
+    paycrc0[i] = 0;
   }
-  if (i == C) npieces[n + C] = 0;
-  if (i >= n) return;
-  paycrc0[i] = 0;  // XOR accumulators of the piece and block kernels
-  eacc[2 * i] = 0;
-  eacc[2 * i + 1] = 0;
-  a6[i] = 0;       // A6 verdicts (the early pass, the front / late checks, the block kernel)
-  const h3c_update_io io = ios[i];
-  uint32_t st = H3C_OK;
-  const uint32_t c = io.chunk;
-  const bool kind_ok = io.kind == H3C_UPD_WRITE || io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND ||
-                       io.kind == H3C_UPD_REMOVE || io.kind == H3C_UPD_COMMIT;
-  if (c >= nchunks || !kind_ok) {
-    st = H3C_ERR_INVALID_ARG;
-  } else if (io.kind != H3C_UPD_COMMIT) {
-    const h3c_chunk_state cs = chunks[c];
-    const bool syncing = (io.flags & H3C_IO_SYNCING) != 0;
-    if (!cs.base || (io.checksum_type != H3C_TYPE_NONE && io.checksum_type != poly_type)) st = H3C_ERR_INVALID_ARG;
-    if (cs.size > cs.chunk_size) st = H3C_ERR_INVALID_ARG;  // a corrupt chunk state
-    // documented limit: a TRUNCATE / EXTEND of a chunk stored (at the start of the batch) under the
-    // other polynomial -- its stored type would be kept (:328-332), and this batch CRCs in its own
-    if (!std_domain && (io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND) && cs.type != H3C_TYPE_NONE &&
-        cs.type != poly_type)
+  if (i == n + C) npieces[i] = 0;
+  if (i < n) {
+    paycrc0[i] = 0;  // XOR accumulators of the piece and block kernels
+    eacc[2 * i] = 0;
+    eacc[2 * i + 1] = 0;
+    a6[i] = 0;       // A6 verdicts (the early pass, the front / late checks, the block kernel)
+    const h3c_update_io io = ios[i];
+    uint32_t st = H3C_OK;
+    const uint32_t c = io.chunk;
+    const bool kind_ok = io.kind == H3C_UPD_WRITE || io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND ||
+                         io.kind == H3C_UPD_REMOVE || io.kind == H3C_UPD_COMMIT;
+    if (c >= nchunks || !kind_ok) {
       st = H3C_ERR_INVALID_ARG;
-    if (io.kind == H3C_UPD_REMOVE) {  // doRemove's form (StorageOperator.cc:808-815); no range check (:141)
-      if (io.offset || io.length || io.checksum_type != H3C_TYPE_NONE || syncing) st = H3C_ERR_INVALID_ARG;
-    } else {
-      // :141-145 against writeIO.chunkSize (H3C_IO_CHUNK_SIZE; else the chunk's own), then :171-180
-      const bool own = !std_domain && (io.flags & H3C_IO_CHUNK_SIZE);
-      const uint32_t wcs = own ? io.chunk_size : cs.chunk_size;
-      if (io.offset >= wcs || (uint64_t)io.offset + io.length > wcs) st = H3C_ERR_INVALID_ARG;
-      if (io.kind == H3C_UPD_WRITE && io.length && !io.payload) st = H3C_ERR_INVALID_ARG;
-      if (syncing && (io.kind != H3C_UPD_WRITE || io.offset)) st = H3C_ERR_INVALID_ARG;
-      if (st == H3C_OK && wcs != cs.chunk_size) st = H3C_ERR_CHUNK_SIZE_MISMATCH;
-      // A6 on a TRUNCATE / EXTEND: create(type, <no data>, length) is {NONE, 0} (:193-207);
-      // the Rust engine verifies only data (engine.rs:297)
-      if (st == H3C_OK && !std_domain && io.kind != H3C_UPD_WRITE && io.checksum_type != H3C_TYPE_NONE && io.length)
-        st = H3C_ERR_CHECKSUM_MISMATCH;
+    } else if (io.kind != H3C_UPD_COMMIT) {
+      const h3c_chunk_state cs = chunks[c];
+      const bool syncing = (io.flags & H3C_IO_SYNCING) != 0;
+      if (!cs.base || (io.checksum_type != H3C_TYPE_NONE && io.checksum_type != poly_type)) st = H3C_ERR_INVALID_ARG;
+      if (cs.size > cs.chunk_size) st = H3C_ERR_INVALID_ARG;  // a corrupt chunk state
+      // documented limit: a TRUNCATE / EXTEND of a chunk stored (at the start of the batch) under the
+      // other polynomial -- its stored type would be kept (:328-332), and this batch CRCs in its own
+      if (!std_domain && (io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND) && cs.type != H3C_TYPE_NONE &&
+          cs.type != poly_type)
+        st = H3C_ERR_INVALID_ARG;
+      if (io.kind == H3C_UPD_REMOVE) {  // doRemove's form (StorageOperator.cc:808-815); no range check (:141)
+        if (io.offset || io.length || io.checksum_type != H3C_TYPE_NONE || syncing) st = H3C_ERR_INVALID_ARG;
+      } else {
+        // :141-145 against writeIO.chunkSize (H3C_IO_CHUNK_SIZE; else the chunk's own), then :171-180
+        const bool own = !std_domain && (io.flags & H3C_IO_CHUNK_SIZE);
+        const uint32_t wcs = own ? io.chunk_size : cs.chunk_size;
+        if (io.offset >= wcs || (uint64_t)io.offset + io.length > wcs) st = H3C_ERR_INVALID_ARG;
+        if (io.kind == H3C_UPD_WRITE && io.length && !io.payload) st = H3C_ERR_INVALID_ARG;
+        if (syncing && (io.kind != H3C_UPD_WRITE || io.offset)) st = H3C_ERR_INVALID_ARG;
+        if (st == H3C_OK && wcs != cs.chunk_size) st = H3C_ERR_CHUNK_SIZE_MISMATCH;
+        // A6 on a TRUNCATE / EXTEND: create(type, <no data>, length) is {NONE, 0} (:193-207);
+        // the Rust engine verifies only data (engine.rs:297)
+        if (st == H3C_OK && !std_domain && io.kind != H3C_UPD_WRITE && io.checksum_type != H3C_TYPE_NONE && io.length)
+          st = H3C_ERR_CHECKSUM_MISMATCH;
+      }
     }
+    status[i] = st;
+    key[i] = c < nchunks ? c : nchunks;
+    idx[i] = i;
+    const bool cand = st == H3C_OK && fold_candidate(io, chunks[c], st);
+    np = (st == H3C_OK && io.kind == H3C_UPD_WRITE && io.length && !cand) ? (io.length + kPieceBytes - 1) / kPieceBytes
+                                                                          : 0;
+    npieces[i] = np;
   }
-  status[i] = st;
-  key[i] = c < nchunks ? c : nchunks;
-  idx[i] = i;
-  const bool cand = st == H3C_OK && fold_candidate(io, chunks[c], st);
-  npieces[i] = (st == H3C_OK && io.kind == H3C_UPD_WRITE && io.length && !cand)
-                   ? (io.length + kPieceBytes - 1) / kPieceBytes : 0;
+  if (!pbase) return;
+  // exclusive scan of the items' piece counts: in the tile, then the tile's base by look-back
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t x = np;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[wave] = x;
+  __syncthreads();
+  uint32_t wpre = 0, tot = 0;
+  for (uint32_t w = 0; w < kPrepTile / 64; ++w) {
+    if (w < wave) wpre += s_w[w];
+    tot += s_w[w];
+  }
+  const uint32_t k = s_tile, nscan = (n + C + 1 + kPrepTile - 1) / kPrepTile;
+  if (k >= nscan) return;  // (whole tile: no item)
+  uint32_t *tbase = sstate + 3;
+  if (i <= n + C) pbase[i] = wpre + x - np;
+  if (t == 0) {
+    st_agent(&tbase[k], tot);
+    stores_done();  // the tile total is at the coherence point before the count
+    s_last = atomicAdd(&sstate[1], 1u) + 1 == nscan;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the last tile: exclusive scan of the nscan tile totals, in place, in chunks of kPrepTile
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nscan; b0 += kPrepTile) {
+    const uint32_t j = b0 + t;
+    const uint32_t v = j < nscan ? ld_agent(&tbase[j]) : 0u;
+    uint32_t y = v;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t z = (uint32_t)__shfl_up((int)y, o, 64);
+      if (lane >= o) y += z;
+    }
+    __syncthreads();  // (s_w reuse)
+    if (lane == 63) s_w[wave] = y;
+    __syncthreads();
+    uint32_t wp = 0, all = 0;
+    for (uint32_t w = 0; w < kPrepTile / 64; ++w) {
+      if (w < wave) wp += s_w[w];
+      all += s_w[w];
+    }
+    if (j < nscan) st_agent(&tbase[j], carry + wp + y - v);
+    carry += all;
+  }
+  if (t == 0) st_agent(&sstate[2], carry);
 }
 
 __device__ __forceinline__ bool applied_kind(uint8_t kind) {
@@ -771,23 +856,6 @@ struct FrontSlot {
 };
 static_assert(sizeof(FrontSlot) == 48, "FrontSlot is 48 bytes");
 
-// Cross-workgroup traffic inside the kernel uses relaxed agent-scope atomics only (sc1 loads and
-// stores, coherent across the XCDs' L2s) and a vmcnt wait before a flag store: a release / acquire
-// at agent scope would write back / invalidate the whole L2 (buffer_wbl2 / buffer_inv sc1) every
-// time -- with one per published hash entry, the first version of this kernel took 117-170 us.
-template <class T>
-__device__ __forceinline__ T ld_agent(T *p) {  // a relaxed load at the coherence point
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <class T>
-__device__ __forceinline__ void st_agent(T *p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void pub_flag(uint32_t *f, uint32_t v) {
-  stores_done();  // this thread's payload stores are at the coherence point before the flag
-  st_agent(f, v);
-}
 __device__ __forceinline__ uint64_t sz_bits(const SzTy &a) {
   uint64_t b;
   __builtin_memcpy(&b, &a, 8);
@@ -806,6 +874,26 @@ __device__ __forceinline__ uint32_t wait_flag(uint32_t *f) {
     if (++spins > kFrontSpin) return 0;
   }
   return v;
+}
+
+// t0 per chunk: the raw CRC of no bytes, the trusted stored value, or the bytes' CRC.
+// Also copies the chunk table to the output table, whose entries of chunks with ops the result
+// kernel replaces (the same chunks on a redone pass, so the copy is made once).
+__device__ __forceinline__ void t0_chunk(uint32_t c, const h3c_chunk_state *__restrict__ chunks, uint8_t poly_type,
+                                         uint32_t exact, uint32_t std_domain, const uint32_t *__restrict__ crc0,
+                                         const PolyConsts *__restrict__ pc, uint32_t *__restrict__ t0v,
+                                         h3c_chunk_state *__restrict__ chunks_out) {
+  const h3c_chunk_state cs = chunks[c];
+  chunks_out[c] = cs;
+  uint32_t t0;
+  if (cs.size == 0 || cs.size > cs.chunk_size) {
+    t0 = 0xFFFFFFFFu;
+  } else if (needs_init(cs, poly_type, exact)) {
+    t0 = crc0[c] ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(cs.size, pc, pc->poly), pc->poly);
+  } else {
+    t0 = std_domain ? ~cs.value : cs.value;
+  }
+  t0v[c] = t0;
 }
 
 // SzTy <-> two dwords (v; cst | tset << 8 | t << 16 | segment-head flag << 24) for shuffles
@@ -859,7 +947,9 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
     uint8_t poly_type, uint32_t std_domain, const PolyConsts *__restrict__ pc, OpPos *__restrict__ pos,
     uint32_t *__restrict__ nfrag, uint32_t *__restrict__ fbase, uint32_t *__restrict__ late,
     uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6, uint32_t *misc, FragDesc *frags, uint64_t *fkey,
-    uint32_t cap, uint32_t *hhead, uint32_t hmask, uint32_t *gnext, uint32_t *prev, uint32_t *fnext, FrontSlot *slots) {
+    uint32_t cap, uint32_t *hhead, uint32_t hmask, uint32_t *gnext, uint32_t *prev, uint32_t *fnext, FrontSlot *slots,
+    const uint32_t *__restrict__ paycrc0, uint32_t exact, uint32_t *__restrict__ t0v,
+    h3c_chunk_state *__restrict__ chunks_out, const uint32_t *sstate) {
   constexpr uint32_t T = kFrontTile, NW = T / 64;
   __shared__ uint32_t s_key[T], s_v[T], s_w[T];         // keys; the inclusive maps (v, packed)
   __shared__ uint32_t s_fex[T + 1];                     // exclusive fragment counts of the tile
@@ -895,6 +985,13 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
   if (valid) {
     io = ios[i];
     st = status[i];
+  }
+  if (sstate) {
+    // the serial path: the A6 verdicts of the ops the piece pass read (the fold candidates' come
+    // later), t0 per chunk (and the output table's copy)
+    if (valid) verify_op(i, ios, paycrc0, pc, std_domain, status, payraw, a6, misc, chunks);
+    for (uint32_t cc = k * T + t; cc < nchunks; cc += gridDim.x * T)
+      t0_chunk(cc, chunks, poly_type, exact, std_domain, paycrc0 + n, pc, t0v, chunks_out);
   }
   const SzTy id{0, 0, 0, 0, 0};
   const SzTy e = valid ? sz_elem_of(io, st, poly_type, std_domain) : id;
@@ -1273,6 +1370,12 @@ __device__ __forceinline__ uint4 load_new(uint64_t src, uint32_t row, uint32_t r
 #define H3C_UIO_BLOCK_WAVES 16
 #endif
 constexpr uint32_t kBlkWaves = H3C_UIO_BLOCK_WAVES, kBlkThreads = 64 * kBlkWaves;
+#ifndef H3C_UIO_SERIAL
+#define H3C_UIO_SERIAL 1  // the front path on one stream (0: the piece pass, A6 and t0 on a second stream)
+#endif
+#ifndef H3C_UIO_LATE_JOIN
+#define H3C_UIO_LATE_JOIN 0  // timing experiment only: the block kernel does not wait for the second stream
+#endif                       // (unsafe: a failed non-fold A6 check would not stop its writes)
 #ifndef H3C_UIO_GRAB
 #define H3C_UIO_GRAB 0  // block kernel: fragments a wave takes per grab from an LDS counter (0: one fixed range per wave; 2 spills, 353 vs 282 us: r03i)
 #endif
@@ -2041,26 +2144,6 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
   }
 }
 
-// t0 per chunk: the raw CRC of no bytes, the trusted stored value, or the bytes' CRC.
-// Also copies the chunk table to the output table, whose entries of chunks with ops the result
-// kernel replaces (the same chunks on a redone pass, so the copy is made once).
-__device__ __forceinline__ void t0_chunk(uint32_t c, const h3c_chunk_state *__restrict__ chunks, uint8_t poly_type,
-                                         uint32_t exact, uint32_t std_domain, const uint32_t *__restrict__ crc0,
-                                         const PolyConsts *__restrict__ pc, uint32_t *__restrict__ t0v,
-                                         h3c_chunk_state *__restrict__ chunks_out) {
-  const h3c_chunk_state cs = chunks[c];
-  chunks_out[c] = cs;
-  uint32_t t0;
-  if (cs.size == 0 || cs.size > cs.chunk_size) {
-    t0 = 0xFFFFFFFFu;
-  } else if (needs_init(cs, poly_type, exact)) {
-    t0 = crc0[c] ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(cs.size, pc, pc->poly), pc->poly);
-  } else {
-    t0 = std_domain ? ~cs.value : cs.value;
-  }
-  t0v[c] = t0;
-}
-
 // After the piece pass: A6 per op and t0 per chunk (the chunk CRCs are items n + c), one launch
 // of max(n, nchunks) threads.
 __global__ void uio_verify_t0_kernel(const h3c_update_io *__restrict__ ios, uint32_t n,
@@ -2399,6 +2482,7 @@ UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st, bool asked) {
   key.ctr = key_in.ctr;
   key.lease1 = key_in.lease1;
   key.lease2 = key_in.lease2;
+  key.hout = key_in.hout;  // (phase B writes the outcome words there)
   key.aux = key_in.aux;
   ++tick;
   for (UpdGraphs &g : cache)
@@ -2511,7 +2595,18 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   const uint32_t ntiles_pb = (uint32_t)((n + kPhaseBTile - 1) / kPhaseBTile);
   const uint32_t pbz_words = ntiles_pb * (uint32_t)(sizeof(PhaseBSlot) / 4) + 1;
   thread_local uint32_t last_frags = 0;
+  // the one-pass front (uio_front_kernel) on the first attempt; test hook H3C_HOOK_UPD_FRONT = 1: the
+  // scan-based stage (redone attempts always take that one)
+  const bool front_path = (h3c_rt::hook(H3C_HOOK_UPD_FRONT) & 1) == 0;
   uint32_t cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * n + 1024, last_frags), 0x7FFFFFF0u);
+  // the prep kernel's grid on the first attempt (its threads cover the piece items and the front
+  // kernel's initialisations) and, on the serial front path, its scan states
+  uint32_t hcap0 = 256;
+  while (hcap0 < cap) hcap0 <<= 1;
+  const uint32_t fz_words0 = front_path ? ntiles_front * (uint32_t)(sizeof(FrontSlot) / 4) : 0u;
+  const uint32_t prep_tiles = (uint32_t)((std::max<size_t>(std::max<size_t>((size_t)n + C + 1, nchunks),
+                                                           std::max<size_t>(fz_words0, front_path ? hcap0 : 0u)) +
+                                          kPrepTile - 1) / kPrepTile);
   size_t sort_tmp = 0, scan_tmp = 0, pscan_tmp = 0, szscan_tmp = 0, ascan_tmp = 0;
   const uint32_t bits = bits_for((uint64_t)nchunks + 1);
   HIP_TRY(sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, n, bits, st));
@@ -2534,6 +2629,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   OpPos *d_pos;
   Aff *d_tel, *d_tscan, *d_sel, *d_sscan;
   void *d_tmp, *d_ptmp;
+  uint32_t *d_sstate;  // the prep kernel's scan states (serial front path)
   auto layout = [&](char *base) -> size_t {  // one layout, run with base 0 to size the lease
     char *cur = base;
     d_status = carve<uint32_t>(cur, n);
@@ -2564,6 +2660,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     d_sscan = carve<Aff>(cur, n);
     d_tmp = carve<char>(cur, tmp_bytes);
     d_ptmp = carve<char>(cur, pscan_tmp);
+    d_sstate = carve<uint32_t>(cur, 3 + (size_t)prep_tiles);
     return (size_t)(cur - base);
   };
   h3c_rt::DeviceLease lease1(dev, layout(nullptr));
@@ -2587,9 +2684,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     return rocprim::exclusive_scan(d_tmp, t, in, out, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), q);
   };
   uint32_t nofold = 0;  // a redo after a failed A6 knows every verdict: no check moves into the block kernel
-  // the one-pass front (uio_front_kernel) on the first attempt; test hook H3C_HOOK_UPD_FRONT = 1: the
-  // scan-based stage (redone attempts always take that one)
-  const bool front = (h3c_rt::hook(H3C_HOOK_UPD_FRONT) & 1) == 0;
+  const bool front = front_path;
   const bool pb1 = (h3c_rt::hook(H3C_HOOK_UPD_FRONT) & 2) == 0;  // phase B in one launch (uio_phaseb_kernel)
   // per attempt (fragment arrays for a guessed count, see below)
   uint32_t hcap = 256;
@@ -2616,12 +2711,27 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   // speculative sizes / cases / fragment counts
   auto phase_a = [&](hipStream_t q) -> int {
     const uint32_t fz_words = front ? ntiles_front * (uint32_t)(sizeof(FrontSlot) / 4) : 0u;
-    const uint32_t prep_threads = std::max<uint32_t>(std::max<uint32_t>(n, nchunks), std::max(fz_words, front ? hcap : 0u));
-    hipLaunchKernelGGL(uio_prep_kernel, dim3((prep_threads + tb) / tb), dim3(tb), 0, q, d_ios, n, d_chunks, nchunks,
+    // one stream on the front path: the prep kernel scans the piece counts itself, the piece pass
+    // follows the sort, and the A6 verdicts and t0 come with the front kernel -- no fork and join
+    // between streams (each cost ~7-10 us in graph replay: profiles/r03l_*)
+    const bool serial = front && H3C_UIO_SERIAL;
+    // (a kernel, not hipMemsetAsync: a memset node at the head of the captured graph was not
+    // ordered before the prep kernel in replays -- stale tickets, r03m-r03p)
+    if (serial) {
+      hipLaunchKernelGGL(uio_zero_kernel, dim3(1), dim3(256), 0, q, d_sstate, 3u + prep_tiles);
+      HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(uio_prep_kernel, dim3(prep_tiles), dim3(kPrepTile), 0, q, d_ios, n, d_chunks, nchunks,
                        poly_type, stdf, exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc, d_a6,
                        reinterpret_cast<uint32_t *>(d_fslot), fz_words, d_hhead, front ? hcap : 0u, d_gnext, d_fnext,
-                       front ? cap : 0u);
+                       front ? cap : 0u, serial ? d_pbase : nullptr, serial ? d_sstate : nullptr);
     HIP_TRY(hipGetLastError());
+    if (serial) {
+      size_t t = tmp_bytes;
+      HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, q));
+      return h3c_rt::launch_uio_piece_crc(q, dev, poly_type, d_ios, n, d_chunks, nchunks, d_pbase, d_sstate + 2,
+                                          d_paycrc0, d_sstate + 3, kPrepTile);
+    }
     // second stream, forked here: the piece counts' scan (its own scratch), one piece-CRC pass over
     // the payloads that are not fold candidates and the chunks CRC'd from their bytes (before the
     // block kernel overwrites them), then A6 and t0; this stream sorts the ops and runs the sizes
@@ -2695,9 +2805,10 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         hipLaunchKernelGGL(uio_front_kernel, dim3(std::max(ntiles_front, 1u)), dim3(kFrontTile), 0, q, d_ios, d_order,
                            d_skey, n, d_chunks, nchunks, d_status, poly_type, stdf, pc, d_pos, d_nfrag, d_fbase,
                            d_late, d_payraw, d_a6, d_misc, d_frag, d_fkey, cap, d_hhead, hcap - 1, d_gnext, d_prev,
-                           d_fnext, d_fslot);
+                           d_fnext, d_fslot, d_paycrc0, exactf, d_t0, d_chunks_out,
+                           H3C_UIO_SERIAL ? d_sstate : nullptr);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipStreamWaitEvent(q, aux->done, 0));  // the early A6 verdicts and t0
+        if (!H3C_UIO_LATE_JOIN && !H3C_UIO_SERIAL) HIP_TRY(hipStreamWaitEvent(q, aux->done, 0));  // the A6 verdicts, t0
         return H3C_OK;
       }
       if (attempt) HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, q));  // the first attempt's counters
@@ -2740,6 +2851,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       return H3C_OK;
     };
     auto phase_b = [&](hipStream_t q) -> int {
+      if (H3C_UIO_LATE_JOIN && !H3C_UIO_SERIAL && front && attempt == 0) HIP_TRY(hipStreamWaitEvent(q, aux->done, 0));
       if (pb1) {
         hipLaunchKernelGGL(uio_phaseb_kernel, dim3(std::max(ntiles_pb, 1u)), dim3(kPhaseBTile), 0, q, d_pos, d_skey, n,
                            d_eacc, d_payraw, pc, d_a6, d_t0, d_chunks, d_chunks_out, nchunks, poly_type, stdf, d_res,
