@@ -373,8 +373,11 @@ __device__ __forceinline__ uint32_t dxpow8_fast(int64_t e, const PolyConsts *__r
 
 // Per-lane LDS addressing of the replicated tables (see kernel header comment): two registers;
 // the tables' remaining offsets ride in the ds_read immediate.
+#ifndef H3C_LUT2
+#define H3C_LUT2 1  // 0: four offset registers (round 2's form, for A/B)
+#endif
 struct LaneLut {
-  uint32_t off[2];
+  uint32_t off[H3C_LUT2 ? 2 : 4];
 };
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -395,6 +398,7 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // address is one v_perm_b32: byte1 <- byte k of r, bytes 0 and 2 <- the lane's
 // lane offset (byte0 = c<<2, byte2 = t>>1: off[t>>1]), byte3 <- 0; the (t&1)<<7 of tables 1 and 3
 // is the ds_read's immediate offset (two offset registers a lane instead of four).
+#if H3C_LUT2
 __device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
   LaneLut L;
   const uint32_t c4 = (lane & 31u) * 4u;
@@ -413,6 +417,26 @@ __device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const L
   const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3 + 128);
   return xor3(t0, t1, t2) ^ t3;
 }
+#else
+__device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
+  LaneLut L;
+  const uint32_t c4 = (lane & 31u) * 4u;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) L.off[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) << 7) | c4;
+  return L;
+}
+__device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const LaneLut &L) {
+  const uint32_t a0 = __builtin_amdgcn_perm(r, L.off[0], 0x0C020400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(r, L.off[1], 0x0C020500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(r, L.off[2], 0x0C020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(r, L.off[3], 0x0C020700u);
+  const uint32_t t0 = *reinterpret_cast<const uint32_t *>(lb + a0);
+  const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1);
+  const uint32_t t2 = *reinterpret_cast<const uint32_t *>(lb + a2);
+  const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3);
+  return xor3(t0, t1, t2) ^ t3;
+}
+#endif
 // LDS dword i holds table ((i>>14)<<1 | (i>>5)&1), entry (i>>6)&255.
 __device__ __forceinline__ uint32_t fill_value_of(const uint32_t (*tab)[256], int i) {
   return tab[((i >> 14) << 1) | ((i >> 5) & 1)][(i >> 6) & 255];

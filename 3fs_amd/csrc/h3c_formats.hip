@@ -9,6 +9,8 @@
 //     client's fold of split-read checksums (src/client/storage/StorageClientImpl.cc:1607-1633).
 //   * the read path's checksum selection + recalculate verify, AioReadJob::setResult
 //     (src/storage/aio/BatchReadJob.cc:24-55), for a batch of completed read jobs.
+#include <cstdio>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -49,6 +51,11 @@ int one(uint8_t type, const void *data, size_t n, uint32_t start_raw, uint32_t *
   uint8_t t = 0;
   return h3c_batch_create(&d, 1, &t, out_raw, stream);
 }
+// folly's signature has no error channel: a wrong checksum would be silent, so fail loudly
+[[noreturn]] void folly_abort(const char *what, int rc) {
+  std::fprintf(stderr, "%s: engine error %d: %s\n", what, rc, h3c_last_error());
+  std::abort();
+}
 }  // namespace
 
 extern "C" {
@@ -59,6 +66,20 @@ int h3c_crc32c(const void *data, size_t n, uint32_t start_raw, uint32_t *out_raw
 
 int h3c_crc32(const void *data, size_t n, uint32_t start_raw, uint32_t *out_raw, void *stream) {
   return one(H3C_TYPE_CRC32, data, n, start_raw, out_raw, stream);
+}
+
+uint32_t h3c_folly_crc32c(const uint8_t *data, size_t nbytes, uint32_t startingChecksum) {
+  uint32_t v = 0;
+  const int rc = one(H3C_TYPE_CRC32C, data, nbytes, startingChecksum, &v, nullptr);
+  if (rc) folly_abort("h3c_folly_crc32c", rc);
+  return v;
+}
+
+uint32_t h3c_folly_crc32(const uint8_t *data, size_t nbytes, uint32_t startingChecksum) {
+  uint32_t v = 0;
+  const int rc = one(H3C_TYPE_CRC32, data, nbytes, startingChecksum, &v, nullptr);
+  if (rc) folly_abort("h3c_folly_crc32", rc);
+  return v;
 }
 
 uint32_t h3c_serde_checksum_mark(uint32_t crc0, int compressed) { return serde_mark(crc0, compressed); }

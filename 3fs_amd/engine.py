@@ -101,6 +101,8 @@ _proto("h3c_combine_fold", _int, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp)
 _proto("h3c_batch_read_result", _int, _u8, _vp, _sz, _vp, _vp, _vp, _vp)
 _proto("h3c_batch_read_result_ex", _int, _u8, _vp, _sz, _vp, _vp, _vp, _vp, _vp)
 _proto("h3c_crc32c", _int, _vp, _sz, _u32, ctypes.POINTER(_u32), _vp)
+_proto("h3c_folly_crc32c", _u32, _vp, _sz, _u32)
+_proto("h3c_folly_crc32", _u32, _vp, _sz, _u32)
 _proto("h3c_crc32", _int, _vp, _sz, _u32, ctypes.POINTER(_u32), _vp)
 _proto("h3c_hostfed_create", _int, _int, _u64, ctypes.POINTER(_vp))
 _proto("h3c_hostfed_run", _int, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp)

@@ -77,6 +77,16 @@ uint32_t h3c_crc32c_shift(uint32_t crc, uint64_t nbytes);
  * Synchronous; for many buffers use h3c_batch_create. */
 int h3c_crc32c(const void *data, size_t n, uint32_t start_raw, uint32_t *out_raw, void *stream);
 int h3c_crc32(const void *data, size_t n, uint32_t start_raw, uint32_t *out_raw, void *stream);
+/* The same with folly's own signature and return convention, for a call site that is switched
+ * by editing only the function name: folly::crc32c(const uint8_t* data, size_t nbytes,
+ * uint32_t startingChecksum = ~0U) (folly/hash/Checksum.h; called at Common.h:158) and
+ * folly::crc32(...) (Common.h:161).  The result is the raw register (no final XOR), as folly's.
+ * folly's signature has no error channel: an engine failure (no device, a HIP error) prints
+ * h3c_last_error() to stderr and aborts rather than return a wrong checksum.  Synchronous, on the
+ * default stream; a call costs a GPU round trip, so per-IO host buffers belong on the CPU
+ *  and this entry is for GPU-resident buffers at folly call sites. */
+uint32_t h3c_folly_crc32c(const uint8_t *data, size_t nbytes, uint32_t startingChecksum);
+uint32_t h3c_folly_crc32(const uint8_t *data, size_t nbytes, uint32_t startingChecksum);
 
 /* ---- engine lifetime ---- */
 

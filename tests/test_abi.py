@@ -87,6 +87,23 @@ def test_no_gpu_fails_loudly(h3c):
     assert ei.value.code in (9001, 9002)
 
 
+def test_folly_signature_entry_aborts_without_a_gpu(h3c):
+    """h3c_folly_crc32c keeps folly::crc32c's signature (no error channel): with no usable GPU it
+    aborts with the engine's error text instead of returning a wrong checksum."""
+    import subprocess
+    import sys
+
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    code = ("import ctypes; lib = ctypes.CDLL(%r); f = lib.h3c_folly_crc32c; f.restype = ctypes.c_uint32; "
+            "f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32]; print(f(b'abc', 3, 0xFFFFFFFF))"
+            % h3c.lib_path)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "h3c_folly_crc32c" in p.stderr, (p.returncode, p.stdout, p.stderr)
+
+
 def test_update_ios_rejects_inconsistent_chunk_state(h3c):
     """A chunk state whose size exceeds its chunk_size is a caller bug: the whole call fails
     with kInvalidArg before any device work (so this runs without a GPU)."""

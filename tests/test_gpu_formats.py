@@ -186,3 +186,20 @@ def test_create_over_data_iterator(h3c, torch_dev):
         assert CI.create_from_iterator(t, iter(over), 1500) == CI(T.NONE, 0)
         assert CI.create_from_iterator(t, iter([(None, 0)]), 0, 77) == CI(t, 77)
     assert CI.create_from_iterator(T.NONE, iter([(buf, n)]), n) == CI(T.NONE, 0)
+
+
+@pytest.mark.parametrize("n", [0, 1, 15, 4096, 65537, 1 << 20])
+def test_folly_signature_entries_match_oracle(h3c, torch_dev, n):
+    """h3c_folly_crc32c / h3c_folly_crc32: folly::crc32c / crc32's own signature (Common.h:158,161)
+    and raw-register result, on device and host buffers, against the CPU oracle."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(n + 7)
+    host = rng.integers(0, 256, size=n, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    torch.cuda.synchronize()
+    lib = h3c.engine.lib
+    for start in (MASK, 0, 0x12345678):
+        dptr = d.data_ptr() if n else None
+        assert lib.h3c_folly_crc32c(dptr, n, start) == orc.crc32c(host, start), (n, start)
+        assert lib.h3c_folly_crc32c(host.ctypes.data if n else None, n, start) == orc.crc32c(host, start)
+        assert lib.h3c_folly_crc32(dptr, n, start) == orc.crc32(host, start), (n, start)
