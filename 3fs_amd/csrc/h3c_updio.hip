@@ -364,29 +364,32 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
   }
   __syncthreads();
   if (!s_last) return;
-  // the last tile: exclusive scan of the nscan tile totals, in place, in chunks of kPrepTile
-  uint32_t carry = 0;
-  for (uint32_t b0 = 0; b0 < nscan; b0 += kPrepTile) {
-    const uint32_t j = b0 + t;
-    const uint32_t v = j < nscan ? ld_agent(&tbase[j]) : 0u;
-    uint32_t y = v;
+  // the last tile: exclusive scan of the nscan tile totals, in place; thread t takes a contiguous
+  // group of them (all its loads in flight at once), the group sums are scanned across the tile
+  const uint32_t G = (nscan + kPrepTile - 1) / kPrepTile, g0 = t * G, g1 = min(g0 + G, nscan);
+  uint32_t gsum = 0;
+  for (uint32_t j = g0; j < g1; ++j) gsum += ld_agent(&tbase[j]);
+  uint32_t y = gsum;
 #pragma unroll
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-      const uint32_t z = (uint32_t)__shfl_up((int)y, o, 64);
-      if (lane >= o) y += z;
-    }
-    __syncthreads();  // (s_w reuse)
-    if (lane == 63) s_w[wave] = y;
-    __syncthreads();
-    uint32_t wp = 0, all = 0;
-    for (uint32_t w = 0; w < kPrepTile / 64; ++w) {
-      if (w < wave) wp += s_w[w];
-      all += s_w[w];
-    }
-    if (j < nscan) st_agent(&tbase[j], carry + wp + y - v);
-    carry += all;
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t z = (uint32_t)__shfl_up((int)y, o, 64);
+    if (lane >= o) y += z;
   }
-  if (t == 0) st_agent(&sstate[2], carry);
+  __syncthreads();  // (s_w reuse)
+  if (lane == 63) s_w[wave] = y;
+  __syncthreads();
+  uint32_t run = 0, all = 0;
+  for (uint32_t w = 0; w < kPrepTile / 64; ++w) {
+    if (w < wave) run += s_w[w];
+    all += s_w[w];
+  }
+  run += y - gsum;  // this group's base
+  for (uint32_t j = g0; j < g1; ++j) {
+    const uint32_t v = ld_agent(&tbase[j]);
+    st_agent(&tbase[j], run);
+    run += v;
+  }
+  if (t == 0) st_agent(&sstate[2], all);
 }
 
 __device__ __forceinline__ bool applied_kind(uint8_t kind) {
@@ -842,6 +845,9 @@ __global__ void uio_heads_kernel(const uint32_t *__restrict__ prev, const uint32
 //      walk their bucket's list for the largest earlier fragment of their key.
 // Waits are bounded: a tile that gives up sets bit 1 of misc[kMiscA6] -- the pass is void, the
 // block kernel writes nothing and the host redoes the batch on the scan-based stage.
+#ifndef H3C_PB_TRACE
+#define H3C_PB_TRACE 0  // 1: phase B tiles 0, 1, the middle one and the last print their step times
+#endif
 #ifndef H3C_FRONT_TRACE
 #define H3C_FRONT_TRACE 0  // 1: tiles 0, 1, the middle one and the last print their step times (diagnostics)
 #endif
@@ -2069,6 +2075,13 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
   if (p0 >= n) return;  // (whole workgroup)
   const uint32_t cnt = min(T, n - p0), tlast = cnt - 1;
   const bool valid = t < cnt;
+#if H3C_PB_TRACE
+  uint64_t tr[6];
+  tr[0] = wall_clock64();
+#define PB_MARK(j) (tr[j] = wall_clock64())
+#else
+#define PB_MARK(j) ((void)0)
+#endif
   const uint32_t p = p0 + t;
   const uint32_t c = valid ? skey[p] : 0xFFFFFFFFu;
   OpPos r{};
@@ -2079,6 +2092,7 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
   const uint32_t c0 = s_key[0];
   const uint32_t head = (t == 0 || c != s_key[t - 1]) ? 1u : 0u;
   PhaseBSlot &me = slots[k];
+  PB_MARK(1);
   // t-scan
   Aff tin = aff_tile_scan(valid ? t_map(r, eacc, payraw, p, pc, a6) : Aff{kOne, 0u}, head, poly, lane, wave, sw);
   if (t == tlast) {
@@ -2101,6 +2115,7 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
     pub_flag(&me.flag[0], 2u);
   }
   __syncthreads();  // (s_c is reused below)
+  PB_MARK(2);
   // s-scan, from each op's t
   Aff sin = aff_tile_scan(valid ? s_map_at(r, c, nchunks, tin, t0v, eacc, payraw, p, pc, a6) : Aff{kOne, 0u}, head,
                           poly, lane, wave, sw);
@@ -2121,6 +2136,7 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
     st_agent(&me.incl[1], aff_bits(sin));
     pub_flag(&me.flag[1], 2u);
   }
+  PB_MARK(3);
   // results
   if (p == 0) {  // the pass's outcome, for the host's one read-back (written through: the last tile copies it)
     st_agent(&misc[kMiscOutF], *d_F);
@@ -2132,6 +2148,17 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
   __shared__ unsigned int sh[8];
   ctr_add_block(sh, ctr, v);
   if (s_void && t == 0) atomicOr(&misc[kMiscPBVoid], 1u);  // the host reruns phase B the scan-based way
+#if H3C_PB_TRACE
+  __syncthreads();
+  PB_MARK(4);
+  {
+    const uint32_t ntl = (n + T - 1) / T;
+    if (t == 0 && (k < 2 || k == ntl / 2 || k + 1 == ntl))
+      printf("phaseb tile %u start %llu loads %llu tscan %llu sscan %llu results %llu (ticks)\n", k,
+             (unsigned long long)tr[0], (unsigned long long)(tr[1] - tr[0]), (unsigned long long)(tr[2] - tr[0]),
+             (unsigned long long)(tr[3] - tr[0]), (unsigned long long)(tr[4] - tr[0]));
+  }
+#endif
   if (hout && t == 0) {
     // the last tile to finish hands the outcome words straight to the caller's pinned host buffer
     // (no device-to-host copy after the kernel); every tile's misc traffic is at the coherence

@@ -7,7 +7,8 @@ T=$1; LOG=$2; CMD=$3
 for attempt in 1 2 3 4 5 6 7 8; do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$CMD" > "$LOG" 2>&1
   rc=$?
-  if grep -q "status=transient" "$LOG" && ! grep -q "run [1-9]" "$LOG"; then
+  if grep -q "status=transient\|taken away by the GPU service\|no free box\|are busy\|backing off" "$LOG" \
+     && ! grep -q "run [1-9][0-9]*\.[0-9]*s of limit" "$LOG"; then
     echo "attempt $attempt: transient, waiting" >&2
     sleep $((60 * attempt))
     continue
