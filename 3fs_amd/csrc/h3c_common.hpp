@@ -3,6 +3,7 @@
 // Everything here has internal linkage (anonymous namespace); the shared runtime
 // state lives behind the h3c_rt:: functions defined in h3c_engine.hip.
 #pragma once
+#include <cstddef>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -245,6 +246,7 @@ struct PolyConsts {
 constexpr int kRedTables = 7;
 constexpr int kRedWords = kRedTables * 4 * 256;  // 7168 dwords = 28 KiB of LDS
 
+static_assert(offsetof(PolyConsts, red) % 16 == 0, "fill_tables copies the fold tables in 16-byte pieces");
 inline void build_consts(PolyConsts &pc, uint32_t poly) {
   std::memset(&pc, 0, sizeof(pc));
   pc.poly = poly;
@@ -366,6 +368,9 @@ __device__ __forceinline__ uint32_t dxpow8_fast(int64_t e, const PolyConsts *__r
 
 #ifndef H3C_PERM_LAYOUT
 #define H3C_PERM_LAYOUT 1
+#endif
+#ifndef H3C_FAST_FILL
+#define H3C_FAST_FILL 1  // fill_tables: one load per table entry (0: one per LDS dword, for A/B)
 #endif
 #ifndef H3C_XOR3_ASM
 #define H3C_XOR3_ASM 1
@@ -490,6 +495,30 @@ __device__ __forceinline__ uint32_t fill_value_of(const uint32_t (*tab)[256], in
   return tab[i >> 13][(i >> 5) & 255];
 }
 #endif
+// The replicated stride tables and the fold tables into LDS (no barrier: the caller's).  With
+// the 32-copy layout each table entry is loaded from HBM / L2 once and its 32 copies -- 128
+// contiguous bytes -- written with 8 ds_write_b128 (the dword-per-copy loop loaded every entry 32
+// times: ~20 us at the start of every workgroup); the fold tables go over in 16-byte pieces.
+// `lds` must be 16-byte aligned; `red_words` a multiple of 4.
+__device__ __forceinline__ void fill_tables(uint32_t *lds, const uint32_t (*tab)[256], const uint32_t *red_g,
+                                            uint32_t red_words, uint32_t tid, uint32_t nthreads) {
+#if H3C_PERM_LAYOUT && H3C_FAST_FILL
+  for (uint32_t e = tid; e < 1024u; e += nthreads) {
+    const uint32_t t = e >> 8, b = e & 255u;
+    const uint32_t v = tab[t][b];
+    uint4 *dst = reinterpret_cast<uint4 *>(lds + (t >> 1) * 16384u + b * 64u + (t & 1u) * 32u);
+    const uint4 q = make_uint4(v, v, v, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[j] = q;
+  }
+  const uint4 *rs = reinterpret_cast<const uint4 *>(red_g);
+  uint4 *rd = reinterpret_cast<uint4 *>(lds + kLdsWords);
+  for (uint32_t i = tid; i < red_words / 4u; i += nthreads) rd[i] = rs[i];
+#else
+  for (uint32_t i = tid; i < (uint32_t)kLdsWords; i += nthreads) lds[i] = fill_value_of(tab, i);
+  for (uint32_t i = tid; i < red_words; i += nthreads) lds[kLdsWords + i] = red_g[i];
+#endif
+}
 // The LDS image of the 1 KiB-stride tables (rows of 64 lanes x 16 B).
 __device__ __forceinline__ uint32_t fill_value(const PolyConsts *__restrict__ pc, int i) {
   return fill_value_of(pc->tab, i);

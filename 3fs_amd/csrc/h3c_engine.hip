@@ -56,12 +56,8 @@ __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__res
                                                            uint32_t total_segs, uint64_t seg_bytes, uint32_t dbg,
                                                            const PolyConsts *__restrict__ pc,
                                                            uint32_t *__restrict__ seg_crc) {
-  __shared__ uint32_t lds[kLdsWords + (H3C_SEG_FOLD_TAB ? kRedWords : 0)];
-  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
-#if H3C_SEG_FOLD_TAB
-  const uint32_t *red_g = &pc->red[0][0][0];
-  for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
-#endif
+  __shared__ alignas(16) uint32_t lds[kLdsWords + (H3C_SEG_FOLD_TAB ? kRedWords : 0)];
+  fill_tables(lds, pc->tab, &pc->red[0][0][0], H3C_SEG_FOLD_TAB ? kRedWords : 0, threadIdx.x, kThreads);
   __syncthreads();
   const uint32_t *red = lds + kLdsWords;
 
@@ -133,10 +129,8 @@ __global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__r
                                                              const uint32_t *__restrict__ expected,
                                                              uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
                                                              uint32_t *__restrict__ mismatch) {
-  __shared__ uint32_t lds[kLdsWords + kRedWords];
-  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
-  const uint32_t *red_g = &pc->red[0][0][0];
-  for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
+  fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kThreads);
   __syncthreads();
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
@@ -308,11 +302,9 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
   constexpr uint32_t NG = 64 / G;                        // chunks per wave step
   constexpr int kRed = (1 + kLw + kLevels) * 1024;       // x^-32, x^-128 (W = 2), the tree levels
   constexpr uint64_t kQ = 16u * G * W;                   // row bytes
-  __shared__ uint32_t lds[kLdsWords + kRed];
-  for (int i = threadIdx.x; i < kLdsWords; i += kThreads)
-    lds[i] = fill_value_of(kQ == 256 ? pc->tabq : kQ == 128 ? pc->tabo : pc->tabf, i);
-  const uint32_t *red_g = &pc->red[0][0][0];
-  for (int i = threadIdx.x; i < kRed; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  __shared__ alignas(16) uint32_t lds[kLdsWords + kRed];
+  fill_tables(lds, kQ == 256 ? pc->tabq : kQ == 128 ? pc->tabo : pc->tabf, &pc->red[0][0][0], kRed, threadIdx.x,
+              kThreads);
   __syncthreads();
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
@@ -482,15 +474,18 @@ __global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni
   constexpr uint32_t kStep = NG * C;  // chunks per wave step
   constexpr int kRed = (1 + kLevels) * 1024;
   constexpr uint64_t kQ = 16u * G;
-  __shared__ uint32_t lds[kUniLdsWords + kRed];
+  __shared__ alignas(16) uint32_t lds[kUniLdsWords + kRed];
   __shared__ uint32_t wg_next;
   {
     const uint32_t(*tab)[256] = kQ == 256 ? pc->tabq : kQ == 128 ? pc->tabo : kQ == 64 ? pc->tabf : kQ == 32 ? pc->tab2 : pc->tab1;
-    for (int i = threadIdx.x; i < kUniLdsWords; i += kUniThreads)
-      lds[i] = kUniCopies == 16 ? fill_value16_of(tab, i) : fill_value_of(tab, i);
+    if constexpr (kUniCopies == 16) {
+      for (int i = threadIdx.x; i < kUniLdsWords; i += kUniThreads) lds[i] = fill_value16_of(tab, i);
+      const uint32_t *red_g = &pc->red[0][0][0];
+      for (int i = threadIdx.x; i < kRed; i += kUniThreads) lds[kUniLdsWords + i] = red_g[i];
+    } else {
+      fill_tables(lds, tab, &pc->red[0][0][0], kRed, threadIdx.x, kUniThreads);
+    }
   }
-  const uint32_t *red_g = &pc->red[0][0][0];
-  for (int i = threadIdx.x; i < kRed; i += kUniThreads) lds[kUniLdsWords + i] = red_g[i];
   const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
 #if H3C_UNI_DYNAMIC
   // The workgroup owns a contiguous range; its waves take steps of kStep chunks from an LDS
@@ -668,16 +663,14 @@ __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(Src src, const u
   constexpr int G = 4, kLevels = 2, NG = 64 / G;
   constexpr uint64_t kQ = 16u * G;
   constexpr int kRed = (1 + kLevels) * 1024;
-  __shared__ uint32_t lds[kLdsWords + kRed];
+  __shared__ alignas(16) uint32_t lds[kLdsWords + kRed];
   const uint32_t total = *d_total;
   // Each workgroup owns a contiguous range; one with none returns before filling its tables (a
   // pass with few or no pieces -- the UpdateIO late pass, usually empty -- costs a launch only).
   const uint32_t wlo = (uint32_t)((uint64_t)blockIdx.x * total / gridDim.x);
   const uint32_t whi = (uint32_t)((uint64_t)(blockIdx.x + 1) * total / gridDim.x);
   if (wlo >= whi) return;
-  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value_of(pc->tabf, i);
-  const uint32_t *red_g = &pc->red[0][0][0];
-  for (int i = threadIdx.x; i < kRed; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  fill_tables(lds, pc->tabf, &pc->red[0][0][0], kRed, threadIdx.x, kThreads);
   __syncthreads();
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);

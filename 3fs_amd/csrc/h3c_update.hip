@@ -252,10 +252,8 @@ __global__ __launch_bounds__(kThreads) void upd_delta_kernel(
     const uint32_t *__restrict__ blk_chunk, const uint32_t *__restrict__ blk_index, const uint8_t *payload,
     uint32_t n, const uint32_t *__restrict__ prev, const uint32_t *__restrict__ final_of,
     const PolyConsts *__restrict__ pc, uint32_t *__restrict__ delta) {
-  __shared__ uint32_t lds[kLdsWords + kRedWords];
-  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
-  const uint32_t *red_g = &pc->red[0][0][0];
-  for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
+  fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kThreads);
   __syncthreads();
   const uint32_t *red = lds + kLdsWords;
   const uint32_t lane = threadIdx.x & 63;
@@ -417,7 +415,7 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
     uint32_t *__restrict__ out_raw, uint32_t *__restrict__ raw_out, uint32_t *__restrict__ n_invalid,
     unsigned long long *__restrict__ counters, uint32_t force_timeout) {
   constexpr uint32_t G4 = 4096;
-  __shared__ uint32_t lds[kLdsWords + kRedWords];
+  __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
   __shared__ uint32_t s_ticket;
   if (threadIdx.x == 0) s_ticket = atomicAdd(&ctl[kCtlTicket], 1u);
   __syncthreads();
@@ -494,9 +492,7 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
     }
   };
   if (lo < hi) start_group(lo);  // the first group's links and rows load while the tables fill
-  for (int i = threadIdx.x; i < kLdsWords; i += kThreads) lds[i] = fill_value(pc, i);
-  const uint32_t *red_g = &pc->red[0][0][0];
-  for (int i = threadIdx.x; i < kRedWords; i += kThreads) lds[kLdsWords + i] = red_g[i];
+  fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kThreads);
   __syncthreads();
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);

@@ -1382,6 +1382,9 @@ constexpr uint32_t kBlkWaves = H3C_UIO_BLOCK_WAVES, kBlkThreads = 64 * kBlkWaves
 #ifndef H3C_UIO_LATE_JOIN
 #define H3C_UIO_LATE_JOIN 0  // timing experiment only: the block kernel does not wait for the second stream
 #endif                       // (unsafe: a failed non-fold A6 check would not stop its writes)
+#ifndef H3C_UIO_EARLY
+#define H3C_UIO_EARLY 1  // block kernel: the first fragment's rows load before the LDS table fill
+#endif
 #ifndef H3C_UIO_GRAB
 #define H3C_UIO_GRAB 0  // block kernel: fragments a wave takes per grab from an LDS counter (0: one fixed range per wave; 2 spills, 353 vs 282 us: r03i)
 #endif
@@ -1543,11 +1546,13 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
                                                uint32_t *__restrict__ eacc, const uint32_t *__restrict__ misc,
                                                uint32_t *lds, uint32_t std_domain, uint32_t *__restrict__ payraw,
                                                uint32_t *__restrict__ a6, uint32_t *misc_w) {
-  for (int i = threadIdx.x; i < kLdsWords; i += kBlkThreads) lds[i] = fill_value(pc, i);
-  const uint32_t *red_g = &pc->red[0][0][0];
-  for (int i = threadIdx.x; i < kRedWords; i += kBlkThreads) lds[kLdsWords + i] = red_g[i];
-  if (threadIdx.x == 0) lds[kLdsWords + kRedWords] = 0;  // the waves' range counter (H3C_UIO_GRAB)
-  __syncthreads();
+  auto fill_lds = [&]() {  // the stride and fold tables (156 KiB), then a barrier
+    fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kBlkThreads);
+    if (threadIdx.x == 0) lds[kLdsWords + kRedWords] = 0;  // the waves' range counter (H3C_UIO_GRAB)
+    __syncthreads();
+  };
+  constexpr bool kEarlyRows = H3C_UIO_EARLY && H3C_UIO_SFIELDS && !H3C_UIO_GRAB;  // first rows before the fill
+  if (!kEarlyRows) fill_lds();
   const uint32_t F = misc[kMiscA6] ? 0u : frag_count(d_F, cap);  // a failed A6: this pass writes nothing
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
@@ -1564,7 +1569,7 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
   const uint32_t wg_hi = (uint32_t)((uint64_t)(blockIdx.x + 1) * F / gridDim.x);
 #else
   const uint32_t lo = (uint32_t)(gw * F / nw), hi = (uint32_t)((gw + 1) * F / nw);
-  if (lo >= hi) return;
+  if (!kEarlyRows && lo >= hi) return;
 #endif
   const uint32_t poly = pc->poly;
   const LaneLut L = make_lut(lane);
@@ -1665,9 +1670,15 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
     cur = nxt;
   }
 #else
-  addr_of(lo, c_blk, c_src, c_w, c_k);
-  load_task_rows(c_blk, c_k & 0xFFFFu, c_k >> 16, c_src, c_w & 0xFFFFu, c_w >> 16, lane, cur);
-  if (lo + 1 < hi) addr_of(lo + 1, n_blk, n_src, n_w, n_k);
+  // the first fragment's rows are in flight while the workgroup fills its LDS tables (a wave with
+  // no fragment still takes part in the fill's barrier)
+  if (lo < hi) {
+    addr_of(lo, c_blk, c_src, c_w, c_k);
+    load_task_rows(c_blk, c_k & 0xFFFFu, c_k >> 16, c_src, c_w & 0xFFFFu, c_w >> 16, lane, cur);
+    if (lo + 1 < hi) addr_of(lo + 1, n_blk, n_src, n_w, n_k);
+  }
+  if (kEarlyRows) fill_lds();
+  if (lo >= hi) return;
   for (uint32_t g = lo; g < hi; ++g) {
     const uint64_t blk = c_blk;
     const uint32_t kk = c_k;
@@ -1769,7 +1780,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_block_kernel(const FragDesc *
                                                              uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6,
                                                              uint32_t *__restrict__ pbz, uint32_t pbz_words,
                                                              uint32_t *__restrict__ misc_w) {
-  __shared__ uint32_t lds[kLdsWords + kRedWords + 1];
+  __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords + 1];
   if (ts && threadIdx.x == 0) atomicMin(&ts[0], (unsigned long long)wall_clock64());
   if (blockIdx.x == 0) {  // uio_phaseb_kernel's tile states and ticket, fresh for every attempt
     for (uint32_t i = threadIdx.x; i < pbz_words; i += blockDim.x) pbz[i] = 0;
