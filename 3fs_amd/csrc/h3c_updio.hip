@@ -249,7 +249,7 @@ __device__ __forceinline__ void pub_flag(uint32_t *f, uint32_t v) {
 // tile of kPrepTile items writes its items' exclusive offsets within the tile to pbase[] and its
 // total to tbase[k]; the last tile to finish turns tbase[] into the tiles' exclusive bases (item
 // i's offset is pbase[i] + tbase[i / kPrepTile]; op_piece_crc_kernel adds them).  `sstate`
-// (zeroed by the caller): [0] the ticket, [1] finished tiles, [2] the total, [3 + k] tbase[k].
+// (zeroed by the caller): [0] unused, [1] finished tiles, [2] the total, [3 + k] tbase[k].
 __global__ void uio_zero_kernel(uint32_t *__restrict__ p, uint32_t n) {
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0;
 }
@@ -262,18 +262,19 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
     uint32_t *__restrict__ a6, uint32_t *__restrict__ fz, uint32_t fz_words, uint32_t *__restrict__ hhead,
     uint32_t hcap, uint32_t *__restrict__ gnext, uint32_t *__restrict__ fnext, uint32_t fcap,
     uint32_t *__restrict__ pbase, uint32_t *sstate) {
-  __shared__ uint32_t s_tile, s_w[kPrepTile / 64], s_last;
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (pbase) {  // ticket order for the look-back (tile k waits only on tiles already running)
-    if (threadIdx.x == 0) s_tile = atomicAdd(&sstate[0], 1u);
-    __syncthreads();
-    i = s_tile * blockDim.x + threadIdx.x;
-  }
-  if (i < fz_words) fz[i] = 0;        // the one-pass front's tile states (uio_front_kernel)
-  if (i < hcap) hhead[i] = 0xFFFFFFFFu;  // ... its link hash's bucket heads
-  if (i < fcap) {                     // ... its bucket lists' next pointers and the chains'
-    gnext[i] = 0xFFFFFFFEu;           // (kPending)
-    fnext[i] = 0xFFFFFFFFu;           // (kNil)
+  __shared__ uint32_t s_w[kPrepTile / 64], s_last;
+  // No tile waits on another (the last one to finish scans the tile totals), so tiles need no
+  // ticket: one agent-scope atomic per tile on one address serialises beyond the XCDs' L2s.
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  // the front kernel's initialisations, grid-strided (the grid may cover only the items)
+  const uint32_t init_n = max(max(fz_words, hcap), fcap);
+  for (uint32_t j = i; j < init_n; j += gridDim.x * blockDim.x) {
+    if (j < fz_words) fz[j] = 0;        // the one-pass front's tile states (uio_front_kernel)
+    if (j < hcap) hhead[j] = 0xFFFFFFFFu;  // ... its link hash's bucket heads
+    if (j < fcap) {                     // ... its bucket lists' next pointers and the chains'
+      gnext[j] = 0xFFFFFFFEu;           // (kPending)
+      fnext[j] = 0xFFFFFFFFu;           // (kNil)
+    }
   }
   if (i < kCtrN) ctr[i] = 0;
   if (i < kMiscN) misc[i] = i == kMiscT0 || i == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;
@@ -353,7 +354,7 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
     if (w < wave) wpre += s_w[w];
     tot += s_w[w];
   }
-  const uint32_t k = s_tile, nscan = (n + C + 1 + kPrepTile - 1) / kPrepTile;
+  const uint32_t k = blockIdx.x, nscan = (n + C + 1 + kPrepTile - 1) / kPrepTile;
   if (k >= nscan) return;  // (whole tile: no item)
   uint32_t *tbase = sstate + 3;
   if (i <= n + C) pbase[i] = wpre + x - np;
@@ -2759,7 +2760,10 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       hipLaunchKernelGGL(uio_zero_kernel, dim3(1), dim3(256), 0, q, d_sstate, 3u + prep_tiles);
       HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(uio_prep_kernel, dim3(prep_tiles), dim3(kPrepTile), 0, q, d_ios, n, d_chunks, nchunks,
+    // serial: one tile per 256 items (the initialisations beyond them grid-stride), so only the
+    // tiles that count toward the last-tile test run
+    const uint32_t ptiles = serial ? (uint32_t)(((size_t)n + C + 1 + kPrepTile - 1) / kPrepTile) : prep_tiles;
+    hipLaunchKernelGGL(uio_prep_kernel, dim3(ptiles), dim3(kPrepTile), 0, q, d_ios, n, d_chunks, nchunks,
                        poly_type, stdf, exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc, d_a6,
                        reinterpret_cast<uint32_t *>(d_fslot), fz_words, d_hhead, front ? hcap : 0u, d_gnext, d_fnext,
                        front ? cap : 0u, serial ? d_pbase : nullptr, serial ? d_sstate : nullptr);
