@@ -253,7 +253,10 @@ __device__ __forceinline__ void pub_flag(uint32_t *f, uint32_t v) {
 __global__ void uio_zero_kernel(uint32_t *__restrict__ p, uint32_t n) {
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0;
 }
-constexpr uint32_t kPrepTile = 256;
+#ifndef H3C_PREP_TILE
+#define H3C_PREP_TILE 1024  // items per prep-kernel tile (a power of two, 64..1024)
+#endif
+constexpr uint32_t kPrepTile = H3C_PREP_TILE;
 __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
     const h3c_update_io *__restrict__ ios, uint32_t n, const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks,
     uint8_t poly_type, uint32_t std_domain, uint32_t exact, uint32_t *__restrict__ status, uint32_t *__restrict__ key,
