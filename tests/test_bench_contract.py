@@ -77,3 +77,23 @@ def test_failed_rank_fails_the_launch():
     that ends the ranks left waiting in the rendezvous."""
     rc, lines, err = _bench(["--gpus", "2", "--dry-run-launch", "1"], {"H3C_BENCH_GRACE_S": "3"})
     assert rc == 3 and not lines
+
+
+def test_more_ranks_than_gpus_is_refused_unless_rehearsal():
+    """WORLD_SIZE > visible GPUs exits non-zero; --allow-shared-devices allows it and
+    the line then reports the distinct devices used (with "rehearsal": true)."""
+    b = load_bench()
+    assert b.check_devices(8, 8, False) is None and b.check_devices(1, 1, False) is None
+    err = b.check_devices(8, 1, False)
+    assert err and "allow-shared-devices" in err
+    assert b.check_devices(8, 1, True) is None
+    assert b.check_devices(2, 0, False)  # no GPU at all
+    assert b.devices_used(8, 1) == 1 and b.devices_used(8, 8) == 8 and b.devices_used(2, 4) == 2
+
+
+def test_oversubscribed_launch_exits_nonzero_on_cpu():
+    """On this GPU-less container every real (non dry-run) rank sees 0 devices: the N=2 launch fails
+    before any GPU work, with the reason on stderr."""
+    rc, lines, err = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], {"H3C_BENCH_GRACE_S": "3"},
+                            timeout=300)
+    assert rc == 2 and not lines and "allow-shared-devices" in err
