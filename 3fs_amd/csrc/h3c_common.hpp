@@ -137,7 +137,7 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
 int launch_uio_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, uint32_t n,
                          const h3c_chunk_state *chunks, uint32_t nchunks, const uint32_t *pbase,
                          const uint32_t *d_total, uint32_t *crc0_out, const uint32_t *tbase = nullptr,
-                         uint32_t tile = 0);  // tbase: item i's offset is pbase[i] + tbase[i / tile]
+                         uint32_t tile = 0, uint32_t *err = nullptr);  // err: set when a piece falls outside its item  // tbase: item i's offset is pbase[i] + tbase[i / tile]
 // Rows (1 KiB, absolute alignment) a byte range touches.
 inline uint32_t host_rows(uint64_t ptr, uint64_t len) {
   return len ? (uint32_t)((((ptr + len + 1023) & ~uint64_t(1023)) - (ptr & ~uint64_t(1023))) / 1024) : 0;
@@ -550,6 +550,22 @@ __device__ __forceinline__ uint4 load_row(uint64_t a) {
   const v4u v = *(gv4p)a;
 #endif
   return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// A row load of a kernel whose rows per chunk are narrower than a 128-byte line (fewer than 8 lanes x
+// 16 B: the small-chunk kernels' 4-lane groups, 64-byte rows).  Nontemporal loads skip the CU's L1, so
+// the two 64-byte halves of a line reach L2 as separate requests, and 7-8 % of the lines were fetched
+// from HBM twice (TCC_MISS 1.077x the lines of an 8 GiB probe; plain loads: 1.000x, at the same speed:
+// scripts/fetchcal.hip, profiles/r04_fetchcal.txt).  Plain loads keep the line in L1 for its other half.
+template <uint64_t kRowBytesPerChunk>
+__device__ __forceinline__ uint4 load_row_w(uint64_t a) {
+  if (kRowBytesPerChunk >= 128) return load_row(a);
+#ifndef H3C_SUBLINE_NT
+  const v4u v = *(gv4p)a;
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return load_row(a);  // (A/B: round 3's nontemporal sub-line rows)
+#endif
 }
 
 // Edge-row load: bytes outside [s, e) read as zero; a piece with no byte inside

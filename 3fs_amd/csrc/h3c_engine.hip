@@ -354,7 +354,7 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
   for (int b = 0; b < kQuadBatch; ++b)
 #pragma unroll
     for (int w = 0; w < W; ++w)
-      cur[b][w] = (uint32_t)b < K ? load_row(la + (uint64_t)b * kQ + 16u * w) : make_uint4(0, 0, 0, 0);
+      cur[b][w] = (uint32_t)b < K ? load_row_w<kQ>(la + (uint64_t)b * kQ + 16u * w) : make_uint4(0, 0, 0, 0);
   for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
     const uint32_t cnt = m.cnt;
     const Desc n = load_desc(hi - g0 > 64 ? g0 + 64 : hi);
@@ -382,13 +382,13 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
           for (int b = 0; b < kQuadBatch; ++b)
 #pragma unroll
             for (int w = 0; w < W; ++w)
-              nxt[b][w] = n0 + b < K ? load_row(la + (uint64_t)(n0 + b) * kQ + 16u * w) : make_uint4(0, 0, 0, 0);
+              nxt[b][w] = n0 + b < K ? load_row_w<kQ>(la + (uint64_t)(n0 + b) * kQ + 16u * w) : make_uint4(0, 0, 0, 0);
         } else {
 #pragma unroll
           for (int b = 0; b < kQuadBatch; ++b)
 #pragma unroll
             for (int w = 0; w < W; ++w)
-              nxt[b][w] = (uint32_t)b < K1 ? load_row(la1 + (uint64_t)b * kQ + 16u * w) : make_uint4(0, 0, 0, 0);
+              nxt[b][w] = (uint32_t)b < K1 ? load_row_w<kQ>(la1 + (uint64_t)b * kQ + 16u * w) : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int b = 0; b < kQuadBatch; ++b) {
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni
   for (int j = 0; j < C; ++j)
 #pragma unroll
     for (int b = 0; b < kUniBatch; ++b)
-      cur[j][b] = valid[j] && (uint32_t)b < K ? load_row(la[j] + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+      cur[j][b] = valid[j] && (uint32_t)b < K ? load_row_w<kQ * C>(la[j] + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
 #if H3C_UNI_DYNAMIC
   for (uint32_t q0 = lo; q0 < hi;) {
     const uint32_t qn = grab();  // the next step, taken now so its rows load during this one's last batch
@@ -569,13 +569,13 @@ __global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni
         for (int b = 0; b < kUniBatch; ++b)
 #pragma unroll
           for (int j = 0; j < C; ++j)
-            nxt[j][b] = valid[j] && n0 + b < K ? load_row(la[j] + (uint64_t)(n0 + b) * kQ) : make_uint4(0, 0, 0, 0);
+            nxt[j][b] = valid[j] && n0 + b < K ? load_row_w<kQ * C>(la[j] + (uint64_t)(n0 + b) * kQ) : make_uint4(0, 0, 0, 0);
       } else {
 #pragma unroll
         for (int b = 0; b < kUniBatch; ++b)
 #pragma unroll
           for (int j = 0; j < C; ++j)
-            nxt[j][b] = valid1[j] && (uint32_t)b < K ? load_row(la1[j] + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+            nxt[j][b] = valid1[j] && (uint32_t)b < K ? load_row_w<kQ * C>(la1[j] + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int b = 0; b < kUniBatch; ++b)
@@ -659,7 +659,8 @@ __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(Src src, const u
                                                                 const uint32_t *__restrict__ d_total,
                                                                 const PolyConsts *__restrict__ pc,
                                                                 uint32_t *__restrict__ crc0_out,
-                                                                const uint32_t *__restrict__ tbase, uint32_t tshift) {
+                                                                const uint32_t *__restrict__ tbase, uint32_t tshift,
+                                                                uint32_t *err) {
   constexpr int G = 4, kLevels = 2, NG = 64 / G;
   constexpr uint64_t kQ = 16u * G;
   constexpr int kRed = (1 + kLevels) * 1024;
@@ -716,8 +717,9 @@ __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(Src src, const u
         S = base + off;
         E = S + plen;
         shift = length - off - plen;
-      } else {  // (a piece table that disagrees with the items: read nothing)
+      } else {  // a piece table that disagrees with the items: read nothing, and fail the call
         valid = false;
+        if (err) atomicOr(err, 1u);
       }
     }
     const uint64_t base = S & ~(kQ - 1);
@@ -729,11 +731,11 @@ __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(Src src, const u
     Streams st{0, 0, 0, 0};
     uint4 cur[4], nxt[4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) cur[b] = (uint32_t)b < K ? load_row(la + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
+    for (int b = 0; b < 4; ++b) cur[b] = (uint32_t)b < K ? load_row_w<kQ>(la + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
     for (uint32_t u0 = 0; u0 < kmax; u0 += 4) {
       const uint32_t n0 = u0 + 4;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) nxt[b] = n0 + b < K ? load_row(la + (uint64_t)(n0 + b) * kQ) : make_uint4(0, 0, 0, 0);
+      for (int b = 0; b < 4; ++b) nxt[b] = n0 + b < K ? load_row_w<kQ>(la + (uint64_t)(n0 + b) * kQ) : make_uint4(0, 0, 0, 0);
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const uint32_t u = u0 + b;
@@ -954,11 +956,11 @@ int current_device(int *dev) {
 }
 
 // h3c_test_hook state: read from the environment once, settable by tests.
-constexpr int kHooks = 7;
+constexpr int kHooks = 9;
 std::atomic<uint64_t> g_hooks[kHooks];
 const bool g_hooks_init = [] {
   const char *names[kHooks] = {nullptr, "H3C_SEG_BYTES", "H3C_DEBUG_FLAGS", "H3C_UPD_SCAN", "H3C_UPD_GRAPHS",
-                                "H3C_UPD_LOOKBACK", "H3C_UPD_FRONT"};
+                                "H3C_UPD_LOOKBACK", "H3C_UPD_FRONT", "H3C_UPD_FAST", "H3C_UPD_GIVEUP"};
   for (int k = 1; k < kHooks; ++k) {
     uint64_t v = 0;
     if (const char *e = std::getenv(names[k])) {
@@ -1193,12 +1195,13 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
 #endif
 int launch_uio_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io *ios, uint32_t n,
                          const h3c_chunk_state *chunks, uint32_t nchunks, const uint32_t *pbase,
-                         const uint32_t *d_total, uint32_t *crc0_out, const uint32_t *tbase, uint32_t tile) {
+                         const uint32_t *d_total, uint32_t *crc0_out, const uint32_t *tbase, uint32_t tile,
+                         uint32_t *err) {
   const DeviceCtx &ctx = g_dev[dev];
   const PolyConsts *pc = ctx.d_consts[type == H3C_TYPE_CRC32 ? 1 : 0];
   hipLaunchKernelGGL(op_piece_crc_kernel<UioPieceSrc>, dim3(std::max(ctx.num_cu * H3C_PIECE_CU_PCT / 100, 1)),
                      dim3(kThreads), 0, st, UioPieceSrc{ios, chunks, n}, pbase, n + nchunks, d_total, pc, crc0_out, tbase,
-                     tbase ? (uint32_t)__builtin_ctz(tile) : 0u);
+                     tbase ? (uint32_t)__builtin_ctz(tile) : 0u, err);
   HIP_TRY(hipGetLastError());
   return H3C_OK;
 }

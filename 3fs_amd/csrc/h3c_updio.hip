@@ -75,7 +75,17 @@ enum { kCtrNone, kCtrReuse, kCtrCombine, kCtrRead, kCtrRecalc, kCtrMismatch, kCt
 // timing when it runs inside a replayed graph (read back with the two words before them)
 // [kMiscTicket]: uio_front_kernel's tile ticket; [kMiscPBVoid]: a uio_phaseb_kernel tile gave up waiting;
 // [kMiscPBDone]: uio_phaseb_kernel's finished tiles (the last one copies [kMiscOutF, kMiscN) to the host);
-enum { kMiscTicket = 0, kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscT0 = 4, kMiscT1 = 6, kMiscPBVoid = 8, kMiscPBDone = 9, kMiscN = 10 };
+// [kMiscFast]: the fast branch's outcome (kFast*; 0 on the general pipeline); [kMiscErr]: a kernel met an
+// inconsistent table (a piece table that disagrees with its items) -- the call fails.
+// Past kMiscN (not copied back): [kMiscFTicket] / [kMiscFDone] uio_fast_kernel's ticket and finished
+// workgroups, [kMiscFVoid] one of its workgroups gave up waiting, [kMiscSlow] (zeroed by
+// uio_zero_kernel, set by the prep kernel) some op of the batch is not one the fast branch takes.
+enum {
+  kMiscTicket = 0, kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscT0 = 4, kMiscT1 = 6, kMiscPBVoid = 8,
+  kMiscPBDone = 9, kMiscFast = 10, kMiscErr = 11, kMiscN = 12,
+  kMiscFTicket = 12, kMiscFDone = 13, kMiscFVoid = 14, kMiscSlow = 15, kMiscWords = 16
+};
+enum : uint32_t { kFastDone = 1, kFastAbort = 2, kFastVoid = 3 };
 
 // ---------------------------------------------------------------- scan elements
 
@@ -250,9 +260,41 @@ __device__ __forceinline__ void pub_flag(uint32_t *f, uint32_t v) {
 // total to tbase[k]; the last tile to finish turns tbase[] into the tiles' exclusive bases (item
 // i's offset is pbase[i] + tbase[i / kPrepTile]; op_piece_crc_kernel adds them).  `sstate`
 // (zeroed by the caller): [0] unused, [1] finished tiles, [2] the total, [3 + k] tbase[k].
-__global__ void uio_zero_kernel(uint32_t *__restrict__ p, uint32_t n) {
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0;
+// Zeroes up to four word ranges, grid-strided (the prep kernel's scan words; on the fast branch also
+// its bucket heads, uio_fast_kernel's look-back granules and misc[kMiscSlow]).
+__global__ void uio_zero_kernel(uint32_t *__restrict__ a, uint32_t na, uint32_t *__restrict__ b, uint32_t nb,
+                                uint32_t *__restrict__ c, uint32_t nc, uint32_t *__restrict__ d, uint32_t nd) {
+  const uint32_t s = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < na + nb + nc + nd; i += s) {
+    if (i < na) a[i] = 0;
+    else if (i < na + nb) b[i - na] = 0;
+    else if (i < na + nb + nc) c[i - na - nb] = 0;
+    else d[i - na - nb - nc] = 0;
+  }
 }
+// ---- the fast branch's per-op tables (see uio_fast_kernel) ----
+// A batch whose every op is a typed, one-block, in-size WRITE (the block-aligned overwrites of
+// BASELINE config 3, or any write inside one 4 KiB block of a chunk stored under the batch's
+// polynomial that keeps its size) needs none of the general pipeline's sizes, cases or fragment
+// numbering: op i is its own one fragment, in sequence order.  The prep kernel builds op i's
+// fragment record and links the ops of one block inside its 1,024-op tile; each tile's last op of
+// a block is pushed on a hash bucket list.  uio_fast_kernel does the rest in one launch.
+struct FastArgs {
+  FragDesc *frag;           // op i's fragment (its 4 KiB block)
+  unsigned long long *key;  // (chunk << 36) | block address >> 12
+  // per op {tprev, tnext, tfirst, bnext}: the previous / next op of the same block in op i's prep tile
+  // (kNil: none); for a tile's last op of a block, the tile's first op of it and the next entry of its
+  // bucket list (the tiles' last ops, entries index + 1; 0 ends a list)
+  uint4 *link;
+  uint32_t *head;           // bucket heads, hmask + 1 of them (zeroed by uio_zero_kernel)
+  uint32_t hmask;
+  unsigned long long *dv;   // per op: {state << 32 | delta CRC} (state 1: applied, 2: failed A6)
+  uint32_t *slow;           // set when some op is not one this branch takes (misc[kMiscSlow])
+  const PolyConsts *pc;
+  uint2 *chain;             // per op (uio_fast_link_kernel): {starts its block's chain, the block's next op}
+};
+__device__ void fast_prep_tile(const FastArgs &fa, uint32_t i, uint32_t n, const h3c_update_io &io,
+                               const h3c_chunk_state &cs, uint32_t st, uint8_t poly_type, uint32_t std_domain);
 #ifndef H3C_PREP_TILE
 #define H3C_PREP_TILE 1024  // items per prep-kernel tile (a power of two, 64..1024)
 #endif
@@ -264,7 +306,7 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
     uint32_t *__restrict__ eacc, unsigned long long *__restrict__ ctr, uint32_t *__restrict__ misc,
     uint32_t *__restrict__ a6, uint32_t *__restrict__ fz, uint32_t fz_words, uint32_t *__restrict__ hhead,
     uint32_t hcap, uint32_t *__restrict__ gnext, uint32_t *__restrict__ fnext, uint32_t fcap,
-    uint32_t *__restrict__ pbase, uint32_t *sstate) {
+    uint32_t *__restrict__ pbase, uint32_t *sstate, FastArgs fa) {
   __shared__ uint32_t s_w[kPrepTile / 64], s_last;
   // No tile waits on another (the last one to finish scans the tile totals), so tiles need no
   // ticket: one agent-scope atomic per tile on one address serialises beyond the XCDs' L2s.
@@ -280,7 +322,7 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
     }
   }
   if (i < kCtrN) ctr[i] = 0;
-  if (i < kMiscN) misc[i] = i == kMiscT0 || i == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;
+  if (i < kMiscSlow) misc[i] = i == kMiscT0 || i == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;  // (kMiscSlow: uio_zero_kernel)
   // chunk items n + c for c < C = max(nchunks, 1) (the piece pass's NP = n + C items), then the
   // scan's extra entry: pbase[n + C] = total
   const uint32_t C = nchunks ? nchunks : 1u;
@@ -295,6 +337,9 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
     paycrc0[i] = 0;
   }
   if (i == n + C) npieces[i] = 0;
+  h3c_update_io f_io{};
+  h3c_chunk_state f_cs{};
+  uint32_t f_st = H3C_ERR_INVALID_ARG;
   if (i < n) {
     paycrc0[i] = 0;  // XOR accumulators of the piece and block kernels
     eacc[2 * i] = 0;
@@ -340,7 +385,11 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
     np = (st == H3C_OK && io.kind == H3C_UPD_WRITE && io.length && !cand) ? (io.length + kPieceBytes - 1) / kPieceBytes
                                                                           : 0;
     npieces[i] = np;
+    f_io = io;
+    f_st = st;
+    if (c < nchunks) f_cs = chunks[c];
   }
+  if (fa.head) fast_prep_tile(fa, i, n, f_io, f_cs, f_st, poly_type, std_domain);  // (the whole workgroup)
   if (!pbase) return;
   // exclusive scan of the items' piece counts: in the tile, then the tile's base by look-back
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -830,6 +879,86 @@ __global__ void uio_heads_kernel(const uint32_t *__restrict__ prev, const uint32
   else frags[k].flags |= kFragHead;
 }
 
+// ---- the fast branch: prep-kernel part ----
+__device__ __forceinline__ uint32_t fast_bucket(unsigned long long key, uint32_t mask) { return (key_hash(key) >> 7) & mask; }
+
+// An op the fast branch takes: a typed WRITE (A6 checked on its payload in uio_fast_kernel) whose
+// bytes lie in one 4 KiB block (absolute addresses) inside the chunk's current size, not a full
+// rewrite and not syncing, into a chunk stored under the batch polynomial.  It keeps the chunk's
+// size and stored type, and its stored checksum follows updateChecksum's case (iv) (raw domain,
+// ChunkReplica.cc:356-390) or copy_on_write (std domain, chunk.rs:89-158): s' = t'.
+__device__ __forceinline__ bool fast_op(const h3c_update_io &io, const h3c_chunk_state &cs, uint32_t st,
+                                        uint8_t poly_type) {
+  if (st != H3C_OK || io.kind != H3C_UPD_WRITE || io.checksum_type != poly_type || !io.length ||
+      (io.flags & H3C_IO_SYNCING) || cs.type != poly_type || cs.size > cs.chunk_size)
+    return false;
+  if ((uint64_t)io.offset + io.length > cs.size || (io.offset == 0 && io.length >= cs.size)) return false;
+  const uint64_t a = cs.base + io.offset;
+  return (a >> 12) == ((a + io.length - 1) >> 12);
+}
+
+// Op i's fragment record and key, and the links of the tile's ops by block (called by every
+// thread of a prep workgroup; i >= n: no op).
+__device__ void fast_prep_tile(const FastArgs &fa, uint32_t i, uint32_t n, const h3c_update_io &io,
+                               const h3c_chunk_state &cs, uint32_t st, uint8_t poly_type, uint32_t std_domain) {
+  __shared__ unsigned long long f_key[2 * kPrepTile];
+  __shared__ uint32_t f_head[2 * kPrepTile], f_nx[kPrepTile];
+  const uint32_t t = threadIdx.x, base = blockIdx.x * kPrepTile;
+  unsigned long long key = kNoKey;
+  bool q = false;
+  if (i < n) {
+    q = fast_op(io, cs, st, poly_type);
+    if (q) {
+      OpPos r{};
+      r.op = i;
+      r.status = H3C_OK;
+      r.nb = r.na = cs.size;
+      r.r0 = io.offset;
+      r.r1 = io.offset + io.length;
+      r.tk = kT_DELTA;
+      r.sk = kS_SET_T;
+      r.tb = r.ta = poly_type;
+      r.pf = kPosFold;
+      uint64_t k64;
+      uint32_t praw;
+      fa.frag[i] = make_frag(r, i, 0, io.chunk, cs, io, fa.pc, std_domain, false, k64, praw);
+      fa.key[i] = k64;
+      key = k64;
+    }
+    fa.dv[i] = 0;
+  }
+  if (__syncthreads_or(i < n && !q) && t == 0) atomicOr(fa.slow, 1u);
+  for (uint32_t e = t; e < 2 * kPrepTile; e += kPrepTile) {
+    f_key[e] = kNoKey;
+    f_head[e] = kNil;
+  }
+  __syncthreads();
+  uint32_t h = kNil;
+  if (key != kNoKey) {
+    h = key_hash(key) & (2 * kPrepTile - 1);
+    for (;;) {
+      const unsigned long long old = atomicCAS(&f_key[h], kNoKey, key);
+      if (old == kNoKey || old == key) break;
+      h = (h + 1) & (2 * kPrepTile - 1);
+    }
+    f_nx[t] = atomicExch(&f_head[h], t);
+  }
+  __syncthreads();
+  if (h == kNil) return;
+  uint32_t pin = kNil, nin = kNil, fst = t;  // the tile's previous / next / first op of this block
+  for (uint32_t u = f_head[h]; u != kNil; u = f_nx[u]) {
+    if (u < t && (pin == kNil || u > pin)) pin = u;
+    if (u > t && (nin == kNil || u < nin)) nin = u;
+    fst = min(fst, u);
+  }
+  uint4 lk = make_uint4(pin == kNil ? kNil : base + pin, nin == kNil ? kNil : base + nin, kNil, 0u);
+  if (nin == kNil) {  // the tile's last op of the block: listed for the later tiles' ops (uio_fast_kernel)
+    lk.z = base + fst;
+    lk.w = atomicExch(&fa.head[fast_bucket(key, fa.hmask)], i + 1);
+  }
+  fa.link[i] = lk;
+}
+
 // ---- one-pass front: sizes, cases, fragment numbering, fragments and chain links ----
 // uio_front_kernel does in one launch what the scan-based stage does in ~10 (size-map scan,
 // classify, fragment-count scan, fragments, tile links, link resolution, chain heads).  A
@@ -876,8 +1005,10 @@ __device__ __forceinline__ SzTy sz_from_bits(uint64_t b) {
   __builtin_memcpy(&a, &b, 8);
   return a;
 }
-// spin until *f != 0; 0 after kFrontSpin polls (the caller voids the pass)
-__device__ __forceinline__ uint32_t wait_flag(uint32_t *f) {
+// spin until *f != 0; 0 after kFrontSpin polls (the caller voids the pass).  force (test hook
+// H3C_HOOK_UPD_GIVEUP): give up at once, as a wait starved of its predecessor's CU would.
+__device__ __forceinline__ uint32_t wait_flag(uint32_t *f, bool force = false) {
+  if (force) return 0;
   uint32_t v;
   for (uint32_t spins = 0; (v = ld_agent(f)) == 0;) {
     __builtin_amdgcn_s_sleep(1);
@@ -959,7 +1090,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
     uint32_t *__restrict__ payraw, uint32_t *__restrict__ a6, uint32_t *misc, FragDesc *frags, uint64_t *fkey,
     uint32_t cap, uint32_t *hhead, uint32_t hmask, uint32_t *gnext, uint32_t *prev, uint32_t *fnext, FrontSlot *slots,
     const uint32_t *__restrict__ paycrc0, uint32_t exact, uint32_t *__restrict__ t0v,
-    h3c_chunk_state *__restrict__ chunks_out, const uint32_t *sstate) {
+    h3c_chunk_state *__restrict__ chunks_out, const uint32_t *sstate, uint32_t force_giveup) {
   constexpr uint32_t T = kFrontTile, NW = T / 64;
   __shared__ uint32_t s_key[T], s_v[T], s_w[T];         // keys; the inclusive maps (v, packed)
   __shared__ uint32_t s_fex[T + 1];                     // exclusive fragment counts of the tile
@@ -1049,7 +1180,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
       uint32_t fl = 3, key = 0xFFFFFFFFu, whole = 0, v = 0, w = 0;
       if (j >= 0) {
         FrontSlot &sl = slots[j];
-        fl = wait_flag(&sl.sz_flag);
+        fl = wait_flag(&sl.sz_flag, force_giveup && k == 1);
         key = ld_agent(&sl.key);
         whole = ld_agent(&sl.whole);
         const SzTy a = sz_from_bits(ld_agent(reinterpret_cast<uint64_t *>(fl == 2 ? &sl.sz_incl : &sl.sz_agg)));
@@ -1451,15 +1582,32 @@ struct FoldIo {
   uint32_t *payraw, *a6;
 };
 
+// Where apply_fragment's results go (lane 0 calls them): the general pipeline's E accumulators
+// and A6 verdicts (GenSink), or the fast branch's per-op granules (FastSink, uio_fast_kernel).
+struct GenSink {
+  uint32_t *eacc, *a6;
+  uint32_t poly;
+  __device__ void fail(uint32_t op) const { a6[op] = 1u; }
+  __device__ void crc(uint32_t p, uint32_t v, uint32_t mult, uint32_t flags) const {
+    if (H3C_UIO_SOLO && (flags & kFragSolo)) {
+      *reinterpret_cast<uint2 *>(eacc + 2 * p) = make_uint2(v, mult);
+    } else {
+      const uint32_t cv = dgf_mul_fast(v, mult, poly);
+      if (cv) atomicXor(&eacc[2 * p], cv);
+    }
+  }
+};
+
 // One fragment on the block rows: its delta CRC (new ^ old) moved to its op's end goes to
 // eacc[p]; then its zero fill and new bytes are applied.  Returns the rows it wrote.
 // kFragA6 (a fold op): the payload's own CRC is folded beside the old bytes' (crc0 is linear:
 // crc0(new ^ old) = crc0(new) ^ crc0(old)), its raw value checked against the client's checksum
 // (ChunkReplica.cc:193-207, engine.rs:297-308); a failed op contributes nothing and writes nothing.
+template <class Sink>
 __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 (&nw)[4], uint32_t flags, uint32_t w,
                                                    uint32_t q, uint32_t z, uint32_t mult, uint32_t p, uint32_t lane,
-                                                   const char *lb, const LaneLut &L, const uint32_t *red, uint32_t poly,
-                                                   uint32_t *__restrict__ eacc, const FoldIo &fx) {
+                                                   const char *lb, const LaneLut &L, const uint32_t *red,
+                                                   const FoldIo &fx, const Sink &sink) {
   const uint32_t w0 = w & 0xFFFFu, w1 = w >> 16, q0 = q & 0xFFFFu, q1 = q >> 16, z0 = z & 0xFFFFu, z1 = z >> 16;
 #if H3C_UIO_FOLD_ILP
   if ((flags & (kFragA6 | kFragCrc)) == (kFragA6 | kFragCrc)) {
@@ -1476,17 +1624,10 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
     uint32_t fv[2];
     wave_fold_tab_n<2>(s2, lane, red, fv);
     if (__builtin_amdgcn_readfirstlane(fv[0]) != fx.expect) {
-      if (lane == 0) fx.a6[fx.op] = 1u;
+      if (lane == 0) sink.fail(fx.op);
       return 0u;
     }
-    if (lane == 0) {
-      if (H3C_UIO_SOLO && (flags & kFragSolo)) {
-        *reinterpret_cast<uint2 *>(eacc + 2 * p) = make_uint2(fv[1], mult);
-      } else {
-        const uint32_t cv = dgf_mul_fast(fv[1], mult, poly);
-        if (cv) atomicXor(&eacc[2 * p], cv);
-      }
-    }
+    if (lane == 0) sink.crc(p, fv[1], mult, flags);
     flags &= ~(kFragA6 | kFragCrc);
   }
 #endif
@@ -1497,7 +1638,7 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
     // the payload's init-0 CRC in its block image against the client's, precomputed (make_frag)
     const bool bad = __builtin_amdgcn_readfirstlane(wave_fold_tab(sn, lane, red)) != fx.expect;
     if (bad) {
-      if (lane == 0) fx.a6[fx.op] = 1u;
+      if (lane == 0) sink.fail(fx.op);
       return 0u;
     }
   }
@@ -1510,14 +1651,7 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
       consume(st, xor4(nw[r], old), lb, L);
     }
     const uint32_t v = wave_fold_tab(st, lane, red);
-    if (lane == 0) {
-      if (H3C_UIO_SOLO && (flags & kFragSolo)) {
-        *reinterpret_cast<uint2 *>(eacc + 2 * p) = make_uint2(v, mult);
-      } else {
-        const uint32_t cv = dgf_mul_fast(v, mult, poly);
-        if (cv) atomicXor(&eacc[2 * p], cv);
-      }
-    }
+    if (lane == 0) sink.crc(p, v, mult, flags);
   }
   uint32_t dirty = 0;
   if (flags & kFragWrite) {
@@ -1576,6 +1710,7 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
   if (!kEarlyRows && lo >= hi) return;
 #endif
   const uint32_t poly = pc->poly;
+  const GenSink sink{eacc, a6, poly};
   const LaneLut L = make_lut(lane);
 #if H3C_UIO_SFIELDS
   // Every field comes from uniform (scalar) loads: the wave walks its fragments in order, the
@@ -1603,8 +1738,7 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
         fx.expect = f3.y;
         fx.len = f3.z;
       }
-      uint32_t dirty = apply_fragment(cb.img, cb.nw, flags, f1.z, f1.w, f2.x, f2.z, f1.x, lane, lb, L, red, poly, eacc,
-                                      fx);
+      uint32_t dirty = apply_fragment(cb.img, cb.nw, flags, f1.z, f1.w, f2.x, f2.z, f1.x, lane, lb, L, red, fx, sink);
       for (uint32_t f = fnext[g]; f != kNil;) {  // later fragments of the same block
         const FragDesc d = frags[f];
         uint4 nw4[4];
@@ -1613,7 +1747,7 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
         const FoldIo fd{d.op, d.expect, d.len, std_domain, pc, payraw, a6};
         dirty |= apply_fragment(cb.img, nw4, d.flags, (uint32_t)d.w0 | ((uint32_t)d.w1 << 16),
                                 (uint32_t)d.q0 | ((uint32_t)d.q1 << 16), (uint32_t)d.z0 | ((uint32_t)d.z1 << 16),
-                                d.mult, d.p, lane, lb, L, red, poly, eacc, fd);
+                                d.mult, d.p, lane, lb, L, red, fd, sink);
         f = fnext[f];
       }
 #pragma unroll
@@ -1747,7 +1881,7 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
           fx.len = dh->len;
         }
         uint32_t dirty = apply_fragment(cur.img, cur.nw, flags, rl(m_w, t), rl(m_q, t), rl(m_z, t), rl(m_mult, t),
-                                        rl(m_p, t), lane, lb, L, red, poly, eacc, fx);
+                                        rl(m_p, t), lane, lb, L, red, fx, sink);
         for (uint32_t f = rl(m_next, t); f != kNil;) {  // later fragments of the same block
           const FragDesc d = frags[f];
           uint4 nw4[4];
@@ -1756,7 +1890,7 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
           const FoldIo fd{d.op, d.expect, d.len, std_domain, pc, payraw, a6};
           dirty |= apply_fragment(cur.img, nw4, d.flags, (uint32_t)d.w0 | ((uint32_t)d.w1 << 16),
                                   (uint32_t)d.q0 | ((uint32_t)d.q1 << 16), (uint32_t)d.z0 | ((uint32_t)d.z1 << 16),
-                                  d.mult, d.p, lane, lb, L, red, poly, eacc, fd);
+                                  d.mult, d.p, lane, lb, L, red, fd, sink);
           f = fnext[f];
         }
 #pragma unroll
@@ -2009,7 +2143,7 @@ __device__ __forceinline__ Aff aff_tile_scan(Aff x, uint32_t head, uint32_t poly
 
 // The carry into the tile's first run (key c0) of scan `which`, from earlier tiles (wave 0).
 __device__ Aff aff_carry(PhaseBSlot *slots, uint32_t k, uint32_t c0, int which, uint32_t poly, uint32_t lane,
-                         uint32_t *gave_up) {
+                         uint32_t *gave_up, bool force = false) {
   const AffOp op{poly};
   Aff carry{kOne, 0u};
   bool done = k == 0;
@@ -2019,7 +2153,7 @@ __device__ Aff aff_carry(PhaseBSlot *slots, uint32_t k, uint32_t c0, int which, 
     unsigned long long a = 0;
     if (j >= 0) {
       PhaseBSlot &sl = slots[j];
-      fl = wait_flag(&sl.flag[which]);
+      fl = wait_flag(&sl.flag[which], force);
       key = ld_agent(&sl.key);
       whole = ld_agent(&sl.whole);
       a = ld_agent(fl == 2 ? &sl.incl[which] : &sl.agg[which]);
@@ -2075,7 +2209,7 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
     const uint32_t *__restrict__ t0v, const h3c_chunk_state *__restrict__ chunks,
     h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks, uint8_t poly_type, uint32_t std_domain,
     h3c_update_result *__restrict__ res, unsigned long long *__restrict__ ctr, const uint32_t *__restrict__ d_F,
-    uint32_t *misc, PhaseBSlot *slots, uint32_t *ticket, uint32_t *hout) {
+    uint32_t *misc, PhaseBSlot *slots, uint32_t *ticket, uint32_t *hout, uint32_t force_giveup) {
   constexpr uint32_t T = kPhaseBTile;
   __shared__ uint32_t s_key[T + 1], sw[48], s_c[2], s_tile, s_void;
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -2117,7 +2251,7 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
     pub_flag(&me.flag[0], 1u);
   }
   if (wave == 0) {
-    const Aff cy = aff_carry(slots, k, c0, 0, poly, lane, &s_void);
+    const Aff cy = aff_carry(slots, k, c0, 0, poly, lane, &s_void, force_giveup && k == 1);
     if (lane == 0) {
       s_c[0] = cy.m;
       s_c[1] = cy.e;
@@ -2186,6 +2320,504 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
   }
 }
 
+// ---- the fast branch: the blocks and A6 checks in one launch, the checksums and results in another ----
+// A fast-branch batch (fast_op: every op one block, no size or type change, case (iv) / copy_on_write)
+// runs, after the prep kernel and uio_fast_link_kernel, in place of the sort, the piece pass, the front
+// kernel, the block kernel and phase B:
+//   uio_fast_kernel: a wave takes a contiguous range of ops in sequence order and runs the chains its
+//     ops start (an op starts its block's chain when no earlier op of the batch writes the block): the
+//     block loaded once, each op's A6 check on its payload rows, its delta CRC (new ^ old), its bytes
+//     applied, the block stored once; a chain's later ops come from chain[].  Each op's delta (or its
+//     failed check) goes to dv[op].  Nothing waits: the kernel ends when its slowest wave does.
+//   uio_fast_tail_kernel: per 1,024-op tile, each op's delta moved to its chunk's end (x^(8e), one op
+//     per lane), the per-chunk XORs in sequence order (lane c holds chunks c and c + 64: <= 128 chunks,
+//     checked by the host), the tile's per-chunk sums published and the earlier tiles' read by all 16
+//     waves at once; every op's result is t0 ^ the XOR of its chunk's deltas up to it; the last tile
+//     writes the chunks' final states, the last to finish the outcome words (to the host buffer).
+// (One kernel with the sums chained across workgroups by look-back measured 320-330 us against this
+// pair's ~270 us: its waves that finished early waited on chains run late by other waves, polling.)
+// The tail's waits are bounded: a tile that gives up sets misc[kMiscFVoid] and the host recomputes the
+// results with uio_fast_recover_kernel (dv[] is complete once uio_fast_kernel has ended).
+// the bucket walks over the tiles' last ops (uio_fast_kernel; restrict pointers, so that uniform
+// walks compile to scalar loads)
+__device__ __forceinline__ bool fast_listed_before(const uint4 *__restrict__ link, const unsigned long long *__restrict__ keys,
+                                                   const uint32_t *__restrict__ bhead, uint32_t hmask,
+                                                   unsigned long long key, uint32_t j) {
+  for (uint32_t e = bhead[fast_bucket(key, hmask)]; e != 0; e = link[e - 1].w)
+    if (e - 1 < j && keys[e - 1] == key) return true;
+  return false;
+}
+// the next op of `key` after m, the last op of the block in m's tile: the first op of the block in the
+// next tile that has one (that tile's last op of the block is listed, with the tile's first beside it)
+__device__ __forceinline__ uint32_t fast_cross_next(const uint4 *__restrict__ link,
+                                                    const unsigned long long *__restrict__ keys,
+                                                    const uint32_t *__restrict__ bhead, uint32_t hmask,
+                                                    unsigned long long key, uint32_t m) {
+  uint32_t best = kNil;
+  for (uint32_t e = bhead[fast_bucket(key, hmask)]; e != 0; e = link[e - 1].w) {
+    const uint32_t j = e - 1;
+    if (j > m && j < best && keys[j] == key) best = j;
+  }
+  return best == kNil ? kNil : link[best].z;
+}
+// Per op: whether it starts its block's chain (no earlier op of the block in its tile, none listed by an
+// earlier tile) and the block's next op (in its tile, else the first in the next tile that has one).
+// One thread per op, between the prep kernel and uio_fast_kernel: the bucket walks' dependent loads run
+// here, all at once, instead of in front of uio_fast_kernel's first row loads and between a chain's ops.
+__global__ void uio_fast_link_kernel(const uint4 *__restrict__ link, const unsigned long long *__restrict__ keys,
+                                     const uint32_t *__restrict__ bhead, uint32_t hmask, uint32_t n,
+                                     const uint32_t *__restrict__ misc, uint2 *__restrict__ chain) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n || misc[kMiscSlow]) return;  // (an abandoned batch: uio_fast_kernel returns at once)
+  const uint4 lk = link[j];
+  const unsigned long long key = keys[j];
+  const bool start = lk.x == kNil && !fast_listed_before(link, keys, bhead, hmask, key, j);
+  const uint32_t next = lk.y != kNil ? lk.y : fast_cross_next(link, keys, bhead, hmask, key, j);
+  chain[j] = make_uint2(start ? 1u : 0u, next);
+}
+
+struct FastSink {  // apply_fragment's results on the fast branch: dv[op] = {1, unshifted delta} or {2, 0}
+  unsigned long long *dv;
+  __device__ void fail(uint32_t op) const { st_agent(&dv[op], 2ull << 32); }
+  __device__ void crc(uint32_t p, uint32_t v, uint32_t, uint32_t) const { st_agent(&dv[p], (1ull << 32) | v); }
+};
+#ifndef H3C_FX
+#define H3C_FX 0
+#endif
+#ifndef H3C_FAST_TRACE
+#define H3C_FAST_TRACE 0  // 1: workgroups 0, 1, the middle one and the last print their step times (diagnostics)
+#endif
+#if H3C_FAST_TRACE >= 2
+// histograms of the waves' step end times (5 us bins from the earliest workgroup start): [0..63] chains
+// done, [64..127] deltas done; [128] 0x7FFFFFFF - the earliest start (low 31 bits), [129] waves counted
+__device__ unsigned int g_ftr[130] = {};
+#endif
+#if H3C_FAST_TRACE
+#define FAST_MARK(i) (ftr[i] = wall_clock64())
+#else
+#define FAST_MARK(i) ((void)0)
+#endif
+constexpr uint32_t kFastCols = 128;  // chunks a fast-branch batch may name (lane c: chunks c, c + 64)
+constexpr uint32_t kFastSpin = 1u << 21;
+constexpr unsigned long long kGranApplied = 4ull << 32;  // look-back granule bit: some op of the chunk applied
+
+
+// t0 of chunk c: the trusted stored value, or (H3C_UPD_EXACT) the CRC of its bytes (prep / piece pass)
+__device__ __forceinline__ uint32_t fast_t0(const h3c_chunk_state &cs, uint32_t c, uint32_t exact, uint32_t std_domain,
+                                            const uint32_t *__restrict__ crc0, const PolyConsts *__restrict__ pc) {
+  if (exact && cs.size && cs.size <= cs.chunk_size)
+    return crc0[c] ^ dgf_mul_fast(0xFFFFFFFFu, dxpow8_fast(cs.size, pc, pc->poly), pc->poly);
+  return std_domain ? ~cs.value : cs.value;
+}
+
+__global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint32_t std_domain,
+                                                             const PolyConsts *__restrict__ pc,
+                                                             const FragDesc *__restrict__ frag,
+                                                             const uint2 *__restrict__ chain, unsigned long long *dv,
+                                                             const uint32_t *__restrict__ misc, unsigned long long *ts) {
+  __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
+  const uint32_t t = threadIdx.x, lane = t & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (misc[kMiscSlow]) return;  // not a fast-branch batch: the host runs the general pipeline
+  if (ts && t == 0) atomicMin(&ts[0], (unsigned long long)wall_clock64());
+#if H3C_FAST_TRACE
+  uint64_t ftr[8];
+  FAST_MARK(0);
+#endif
+  const uint64_t gw = (uint64_t)blockIdx.x * kBlkWaves + wave, nw = (uint64_t)gridDim.x * kBlkWaves;
+  const uint32_t lo = (uint32_t)(gw * n / nw), hi = (uint32_t)((gw + 1) * n / nw);
+  const uint32_t *red = lds + kLdsWords;
+  const char *lb = reinterpret_cast<const char *>(lds);
+  const LaneLut Lt = make_lut(lane);
+  const FastSink sink{dv};
+  const uint4 *__restrict__ rec = reinterpret_cast<const uint4 *>(frag);  // 4 x 16 bytes per record
+  // the chain starts of the group at g0 (lanes: one op each) and, among them, those whose block has
+  // later ops in the batch (their chains run without the next start's rows in flight: the registers
+  // hold the block, one payload and the next start's rows only when the chain is one op)
+  auto starts = [&](uint32_t g0, uint64_t &cm) -> uint64_t {
+    const uint32_t j = g0 + lane;
+    bool hd = false, cn = false;
+    if (j < hi) {
+      const uint2 ch = chain[j];
+      hd = ch.x != 0;
+      cn = hd && ch.y != kNil;
+    }
+    cm = __builtin_amdgcn_ballot_w64(cn);
+    return __builtin_amdgcn_ballot_w64(hd);
+  };
+  // the next chain start at or after group g0 (g0 and the masks advance): kNil when none is left
+  auto next_start = [&](uint32_t &g0, uint64_t &hm, uint64_t &cm, bool &cont) -> uint32_t {
+    while (!hm) {
+      g0 += 64;
+      if (g0 >= hi) return kNil;
+      hm = starts(g0, cm);
+    }
+    const uint32_t b = (uint32_t)__builtin_ctzll(hm);
+    cont = (cm >> b) & 1u;
+    hm &= hm - 1;
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(g0 + b));
+  };
+  // 1 + 2: the wave's chains in order.  A one-op chain runs with the next start's rows in flight (and
+  // the addresses of the one after it loaded); a longer one walks its block's later ops (their payload
+  // rows into cur.nw) with nothing else in flight.  The first chain's rows load before the workgroup
+  // fills its LDS tables.  One apply site for every op keeps the registers within 128.
+  struct Addr {
+    uint64_t blk, src;
+    uint32_t w, k;
+  };
+  auto addr_of = [&](uint32_t g, Addr &d) {  // (scalar record loads)
+    const uint4 x = rec[4 * (size_t)g], y = rec[4 * (size_t)g + 1], z = rec[4 * (size_t)g + 2];
+    d.blk = (uint64_t)x.x | ((uint64_t)x.y << 32);
+    d.src = (uint64_t)x.z | ((uint64_t)x.w << 32);
+    d.w = y.z;
+    d.k = z.y;
+  };
+  auto rows_at = [&](const Addr &d, BlockRows &b) {
+    load_task_rows(d.blk, d.k & 0xFFFFu, d.k >> 16, d.src, d.w & 0xFFFFu, d.w >> 16, lane, b);
+  };
+  BlockRows cur, nxt;
+  uint32_t g0 = lo, op = kNil, nh = kNil, nh2 = kNil;
+  uint64_t hm = 0, cm = 0;
+  bool cont = false, ncont = false, ncont2 = false;
+  Addr an{}, an2{};
+  if (lo < hi) {
+    hm = starts(lo, cm);
+    op = next_start(g0, hm, cm, cont);
+    if (op != kNil) {
+      Addr a0;
+      addr_of(op, a0);
+      rows_at(a0, cur);
+      nh = next_start(g0, hm, cm, ncont);
+      if (nh != kNil) {
+        addr_of(nh, an);
+        nh2 = next_start(g0, hm, cm, ncont2);
+        if (nh2 != kNil) addr_of(nh2, an2);
+      }
+    }
+  }
+  FAST_MARK(1);
+  fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
+  __syncthreads();
+  FAST_MARK(2);
+  uint32_t head_op = op, dirty = 0;
+  while (op != kNil) {
+    if (op == head_op && !cont && nh != kNil) rows_at(an, nxt);  // a one-op chain: the next start's rows
+    {
+      const uint4 f1 = rec[4 * (size_t)op + 1], f2 = rec[4 * (size_t)op + 2], f3 = rec[4 * (size_t)op + 3];
+      const FoldIo fx{f3.x, f3.y, f3.z, std_domain, pc, nullptr, nullptr};
+      dirty |= apply_fragment(cur.img, cur.nw, f2.w, f1.z, f1.w, f2.x, f2.z, f1.x, lane, lb, Lt, red, fx, sink);
+    }
+    if (cont) {  // the block's next op
+      const uint32_t nx = (uint32_t)__builtin_amdgcn_readfirstlane((int)chain[op].y);
+      if (nx != kNil) {
+        const uint4 b0 = rec[4 * (size_t)nx], b1 = rec[4 * (size_t)nx + 1];
+        const uint64_t src = (uint64_t)b0.z | ((uint64_t)b0.w << 32);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cur.nw[r] = load_new(src, r, 1024u * r + 16u * lane, b1.z & 0xFFFFu, b1.z >> 16);
+        op = nx;
+        continue;
+      }
+    }
+    {  // the chain is done: its block's changed rows, once
+      const uint4 a = rec[4 * (size_t)head_op], c2 = rec[4 * (size_t)head_op + 2];
+      const uint64_t blk = (uint64_t)a.x | ((uint64_t)a.y << 32);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (dirty & (1u << r)) store_masked(blk, 1024u * r + 16u * lane, cur.img[r], c2.y & 0xFFFFu, c2.y >> 16);
+    }
+    dirty = 0;
+    if (nh == kNil) break;
+    if (!cont) cur = nxt;
+    else rows_at(an, cur);  // (nothing was in flight)
+    op = head_op = nh;
+    cont = ncont;
+    nh = nh2;
+    an = an2;
+    ncont = ncont2;
+    nh2 = kNil;
+    if (nh != kNil) {  // the addresses two chains ahead
+      nh2 = next_start(g0, hm, cm, ncont2);
+      if (nh2 != kNil) addr_of(nh2, an2);
+    }
+  }
+#if H3C_FAST_TRACE
+  FAST_MARK(3);
+  if (lane == 0 && ((blockIdx.x < 2 || blockIdx.x == gridDim.x / 2 || blockIdx.x + 1 == gridDim.x) && wave < 2))
+    printf("fast wg %u wave %u start %llu first-rows %llu fill %llu chains %llu (ticks)\n", blockIdx.x, wave,
+           (unsigned long long)ftr[0], (unsigned long long)(ftr[1] - ftr[0]), (unsigned long long)(ftr[2] - ftr[0]),
+           (unsigned long long)(ftr[3] - ftr[0]));
+#endif
+  if (ts) {  // one stamp per workgroup, once all its waves are done
+    __syncthreads();
+    if (t == 0) atomicMax(&ts[1], (unsigned long long)wall_clock64());
+  }
+}
+
+// The per-chunk XOR of the deltas in sequence order, every op's result, the chunks' final states, the
+// counters and the outcome words (see above); tile k = ops [1024 k, 1024 k + 1024).
+constexpr uint32_t kTailTile = 1024;
+__global__ __launch_bounds__(kTailTile) void uio_fast_tail_kernel(
+    const h3c_chunk_state *__restrict__ chunks, h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks, uint32_t n,
+    uint8_t poly_type, uint32_t std_domain, uint32_t exact, const uint32_t *__restrict__ crc0,
+    const PolyConsts *__restrict__ pc, const FragDesc *__restrict__ frag, const unsigned long long *__restrict__ keys,
+    const unsigned long long *__restrict__ dv, uint32_t *misc, unsigned long long *gran,
+    h3c_update_result *__restrict__ res, unsigned long long *__restrict__ ctr, uint32_t *hout, uint32_t force_giveup) {
+  constexpr uint32_t NW = kTailTile / 64, kWC = NW * kFastCols;
+  __shared__ uint32_t wagg[kWC], wapp[kWC], wlb[kWC], wlba[kWC], wbase[kFastCols], wsz[kFastCols];
+  __shared__ uint32_t s_void, s_bad;
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, k = blockIdx.x, ntiles = gridDim.x;
+  if (misc[kMiscSlow]) {  // not a fast-branch batch: nothing was done; the outcome says so
+    if (k == 0 && t == 0) {
+      misc[kMiscFast] = kFastAbort;
+      if (hout)
+        for (uint32_t w = kMiscOutF; w < kMiscN; ++w) hout[w - kMiscOutF] = misc[w];
+    }
+    return;
+  }
+  // test hook (H3C_HOOK_UPD_GIVEUP bit 2): tile 1 gives up its wait at once, as a starved one would
+  if (t == 0) {
+    s_void = force_giveup && k == 1 ? 1u : 0u;
+    s_bad = 0;
+  }
+  const uint32_t poly = pc->poly;
+  const uint32_t j = k * kTailTile + t;
+  // each op's delta moved to its chunk's end
+  uint32_t c = kNil, v = 0, st = 0;
+  if (j < n) {
+    c = (uint32_t)(keys[j] >> 36);
+    const unsigned long long g = dv[j];
+    st = (uint32_t)(g >> 32);
+    if (st == 1) v = dgf_mul_fast((uint32_t)g, frag[j].mult, poly);
+  }
+  // in the wave: each op's inclusive XOR of its chunk's deltas, the wave's per-chunk sums (lanes c, c + 64)
+  uint32_t acc0 = 0, acc1 = 0, ip = 0, app0 = 0, app1 = 0;
+  for (uint32_t u = 0; u < 64; ++u) {
+    const uint32_t cu = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)u);
+    const uint32_t vu = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)u);
+    const uint32_t oku = __builtin_amdgcn_readlane((int)st, (int)u) == 1 ? 1u : 0u;
+    if (lane >= u && c == cu) ip ^= vu;
+    if (cu == lane) {
+      acc0 ^= vu;
+      app0 |= oku;
+    }
+    if (cu == lane + 64) {
+      acc1 ^= vu;
+      app1 |= oku;
+    }
+  }
+  wagg[wave * kFastCols + lane] = acc0;
+  wagg[wave * kFastCols + 64 + lane] = acc1;
+  wapp[wave * kFastCols + lane] = app0;
+  wapp[wave * kFastCols + 64 + lane] = app1;
+  __syncthreads();
+  const bool two = nchunks > 64;
+  if (wave == 0) {  // the tile's sums, published
+    uint32_t a0 = 0, a1 = 0, p0 = 0, p1 = 0;
+    for (uint32_t w = 0; w < NW; ++w) {
+      a0 ^= wagg[w * kFastCols + lane];
+      a1 ^= wagg[w * kFastCols + 64 + lane];
+      p0 |= wapp[w * kFastCols + lane];
+      p1 |= wapp[w * kFastCols + 64 + lane];
+    }
+    unsigned long long *row = gran + (uint64_t)k * kFastCols;
+    if (lane < nchunks) st_agent(&row[lane], (1ull << 32) | (p0 ? kGranApplied : 0ull) | a0);
+    if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], (1ull << 32) | (p1 ? kGranApplied : 0ull) | a1);
+  }
+  // the earlier tiles' sums, read by all waves at once (wave w: tiles w, w + 16, ...)
+  {
+    const uint32_t spin = kFastSpin;
+    const bool c0 = lane < nchunks, c1 = two && lane + 64 < nchunks;
+    uint32_t x0 = 0, x1 = 0, q0 = 0, q1 = 0;
+    constexpr uint32_t kB = 4;  // tiles in flight per wave
+    for (uint32_t r0 = wave; r0 < k; r0 += kB * NW) {
+      unsigned long long g0v[kB], g1v[kB];
+#pragma unroll
+      for (uint32_t b = 0; b < kB; ++b) {
+        const uint32_t r = r0 + b * NW;
+        g0v[b] = r < k && c0 ? ld_agent(&gran[(uint64_t)r * kFastCols + lane]) : (1ull << 32);
+        g1v[b] = r < k && c1 ? ld_agent(&gran[(uint64_t)r * kFastCols + 64 + lane]) : (1ull << 32);
+      }
+#pragma unroll
+      for (uint32_t b = 0; b < kB; ++b) {
+        const uint32_t r = r0 + b * NW;
+        for (uint32_t spins = 0; (g0v[b] >> 32) == 0 || (g1v[b] >> 32) == 0;) {  // not yet published
+          if (spins++ >= spin) {  // an earlier tile never published: give up (the host recomputes the results)
+            s_void = 1;
+            g0v[b] = g1v[b] = 1ull << 32;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(4);
+          if ((g0v[b] >> 32) == 0) g0v[b] = ld_agent(&gran[(uint64_t)r * kFastCols + lane]);
+          if ((g1v[b] >> 32) == 0) g1v[b] = ld_agent(&gran[(uint64_t)r * kFastCols + 64 + lane]);
+        }
+        x0 ^= (uint32_t)g0v[b];
+        x1 ^= (uint32_t)g1v[b];
+        q0 |= (g0v[b] & kGranApplied) ? 1u : 0u;
+        q1 |= (g1v[b] & kGranApplied) ? 1u : 0u;
+      }
+    }
+    wlb[wave * kFastCols + lane] = x0;
+    wlb[wave * kFastCols + 64 + lane] = x1;
+    wlba[wave * kFastCols + lane] = q0;
+    wlba[wave * kFastCols + 64 + lane] = q1;
+  }
+  __syncthreads();
+  if (wave < 2) {  // per chunk (thread c < 128): t0 ^ the earlier tiles' deltas; the last tile's final states
+    const uint32_t cc = t;
+    uint32_t e = 0, q = 0;
+    for (uint32_t w = 0; w < NW; ++w) {
+      e ^= wlb[w * kFastCols + cc];
+      q |= wlba[w * kFastCols + cc];
+    }
+    h3c_chunk_state cs{};
+    uint32_t t0 = 0;
+    if (cc < nchunks) {
+      cs = chunks[cc];
+      t0 = fast_t0(cs, cc, exact, std_domain, crc0, pc);
+    }
+    wbase[cc] = t0 ^ e;
+    wsz[cc] = cs.size;
+    if (k + 1 == ntiles && cc < nchunks) {
+      uint32_t a = e, p = q;
+      for (uint32_t w = 0; w < NW; ++w) {
+        a ^= wagg[w * kFastCols + cc];
+        p |= wapp[w * kFastCols + cc];
+      }
+      h3c_chunk_state f = cs;
+      if (p) {  // (a chunk whose ops all failed A6 keeps its stored value)
+        f.value = std_domain ? ~(t0 ^ a) : (t0 ^ a);
+        f.type = poly_type;
+      }
+      chunks_out[cc] = f;
+      if (exact && cs.size && cs.type == poly_type && t0 != (std_domain ? ~cs.value : cs.value))
+        atomicAdd(&ctr[kCtrStale], 1ull);
+    }
+  }
+  __syncthreads();
+  // every op's result: t0 ^ its chunk's deltas up to it (earlier tiles, this tile's earlier waves, the wave)
+  if (j < n) {
+    uint32_t sv = wbase[c] ^ ip;
+    for (uint32_t w = 0; w < wave; ++w) sv ^= wagg[w * kFastCols + c];
+    h3c_update_result o{};
+    o.status = st == 1 ? H3C_OK : H3C_ERR_CHECKSUM_MISMATCH;
+    o.size = wsz[c];
+    o.type = poly_type;  // (a failed op reports the stored type: the batch polynomial here)
+    o.value = st == 1 ? (std_domain ? ~sv : sv) : (std_domain ? 0u : sv);  // engine.rs:303 / ChunkReplica.cc:174
+    res[j] = o;
+    if (st != 1 && st != 2) s_bad = 1;  // an op with no delta: cannot happen after a complete uio_fast_kernel
+  }
+  {
+    uint32_t v8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    v8[std_domain ? kCtrRecalc : kCtrRead] = j < n && st == 1;  // updateChecksum (iv) (:389) / copy_on_write (chunk.rs:153)
+    v8[kCtrMismatch] = j < n && st == 2;
+    __shared__ unsigned int sh[8];
+    ctr_add_block(sh, ctr, v8);
+  }
+  __syncthreads();
+  if (t == 0) {
+    if (s_void) atomicOr(&misc[kMiscFVoid], 1u);
+    if (s_bad) atomicOr(&misc[kMiscErr], 1u);
+    stores_done();
+    if (atomicAdd(&misc[kMiscFDone], 1u) + 1 == ntiles) {  // the last to finish: the outcome words
+      st_agent(&misc[kMiscFast], ld_agent(&misc[kMiscFVoid]) ? (uint32_t)kFastVoid : (uint32_t)kFastDone);
+      if (hout)
+#pragma unroll
+        for (uint32_t w = kMiscOutF; w < kMiscN; ++w) hout[w - kMiscOutF] = ld_agent(&misc[w]);
+    }
+  }
+}
+
+// After a void fast pass (a workgroup gave up waiting): the results, final states and counters again
+// from dv[], which the pass completed, by one workgroup walking the ops in tiles of 1,024.
+__global__ __launch_bounds__(1024) void uio_fast_recover_kernel(
+    const h3c_chunk_state *__restrict__ chunks, h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks, uint32_t n,
+    uint8_t poly_type, uint32_t std_domain, uint32_t exact, const uint32_t *__restrict__ crc0,
+    const PolyConsts *__restrict__ pc, FastArgs fa, uint32_t *misc, h3c_update_result *__restrict__ res,
+    unsigned long long *__restrict__ ctr) {
+  __shared__ uint32_t wagg[16][kFastCols], run[kFastCols], t0s[kFastCols], szs[kFastCols];
+  __shared__ unsigned int app[kFastCols], cnt_ok, cnt_bad, bad_state;
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, poly = pc->poly;
+  if (t < kFastCols) {
+    run[t] = 0;
+    app[t] = 0;
+    t0s[t] = 0;
+    szs[t] = 0;
+    if (t < nchunks) {
+      t0s[t] = fast_t0(chunks[t], t, exact, std_domain, crc0, pc);
+      szs[t] = chunks[t].size;
+    }
+  }
+  if (t == 0) cnt_ok = cnt_bad = bad_state = 0;
+  __syncthreads();
+  for (uint32_t b = 0; b < n; b += 1024) {
+    const uint32_t j = b + t;
+    uint32_t c = kNil, v = 0, st = 0;
+    if (j < n) {
+      c = (uint32_t)(fa.key[j] >> 36);
+      const unsigned long long g = ld_agent(&fa.dv[j]);
+      st = (uint32_t)(g >> 32);
+      if (st == 1) v = dgf_mul_fast((uint32_t)g, fa.frag[j].mult, poly);
+      if (st == 1) atomicAdd(&cnt_ok, 1u);
+      else if (st == 2) atomicAdd(&cnt_bad, 1u);
+      else atomicOr(&bad_state, 1u);
+      if (st == 1 && c < kFastCols) atomicOr(&app[c], 1u);
+    }
+    uint32_t acc0 = 0, acc1 = 0, ip = 0;
+    for (uint32_t u = 0; u < 64; ++u) {
+      const uint32_t cu = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)u);
+      const uint32_t vu = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)u);
+      if (lane >= u && c == cu) ip ^= vu;
+      if (cu == lane) acc0 ^= vu;
+      if (cu == lane + 64) acc1 ^= vu;
+    }
+    wagg[wave][lane] = acc0;
+    wagg[wave][64 + lane] = acc1;
+    __syncthreads();
+    if (j < n && c < kFastCols) {
+      uint32_t e = run[c];
+      for (uint32_t w = 0; w < wave; ++w) e ^= wagg[w][c];
+      const uint32_t sv = t0s[c] ^ e ^ ip;
+      h3c_update_result o{};
+      o.status = st == 1 ? H3C_OK : H3C_ERR_CHECKSUM_MISMATCH;
+      o.size = szs[c];
+      o.type = poly_type;
+      o.value = st == 1 ? (std_domain ? ~sv : sv) : (std_domain ? 0u : sv);
+      res[j] = o;
+    }
+    __syncthreads();
+    if (t < kFastCols) {
+      uint32_t x = 0;
+      for (uint32_t w = 0; w < 16; ++w) x ^= wagg[w][t];
+      run[t] ^= x;
+    }
+    __syncthreads();
+  }
+  if (t < nchunks) {
+    const h3c_chunk_state cs = chunks[t];
+    h3c_chunk_state f = cs;
+    if (app[t]) {
+      f.value = std_domain ? ~(t0s[t] ^ run[t]) : (t0s[t] ^ run[t]);
+      f.type = poly_type;
+    }
+    chunks_out[t] = f;
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t stale = 0;
+    for (uint32_t c = 0; c < nchunks; ++c) {
+      const h3c_chunk_state cs = chunks[c];
+      stale += exact && cs.size && cs.type == poly_type && t0s[c] != (std_domain ? ~cs.value : cs.value);
+    }
+    for (int k = 0; k < kCtrN; ++k) ctr[k] = 0;
+    ctr[std_domain ? kCtrRecalc : kCtrRead] = cnt_ok;
+    ctr[kCtrMismatch] = cnt_bad;
+    ctr[kCtrStale] = stale;
+    misc[kMiscFast] = kFastDone;
+    misc[kMiscFVoid] = 0;
+    if (bad_state) misc[kMiscErr] = 1u;  // an op with no published delta: cannot happen after a complete pass
+  }
+}
+
 // After the piece pass: A6 per op and t0 per chunk (the chunk CRCs are items n + c), one launch
 // of max(n, nchunks) threads.
 __global__ void uio_verify_t0_kernel(const h3c_update_io *__restrict__ ios, uint32_t n,
@@ -2206,7 +2838,10 @@ __global__ void uio_commit_kernel(const h3c_chunk_state *__restrict__ fin, h3c_c
                                   uint32_t nchunks, const uint32_t *__restrict__ out, uint32_t cap) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   // out: kMiscOutF, kMiscOutA6, ... kMiscPBVoid (a void phase B is redone before its outputs count)
-  if (c < nchunks && out[0] <= cap && !out[1] && !out[kMiscPBVoid - kMiscOutF]) chunks[c] = fin[c];
+  // (and the fast branch, when it ran, finished with valid results; no kernel met a corrupt table)
+  if (c < nchunks && out[0] <= cap && !out[1] && !out[kMiscPBVoid - kMiscOutF] &&
+      out[kMiscFast - kMiscOutF] <= kFastDone && !out[kMiscErr - kMiscOutF])
+    chunks[c] = fin[c];
 }
 
 // H3C_UPD_EXACT: chunks whose stored checksum of the batch polynomial disagrees with the bytes.
@@ -2392,7 +3027,12 @@ hipError_t sort_pairs(void *tmp, size_t &tmp_bytes, const uint32_t *k, uint32_t 
 
 
 // ---- per-thread cache of captured pipeline graphs (update_core) ----
-std::atomic<uint64_t> g_graph_stats[3];  // replays, captures, capture failures (h3c_diag_counter)
+// h3c_diag_counter: 0 graph replays, 1 captures, 2 capture failures, 3 front-void redos, 4 phase-B
+// reruns, 5 failed-A6 redos, 6 short fragment guesses, 7 fast-branch batches, 8 fast-branch attempts
+// abandoned (an op did not qualify), 9 fast-branch recoveries, 10 graphs refused by the topology check
+enum { kDiagReplay, kDiagCapture, kDiagCaptureFail, kDiagFrontVoid, kDiagPBVoid, kDiagA6Redo, kDiagShortF,
+       kDiagFast, kDiagFastAbort, kDiagFastVoid, kDiagTopology, kDiagN };
+std::atomic<uint64_t> g_graph_stats[kDiagN];
 struct UpdGraphKey {
   int dev;
   uint8_t poly;
@@ -2433,6 +3073,16 @@ struct ThreadRes {
   UpdGraphs cache[4];
   UpdGraphKey recent[4] = {};  // keys of the last plain calls (lease pools may alternate buffers)
   uint32_t recent_next = 0;
+  // the fast branch's last outcome per batch shape and tables: a shape whose last batch did not
+  // qualify goes straight to the general pipeline (an abandoned attempt costs a prep launch and a
+  // synchronisation); it is tried again after kFastRetry general batches
+  struct FastPred {
+    int dev = -1;
+    uint32_t flags = 0, n = 0, nchunks = 0, general_runs = 0;
+    const void *chunks = nullptr, *ios = nullptr;
+    uint8_t poly = 0, slow = 0;
+    uint64_t used = 0;
+  } pred[8];
   uint64_t tick = 0;
   ~ThreadRes() {
     std::lock_guard<std::mutex> lk(g_res.mu);
@@ -2486,6 +3136,31 @@ int aux_stream(int dev, AuxStream *&out) {
   }
   out = &a;
   return H3C_OK;
+}
+
+constexpr uint32_t kFastRetry = 64;
+ThreadRes::FastPred &fast_pred(int dev, uint8_t poly, uint32_t flags, uint32_t n, uint32_t nchunks, const void *chunks,
+                               const void *ios) {
+  ThreadRes &tr = tres();
+  ThreadRes::FastPred *victim = &tr.pred[0];
+  for (ThreadRes::FastPred &p : tr.pred) {
+    if (p.dev == dev && p.poly == poly && p.flags == flags && p.n == n && p.nchunks == nchunks && p.chunks == chunks &&
+        p.ios == ios) {
+      p.used = ++tr.tick;
+      return p;
+    }
+    if (p.used < victim->used) victim = &p;
+  }
+  *victim = ThreadRes::FastPred{};
+  victim->dev = dev;
+  victim->poly = poly;
+  victim->flags = flags;
+  victim->n = n;
+  victim->nchunks = nchunks;
+  victim->chunks = chunks;
+  victim->ios = ios;
+  victim->used = ++tr.tick;
+  return *victim;
 }
 
 UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st, bool asked) {
@@ -2672,6 +3347,20 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   Aff *d_tel, *d_tscan, *d_sel, *d_sscan;
   void *d_tmp, *d_ptmp;
   uint32_t *d_sstate;  // the prep kernel's scan states (serial front path)
+  // the fast branch (uio_fast_kernel): tried first when the batch names <= 128 chunks, unless this
+  // thread's last batch of the same shape and tables did not qualify (or the test hook says otherwise)
+  const uint64_t fast_hook = h3c_rt::hook(H3C_HOOK_UPD_FAST);
+  const uint32_t giveup = (uint32_t)h3c_rt::hook(H3C_HOOK_UPD_GIVEUP);
+  const bool fast_able = fast_hook != 1 && nchunks >= 1 && nchunks <= kFastCols;
+  ThreadRes::FastPred *fpred = fast_able ? &fast_pred(dev, poly_type, flags & ~H3C_UPD_GRAPHS, n, nchunks, d_chunks, d_ios)
+                                         : nullptr;
+  const bool try_fast = fast_able && (fast_hook == 2 || !fpred->slow || fpred->general_runs >= kFastRetry);
+  const uint32_t nwg_fast = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
+  const uint32_t ntiles_tail = (uint32_t)std::max<size_t>(1, ((size_t)n + 1023) / 1024);  // uio_fast_tail_kernel
+  uint32_t hcap_fast = 256;
+  while (hcap_fast < 2 * n) hcap_fast <<= 1;
+  FastArgs fa{};
+  unsigned long long *d_gran = nullptr;
   auto layout = [&](char *base) -> size_t {  // one layout, run with base 0 to size the lease
     char *cur = base;
     d_status = carve<uint32_t>(cur, n);
@@ -2703,11 +3392,23 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     d_tmp = carve<char>(cur, tmp_bytes);
     d_ptmp = carve<char>(cur, pscan_tmp);
     d_sstate = carve<uint32_t>(cur, 3 + (size_t)prep_tiles);
+    if (fast_able) {
+      fa.frag = carve<FragDesc>(cur, n);
+      fa.key = carve<unsigned long long>(cur, n);
+      fa.link = carve<uint4>(cur, n);
+      fa.head = carve<uint32_t>(cur, hcap_fast);
+      fa.hmask = hcap_fast - 1;
+      fa.dv = carve<unsigned long long>(cur, n);
+      fa.chain = carve<uint2>(cur, n);
+      d_gran = carve<unsigned long long>(cur, (size_t)ntiles_tail * kFastCols);
+    }
     return (size_t)(cur - base);
   };
   h3c_rt::DeviceLease lease1(dev, layout(nullptr));
   if (!lease1.ok()) return H3C_ERR_HIP;
   layout(lease1.data());
+  fa.slow = d_misc + kMiscSlow;
+  fa.pc = pc;
   h3c_rt::PinnedLease pin(4096);
   if (!pin.ok()) return H3C_ERR_HIP;
   uint32_t *h_F = reinterpret_cast<uint32_t *>(pin.data());
@@ -2760,7 +3461,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     // (a kernel, not hipMemsetAsync: a memset node at the head of the captured graph was not
     // ordered before the prep kernel in replays -- stale tickets, r03m-r03p)
     if (serial) {
-      hipLaunchKernelGGL(uio_zero_kernel, dim3(1), dim3(256), 0, q, d_sstate, 3u + prep_tiles);
+      hipLaunchKernelGGL(uio_zero_kernel, dim3(1), dim3(256), 0, q, d_sstate, 3u + prep_tiles, nullptr, 0u, nullptr,
+                         0u, nullptr, 0u);
       HIP_TRY(hipGetLastError());
     }
     // serial: one tile per 256 items (the initialisations beyond them grid-stride), so only the
@@ -2769,13 +3471,13 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     hipLaunchKernelGGL(uio_prep_kernel, dim3(ptiles), dim3(kPrepTile), 0, q, d_ios, n, d_chunks, nchunks,
                        poly_type, stdf, exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc, d_a6,
                        reinterpret_cast<uint32_t *>(d_fslot), fz_words, d_hhead, front ? hcap : 0u, d_gnext, d_fnext,
-                       front ? cap : 0u, serial ? d_pbase : nullptr, serial ? d_sstate : nullptr);
+                       front ? cap : 0u, serial ? d_pbase : nullptr, serial ? d_sstate : nullptr, FastArgs{});
     HIP_TRY(hipGetLastError());
     if (serial) {
       size_t t = tmp_bytes;
       HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, q));
       return h3c_rt::launch_uio_piece_crc(q, dev, poly_type, d_ios, n, d_chunks, nchunks, d_pbase, d_sstate + 2,
-                                          d_paycrc0, d_sstate + 3, kPrepTile);
+                                          d_paycrc0, d_sstate + 3, kPrepTile, d_misc + kMiscErr);
     }
     // second stream, forked here: the piece counts' scan (its own scratch), one piece-CRC pass over
     // the payloads that are not fold candidates and the chunks CRC'd from their bytes (before the
@@ -2795,7 +3497,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       HIP_TRY(sort_pairs(d_tmp, t, d_key, d_skey, d_idx, d_order, n, bits, q));
     }
     int r = h3c_rt::launch_uio_piece_crc(aux->st, dev, poly_type, d_ios, n, d_chunks, nchunks, d_pbase, d_pbase + NP,
-                                         d_paycrc0);
+                                         d_paycrc0, nullptr, 0u, d_misc + kMiscErr);
     if (r) return r;
     hipLaunchKernelGGL(uio_verify_t0_kernel, dim3(vb), dim3(tb), 0, aux->st, d_ios, n, d_chunks, nchunks, poly_type,
                        exactf, stdf, d_paycrc0, pc, d_status, d_payraw, d_a6, d_misc, d_t0, d_chunks_out, 1u);
@@ -2816,7 +3518,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                                       aux->st));
     }
     r = h3c_rt::launch_uio_piece_crc(aux->st, dev, poly_type, d_ios, n, d_chunks, 0, d_lbase, d_lbase + n,
-                                     d_paycrc0);
+                                     d_paycrc0, nullptr, 0u, d_misc + kMiscErr);
     if (r) return r;
     hipLaunchKernelGGL(uio_late_verify_kernel, dim3(gb), dim3(tb), 0, aux->st, d_ios, n, d_late, d_paycrc0, pc, stdf,
                        d_status, d_payraw, d_a6, d_misc);
@@ -2824,6 +3526,123 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     HIP_TRY(hipEventRecord(aux->done, aux->st));
     return H3C_OK;
   };
+
+  // ---- the fast branch: zero, prep (with the fast tables), [piece pass: exact mode's chunk CRCs],
+  // uio_fast_kernel -- four launches at most, one graph on request.  An op that does not qualify makes
+  // uio_fast_kernel return at once (nothing written); the general pipeline below then runs the batch.
+  if (try_fast) {
+    const uint32_t ptiles_f = (uint32_t)(((size_t)n + C + 1 + kPrepTile - 1) / kPrepTile);
+    const uint32_t zwords = hcap_fast + 2 * ntiles_tail * kFastCols + 1 + (exact ? 3u + prep_tiles : 0u);
+    const uint32_t zb = 256, zg = std::max(1u, std::min(1024u, (zwords + 4 * zb - 1) / (4 * zb)));
+    unsigned long long *d_ts = reinterpret_cast<unsigned long long *>(d_misc + kMiscT0);
+    auto fast_kernel = [&](hipStream_t q, bool timed) -> int {
+      hipLaunchKernelGGL(uio_fast_kernel, dim3(nwg_fast), dim3(kBlkThreads), 0, q, n, stdf, pc, fa.frag, fa.chain,
+                         fa.dv, d_misc, timed ? d_ts : nullptr);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(uio_fast_tail_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, d_chunks, d_chunks_out,
+                         nchunks, n, poly_type, stdf, exactf, d_paycrc0 + n, pc, fa.frag, fa.key, fa.dv, d_misc,
+                         d_gran, d_res, d_ctr, d_hF, (giveup & 4) ? 1u : 0u);
+      HIP_TRY(hipGetLastError());
+      return H3C_OK;
+    };
+    auto fast_front = [&](hipStream_t q) -> int {  // zero, prep, [piece pass]
+      hipLaunchKernelGGL(uio_zero_kernel, dim3(zg), dim3(zb), 0, q, fa.head, hcap_fast,
+                         reinterpret_cast<uint32_t *>(d_gran), 2 * ntiles_tail * kFastCols, d_misc + kMiscSlow, 1u,
+                         exact ? d_sstate : nullptr, exact ? 3u + prep_tiles : 0u);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(uio_prep_kernel, dim3(ptiles_f), dim3(kPrepTile), 0, q, d_ios, n, d_chunks, nchunks, poly_type,
+                         stdf, exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc, d_a6, nullptr, 0u,
+                         nullptr, 0u, nullptr, nullptr, 0u, exact ? d_pbase : nullptr, exact ? d_sstate : nullptr, fa);
+      HIP_TRY(hipGetLastError());
+      if (exact) {  // the chunks' CRCs before uio_fast_kernel writes them (t0 from the bytes)
+        const int r = h3c_rt::launch_uio_piece_crc(q, dev, poly_type, d_ios, n, d_chunks, nchunks, d_pbase,
+                                                   d_sstate + 2, d_paycrc0, d_sstate + 3, kPrepTile, d_misc + kMiscErr);
+        if (r) return r;
+      }
+      hipLaunchKernelGGL(uio_fast_link_kernel, dim3((n + 255) / 256), dim3(256), 0, q, fa.link, fa.key, fa.head,
+                         fa.hmask, n, d_misc, fa.chain);
+      HIP_TRY(hipGetLastError());
+      return H3C_OK;
+    };
+    const UpdGraphKey fkey{dev, poly_type, flags | 0x80000000u, n, nchunks, 0u, hcap_fast, d_chunks, d_chunks_out,
+                           d_ios, d_res, d_ctr, lease1.data(), nullptr, d_hF, nullptr};
+    UpdGraphs *gr = upd_graphs(fkey, st, (flags & H3C_UPD_GRAPHS) != 0);
+    if (gr && !gr->g && !gr->failed) {
+      hipStream_t cst = capture_stream(dev);
+      rc = cst ? capture_graph(cst, [&] {
+        int r = fast_front(cst);
+        if (!r) r = fast_kernel(cst, true);
+        if (!r && epi_graph) r = epilogue(cst, d_misc + kMiscOutF, cap);
+        return r;
+      }, gr->g) : H3C_ERR_HIP;
+      g_graph_stats[rc ? kDiagCaptureFail : kDiagCapture].fetch_add(1);
+      if (rc) {
+        gr->failed = true;
+        (void)hipGetLastError();
+      }
+      rc = H3C_OK;
+    }
+    const bool use_graph = gr && gr->g && !gr->failed;
+    if (use_graph) {
+      HIP_TRY(hipGraphLaunch(gr->g, st));
+      g_graph_stats[kDiagReplay].fetch_add(1);
+    } else {
+      rc = fast_front(st);
+      if (rc) return rc;
+      rc = fast_kernel(st, true);  // (timed by its own wall-clock stamps: an abandoned attempt counts nothing)
+      if (rc) return rc;
+    }
+    if (!(use_graph && epi_graph)) {
+      rc = epilogue(st, d_misc + kMiscOutF, cap);
+      if (rc) return rc;
+    }
+    const hipError_t se = hipStreamSynchronize(st);
+    if (se != hipSuccess) {
+      drain.armed = drain_aux.armed = false;
+      h3c_rt::set_error("h3c_update_ios (fast branch)", se);
+      return H3C_ERR_HIP;
+    }
+    const uint32_t fs = h_F[kMiscFast - kMiscOutF];
+    if (h_F[kMiscErr - kMiscOutF]) {
+      drain.armed = drain_aux.armed = false;
+      h3c_rt::set_error_text("h3c_update_ios: a piece table disagrees with its items (corrupt scratch)");
+      return H3C_ERR_HIP;
+    }
+    if (fs == kFastDone || fs == kFastVoid) {
+      if (h3c_rt::prof_enabled()) {  // the kernel's own wall-clock span (hipEvents carry no time in a graph)
+        uint64_t t0, t1;
+        std::memcpy(&t0, h_F + (kMiscT0 - kMiscOutF), 8);
+        std::memcpy(&t1, h_F + (kMiscT1 - kMiscOutF), 8);
+        const int khz = h3c_rt::device_wall_clock_khz(dev);
+        if (t1 > t0 && khz > 0) h3c_rt::prof_add(H3C_PROF_UPDIO, (float)((double)(t1 - t0) / khz), 3ull * kBlk * n);
+      }
+      g_graph_stats[kDiagFast].fetch_add(1);
+      fpred->slow = 0;
+      if (fs == kFastVoid) {  // a workgroup gave up waiting: the bytes and deltas are complete, the results not
+        g_graph_stats[kDiagFastVoid].fetch_add(1);
+        hipLaunchKernelGGL(uio_fast_recover_kernel, dim3(1), dim3(1024), 0, st, d_chunks, d_chunks_out, nchunks, n,
+                           poly_type, stdf, exactf, d_paycrc0 + n, pc, fa, d_misc, d_res, d_ctr);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(h_F, d_misc + kMiscOutF, 4 * (kMiscN - kMiscOutF), hipMemcpyDeviceToHost, st));
+        rc = epilogue(st, d_misc + kMiscOutF, cap);
+        if (rc) return rc;
+        const hipError_t se2 = hipStreamSynchronize(st);
+        if (se2 != hipSuccess || h_F[kMiscErr - kMiscOutF]) {
+          drain.armed = drain_aux.armed = false;
+          if (se2 != hipSuccess) h3c_rt::set_error("h3c_update_ios (fast-branch recovery)", se2);
+          else h3c_rt::set_error_text("h3c_update_ios: fast-branch recovery found an op with no delta");
+          return H3C_ERR_HIP;
+        }
+      }
+      drain.armed = drain_aux.armed = false;
+      return H3C_OK;
+    }
+    // kFastAbort: some op does not qualify -- the general pipeline runs the batch
+    g_graph_stats[kDiagFastAbort].fetch_add(1);
+    fpred->slow = 1;
+    fpred->general_runs = 0;
+  }
+  if (fpred) ++fpred->general_runs;
 
   // ---- fragments, blocks, scans, results (redone once if the fragment guess was short) ----
   for (int attempt = 0;; ++attempt) {
@@ -2851,7 +3670,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                            d_skey, n, d_chunks, nchunks, d_status, poly_type, stdf, pc, d_pos, d_nfrag, d_fbase,
                            d_late, d_payraw, d_a6, d_misc, d_frag, d_fkey, cap, d_hhead, hcap - 1, d_gnext, d_prev,
                            d_fnext, d_fslot, d_paycrc0, exactf, d_t0, d_chunks_out,
-                           H3C_UIO_SERIAL ? d_sstate : nullptr);
+                           H3C_UIO_SERIAL ? d_sstate : nullptr, giveup & 1u);
         HIP_TRY(hipGetLastError());
         if (!H3C_UIO_LATE_JOIN && !H3C_UIO_SERIAL) HIP_TRY(hipStreamWaitEvent(q, aux->done, 0));  // the A6 verdicts, t0
         return H3C_OK;
@@ -2901,7 +3720,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         hipLaunchKernelGGL(uio_phaseb_kernel, dim3(std::max(ntiles_pb, 1u)), dim3(kPhaseBTile), 0, q, d_pos, d_skey, n,
                            d_eacc, d_payraw, pc, d_a6, d_t0, d_chunks, d_chunks_out, nchunks, poly_type, stdf, d_res,
                            d_ctr, d_F, d_misc, reinterpret_cast<PhaseBSlot *>(d_pbz), d_pbz + pbz_words - 1,
-                           d_hF);
+                           d_hF, (giveup >> 1) & 1u);
         HIP_TRY(hipGetLastError());
       } else {
         const int r = phase_b_scans(q);
@@ -2951,16 +3770,16 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       if (rc) {  // not capturable here: plain launches from now on for this shape
         gr->failed = true;
         (void)hipGetLastError();
-        g_graph_stats[2].fetch_add(1);
+        g_graph_stats[kDiagCaptureFail].fetch_add(1);
       } else {
-        g_graph_stats[1].fetch_add(1);
+        g_graph_stats[kDiagCapture].fetch_add(1);
       }
       rc = H3C_OK;
     }
     const bool use_graph = gr && gr->g && !gr->failed;
     if (use_graph) {
       HIP_TRY(hipGraphLaunch(gr->g, st));
-      g_graph_stats[0].fetch_add(1);
+      g_graph_stats[kDiagReplay].fetch_add(1);
     } else {
       if (attempt == 0) {
         rc = phase_a(st);
@@ -2998,6 +3817,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       if (t1 > t0 && khz > 0) h3c_rt::prof_add(H3C_PROF_UPDIO, (float)((double)(t1 - t0) / khz), alg_bytes);
     }
     if (h_F[kMiscPBVoid - kMiscOutF] && h_F[0] <= cap && !h_F[1]) {
+      g_graph_stats[kDiagPBVoid].fetch_add(1);
       // a phase-B tile gave up waiting (its CU starved by other work): the chunk bytes are
       // written and right; redo phase B the scan-based way over the same state, then the epilogue
       HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, st));
@@ -3019,10 +3839,17 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         return H3C_ERR_HIP;
       }
     }
+    if (h_F[kMiscErr - kMiscOutF]) {
+      drain.armed = drain_aux.armed = false;
+      h3c_rt::set_error_text("h3c_update_ios: a piece table disagrees with its items (corrupt scratch)");
+      return H3C_ERR_HIP;
+    }
     const uint32_t F = h_F[0], a6_failed = h_F[1];
     const bool void_pass = (a6_failed & kMiscVoid) != 0;  // a front tile gave up waiting: F means nothing
     if (!void_pass) last_frags = F;
     if (F <= cap && !a6_failed) break;
+    // a redo: counted by its cause (h3c_diag_counter 3, 5, 6)
+    g_graph_stats[void_pass ? kDiagFrontVoid : (a6_failed & 1u) ? kDiagA6Redo : kDiagShortF].fetch_add(1);
     if (attempt >= 2) {  // cannot happen: a redo knows the verdicts, and the count after the first redo
       drain.armed = drain_aux.armed = false;
       h3c_rt::set_error_text("h3c_update_ios: fragment count changed between attempts");
@@ -3043,7 +3870,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         HIP_TRY(rocprim::exclusive_scan(d_tmp, t, d_np, d_pbase, 0u, NP + 1, rocprim::plus<uint32_t>(), st));
       }
       rc = h3c_rt::launch_uio_piece_crc(st, dev, poly_type, d_ios, n, d_chunks, nchunks, d_pbase, d_pbase + NP,
-                                        d_paycrc0);
+                                        d_paycrc0, nullptr, 0u, d_misc + kMiscErr);
       if (rc) return rc;
       hipLaunchKernelGGL(uio_verify_t0_kernel, dim3(vb), dim3(tb), 0, st, d_ios, n, d_chunks, nchunks, poly_type,
                          exactf, stdf, d_paycrc0, pc, d_status, d_payraw, d_a6, d_misc, d_t0, d_chunks_out, 0u);
@@ -3079,7 +3906,7 @@ void counters_from(const unsigned long long *h, h3c_update_counters *c) {
 }  // namespace
 
 extern "C" uint64_t h3c_diag_counter(int which) {
-  return which >= 0 && which < 3 ? g_graph_stats[which].load() : 0;
+  return which >= 0 && which < kDiagN ? g_graph_stats[which].load() : 0;
 }
 
 extern "C" int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks, const h3c_update_io *ios,

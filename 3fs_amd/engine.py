@@ -354,12 +354,23 @@ def sync_bench(threads: int, nbytes: int, calls: int, api: str = "verify"):
 
 
 HOOK_SEG_BYTES, HOOK_DEBUG_FLAGS, HOOK_UPD_SCAN, HOOK_UPD_GRAPHS, HOOK_UPD_LOOKBACK, HOOK_UPD_FRONT = 1, 2, 3, 4, 5, 6
+HOOK_UPD_FAST, HOOK_UPD_GIVEUP = 7, 8
 UPD_SCAN_PATHS = {"default": 0, "fused": 1, "tiles": 2, "sort": 3}
+
+# h3c_diag_counter indices (include/h3c_crc.h): process-wide, monotonic
+DIAG_NAMES = ("graph_replays", "graph_captures", "graph_capture_failures", "redo_front_void", "rerun_phase_b_void",
+              "redo_failed_a6", "redo_short_fragment_guess", "fast_batches", "fast_abandoned", "fast_recovered",
+              "graph_topology_refused")
 
 
 def diag_counter(which: int) -> int:
-    """h3c_diag_counter: 0 UpdateIO graph replays, 1 captures, 2 capture failures."""
+    """h3c_diag_counter(which): see DIAG_NAMES (0 UpdateIO graph replays, 1 captures, ...)."""
     return int(lib.h3c_diag_counter(int(which)))
+
+
+def diag_counters() -> dict:
+    """Every h3c_diag_counter by name."""
+    return {name: diag_counter(k) for k, name in enumerate(DIAG_NAMES)}
 
 
 def set_test_hook(key: int, value: int) -> None:

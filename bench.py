@@ -219,6 +219,7 @@ PATTERN_CEILING = {
     "upd_delta_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
     "upd_fused_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
     "uio_block_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
+    "uio_fast_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
 }
 
 
@@ -418,6 +419,9 @@ def run_updio(args, cx: Ctx) -> dict:
     g = np.random.default_rng(SEED + cx.rank)
     wc = g.integers(0, nchunks, nw).astype(np.uint32)
     wb = g.integers(0, bpc, nw).astype(np.uint32)
+    if getattr(args, "updio_order", "random") == "chunk":  # diagnostics: the ops grouped by chunk
+        o = np.argsort(wc, kind="stable")
+        wc, wb = wc[o], wb[o]
     plan = h3c.Plan.uniform(chunks.data_ptr(), clen, nchunks, device=cx.local)
     raw0 = torch.zeros(nchunks, dtype=torch.int32, device=cx.dev)
     plan.run(raw0, stream=cx.stream)
@@ -448,9 +452,16 @@ def run_updio(args, cx: Ctx) -> dict:
     def step():
         h3c.update_ios_dev(d_state, d_ios, d_res, stream=cx.stream, exact=exact, counters=d_ctr, graphs=True)
 
-    g0 = [h3c.diag_counter(k) for k in range(3)]
+    g0 = h3c.diag_counters()
     elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDIO)
-    graphs = dict(zip(("replays", "captures", "capture_failures"), (h3c.diag_counter(k) - g0[k] for k in range(3))))
+    diag = {k: v - g0[k] for k, v in h3c.diag_counters().items()}
+    graphs = {"replays": diag["graph_replays"], "captures": diag["graph_captures"],
+              "capture_failures": diag["graph_capture_failures"]}
+    # every redo / recovery / abandoned attempt the engine counts (h3c_diag_counter 3-9), over warmup +
+    # timed steps: all 0 on config 3, which must run every step on the fast branch
+    redo = {k: diag[k] for k in ("redo_front_void", "rerun_phase_b_void", "redo_failed_a6", "redo_short_fragment_guess",
+                                 "fast_abandoned", "fast_recovered")}
+    fast_steps = diag["fast_batches"]
     torch.cuda.synchronize()
     fin = d_state.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)
     res = d_res.cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)
@@ -460,7 +471,7 @@ def run_updio(args, cx: Ctx) -> dict:
     torch.cuda.synchronize()
     fresh_np = fresh.cpu().numpy().view(np.uint32)
     ok = bool((res["status"] == 0).all()) and np.array_equal(fresh_np, fin["value"])
-    ok = ok and counters["read_chunk"] == nw
+    ok = ok and counters["read_chunk"] == nw and not any(redo.values())
 
     # the same step through the host-array entry: tables over PCIe, inside the timed region
     state["value"] = fin["value"]
@@ -480,7 +491,8 @@ def run_updio(args, cx: Ctx) -> dict:
     plan.close()
     pplan.close()
     writes = nw * args.steps * cx.world
-    rl = roofline(prof, HBM_PEAK_GBPS, kernel="uio_block_kernel")
+    fast = fast_steps == args.steps + args.warmup
+    rl = roofline(prof, HBM_PEAK_GBPS, kernel="uio_fast_kernel" if fast else "uio_block_kernel")
     out = {
         "metric": "partial-update writes/s through the general UpdateIO path (4 KiB writes into 64 MiB chunks)",
         "value": round(writes / elapsed, 1),
@@ -499,6 +511,8 @@ def run_updio(args, cx: Ctx) -> dict:
         "algorithmic_gbps": round(writes * 3 * G / elapsed / 1e9, 1),
         "counters": counters,
         "graphs": graphs,  # UpdateIO pipeline graph use over warmup + timed steps (one thread: replays)
+        "branch": "fast (uio_fast_kernel)" if fast else f"general ({fast_steps} of {args.steps + args.warmup} fast)",
+        "redo": redo,
         "pcie_inclusive": {"entry": "h3c_update_ios_ex (host tables in pinned memory)",
                            "value": round(nw * hsteps * cx.world / helapsed, 1), "unit": "writes/s",
                            "ms_per_step": round(helapsed / hsteps * 1e3, 4), "steps": hsteps},
@@ -895,6 +909,8 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--exact", action="store_true", help="updio / update: do not trust stored checksums")
+    ap.add_argument("--updio-order", choices=["random", "chunk"], default="random",
+                    help="updio diagnostics: chunk = the same writes grouped by chunk (sequence order within)")
     ap.add_argument("--sync-threads", type=int, default=32)
     ap.add_argument("--sync-kib", default="4,128,1024", help="sync: buffer sizes (KiB), comma-separated")
     args = ap.parse_args()

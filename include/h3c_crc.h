@@ -435,13 +435,30 @@ enum h3c_hook {
   H3C_HOOK_UPD_LOOKBACK = 5, /* h3c_update_blocks fused path: 1 makes the workgroup with ticket 1 give up
                                its look-back at once, as a starved wait would (the void-batch report:
                                *n_invalid = UINT32_MAX, counters.invalid = UINT64_MAX) */
-  H3C_HOOK_UPD_FRONT = 6     /* h3c_update_ios, bit mask: 1 runs the sizes / cases / fragments as the
+  H3C_HOOK_UPD_FRONT = 6,    /* h3c_update_ios, bit mask: 1 runs the sizes / cases / fragments as the
                                scan-based stage (~10 launches) instead of the one-pass front kernel; 2 runs
                                phase B (t / s scans, results) as 5 launches instead of one */
+  H3C_HOOK_UPD_FAST = 7,     /* h3c_update_ios: 1 never tries the fast branch (every batch takes the general
+                               pipeline); 2 tries it first on every batch, whatever the last outcome of the
+                               batch shape was (default 0: tried first unless this thread's last batch of the
+                               same shape and tables did not qualify) */
+  H3C_HOOK_UPD_GIVEUP = 8    /* h3c_update_ios, bit mask: a starved wait forced (spin limit 0) in the tile or
+                               workgroup with ticket 1 of -- 1: uio_front_kernel (the pass is void and redone on
+                               the scan-based stage), 2: uio_phaseb_kernel (phase B rerun the scan-based way),
+                               4: uio_fast_kernel's look-back (results recomputed by the recovery kernel) */
 };
 int h3c_test_hook(int key, uint64_t value);
-/* Engine-internal counters for tests: 0 = h3c_update_ios pipeline graph replays, 1 = graph
- * captures, 2 = capture failures. */
+/* Engine-internal counters (process-wide, monotonic) for tests and benches:
+ *   0 h3c_update_ios pipeline graph replays, 1 graph captures, 2 capture failures,
+ *   3 general-pipeline batches redone because a front tile gave up waiting (a void pass),
+ *   4 phase B reruns because a phase-B tile gave up waiting,
+ *   5 batches redone because a speculative A6 check failed (non-fold payloads),
+ *   6 batches redone because the fragment count exceeded its guess,
+ *   7 batches run by the fast branch (uio_fast_kernel),
+ *   8 fast-branch attempts abandoned because an op did not qualify (the general pipeline ran),
+ *   9 fast-branch batches whose results were recomputed after a workgroup gave up waiting,
+ *   10 captured graphs refused by the topology check (a memset / memcpy node, or a kernel node not
+ *      ordered after the graph's root) and run as plain launches instead. */
 uint64_t h3c_diag_counter(int which);
 
 #ifdef __cplusplus

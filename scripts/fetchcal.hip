@@ -14,8 +14,15 @@
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef const v4u __attribute__((address_space(1))) *gv4p;
 
-// G lanes per chunk, B rows in flight per lane (as scripts/smallbw.hip)
-template <int G, int B>
+template <bool NT>
+__device__ __forceinline__ v4u ld(const char *a) {
+  if (NT) return __builtin_nontemporal_load((gv4p)a);
+  return *(gv4p)a;
+}
+// G lanes per chunk, B rows in flight per lane (as scripts/smallbw.hip); NT: nontemporal loads;
+// SPAN: a lane's two consecutive loads are the two 16-byte halves of its 32 bytes of a 128-byte
+// row (lanes at 32 gl, then 32 gl + 16), so every load instruction touches each chunk's whole line
+template <int G, int B, bool NT = true, bool SPAN = false>
 __device__ __forceinline__ void walk_body(const char *p, uint32_t nchunks, uint32_t chunk, uint32_t *out) {
   constexpr uint32_t NG = 64 / G, kQ = 16 * G;
   const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
@@ -26,12 +33,15 @@ __device__ __forceinline__ void walk_body(const char *p, uint32_t nchunks, uint3
   for (uint32_t q0 = lo; q0 < hi; q0 += NG) {
     const uint32_t t = q0 + grp;
     if (t >= hi) break;
-    const char *la = p + (uint64_t)t * chunk + 16 * gl;
+    const char *cb = p + (uint64_t)t * chunk;
     for (uint32_t u0 = 0; u0 < K; u0 += B) {
       v4u v[B];
 #pragma unroll
-      for (int b = 0; b < B; ++b)
-        v[b] = u0 + b < K ? __builtin_nontemporal_load((gv4p)(la + (uint64_t)(u0 + b) * kQ)) : v4u{0, 0, 0, 0};
+      for (int b = 0; b < B; ++b) {
+        const uint32_t u = u0 + b;
+        const uint64_t off = SPAN ? (uint64_t)(u >> 1) * (2 * kQ) + 32 * gl + (u & 1) * 16 : (uint64_t)u * kQ + 16 * gl;
+        v[b] = u < K ? ld<NT>(cb + off) : v4u{0, 0, 0, 0};
+      }
 #pragma unroll
       for (int b = 0; b < B; ++b) acc ^= v[b];
     }
@@ -40,6 +50,19 @@ __device__ __forceinline__ void walk_body(const char *p, uint32_t nchunks, uint3
 }
 __global__ __launch_bounds__(1024) void fetchcal_rows4(const char *p, uint32_t n, uint32_t chunk, uint32_t *o) {
   walk_body<4, 4>(p, n, chunk, o);
+}
+__global__ __launch_bounds__(1024) void fetchcal_rows4_plain(const char *p, uint32_t n, uint32_t chunk, uint32_t *o) {
+  walk_body<4, 4, false>(p, n, chunk, o);
+}
+__global__ __launch_bounds__(1024) void fetchcal_rows4_span(const char *p, uint32_t n, uint32_t chunk, uint32_t *o) {
+  walk_body<4, 4, true, true>(p, n, chunk, o);
+}
+__global__ __launch_bounds__(1024) void fetchcal_rows4_span_plain(const char *p, uint32_t n, uint32_t chunk,
+                                                                  uint32_t *o) {
+  walk_body<4, 4, false, true>(p, n, chunk, o);
+}
+__global__ __launch_bounds__(1024) void fetchcal_rows4_b8(const char *p, uint32_t n, uint32_t chunk, uint32_t *o) {
+  walk_body<4, 8>(p, n, chunk, o);
 }
 __global__ __launch_bounds__(1024) void fetchcal_rows8(const char *p, uint32_t n, uint32_t chunk, uint32_t *o) {
   walk_body<8, 4>(p, n, chunk, o);
@@ -70,11 +93,15 @@ int main() {
       (void)hipEventElapsedTime(&ms, a, b);
       best = ms < best ? ms : best;
     }
-    printf("%-8s bytes per launch %llu  best %.1f GB/s\n", name, (unsigned long long)bytes, bytes / (best / 1e3) / 1e9);
+    printf("%-18s bytes per launch %llu  best %.1f GB/s\n", name, (unsigned long long)bytes, bytes / (best / 1e3) / 1e9);
     return true;
   };
   const uint32_t chunk = 4096, n = (uint32_t)(bytes / chunk);
   bool ok = run("rows4", [&] { fetchcal_rows4<<<cus, 1024>>>(d, n, chunk, o); }) &&
+            run("rows4_plain", [&] { fetchcal_rows4_plain<<<cus, 1024>>>(d, n, chunk, o); }) &&
+            run("rows4_span", [&] { fetchcal_rows4_span<<<cus, 1024>>>(d, n, chunk, o); }) &&
+            run("rows4_span_plain", [&] { fetchcal_rows4_span_plain<<<cus, 1024>>>(d, n, chunk, o); }) &&
+            run("rows4_b8", [&] { fetchcal_rows4_b8<<<cus, 1024>>>(d, n, chunk, o); }) &&
             run("rows8", [&] { fetchcal_rows8<<<cus, 1024>>>(d, n, chunk, o); }) &&
             run("wide", [&] { fetchcal_wide<<<cus, 1024>>>(d, n, chunk, o); });
   return ok && hipDeviceSynchronize() == hipSuccess ? 0 : 1;

@@ -15,8 +15,9 @@ def load(d):
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            key = next((k for k in ("fetchcal_rows4", "fetchcal_rows8", "fetchcal_wide", "seg_uni_kernel",
-                                    "seg_crc_kernel") if k in name), None)
+            key = next((k for k in ("fetchcal_rows4_span_plain", "fetchcal_rows4_span", "fetchcal_rows4_plain",
+                                    "fetchcal_rows4_b8", "fetchcal_rows4", "fetchcal_rows8", "fetchcal_wide",
+                                    "seg_uni_kernel", "seg_crc_kernel") if k in name), None)
             if key:
                 acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return acc

@@ -30,7 +30,8 @@ class Scenario:
     value is off by a random error (bit rot / a torn write) -- the oracle replays the
     reference literally, so its results are what the engine must return in exact mode."""
 
-    def __init__(self, h3c, torch, dev, nchunks, chunk_size, rng, init="mixed", empty_type=orc.CRC32C, stale=0.0):
+    def __init__(self, h3c, torch, dev, nchunks, chunk_size, rng, init="mixed", empty_type=orc.CRC32C, stale=0.0,
+                 crc_type=orc.CRC32C, sizes=None):
         self.h3c, self.torch, self.dev, self.rng = h3c, torch, dev, rng
         self.nchunks, self.chunk_size = nchunks, chunk_size
         self.host = np.zeros((nchunks, chunk_size), dtype=np.uint8)
@@ -38,14 +39,14 @@ class Scenario:
         self.stale_chunks = 0
         for c in range(nchunks):
             kind = init if init != "mixed" else ["empty", "crc", "none", "crc"][c % 4]
-            size = 0 if kind == "empty" else int(rng.integers(1, chunk_size + 1))
+            size = 0 if kind == "empty" else int(rng.integers(1, chunk_size + 1)) if sizes is None else sizes[c]
             self.host[c, :size] = rng.integers(0, 256, size, dtype=np.uint8)
             if kind == "crc":
-                v = orc.crc32c(self.host[c, :size])
+                v = orc.crc32c(self.host[c, :size]) if crc_type == orc.CRC32C else orc.crc32(self.host[c, :size])
                 if stale and rng.random() < stale:
                     v ^= int(rng.integers(1, 1 << 32))
                     self.stale_chunks += 1
-                self.meta.append({"size": size, "type": orc.CRC32C, "value": v})
+                self.meta.append({"size": size, "type": crc_type, "value": v})
             elif kind == "none":
                 self.meta.append({"size": size, "type": orc.NONE, "value": 0})
             else:
