@@ -9,11 +9,18 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <shared_mutex>
 #include <string>
 
 #include "h3c_crc.h"
 
 namespace h3c_rt {
+// HIP fails a launch into the legacy default stream made while any stream of the process is capturing.
+// The engine's own captures (h3c_update_ios with H3C_UPD_GRAPHS) hold this gate exclusively; its
+// synchronous entries that launch onto the legacy stream (stream == NULL: h3c_batch_create / verify,
+// h3c_crc32c, the folly-signature entries) hold it shared, so they wait out an engine capture instead of
+// failing (and the folly entries aborting).  Captures by other libraries remain the caller's concern.
+std::shared_mutex &capture_gate();
 // Per-device constant block for `type` (H3C_TYPE_CRC32C / H3C_TYPE_CRC32), built on first use.
 const void *device_consts(int dev, int type);
 int device_num_cu(int dev);

@@ -984,6 +984,10 @@ const void *device_consts(int dev, int type) {
 int device_num_cu(int dev) { return (dev >= 0 && dev < kMaxDevices) ? g_dev[dev].num_cu : 0; }
 int device_wall_clock_khz(int dev) { return (dev >= 0 && dev < kMaxDevices) ? g_dev[dev].wall_khz : 0; }
 uint64_t hook(int key) { return (key > 0 && key < kHooks) ? g_hooks[key].load(std::memory_order_relaxed) : 0; }
+std::shared_mutex &capture_gate() {
+  static std::shared_mutex m;
+  return m;
+}
 int current_device(int *dev) { return ::current_device(dev); }
 void set_error(const char *what, hipError_t e) { ::set_error(what, e); }
 void set_error_text(const char *text) { g_last_error = text; }
@@ -1646,6 +1650,9 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
   if (!scratch.ok()) return H3C_ERR_HIP;
   char *const arena = scratch.data();
   uint32_t mis = 0;
+  // launches onto the legacy stream wait out an engine graph capture (h3c_rt::capture_gate)
+  std::shared_lock<std::shared_mutex> gate;
+  if (!st) gate = std::shared_lock<std::shared_mutex>(h3c_rt::capture_gate());
   auto body = [&]() -> int {
     // stage host payloads and point their DevChunks at the staged copies
     uint64_t off = off_stage;

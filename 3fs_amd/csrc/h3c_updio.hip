@@ -2439,8 +2439,8 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
     bool hd = false, cn = false;
     if (j < hi) {
       const uint2 ch = chain[j];
-      hd = ch.x != 0;
-      cn = hd && ch.y != kNil;
+      hd = (H3C_FX & 64) ? true : ch.x != 0;  // (FX 64: timing experiment, every op its own chain: wrong results)
+      cn = hd && ch.y != kNil && !(H3C_FX & 64);
     }
     cm = __builtin_amdgcn_ballot_w64(cn);
     return __builtin_amdgcn_ballot_w64(hd);
@@ -2501,7 +2501,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
   FAST_MARK(2);
   uint32_t head_op = op, dirty = 0;
   while (op != kNil) {
-    if (op == head_op && !cont && nh != kNil) rows_at(an, nxt);  // a one-op chain: the next start's rows
+    if (op == head_op && nh != kNil) rows_at(an, nxt);  // the next chain's rows, in flight meanwhile
     {
       const uint4 f1 = rec[4 * (size_t)op + 1], f2 = rec[4 * (size_t)op + 2], f3 = rec[4 * (size_t)op + 3];
       const FoldIo fx{f3.x, f3.y, f3.z, std_domain, pc, nullptr, nullptr};
@@ -2527,8 +2527,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
     }
     dirty = 0;
     if (nh == kNil) break;
-    if (!cont) cur = nxt;
-    else rows_at(an, cur);  // (nothing was in flight)
+    cur = nxt;
     op = head_op = nh;
     cont = ncont;
     nh = nh2;
@@ -2579,8 +2578,19 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_tail_kernel(
     s_void = force_giveup && k == 1 ? 1u : 0u;
     s_bad = 0;
   }
+#if H3C_FAST_TRACE
+  uint64_t ftr[8];
+  FAST_MARK(0);
+#endif
   const uint32_t poly = pc->poly;
   const uint32_t j = k * kTailTile + t;
+  // the chunk table (threads c < 128), loaded first: its round trip overlaps the deltas'
+  h3c_chunk_state cs{};
+  uint32_t t0 = 0;
+  if (t < nchunks && t < kFastCols) {
+    cs = chunks[t];
+    t0 = fast_t0(cs, t, exact, std_domain, crc0, pc);
+  }
   // each op's delta moved to its chunk's end
   uint32_t c = kNil, v = 0, st = 0;
   if (j < n) {
@@ -2589,27 +2599,35 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_tail_kernel(
     st = (uint32_t)(g >> 32);
     if (st == 1) v = dgf_mul_fast((uint32_t)g, frag[j].mult, poly);
   }
-  // in the wave: each op's inclusive XOR of its chunk's deltas, the wave's per-chunk sums (lanes c, c + 64)
-  uint32_t acc0 = 0, acc1 = 0, ip = 0, app0 = 0, app1 = 0;
-  for (uint32_t u = 0; u < 64; ++u) {
-    const uint32_t cu = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)u);
-    const uint32_t vu = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)u);
-    const uint32_t oku = __builtin_amdgcn_readlane((int)st, (int)u) == 1 ? 1u : 0u;
-    if (lane >= u && c == cu) ip ^= vu;
-    if (cu == lane) {
-      acc0 ^= vu;
-      app0 |= oku;
-    }
-    if (cu == lane + 64) {
-      acc1 ^= vu;
-      app1 |= oku;
-    }
+  // in the wave: each op's inclusive XOR of its chunk's deltas (XOR is order-free: the lanes at or before
+  // this one with the same chunk, found with 8 ballots over the chunk index, usually one or two), and the
+  // wave's per-chunk sums in LDS
+  __shared__ uint32_t lv[kTailTile];
+  lv[t] = v;
+  uint64_t same = __builtin_amdgcn_ballot_w64(c != kNil);
+#pragma unroll
+  for (uint32_t b = 0; b < 8; ++b) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64((c >> b) & 1u);
+    same &= ((c >> b) & 1u) ? m : ~m;
   }
-  wagg[wave * kFastCols + lane] = acc0;
-  wagg[wave * kFastCols + 64 + lane] = acc1;
-  wapp[wave * kFastCols + lane] = app0;
-  wapp[wave * kFastCols + 64 + lane] = app1;
+  uint32_t ip = 0;
+  for (uint64_t m = same & (lane == 63 ? ~0ull : ((2ull << lane) - 1)); m; m &= m - 1)
+    ip ^= lv[(t & ~63u) + (uint32_t)__builtin_ctzll(m)];
+  // the wave's sum per chunk: the highest lane of each chunk holds it (ip over all its lanes)
+  const bool top = c != kNil && (same >> lane) <= 1;  // no higher lane with this chunk
+  const uint64_t okm = __builtin_amdgcn_ballot_w64(st == 1);
+  wagg[wave * kFastCols + lane] = 0;
+  wagg[wave * kFastCols + 64 + lane] = 0;
+  wapp[wave * kFastCols + lane] = 0;
+  wapp[wave * kFastCols + 64 + lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  if (top) {
+    wagg[wave * kFastCols + c] = ip;
+    wapp[wave * kFastCols + c] = (same & okm) ? 1u : 0u;
+  }
+  FAST_MARK(1);
   __syncthreads();
+  FAST_MARK(2);
   const bool two = nchunks > 64;
   if (wave == 0) {  // the tile's sums, published
     uint32_t a0 = 0, a1 = 0, p0 = 0, p1 = 0;
@@ -2662,18 +2680,13 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_tail_kernel(
     wlba[wave * kFastCols + 64 + lane] = q1;
   }
   __syncthreads();
+  FAST_MARK(3);
   if (wave < 2) {  // per chunk (thread c < 128): t0 ^ the earlier tiles' deltas; the last tile's final states
     const uint32_t cc = t;
     uint32_t e = 0, q = 0;
     for (uint32_t w = 0; w < NW; ++w) {
       e ^= wlb[w * kFastCols + cc];
       q |= wlba[w * kFastCols + cc];
-    }
-    h3c_chunk_state cs{};
-    uint32_t t0 = 0;
-    if (cc < nchunks) {
-      cs = chunks[cc];
-      t0 = fast_t0(cs, cc, exact, std_domain, crc0, pc);
     }
     wbase[cc] = t0 ^ e;
     wsz[cc] = cs.size;
@@ -2694,6 +2707,7 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_tail_kernel(
     }
   }
   __syncthreads();
+  FAST_MARK(4);
   // every op's result: t0 ^ its chunk's deltas up to it (earlier tiles, this tile's earlier waves, the wave)
   if (j < n) {
     uint32_t sv = wbase[c] ^ ip;
@@ -2714,6 +2728,14 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_tail_kernel(
     ctr_add_block(sh, ctr, v8);
   }
   __syncthreads();
+#if H3C_FAST_TRACE
+  FAST_MARK(5);
+  if (t == 0 && (k < 2 || k == ntiles / 2 || k + 1 == ntiles))
+    printf("tail tile %u start %llu deltas %llu summed %llu lookback %llu t0 %llu results %llu (ticks)\n", k,
+           (unsigned long long)ftr[0], (unsigned long long)(ftr[1] - ftr[0]), (unsigned long long)(ftr[2] - ftr[0]),
+           (unsigned long long)(ftr[3] - ftr[0]), (unsigned long long)(ftr[4] - ftr[0]),
+           (unsigned long long)(ftr[5] - ftr[0]));
+#endif
   if (t == 0) {
     if (s_void) atomicOr(&misc[kMiscFVoid], 1u);
     if (s_bad) atomicOr(&misc[kMiscErr], 1u);
@@ -3257,9 +3279,68 @@ hipStream_t capture_stream(int dev) {
 // and thread), so the lock costs nothing in steady state.
 std::mutex g_capture_mu;
 
+// The shape of a captured graph (h3c_diag_last_graph): node count, root count, memset + memcpy nodes,
+// kernel nodes, nodes reachable from the first root through edges, edges, the largest out-degree.
+struct GraphShape {
+  uint64_t nodes = 0, roots = 0, copies = 0, kernels = 0, reachable = 0, edges = 0, max_out = 0;
+};
+thread_local GraphShape t_last_graph;
+
+// The engine's pipelines are chains of kernel nodes on one stream.  A captured graph is instantiated
+// only if it is one: a single root, every node reachable from it, and no memset / memcpy node (round 3:
+// a hipMemsetAsync at the head of the captured UpdateIO pipeline became a memset node that replays did
+// not order before the prep kernel -- stale tickets, an illegal access; profiles/r04_graph_probe.txt
+// records what HIP captures for that form).  Anything else runs as plain launches (h3c_diag_counter 10).
+bool graph_is_a_chain(hipGraph_t g, GraphShape &sh) {
+  sh = GraphShape{};
+  size_t nn = 0, nr = 0, ne = 0;
+  if (hipGraphGetNodes(g, nullptr, &nn) != hipSuccess || hipGraphGetRootNodes(g, nullptr, &nr) != hipSuccess ||
+      hipGraphGetEdges(g, nullptr, nullptr, &ne) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  std::vector<hipGraphNode_t> nodes(nn), roots(nr), from(ne), to(ne);
+  if ((nn && hipGraphGetNodes(g, nodes.data(), &nn) != hipSuccess) ||
+      (nr && hipGraphGetRootNodes(g, roots.data(), &nr) != hipSuccess) ||
+      (ne && hipGraphGetEdges(g, from.data(), to.data(), &ne) != hipSuccess)) {
+    (void)hipGetLastError();
+    return false;
+  }
+  sh.nodes = nn;
+  sh.roots = nr;
+  sh.edges = ne;
+  for (hipGraphNode_t x : nodes) {
+    hipGraphNodeType ty = hipGraphNodeTypeCount;
+    if (hipGraphNodeGetType(x, &ty) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    sh.copies += ty == hipGraphNodeTypeMemset || ty == hipGraphNodeTypeMemcpy;
+    sh.kernels += ty == hipGraphNodeTypeKernel;
+  }
+  std::vector<hipGraphNode_t> seen, todo;
+  if (nr) todo.push_back(roots[0]);
+  while (!todo.empty()) {
+    const hipGraphNode_t x = todo.back();
+    todo.pop_back();
+    if (std::find(seen.begin(), seen.end(), x) != seen.end()) continue;
+    seen.push_back(x);
+    uint64_t out = 0;
+    for (size_t e = 0; e < ne; ++e)
+      if (from[e] == x) {
+        todo.push_back(to[e]);
+        ++out;
+      }
+    sh.max_out = std::max(sh.max_out, out);
+  }
+  sh.reachable = seen.size();
+  return nr == 1 && sh.copies == 0 && sh.reachable == nn;
+}
+
 template <class Body>
 int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out) {
   std::lock_guard<std::mutex> lk(g_capture_mu);
+  std::unique_lock<std::shared_mutex> gate(h3c_rt::capture_gate());  // (legacy-stream entries wait it out)
   // Relaxed: the capture makes no synchronous or allocating call itself, and it should not make
   // other threads' calls fail (under the thread-local mode a 16-thread stress saw another
   // thread's hipMemcpy fail; see upd_graphs for the legacy-stream limit that remains).
@@ -3275,6 +3356,13 @@ int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out) {
     if (g) (void)hipGraphDestroy(g);
     if (!r) h3c_rt::set_error("graph capture: hipStreamEndCapture", e);  // (else the body's error stays)
     return r ? r : H3C_ERR_HIP;
+  }
+  if (!graph_is_a_chain(g, t_last_graph)) {  // not instantiated: plain launches for this shape
+    (void)hipGraphDestroy(g);
+    g_graph_stats[kDiagTopology].fetch_add(1);
+    h3c_rt::set_error_text("graph capture: the captured pipeline is not one chain of kernel nodes");
+    out = nullptr;
+    return H3C_ERR_HIP;
   }
   const hipError_t ie = hipGraphInstantiate(&out, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
@@ -3904,6 +3992,14 @@ void counters_from(const unsigned long long *h, h3c_update_counters *c) {
 }
 
 }  // namespace
+
+extern "C" int h3c_diag_last_graph(uint64_t *out7) {
+  if (!out7) return H3C_ERR_INVALID_ARG;
+  const GraphShape &g = t_last_graph;
+  const uint64_t v[7] = {g.nodes, g.roots, g.copies, g.kernels, g.reachable, g.edges, g.max_out};
+  std::memcpy(out7, v, sizeof(v));
+  return H3C_OK;
+}
 
 extern "C" uint64_t h3c_diag_counter(int which) {
   return which >= 0 && which < kDiagN ? g_graph_stats[which].load() : 0;

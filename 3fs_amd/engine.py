@@ -89,6 +89,7 @@ _proto("h3c_update_blocks_ex", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, 
 _proto("h3c_test_hook", _int, _int, _u64)
 _proto("h3c_set_coalescing", _int, _int)
 _proto("h3c_diag_counter", _u64, _int)
+_proto("h3c_diag_last_graph", _int, _vp)
 _proto("h3c_diag_sync_bench", _int, _int, _u64, _int, _int, _vp, _vp)
 _proto("h3c_update_ios_dev", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp)
 _proto("h3c_serde_checksum_mark", _u32, _u32, _int)
@@ -366,6 +367,13 @@ DIAG_NAMES = ("graph_replays", "graph_captures", "graph_capture_failures", "redo
 def diag_counter(which: int) -> int:
     """h3c_diag_counter(which): see DIAG_NAMES (0 UpdateIO graph replays, 1 captures, ...)."""
     return int(lib.h3c_diag_counter(int(which)))
+
+
+def diag_last_graph() -> dict:
+    """h3c_diag_last_graph: the shape of the last UpdateIO graph this thread captured."""
+    out = (ctypes.c_uint64 * 7)()
+    _check(lib.h3c_diag_last_graph(ctypes.cast(out, ctypes.c_void_p)))
+    return dict(zip(("nodes", "roots", "copies", "kernels", "reachable", "edges", "max_out"), map(int, out)))
 
 
 def diag_counters() -> dict:

@@ -84,7 +84,11 @@ int h3c_crc32(const void *data, size_t n, uint32_t start_raw, uint32_t *out_raw,
  * folly's signature has no error channel: an engine failure (no device, a HIP error) prints
  * h3c_last_error() to stderr and aborts rather than return a wrong checksum.  Synchronous, on the
  * default stream; a call costs a GPU round trip, so per-IO host buffers belong on the CPU
- *  and this entry is for GPU-resident buffers at folly call sites. */
+ *  and this entry is for GPU-resident buffers at folly call sites.  Graph captures:
+ * HIP fails legacy-stream launches while any stream of the process captures; these entries (and every
+ * synchronous entry called with stream == NULL) wait while the engine itself captures an UpdateIO graph
+ * (H3C_UPD_GRAPHS), so they never abort on the engine's own captures.  A caller that captures graphs
+ * of its own must not call them meanwhile. */
 uint32_t h3c_folly_crc32c(const uint8_t *data, size_t nbytes, uint32_t startingChecksum);
 uint32_t h3c_folly_crc32(const uint8_t *data, size_t nbytes, uint32_t startingChecksum);
 
@@ -460,6 +464,11 @@ int h3c_test_hook(int key, uint64_t value);
  *   10 captured graphs refused by the topology check (a memset / memcpy node, or a kernel node not
  *      ordered after the graph's root) and run as plain launches instead. */
 uint64_t h3c_diag_counter(int which);
+/* The shape of the last graph this thread captured for h3c_update_ios (tests): out7 = {nodes, root
+ * nodes, memset + memcpy nodes, kernel nodes, nodes reachable from the first root, edges, the largest
+ * out-degree}.  A graph is instantiated only when it is one chain of kernel nodes (one root, every
+ * node reachable, no memset / memcpy node); else the shape runs as plain launches (counter 10). */
+int h3c_diag_last_graph(uint64_t *out7);
 
 #ifdef __cplusplus
 }

@@ -8,12 +8,16 @@
 //                                                      (src/storage/store/ChunkReplica.cc:131-394), batched
 //   BatchReadResults::setResults                       AioReadJob::setResult (src/storage/aio/BatchReadJob.cc:24-55)
 //   Checksum::calcSerde                                src/common/net/MessageHeader.h:32-37
+//   VersionGate                                        the version / state checks of ChunkReplica::update
+//                                                      (:171-247) and ChunkReplica::commit (:397-467), on
+//                                                      the host (no payload work: see INTEGRATION.md §1)
 //
 // Every payload byte is checksummed on the GPU; the classes hold no device state.
 #pragma once
 
 #include <cstddef>
 #include <cstdint>
+#include <optional>
 #include <vector>
 
 #include "h3c_checksum_info.hpp"
@@ -25,9 +29,17 @@ namespace h3c {
 enum StatusCode : uint32_t {
   kOK = 0,
   kInvalidArg = 3,
+  kChunkNotClean = 4005,
+  kChunkStaleUpdate = 4006,
+  kChunkMissingUpdate = 4007,
+  kChunkCommittedUpdate = 4008,
   kChunkReadFailed = 4010,
+  kChunkAdvanceUpdate = 4012,
   kChunkSizeMismatch = 4015,
+  kChunkStaleCommit = 4023,
   kChecksumMismatch = 4080,
+  kChainVersionMismatch = 4081,
+  kChunkVersionMismatch = 4082,
 };
 
 // UpdateType (Common.h:51-58).
@@ -43,7 +55,9 @@ struct UpdateIO {
   ChecksumInfo checksum;
   const uint8_t *data = nullptr;
   bool isSyncing = false;  // UpdateOptions.isSyncing (ChunkReplica.cc:211-215, 289): WRITE at offset 0
-  uint32_t chunkSize = 0;  // UpdateIO.chunkSize; 0: not carried (the chunk's own innerFileId.chunkSize is used)
+  // UpdateIO.chunkSize (H3C_IO_CHUNK_SIZE): the range check (:141-145) and the 4015 check (:171-180) use it;
+  // not carried: the chunk's own innerFileId.chunkSize stands in (a carried 0 fails as the reference's would)
+  std::optional<uint32_t> chunkSize;
 
   bool isWrite() const { return updateType == UpdateType::WRITE; }
   bool isRemove() const { return updateType == UpdateType::REMOVE; }
@@ -91,7 +105,7 @@ struct ChunkReplicaBatch {
                             ios[i].checksum.value, (uint8_t)ios[i].checksum.type, (uint8_t)ios[i].updateType,
                             (uint8_t)((ios[i].isSyncing ? H3C_IO_SYNCING : 0u) |
                                       (ios[i].chunkSize ? H3C_IO_CHUNK_SIZE : 0u)),
-                            0, ios[i].chunkSize};
+                            0, ios[i].chunkSize.value_or(0u)};
     std::vector<h3c_update_result> res(ios.size());
     const int rc = h3c_update_ios_ex((uint8_t)checksumType, cs.data(), (uint32_t)cs.size(), io.data(),
                                      (uint32_t)io.size(), res.data(), flags, counters, stream);
@@ -141,6 +155,101 @@ struct BatchReadResults {
     for (size_t i = 0; i < jobs.size(); ++i)
       results[i] = IOResult{st[i], jobs[i].length, ChecksumInfo{(ChecksumType)t[i], v[i]}, jobs[i].chunkLen};
     return H3C_OK;
+  }
+};
+
+// ChunkState (Common.h:60-64) and the version fields of ChunkMetadata (Common.h:662-676).
+enum class ChunkState : uint8_t { COMMIT = 0, DIRTY = 1, CLEAN = 2 };
+struct ChunkVersion {
+  uint32_t updateVer = 0, commitVer = 0, chainVer = 0;
+  ChunkState chunkState = ChunkState::CLEAN;
+};
+// One update or commit of a chunk as the gate sees it.
+struct VersionedOp {
+  uint32_t chunk = 0;           // index into the batch's chunk table
+  bool isCommit = false;        // ChunkReplica::commit (CommitIO) rather than ChunkReplica::update
+  uint32_t updateVer = 0;       // UpdateIO.updateVer (0: the next one) / CommitIO.commitVer
+  uint32_t commitChainVer = 0;  // job.commitChainVer()
+  bool isSyncing = false;       // UpdateOptions.isSyncing
+  bool isForce = false;         // CommitIO.isForce
+  bool checksumOk = true;       // the op's client-checksum verify passed (ChunkReplica.cc:193-207), if known
+};
+
+// The version / state gate that stays on the host.  ChunkReplica::update rejects an op
+// before touching its bytes when the chunk is DIRTY and the op is not syncing (4005, :181-185), when a
+// committed chunk's chain version is newer than the op's (4081, :186-191), and -- after the checksum
+// verify at :193-207 -- when updateVer is committed (4008), stale (4006), missing one (4007) or, for
+// updateVer 0, too far ahead (4012) (:211-239); a successful op sets updateVer and, at its end, a CLEAN
+// state and the op's chain version (:241-244, :298).  ChunkReplica::commit checks chain (4081) and commit
+// versions (4082), a DIRTY chunk (4005) and stale commits (4023) (:419-446) and marks a fully committed
+// chunk COMMIT (:448-451).  run() replays these in sequence order per chunk and returns each op's status
+// (0: admitted); `versions` end as the reference's metadata would.  The checksum verify sits between the
+// two groups of checks: an op with checksumOk == false fails with 4080 after the first group, as the
+// reference's does, and changes no version.  Ops admitted here go to h3c_update_ios; the others are
+// answered with their status and not submitted.
+struct VersionGate {
+  static void run(std::vector<ChunkVersion> &versions, const std::vector<VersionedOp> &ops,
+                  std::vector<uint32_t> &status) {
+    status.assign(ops.size(), kOK);
+    for (size_t i = 0; i < ops.size(); ++i) {
+      const VersionedOp &op = ops[i];
+      if (op.chunk >= versions.size()) {
+        status[i] = kInvalidArg;
+        continue;
+      }
+      ChunkVersion &m = versions[op.chunk];
+      if (op.isCommit) {  // ChunkReplica::commit (:419-451)
+        if (op.commitChainVer < m.chainVer) {
+          status[i] = kChainVersionMismatch;
+        } else if (op.updateVer > m.updateVer) {
+          status[i] = kChunkVersionMismatch;
+        } else if (op.isForce) {
+          m.chunkState = ChunkState::CLEAN;
+          m.commitVer = op.updateVer;
+        } else if (m.chunkState == ChunkState::DIRTY) {
+          status[i] = kChunkNotClean;
+        } else if (m.commitVer < op.updateVer) {
+          m.commitVer = op.updateVer;
+        } else {
+          status[i] = kChunkStaleCommit;
+        }
+        if (status[i] == kOK && m.commitVer == m.updateVer) {
+          m.chunkState = ChunkState::COMMIT;
+          m.chainVer = op.commitChainVer;
+        }
+        continue;
+      }
+      if (m.chunkState == ChunkState::DIRTY && !op.isSyncing) {  // :181-185
+        status[i] = kChunkNotClean;
+        continue;
+      }
+      if (op.commitChainVer < m.chainVer && m.chunkState == ChunkState::COMMIT) {  // :186-191
+        status[i] = kChainVersionMismatch;
+        continue;
+      }
+      if (!op.checksumOk) {  // :193-207 (the reference returns before any version change)
+        status[i] = kChecksumMismatch;
+        continue;
+      }
+      uint32_t uv = m.updateVer, cv = m.commitVer;
+      if (op.isSyncing) {  // :211-215
+        uv = op.updateVer;
+        cv = op.updateVer - 1;
+      } else if (op.updateVer > 0) {  // :216-232
+        if (op.updateVer <= m.commitVer) status[i] = kChunkCommittedUpdate;
+        else if (op.updateVer <= m.updateVer) status[i] = kChunkStaleUpdate;
+        else if (op.updateVer > m.updateVer + 1) status[i] = kChunkMissingUpdate;
+        else uv = op.updateVer;
+      } else {  // :233-239
+        uv = m.updateVer + 1;
+        if (uv > m.commitVer + 1) status[i] = kChunkAdvanceUpdate;
+      }
+      if (status[i] != kOK) continue;  // (the meta copy with the changed versions is never stored)
+      m.updateVer = uv;
+      m.commitVer = cv;
+      m.chainVer = op.commitChainVer;  // :241
+      m.chunkState = ChunkState::CLEAN;  // DIRTY during the write, CLEAN at :298
+    }
   }
 };
 

@@ -15,6 +15,7 @@
 //   serde                      Checksum::calcSerde (MessageHeader.h:32-37)
 //   data_iterator              ChecksumInfo::create over a DataIterator (Common.h:120-172):
 //                              1 MiB memory slices, ragged pieces, short / overlong iteration
+//   version_gate               VersionGate: ChunkReplica::update / commit's version and state checks
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -408,8 +409,66 @@ static void data_iterator(bool gpu) {
   (void)hipFree(dev);
 }
 
+// VersionGate: the version / state checks of ChunkReplica::update (:171-247) and ::commit (:397-467)
+// replayed on the host in sequence order, each case of the reference once, including
+// the cascade of a failed checksum verify (the chunk's updateVer stays, so the next op misses one).
+static void version_gate() {
+  std::vector<ChunkVersion> v(4);
+  v[1].chunkState = ChunkState::DIRTY;
+  v[2].chunkState = ChunkState::COMMIT;
+  v[2].chainVer = 7;
+  v[2].updateVer = v[2].commitVer = 5;
+  auto up = [](uint32_t c, uint32_t ver, uint32_t chain = 1, bool ok = true, bool sync = false) {
+    VersionedOp o;
+    o.chunk = c;
+    o.updateVer = ver;
+    o.commitChainVer = chain;
+    o.checksumOk = ok;
+    o.isSyncing = sync;
+    return o;
+  };
+  auto commit = [](uint32_t c, uint32_t ver, uint32_t chain = 1, bool force = false) {
+    VersionedOp o;
+    o.chunk = c;
+    o.isCommit = true;
+    o.updateVer = ver;
+    o.commitChainVer = chain;
+    o.isForce = force;
+    return o;
+  };
+  const std::vector<VersionedOp> ops = {
+      up(0, 1), up(0, 2), up(0, 2),              // admitted, admitted, stale (4006)
+      up(0, 4),                                  // missing one (4007)
+      up(0, 0),                                  // updateVer 0: 3 > commitVer 0 + 1 -> advance (4012)
+      commit(0, 2), up(0, 1),                    // commit 2; then 1 <= commitVer: committed (4008)
+      up(0, 3, 1, false), up(0, 4),              // checksum fails (4080, nothing changes); 4 misses 3 (4007)
+      up(0, 3),                                  // 3 admitted
+      up(1, 1),                                  // DIRTY and not syncing (4005)
+      up(1, 9, 1, true, true),                   // syncing on a DIRTY chunk: updateVer 9, commitVer 8
+      up(2, 6, 3),                               // COMMIT with a newer chain version than the op's (4081)
+      up(2, 6, 7),                               // same chain version: admitted
+      commit(2, 9, 7),                           // commit beyond updateVer (4082)
+      commit(2, 5, 7),                           // commit 5 <= commitVer 5: stale commit (4023)
+      commit(2, 6, 8),                           // commit 6 == updateVer: COMMIT, chainVer 8
+      up(9, 1),                                  // no such chunk (kInvalidArg)
+      up(3, 0), up(3, 0),                        // updateVer 0: 1 admitted, then 2 > 0 + 1 (4012)
+  };
+  const std::vector<uint32_t> want = {0, 0, 4006, 4007, 4012, 0, 4008, 4080, 4007, 0, 4005, 0, 4081, 0, 4082, 4023,
+                                      0, 3, 0, 4012};
+  std::vector<uint32_t> st;
+  VersionGate::run(v, ops, st);
+  CHECK(st == want);
+  for (size_t i = 0; i < st.size() && i < want.size(); ++i)
+    if (st[i] != want[i]) std::fprintf(stderr, "  op %zu: %u, want %u\n", i, st[i], want[i]);
+  CHECK(v[0].updateVer == 3 && v[0].commitVer == 2 && v[0].chunkState == ChunkState::CLEAN);
+  CHECK(v[1].updateVer == 9 && v[1].commitVer == 8 && v[1].chunkState == ChunkState::CLEAN);
+  CHECK(v[2].updateVer == 6 && v[2].commitVer == 6 && v[2].chunkState == ChunkState::COMMIT && v[2].chainVer == 8);
+  CHECK(v[3].updateVer == 1 && v[3].commitVer == 0);
+}
+
 int main(int argc, char **argv) {
   const bool gpu = argc > 1 && std::string(argv[1]) == "gpu";
+  version_gate();
   serde(false);
   data_iterator(gpu);
   if (gpu) {

@@ -348,3 +348,30 @@ def test_config3_shape_counts_no_redo(h3c, torch_dev, hooks):
     assert d["fast_batches"] == 1
     assert all(d[k] == 0 for k in ("redo_front_void", "rerun_phase_b_void", "redo_failed_a6",
                                    "redo_short_fragment_guess", "fast_abandoned", "fast_recovered")), d
+
+
+@pytest.mark.parametrize("fast", [False, True])
+def test_captured_pipeline_is_one_chain(h3c, torch_dev, hooks, fast):
+    """every captured UpdateIO pipeline is one chain of kernel nodes -- one root, every
+    node reachable from it through edges, no memset / memcpy node, no fork (h3c_diag_last_graph); the
+    engine refuses to instantiate anything else (h3c_diag_counter 10 stays 0 here)."""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_GRAPHS, 2)
+    hooks(h3c.HOOK_UPD_FAST, 2 if fast else 1)
+    rng = np.random.default_rng(31 + fast)
+    sc = fast_scenario(h3c, torch, dev, rng, nchunks=8, chunk_size=64 << 10, nops=3000, bad=0.0) if fast else \
+        random_scenario(h3c, torch, dev, rng, nchunks=8, chunk_size=64 << 10, nops=3000)
+    chunks, ios = sc.device_ios()
+    d_chunks = torch.from_numpy(chunks.view(np.uint8).copy()).to(dev)
+    d_ios = torch.from_numpy(ios.view(np.uint8).copy()).to(dev)
+    d_res = torch.zeros(len(ios) * 16, dtype=torch.uint8, device=dev)
+    b = h3c.diag_counters()
+    for _ in range(6):  # plain until the shape repeats on the same scratch leases, one capture, replays
+        h3c.update_ios_dev(d_chunks, d_ios, d_res, graphs=True)
+        torch.cuda.synchronize()
+    d = {k: v - b[k] for k, v in h3c.diag_counters().items()}
+    assert d["graph_captures"] >= 1 and d["graph_topology_refused"] == 0 and d["graph_replays"] >= 1, d
+    g = h3c.diag_last_graph()
+    assert g["copies"] == 0 and g["roots"] == 1 and g["reachable"] == g["nodes"] == g["kernels"], g
+    assert g["edges"] == g["nodes"] - 1 and g["max_out"] == 1, g
+    assert g["nodes"] >= (5 if fast else 8), g
