@@ -383,7 +383,7 @@ constexpr uint32_t kFusedCols = 128;    // chunk columns of the look-back: lane 
 constexpr uint32_t kFusedMaxWG = 1024;  // granule rows reserved in the workspace
 constexpr uint32_t kGranAgg = 1, kGranIncl = 2;
 constexpr uint32_t kSpinLimit = 1u << 22;  // bounded look-back spins (about a quarter second)
-enum { kCtlTicket = 0, kCtlErr = 1, kCtlTimeout = 2, kCtlWords = 64 };
+enum { kCtlTicket = 0, kCtlErr = 1, kCtlTimeout = 2, kCtlDone = 3, kCtlWords = 64 };
 typedef unsigned long long __attribute__((address_space(1))) gu64;
 
 __device__ __forceinline__ void gran_store(uint64_t *p, uint32_t state, uint32_t v) {
@@ -618,6 +618,13 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
     if (two && lane + 64 < nchunks) gran_store(row + 64 + lane, kGranIncl, x1 ^ a1);
     wexcl[lane] = x0;
     wexcl[64 + lane] = x1;
+    // every workgroup but the last counts itself done once its flag (if it gave up) is out: the last
+    // one reads the flag only after all the others' counts (look-back may have passed a workgroup's
+    // aggregate before that workgroup gave up and raised the flag)
+    if (L != nwg - 1 && lane == 0) {
+      __threadfence();
+      atomicAdd(&ctl[kCtlDone], 1u);
+    }
     if (L == nwg - 1) {  // the last workgroup: final checksums, counts
       const uint32_t t0 = x0 ^ a0, t1 = x1 ^ a1;
       uint32_t stale = 0;
@@ -632,6 +639,17 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
       for (int o = 32; o >= 1; o >>= 1) stale += __shfl_xor(stale, o, 64);
       if (lane == 0) {
         __threadfence();
+        // wait (bounded) for every other workgroup's done count; a count that never comes voids the batch
+        bool late = false;
+        for (uint32_t spins = 0;
+             __hip_atomic_load(&ctl[kCtlDone], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nwg - 1;) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > kSpinLimit) {
+            late = true;
+            break;
+          }
+        }
+        if (late) atomicExch(&ctl[kCtlTimeout], 1u);
         const uint32_t inv = __hip_atomic_load(&ctl[kCtlErr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // every workgroup's inclusive granule was read (directly or through a later one's) before
         // this: a workgroup that gave up had raised the flag first

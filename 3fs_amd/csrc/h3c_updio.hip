@@ -908,22 +908,9 @@ __device__ void fast_prep_tile(const FastArgs &fa, uint32_t i, uint32_t n, const
   bool q = false;
   if (i < n) {
     q = fast_op(io, cs, st, poly_type);
-    if (q) {
-      OpPos r{};
-      r.op = i;
-      r.status = H3C_OK;
-      r.nb = r.na = cs.size;
-      r.r0 = io.offset;
-      r.r1 = io.offset + io.length;
-      r.tk = kT_DELTA;
-      r.sk = kS_SET_T;
-      r.tb = r.ta = poly_type;
-      r.pf = kPosFold;
-      uint64_t k64;
-      uint32_t praw;
-      fa.frag[i] = make_frag(r, i, 0, io.chunk, cs, io, fa.pc, std_domain, false, k64, praw);
-      fa.key[i] = k64;
-      key = k64;
+    if (q) {  // (the fragment record itself is made by uio_fast_link_kernel)
+      key = ((unsigned long long)io.chunk << 36) | ((cs.base + io.offset) >> 12);  // make_frag's key
+      fa.key[i] = key;
     }
     fa.dv[i] = 0;
   }
@@ -2364,11 +2351,33 @@ __device__ __forceinline__ uint32_t fast_cross_next(const uint4 *__restrict__ li
 // earlier tile) and the block's next op (in its tile, else the first in the next tile that has one).
 // One thread per op, between the prep kernel and uio_fast_kernel: the bucket walks' dependent loads run
 // here, all at once, instead of in front of uio_fast_kernel's first row loads and between a chain's ops.
+// It also makes op j's fragment record (make_frag: the op's one block), whose table lookups and GF(2)
+// multiplies overlap the walks' round trips.
 __global__ void uio_fast_link_kernel(const uint4 *__restrict__ link, const unsigned long long *__restrict__ keys,
                                      const uint32_t *__restrict__ bhead, uint32_t hmask, uint32_t n,
-                                     const uint32_t *__restrict__ misc, uint2 *__restrict__ chain) {
+                                     const uint32_t *__restrict__ misc, uint2 *__restrict__ chain,
+                                     const h3c_update_io *__restrict__ ios, const h3c_chunk_state *__restrict__ chunks,
+                                     uint8_t poly_type, uint32_t std_domain, const PolyConsts *__restrict__ pc,
+                                     FragDesc *__restrict__ frag) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n || misc[kMiscSlow]) return;  // (an abandoned batch: uio_fast_kernel returns at once)
+  {
+    const h3c_update_io io = ios[j];
+    const h3c_chunk_state cs = chunks[io.chunk];
+    OpPos r{};
+    r.op = j;
+    r.status = H3C_OK;
+    r.nb = r.na = cs.size;
+    r.r0 = io.offset;
+    r.r1 = io.offset + io.length;
+    r.tk = kT_DELTA;
+    r.sk = kS_SET_T;
+    r.tb = r.ta = poly_type;
+    r.pf = kPosFold;
+    uint64_t k64;
+    uint32_t praw;
+    frag[j] = make_frag(r, j, 0, io.chunk, cs, io, pc, std_domain, false, k64, praw);
+  }
   const uint4 lk = link[j];
   const unsigned long long key = keys[j];
   const bool start = lk.x == kNil && !fast_listed_before(link, keys, bhead, hmask, key, j);
@@ -2481,12 +2490,18 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
   bool cont = false, ncont = false, ncont2 = false;
   Addr an{}, an2{};
   if (lo < hi) {
+    // speculation: the range's first op starts its chain (~95 % on random writes), so its rows load
+    // before the chain starts are known; if it does not, the first start's rows load afterwards
+    Addr a0;
+    addr_of(lo, a0);
+    rows_at(a0, cur);
     hm = starts(lo, cm);
     op = next_start(g0, hm, cm, cont);
     if (op != kNil) {
-      Addr a0;
-      addr_of(op, a0);
-      rows_at(a0, cur);
+      if (op != lo) {
+        addr_of(op, a0);
+        rows_at(a0, cur);
+      }
       nh = next_start(g0, hm, cm, ncont);
       if (nh != kNil) {
         addr_of(nh, an);
@@ -3553,8 +3568,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                          0u, nullptr, 0u);
       HIP_TRY(hipGetLastError());
     }
-    // serial: one tile per 256 items (the initialisations beyond them grid-stride), so only the
-    // tiles that count toward the last-tile test run
+    // serial: one tile per kPrepTile items (the initialisations beyond them grid-stride), so only
+    // the tiles that count toward the last-tile test run
     const uint32_t ptiles = serial ? (uint32_t)(((size_t)n + C + 1 + kPrepTile - 1) / kPrepTile) : prep_tiles;
     hipLaunchKernelGGL(uio_prep_kernel, dim3(ptiles), dim3(kPrepTile), 0, q, d_ios, n, d_chunks, nchunks,
                        poly_type, stdf, exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc, d_a6,
@@ -3648,7 +3663,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         if (r) return r;
       }
       hipLaunchKernelGGL(uio_fast_link_kernel, dim3((n + 255) / 256), dim3(256), 0, q, fa.link, fa.key, fa.head,
-                         fa.hmask, n, d_misc, fa.chain);
+                         fa.hmask, n, d_misc, fa.chain, d_ios, d_chunks, poly_type, stdf, pc, fa.frag);
       HIP_TRY(hipGetLastError());
       return H3C_OK;
     };

@@ -483,6 +483,18 @@ def run_updio(args, cx: Ctx) -> dict:
         h3c.update_ios(state, ios, stream=cx.stream, out=hres, exact=exact, counters=hctr, graphs=True)
 
     helapsed, _ = cx.timed(hstep, hsteps, min(args.warmup, 2), h3c.engine.PROF_UPDIO)
+
+    # the device-table step again with plain launches (graphs=False): what a caller that does not
+    # opt into H3C_UPD_GRAPHS gets
+    d_state.copy_(torch.from_numpy(state.view(np.uint8).copy()).to(cx.dev))
+
+    def pstep():
+        h3c.update_ios_dev(d_state, d_ios, d_res, stream=cx.stream, exact=exact, counters=d_ctr, graphs=False)
+
+    pelapsed, _ = cx.timed(pstep, hsteps, min(args.warmup, 2), h3c.engine.PROF_UPDIO)
+    torch.cuda.synchronize()
+    state["value"] = d_state.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)["value"]
+    ok = ok and bool((d_res.cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)["status"] == 0).all())
     plan.run(fresh, stream=cx.stream)
     torch.cuda.synchronize()
     ok = ok and bool((hres["status"] == 0).all()) and np.array_equal(fresh.cpu().numpy().view(np.uint32),
@@ -516,6 +528,9 @@ def run_updio(args, cx: Ctx) -> dict:
         "pcie_inclusive": {"entry": "h3c_update_ios_ex (host tables in pinned memory)",
                            "value": round(nw * hsteps * cx.world / helapsed, 1), "unit": "writes/s",
                            "ms_per_step": round(helapsed / hsteps * 1e3, 4), "steps": hsteps},
+        "graphs_off": {"entry": "h3c_update_ios_dev, graphs=False (plain launches)",
+                       "value": round(nw * hsteps * cx.world / pelapsed, 1), "unit": "writes/s",
+                       "ms_per_step": round(pelapsed / hsteps * 1e3, 4), "steps": hsteps},
         "roofline": rl,
     }
     if cx.world == 1 and not args.no_cpu_baseline:
