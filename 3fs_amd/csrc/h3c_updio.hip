@@ -42,6 +42,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -291,7 +292,9 @@ struct FastArgs {
   unsigned long long *dv;   // per op: {state << 32 | delta CRC} (state 1: applied, 2: failed A6)
   uint32_t *slow;           // set when some op is not one this branch takes (misc[kMiscSlow])
   const PolyConsts *pc;
-  uint2 *chain;             // per op (uio_fast_link_kernel): {starts its block's chain, the block's next op}
+  uint4 *chain;             // per op (uio_fast_link_kernel): {bit 31: starts its block's chain, bits 0-25: the
+                            //  next op's new bytes w0 | w1 << 13; the block's next op; the next op's payload
+                            //  address at block offset 0 (lo, hi)}
 };
 __device__ void fast_prep_tile(const FastArgs &fa, uint32_t i, uint32_t n, const h3c_update_io &io,
                                const h3c_chunk_state &cs, uint32_t st, uint8_t poly_type, uint32_t std_domain);
@@ -2355,7 +2358,7 @@ __device__ __forceinline__ uint32_t fast_cross_next(const uint4 *__restrict__ li
 // multiplies overlap the walks' round trips.
 __global__ void uio_fast_link_kernel(const uint4 *__restrict__ link, const unsigned long long *__restrict__ keys,
                                      const uint32_t *__restrict__ bhead, uint32_t hmask, uint32_t n,
-                                     const uint32_t *__restrict__ misc, uint2 *__restrict__ chain,
+                                     const uint32_t *__restrict__ misc, uint4 *__restrict__ chain,
                                      const h3c_update_io *__restrict__ ios, const h3c_chunk_state *__restrict__ chunks,
                                      uint8_t poly_type, uint32_t std_domain, const PolyConsts *__restrict__ pc,
                                      FragDesc *__restrict__ frag) {
@@ -2382,7 +2385,19 @@ __global__ void uio_fast_link_kernel(const uint4 *__restrict__ link, const unsig
   const unsigned long long key = keys[j];
   const bool start = lk.x == kNil && !fast_listed_before(link, keys, bhead, hmask, key, j);
   const uint32_t next = lk.y != kNil ? lk.y : fast_cross_next(link, keys, bhead, hmask, key, j);
-  chain[j] = make_uint2(start ? 1u : 0u, next);
+  uint4 e = make_uint4(start ? 1u << 31 : 0u, next, 0u, 0u);
+  if (next != kNil) {  // the next op's payload rows (its record is another thread's, being written now)
+    const h3c_update_io nio = ios[next];
+    const h3c_chunk_state cs = chunks[nio.chunk];
+    const uint64_t blk = (cs.base + nio.offset) & ~(uint64_t)(kBlk - 1);
+    const int64_t rel = (int64_t)blk - (int64_t)cs.base;
+    const uint64_t src = nio.payload + (uint64_t)rel - (uint64_t)nio.offset;
+    const uint32_t w0 = rel_clamp(nio.offset, rel), w1 = rel_clamp((int64_t)nio.offset + nio.length, rel);
+    e.x |= w0 | (w1 << 13);
+    e.z = (uint32_t)src;
+    e.w = (uint32_t)(src >> 32);
+  }
+  chain[j] = e;
 }
 
 struct FastSink {  // apply_fragment's results on the fast branch: dv[op] = {1, unshifted delta} or {2, 0}
@@ -2407,6 +2422,9 @@ __device__ unsigned int g_ftr[130] = {};
 #define FAST_MARK(i) ((void)0)
 #endif
 constexpr uint32_t kFastCols = 128;  // chunks a fast-branch batch may name (lane c: chunks c, c + 64)
+#ifndef H3C_FAST_GRAB
+#define H3C_FAST_GRAB 1  // 1: a workgroup's waves take their chain starts from an LDS counter (0: static ranges)
+#endif
 constexpr uint32_t kFastSpin = 1u << 21;
 constexpr unsigned long long kGranApplied = 4ull << 32;  // look-back granule bit: some op of the chunk applied
 
@@ -2422,7 +2440,7 @@ __device__ __forceinline__ uint32_t fast_t0(const h3c_chunk_state &cs, uint32_t 
 __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint32_t std_domain,
                                                              const PolyConsts *__restrict__ pc,
                                                              const FragDesc *__restrict__ frag,
-                                                             const uint2 *__restrict__ chain, unsigned long long *dv,
+                                                             const uint4 *__restrict__ chain, unsigned long long *dv,
                                                              const uint32_t *__restrict__ misc, unsigned long long *ts) {
   __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
   const uint32_t t = threadIdx.x, lane = t & 63;
@@ -2447,8 +2465,8 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
     const uint32_t j = g0 + lane;
     bool hd = false, cn = false;
     if (j < hi) {
-      const uint2 ch = chain[j];
-      hd = (H3C_FX & 64) ? true : ch.x != 0;  // (FX 64: timing experiment, every op its own chain: wrong results)
+      const uint4 ch = chain[j];
+      hd = (H3C_FX & 64) ? true : (ch.x >> 31) != 0;  // (FX 64: timing experiment, every op its own chain: wrong results)
       cn = hd && ch.y != kNil && !(H3C_FX & 64);
     }
     cm = __builtin_amdgcn_ballot_w64(cn);
@@ -2489,6 +2507,59 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
   uint64_t hm = 0, cm = 0;
   bool cont = false, ncont = false, ncont2 = false;
   Addr an{}, an2{};
+#if H3C_FAST_GRAB
+  // Dynamic: a chain's later ops run on the wave of its start, so static ranges leave waves with a few
+  // chains more than others finishing last.  The workgroup's ops [wlo, whi) are handed out one at a
+  // time by an LDS counter (a wave skips the ops that do not start a chain); each wave's first op is
+  // wlo + wave, whose rows load (speculatively: ~95 % start a chain) before the table fill.
+  __shared__ uint32_t s_grab;
+  (void)next_start, (void)g0, (void)hm, (void)cm;  // (the static form's)
+  const uint32_t wlo = (uint32_t)((uint64_t)blockIdx.x * kBlkWaves * n / nw);
+  const uint32_t whi = (uint32_t)((uint64_t)(blockIdx.x + 1) * kBlkWaves * n / nw);
+  const uint32_t first = wlo + wave;
+  if (first < whi) {
+    Addr a0;
+    addr_of(first, a0);
+    rows_at(a0, cur);
+  }
+  if (t == 0) s_grab = wlo + kBlkWaves;
+  auto is_start = [&](uint32_t j, bool &cn) -> bool {
+    const uint4 ch = chain[j];
+    cn = ch.y != kNil;
+    return (ch.x >> 31) != 0;
+  };
+  auto grab = [&](bool &cn) -> uint32_t {
+    for (;;) {
+      uint32_t j = 0;
+      if (lane == 0) j = atomicAdd(&s_grab, 1u);
+      j = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
+      if (j >= whi) return kNil;
+      if (is_start(j, cn)) return j;
+    }
+  };
+  FAST_MARK(1);
+  fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
+  __syncthreads();
+  FAST_MARK(2);
+  if (first < whi && is_start(first, cont)) {
+    op = first;
+  } else {
+    op = grab(cont);
+    if (op != kNil) {
+      Addr a0;
+      addr_of(op, a0);
+      rows_at(a0, cur);
+    }
+  }
+  if (op != kNil) {
+    nh = grab(ncont);
+    if (nh != kNil) {
+      addr_of(nh, an);
+      nh2 = grab(ncont2);
+      if (nh2 != kNil) addr_of(nh2, an2);
+    }
+  }
+#else
   if (lo < hi) {
     // speculation: the range's first op starts its chain (~95 % on random writes), so its rows load
     // before the chain starts are known; if it does not, the first start's rows load afterwards
@@ -2514,21 +2585,24 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
   fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
   __syncthreads();
   FAST_MARK(2);
+#endif
   uint32_t head_op = op, dirty = 0;
   while (op != kNil) {
     if (op == head_op && nh != kNil) rows_at(an, nxt);  // the next chain's rows, in flight meanwhile
+    uint4 cx = make_uint4(0u, kNil, 0u, 0u);
+    if (cont) cx = chain[op];  // the block's next op and its payload address: the load overlaps the apply
     {
       const uint4 f1 = rec[4 * (size_t)op + 1], f2 = rec[4 * (size_t)op + 2], f3 = rec[4 * (size_t)op + 3];
       const FoldIo fx{f3.x, f3.y, f3.z, std_domain, pc, nullptr, nullptr};
       dirty |= apply_fragment(cur.img, cur.nw, f2.w, f1.z, f1.w, f2.x, f2.z, f1.x, lane, lb, Lt, red, fx, sink);
     }
     if (cont) {  // the block's next op
-      const uint32_t nx = (uint32_t)__builtin_amdgcn_readfirstlane((int)chain[op].y);
+      const uint32_t nx = cx.y;
       if (nx != kNil) {
-        const uint4 b0 = rec[4 * (size_t)nx], b1 = rec[4 * (size_t)nx + 1];
-        const uint64_t src = (uint64_t)b0.z | ((uint64_t)b0.w << 32);
+        const uint64_t src = (uint64_t)cx.z | ((uint64_t)cx.w << 32);
+        const uint32_t w0 = cx.x & 0x1FFFu, w1 = (cx.x >> 13) & 0x1FFFu;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cur.nw[r] = load_new(src, r, 1024u * r + 16u * lane, b1.z & 0xFFFFu, b1.z >> 16);
+        for (int r = 0; r < 4; ++r) cur.nw[r] = load_new(src, r, 1024u * r + 16u * lane, w0, w1);
         op = nx;
         continue;
       }
@@ -2550,7 +2624,11 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
     ncont = ncont2;
     nh2 = kNil;
     if (nh != kNil) {  // the addresses two chains ahead
+#if H3C_FAST_GRAB
+      nh2 = grab(ncont2);
+#else
       nh2 = next_start(g0, hm, cm, ncont2);
+#endif
       if (nh2 != kNil) addr_of(nh2, an2);
     }
   }
@@ -2567,6 +2645,16 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
   }
 }
 
+// The outcome words into the caller's pinned host buffer, the fast-branch word last: the host polls
+// it (update_core) and reads the others once it is set.
+__device__ __forceinline__ void fast_outcome_to_host(const uint32_t *misc, uint32_t *hout, uint32_t fs) {
+#pragma unroll
+  for (uint32_t w = kMiscOutF; w < kMiscN; ++w)
+    if (w != kMiscFast) hout[w - kMiscOutF] = ld_agent(&misc[w]);
+  __threadfence_system();
+  __hip_atomic_store(&hout[kMiscFast - kMiscOutF], fs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The per-chunk XOR of the deltas in sequence order, every op's result, the chunks' final states, the
 // counters and the outcome words (see above); tile k = ops [1024 k, 1024 k + 1024).
 constexpr uint32_t kTailTile = 1024;
@@ -2575,16 +2663,16 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_tail_kernel(
     uint8_t poly_type, uint32_t std_domain, uint32_t exact, const uint32_t *__restrict__ crc0,
     const PolyConsts *__restrict__ pc, const FragDesc *__restrict__ frag, const unsigned long long *__restrict__ keys,
     const unsigned long long *__restrict__ dv, uint32_t *misc, unsigned long long *gran,
-    h3c_update_result *__restrict__ res, unsigned long long *__restrict__ ctr, uint32_t *hout, uint32_t force_giveup) {
+    h3c_update_result *__restrict__ res, unsigned long long *__restrict__ ctr, uint32_t *hout, uint32_t force_giveup,
+    h3c_chunk_state *commit) {
   constexpr uint32_t NW = kTailTile / 64, kWC = NW * kFastCols;
   __shared__ uint32_t wagg[kWC], wapp[kWC], wlb[kWC], wlba[kWC], wbase[kFastCols], wsz[kFastCols];
-  __shared__ uint32_t s_void, s_bad;
+  __shared__ uint32_t s_void, s_bad, s_last;
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, k = blockIdx.x, ntiles = gridDim.x;
   if (misc[kMiscSlow]) {  // not a fast-branch batch: nothing was done; the outcome says so
     if (k == 0 && t == 0) {
       misc[kMiscFast] = kFastAbort;
-      if (hout)
-        for (uint32_t w = kMiscOutF; w < kMiscN; ++w) hout[w - kMiscOutF] = misc[w];
+      if (hout) fast_outcome_to_host(misc, hout, kFastAbort);
     }
     return;
   }
@@ -2716,10 +2804,17 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_tail_kernel(
         f.value = std_domain ? ~(t0 ^ a) : (t0 ^ a);
         f.type = poly_type;
       }
-      chunks_out[cc] = f;
+      // write-through: the last tile to finish reads them back to commit them
+      static_assert(sizeof(h3c_chunk_state) % 8 == 0, "chunk state in 8-byte words");
+      unsigned long long fw[sizeof(h3c_chunk_state) / 8];
+      __builtin_memcpy(fw, &f, sizeof f);
+      unsigned long long *o = reinterpret_cast<unsigned long long *>(chunks_out + cc);
+#pragma unroll
+      for (uint32_t w = 0; w < sizeof(h3c_chunk_state) / 8; ++w) st_agent(&o[w], fw[w]);
       if (exact && cs.size && cs.type == poly_type && t0 != (std_domain ? ~cs.value : cs.value))
         atomicAdd(&ctr[kCtrStale], 1ull);
     }
+    stores_done();  // (waves 0 and 1: the final states at the coherence point before the done count)
   }
   __syncthreads();
   FAST_MARK(4);
@@ -2755,12 +2850,201 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_tail_kernel(
     if (s_void) atomicOr(&misc[kMiscFVoid], 1u);
     if (s_bad) atomicOr(&misc[kMiscErr], 1u);
     stores_done();
-    if (atomicAdd(&misc[kMiscFDone], 1u) + 1 == ntiles) {  // the last to finish: the outcome words
-      st_agent(&misc[kMiscFast], ld_agent(&misc[kMiscFVoid]) ? (uint32_t)kFastVoid : (uint32_t)kFastDone);
-      if (hout)
+    s_last = atomicAdd(&misc[kMiscFDone], 1u) + 1 == ntiles;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the last tile to finish: every tile has read the input table, so a complete pass commits the final
+  // states in place (the device-table entry; uio_commit_kernel's work), then the outcome words
+  const uint32_t fs = ld_agent(&misc[kMiscFVoid]) ? (uint32_t)kFastVoid : (uint32_t)kFastDone;
+  const bool ok = fs == kFastDone && !ld_agent(&misc[kMiscErr]);
+  if (commit && ok && t < nchunks) {
+    const unsigned long long *in = reinterpret_cast<const unsigned long long *>(chunks_out + t);
+    unsigned long long *o = reinterpret_cast<unsigned long long *>(commit + t);
 #pragma unroll
-        for (uint32_t w = kMiscOutF; w < kMiscN; ++w) hout[w - kMiscOutF] = ld_agent(&misc[w]);
+    for (uint32_t w = 0; w < sizeof(h3c_chunk_state) / 8; ++w) o[w] = ld_agent(&in[w]);
+  }
+  if (t == 0) {
+    st_agent(&misc[kMiscFast], fs);
+    if (hout) fast_outcome_to_host(misc, hout, fs);
+  }
+}
+
+// The tail in two launches with no waiting (H3C_FAST_TAIL2, the default): uio_fast_sum_kernel writes each
+// tile's per-chunk sums (one row of gran per tile) and each op's XOR within its tile; uio_fast_res_kernel
+// reads, per tile, the rows of the tiles before it -- complete at the launch boundary -- and writes the
+// results; its last tile the final states, its last to finish the commit and the outcome words.  (The
+// one-launch form chained the tiles by look-back: ~27 us, most of it waiting on late-starting tiles.)
+#ifndef H3C_FAST_TAIL2
+#define H3C_FAST_TAIL2 1
+#endif
+__global__ __launch_bounds__(kTailTile) void uio_fast_sum_kernel(uint32_t n, const PolyConsts *__restrict__ pc,
+                                                                const FragDesc *__restrict__ frag,
+                                                                const unsigned long long *__restrict__ keys,
+                                                                const unsigned long long *__restrict__ dv,
+                                                                const uint32_t *__restrict__ misc,
+                                                                unsigned long long *__restrict__ gran,
+                                                                uint2 *__restrict__ part, uint32_t *merr) {
+  constexpr uint32_t NW = kTailTile / 64;
+  __shared__ uint32_t wagg[NW * kFastCols], wapp[NW * kFastCols], lv[kTailTile];
+  __shared__ uint32_t s_bad;
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, k = blockIdx.x;
+  if (misc[kMiscSlow]) return;
+  if (t == 0) s_bad = 0;
+  const uint32_t poly = pc->poly;
+  const uint32_t j = k * kTailTile + t;
+  uint32_t c = kNil, v = 0, st = 0;
+  if (j < n) {  // each op's delta moved to its chunk's end
+    c = (uint32_t)(keys[j] >> 36);
+    const unsigned long long g = dv[j];
+    st = (uint32_t)(g >> 32);
+    if (st == 1) v = dgf_mul_fast((uint32_t)g, frag[j].mult, poly);
+    if (st != 1 && st != 2) s_bad = 1;  // an op with no delta: cannot happen after a complete uio_fast_kernel
+  }
+  // in the wave: each op's inclusive XOR of its chunk's deltas (lanes at or before this one with the
+  // same chunk, from 8 ballots over the chunk index); the wave's per-chunk sums into LDS
+  lv[t] = v;
+  uint64_t same = __builtin_amdgcn_ballot_w64(c != kNil);
+#pragma unroll
+  for (uint32_t b = 0; b < 8; ++b) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64((c >> b) & 1u);
+    same &= ((c >> b) & 1u) ? m : ~m;
+  }
+  uint32_t ip = 0;
+  for (uint64_t m = same & (lane == 63 ? ~0ull : ((2ull << lane) - 1)); m; m &= m - 1)
+    ip ^= lv[(t & ~63u) + (uint32_t)__builtin_ctzll(m)];
+  const bool top = c != kNil && (same >> lane) <= 1;  // no higher lane with this chunk
+  const uint64_t okm = __builtin_amdgcn_ballot_w64(st == 1);
+  wagg[wave * kFastCols + lane] = 0;
+  wagg[wave * kFastCols + 64 + lane] = 0;
+  wapp[wave * kFastCols + lane] = 0;
+  wapp[wave * kFastCols + 64 + lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  if (top) {
+    wagg[wave * kFastCols + c] = ip;
+    wapp[wave * kFastCols + c] = (same & okm) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (t < kFastCols) {  // the tile's row: per chunk {some op applied, XOR of the deltas}
+    uint32_t a = 0, p = 0;
+    for (uint32_t w = 0; w < NW; ++w) {
+      a ^= wagg[w * kFastCols + t];
+      p |= wapp[w * kFastCols + t];
     }
+    gran[(uint64_t)k * kFastCols + t] = (p ? kGranApplied : 0ull) | a;
+  }
+  if (j < n) {  // the op's XOR within the tile (earlier waves' sums of its chunk, then the wave's)
+    uint32_t sv = ip;
+    for (uint32_t w = 0; w < wave; ++w) sv ^= wagg[w * kFastCols + c];
+    part[j] = make_uint2(sv, c | (st << 8));
+  }
+  if (t == 0 && s_bad) atomicOr(merr, 1u);
+}
+
+__global__ __launch_bounds__(kTailTile) void uio_fast_res_kernel(
+    const h3c_chunk_state *__restrict__ chunks, h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks, uint32_t n,
+    uint8_t poly_type, uint32_t std_domain, uint32_t exact, const uint32_t *__restrict__ crc0,
+    const PolyConsts *__restrict__ pc, const unsigned long long *__restrict__ gran, const uint2 *__restrict__ part,
+    uint32_t *misc, h3c_update_result *__restrict__ res, unsigned long long *__restrict__ ctr, uint32_t *hout,
+    uint32_t force_giveup, h3c_chunk_state *commit) {
+  constexpr uint32_t NR = kTailTile / kFastCols;  // row groups read in parallel (thread t: column t % 128)
+  __shared__ uint32_t px[NR * kFastCols], pq[NR * kFastCols], wbase[kFastCols], wsz[kFastCols];
+  __shared__ uint32_t s_last;
+  const uint32_t t = threadIdx.x, k = blockIdx.x, ntiles = gridDim.x;
+  if (misc[kMiscSlow]) {  // not a fast-branch batch: nothing was done; the outcome says so
+    if (k == 0 && t == 0) {
+      misc[kMiscFast] = kFastAbort;
+      if (hout) fast_outcome_to_host(misc, hout, kFastAbort);
+    }
+    return;
+  }
+  const uint32_t j = k * kTailTile + t;
+  uint2 pj = make_uint2(0u, 0u);
+  if (j < n) pj = part[j];  // (its round trip overlaps the rows')
+  h3c_chunk_state cs{};
+  uint32_t t0 = 0;
+  if (t < nchunks && t < kFastCols) {
+    cs = chunks[t];
+    t0 = fast_t0(cs, t, exact, std_domain, crc0, pc);
+  }
+  {  // the earlier tiles' rows: column t % 128, rows t / 128 + NR i (all loads in flight at once)
+    const uint32_t col = t % kFastCols, r0 = t / kFastCols;
+    uint32_t x = 0, q = 0;
+    for (uint32_t r = r0; r < k; r += NR) {
+      const unsigned long long g = gran[(uint64_t)r * kFastCols + col];
+      x ^= (uint32_t)g;
+      q |= (g & kGranApplied) ? 1u : 0u;
+    }
+    px[r0 * kFastCols + col] = x;
+    pq[r0 * kFastCols + col] = q;
+  }
+  __syncthreads();
+  if (t < kFastCols) {
+    uint32_t e = 0, q = 0;
+    for (uint32_t r = 0; r < NR; ++r) {
+      e ^= px[r * kFastCols + t];
+      q |= pq[r * kFastCols + t];
+    }
+    wbase[t] = t0 ^ e;
+    wsz[t] = cs.size;
+    if (k + 1 == ntiles && t < nchunks) {  // the final states: the earlier tiles, then this tile's own row
+      const unsigned long long own = gran[(uint64_t)k * kFastCols + t];
+      const uint32_t a = e ^ (uint32_t)own;
+      const bool p = q || (own & kGranApplied);
+      h3c_chunk_state f = cs;
+      if (p) {  // (a chunk whose ops all failed A6 keeps its stored value)
+        f.value = std_domain ? ~(t0 ^ a) : (t0 ^ a);
+        f.type = poly_type;
+      }
+      unsigned long long fw[sizeof(h3c_chunk_state) / 8];
+      __builtin_memcpy(fw, &f, sizeof f);
+      unsigned long long *o = reinterpret_cast<unsigned long long *>(chunks_out + t);
+#pragma unroll
+      for (uint32_t w = 0; w < sizeof(h3c_chunk_state) / 8; ++w) st_agent(&o[w], fw[w]);
+      if (exact && cs.size && cs.type == poly_type && t0 != (std_domain ? ~cs.value : cs.value))
+        atomicAdd(&ctr[kCtrStale], 1ull);
+      stores_done();
+    }
+  }
+  __syncthreads();
+  const uint32_t c = pj.y & 0xFFu, st = pj.y >> 8;
+  if (j < n) {  // every op's result: t0 ^ its chunk's deltas up to it
+    const uint32_t sv = wbase[c] ^ pj.x;
+    h3c_update_result o{};
+    o.status = st == 1 ? H3C_OK : H3C_ERR_CHECKSUM_MISMATCH;
+    o.size = wsz[c];
+    o.type = poly_type;  // (a failed op reports the stored type: the batch polynomial here)
+    o.value = st == 1 ? (std_domain ? ~sv : sv) : (std_domain ? 0u : sv);  // engine.rs:303 / ChunkReplica.cc:174
+    res[j] = o;
+  }
+  {
+    uint32_t v8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    v8[std_domain ? kCtrRecalc : kCtrRead] = j < n && st == 1;  // updateChecksum (iv) (:389) / copy_on_write (chunk.rs:153)
+    v8[kCtrMismatch] = j < n && st == 2;
+    __shared__ unsigned int sh[8];
+    ctr_add_block(sh, ctr, v8);
+  }
+  __syncthreads();
+  if (t == 0) {
+    // test hook (H3C_HOOK_UPD_GIVEUP bit 2): tile 1 reports the pass void, as the look-back form's
+    // starved tile did, so that uio_fast_recover_kernel stays covered
+    if (force_giveup && k == 1) atomicOr(&misc[kMiscFVoid], 1u);
+    stores_done();
+    s_last = atomicAdd(&misc[kMiscFDone], 1u) + 1 == ntiles;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const uint32_t fs = ld_agent(&misc[kMiscFVoid]) ? (uint32_t)kFastVoid : (uint32_t)kFastDone;
+  const bool ok = fs == kFastDone && !ld_agent(&misc[kMiscErr]);
+  if (commit && ok && t < nchunks) {
+    const unsigned long long *in = reinterpret_cast<const unsigned long long *>(chunks_out + t);
+    unsigned long long *o = reinterpret_cast<unsigned long long *>(commit + t);
+#pragma unroll
+    for (uint32_t w = 0; w < sizeof(h3c_chunk_state) / 8; ++w) o[w] = ld_agent(&in[w]);
+  }
+  if (t == 0) {
+    st_agent(&misc[kMiscFast], fs);
+    if (hout) fast_outcome_to_host(misc, hout, fs);
   }
 }
 
@@ -3389,15 +3673,30 @@ int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out) {
   return H3C_OK;
 }
 
+// Spin (bounded) until the device sets a pinned host word; a blocking stream wait follows either way.
+constexpr uint32_t kFastPollUs = 2000;
+void poll_host_word(const uint32_t *w, uint32_t max_us) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 0; !__atomic_load_n(w, __ATOMIC_ACQUIRE); ++i) {
+    __builtin_ia32_pause();
+    if ((i & 255) == 255 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(max_us))
+      return;
+  }
+}
+
 // The pipeline on device arrays: chunks_in (read), chunks_out (final states; may not alias
 // chunks_in), ios, results, ctr (h3c_update_counters layout, 8 x u64).  `epilogue` enqueues the
 // caller's copies of the outputs before the final synchronisation; with `epi_graph` (its work is
 // device-only and its arguments are part of the graph key) it is captured into the batch's graph.
+// `commit_dev` (the device-table entry: the epilogue is its commit): the fast branch's tail commits the
+// final states there itself and the epilogue runs only if the batch leaves the fast branch.
 // Synchronous.
 template <class Epilogue>
 int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_state *d_chunks_out, uint32_t nchunks,
                 const h3c_update_io *d_ios, uint32_t n, h3c_update_result *d_res, uint32_t flags,
-                unsigned long long *d_ctr, hipStream_t st, int dev, Epilogue epilogue, bool epi_graph = false) {
+                unsigned long long *d_ctr, hipStream_t st, int dev, Epilogue epilogue, bool epi_graph = false,
+                h3c_chunk_state *commit_dev = nullptr) {
   const bool std_domain = (flags & H3C_UPD_STD_DOMAIN) != 0;
   const bool exact = (flags & H3C_UPD_EXACT) != 0;
   flags &= H3C_UPD_STD_DOMAIN | H3C_UPD_EXACT | H3C_UPD_GRAPHS;
@@ -3464,6 +3763,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   while (hcap_fast < 2 * n) hcap_fast <<= 1;
   FastArgs fa{};
   unsigned long long *d_gran = nullptr;
+  uint2 *d_part = nullptr;  // uio_fast_sum_kernel -> uio_fast_res_kernel: each op's XOR in its tile, chunk, state
   auto layout = [&](char *base) -> size_t {  // one layout, run with base 0 to size the lease
     char *cur = base;
     d_status = carve<uint32_t>(cur, n);
@@ -3502,8 +3802,9 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       fa.head = carve<uint32_t>(cur, hcap_fast);
       fa.hmask = hcap_fast - 1;
       fa.dv = carve<unsigned long long>(cur, n);
-      fa.chain = carve<uint2>(cur, n);
+      fa.chain = carve<uint4>(cur, n);
       d_gran = carve<unsigned long long>(cur, (size_t)ntiles_tail * kFastCols);
+      d_part = carve<uint2>(cur, n);
     }
     return (size_t)(cur - base);
   };
@@ -3635,22 +3936,33 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   // uio_fast_kernel return at once (nothing written); the general pipeline below then runs the batch.
   if (try_fast) {
     const uint32_t ptiles_f = (uint32_t)(((size_t)n + C + 1 + kPrepTile - 1) / kPrepTile);
-    const uint32_t zwords = hcap_fast + 2 * ntiles_tail * kFastCols + 1 + (exact ? 3u + prep_tiles : 0u);
+    // (the two-launch tail writes every row of gran itself: nothing to zero there)
+    const uint32_t gwords = H3C_FAST_TAIL2 ? 0u : 2 * ntiles_tail * kFastCols;
+    const uint32_t zwords = hcap_fast + gwords + 1 + (exact ? 3u + prep_tiles : 0u);
     const uint32_t zb = 256, zg = std::max(1u, std::min(1024u, (zwords + 4 * zb - 1) / (4 * zb)));
     unsigned long long *d_ts = reinterpret_cast<unsigned long long *>(d_misc + kMiscT0);
     auto fast_kernel = [&](hipStream_t q, bool timed) -> int {
       hipLaunchKernelGGL(uio_fast_kernel, dim3(nwg_fast), dim3(kBlkThreads), 0, q, n, stdf, pc, fa.frag, fa.chain,
                          fa.dv, d_misc, timed ? d_ts : nullptr);
       HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(uio_fast_tail_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, d_chunks, d_chunks_out,
-                         nchunks, n, poly_type, stdf, exactf, d_paycrc0 + n, pc, fa.frag, fa.key, fa.dv, d_misc,
-                         d_gran, d_res, d_ctr, d_hF, (giveup & 4) ? 1u : 0u);
+      if (H3C_FAST_TAIL2) {
+        hipLaunchKernelGGL(uio_fast_sum_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, n, pc, fa.frag, fa.key,
+                           fa.dv, d_misc, d_gran, d_part, d_misc + kMiscErr);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(uio_fast_res_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, d_chunks, d_chunks_out,
+                           nchunks, n, poly_type, stdf, exactf, d_paycrc0 + n, pc, d_gran, d_part, d_misc, d_res,
+                           d_ctr, d_hF, (giveup & 4) ? 1u : 0u, commit_dev);
+      } else {
+        hipLaunchKernelGGL(uio_fast_tail_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, d_chunks, d_chunks_out,
+                           nchunks, n, poly_type, stdf, exactf, d_paycrc0 + n, pc, fa.frag, fa.key, fa.dv, d_misc,
+                           d_gran, d_res, d_ctr, d_hF, (giveup & 4) ? 1u : 0u, commit_dev);
+      }
       HIP_TRY(hipGetLastError());
       return H3C_OK;
     };
     auto fast_front = [&](hipStream_t q) -> int {  // zero, prep, [piece pass]
       hipLaunchKernelGGL(uio_zero_kernel, dim3(zg), dim3(zb), 0, q, fa.head, hcap_fast,
-                         reinterpret_cast<uint32_t *>(d_gran), 2 * ntiles_tail * kFastCols, d_misc + kMiscSlow, 1u,
+                         reinterpret_cast<uint32_t *>(d_gran), gwords, d_misc + kMiscSlow, 1u,
                          exact ? d_sstate : nullptr, exact ? 3u + prep_tiles : 0u);
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(uio_prep_kernel, dim3(ptiles_f), dim3(kPrepTile), 0, q, d_ios, n, d_chunks, nchunks, poly_type,
@@ -3675,7 +3987,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       rc = cst ? capture_graph(cst, [&] {
         int r = fast_front(cst);
         if (!r) r = fast_kernel(cst, true);
-        if (!r && epi_graph) r = epilogue(cst, d_misc + kMiscOutF, cap);
+        if (!r && epi_graph && !commit_dev) r = epilogue(cst, d_misc + kMiscOutF, cap);
         return r;
       }, gr->g) : H3C_ERR_HIP;
       g_graph_stats[rc ? kDiagCaptureFail : kDiagCapture].fetch_add(1);
@@ -3686,6 +3998,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       rc = H3C_OK;
     }
     const bool use_graph = gr && gr->g && !gr->failed;
+    uint32_t *h_fs = &h_F[kMiscFast - kMiscOutF];  // set last by the tail (fast_outcome_to_host)
+    __atomic_store_n(h_fs, 0u, __ATOMIC_RELAXED);
     if (use_graph) {
       HIP_TRY(hipGraphLaunch(gr->g, st));
       g_graph_stats[kDiagReplay].fetch_add(1);
@@ -3695,10 +4009,13 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       rc = fast_kernel(st, true);  // (timed by its own wall-clock stamps: an abandoned attempt counts nothing)
       if (rc) return rc;
     }
-    if (!(use_graph && epi_graph)) {
+    if (!(use_graph && epi_graph) && !commit_dev) {
       rc = epilogue(st, d_misc + kMiscOutF, cap);
       if (rc) return rc;
     }
+    // the outcome word polled for up to kFastPollUs before the blocking synchronisation: a blocking wait
+    // that starts while the batch runs wakes ~10-20 us after it ends
+    poll_host_word(h_fs, kFastPollUs);
     const hipError_t se = hipStreamSynchronize(st);
     if (se != hipSuccess) {
       drain.armed = drain_aux.armed = false;
@@ -4099,7 +4416,7 @@ extern "C" int h3c_update_ios_dev(uint8_t poly_type, h3c_chunk_state *chunks_dev
                        HIP_TRY(hipGetLastError());
                      }
                      return H3C_OK;
-                   }, true);
+                   }, true, nchunks ? chunks_dev : nullptr);
   if (rc) return rc;
   drain.armed = false;
   return H3C_OK;

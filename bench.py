@@ -216,6 +216,7 @@ class Ctx:
 PATTERN_CEILING = {
     "seg_crc_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
     "seg_quad_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
+    "seg_uni_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
     "upd_delta_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
     "upd_fused_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
     "uio_block_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
@@ -300,7 +301,9 @@ def run_verify(args, cx: Ctx) -> dict:
         "verified": verified,
         "pct_hbm_peak": round(100.0 * (n * clen) / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 2),
         # chunks of <= 16 KiB (one segment each) run the small-chunk kernel
-        "roofline": roofline(prof, HBM_PEAK_GBPS, kernel="seg_quad_kernel" if clen <= (16 << 10) else "seg_crc_kernel"),
+        # (a uniform plan of such chunks, rows of 64 / 256 bytes: seg_uni_kernel, §4.1 5c)
+        "roofline": roofline(prof, HBM_PEAK_GBPS, kernel=("seg_uni_kernel" if clen % 64 == 0 else "seg_quad_kernel")
+                             if clen <= (16 << 10) else "seg_crc_kernel"),
     }
     if cx.world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(stored_host, clen, args.cpu_seconds)
