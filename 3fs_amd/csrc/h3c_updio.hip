@@ -326,11 +326,14 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
   }
   if (i < kCtrN) ctr[i] = 0;
   if (i < kMiscSlow) misc[i] = i == kMiscT0 || i == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;  // (kMiscSlow: uio_zero_kernel)
+  // the fast branch without the piece pass (not exact): only the validation feeds it (fast_prep_tile);
+  // the general pipeline's arrays are not written (a batch that leaves the branch runs its own prep)
+  const bool lean = fa.head && !pbase;
   // chunk items n + c for c < C = max(nchunks, 1) (the piece pass's NP = n + C items), then the
   // scan's extra entry: pbase[n + C] = total
   const uint32_t C = nchunks ? nchunks : 1u;
   uint32_t np = 0;
-  if (i >= n && i < n + C) {
+  if (!lean && i >= n && i < n + C) {
     const uint32_t c = i - n;
     if (c < nchunks) {
       const h3c_chunk_state cs = chunks[c];
@@ -339,15 +342,17 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
     npieces[i] = np;
     paycrc0[i] = 0;
   }
-  if (i == n + C) npieces[i] = 0;
+  if (!lean && i == n + C) npieces[i] = 0;
   h3c_update_io f_io{};
   h3c_chunk_state f_cs{};
   uint32_t f_st = H3C_ERR_INVALID_ARG;
   if (i < n) {
-    paycrc0[i] = 0;  // XOR accumulators of the piece and block kernels
-    eacc[2 * i] = 0;
-    eacc[2 * i + 1] = 0;
-    a6[i] = 0;       // A6 verdicts (the early pass, the front / late checks, the block kernel)
+    if (!lean) {
+      paycrc0[i] = 0;  // XOR accumulators of the piece and block kernels
+      eacc[2 * i] = 0;
+      eacc[2 * i + 1] = 0;
+      a6[i] = 0;       // A6 verdicts (the early pass, the front / late checks, the block kernel)
+    }
     const h3c_update_io io = ios[i];
     uint32_t st = H3C_OK;
     const uint32_t c = io.chunk;
@@ -381,13 +386,15 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
           st = H3C_ERR_CHECKSUM_MISMATCH;
       }
     }
-    status[i] = st;
-    key[i] = c < nchunks ? c : nchunks;
-    idx[i] = i;
-    const bool cand = st == H3C_OK && fold_candidate(io, chunks[c], st);
-    np = (st == H3C_OK && io.kind == H3C_UPD_WRITE && io.length && !cand) ? (io.length + kPieceBytes - 1) / kPieceBytes
-                                                                          : 0;
-    npieces[i] = np;
+    if (!lean) {
+      status[i] = st;
+      key[i] = c < nchunks ? c : nchunks;
+      idx[i] = i;
+      const bool cand = st == H3C_OK && fold_candidate(io, chunks[c], st);
+      np = (st == H3C_OK && io.kind == H3C_UPD_WRITE && io.length && !cand) ? (io.length + kPieceBytes - 1) / kPieceBytes
+                                                                            : 0;
+      npieces[i] = np;
+    }
     f_io = io;
     f_st = st;
     if (c < nchunks) f_cs = chunks[c];
@@ -2319,15 +2326,14 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
 //     block loaded once, each op's A6 check on its payload rows, its delta CRC (new ^ old), its bytes
 //     applied, the block stored once; a chain's later ops come from chain[].  Each op's delta (or its
 //     failed check) goes to dv[op].  Nothing waits: the kernel ends when its slowest wave does.
-//   uio_fast_tail_kernel: per 1,024-op tile, each op's delta moved to its chunk's end (x^(8e), one op
-//     per lane), the per-chunk XORs in sequence order (lane c holds chunks c and c + 64: <= 128 chunks,
-//     checked by the host), the tile's per-chunk sums published and the earlier tiles' read by all 16
-//     waves at once; every op's result is t0 ^ the XOR of its chunk's deltas up to it; the last tile
-//     writes the chunks' final states, the last to finish the outcome words (to the host buffer).
+//   uio_fast_sum_kernel + uio_fast_res_kernel (the tail): per 1,024-op tile, each op's delta moved to its
+//     chunk's end (x^(8e), one op per lane), the per-chunk XORs in sequence order (<= 128 chunks, checked
+//     by the host), every op's result t0 ^ the XOR of its chunk's deltas up to it, the final states, the
+//     commit (device-table entry) and the outcome words (to the host buffer).
 // (One kernel with the sums chained across workgroups by look-back measured 320-330 us against this
-// pair's ~270 us: its waves that finished early waited on chains run late by other waves, polling.)
-// The tail's waits are bounded: a tile that gives up sets misc[kMiscFVoid] and the host recomputes the
-// results with uio_fast_recover_kernel (dv[] is complete once uio_fast_kernel has ended).
+// form's ~300 us: its waves that finished early waited on chains run late by other waves, polling.)
+// uio_fast_recover_kernel recomputes the results from dv[] when a pass reports itself void (kept for
+// the test hook H3C_HOOK_UPD_GIVEUP bit 2; the two-launch tail has no wait to give up).
 // the bucket walks over the tiles' last ops (uio_fast_kernel; restrict pointers, so that uniform
 // walks compile to scalar loads)
 __device__ __forceinline__ bool fast_listed_before(const uint4 *__restrict__ link, const unsigned long long *__restrict__ keys,
@@ -2358,12 +2364,12 @@ __device__ __forceinline__ uint32_t fast_cross_next(const uint4 *__restrict__ li
 // multiplies overlap the walks' round trips.
 __global__ void uio_fast_link_kernel(const uint4 *__restrict__ link, const unsigned long long *__restrict__ keys,
                                      const uint32_t *__restrict__ bhead, uint32_t hmask, uint32_t n,
-                                     const uint32_t *__restrict__ misc, uint4 *__restrict__ chain,
+                                     const uint32_t *__restrict__ slow, uint4 *__restrict__ chain,
                                      const h3c_update_io *__restrict__ ios, const h3c_chunk_state *__restrict__ chunks,
                                      uint8_t poly_type, uint32_t std_domain, const PolyConsts *__restrict__ pc,
                                      FragDesc *__restrict__ frag) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n || misc[kMiscSlow]) return;  // (an abandoned batch: uio_fast_kernel returns at once)
+  if (j >= n || *slow) return;  // (an abandoned batch: uio_fast_kernel returns at once)
   {
     const h3c_update_io io = ios[j];
     const h3c_chunk_state cs = chunks[io.chunk];
@@ -2422,10 +2428,11 @@ __device__ unsigned int g_ftr[130] = {};
 #define FAST_MARK(i) ((void)0)
 #endif
 constexpr uint32_t kFastCols = 128;  // chunks a fast-branch batch may name (lane c: chunks c, c + 64)
+// FastScratch words: [0] the slow word, [1, ...) the bucket heads
+constexpr uint32_t kScratchHeads = 1;
 #ifndef H3C_FAST_GRAB
 #define H3C_FAST_GRAB 1  // 1: a workgroup's waves take their chain starts from an LDS counter (0: static ranges)
 #endif
-constexpr uint32_t kFastSpin = 1u << 21;
 constexpr unsigned long long kGranApplied = 4ull << 32;  // look-back granule bit: some op of the chunk applied
 
 
@@ -2441,11 +2448,13 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
                                                              const PolyConsts *__restrict__ pc,
                                                              const FragDesc *__restrict__ frag,
                                                              const uint4 *__restrict__ chain, unsigned long long *dv,
-                                                             const uint32_t *__restrict__ misc, unsigned long long *ts) {
+                                                             const uint32_t *__restrict__ slow, unsigned long long *ts,
+                                                             const unsigned long long *__restrict__ keys,
+                                                             uint32_t *heads, uint32_t hmask) {
   __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
   const uint32_t t = threadIdx.x, lane = t & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  if (misc[kMiscSlow]) return;  // not a fast-branch batch: the host runs the general pipeline
+  if (*slow) return;  // not a fast-branch batch: the host runs the general pipeline
   if (ts && t == 0) atomicMin(&ts[0], (unsigned long long)wall_clock64());
 #if H3C_FAST_TRACE
   uint64_t ftr[8];
@@ -2512,8 +2521,13 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
   // chains more than others finishing last.  The workgroup's ops [wlo, whi) are handed out one at a
   // time by an LDS counter (a wave skips the ops that do not start a chain); each wave's first op is
   // wlo + wave, whose rows load (speculatively: ~95 % start a chain) before the table fill.
-  __shared__ uint32_t s_grab;
   (void)next_start, (void)g0, (void)hm, (void)cm;  // (the static form's)
+  auto is_start = [&](uint32_t j, bool &cn) -> bool {
+    const uint4 ch = chain[j];
+    cn = ch.y != kNil;
+    return (ch.x >> 31) != 0;
+  };
+  __shared__ uint32_t s_grab;
   const uint32_t wlo = (uint32_t)((uint64_t)blockIdx.x * kBlkWaves * n / nw);
   const uint32_t whi = (uint32_t)((uint64_t)(blockIdx.x + 1) * kBlkWaves * n / nw);
   const uint32_t first = wlo + wave;
@@ -2523,11 +2537,6 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
     rows_at(a0, cur);
   }
   if (t == 0) s_grab = wlo + kBlkWaves;
-  auto is_start = [&](uint32_t j, bool &cn) -> bool {
-    const uint4 ch = chain[j];
-    cn = ch.y != kNil;
-    return (ch.x >> 31) != 0;
-  };
   auto grab = [&](bool &cn) -> uint32_t {
     for (;;) {
       uint32_t j = 0;
@@ -2596,6 +2605,9 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
       const FoldIo fx{f3.x, f3.y, f3.z, std_domain, pc, nullptr, nullptr};
       dirty |= apply_fragment(cur.img, cur.nw, f2.w, f1.z, f1.w, f2.x, f2.z, f1.x, lane, lb, Lt, red, fx, sink);
     }
+    // the op's bucket head cleared for the next batch (FastScratch; uio_fast_link_kernel, its only reader,
+    // has ended)
+    if (lane == 0) heads[fast_bucket(keys[op], hmask)] = 0;
     if (cont) {  // the block's next op
       const uint32_t nx = cx.y;
       if (nx != kNil) {
@@ -2655,241 +2667,32 @@ __device__ __forceinline__ void fast_outcome_to_host(const uint32_t *misc, uint3
   __hip_atomic_store(&hout[kMiscFast - kMiscOutF], fs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The per-chunk XOR of the deltas in sequence order, every op's result, the chunks' final states, the
-// counters and the outcome words (see above); tile k = ops [1024 k, 1024 k + 1024).
-constexpr uint32_t kTailTile = 1024;
-__global__ __launch_bounds__(kTailTile) void uio_fast_tail_kernel(
-    const h3c_chunk_state *__restrict__ chunks, h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks, uint32_t n,
-    uint8_t poly_type, uint32_t std_domain, uint32_t exact, const uint32_t *__restrict__ crc0,
-    const PolyConsts *__restrict__ pc, const FragDesc *__restrict__ frag, const unsigned long long *__restrict__ keys,
-    const unsigned long long *__restrict__ dv, uint32_t *misc, unsigned long long *gran,
-    h3c_update_result *__restrict__ res, unsigned long long *__restrict__ ctr, uint32_t *hout, uint32_t force_giveup,
-    h3c_chunk_state *commit) {
-  constexpr uint32_t NW = kTailTile / 64, kWC = NW * kFastCols;
-  __shared__ uint32_t wagg[kWC], wapp[kWC], wlb[kWC], wlba[kWC], wbase[kFastCols], wsz[kFastCols];
-  __shared__ uint32_t s_void, s_bad, s_last;
-  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, k = blockIdx.x, ntiles = gridDim.x;
-  if (misc[kMiscSlow]) {  // not a fast-branch batch: nothing was done; the outcome says so
-    if (k == 0 && t == 0) {
-      misc[kMiscFast] = kFastAbort;
-      if (hout) fast_outcome_to_host(misc, hout, kFastAbort);
-    }
-    return;
-  }
-  // test hook (H3C_HOOK_UPD_GIVEUP bit 2): tile 1 gives up its wait at once, as a starved one would
-  if (t == 0) {
-    s_void = force_giveup && k == 1 ? 1u : 0u;
-    s_bad = 0;
-  }
-#if H3C_FAST_TRACE
-  uint64_t ftr[8];
-  FAST_MARK(0);
-#endif
-  const uint32_t poly = pc->poly;
-  const uint32_t j = k * kTailTile + t;
-  // the chunk table (threads c < 128), loaded first: its round trip overlaps the deltas'
-  h3c_chunk_state cs{};
-  uint32_t t0 = 0;
-  if (t < nchunks && t < kFastCols) {
-    cs = chunks[t];
-    t0 = fast_t0(cs, t, exact, std_domain, crc0, pc);
-  }
-  // each op's delta moved to its chunk's end
-  uint32_t c = kNil, v = 0, st = 0;
-  if (j < n) {
-    c = (uint32_t)(keys[j] >> 36);
-    const unsigned long long g = dv[j];
-    st = (uint32_t)(g >> 32);
-    if (st == 1) v = dgf_mul_fast((uint32_t)g, frag[j].mult, poly);
-  }
-  // in the wave: each op's inclusive XOR of its chunk's deltas (XOR is order-free: the lanes at or before
-  // this one with the same chunk, found with 8 ballots over the chunk index, usually one or two), and the
-  // wave's per-chunk sums in LDS
-  __shared__ uint32_t lv[kTailTile];
-  lv[t] = v;
-  uint64_t same = __builtin_amdgcn_ballot_w64(c != kNil);
-#pragma unroll
-  for (uint32_t b = 0; b < 8; ++b) {
-    const uint64_t m = __builtin_amdgcn_ballot_w64((c >> b) & 1u);
-    same &= ((c >> b) & 1u) ? m : ~m;
-  }
-  uint32_t ip = 0;
-  for (uint64_t m = same & (lane == 63 ? ~0ull : ((2ull << lane) - 1)); m; m &= m - 1)
-    ip ^= lv[(t & ~63u) + (uint32_t)__builtin_ctzll(m)];
-  // the wave's sum per chunk: the highest lane of each chunk holds it (ip over all its lanes)
-  const bool top = c != kNil && (same >> lane) <= 1;  // no higher lane with this chunk
-  const uint64_t okm = __builtin_amdgcn_ballot_w64(st == 1);
-  wagg[wave * kFastCols + lane] = 0;
-  wagg[wave * kFastCols + 64 + lane] = 0;
-  wapp[wave * kFastCols + lane] = 0;
-  wapp[wave * kFastCols + 64 + lane] = 0;
-  __builtin_amdgcn_wave_barrier();
-  if (top) {
-    wagg[wave * kFastCols + c] = ip;
-    wapp[wave * kFastCols + c] = (same & okm) ? 1u : 0u;
-  }
-  FAST_MARK(1);
-  __syncthreads();
-  FAST_MARK(2);
-  const bool two = nchunks > 64;
-  if (wave == 0) {  // the tile's sums, published
-    uint32_t a0 = 0, a1 = 0, p0 = 0, p1 = 0;
-    for (uint32_t w = 0; w < NW; ++w) {
-      a0 ^= wagg[w * kFastCols + lane];
-      a1 ^= wagg[w * kFastCols + 64 + lane];
-      p0 |= wapp[w * kFastCols + lane];
-      p1 |= wapp[w * kFastCols + 64 + lane];
-    }
-    unsigned long long *row = gran + (uint64_t)k * kFastCols;
-    if (lane < nchunks) st_agent(&row[lane], (1ull << 32) | (p0 ? kGranApplied : 0ull) | a0);
-    if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], (1ull << 32) | (p1 ? kGranApplied : 0ull) | a1);
-  }
-  // the earlier tiles' sums, read by all waves at once (wave w: tiles w, w + 16, ...)
-  {
-    const uint32_t spin = kFastSpin;
-    const bool c0 = lane < nchunks, c1 = two && lane + 64 < nchunks;
-    uint32_t x0 = 0, x1 = 0, q0 = 0, q1 = 0;
-    constexpr uint32_t kB = 4;  // tiles in flight per wave
-    for (uint32_t r0 = wave; r0 < k; r0 += kB * NW) {
-      unsigned long long g0v[kB], g1v[kB];
-#pragma unroll
-      for (uint32_t b = 0; b < kB; ++b) {
-        const uint32_t r = r0 + b * NW;
-        g0v[b] = r < k && c0 ? ld_agent(&gran[(uint64_t)r * kFastCols + lane]) : (1ull << 32);
-        g1v[b] = r < k && c1 ? ld_agent(&gran[(uint64_t)r * kFastCols + 64 + lane]) : (1ull << 32);
-      }
-#pragma unroll
-      for (uint32_t b = 0; b < kB; ++b) {
-        const uint32_t r = r0 + b * NW;
-        for (uint32_t spins = 0; (g0v[b] >> 32) == 0 || (g1v[b] >> 32) == 0;) {  // not yet published
-          if (spins++ >= spin) {  // an earlier tile never published: give up (the host recomputes the results)
-            s_void = 1;
-            g0v[b] = g1v[b] = 1ull << 32;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(4);
-          if ((g0v[b] >> 32) == 0) g0v[b] = ld_agent(&gran[(uint64_t)r * kFastCols + lane]);
-          if ((g1v[b] >> 32) == 0) g1v[b] = ld_agent(&gran[(uint64_t)r * kFastCols + 64 + lane]);
-        }
-        x0 ^= (uint32_t)g0v[b];
-        x1 ^= (uint32_t)g1v[b];
-        q0 |= (g0v[b] & kGranApplied) ? 1u : 0u;
-        q1 |= (g1v[b] & kGranApplied) ? 1u : 0u;
-      }
-    }
-    wlb[wave * kFastCols + lane] = x0;
-    wlb[wave * kFastCols + 64 + lane] = x1;
-    wlba[wave * kFastCols + lane] = q0;
-    wlba[wave * kFastCols + 64 + lane] = q1;
-  }
-  __syncthreads();
-  FAST_MARK(3);
-  if (wave < 2) {  // per chunk (thread c < 128): t0 ^ the earlier tiles' deltas; the last tile's final states
-    const uint32_t cc = t;
-    uint32_t e = 0, q = 0;
-    for (uint32_t w = 0; w < NW; ++w) {
-      e ^= wlb[w * kFastCols + cc];
-      q |= wlba[w * kFastCols + cc];
-    }
-    wbase[cc] = t0 ^ e;
-    wsz[cc] = cs.size;
-    if (k + 1 == ntiles && cc < nchunks) {
-      uint32_t a = e, p = q;
-      for (uint32_t w = 0; w < NW; ++w) {
-        a ^= wagg[w * kFastCols + cc];
-        p |= wapp[w * kFastCols + cc];
-      }
-      h3c_chunk_state f = cs;
-      if (p) {  // (a chunk whose ops all failed A6 keeps its stored value)
-        f.value = std_domain ? ~(t0 ^ a) : (t0 ^ a);
-        f.type = poly_type;
-      }
-      // write-through: the last tile to finish reads them back to commit them
-      static_assert(sizeof(h3c_chunk_state) % 8 == 0, "chunk state in 8-byte words");
-      unsigned long long fw[sizeof(h3c_chunk_state) / 8];
-      __builtin_memcpy(fw, &f, sizeof f);
-      unsigned long long *o = reinterpret_cast<unsigned long long *>(chunks_out + cc);
-#pragma unroll
-      for (uint32_t w = 0; w < sizeof(h3c_chunk_state) / 8; ++w) st_agent(&o[w], fw[w]);
-      if (exact && cs.size && cs.type == poly_type && t0 != (std_domain ? ~cs.value : cs.value))
-        atomicAdd(&ctr[kCtrStale], 1ull);
-    }
-    stores_done();  // (waves 0 and 1: the final states at the coherence point before the done count)
-  }
-  __syncthreads();
-  FAST_MARK(4);
-  // every op's result: t0 ^ its chunk's deltas up to it (earlier tiles, this tile's earlier waves, the wave)
-  if (j < n) {
-    uint32_t sv = wbase[c] ^ ip;
-    for (uint32_t w = 0; w < wave; ++w) sv ^= wagg[w * kFastCols + c];
-    h3c_update_result o{};
-    o.status = st == 1 ? H3C_OK : H3C_ERR_CHECKSUM_MISMATCH;
-    o.size = wsz[c];
-    o.type = poly_type;  // (a failed op reports the stored type: the batch polynomial here)
-    o.value = st == 1 ? (std_domain ? ~sv : sv) : (std_domain ? 0u : sv);  // engine.rs:303 / ChunkReplica.cc:174
-    res[j] = o;
-    if (st != 1 && st != 2) s_bad = 1;  // an op with no delta: cannot happen after a complete uio_fast_kernel
-  }
-  {
-    uint32_t v8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    v8[std_domain ? kCtrRecalc : kCtrRead] = j < n && st == 1;  // updateChecksum (iv) (:389) / copy_on_write (chunk.rs:153)
-    v8[kCtrMismatch] = j < n && st == 2;
-    __shared__ unsigned int sh[8];
-    ctr_add_block(sh, ctr, v8);
-  }
-  __syncthreads();
-#if H3C_FAST_TRACE
-  FAST_MARK(5);
-  if (t == 0 && (k < 2 || k == ntiles / 2 || k + 1 == ntiles))
-    printf("tail tile %u start %llu deltas %llu summed %llu lookback %llu t0 %llu results %llu (ticks)\n", k,
-           (unsigned long long)ftr[0], (unsigned long long)(ftr[1] - ftr[0]), (unsigned long long)(ftr[2] - ftr[0]),
-           (unsigned long long)(ftr[3] - ftr[0]), (unsigned long long)(ftr[4] - ftr[0]),
-           (unsigned long long)(ftr[5] - ftr[0]));
-#endif
-  if (t == 0) {
-    if (s_void) atomicOr(&misc[kMiscFVoid], 1u);
-    if (s_bad) atomicOr(&misc[kMiscErr], 1u);
-    stores_done();
-    s_last = atomicAdd(&misc[kMiscFDone], 1u) + 1 == ntiles;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  // the last tile to finish: every tile has read the input table, so a complete pass commits the final
-  // states in place (the device-table entry; uio_commit_kernel's work), then the outcome words
-  const uint32_t fs = ld_agent(&misc[kMiscFVoid]) ? (uint32_t)kFastVoid : (uint32_t)kFastDone;
-  const bool ok = fs == kFastDone && !ld_agent(&misc[kMiscErr]);
-  if (commit && ok && t < nchunks) {
-    const unsigned long long *in = reinterpret_cast<const unsigned long long *>(chunks_out + t);
-    unsigned long long *o = reinterpret_cast<unsigned long long *>(commit + t);
-#pragma unroll
-    for (uint32_t w = 0; w < sizeof(h3c_chunk_state) / 8; ++w) o[w] = ld_agent(&in[w]);
-  }
-  if (t == 0) {
-    st_agent(&misc[kMiscFast], fs);
-    if (hout) fast_outcome_to_host(misc, hout, fs);
-  }
-}
+constexpr uint32_t kTailTile = 1024;  // ops per tile of the tail kernels
 
-// The tail in two launches with no waiting (H3C_FAST_TAIL2, the default): uio_fast_sum_kernel writes each
-// tile's per-chunk sums (one row of gran per tile) and each op's XOR within its tile; uio_fast_res_kernel
-// reads, per tile, the rows of the tiles before it -- complete at the launch boundary -- and writes the
-// results; its last tile the final states, its last to finish the commit and the outcome words.  (The
-// one-launch form chained the tiles by look-back: ~27 us, most of it waiting on late-starting tiles.)
-#ifndef H3C_FAST_TAIL2
-#define H3C_FAST_TAIL2 1
-#endif
+// The tail in two launches with no waiting: uio_fast_sum_kernel writes each tile's per-chunk sums (one row
+// of gran per tile) and each op's XOR within its tile; uio_fast_res_kernel reads, per tile, the rows of
+// the tiles before it -- complete at the launch boundary -- and writes the results; its last tile the
+// final states, its last to finish the commit and the outcome words.  (Round 4's first form, one launch
+// chaining the tiles by look-back, took ~27 us against ~19 us: most of it waiting on late-starting tiles.)
+// They also keep the fast scratch clean for the next batch (FastScratch: the slow word and bucket heads
+// are zero between batches): uio_fast_kernel clears the bucket of every op it runs; when the batch was
+// not a fast one, the sum kernel clears every bucket and the results kernel's last tile the slow word.
 __global__ __launch_bounds__(kTailTile) void uio_fast_sum_kernel(uint32_t n, const PolyConsts *__restrict__ pc,
                                                                 const FragDesc *__restrict__ frag,
                                                                 const unsigned long long *__restrict__ keys,
                                                                 const unsigned long long *__restrict__ dv,
-                                                                const uint32_t *__restrict__ misc,
+                                                                const uint32_t *__restrict__ slow,
+                                                                uint32_t *__restrict__ heads, uint32_t hmask,
                                                                 unsigned long long *__restrict__ gran,
                                                                 uint2 *__restrict__ part, uint32_t *merr) {
   constexpr uint32_t NW = kTailTile / 64;
   __shared__ uint32_t wagg[NW * kFastCols], wapp[NW * kFastCols], lv[kTailTile];
   __shared__ uint32_t s_bad;
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, k = blockIdx.x;
-  if (misc[kMiscSlow]) return;
+  if (*slow) {  // not a fast-branch batch (keys may be partial): every bucket head cleared
+    for (uint32_t i = k * kTailTile + t; i <= hmask; i += gridDim.x * kTailTile) heads[i] = 0;
+    return;
+  }
   if (t == 0) s_bad = 0;
   const uint32_t poly = pc->poly;
   const uint32_t j = k * kTailTile + t;
@@ -2945,14 +2748,15 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_res_kernel(
     const h3c_chunk_state *__restrict__ chunks, h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks, uint32_t n,
     uint8_t poly_type, uint32_t std_domain, uint32_t exact, const uint32_t *__restrict__ crc0,
     const PolyConsts *__restrict__ pc, const unsigned long long *__restrict__ gran, const uint2 *__restrict__ part,
-    uint32_t *misc, h3c_update_result *__restrict__ res, unsigned long long *__restrict__ ctr, uint32_t *hout,
-    uint32_t force_giveup, h3c_chunk_state *commit) {
+    uint32_t *misc, uint32_t *slow, h3c_update_result *__restrict__ res, unsigned long long *__restrict__ ctr,
+    uint32_t *hout, uint32_t force_giveup, h3c_chunk_state *commit) {
   constexpr uint32_t NR = kTailTile / kFastCols;  // row groups read in parallel (thread t: column t % 128)
   __shared__ uint32_t px[NR * kFastCols], pq[NR * kFastCols], wbase[kFastCols], wsz[kFastCols];
   __shared__ uint32_t s_last;
   const uint32_t t = threadIdx.x, k = blockIdx.x, ntiles = gridDim.x;
-  if (misc[kMiscSlow]) {  // not a fast-branch batch: nothing was done; the outcome says so
-    if (k == 0 && t == 0) {
+  if (ld_agent(slow)) {  // not a fast-branch batch: nothing was done; the outcome says so
+    if (t == 0 && atomicAdd(&misc[kMiscFDone], 1u) + 1 == ntiles) {  // (every tile has read the slow word)
+      st_agent(slow, 0u);
       misc[kMiscFast] = kFastAbort;
       if (hout) fast_outcome_to_host(misc, hout, kFastAbort);
     }
@@ -2967,13 +2771,22 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_res_kernel(
     cs = chunks[t];
     t0 = fast_t0(cs, t, exact, std_domain, crc0, pc);
   }
-  {  // the earlier tiles' rows: column t % 128, rows t / 128 + NR i (all loads in flight at once)
+  {  // the earlier tiles' rows: column t % 128, rows t / 128 + NR i, 8 loads in flight per thread
     const uint32_t col = t % kFastCols, r0 = t / kFastCols;
     uint32_t x = 0, q = 0;
-    for (uint32_t r = r0; r < k; r += NR) {
-      const unsigned long long g = gran[(uint64_t)r * kFastCols + col];
-      x ^= (uint32_t)g;
-      q |= (g & kGranApplied) ? 1u : 0u;
+    constexpr uint32_t kU = 8;
+    for (uint32_t rb = r0; rb < k; rb += kU * NR) {
+      unsigned long long g[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t r = rb + u * NR;
+        g[u] = r < k ? gran[(uint64_t)r * kFastCols + col] : 0ull;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        x ^= (uint32_t)g[u];
+        q |= (g[u] & kGranApplied) ? 1u : 0u;
+      }
     }
     px[r0 * kFastCols + col] = x;
     pq[r0 * kFastCols + col] = q;
@@ -3047,6 +2860,7 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_res_kernel(
     if (hout) fast_outcome_to_host(misc, hout, fs);
   }
 }
+
 
 // After a void fast pass (a workgroup gave up waiting): the results, final states and counters again
 // from dv[], which the pass completed, by one workgroup walking the ops in tiles of 1,024.
@@ -3378,11 +3192,21 @@ struct UpdGraphs {
 // next thread that needs one on the same device takes it from there; graph execs of ended threads
 // are destroyed by the next update call.  A caller that spawns short-lived threads therefore
 // reuses a bounded set of streams instead of leaking them.
+// The fast branch's per-thread scratch: the slow word and the bucket heads, zero between batches (the
+// batch's tail kernels clear what it set), so no launch zeroes them per batch.  `dirty`: not known to be
+// zero (new, or a batch that did not reach its outcome) -- zeroed before the next use.
+struct FastScratch {
+  int dev = -1;
+  uint32_t *p = nullptr;
+  size_t words = 0;
+  bool dirty = true;
+};
 struct ResPool {
   std::mutex mu;
   std::vector<AuxStream> aux;
   std::vector<std::pair<int, hipStream_t>> cap;
   std::vector<hipGraphExec_t> dead;
+  std::vector<FastScratch> scratch;
 };
 ResPool g_res;
 
@@ -3405,8 +3229,14 @@ struct ThreadRes {
     uint64_t used = 0;
   } pred[8];
   uint64_t tick = 0;
+  std::vector<FastScratch> fscratch;  // one per device
   ~ThreadRes() {
     std::lock_guard<std::mutex> lk(g_res.mu);
+    for (FastScratch &f : fscratch)
+      if (f.p) {
+        f.dirty = true;  // (the next owner zeroes it)
+        g_res.scratch.push_back(f);
+      }
     for (AuxStream &a : aux)
       if (a.st) g_res.aux.push_back(a);
     for (int i = 0; i < 8; ++i)
@@ -3419,6 +3249,49 @@ ThreadRes &tres() {
   thread_local ThreadRes r;
   return r;
 }
+
+// This thread's fast scratch on `dev` with at least `words` words (nullptr: allocation failed).
+FastScratch *fast_scratch(int dev, size_t words) {
+  ThreadRes &r = tres();
+  FastScratch *f = nullptr;
+  for (FastScratch &x : r.fscratch)
+    if (x.dev == dev) f = &x;
+  if (f && f->words >= words) return f;
+  if (f) {  // too small: freed (this thread's earlier batches have completed)
+    (void)hipFree(f->p);
+    f->p = nullptr;
+    f->words = 0;
+  } else {
+    r.fscratch.emplace_back();
+    f = &r.fscratch.back();
+    f->dev = dev;
+  }
+  {  // an ended thread's scratch, if one is large enough
+    std::lock_guard<std::mutex> lk(g_res.mu);
+    for (size_t i = 0; i < g_res.scratch.size(); ++i)
+      if (g_res.scratch[i].dev == dev && g_res.scratch[i].words >= words) {
+        *f = g_res.scratch[i];
+        g_res.scratch.erase(g_res.scratch.begin() + (long)i);
+        f->dirty = true;
+        return f;
+      }
+  }
+  const size_t w = std::max<size_t>(words, 1 + 4096);
+  if (hipMalloc(reinterpret_cast<void **>(&f->p), w * 4) != hipSuccess) {
+    f->p = nullptr;
+    f->words = 0;
+    return nullptr;
+  }
+  f->words = w;
+  f->dirty = true;
+  return f;
+}
+struct ScratchGuard {  // marks the scratch suspect unless the batch's outcome was read (disarm)
+  FastScratch *f;
+  ~ScratchGuard() {
+    if (f) f->dirty = true;
+  }
+};
 
 void drain_dead_graphs() {
   std::vector<hipGraphExec_t> dead;
@@ -3675,14 +3548,29 @@ int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out) {
 
 // Spin (bounded) until the device sets a pinned host word; a blocking stream wait follows either way.
 constexpr uint32_t kFastPollUs = 2000;
-void poll_host_word(const uint32_t *w, uint32_t max_us) {
+bool poll_host_word(const uint32_t *w, uint32_t max_us) {
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t i = 0; !__atomic_load_n(w, __ATOMIC_ACQUIRE); ++i) {
     __builtin_ia32_pause();
     if ((i & 255) == 255 &&
         std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(max_us))
-      return;
+      return false;
   }
+  return true;
+}
+
+// The stream's work done: hipStreamQuery polled for up to max_us (once the outcome word is set, the
+// last kernel is ending; hipStreamSynchronize took 8-14 us more to return, profiles/r04_updio_host_timeline.txt),
+// then the blocking wait.
+hipError_t stream_wait(hipStream_t st, uint32_t max_us) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 0;; ++i) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q != hipErrorNotReady) return q;
+    __builtin_ia32_pause();
+    if ((i & 15) == 15 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(max_us)) break;
+  }
+  return hipStreamSynchronize(st);
 }
 
 // The pipeline on device arrays: chunks_in (read), chunks_out (final states; may not alias
@@ -3728,15 +3616,35 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                                           kPrepTile - 1) / kPrepTile);
   size_t sort_tmp = 0, scan_tmp = 0, pscan_tmp = 0, szscan_tmp = 0, ascan_tmp = 0;
   const uint32_t bits = bits_for((uint64_t)nchunks + 1);
-  HIP_TRY(sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, n, bits, st));
-  HIP_TRY(rocprim::exclusive_scan(nullptr, scan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)n + 1,
-                                  rocprim::plus<uint32_t>(), st));
-  HIP_TRY(rocprim::exclusive_scan(nullptr, pscan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
-                                  (size_t)n + C + 1, rocprim::plus<uint32_t>(), st));
-  HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, szscan_tmp, (uint32_t *)nullptr, (SzTy *)nullptr, (SzTy *)nullptr,
-                                         (size_t)n, SzTyOp(), rocprim::equal_to<uint32_t>(), st));
-  HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, ascan_tmp, (uint32_t *)nullptr, (Aff *)nullptr, (Aff *)nullptr,
-                                         (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
+  // rocPRIM's scratch sizes: each query makes ~6 device-property calls (~14 us per batch in all,
+  // profiles/r04_updio_host_timeline.txt), so they are kept per thread for the last shapes seen
+  struct TmpSizes {
+    int dev = -1;
+    uint32_t n = 0, C = 0, bits = 0;
+    size_t v[5] = {};
+  };
+  thread_local TmpSizes tmp_cache[4];
+  thread_local uint32_t tmp_next = 0;
+  TmpSizes *ts_hit = nullptr;
+  for (TmpSizes &x : tmp_cache)
+    if (x.dev == dev && x.n == n && x.C == C && x.bits == bits) ts_hit = &x;
+  if (ts_hit) {
+    sort_tmp = ts_hit->v[0], scan_tmp = ts_hit->v[1], pscan_tmp = ts_hit->v[2], szscan_tmp = ts_hit->v[3];
+    ascan_tmp = ts_hit->v[4];
+  } else {
+    HIP_TRY(sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, n, bits, st));
+    HIP_TRY(rocprim::exclusive_scan(nullptr, scan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)n + 1,
+                                    rocprim::plus<uint32_t>(), st));
+    HIP_TRY(rocprim::exclusive_scan(nullptr, pscan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
+                                    (size_t)n + C + 1, rocprim::plus<uint32_t>(), st));
+    HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, szscan_tmp, (uint32_t *)nullptr, (SzTy *)nullptr, (SzTy *)nullptr,
+                                           (size_t)n, SzTyOp(), rocprim::equal_to<uint32_t>(), st));
+    HIP_TRY(rocprim::inclusive_scan_by_key(nullptr, ascan_tmp, (uint32_t *)nullptr, (Aff *)nullptr, (Aff *)nullptr,
+                                           (size_t)n, AffOp{poly}, rocprim::equal_to<uint32_t>(), st));
+    TmpSizes &e = tmp_cache[tmp_next++ % 4];
+    e.dev = dev, e.n = n, e.C = C, e.bits = bits;
+    e.v[0] = sort_tmp, e.v[1] = scan_tmp, e.v[2] = pscan_tmp, e.v[3] = szscan_tmp, e.v[4] = ascan_tmp;
+  }
   const size_t tmp_bytes =
       std::max(std::max(std::max(sort_tmp, scan_tmp), std::max(szscan_tmp, ascan_tmp)), pscan_tmp);
   const size_t N1 = (size_t)n + 1, NP = (size_t)n + C;  // NP: piece-pass items (ops, then chunks)
@@ -3758,7 +3666,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                                          : nullptr;
   const bool try_fast = fast_able && (fast_hook == 2 || !fpred->slow || fpred->general_runs >= kFastRetry);
   const uint32_t nwg_fast = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
-  const uint32_t ntiles_tail = (uint32_t)std::max<size_t>(1, ((size_t)n + 1023) / 1024);  // uio_fast_tail_kernel
+  const uint32_t ntiles_tail = (uint32_t)std::max<size_t>(1, ((size_t)n + 1023) / 1024);  // the tail kernels
   uint32_t hcap_fast = 256;
   while (hcap_fast < 2 * n) hcap_fast <<= 1;
   FastArgs fa{};
@@ -3799,8 +3707,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       fa.frag = carve<FragDesc>(cur, n);
       fa.key = carve<unsigned long long>(cur, n);
       fa.link = carve<uint4>(cur, n);
-      fa.head = carve<uint32_t>(cur, hcap_fast);
-      fa.hmask = hcap_fast - 1;
+      fa.hmask = hcap_fast - 1;  // (fa.head, fa.slow: the thread's FastScratch)
       fa.dv = carve<unsigned long long>(cur, n);
       fa.chain = carve<uint4>(cur, n);
       d_gran = carve<unsigned long long>(cur, (size_t)ntiles_tail * kFastCols);
@@ -3811,7 +3718,6 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   h3c_rt::DeviceLease lease1(dev, layout(nullptr));
   if (!lease1.ok()) return H3C_ERR_HIP;
   layout(lease1.data());
-  fa.slow = d_misc + kMiscSlow;
   fa.pc = pc;
   h3c_rt::PinnedLease pin(4096);
   if (!pin.ok()) return H3C_ERR_HIP;
@@ -3936,35 +3842,39 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   // uio_fast_kernel return at once (nothing written); the general pipeline below then runs the batch.
   if (try_fast) {
     const uint32_t ptiles_f = (uint32_t)(((size_t)n + C + 1 + kPrepTile - 1) / kPrepTile);
-    // (the two-launch tail writes every row of gran itself: nothing to zero there)
-    const uint32_t gwords = H3C_FAST_TAIL2 ? 0u : 2 * ntiles_tail * kFastCols;
-    const uint32_t zwords = hcap_fast + gwords + 1 + (exact ? 3u + prep_tiles : 0u);
-    const uint32_t zb = 256, zg = std::max(1u, std::min(1024u, (zwords + 4 * zb - 1) / (4 * zb)));
+    // the slow word and the bucket heads: this thread's scratch, zero between batches (the tail clears
+    // what the batch set); a new or suspect scratch is zeroed here, before the batch and outside any capture
+    FastScratch *fsc = fast_scratch(dev, kScratchHeads + (size_t)hcap_fast);
+    if (!fsc) return H3C_ERR_HIP;
+    fa.slow = fsc->p;
+    fa.head = fsc->p + kScratchHeads;
+    if (fsc->dirty) {
+      const uint32_t zw = kScratchHeads + hcap_fast, zg = std::min(1024u, (zw + 1023) / 1024);
+      hipLaunchKernelGGL(uio_zero_kernel, dim3(zg), dim3(256), 0, st, fsc->p, zw, nullptr, 0u, nullptr, 0u, nullptr, 0u);
+      HIP_TRY(hipGetLastError());
+      fsc->dirty = false;
+    }
+    ScratchGuard sguard{fsc};  // (any return before the batch's outcome is read marks it suspect)
     unsigned long long *d_ts = reinterpret_cast<unsigned long long *>(d_misc + kMiscT0);
     auto fast_kernel = [&](hipStream_t q, bool timed) -> int {
       hipLaunchKernelGGL(uio_fast_kernel, dim3(nwg_fast), dim3(kBlkThreads), 0, q, n, stdf, pc, fa.frag, fa.chain,
-                         fa.dv, d_misc, timed ? d_ts : nullptr);
+                         fa.dv, fa.slow, timed ? d_ts : nullptr, fa.key, fa.head, fa.hmask);
       HIP_TRY(hipGetLastError());
-      if (H3C_FAST_TAIL2) {
-        hipLaunchKernelGGL(uio_fast_sum_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, n, pc, fa.frag, fa.key,
-                           fa.dv, d_misc, d_gran, d_part, d_misc + kMiscErr);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(uio_fast_res_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, d_chunks, d_chunks_out,
-                           nchunks, n, poly_type, stdf, exactf, d_paycrc0 + n, pc, d_gran, d_part, d_misc, d_res,
-                           d_ctr, d_hF, (giveup & 4) ? 1u : 0u, commit_dev);
-      } else {
-        hipLaunchKernelGGL(uio_fast_tail_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, d_chunks, d_chunks_out,
-                           nchunks, n, poly_type, stdf, exactf, d_paycrc0 + n, pc, fa.frag, fa.key, fa.dv, d_misc,
-                           d_gran, d_res, d_ctr, d_hF, (giveup & 4) ? 1u : 0u, commit_dev);
-      }
+      hipLaunchKernelGGL(uio_fast_sum_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, n, pc, fa.frag, fa.key, fa.dv,
+                         fa.slow, fa.head, fa.hmask, d_gran, d_part, d_misc + kMiscErr);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(uio_fast_res_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, d_chunks, d_chunks_out,
+                         nchunks, n, poly_type, stdf, exactf, d_paycrc0 + n, pc, d_gran, d_part, d_misc, fa.slow,
+                         d_res, d_ctr, d_hF, (giveup & 4) ? 1u : 0u, commit_dev);
       HIP_TRY(hipGetLastError());
       return H3C_OK;
     };
-    auto fast_front = [&](hipStream_t q) -> int {  // zero, prep, [piece pass]
-      hipLaunchKernelGGL(uio_zero_kernel, dim3(zg), dim3(zb), 0, q, fa.head, hcap_fast,
-                         reinterpret_cast<uint32_t *>(d_gran), gwords, d_misc + kMiscSlow, 1u,
-                         exact ? d_sstate : nullptr, exact ? 3u + prep_tiles : 0u);
-      HIP_TRY(hipGetLastError());
+    auto fast_front = [&](hipStream_t q) -> int {  // [zero: exact mode's scan states], prep, [piece pass], link
+      if (exact) {
+        hipLaunchKernelGGL(uio_zero_kernel, dim3(1), dim3(256), 0, q, d_sstate, 3u + prep_tiles, nullptr, 0u, nullptr,
+                           0u, nullptr, 0u);
+        HIP_TRY(hipGetLastError());
+      }
       hipLaunchKernelGGL(uio_prep_kernel, dim3(ptiles_f), dim3(kPrepTile), 0, q, d_ios, n, d_chunks, nchunks, poly_type,
                          stdf, exactf, d_status, d_key, d_idx, d_np, d_paycrc0, d_eacc, d_ctr, d_misc, d_a6, nullptr, 0u,
                          nullptr, 0u, nullptr, nullptr, 0u, exact ? d_pbase : nullptr, exact ? d_sstate : nullptr, fa);
@@ -3975,12 +3885,12 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         if (r) return r;
       }
       hipLaunchKernelGGL(uio_fast_link_kernel, dim3((n + 255) / 256), dim3(256), 0, q, fa.link, fa.key, fa.head,
-                         fa.hmask, n, d_misc, fa.chain, d_ios, d_chunks, poly_type, stdf, pc, fa.frag);
+                         fa.hmask, n, fa.slow, fa.chain, d_ios, d_chunks, poly_type, stdf, pc, fa.frag);
       HIP_TRY(hipGetLastError());
       return H3C_OK;
     };
     const UpdGraphKey fkey{dev, poly_type, flags | 0x80000000u, n, nchunks, 0u, hcap_fast, d_chunks, d_chunks_out,
-                           d_ios, d_res, d_ctr, lease1.data(), nullptr, d_hF, nullptr};
+                           d_ios, d_res, d_ctr, lease1.data(), fsc->p, d_hF, nullptr};
     UpdGraphs *gr = upd_graphs(fkey, st, (flags & H3C_UPD_GRAPHS) != 0);
     if (gr && !gr->g && !gr->failed) {
       hipStream_t cst = capture_stream(dev);
@@ -4015,8 +3925,28 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     }
     // the outcome word polled for up to kFastPollUs before the blocking synchronisation: a blocking wait
     // that starts while the batch runs wakes ~10-20 us after it ends
-    poll_host_word(h_fs, kFastPollUs);
-    const hipError_t se = hipStreamSynchronize(st);
+    const bool seen = poll_host_word(h_fs, kFastPollUs);
+    if (seen && commit_dev && *h_fs == kFastDone && !h_F[kMiscErr - kMiscOutF]) {
+      // The device-table entry, done on the fast branch: the tail has committed the states and written
+      // every output before the outcome word, and no further work of this call follows, so the call
+      // returns without waiting for the stream's completion signal (~13 us after the last kernel ends,
+      // profiles/r04_updio_host_timeline.txt).  Later work on `stream` is ordered after the batch; other
+      // streams order themselves on an event recorded on `stream`, as for any enqueued work (h3c_crc.h).
+      // (No hipStreamQuery here: one call took ~7 us; a fault would have kept the outcome word unset.)
+      if (h3c_rt::prof_enabled()) {
+        uint64_t t0, t1;
+        std::memcpy(&t0, h_F + (kMiscT0 - kMiscOutF), 8);
+        std::memcpy(&t1, h_F + (kMiscT1 - kMiscOutF), 8);
+        const int khz = h3c_rt::device_wall_clock_khz(dev);
+        if (t1 > t0 && khz > 0) h3c_rt::prof_add(H3C_PROF_UPDIO, (float)((double)(t1 - t0) / khz), 3ull * kBlk * n);
+      }
+      g_graph_stats[kDiagFast].fetch_add(1);
+      fpred->slow = 0;
+      sguard.f = nullptr;
+      drain.armed = drain_aux.armed = false;
+      return H3C_OK;
+    }
+    const hipError_t se = stream_wait(st, kFastPollUs);
     if (se != hipSuccess) {
       drain.armed = drain_aux.armed = false;
       h3c_rt::set_error("h3c_update_ios (fast branch)", se);
@@ -4028,6 +3958,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       h3c_rt::set_error_text("h3c_update_ios: a piece table disagrees with its items (corrupt scratch)");
       return H3C_ERR_HIP;
     }
+    sguard.f = nullptr;  // the tail ran to its outcome: the scratch is clean again
     if (fs == kFastDone || fs == kFastVoid) {
       if (h3c_rt::prof_enabled()) {  // the kernel's own wall-clock span (hipEvents carry no time in a graph)
         uint64_t t0, t1;

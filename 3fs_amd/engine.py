@@ -469,6 +469,31 @@ def update_ios_dev(chunks, ios, results, type_: int = ChecksumType.CRC32C, std_d
                                   _stream_handle(stream)))
 
 
+class UpdateIosDev:
+    """update_ios_dev bound once to its tables: the checks and pointers of the first call are kept and
+    run() makes only the C call (h3c_update_ios_dev), as a C++ caller repeating a batch on the same
+    buffers does.  The tensors must stay alive and in place while the object is used."""
+
+    def __init__(self, chunks, ios, results, type_: int = ChecksumType.CRC32C, std_domain: bool = False,
+                 exact: bool = False, counters=None, stream=None, graphs: bool = False):
+        for t, rec in ((chunks, CHUNK_STATE_DTYPE), (ios, UPDATE_IO_DTYPE), (results, UPDATE_RESULT_DTYPE)):
+            if not t.is_cuda or not t.is_contiguous() or (t.numel() * t.element_size()) % rec.itemsize:
+                raise ValueError("chunks / ios / results must be contiguous GPU tensors of whole records")
+        n = ios.numel() * ios.element_size() // UPDATE_IO_DTYPE.itemsize
+        if results.numel() * results.element_size() != n * UPDATE_RESULT_DTYPE.itemsize:
+            raise ValueError("results must hold one record per op")
+        if counters is not None and (not counters.is_cuda or counters.numel() * counters.element_size() != 64):
+            raise ValueError("counters must be a GPU tensor of 8 x 64-bit")
+        flags = (UPD_STD_DOMAIN if std_domain else 0) | (UPD_EXACT if exact else 0) | (UPD_GRAPHS if graphs else 0)
+        self._keep = (chunks, ios, results, counters)
+        self._args = (int(type_), chunks.data_ptr(), chunks.numel() * chunks.element_size() // CHUNK_STATE_DTYPE.itemsize,
+                      ios.data_ptr(), n, results.data_ptr(), flags,
+                      counters.data_ptr() if counters is not None else None, _stream_handle(stream))
+
+    def run(self) -> None:
+        _check(lib.h3c_update_ios_dev(*self._args))
+
+
 READ_JOB_DTYPE = np.dtype([("data", "<u8"), ("length", "<u8"), ("chunk_len", "<u8"), ("offset", "<u4"),
                            ("chunk_value", "<u4"), ("chunk_type", "u1"), ("mem", "u1"), ("recalculate", "u1"),
                            ("reserved", "u1", 5)])

@@ -452,8 +452,11 @@ def run_updio(args, cx: Ctx) -> dict:
     d_res = torch.zeros(nw * h3c.UPDATE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=cx.dev)
     d_ctr = torch.zeros(8, dtype=torch.int64, device=cx.dev)
 
-    def step():
-        h3c.update_ios_dev(d_state, d_ios, d_res, stream=cx.stream, exact=exact, counters=d_ctr, graphs=True)
+    # (bound once: the step is the C call, as for a C++ caller; update_ios_dev re-checks the tensors).
+    # --updio-graphs picks the headline form; the other is timed beside it (`other_form`)
+    hg = bool(getattr(args, "updio_graphs", 1))
+    step = h3c.UpdateIosDev(d_state, d_ios, d_res, stream=cx.stream, exact=exact, counters=d_ctr,
+                            graphs=hg).run
 
     g0 = h3c.diag_counters()
     elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDIO)
@@ -483,16 +486,15 @@ def run_updio(args, cx: Ctx) -> dict:
     hsteps = max(1, min(args.steps, 20))
 
     def hstep():
-        h3c.update_ios(state, ios, stream=cx.stream, out=hres, exact=exact, counters=hctr, graphs=True)
+        h3c.update_ios(state, ios, stream=cx.stream, out=hres, exact=exact, counters=hctr)
 
     helapsed, _ = cx.timed(hstep, hsteps, min(args.warmup, 2), h3c.engine.PROF_UPDIO)
 
-    # the device-table step again with plain launches (graphs=False): what a caller that does not
-    # opt into H3C_UPD_GRAPHS gets
+    # the device-table step again in the other form (graphs on / off)
     d_state.copy_(torch.from_numpy(state.view(np.uint8).copy()).to(cx.dev))
 
-    def pstep():
-        h3c.update_ios_dev(d_state, d_ios, d_res, stream=cx.stream, exact=exact, counters=d_ctr, graphs=False)
+    pstep = h3c.UpdateIosDev(d_state, d_ios, d_res, stream=cx.stream, exact=exact, counters=d_ctr,
+                             graphs=not hg).run
 
     pelapsed, _ = cx.timed(pstep, hsteps, min(args.warmup, 2), h3c.engine.PROF_UPDIO)
     torch.cuda.synchronize()
@@ -525,13 +527,14 @@ def run_updio(args, cx: Ctx) -> dict:
         # the A6 check of a one-block write runs inside the block kernel on the payload it reads
         "algorithmic_gbps": round(writes * 3 * G / elapsed / 1e9, 1),
         "counters": counters,
-        "graphs": graphs,  # UpdateIO pipeline graph use over warmup + timed steps (one thread: replays)
+        "graphs": graphs,  # the headline leg's graph use over warmup + timed steps (--updio-graphs)
         "branch": "fast (uio_fast_kernel)" if fast else f"general ({fast_steps} of {args.steps + args.warmup} fast)",
         "redo": redo,
         "pcie_inclusive": {"entry": "h3c_update_ios_ex (host tables in pinned memory)",
                            "value": round(nw * hsteps * cx.world / helapsed, 1), "unit": "writes/s",
                            "ms_per_step": round(helapsed / hsteps * 1e3, 4), "steps": hsteps},
-        "graphs_off": {"entry": "h3c_update_ios_dev, graphs=False (plain launches)",
+        "other_form": {"entry": "h3c_update_ios_dev, " + ("plain launches" if hg else
+                                                           "H3C_UPD_GRAPHS: one graph replay per batch"),
                        "value": round(nw * hsteps * cx.world / pelapsed, 1), "unit": "writes/s",
                        "ms_per_step": round(pelapsed / hsteps * 1e3, 4), "steps": hsteps},
         "roofline": rl,
@@ -929,6 +932,9 @@ def main() -> int:
     ap.add_argument("--exact", action="store_true", help="updio / update: do not trust stored checksums")
     ap.add_argument("--updio-order", choices=["random", "chunk"], default="random",
                     help="updio diagnostics: chunk = the same writes grouped by chunk (sequence order within)")
+    ap.add_argument("--updio-graphs", type=int, choices=[0, 1], default=1,
+                    help="updio: the headline leg as one replayed graph per batch (1) or plain launches (0); "
+                         "the other form is timed beside it")
     ap.add_argument("--sync-threads", type=int, default=32)
     ap.add_argument("--sync-kib", default="4,128,1024", help="sync: buffer sizes (KiB), comma-separated")
     args = ap.parse_args()
@@ -951,7 +957,9 @@ def main() -> int:
     fn = {"verify": run_verify, "update": run_update, "updio": run_updio, "hostfed": run_hostfed,
           "shard4m": run_shard4m, "mixed": run_mixed, "sync": run_sync}[args.workload]
     if args.workload in ("hostfed", "updio") and args.steps == 50:
-        args.steps, args.warmup = (5, 1) if args.workload == "hostfed" else (10, 2)
+        # (updio: a batch is ~0.34 ms; 100 timed batches after 20 warm ones -- 10 after 2 left the timed
+        # leg within the GPU's clock ramp, ~2-3 % slower than the same leg run later)
+        args.steps, args.warmup = (5, 1) if args.workload == "hostfed" else (100, 20)
     res = fn(args, cx)
     if args.workload == "verify" and args.hostfed_extra_gib > 0 and (args.chunks, args.chunk_kib) == (8192, 1024):
         # BASELINE asks for host-fed throughput at 1/2/4/8 GPUs too: the driver's scaling runs

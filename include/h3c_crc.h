@@ -301,8 +301,12 @@ int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchun
                       void *stream);
 /* The same with every array in device memory (chunk table in / out, ops, results, counters -- the
  * latter may be NULL): for callers whose op tables already live in HBM; no PCIe traffic.  A chunk
- * whose size exceeds its chunk_size fails its ops with H3C_ERR_INVALID_ARG.  Synchronous on
- * `stream` (the host reads the fragment count back once, at the end). */
+ * whose size exceeds its chunk_size fails its ops with H3C_ERR_INVALID_ARG.  Returns once the
+ * batch's outcome is known (the host reads its outcome words back once, at the end): every output
+ * is then complete for work ordered after the batch on `stream`; work on another stream orders
+ * itself with an event recorded on `stream`.  (On the fast branch the call returns when the last
+ * kernel has written its outputs and its outcome, without waiting for the stream's completion
+ * signal; other paths synchronise the stream.) */
 int h3c_update_ios_dev(uint8_t poly_type, h3c_chunk_state *chunks_dev, uint32_t nchunks, const h3c_update_io *ios_dev,
                        uint32_t n, h3c_update_result *results_dev, uint32_t flags, h3c_update_counters *counters_dev,
                        void *stream);

@@ -8,7 +8,7 @@ O=gpurun_out
 T="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
 timeout -k 10 600 $T tests/test_gpu_updio_fast.py tests/test_gpu_update.py > $O/r04h_fast.log 2>&1 || { echo FAST_TESTS_FAIL; tail -40 $O/r04h_fast.log; exit 1; }
 grep -c PASSED $O/r04h_fast.log
-line() { tail -1 $1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$2', d['ms_per_step'], d['roofline']['kernel_avg_us'], d['graphs_off']['ms_per_step'], d['branch'][:4], d['verified'])"; }
+line() { tail -1 $1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$2', d['ms_per_step'], d['roofline']['kernel_avg_us'], d['other_form']['ms_per_step'], d['branch'][:4], d['verified'])"; }
 for rep in 1 2; do
   timeout -k 10 300 python -u bench.py --workload updio --no-cpu-baseline > $O/r04h_cur.jsonl 2> $O/r04h_cur.err || { echo BENCH_FAIL; tail -20 $O/r04h_cur.err; exit 1; }
   line $O/r04h_cur.jsonl cur

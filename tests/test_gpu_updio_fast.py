@@ -287,8 +287,12 @@ def test_fast_branch_repeated_batches(h3c, torch_dev, hooks, graphs):
     d_res = torch.zeros(len(ios) * 16, dtype=torch.uint8, device=dev)
     d_ctr = torch.zeros(8, dtype=torch.int64, device=dev)
     b = h3c.diag_counters()
+    bound = h3c.UpdateIosDev(d_chunks, d_ios, d_res, counters=d_ctr, graphs=graphs)  # (odd batches: the bound call)
     for k in range(5):
-        h3c.update_ios_dev(d_chunks, d_ios, d_res, counters=d_ctr, graphs=graphs)
+        if k % 2:
+            bound.run()
+        else:
+            h3c.update_ios_dev(d_chunks, d_ios, d_res, counters=d_ctr, graphs=graphs)
         torch.cuda.synchronize()
         fin = d_chunks.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)
         got = sc.slab.cpu().numpy()
