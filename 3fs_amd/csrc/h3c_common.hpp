@@ -29,12 +29,20 @@ int device_wall_clock_khz(int dev);  // the rate of the device's wall_clock64() 
 int current_device(int *dev);
 void set_error(const char *what, hipError_t e);
 void set_error_text(const char *text);
-// Profiling hooks (h3c_profile_enable): event pair around a launch, per kind.
+// Profiling hooks (h3c_profile_enable), per kind.  prof_stamp: the kernel stamps its own first
+// workgroup start and last workgroup end on the device wall clock into a slot (`ts`, passed to
+// the kernel; stamp_begin / stamp_end) -- nothing is added to the stream.  prof_begin: an event
+// pair around the launch (for pipelines of copies and kernels; an event record costs the stream
+// ~6 us, profiles/r04_*_rocprof_kernel_stats.csv timelines).
 struct ProfToken {
   bool on = false;
   hipEvent_t a = nullptr, b = nullptr;
+  unsigned long long *ts = nullptr;  // prof_stamp's slot (device), or nullptr
+  int dev = -1;
+  int slot = -1;
 };
 hipError_t prof_begin(hipStream_t st, ProfToken &t);
+hipError_t prof_stamp(int dev, ProfToken &t);
 hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes);
 // For launches timed by hipEvents recorded inside a replayed graph: whether profiling is on, and
 // one launch's measured time added to the totals.
@@ -322,6 +330,19 @@ inline void set_fold_consts(DevChunk &c, uint64_t seg_bytes, uint32_t poly) {
 }
 
 // ---------------------------------------------------------------- device GF(2)
+// h3c_rt::prof_stamp's kernel side: the first workgroup's start (atomicMin) and the last
+// workgroup's end (atomicMax) on the device wall clock; one atomic each per workgroup.  The
+// stamped kernels are wrappers around a body function, so every wave reaches stamp_end (a body's
+// early return comes back to it); the bodies have no barrier after their early returns.
+__device__ __forceinline__ void stamp_begin(unsigned long long *ts) {
+  if (ts && threadIdx.x == 0) atomicMin(&ts[0], (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void stamp_end(unsigned long long *ts) {
+  if (!ts) return;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&ts[1], (unsigned long long)wall_clock64());
+}
+
 __device__ __forceinline__ uint32_t dgf_mul(uint32_t a, uint32_t b, uint32_t poly) {
   uint32_t p = 0;
 #pragma unroll 4

@@ -52,7 +52,7 @@
 namespace {
 
 // Kernel A: one wave per segment; waves take contiguous segment ranges.
-__global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+__device__ __forceinline__ void seg_crc_kernel_body(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                            uint32_t total_segs, uint64_t seg_bytes, uint32_t dbg,
                                                            const PolyConsts *__restrict__ pc,
                                                            uint32_t *__restrict__ seg_crc) {
@@ -94,6 +94,15 @@ __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__res
     if (lane == 0) seg_crc[s] = v;
   }
 }
+__global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+                                                           uint32_t total_segs, uint64_t seg_bytes, uint32_t dbg,
+                                                           const PolyConsts *__restrict__ pc,
+                                                           uint32_t *__restrict__ seg_crc,
+                                                           unsigned long long *ts) {  // ts: h3c_rt::prof_stamp's slot, or nullptr
+  stamp_begin(ts);
+  seg_crc_kernel_body(chunks, nchunks, total_segs, seg_bytes, dbg, pc, seg_crc);
+  stamp_end(ts);
+}
 
 // Kernel A': batches whose every chunk is one short segment (<= kSmallRows rows, e.g. 4 KiB
 // read / write buffers).  Per segment the big kernel pays dependent metadata loads and a
@@ -124,7 +133,7 @@ __device__ __forceinline__ uint4 mask_row(uint4 v, uint64_t a, uint64_t S, uint6
 }
 
 template <int R>
-__global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+__device__ __forceinline__ void seg_small_kernel_body(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                              const PolyConsts *__restrict__ pc,
                                                              const uint32_t *__restrict__ expected,
                                                              uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
@@ -233,6 +242,17 @@ __global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__r
     }
   }
 }
+template <int R>
+__global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+                                                             const PolyConsts *__restrict__ pc,
+                                                             const uint32_t *__restrict__ expected,
+                                                             uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                                             uint32_t *__restrict__ mismatch,
+                                                             unsigned long long *ts) {  // ts: h3c_rt::prof_stamp's slot, or nullptr
+  stamp_begin(ts);
+  seg_small_kernel_body<R>(chunks, nchunks, pc, expected, out_raw, ok, mismatch);
+  stamp_end(ts);
+}
 
 // Kernel A'': the same batches with several chunks per wave.  A group of G lanes owns one
 // chunk and walks it in rows of 16*G bytes (tables with stride x^(8*16*G)); the 64/G
@@ -289,7 +309,7 @@ __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) { return (u
 // G lanes per chunk, each reading W adjacent 16-byte pieces of a row of 16*G*W bytes
 // (16 x 1: 256-byte rows, four chunks per wave; 4 x 1: 64-byte rows, sixteen chunks).
 template <int G, int W>
-__global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+__device__ __forceinline__ void seg_quad_kernel_body(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                            const PolyConsts *__restrict__ pc,
                                                            const uint32_t *__restrict__ expected,
                                                            uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
@@ -449,6 +469,17 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
     m = n;
   }
 }
+template <int G, int W>
+__global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+                                                           const PolyConsts *__restrict__ pc,
+                                                           const uint32_t *__restrict__ expected,
+                                                           uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                                           uint32_t *__restrict__ mismatch,
+                                                            unsigned long long *ts) {  // ts: h3c_rt::prof_stamp's slot, or nullptr
+  stamp_begin(ts);
+  seg_quad_kernel_body<G, W>(chunks, nchunks, pc, expected, out_raw, ok, mismatch);
+  stamp_end(ts);
+}
 
 // Kernel A4: seg_quad_kernel<G, 1> for a batch whose chunks all have one length, a multiple of
 // the 16*G-byte row, at row-aligned addresses, with one start value -- a plan or verify of
@@ -461,7 +492,7 @@ __global__ __launch_bounds__(kThreads) void seg_quad_kernel(const DevChunk *__re
 // reads at ~7.0 TB/s against ~6.1 TB/s for 4 lanes' 64-byte rows) while a wave step still
 // covers 16 chunks and their folds overlap (profiles/r02_small_pattern_ceiling.txt).
 template <int G, int C = 1>
-__global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni_kernel(const DevChunk *__restrict__ chunks, uint64_t base,
+__device__ __forceinline__ void seg_uni_kernel_body(const DevChunk *__restrict__ chunks, uint64_t base,
                                                           uint64_t stride, uint32_t nchunks, uint32_t K, uint32_t xs,
                                                           const PolyConsts *__restrict__ pc,
                                                           const uint32_t *__restrict__ expected,
@@ -630,6 +661,18 @@ __global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni
     q0 = qn;
 #endif
   }
+}
+template <int G, int C = 1>
+__global__ __launch_bounds__(kUniThreads, kUniCopies == 16 ? 6 : 1) void seg_uni_kernel(const DevChunk *__restrict__ chunks, uint64_t base,
+                                                          uint64_t stride, uint32_t nchunks, uint32_t K, uint32_t xs,
+                                                          const PolyConsts *__restrict__ pc,
+                                                          const uint32_t *__restrict__ expected,
+                                                          uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                                          uint32_t *__restrict__ mismatch,
+                                                                                        unsigned long long *ts) {  // ts: h3c_rt::prof_stamp's slot, or nullptr
+  stamp_begin(ts);
+  seg_uni_kernel_body<G, C>(chunks, base, stride, nchunks, K, xs, pc, expected, out_raw, ok, mismatch);
+  stamp_end(ts);
 }
 
 // Kernel A''': CRCs of ranges listed in device memory, without host-built descriptors (the
@@ -995,15 +1038,25 @@ void set_error_text(const char *text) { g_last_error = text; }
 
 namespace {
 
-// ---- profiling: HIP event pairs around the hot kernels, per kind ----
+// ---- profiling: the hot kernels' own wall-clock stamps (or event pairs), per kind ----
 struct ProfRec {
-  hipEvent_t a, b;
+  hipEvent_t a, b;  // (event records)
   uint64_t bytes;
   int kind;
+  int dev = -1, slot = -1;  // (stamp records: a slot of the device's stamp pool)
+};
+// Per device: kProfSlots stamp slots {first start, last end}, {~0, 0} when free; handed out in
+// order between h3c_profile_read calls (which read them back and free them).  A launch past the
+// last slot is not timed.
+constexpr int kProfSlots = 8192;
+struct StampPool {
+  unsigned long long *d = nullptr;
+  int next = 0;
 };
 constexpr int kProfKinds = 4;
 std::mutex g_prof_mu;
 std::vector<ProfRec> g_prof;
+StampPool g_stamps[kMaxDevices];
 std::atomic<int> g_prof_on{0};
 double g_prof_ms_done[kProfKinds] = {0, 0, 0, 0};
 uint64_t g_prof_launch_done[kProfKinds] = {0, 0, 0, 0}, g_prof_bytes_done[kProfKinds] = {0, 0, 0, 0};
@@ -1102,8 +1155,39 @@ hipError_t prof_begin(hipStream_t st, ProfToken &t) {
   if (e == hipSuccess) e = hipEventRecord(t.a, st);
   return e;
 }
+hipError_t prof_stamp(int dev, ProfToken &t) {
+  t.on = g_prof_on.load() != 0;
+  t.ts = nullptr;
+  if (!t.on || dev < 0 || dev >= kMaxDevices) return hipSuccess;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  StampPool &p = g_stamps[dev];
+  if (!p.d) {
+    std::vector<unsigned long long> init(2 * kProfSlots);
+    for (int i = 0; i < kProfSlots; ++i) init[2 * i] = ~0ull, init[2 * i + 1] = 0;
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p.d), init.size() * 8);
+    if (e == hipSuccess) e = hipMemcpy(p.d, init.data(), init.size() * 8, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      p.d = nullptr;
+      return e;
+    }
+  }
+  if (p.next >= kProfSlots) return hipSuccess;  // (pool used up: this launch is not timed)
+  t.dev = dev;
+  t.slot = p.next++;
+  t.ts = p.d + 2 * t.slot;
+  return hipSuccess;
+}
 hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes) {
   if (!t.on) return hipSuccess;
+  if (t.ts) {  // stamped by the kernel itself
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    ProfRec r{nullptr, nullptr, bytes, kind};
+    r.dev = t.dev;
+    r.slot = t.slot;
+    g_prof.push_back(r);
+    return hipSuccess;
+  }
+  if (!t.a) return hipSuccess;  // (a stamped launch with no slot left)
   hipError_t e = hipEventRecord(t.b, st);
   std::lock_guard<std::mutex> lk(g_prof_mu);
   g_prof.push_back(ProfRec{t.a, t.b, bytes, kind});
@@ -1129,44 +1213,44 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
   if (small_rows && nchunks && !(dbg & 2u)) {  // test hook: H3C_DEBUG_FLAGS bit1 disables it
     const uint32_t blocks = std::min<uint32_t>(ctx.num_cu, (nchunks + kWavesPerBlock - 1) / kWavesPerBlock);
     ProfToken tok;
-    if (prof_kind >= 0) HIP_TRY(prof_begin(st, tok));
+    if (prof_kind >= 0) HIP_TRY(prof_stamp(dev, tok));
     if (H3C_SMALL_QUAD && uni && uni->lanes && !(dbg & 4u)) {  // test hook: H3C_DEBUG_FLAGS bit2 disables it
       const DevChunk *dc = uni->contiguous ? nullptr : d_chunks;
       const uint32_t ublocks = std::min<uint32_t>(ctx.num_cu * (kUniCopies == 16 ? 2 : 1),
                                                   (nchunks + kUniWaves - 1) / kUniWaves);
       if (uni->lanes == 1)
         hipLaunchKernelGGL(seg_uni_kernel<1>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
-                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch, tok.ts);
       else if (uni->lanes == 2)
         hipLaunchKernelGGL(seg_uni_kernel<2>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
-                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch, tok.ts);
       else if (uni->lanes == 4)
         hipLaunchKernelGGL(seg_uni_kernel<4>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
-                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch, tok.ts);
       else if (uni->lanes == 8 && uni->pair)
         hipLaunchKernelGGL((seg_uni_kernel<8, 2>), dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
-                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch, tok.ts);
       else if (uni->lanes == 8)
         hipLaunchKernelGGL(seg_uni_kernel<8>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
-                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch, tok.ts);
       else
         hipLaunchKernelGGL(seg_uni_kernel<16>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
-                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch);
+                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch, tok.ts);
     } else if (H3C_SMALL_QUAD)
       // up to ~5 KiB chunks 4 lanes per chunk (4 KiB: +8 % over 8 lanes, +13 % over 16);
       // 16 lanes above (4 lanes lose 10 % at 8 and 16 KiB): profiles/r01d_small_lanes_ab.txt
       if (small_rows <= 6)
         hipLaunchKernelGGL((seg_quad_kernel<H3C_SMALL_LANES_LO, H3C_SMALL_PIECES_LO>), dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks,
-                           pc, expected, out_raw, ok, mismatch);
+                           pc, expected, out_raw, ok, mismatch, tok.ts);
       else
         hipLaunchKernelGGL((seg_quad_kernel<H3C_SMALL_LANES_HI, H3C_SMALL_PIECES_HI>), dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
-                           out_raw, ok, mismatch);
+                           out_raw, ok, mismatch, tok.ts);
     else if (small_rows <= 4)
       hipLaunchKernelGGL(seg_small_kernel<4>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
-                         out_raw, ok, mismatch);
+                         out_raw, ok, mismatch, tok.ts);
     else
       hipLaunchKernelGGL(seg_small_kernel<8>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
-                         out_raw, ok, mismatch);
+                         out_raw, ok, mismatch, tok.ts);
     HIP_TRY(hipGetLastError());
     if (prof_kind >= 0) HIP_TRY(prof_end(st, tok, prof_kind, payload_bytes));
     return H3C_OK;
@@ -1174,9 +1258,9 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
   if (total_segs) {
     const uint32_t blocks = std::min<uint32_t>(ctx.num_cu, (total_segs + kWavesPerBlock - 1) / kWavesPerBlock);
     ProfToken tok;
-    if (prof_kind >= 0) HIP_TRY(prof_begin(st, tok));
+    if (prof_kind >= 0) HIP_TRY(prof_stamp(dev, tok));
     hipLaunchKernelGGL(seg_crc_kernel, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, total_segs, seg_bytes,
-                       dbg, pc, d_segcrc);
+                       dbg, pc, d_segcrc, tok.ts);
     HIP_TRY(hipGetLastError());
     if (prof_kind >= 0) HIP_TRY(prof_end(st, tok, prof_kind, payload_bytes));
   }
@@ -1450,7 +1534,39 @@ void h3c_profile_enable(int on) { g_prof_on.store(on ? 1 : 0); }
 int h3c_profile_read(int kind, double *kernel_ms, uint64_t *launches, uint64_t *bytes, int reset) {
   if (kind < 0 || kind >= kProfKinds) return H3C_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(g_prof_mu);
+  // the stamp slots in use, per device: read back once every launch has ended, then freed
+  for (int d = 0; d < kMaxDevices; ++d) {
+    StampPool &p = g_stamps[d];
+    if (!p.d || !p.next) continue;
+    int prev = -1;
+    HIP_TRY(hipGetDevice(&prev));
+    HIP_TRY(hipSetDevice(d));
+    std::vector<unsigned long long> v(2 * (size_t)p.next);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(v.data(), p.d, v.size() * 8, hipMemcpyDeviceToHost);
+    std::vector<unsigned long long> init(v.size());
+    for (size_t i = 0; i < init.size(); i += 2) init[i] = ~0ull, init[i + 1] = 0;
+    if (e == hipSuccess) e = hipMemcpy(p.d, init.data(), init.size() * 8, hipMemcpyHostToDevice);
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+      set_error("h3c_profile_read (stamps)", e);
+      return H3C_ERR_HIP;
+    }
+    const int khz = h3c_rt::device_wall_clock_khz(d);
+    for (auto &r : g_prof) {
+      if (r.dev != d || r.slot < 0) continue;
+      const unsigned long long t0 = v[2 * (size_t)r.slot], t1 = v[2 * (size_t)r.slot + 1];
+      if (t1 > t0 && t0 != ~0ull && khz > 0) {
+        g_prof_ms_done[r.kind] += (double)(t1 - t0) / khz;
+        g_prof_launch_done[r.kind] += 1;
+        g_prof_bytes_done[r.kind] += r.bytes;
+      }
+      r.slot = -2;  // (done)
+    }
+    p.next = 0;
+  }
   for (auto &r : g_prof) {
+    if (r.slot != -1) continue;  // (stamp records were read above)
     HIP_TRY(hipEventSynchronize(r.b));
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));

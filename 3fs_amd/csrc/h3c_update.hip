@@ -247,7 +247,7 @@ __device__ uint32_t delta_crc0(uint64_t pnew, uint64_t pold, uint64_t dst, uint6
   return wave_fold_tab(st, lane, red);
 }
 
-__global__ __launch_bounds__(kThreads) void upd_delta_kernel(
+__device__ __forceinline__ void upd_delta_kernel_body(
     const uint64_t *__restrict__ chunk_base, uint32_t nchunks, uint32_t bpc, uint32_t block_bytes,
     const uint32_t *__restrict__ blk_chunk, const uint32_t *__restrict__ blk_index, const uint8_t *payload,
     uint32_t n, const uint32_t *__restrict__ prev, const uint32_t *__restrict__ final_of,
@@ -377,6 +377,16 @@ __global__ __launch_bounds__(kThreads) void upd_delta_kernel(
     }
   }
 }
+__global__ __launch_bounds__(kThreads) void upd_delta_kernel(
+    const uint64_t *__restrict__ chunk_base, uint32_t nchunks, uint32_t bpc, uint32_t block_bytes,
+    const uint32_t *__restrict__ blk_chunk, const uint32_t *__restrict__ blk_index, const uint8_t *payload,
+    uint32_t n, const uint32_t *__restrict__ prev, const uint32_t *__restrict__ final_of,
+    const PolyConsts *__restrict__ pc, uint32_t *__restrict__ delta,
+                                                             unsigned long long *ts) {  // ts: h3c_rt::prof_stamp's slot, or nullptr
+  stamp_begin(ts);
+  upd_delta_kernel_body(chunk_base, nchunks, bpc, block_bytes, blk_chunk, blk_index, payload, n, prev, final_of, pc, delta);
+  stamp_end(ts);
+}
 
 // ---- fused path: links, deltas, write-back and per-chunk prefix in one launch ----
 constexpr uint32_t kFusedCols = 128;    // chunk columns of the look-back: lane c holds chunks c and c + 64
@@ -405,7 +415,7 @@ __device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
 // from the tile link or the hash of per-tile last writers -- then the wave walks the group as
 // upd_delta_kernel does.  Afterwards each write's v = delta * sh[b] is folded into the running
 // XOR of its chunk (lane c mod 64), whose value right after the write is kept in inpre[i].
-__global__ __launch_bounds__(kThreads) void upd_fused_kernel(
+__device__ __forceinline__ void upd_fused_kernel_body(
     const uint64_t *__restrict__ chunk_base, uint32_t nchunks, uint32_t bpc, const uint32_t *__restrict__ blk_chunk,
     const uint32_t *__restrict__ blk_index, const uint8_t *payload, uint32_t n, const uint32_t *__restrict__ prev,
     const uint32_t *__restrict__ hhead, uint32_t hmask, const uint32_t *__restrict__ nkey,
@@ -692,6 +702,20 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
     const uint32_t x0 = __shfl(be0, c & 63, 64), x1 = __shfl(be1, c & 63, 64);
     if (i < hi) out_raw[i] = ok ? (c < 64 ? x0 : x1) ^ inpre[i] : 0u;
   }
+}
+__global__ __launch_bounds__(kThreads) void upd_fused_kernel(
+    const uint64_t *__restrict__ chunk_base, uint32_t nchunks, uint32_t bpc, const uint32_t *__restrict__ blk_chunk,
+    const uint32_t *__restrict__ blk_index, const uint8_t *payload, uint32_t n, const uint32_t *__restrict__ prev,
+    const uint32_t *__restrict__ hhead, uint32_t hmask, const uint32_t *__restrict__ nkey,
+    const uint32_t *__restrict__ next, const uint32_t *__restrict__ sh, const PolyConsts *__restrict__ pc,
+    const uint32_t *__restrict__ raw_base, const uint32_t *__restrict__ raw_in, uint32_t exact, uint32_t reuse_case,
+    const uint32_t *__restrict__ touched, uint32_t *ctl, uint64_t *gran, uint32_t *__restrict__ inpre,
+    uint32_t *__restrict__ out_raw, uint32_t *__restrict__ raw_out, uint32_t *__restrict__ n_invalid,
+    unsigned long long *__restrict__ counters, uint32_t force_timeout,
+                                                             unsigned long long *ts) {  // ts: h3c_rt::prof_stamp's slot, or nullptr
+  stamp_begin(ts);
+  upd_fused_kernel_body(chunk_base, nchunks, bpc, blk_chunk, blk_index, payload, n, prev, hhead, hmask, nkey, next, sh, pc, raw_base, raw_in, exact, reuse_case, touched, ctl, gran, inpre, out_raw, raw_out, n_invalid, counters, force_timeout);
+  stamp_end(ts);
 }
 
 // H3C_UPD_EXACT: create descriptors for the chunk set (uniform length, start 0).
@@ -1074,12 +1098,12 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
   if (rc) return rc;
   if (path == kPathFused) {
     h3c_rt::ProfToken tok;
-    HIP_TRY(h3c_rt::prof_begin(st, tok));
+    HIP_TRY(h3c_rt::prof_stamp(dev, tok));
     hipLaunchKernelGGL(upd_fused_kernel, dim3(fused_wg), dim3(kThreads), 0, st, chunk_base_dev, nchunks, bpc,
                        blk_chunk_dev, blk_index_dev, static_cast<const uint8_t *>(payload_dev), n_blocks, w.prev,
                        w.hhead, w.hcap - 1, w.nkey, w.next, sh, pc, raw_base, chunk_raw_in_dev, exact ? 1u : 0u,
                        reuse_case, w.touched, w.ctl, w.gran, w.scan, out_raw_dev, chunk_raw_out_dev, n_invalid_dev,
-                       counters_dev, (uint32_t)(h3c_rt::hook(H3C_HOOK_UPD_LOOKBACK) == 1));
+                       counters_dev, (uint32_t)(h3c_rt::hook(H3C_HOOK_UPD_LOOKBACK) == 1), tok.ts);
     HIP_TRY(hipGetLastError());
     // algorithmic bytes: read new + read old + write back, per block write
     HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDATE, 3ull * block_bytes * n_blocks));
@@ -1090,10 +1114,10 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
   HIP_TRY(hipGetLastError());
   const uint32_t blocks = std::min<uint32_t>(num_cu, (n_blocks + kWavesPerBlock - 1) / kWavesPerBlock);
   h3c_rt::ProfToken tok;
-  HIP_TRY(h3c_rt::prof_begin(st, tok));
+  HIP_TRY(h3c_rt::prof_stamp(dev, tok));
   hipLaunchKernelGGL(upd_delta_kernel, dim3(blocks), dim3(kThreads), 0, st, chunk_base_dev, nchunks, bpc, block_bytes,
                      blk_chunk_dev, blk_index_dev, static_cast<const uint8_t *>(payload_dev), n_blocks, w.prev,
-                     w.final_of, pc, w.delta);
+                     w.final_of, pc, w.delta, tok.ts);
   HIP_TRY(hipGetLastError());
   HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDATE, 3ull * block_bytes * n_blocks));
   if (path == kPathTiles) {
