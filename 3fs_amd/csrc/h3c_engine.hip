@@ -51,11 +51,19 @@
 
 namespace {
 
-// Kernel A: one wave per segment; waves take contiguous segment ranges.
+#ifndef H3C_SEG_FUSE_FIN
+#define H3C_SEG_FUSE_FIN 1  // batches of one segment per chunk finish in seg_crc_kernel (0: finalize_kernel, A/B)
+#endif
+// Kernel A: one wave per segment; waves take contiguous segment ranges.  With `fin` (every chunk
+// exactly one segment: config 2's 1 MiB chunks) the wave finishes its chunk itself -- the init's
+// share, the result, the verify flag and count -- and no finalize launch follows.
 __device__ __forceinline__ void seg_crc_kernel_body(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                            uint32_t total_segs, uint64_t seg_bytes, uint32_t dbg,
                                                            const PolyConsts *__restrict__ pc,
-                                                           uint32_t *__restrict__ seg_crc) {
+                                                           uint32_t *__restrict__ seg_crc, uint32_t fin,
+                                                           const uint32_t *__restrict__ expected,
+                                                           uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                                           uint32_t *__restrict__ mismatch) {
   __shared__ alignas(16) uint32_t lds[kLdsWords + (H3C_SEG_FOLD_TAB ? kRedWords : 0)];
   fill_tables(lds, pc->tab, &pc->red[0][0][0], H3C_SEG_FOLD_TAB ? kRedWords : 0, threadIdx.x, kThreads);
   __syncthreads();
@@ -90,17 +98,38 @@ __device__ __forceinline__ void seg_crc_kernel_body(const DevChunk *__restrict__
     const uint64_t len = chunks[c].len;
     const uint64_t S = p + k * seg_bytes;
     const uint64_t E = p + min(len, (k + 1) * seg_bytes);
+    // (fin: the chunk's result slot, init share and expected value, loaded before the segment so
+    // that their round trip overlaps it)
+    uint32_t idx = 0, xs = 0, ex = 0;
+    if (fin) {
+      idx = chunks[c].out_idx;
+      xs = (chunks[c].flags & kFlagNone) ? 0u : chunks[c].xstart;
+      if (expected) ex = expected[idx];
+    }
     const uint32_t v = segment_crc0(S, E, lane, lb, L, fix, red, pc, poly, dbg);
-    if (lane == 0) seg_crc[s] = v;
+    if (!fin) {
+      if (lane == 0) seg_crc[s] = v;
+    } else if (lane == 0) {  // (finalize_kernel's one-segment case)
+      const uint32_t raw = (chunks[c].flags & kFlagNone) ? 0u : v ^ xs;
+      out_raw[idx] = raw;
+      if (expected) {
+        const bool good = raw == ex;
+        ok[idx] = good ? 1 : 0;
+        if (!good && mismatch) atomicAdd(mismatch, 1u);
+      }
+    }
   }
 }
 __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                            uint32_t total_segs, uint64_t seg_bytes, uint32_t dbg,
                                                            const PolyConsts *__restrict__ pc,
-                                                           uint32_t *__restrict__ seg_crc,
+                                                           uint32_t *__restrict__ seg_crc, uint32_t fin,
+                                                           const uint32_t *__restrict__ expected,
+                                                           uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
+                                                           uint32_t *__restrict__ mismatch,
                                                            unsigned long long *ts) {  // ts: h3c_rt::prof_stamp's slot, or nullptr
   stamp_begin(ts);
-  seg_crc_kernel_body(chunks, nchunks, total_segs, seg_bytes, dbg, pc, seg_crc);
+  seg_crc_kernel_body(chunks, nchunks, total_segs, seg_bytes, dbg, pc, seg_crc, fin, expected, out_raw, ok, mismatch);
   stamp_end(ts);
 }
 
@@ -1255,15 +1284,18 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
     if (prof_kind >= 0) HIP_TRY(prof_end(st, tok, prof_kind, payload_bytes));
     return H3C_OK;
   }
+  // every chunk exactly one segment: the segment kernel finishes the chunks (no finalize launch)
+  const bool fin = H3C_SEG_FUSE_FIN && total_segs && total_segs == nchunks && max_chunk_segs == 1;
   if (total_segs) {
     const uint32_t blocks = std::min<uint32_t>(ctx.num_cu, (total_segs + kWavesPerBlock - 1) / kWavesPerBlock);
     ProfToken tok;
     if (prof_kind >= 0) HIP_TRY(prof_stamp(dev, tok));
     hipLaunchKernelGGL(seg_crc_kernel, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, total_segs, seg_bytes,
-                       dbg, pc, d_segcrc, tok.ts);
+                       dbg, pc, d_segcrc, fin ? 1u : 0u, expected, out_raw, ok, mismatch, tok.ts);
     HIP_TRY(hipGetLastError());
     if (prof_kind >= 0) HIP_TRY(prof_end(st, tok, prof_kind, payload_bytes));
   }
+  if (fin) return H3C_OK;
   const uint32_t seg_mul = hxpow8n(seg_bytes, poly);
   const uint32_t fb = (nchunks + 255) / 256;
   hipLaunchKernelGGL(finalize_kernel, dim3(fb), dim3(256), 0, st, d_chunks, nchunks, total_segs, seg_mul,
