@@ -302,6 +302,7 @@ __device__ void fast_prep_tile(const FastArgs &fa, uint32_t i, uint32_t n, const
 #define H3C_PREP_TILE 1024  // items per prep-kernel tile (a power of two, 64..1024)
 #endif
 constexpr uint32_t kPrepTile = H3C_PREP_TILE;
+constexpr uint32_t kFastChunksLds = 128;  // (= kFastCols: the chunks a fast-branch batch may name)
 __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
     const h3c_update_io *__restrict__ ios, uint32_t n, const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks,
     uint8_t poly_type, uint32_t std_domain, uint32_t exact, uint32_t *__restrict__ status, uint32_t *__restrict__ key,
@@ -327,8 +328,17 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
   if (i < kCtrN) ctr[i] = 0;
   if (i < kMiscSlow) misc[i] = i == kMiscT0 || i == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;  // (kMiscSlow: uio_zero_kernel)
   // the fast branch without the piece pass (not exact): only the validation feeds it (fast_prep_tile);
-  // the general pipeline's arrays are not written (a batch that leaves the branch runs its own prep)
+  // the general pipeline's arrays are not written (a batch that leaves the branch runs its own prep).
+  // Its chunk table (<= kFastCols states) is read into LDS beside the ops' loads, so an op's chunk
+  // state is not a second round trip after its op record.
   const bool lean = fa.head && !pbase;
+  __shared__ h3c_chunk_state s_cs[kFastChunksLds];
+  h3c_update_io io_pre{};
+  if (i < n) io_pre = ios[i];
+  if (lean) {
+    if (threadIdx.x < nchunks && threadIdx.x < kFastChunksLds) s_cs[threadIdx.x] = chunks[threadIdx.x];
+    __syncthreads();
+  }
   // chunk items n + c for c < C = max(nchunks, 1) (the piece pass's NP = n + C items), then the
   // scan's extra entry: pbase[n + C] = total
   const uint32_t C = nchunks ? nchunks : 1u;
@@ -353,7 +363,7 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
       eacc[2 * i + 1] = 0;
       a6[i] = 0;       // A6 verdicts (the early pass, the front / late checks, the block kernel)
     }
-    const h3c_update_io io = ios[i];
+    const h3c_update_io io = io_pre;
     uint32_t st = H3C_OK;
     const uint32_t c = io.chunk;
     const bool kind_ok = io.kind == H3C_UPD_WRITE || io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND ||
@@ -361,7 +371,7 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
     if (c >= nchunks || !kind_ok) {
       st = H3C_ERR_INVALID_ARG;
     } else if (io.kind != H3C_UPD_COMMIT) {
-      const h3c_chunk_state cs = chunks[c];
+      const h3c_chunk_state cs = lean ? s_cs[c] : chunks[c];
       const bool syncing = (io.flags & H3C_IO_SYNCING) != 0;
       if (!cs.base || (io.checksum_type != H3C_TYPE_NONE && io.checksum_type != poly_type)) st = H3C_ERR_INVALID_ARG;
       if (cs.size > cs.chunk_size) st = H3C_ERR_INVALID_ARG;  // a corrupt chunk state
@@ -397,7 +407,7 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
     }
     f_io = io;
     f_st = st;
-    if (c < nchunks) f_cs = chunks[c];
+    if (c < nchunks) f_cs = lean ? s_cs[c] : chunks[c];
   }
   if (fa.head) fast_prep_tile(fa, i, n, f_io, f_cs, f_st, poly_type, std_domain);  // (the whole workgroup)
   if (!pbase) return;
@@ -2366,13 +2376,25 @@ __global__ void uio_fast_link_kernel(const uint4 *__restrict__ link, const unsig
                                      const uint32_t *__restrict__ bhead, uint32_t hmask, uint32_t n,
                                      const uint32_t *__restrict__ slow, uint4 *__restrict__ chain,
                                      const h3c_update_io *__restrict__ ios, const h3c_chunk_state *__restrict__ chunks,
-                                     uint8_t poly_type, uint32_t std_domain, const PolyConsts *__restrict__ pc,
-                                     FragDesc *__restrict__ frag) {
+                                     uint32_t nchunks, uint8_t poly_type, uint32_t std_domain,
+                                     const PolyConsts *__restrict__ pc, FragDesc *__restrict__ frag) {
+  // the chunk table (<= 128 states) into LDS beside the op's own loads: its chunk state is not a
+  // second round trip after the op record
+  __shared__ h3c_chunk_state s_cs[kFastChunksLds];
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  h3c_update_io io{};
+  uint4 lk{};
+  unsigned long long key = 0;
+  if (j < n) {
+    io = ios[j];
+    lk = link[j];
+    key = keys[j];
+  }
+  if (threadIdx.x < nchunks && threadIdx.x < kFastChunksLds) s_cs[threadIdx.x] = chunks[threadIdx.x];
+  __syncthreads();
   if (j >= n || *slow) return;  // (an abandoned batch: uio_fast_kernel returns at once)
+  const h3c_chunk_state cs = s_cs[io.chunk];  // (the host sends only batches of <= 128 chunks here)
   {
-    const h3c_update_io io = ios[j];
-    const h3c_chunk_state cs = chunks[io.chunk];
     OpPos r{};
     r.op = j;
     r.status = H3C_OK;
@@ -2387,14 +2409,11 @@ __global__ void uio_fast_link_kernel(const uint4 *__restrict__ link, const unsig
     uint32_t praw;
     frag[j] = make_frag(r, j, 0, io.chunk, cs, io, pc, std_domain, false, k64, praw);
   }
-  const uint4 lk = link[j];
-  const unsigned long long key = keys[j];
   const bool start = lk.x == kNil && !fast_listed_before(link, keys, bhead, hmask, key, j);
   const uint32_t next = lk.y != kNil ? lk.y : fast_cross_next(link, keys, bhead, hmask, key, j);
   uint4 e = make_uint4(start ? 1u << 31 : 0u, next, 0u, 0u);
-  if (next != kNil) {  // the next op's payload rows (its record is another thread's, being written now)
-    const h3c_update_io nio = ios[next];
-    const h3c_chunk_state cs = chunks[nio.chunk];
+  if (next != kNil) {  // the next op's payload rows (its record is another thread's, being written now;
+    const h3c_update_io nio = ios[next];  // its chunk is this op's)
     const uint64_t blk = (cs.base + nio.offset) & ~(uint64_t)(kBlk - 1);
     const int64_t rel = (int64_t)blk - (int64_t)cs.base;
     const uint64_t src = nio.payload + (uint64_t)rel - (uint64_t)nio.offset;
@@ -2687,22 +2706,26 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_sum_kernel(uint32_t n, con
                                                                 uint2 *__restrict__ part, uint32_t *merr) {
   constexpr uint32_t NW = kTailTile / 64;
   __shared__ uint32_t wagg[NW * kFastCols], wapp[NW * kFastCols], lv[kTailTile];
-  __shared__ uint32_t s_bad;
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, k = blockIdx.x;
+  const uint32_t j = k * kTailTile + t;
+  // the op's loads issued before the slow word is known (their round trips overlap)
+  unsigned long long kj = 0, g = 0;
+  uint32_t mult = 0;
+  if (j < n) {
+    kj = keys[j];
+    g = dv[j];
+    mult = frag[j].mult;
+  }
   if (*slow) {  // not a fast-branch batch (keys may be partial): every bucket head cleared
     for (uint32_t i = k * kTailTile + t; i <= hmask; i += gridDim.x * kTailTile) heads[i] = 0;
     return;
   }
-  if (t == 0) s_bad = 0;
   const uint32_t poly = pc->poly;
-  const uint32_t j = k * kTailTile + t;
   uint32_t c = kNil, v = 0, st = 0;
   if (j < n) {  // each op's delta moved to its chunk's end
-    c = (uint32_t)(keys[j] >> 36);
-    const unsigned long long g = dv[j];
+    c = (uint32_t)(kj >> 36);
     st = (uint32_t)(g >> 32);
-    if (st == 1) v = dgf_mul_fast((uint32_t)g, frag[j].mult, poly);
-    if (st != 1 && st != 2) s_bad = 1;  // an op with no delta: cannot happen after a complete uio_fast_kernel
+    if (st == 1) v = dgf_mul_fast((uint32_t)g, mult, poly);
   }
   // in the wave: each op's inclusive XOR of its chunk's deltas (lanes at or before this one with the
   // same chunk, from 8 ballots over the chunk index); the wave's per-chunk sums into LDS
@@ -2727,7 +2750,8 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_sum_kernel(uint32_t n, con
     wagg[wave * kFastCols + c] = ip;
     wapp[wave * kFastCols + c] = (same & okm) ? 1u : 0u;
   }
-  __syncthreads();
+  // (an op with no delta cannot happen after a complete uio_fast_kernel: the call then fails)
+  const int bad = __syncthreads_or(j < n && st != 1 && st != 2);
   if (t < kFastCols) {  // the tile's row: per chunk {some op applied, XOR of the deltas}
     uint32_t a = 0, p = 0;
     for (uint32_t w = 0; w < NW; ++w) {
@@ -2741,7 +2765,7 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_sum_kernel(uint32_t n, con
     for (uint32_t w = 0; w < wave; ++w) sv ^= wagg[w * kFastCols + c];
     part[j] = make_uint2(sv, c | (st << 8));
   }
-  if (t == 0 && s_bad) atomicOr(merr, 1u);
+  if (t == 0 && bad) atomicOr(merr, 1u);
 }
 
 __global__ __launch_bounds__(kTailTile) void uio_fast_res_kernel(
@@ -2754,6 +2778,12 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_res_kernel(
   __shared__ uint32_t px[NR * kFastCols], pq[NR * kFastCols], wbase[kFastCols], wsz[kFastCols];
   __shared__ uint32_t s_last;
   const uint32_t t = threadIdx.x, k = blockIdx.x, ntiles = gridDim.x;
+  // the op's and the chunk table's loads issued before the slow word is known (round trips overlap)
+  const uint32_t j = k * kTailTile + t;
+  uint2 pj = make_uint2(0u, 0u);
+  if (j < n) pj = part[j];
+  h3c_chunk_state cs{};
+  if (t < nchunks && t < kFastCols) cs = chunks[t];
   if (ld_agent(slow)) {  // not a fast-branch batch: nothing was done; the outcome says so
     if (t == 0 && atomicAdd(&misc[kMiscFDone], 1u) + 1 == ntiles) {  // (every tile has read the slow word)
       st_agent(slow, 0u);
@@ -2762,15 +2792,8 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_res_kernel(
     }
     return;
   }
-  const uint32_t j = k * kTailTile + t;
-  uint2 pj = make_uint2(0u, 0u);
-  if (j < n) pj = part[j];  // (its round trip overlaps the rows')
-  h3c_chunk_state cs{};
   uint32_t t0 = 0;
-  if (t < nchunks && t < kFastCols) {
-    cs = chunks[t];
-    t0 = fast_t0(cs, t, exact, std_domain, crc0, pc);
-  }
+  if (t < nchunks && t < kFastCols) t0 = fast_t0(cs, t, exact, std_domain, crc0, pc);
   {  // the earlier tiles' rows: column t % 128, rows t / 128 + NR i, 8 loads in flight per thread
     const uint32_t col = t % kFastCols, r0 = t / kFastCols;
     uint32_t x = 0, q = 0;
@@ -3885,7 +3908,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         if (r) return r;
       }
       hipLaunchKernelGGL(uio_fast_link_kernel, dim3((n + 255) / 256), dim3(256), 0, q, fa.link, fa.key, fa.head,
-                         fa.hmask, n, fa.slow, fa.chain, d_ios, d_chunks, poly_type, stdf, pc, fa.frag);
+                         fa.hmask, n, fa.slow, fa.chain, d_ios, d_chunks, nchunks, poly_type, stdf, pc, fa.frag);
       HIP_TRY(hipGetLastError());
       return H3C_OK;
     };
