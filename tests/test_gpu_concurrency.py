@@ -281,3 +281,85 @@ def test_update_blocks_captured_in_hip_graph_cold_cache(h3c, torch_dev, exact):
     assert torch.equal(fresh, raw_out)
     assert ctr.cpu().tolist() == [0, 0, 0, nw, 0, 0, 0, 0]
     plan.close()
+
+
+def _fast_tables(h3c, torch, dev, rng, nchunks, cl, nw, seed):
+    """A fast-branch batch (one-block 4 KiB writes) on its own slab: device tables and the expected
+    final checksums after k applications are computed by the caller from the returned host copy."""
+    G = 4096
+    slab = torch.empty(nchunks * cl, dtype=torch.uint8, device=dev)
+    h3c.fill_splitmix(slab, cl, nchunks, cl, seed)
+    host = slab.cpu().numpy().reshape(nchunks, cl).copy()
+    st = np.zeros(nchunks, dtype=h3c.CHUNK_STATE_DTYPE)
+    for c in range(nchunks):
+        st[c] = (slab.data_ptr() + c * cl, cl, cl, orc.crc32c(host[c]), 1, 0)
+    pay = rng.integers(0, 256, (nw, G), dtype=np.uint8)
+    dpay = torch.from_numpy(pay.reshape(-1)).to(dev)
+    io = np.zeros(nw, dtype=h3c.UPDATE_IO_DTYPE)
+    for i in range(nw):
+        c, b = int(rng.integers(0, nchunks)), int(rng.integers(0, cl // G))
+        io[i] = (dpay.data_ptr() + i * G, c, b * G, G, orc.crc32c(pay[i]), 1, h3c.UPD_WRITE, 0, 0, 0)
+        host[c, b * G:(b + 1) * G] = pay[i]
+    d_state = torch.from_numpy(st.view(np.uint8).copy()).to(dev)
+    d_ios = torch.from_numpy(io.view(np.uint8).copy()).to(dev)
+    d_res = torch.zeros(nw * h3c.UPDATE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    final = [orc.crc32c(host[c]) for c in range(nchunks)]
+    return slab, dpay, d_state, d_ios, d_res, final
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fast_branch_threads_beside_legacy_stream_calls(h3c, torch_dev, graphs):
+    """Update threads repeating device-table fast-branch batches (each its own tables, stream and
+    per-thread scratch; with graphs, captures happen during the run) while other threads make
+    synchronous legacy-default-stream verify calls: every batch's final checksums equal the CRC of
+    the chunks' bytes and every verify is right (a capture holds h3c_rt::capture_gate(), which the
+    legacy-stream entries wait out instead of failing)."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(7)
+    nupd, nleg, reps = 4, 4, 6
+    tabs = [_fast_tables(h3c, torch, dev, rng, 8, 1 << 20, 600, 300 + k) for k in range(nupd)]
+    host = [[rng.integers(0, 256, 4096 * (1 + j), dtype=np.uint8) for j in range(4)] for _ in range(nleg)]
+    want = [[orc.crc32c(d) for d in hs] for hs in host]
+    torch.cuda.synchronize()
+    errors = []
+    start = threading.Barrier(nupd + nleg)
+
+    def upd(k):
+        try:
+            slab, dpay, d_state, d_ios, d_res, final = tabs[k]
+            s = torch.cuda.Stream(device=dev)
+            bound = h3c.UpdateIosDev(d_state, d_ios, d_res, stream=s, graphs=graphs)
+            start.wait()
+            for r in range(reps):
+                bound.run()
+                s.synchronize()
+                fin = d_state.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)
+                if list(map(int, fin["value"])) != final:  # (the same writes again: same bytes, same values)
+                    errors.append((k, r, "state"))
+                if not (d_res.cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)["status"] == 0).all():
+                    errors.append((k, r, "status"))
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    def leg(k):
+        try:
+            start.wait()
+            for r in range(3 * reps):
+                t, v = h3c.batch_create(host[k])  # (stream None: the legacy default stream)
+                if list(map(int, v)) != want[k]:
+                    errors.append(("legacy", k, r))
+        except Exception as e:  # noqa: BLE001
+            errors.append(("legacy", k, repr(e)))
+
+    b = h3c.diag_counters()
+    threads = [threading.Thread(target=upd, args=(k,)) for k in range(nupd)]
+    threads += [threading.Thread(target=leg, args=(k,)) for k in range(nleg)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors[:5]
+    d = {k: v - b[k] for k, v in h3c.diag_counters().items()}
+    assert d["fast_batches"] == nupd * reps and d["fast_abandoned"] == 0, d
+    if graphs:
+        assert d["graph_capture_failures"] == 0, d
