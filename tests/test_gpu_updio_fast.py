@@ -160,6 +160,41 @@ def test_fast_branch_128_chunks_and_failed_checks(h3c, torch_dev, hooks):
     check_both(h3c, hooks, sc, dev_api=True)
 
 
+def test_fast_branch_chunks_sharing_blocks(h3c, torch_dev, hooks):
+    """Chunks packed at a stride that is not a multiple of 4 KiB, so neighbouring chunks share absolute
+    4 KiB blocks: small writes inside one absolute block of either chunk make two chains (two keys) on
+    the same physical block, each storing only its own chunk's bytes.  Both branches and the oracle
+    agree, and so do the bytes of the shared blocks."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(29)
+    cs = 3 * BLK + 1000  # (chunk c starts 1000 * c bytes past a block boundary, mod 4 KiB)
+    sc = fast_scenario(h3c, torch, dev, rng, nchunks=16, chunk_size=cs, nops=0)
+    base = sc.slab.data_ptr()
+    for _ in range(3000):
+        c = int(rng.integers(0, 16))
+        size = sc.meta[c]["size"]
+        o = int(rng.integers(0, size))
+        a = base + c * cs + o
+        room = min(size - o, (a | (BLK - 1)) + 1 - a)
+        ln = int(rng.integers(1, room + 1))
+        if o == 0 and ln >= size:
+            continue
+        sc.add(orc.UPD_WRITE, c, o, ln, orc.CRC32C, good=rng.random() >= 0.02)
+    check_both(h3c, hooks, sc)
+
+
+def test_fast_branch_single_op_and_two_ops(h3c, torch_dev, hooks):
+    """The smallest batches: one op, then two ops on the same block (a chain of two)."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(31)
+    sc = fast_scenario(h3c, torch, dev, rng, nchunks=1, chunk_size=64 << 10, nops=1, bad=0.0)
+    check_both(h3c, hooks, sc)
+    sc = fast_scenario(h3c, torch, dev, rng, nchunks=2, chunk_size=64 << 10, nops=0)
+    sc.add(orc.UPD_WRITE, 1, 5 * BLK + 100, 300, orc.CRC32C)
+    sc.add(orc.UPD_WRITE, 1, 5 * BLK + 200, 3000, orc.CRC32C)
+    check_both(h3c, hooks, sc)
+
+
 def test_fast_branch_129_chunks_takes_the_general_pipeline(h3c, torch_dev, hooks):
     torch, dev = torch_dev
     rng = np.random.default_rng(10)
