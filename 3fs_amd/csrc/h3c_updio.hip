@@ -2452,6 +2452,9 @@ constexpr uint32_t kScratchHeads = 1;
 #ifndef H3C_FAST_GRAB
 #define H3C_FAST_GRAB 1  // 1: a workgroup's waves take their chain starts from an LDS counter (0: static ranges)
 #endif
+#ifndef H3C_FAST_LPT
+#define H3C_FAST_LPT 1  // the counter hands out the chains with later ops first, then the one-op chains
+#endif
 constexpr unsigned long long kGranApplied = 4ull << 32;  // look-back granule bit: some op of the chunk applied
 
 
@@ -2556,6 +2559,31 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
     rows_at(a0, cur);
   }
   if (t == 0) s_grab = wlo + kBlkWaves;
+#if H3C_FAST_LPT
+  // Longest first: after the static first ops, the counter hands out the starts of chains with later ops
+  // (their continuations' exposed round trips), a second counter then the one-op chains, so the
+  // workgroup's last waves end on short work.
+  __shared__ uint32_t s_grab2;
+  if (t == 0) s_grab2 = wlo + kBlkWaves;
+  bool one_ops = false;  // (this wave has moved on to the second counter)
+  auto grab = [&](bool &cn) -> uint32_t {
+    for (;;) {
+      uint32_t j = 0;
+      if (lane == 0) j = atomicAdd(one_ops ? &s_grab2 : &s_grab, 1u);
+      j = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
+      if (j >= whi) {
+        if (one_ops) return kNil;
+        one_ops = true;
+        continue;
+      }
+      bool c;
+      if (is_start(j, c) && c != one_ops) {
+        cn = c;
+        return j;
+      }
+    }
+  };
+#else
   auto grab = [&](bool &cn) -> uint32_t {
     for (;;) {
       uint32_t j = 0;
@@ -2565,6 +2593,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
       if (is_start(j, cn)) return j;
     }
   };
+#endif
   FAST_MARK(1);
   fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
   __syncthreads();
