@@ -2436,10 +2436,10 @@ struct FastSink {  // apply_fragment's results on the fast branch: dv[op] = {1, 
 #ifndef H3C_FAST_TRACE
 #define H3C_FAST_TRACE 0  // 1: workgroups 0, 1, the middle one and the last print their step times (diagnostics)
 #endif
-#if H3C_FAST_TRACE >= 2
-// histograms of the waves' step end times (5 us bins from the earliest workgroup start): [0..63] chains
-// done, [64..127] deltas done; [128] 0x7FFFFFFF - the earliest start (low 31 bits), [129] waves counted
-__device__ unsigned int g_ftr[130] = {};
+#if H3C_FAST_TRACE == 3
+// each workgroup's start and end of the last uio_fast_kernel launch (diagnostics; h3c_diag_fast_wg,
+// scripts/fast_wg_trace.py)
+__device__ unsigned long long g_fast_wg[2 * 1024];
 #endif
 #if H3C_FAST_TRACE
 #define FAST_MARK(i) (ftr[i] = wall_clock64())
@@ -2702,6 +2702,12 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
   if (ts) {  // one stamp per workgroup, once all its waves are done
     __syncthreads();
     if (t == 0) atomicMax(&ts[1], (unsigned long long)wall_clock64());
+#if H3C_FAST_TRACE == 3
+    if (t == 0 && blockIdx.x < 1024) {
+      g_fast_wg[2 * blockIdx.x] = ftr[0];
+      g_fast_wg[2 * blockIdx.x + 1] = wall_clock64();
+    }
+#endif
   }
 }
 
@@ -4409,3 +4415,9 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
                               uint32_t n, h3c_update_result *results, uint32_t flags, void *stream) {
   return h3c_update_ios_ex(poly_type, chunks, nchunks, ios, n, results, flags, nullptr, stream);
 }
+
+#if H3C_FAST_TRACE == 3
+extern "C" int h3c_diag_fast_wg(unsigned long long *out, int n) {  // (trace builds only)
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_wg), 16ull * (unsigned)n) == hipSuccess ? 0 : -1;
+}
+#endif
