@@ -2452,6 +2452,9 @@ constexpr uint32_t kScratchHeads = 1;
 #ifndef H3C_FAST_GRAB
 #define H3C_FAST_GRAB 1  // 1: a workgroup's waves take their chain starts from an LDS counter (0: static ranges)
 #endif
+#ifndef H3C_FAST_WG_MULT
+#define H3C_FAST_WG_MULT 1  // uio_fast_kernel workgroups per CU over the launch (one resident at a time)
+#endif
 #ifndef H3C_FAST_LPT
 #define H3C_FAST_LPT 1  // the counter hands out the chains with later ops first, then the one-op chains
 #endif
@@ -3723,7 +3726,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   ThreadRes::FastPred *fpred = fast_able ? &fast_pred(dev, poly_type, flags & ~H3C_UPD_GRAPHS, n, nchunks, d_chunks, d_ios)
                                          : nullptr;
   const bool try_fast = fast_able && (fast_hook == 2 || !fpred->slow || fpred->general_runs >= kFastRetry);
-  const uint32_t nwg_fast = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
+  const uint32_t nwg_fast = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev)) * H3C_FAST_WG_MULT;
   const uint32_t ntiles_tail = (uint32_t)std::max<size_t>(1, ((size_t)n + 1023) / 1024);  // the tail kernels
   uint32_t hcap_fast = 256;
   while (hcap_fast < 2 * n) hcap_fast <<= 1;
