@@ -78,13 +78,13 @@ enum { kCtrNone, kCtrReuse, kCtrCombine, kCtrRead, kCtrRecalc, kCtrMismatch, kCt
 // [kMiscPBDone]: uio_phaseb_kernel's finished tiles (the last one copies [kMiscOutF, kMiscN) to the host);
 // [kMiscFast]: the fast branch's outcome (kFast*; 0 on the general pipeline); [kMiscErr]: a kernel met an
 // inconsistent table (a piece table that disagrees with its items) -- the call fails.
-// Past kMiscN (not copied back): [kMiscFTicket] / [kMiscFDone] uio_fast_kernel's ticket and finished
-// workgroups, [kMiscFVoid] one of its workgroups gave up waiting, [kMiscSlow] (zeroed by
-// uio_zero_kernel, set by the prep kernel) some op of the batch is not one the fast branch takes.
+// Past kMiscN (not copied back): [kMiscFDone] the fast tail's finished workgroups, [kMiscFVoid] one of
+// its workgroups reported the pass void; [kMiscSlow] is unused (the slow word lives in the thread's
+// FastScratch); [12] is unused.
 enum {
   kMiscTicket = 0, kMiscA6 = 1, kMiscOutF = 2, kMiscOutA6 = 3, kMiscT0 = 4, kMiscT1 = 6, kMiscPBVoid = 8,
   kMiscPBDone = 9, kMiscFast = 10, kMiscErr = 11, kMiscN = 12,
-  kMiscFTicket = 12, kMiscFDone = 13, kMiscFVoid = 14, kMiscSlow = 15, kMiscWords = 16
+  kMiscFDone = 13, kMiscFVoid = 14, kMiscSlow = 15, kMiscWords = 16
 };
 enum : uint32_t { kFastDone = 1, kFastAbort = 2, kFastVoid = 3 };
 
@@ -261,8 +261,8 @@ __device__ __forceinline__ void pub_flag(uint32_t *f, uint32_t v) {
 // total to tbase[k]; the last tile to finish turns tbase[] into the tiles' exclusive bases (item
 // i's offset is pbase[i] + tbase[i / kPrepTile]; op_piece_crc_kernel adds them).  `sstate`
 // (zeroed by the caller): [0] unused, [1] finished tiles, [2] the total, [3 + k] tbase[k].
-// Zeroes up to four word ranges, grid-strided (the prep kernel's scan words; on the fast branch also
-// its bucket heads, uio_fast_kernel's look-back granules and misc[kMiscSlow]).
+// Zeroes up to four word ranges, grid-strided (the prep kernel's scan words; a new or suspect
+// FastScratch before the fast branch uses it).
 __global__ void uio_zero_kernel(uint32_t *__restrict__ a, uint32_t na, uint32_t *__restrict__ b, uint32_t nb,
                                 uint32_t *__restrict__ c, uint32_t nc, uint32_t *__restrict__ d, uint32_t nd) {
   const uint32_t s = gridDim.x * blockDim.x;
@@ -290,7 +290,7 @@ struct FastArgs {
   uint32_t *head;           // bucket heads, hmask + 1 of them (zeroed by uio_zero_kernel)
   uint32_t hmask;
   unsigned long long *dv;   // per op: {state << 32 | delta CRC} (state 1: applied, 2: failed A6)
-  uint32_t *slow;           // set when some op is not one this branch takes (misc[kMiscSlow])
+  uint32_t *slow;           // set when some op is not one this branch takes (FastScratch word 0)
   const PolyConsts *pc;
   uint4 *chain;             // per op (uio_fast_link_kernel): {bit 31: starts its block's chain, bits 0-25: the
                             //  next op's new bytes w0 | w1 << 13; the block's next op; the next op's payload
@@ -2377,7 +2377,8 @@ __global__ void uio_fast_link_kernel(const uint4 *__restrict__ link, const unsig
                                      const uint32_t *__restrict__ slow, uint4 *__restrict__ chain,
                                      const h3c_update_io *__restrict__ ios, const h3c_chunk_state *__restrict__ chunks,
                                      uint32_t nchunks, uint8_t poly_type, uint32_t std_domain,
-                                     const PolyConsts *__restrict__ pc, FragDesc *__restrict__ frag) {
+                                     const PolyConsts *__restrict__ pc, FragDesc *__restrict__ frag,
+                                     uint32_t *__restrict__ heavy, uint32_t *heavy_n) {
   // the chunk table (<= 128 states) into LDS beside the op's own loads: its chunk state is not a
   // second round trip after the op record
   __shared__ h3c_chunk_state s_cs[kFastChunksLds];
@@ -2394,6 +2395,7 @@ __global__ void uio_fast_link_kernel(const uint4 *__restrict__ link, const unsig
   __syncthreads();
   if (j >= n || *slow) return;  // (an abandoned batch: uio_fast_kernel returns at once)
   const h3c_chunk_state cs = s_cs[io.chunk];  // (the host sends only batches of <= 128 chunks here)
+  const uint32_t lane = threadIdx.x & 63;
   {
     OpPos r{};
     r.op = j;
@@ -2423,6 +2425,17 @@ __global__ void uio_fast_link_kernel(const uint4 *__restrict__ link, const unsig
     e.w = (uint32_t)(src >> 32);
   }
   chain[j] = e;
+  // the starts of chains with later ops, listed per 64-op segment (this wave's; no atomics: heavy[64 s + k],
+  // heavy_n[s] the count): uio_fast_kernel deals the segments out round-robin over its workgroups, whose
+  // contiguous ranges would otherwise carry the batch's early starts' later ops -- early ranges ran ~10 %
+  // more ops than late ones (profiles/r04_updio_fast_wg_ends.txt)
+  if (heavy) {
+    const bool hv = start && next != kNil;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(hv);
+    const uint32_t seg = j >> 6;
+    if (hv) heavy[64 * seg + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1))] = j;
+    if (lane == 0) heavy_n[seg] = (uint32_t)__builtin_popcountll(m);  // (lane 0 is active: j = 64 seg < n)
+  }
 }
 
 struct FastSink {  // apply_fragment's results on the fast branch: dv[op] = {1, unshifted delta} or {2, 0}
@@ -2440,6 +2453,7 @@ struct FastSink {  // apply_fragment's results on the fast branch: dv[op] = {1, 
 // each workgroup's start and end of the last uio_fast_kernel launch (diagnostics; h3c_diag_fast_wg,
 // scripts/fast_wg_trace.py)
 __device__ unsigned long long g_fast_wg[2 * 1024];
+__device__ uint32_t g_fast_rot;  // workgroup b takes range (b + g_fast_rot) % grid (h3c_diag_fast_rot)
 #endif
 #if H3C_FAST_TRACE
 #define FAST_MARK(i) (ftr[i] = wall_clock64())
@@ -2475,7 +2489,9 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
                                                              const uint4 *__restrict__ chain, unsigned long long *dv,
                                                              const uint32_t *__restrict__ slow, unsigned long long *ts,
                                                              const unsigned long long *__restrict__ keys,
-                                                             uint32_t *heads, uint32_t hmask) {
+                                                             uint32_t *heads, uint32_t hmask,
+                                                             const uint32_t *__restrict__ heavy,
+                                                             const uint32_t *__restrict__ heavy_n) {
   __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
   const uint32_t t = threadIdx.x, lane = t & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -2553,35 +2569,55 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
     return (ch.x >> 31) != 0;
   };
   __shared__ uint32_t s_grab;
-  const uint32_t wlo = (uint32_t)((uint64_t)blockIdx.x * kBlkWaves * n / nw);
-  const uint32_t whi = (uint32_t)((uint64_t)(blockIdx.x + 1) * kBlkWaves * n / nw);
+#if H3C_FAST_TRACE == 3
+  const uint32_t rb = (blockIdx.x + g_fast_rot) % gridDim.x;  // (diagnostics: the range a workgroup takes, rotated)
+#else
+  const uint32_t rb = blockIdx.x;
+#endif
+  const uint32_t wlo = (uint32_t)((uint64_t)rb * kBlkWaves * n / nw);
+  const uint32_t whi = (uint32_t)((uint64_t)(rb + 1) * kBlkWaves * n / nw);
   const uint32_t first = wlo + wave;
   if (first < whi) {
     Addr a0;
     addr_of(first, a0);
     rows_at(a0, cur);
   }
-  if (t == 0) s_grab = wlo + kBlkWaves;
+  if (t == 0) s_grab = wlo + kBlkWaves;  // (the LPT form resets it below)
 #if H3C_FAST_LPT
   // Longest first: after the static first ops, the counter hands out the starts of chains with later ops
   // (their continuations' exposed round trips), a second counter then the one-op chains, so the
-  // workgroup's last waves end on short work.
+  // workgroup's last waves end on short work.  The chains with later ops come from the link kernel's list,
+  // dealt round-robin (entries rb, rb + grid, ...): by range, the batch's early ranges would run most of
+  // them (a block's first write starts its chain).
   __shared__ uint32_t s_grab2;
-  if (t == 0) s_grab2 = wlo + kBlkWaves;
+  if (t == 0) {
+    s_grab2 = wlo + kBlkWaves;
+    s_grab = 0;  // (the list counter)
+  }
+  const uint32_t nseg = heavy ? (n + 63) / 64 : 0u;
   bool one_ops = false;  // (this wave has moved on to the second counter)
   auto grab = [&](bool &cn) -> uint32_t {
     for (;;) {
       uint32_t j = 0;
       if (lane == 0) j = atomicAdd(one_ops ? &s_grab2 : &s_grab, 1u);
       j = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
-      if (j >= whi) {
-        if (one_ops) return kNil;
-        one_ops = true;
+      if (!one_ops) {  // the list: entry j & 63 of segment rb + (j >> 6) * grid
+        const uint64_t sg = (uint64_t)rb + (uint64_t)(j >> 6) * gridDim.x;
+        if (sg >= nseg) {
+          one_ops = true;
+          continue;
+        }
+        if ((j & 63u) < heavy_n[sg]) {
+          cn = true;
+          return heavy[64 * sg + (j & 63u)];
+        }
+        if (lane == 0) atomicMax(&s_grab, (j | 63u) + 1u);  // (the segment's rest is empty: skip it)
         continue;
       }
+      if (j >= whi) return kNil;
       bool c;
-      if (is_start(j, c) && c != one_ops) {
-        cn = c;
+      if (is_start(j, c) && !c) {  // (a start with later ops is on the list)
+        cn = false;
         return j;
       }
     }
@@ -2601,7 +2637,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
   fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
   __syncthreads();
   FAST_MARK(2);
-  if (first < whi && is_start(first, cont)) {
+  if (first < whi && is_start(first, cont) && (!H3C_FAST_LPT || !cont)) {  // (LPT: those are on the list)
     op = first;
   } else {
     op = grab(cont);
@@ -3733,6 +3769,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   FastArgs fa{};
   unsigned long long *d_gran = nullptr;
   uint2 *d_part = nullptr;  // uio_fast_sum_kernel -> uio_fast_res_kernel: each op's XOR in its tile, chunk, state
+  uint32_t *d_heavy = nullptr;  // uio_fast_link_kernel -> uio_fast_kernel: the starts of chains with later ops
   auto layout = [&](char *base) -> size_t {  // one layout, run with base 0 to size the lease
     char *cur = base;
     d_status = carve<uint32_t>(cur, n);
@@ -3773,6 +3810,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       fa.chain = carve<uint4>(cur, n);
       d_gran = carve<unsigned long long>(cur, (size_t)ntiles_tail * kFastCols);
       d_part = carve<uint2>(cur, n);
+      d_heavy = carve<uint32_t>(cur, 64 * (((size_t)n + 63) / 64) + ((size_t)n + 63) / 64);
     }
     return (size_t)(cur - base);
   };
@@ -3919,7 +3957,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     unsigned long long *d_ts = reinterpret_cast<unsigned long long *>(d_misc + kMiscT0);
     auto fast_kernel = [&](hipStream_t q, bool timed) -> int {
       hipLaunchKernelGGL(uio_fast_kernel, dim3(nwg_fast), dim3(kBlkThreads), 0, q, n, stdf, pc, fa.frag, fa.chain,
-                         fa.dv, fa.slow, timed ? d_ts : nullptr, fa.key, fa.head, fa.hmask);
+                         fa.dv, fa.slow, timed ? d_ts : nullptr, fa.key, fa.head, fa.hmask,
+                         H3C_FAST_LPT ? d_heavy : nullptr, d_heavy + 64 * (((size_t)n + 63) / 64));
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(uio_fast_sum_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, n, pc, fa.frag, fa.key, fa.dv,
                          fa.slow, fa.head, fa.hmask, d_gran, d_part, d_misc + kMiscErr);
@@ -3946,7 +3985,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         if (r) return r;
       }
       hipLaunchKernelGGL(uio_fast_link_kernel, dim3((n + 255) / 256), dim3(256), 0, q, fa.link, fa.key, fa.head,
-                         fa.hmask, n, fa.slow, fa.chain, d_ios, d_chunks, nchunks, poly_type, stdf, pc, fa.frag);
+                         fa.hmask, n, fa.slow, fa.chain, d_ios, d_chunks, nchunks, poly_type, stdf, pc, fa.frag,
+                         H3C_FAST_LPT ? d_heavy : nullptr, d_heavy + 64 * (((size_t)n + 63) / 64));
       HIP_TRY(hipGetLastError());
       return H3C_OK;
     };
@@ -4422,5 +4462,8 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
 #if H3C_FAST_TRACE == 3
 extern "C" int h3c_diag_fast_wg(unsigned long long *out, int n) {  // (trace builds only)
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_wg), 16ull * (unsigned)n) == hipSuccess ? 0 : -1;
+}
+extern "C" int h3c_diag_fast_rot(uint32_t rot) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_fast_rot), &rot, 4) == hipSuccess ? 0 : -1;
 }
 #endif
