@@ -73,7 +73,8 @@ __device__ __forceinline__ void store_row(uint64_t a, uint4 v) {
 
 #ifndef H3C_UPD_EXPERIMENT
 #define H3C_UPD_EXPERIMENT 0  // timing-only builds: bit0 skips write-back, bit1 skips the CRC math,
-                              // fused kernel: bit2 skips the hash walk, bit3 stops after the writes
+                              // fused kernel: bit2 skips the hash walk, bit3 stops after the writes,
+                              // bit5 skips the look-back, bit6 the last workgroup's wait, bit7 the ticket
 #endif
 
 // rocPRIM picks merge sort below this many items.  Forcing its onesweep radix passes
@@ -392,6 +393,10 @@ __global__ __launch_bounds__(kThreads) void upd_delta_kernel(
 constexpr uint32_t kFusedCols = 128;    // chunk columns of the look-back: lane c holds chunks c and c + 64
 constexpr uint32_t kFusedMaxWG = 1024;  // granule rows reserved in the workspace
 constexpr uint32_t kGranAgg = 1, kGranIncl = 2;
+#ifndef H3C_UPD_LOOK_WIN
+#define H3C_UPD_LOOK_WIN 4
+#endif
+constexpr uint32_t kLookWin = H3C_UPD_LOOK_WIN;  // look-back rows read per column per round trip
 constexpr uint32_t kSpinLimit = 1u << 22;  // bounded look-back spins (about a quarter second)
 enum { kCtlTicket = 0, kCtlErr = 1, kCtlTimeout = 2, kCtlDone = 3, kCtlWords = 64 };
 typedef unsigned long long __attribute__((address_space(1))) gu64;
@@ -427,7 +432,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
   constexpr uint32_t G4 = 4096;
   __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
   __shared__ uint32_t s_ticket;
-  if (threadIdx.x == 0) s_ticket = atomicAdd(&ctl[kCtlTicket], 1u);
+  if (threadIdx.x == 0) s_ticket = (H3C_UPD_EXPERIMENT & 128) ? blockIdx.x : atomicAdd(&ctl[kCtlTicket], 1u);
   __syncthreads();
   const uint32_t L = s_ticket, nwg = gridDim.x;
   const uint32_t lane = threadIdx.x & 63;
@@ -529,9 +534,14 @@ __device__ __forceinline__ void upd_fused_kernel_body(
       }
       if (valid) {
         Streams st{0, 0, 0, 0};
+#if H3C_UPD_EXPERIMENT & 2  // timing experiment: no CRC compute (loads kept alive)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) st.s0 ^= vn[u].x ^ vo[u].x ^ vn[u].y ^ vo[u].y ^ vn[u].z ^ vo[u].z ^ vn[u].w ^ vo[u].w;
+#else
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           consume(st, make_uint4(vn[u].x ^ vo[u].x, vn[u].y ^ vo[u].y, vn[u].z ^ vo[u].z, vn[u].w ^ vo[u].w), lb, Lt);
+#endif
         const uint64_t dst = rl64(m_dst, t);
         if (dst) {  // first writer of the slot: leave the slot's final bytes in the chunk
           const uint64_t fin = rl64(m_fin, t);
@@ -588,7 +598,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     const bool two = nchunks > 64;
     uint64_t *row = gran + (uint64_t)L * kFusedCols;
     uint32_t x0 = 0, x1 = 0;
-    if (L > 0) {
+    if (L > 0 && !(H3C_UPD_EXPERIMENT & 32)) {  // (experiment bit5: no look-back)
       if (lane < nchunks) gran_store(row + lane, kGranAgg, a0);
       if (two && lane + 64 < nchunks) gran_store(row + 64 + lane, kGranAgg, a1);
       int j0 = lane < nchunks ? (int)L - 1 : -1, j1 = two && lane + 64 < nchunks ? (int)L - 1 : -1;
@@ -596,24 +606,27 @@ __device__ __forceinline__ void upd_fused_kernel_body(
       const uint32_t limit = force_timeout && L == 1 ? 0u : kSpinLimit;
       for (uint32_t spins = 0; __builtin_amdgcn_ballot_w64(j0 >= 0 || j1 >= 0) != 0;) {
         bool moved = false;
-        if (j0 >= 0) {
-          const uint64_t g = gran_load(gran + (uint64_t)j0 * kFusedCols + lane);
-          const uint32_t state = (uint32_t)(g >> 32);
-          if (state) {
-            x0 ^= (uint32_t)g;
-            j0 = state == kGranIncl ? -1 : j0 - 1;
-            moved = true;
+        // a window of kLookWin rows per column in one round trip: a predecessor that has just posted
+        // its aggregate is passed together with the inclusive row below it
+        auto look = [&](int &j, uint32_t &x, uint32_t col) {
+          if (j < 0) return;
+          const int top = j;
+          uint64_t g[kLookWin];
+#pragma unroll
+          for (int w = 0; w < (int)kLookWin; ++w)
+            g[w] = top - w >= 0 ? gran_load(gran + (uint64_t)(top - w) * kFusedCols + col) : 0ull;
+#pragma unroll
+          for (int w = 0; w < (int)kLookWin; ++w) {
+            const uint32_t state = (uint32_t)(g[w] >> 32);
+            if (top - w >= 0 && j == top - w && state) {
+              x ^= (uint32_t)g[w];
+              j = state == kGranIncl ? -1 : j - 1;
+              moved = true;
+            }
           }
-        }
-        if (j1 >= 0) {
-          const uint64_t g = gran_load(gran + (uint64_t)j1 * kFusedCols + 64 + lane);
-          const uint32_t state = (uint32_t)(g >> 32);
-          if (state) {
-            x1 ^= (uint32_t)g;
-            j1 = state == kGranIncl ? -1 : j1 - 1;
-            moved = true;
-          }
-        }
+        };
+        look(j0, x0, lane);
+        look(j1, x1, 64 + lane);
         if (__builtin_amdgcn_ballot_w64(moved) == 0 || limit == 0) {
           __builtin_amdgcn_s_sleep(2);
           if (++spins > limit) {  // a predecessor never published: give up, flag the batch
@@ -630,11 +643,10 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     wexcl[64 + lane] = x1;
     // every workgroup but the last counts itself done once its flag (if it gave up) is out: the last
     // one reads the flag only after all the others' counts (look-back may have passed a workgroup's
-    // aggregate before that workgroup gave up and raised the flag)
-    if (L != nwg - 1 && lane == 0) {
-      __threadfence();
-      atomicAdd(&ctl[kCtlDone], 1u);
-    }
+    // aggregate before that workgroup gave up and raised the flag).  The give-up branch fences its
+    // flag; the count itself needs no fence: an agent-scope release here wrote back the XCD's L2
+    // (buffer_wbl2) once per workgroup, ~3 us of the kernel (profiles/r04_update_tail_ab.txt).
+    if (L != nwg - 1 && lane == 0) atomicAdd(&ctl[kCtlDone], 1u);
     if (L == nwg - 1) {  // the last workgroup: final checksums, counts
       const uint32_t t0 = x0 ^ a0, t1 = x1 ^ a1;
       uint32_t stale = 0;
@@ -648,10 +660,10 @@ __device__ __forceinline__ void upd_fused_kernel_body(
       }
       for (int o = 32; o >= 1; o >>= 1) stale += __shfl_xor(stale, o, 64);
       if (lane == 0) {
-        __threadfence();
         // wait (bounded) for every other workgroup's done count; a count that never comes voids the batch
+        // (the counts and flags are agent-scope atomics at the coherence point: no L2 write-back needed)
         bool late = false;
-        for (uint32_t spins = 0;
+        for (uint32_t spins = 0; !(H3C_UPD_EXPERIMENT & 64) &&  // (experiment bit6: no wait for the counts)
              __hip_atomic_load(&ctl[kCtlDone], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nwg - 1;) {
           __builtin_amdgcn_s_sleep(2);
           if (++spins > kSpinLimit) {
@@ -659,6 +671,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
             break;
           }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last count read before the flags
         if (late) atomicExch(&ctl[kCtlTimeout], 1u);
         const uint32_t inv = __hip_atomic_load(&ctl[kCtlErr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // every workgroup's inclusive granule was read (directly or through a later one's) before

@@ -1,14 +1,14 @@
 #!/bin/bash
-# Build the engine with extra defines into 3fs_amd/_lib/variants/lib_<name>.so (A/B runs).
-#   bash scripts/build_variant.sh <name> -DFOO=1 ...
+# Builds the working tree's engine with extra compile flags into 3fs_amd/_lib/diag/<name>/ for same-box
+# A/Bs (H3C_LIB_PATH).  usage: scripts/build_variant.sh <name> [-DFLAG=V ...]
 set -e
-R=$(cd "$(dirname "$0")/.." && pwd)
-cd "$R"
 name=$1; shift
-O=3fs_amd/_lib/variants/obj/$name
-mkdir -p $O
+R=$(cd $(dirname $0)/.. && pwd)
+O=$R/3fs_amd/_lib/diag/$name
+mkdir -p $O/obj
 for f in h3c_engine h3c_update h3c_hostfed h3c_updio h3c_formats; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -I include -c 3fs_amd/csrc/$f.hip -o $O/$f.o &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I $R/include "$@" -c $R/3fs_amd/csrc/$f.hip -o $O/obj/$f.o &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o 3fs_amd/_lib/variants/lib_$name.so $O/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libh3c_crc.so $O/obj/*.o
+echo $O/libh3c_crc.so
