@@ -71,6 +71,9 @@ __device__ __forceinline__ void store_row(uint64_t a, uint4 v) {
 #endif
 }
 
+#ifndef H3C_UPD_WG_BAL
+#define H3C_UPD_WG_BAL 1  // fused path: the fewest workgroups that keep the most writes per wave
+#endif
 #ifndef H3C_UPD_EXPERIMENT
 #define H3C_UPD_EXPERIMENT 0  // timing-only builds: bit0 skips write-back, bit1 skips the CRC math,
                               // fused kernel: bit2 skips the hash walk, bit3 stops after the writes,
@@ -1083,7 +1086,14 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
   const uint32_t poly = type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
   const uint32_t reuse_case = (uint64_t)block_bytes == chunk_len ? 1u : 0u;  // a block write replaces the chunk
   const int path = pick_path(n_blocks, nchunks, block_bytes);
-  const uint32_t fused_wg = std::min<uint32_t>(std::min(num_cu, kFusedMaxWG), (n_blocks + kWavesPerBlock - 1) / kWavesPerBlock);
+  uint32_t fused_wg = std::min<uint32_t>(std::min(num_cu, kFusedMaxWG), (n_blocks + kWavesPerBlock - 1) / kWavesPerBlock);
+#if H3C_UPD_WG_BAL  // the fewest workgroups with the same most writes per wave (100k writes: 250, 25 per wave,
+                    // instead of 256 with 24-25: -1 us, profiles/r04_update_tail_ab.txt)
+  {
+    const uint64_t per = ((uint64_t)n_blocks + (uint64_t)fused_wg * kWavesPerBlock - 1) / ((uint64_t)fused_wg * kWavesPerBlock);
+    fused_wg = (uint32_t)std::max<uint64_t>(1, ((uint64_t)n_blocks + per * kWavesPerBlock - 1) / (per * kWavesPerBlock));
+  }
+#endif
   // one memset: hash heads, control words, touched flags and the granule rows in use
   const size_t zero = path == kPathFused ? (size_t)((char *)(w.gran + (size_t)fused_wg * kFusedCols) - (char *)w.hhead)
                                          : (size_t)((char *)w.gran - (char *)w.hhead);
