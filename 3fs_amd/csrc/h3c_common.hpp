@@ -9,8 +9,10 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <initializer_list>
 #include <shared_mutex>
 #include <string>
+#include <type_traits>
 
 #include "h3c_crc.h"
 
@@ -168,6 +170,65 @@ uint32_t small_rows_bound(uint64_t max_len, uint32_t max_segs);
 uint64_t pick_seg(uint64_t total_bytes, int dev);
 // h3c_test_hook values (0 = default; initialised once from the environment).
 uint64_t hook(int key);
+
+// ---- kernel argument layouts, for auditing the pointers baked into captured graphs ----
+// A captured graph replays its kernels with the argument values of the capture.  update_core keys its
+// graph cache by every buffer the pipeline touches (UpdGraphKey); before a graph is instantiated, every
+// pointer argument of every kernel node is checked to lie inside one of those buffers or the library's
+// constant tables (a pointer outside them would replay into memory the key does not name).  HIP gives a
+// node's argument values but not their types, so each kernel that can be captured registers its layout:
+// per argument its size, alignment and the offsets of the pointers inside it (a pointer argument: 0; a
+// struct argument: its pointer members, by an ArgLayout<> specialisation).
+struct ArgSpec {
+  uint16_t size = 0, align = 1;
+  uint8_t nptr = 0;
+  uint16_t ptr_off[12] = {};
+};
+struct KernelSig {
+  const void *fn = nullptr;
+  const char *name = nullptr;
+  uint32_t nargs = 0;
+  ArgSpec args[40];
+};
+template <class T, class = void>
+struct ArgLayout {
+  static_assert(std::is_arithmetic<T>::value || std::is_enum<T>::value,
+                "a struct kernel argument needs an ArgLayout<> specialisation naming its pointer members");
+  static void fill(ArgSpec &a) {
+    a.size = sizeof(T);
+    a.align = alignof(T);
+  }
+};
+template <class T>
+struct ArgLayout<T *, void> {
+  static void fill(ArgSpec &a) {
+    a.size = sizeof(T *);
+    a.align = alignof(T *);
+    a.nptr = 1;
+    a.ptr_off[0] = 0;
+  }
+};
+// a struct argument whose pointer members sit at `offs` (offsetof each)
+template <class S>
+inline void struct_arg(ArgSpec &a, std::initializer_list<size_t> offs) {
+  a.size = sizeof(S);
+  a.align = alignof(S);
+  for (size_t o : offs) a.ptr_off[a.nptr++] = (uint16_t)o;
+}
+template <class... A>
+KernelSig kernel_sig(void (*f)(A...), const char *name) {
+  static_assert(sizeof...(A) <= 40, "too many kernel arguments for KernelSig");
+  KernelSig s;
+  s.fn = reinterpret_cast<const void *>(f);
+  s.name = name;
+  s.nargs = sizeof...(A);
+  uint32_t i = 0;
+  (void)i;
+  (ArgLayout<typename std::remove_cv<A>::type>::fill(s.args[i++]), ...);
+  return s;
+}
+// op_piece_crc_kernel<UioPieceSrc>'s layout (its argument struct is h3c_engine.hip's own).
+KernelSig uio_piece_kernel_sig();
 }  // namespace h3c_rt
 
 #define HIP_TRY(expr)               \

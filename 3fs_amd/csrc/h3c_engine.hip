@@ -1028,11 +1028,12 @@ int current_device(int *dev) {
 }
 
 // h3c_test_hook state: read from the environment once, settable by tests.
-constexpr int kHooks = 9;
+constexpr int kHooks = 10;
 std::atomic<uint64_t> g_hooks[kHooks];
 const bool g_hooks_init = [] {
   const char *names[kHooks] = {nullptr, "H3C_SEG_BYTES", "H3C_DEBUG_FLAGS", "H3C_UPD_SCAN", "H3C_UPD_GRAPHS",
-                                "H3C_UPD_LOOKBACK", "H3C_UPD_FRONT", "H3C_UPD_FAST", "H3C_UPD_GIVEUP"};
+                                "H3C_UPD_LOOKBACK", "H3C_UPD_FRONT", "H3C_UPD_FAST", "H3C_UPD_GIVEUP",
+                                "H3C_FAST_POLL_US"};
   for (int k = 1; k < kHooks; ++k) {
     uint64_t v = 0;
     if (const char *e = std::getenv(names[k])) {
@@ -1204,16 +1205,24 @@ hipError_t prof_stamp(int dev, ProfToken &t) {
   t.dev = dev;
   t.slot = p.next++;
   t.ts = p.d + 2 * t.slot;
+  // the slot's record exists from now on (kind -1 until prof_end fills it in), so that an
+  // h3c_profile_read in between neither frees nor re-initialises a slot still in flight
+  ProfRec r{nullptr, nullptr, 0, -1};
+  r.dev = dev;
+  r.slot = t.slot;
+  g_prof.push_back(r);
   return hipSuccess;
 }
 hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes) {
   if (!t.on) return hipSuccess;
-  if (t.ts) {  // stamped by the kernel itself
+  if (t.ts) {  // stamped by the kernel itself: its pending record gets its kind and bytes
     std::lock_guard<std::mutex> lk(g_prof_mu);
-    ProfRec r{nullptr, nullptr, bytes, kind};
-    r.dev = t.dev;
-    r.slot = t.slot;
-    g_prof.push_back(r);
+    for (size_t i = g_prof.size(); i-- > 0;)
+      if (g_prof[i].kind == -1 && g_prof[i].dev == t.dev && g_prof[i].slot == t.slot) {
+        g_prof[i].kind = kind;
+        g_prof[i].bytes = bytes;
+        break;
+      }
     return hipSuccess;
   }
   if (!t.a) return hipSuccess;  // (a stamped launch with no slot left)
@@ -1325,6 +1334,13 @@ int launch_uio_piece_crc(hipStream_t st, int dev, int type, const h3c_update_io 
   HIP_TRY(hipGetLastError());
   return H3C_OK;
 }
+template <>
+struct ArgLayout<UioPieceSrc, void> {
+  static void fill(ArgSpec &a) {
+    struct_arg<UioPieceSrc>(a, {offsetof(UioPieceSrc, ios), offsetof(UioPieceSrc, chunks)});
+  }
+};
+KernelSig uio_piece_kernel_sig() { return kernel_sig(op_piece_crc_kernel<UioPieceSrc>, "op_piece_crc_kernel<UioPieceSrc>"); }
 
 // Chunks of at most this many 1 KiB rows take the small-chunk kernel when every chunk of
 // the batch is one segment: seg_quad_kernel beats the segment kernel + finalize up to
@@ -1576,28 +1592,45 @@ int h3c_profile_read(int kind, double *kernel_ms, uint64_t *launches, uint64_t *
     std::vector<unsigned long long> v(2 * (size_t)p.next);
     hipError_t e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(v.data(), p.d, v.size() * 8, hipMemcpyDeviceToHost);
-    std::vector<unsigned long long> init(v.size());
-    for (size_t i = 0; i < init.size(); i += 2) init[i] = ~0ull, init[i + 1] = 0;
-    if (e == hipSuccess) e = hipMemcpy(p.d, init.data(), init.size() * 8, hipMemcpyHostToDevice);
+    bool pend = false;
+    for (auto &r : g_prof) pend = pend || (r.dev == d && r.slot >= 0 && r.kind == -1);
+    if (!pend) {  // every slot handed out is recorded: the pool rewinds (else slots are freed one by one below)
+      std::vector<unsigned long long> init(v.size());
+      for (size_t i = 0; i < init.size(); i += 2) init[i] = ~0ull, init[i + 1] = 0;
+      if (e == hipSuccess) e = hipMemcpy(p.d, init.data(), init.size() * 8, hipMemcpyHostToDevice);
+    }
     (void)hipSetDevice(prev);
     if (e != hipSuccess) {
       set_error("h3c_profile_read (stamps)", e);
       return H3C_ERR_HIP;
     }
     const int khz = h3c_rt::device_wall_clock_khz(d);
+    bool pending = false;  // a slot handed out whose launch is not recorded yet (prof_stamp .. prof_end)
+    for (auto &r : g_prof) pending = pending || (r.dev == d && r.slot >= 0 && r.kind == -1);
     for (auto &r : g_prof) {
-      if (r.dev != d || r.slot < 0) continue;
+      if (r.dev != d || r.slot < 0 || r.kind == -1) continue;
       const unsigned long long t0 = v[2 * (size_t)r.slot], t1 = v[2 * (size_t)r.slot + 1];
       if (t1 > t0 && t0 != ~0ull && khz > 0) {
         g_prof_ms_done[r.kind] += (double)(t1 - t0) / khz;
         g_prof_launch_done[r.kind] += 1;
         g_prof_bytes_done[r.kind] += r.bytes;
       }
+      if (pending) {  // only the slots read here are freed; the pool is not rewound past a pending one
+        (void)hipSetDevice(d);
+        const unsigned long long fr[2] = {~0ull, 0ull};
+        (void)hipMemcpy(p.d + 2 * (size_t)r.slot, fr, 16, hipMemcpyHostToDevice);
+        (void)hipSetDevice(prev);
+      }
       r.slot = -2;  // (done)
     }
-    p.next = 0;
+    if (!pending) p.next = 0;
   }
+  std::vector<ProfRec> keep;  // pending stamp records stay for the next read
   for (auto &r : g_prof) {
+    if (r.kind == -1) {
+      keep.push_back(r);
+      continue;
+    }
     if (r.slot != -1) continue;  // (stamp records were read above)
     HIP_TRY(hipEventSynchronize(r.b));
     float ms = 0;
@@ -1608,7 +1641,7 @@ int h3c_profile_read(int kind, double *kernel_ms, uint64_t *launches, uint64_t *
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
   }
-  g_prof.clear();
+  g_prof.swap(keep);
   if (kernel_ms) *kernel_ms = g_prof_ms_done[kind];
   if (launches) *launches = g_prof_launch_done[kind];
   if (bytes) *bytes = g_prof_bytes_done[kind];

@@ -2934,6 +2934,9 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_res_kernel(
     __shared__ unsigned int sh[8];
     ctr_add_block(sh, ctr, v8);
   }
+  // Every wave's result and counter stores complete (each wave waits for its own) before the tile
+  // counts itself done: the count is what the last tile's outcome word stands on.
+  stores_done();
   __syncthreads();
   if (t == 0) {
     // test hook (H3C_HOOK_UPD_GIVEUP bit 2): tile 1 reports the pass void, as the look-back form's
@@ -2952,6 +2955,12 @@ __global__ __launch_bounds__(kTailTile) void uio_fast_res_kernel(
 #pragma unroll
     for (uint32_t w = 0; w < sizeof(h3c_chunk_state) / 8; ++w) o[w] = ld_agent(&in[w]);
   }
+  // The outcome word ends the batch for the host: update_core returns on it and the leases holding
+  // misc and chunks_out go back to their pools.  So every wave of this tile has finished reading misc
+  // and chunks_out, and its commit stores are complete, before thread 0 publishes it (the commit of
+  // chunks 64..127 is wave 1's; __threadfence_system() orders only wave 0's own accesses).
+  stores_done();
+  __syncthreads();
   if (t == 0) {
     st_agent(&misc[kMiscFast], fs);
     if (hout) fast_outcome_to_host(misc, hout, fs);
@@ -3261,9 +3270,10 @@ hipError_t sort_pairs(void *tmp, size_t &tmp_bytes, const uint32_t *k, uint32_t 
 // ---- per-thread cache of captured pipeline graphs (update_core) ----
 // h3c_diag_counter: 0 graph replays, 1 captures, 2 capture failures, 3 front-void redos, 4 phase-B
 // reruns, 5 failed-A6 redos, 6 short fragment guesses, 7 fast-branch batches, 8 fast-branch attempts
-// abandoned (an op did not qualify), 9 fast-branch recoveries, 10 graphs refused by the topology check
+// abandoned (an op did not qualify), 9 fast-branch recoveries, 10 graphs refused by the topology check,
+// 11 graphs refused by the pointer audit (graph_pointers_in_key)
 enum { kDiagReplay, kDiagCapture, kDiagCaptureFail, kDiagFrontVoid, kDiagPBVoid, kDiagA6Redo, kDiagShortF,
-       kDiagFast, kDiagFastAbort, kDiagFastVoid, kDiagTopology, kDiagN };
+       kDiagFast, kDiagFastAbort, kDiagFastVoid, kDiagTopology, kDiagPtrAudit, kDiagN };
 std::atomic<uint64_t> g_graph_stats[kDiagN];
 struct UpdGraphKey {
   int dev;
@@ -3321,6 +3331,7 @@ struct ThreadRes {
   struct FastPred {
     int dev = -1;
     uint32_t flags = 0, n = 0, nchunks = 0, general_runs = 0;
+    uint32_t last_us = 0;  // the last fast batch's time from its first launch to the outcome word (host clock)
     const void *chunks = nullptr, *ios = nullptr;
     uint8_t poly = 0, slow = 0;
     uint64_t used = 0;
@@ -3468,7 +3479,7 @@ UpdGraphs *upd_graphs(const UpdGraphKey &key_in, hipStream_t st, bool asked) {
   // the caller's own threads), so only the caller can promise that none launches meanwhile.
   // Test hook: 1 never captures, 2 captures without the flag.
   const uint64_t hk = h3c_rt::hook(H3C_HOOK_UPD_GRAPHS);
-  if (hk == 1 || (!asked && hk != 2)) return nullptr;
+  if (hk == 1 || (!asked && hk != 2 && hk != 3)) return nullptr;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
     (void)hipGetLastError();
@@ -3606,8 +3617,142 @@ bool graph_is_a_chain(hipGraph_t g, GraphShape &sh) {
   return nr == 1 && sh.copies == 0 && sh.reachable == nn;
 }
 
+}  // namespace
+// The struct arguments of capturable kernels: their pointer members (h3c_rt::ArgLayout).
+namespace h3c_rt {
+template <>
+struct ArgLayout<FastArgs, void> {
+  static void fill(ArgSpec &a) {
+    struct_arg<FastArgs>(a, {offsetof(FastArgs, frag), offsetof(FastArgs, key), offsetof(FastArgs, link),
+                             offsetof(FastArgs, head), offsetof(FastArgs, dv), offsetof(FastArgs, slow),
+                             offsetof(FastArgs, pc), offsetof(FastArgs, chain)});
+  }
+};
+template <>
+struct ArgLayout<TMapFn, void> {
+  static void fill(ArgSpec &a) {
+    struct_arg<TMapFn>(a, {offsetof(TMapFn, pos), offsetof(TMapFn, eacc), offsetof(TMapFn, payraw),
+                           offsetof(TMapFn, pc), offsetof(TMapFn, a6)});
+  }
+};
+template <>
+struct ArgLayout<SMapFn, void> {
+  static void fill(ArgSpec &a) {
+    struct_arg<SMapFn>(a, {offsetof(SMapFn, pos), offsetof(SMapFn, skey), offsetof(SMapFn, tscan),
+                           offsetof(SMapFn, t0v), offsetof(SMapFn, eacc), offsetof(SMapFn, payraw),
+                           offsetof(SMapFn, pc), offsetof(SMapFn, a6)});
+  }
+};
+}  // namespace h3c_rt
+namespace {
+
+// Every kernel update_core may enqueue while capturing, with its argument layout.  A captured graph
+// holding a kernel not listed here (rocPRIM's, on the paths that call it) is not instantiated.
+const std::vector<h3c_rt::KernelSig> &capturable_kernels() {
+  using h3c_rt::kernel_sig;
+  static const std::vector<h3c_rt::KernelSig> sigs = {
+#define H3C_SIG(k) kernel_sig(k, #k)
+      H3C_SIG(uio_zero_kernel), H3C_SIG(uio_prep_kernel), H3C_SIG(csort_count_kernel),
+      H3C_SIG(csort_scatter_kernel), H3C_SIG(uio_verify_t0_kernel), H3C_SIG(uio_sz_elem_kernel),
+      H3C_SIG(uio_classify_kernel), H3C_SIG(uio_late_verify_kernel), H3C_SIG(uio_front_kernel),
+      H3C_SIG(uio_frag_kernel), H3C_SIG(uio_tlink_kernel), H3C_SIG(uio_resolve_kernel), H3C_SIG(uio_heads_kernel),
+      H3C_SIG(uio_block_kernel), H3C_SIG(uio_phaseb_kernel), H3C_SIG(uio_elem_kernel<TMapFn>),
+      H3C_SIG(uio_elem_kernel<SMapFn>), H3C_SIG(uio_result_kernel), H3C_SIG(uio_stale_kernel),
+      H3C_SIG(uio_commit_kernel), H3C_SIG(uio_fast_link_kernel), H3C_SIG(uio_fast_kernel),
+      H3C_SIG(uio_fast_sum_kernel), H3C_SIG(uio_fast_res_kernel), h3c_rt::uio_piece_kernel_sig(),
+#undef H3C_SIG
+  };
+  return sigs;
+}
+
+// What the last capture's pointer audit saw (h3c_diag_last_graph_audit): kernel nodes audited, pointer
+// arguments checked, pointers outside every named buffer, kernel nodes with no registered layout.
+struct GraphAudit {
+  uint64_t kernels = 0, pointers = 0, outside = 0, unknown = 0;
+};
+thread_local GraphAudit t_last_audit;
+struct AddrRange {
+  uint64_t lo, hi;  // [lo, hi)
+};
+
+// Every pointer argument of every kernel node of `g` is null or lies inside one of `allow` (the
+// buffers named by the batch's UpdGraphKey and the library's constant tables).  A kernel node whose
+// function has no registered layout fails the audit (its arguments cannot be read).
+bool graph_pointers_in_key(hipGraph_t g, const std::vector<AddrRange> &allow, GraphAudit &au) {
+  au = GraphAudit{};
+  size_t nn = 0;
+  if (hipGraphGetNodes(g, nullptr, &nn) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  std::vector<hipGraphNode_t> nodes(nn);
+  if (nn && hipGraphGetNodes(g, nodes.data(), &nn) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const std::vector<h3c_rt::KernelSig> &sigs = capturable_kernels();
+  bool ok = true;
+  for (hipGraphNode_t x : nodes) {
+    hipGraphNodeType ty = hipGraphNodeTypeCount;
+    if (hipGraphNodeGetType(x, &ty) != hipSuccess || ty != hipGraphNodeTypeKernel) {
+      (void)hipGetLastError();
+      continue;  // (graph_is_a_chain refuses every other node type)
+    }
+    hipKernelNodeParams p{};
+    if (hipGraphKernelNodeGetParams(x, &p) != hipSuccess) {
+      (void)hipGetLastError();
+      ++au.unknown;
+      ok = false;
+      continue;
+    }
+    ++au.kernels;
+    const h3c_rt::KernelSig *sig = nullptr;
+    for (const h3c_rt::KernelSig &s : sigs)
+      if (s.fn == p.func) sig = &s;
+    // the argument values: one pointer per argument (kernelParams), or one packed buffer (`extra`)
+    const char *packed = nullptr;
+    size_t packed_size = 0;
+    if (!p.kernelParams && p.extra) {
+      for (void **e = p.extra; *e != HIP_LAUNCH_PARAM_END; e += 2) {
+        if (*e == HIP_LAUNCH_PARAM_BUFFER_POINTER) packed = static_cast<const char *>(e[1]);
+        if (*e == HIP_LAUNCH_PARAM_BUFFER_SIZE) packed_size = *static_cast<const size_t *>(e[1]);
+      }
+    }
+    if (!sig || (!p.kernelParams && !packed)) {
+      ++au.unknown;
+      ok = false;
+      continue;
+    }
+    size_t off = 0;
+    for (uint32_t i = 0; i < sig->nargs; ++i) {
+      const h3c_rt::ArgSpec &a = sig->args[i];
+      off = (off + a.align - 1) / a.align * a.align;
+      const char *v = p.kernelParams ? static_cast<const char *>(p.kernelParams[i]) : packed + off;
+      off += a.size;
+      if (!p.kernelParams && off > packed_size) {
+        ++au.unknown;
+        ok = false;
+        break;
+      }
+      for (uint32_t q = 0; q < a.nptr; ++q) {
+        uint64_t ptr = 0;
+        std::memcpy(&ptr, v + a.ptr_off[q], sizeof(ptr));
+        ++au.pointers;
+        if (!ptr) continue;
+        bool in = false;
+        for (const AddrRange &r : allow) in = in || (ptr >= r.lo && ptr < r.hi);
+        if (!in) {
+          ++au.outside;
+          ok = false;
+        }
+      }
+    }
+  }
+  return ok && au.kernels;
+}
+
 template <class Body>
-int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out) {
+int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out, const std::vector<AddrRange> &allow) {
   std::lock_guard<std::mutex> lk(g_capture_mu);
   std::unique_lock<std::shared_mutex> gate(h3c_rt::capture_gate());  // (legacy-stream entries wait it out)
   // Relaxed: the capture makes no synchronous or allocating call itself, and it should not make
@@ -3633,6 +3778,13 @@ int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out) {
     out = nullptr;
     return H3C_ERR_HIP;
   }
+  if (!graph_pointers_in_key(g, allow, t_last_audit)) {  // a baked-in pointer the key does not name
+    (void)hipGraphDestroy(g);
+    g_graph_stats[kDiagPtrAudit].fetch_add(1);
+    h3c_rt::set_error_text("graph capture: a kernel argument points outside the buffers of the graph key");
+    out = nullptr;
+    return H3C_ERR_HIP;
+  }
   const hipError_t ie = hipGraphInstantiate(&out, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   if (ie != hipSuccess) {
@@ -3644,7 +3796,17 @@ int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out) {
 }
 
 // Spin (bounded) until the device sets a pinned host word; a blocking stream wait follows either way.
-constexpr uint32_t kFastPollUs = 2000;
+// The bound: h3c_test_hook(H3C_HOOK_FAST_POLL_US) / H3C_FAST_POLL_US when set, else twice the time this
+// thread's last fast batch of the same shape took to reach its outcome (+ 50 us), within
+// [kFastPollMinUs, kFastPollUs] -- a caller's core is not burnt for milliseconds on a batch known to take
+// 0.3 ms, and a batch that runs long (a contended GPU) falls back to the blocking wait.
+constexpr uint32_t kFastPollUs = 2000, kFastPollMinUs = 100;
+uint32_t fast_poll_budget_us(uint32_t last_us) {
+  const uint64_t hk = h3c_rt::hook(H3C_HOOK_FAST_POLL_US);
+  if (hk) return (uint32_t)std::min<uint64_t>(hk, 1000000u);
+  if (!last_us) return kFastPollUs;
+  return std::min(kFastPollUs, std::max(kFastPollMinUs, 2 * last_us + 50));
+}
 bool poll_host_word(const uint32_t *w, uint32_t max_us) {
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t i = 0; !__atomic_load_n(w, __ATOMIC_ACQUIRE); ++i) {
@@ -3814,7 +3976,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     }
     return (size_t)(cur - base);
   };
-  h3c_rt::DeviceLease lease1(dev, layout(nullptr));
+  const size_t lease1_bytes = layout(nullptr);
+  h3c_rt::DeviceLease lease1(dev, lease1_bytes);
   if (!lease1.ok()) return H3C_ERR_HIP;
   layout(lease1.data());
   fa.pc = pc;
@@ -3826,6 +3989,28 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   AuxStream *aux = nullptr;
   int rc = aux_stream(dev, aux);
   if (rc) return rc;
+  // The buffers a captured graph of this batch may point into: those its UpdGraphKey names (the
+  // caller's tables, the leases, the pinned outcome words, the thread's fast scratch) and the library's
+  // constant tables.  Test hook H3C_HOOK_UPD_GRAPHS = 3 leaves lease1 out, so that the audit's refusal
+  // path is exercised (every pipeline kernel points into lease1).
+  auto allow_of = [&](const void *lease2, size_t lease2_bytes, const void *scratch, size_t scratch_bytes) {
+    std::vector<AddrRange> a;
+    auto add = [&](const void *p, size_t bytes) {
+      if (p && bytes) a.push_back(AddrRange{(uint64_t)(uintptr_t)p, (uint64_t)(uintptr_t)p + bytes});
+    };
+    add(d_chunks, sizeof(h3c_chunk_state) * (size_t)nchunks);
+    add(d_chunks_out, sizeof(h3c_chunk_state) * (size_t)C);
+    add(d_ios, sizeof(h3c_update_io) * (size_t)n);
+    add(d_res, sizeof(h3c_update_result) * (size_t)n);
+    add(d_ctr, 8 * (size_t)kCtrN);
+    if (h3c_rt::hook(H3C_HOOK_UPD_GRAPHS) != 3) add(lease1.data(), lease1_bytes);
+    add(lease2, lease2_bytes);
+    add(d_hF, 4096);
+    add(scratch, scratch_bytes);
+    add(h3c_rt::device_consts(dev, H3C_TYPE_CRC32C), sizeof(PolyConsts));
+    add(h3c_rt::device_consts(dev, H3C_TYPE_CRC32), sizeof(PolyConsts));
+    return a;
+  };
 
   StreamDrain drain{st, true};  // every return below waits for both streams before the leases go back
   StreamDrain drain_aux{aux->st, true};
@@ -4000,7 +4185,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         if (!r) r = fast_kernel(cst, true);
         if (!r && epi_graph && !commit_dev) r = epilogue(cst, d_misc + kMiscOutF, cap);
         return r;
-      }, gr->g) : H3C_ERR_HIP;
+      }, gr->g, allow_of(nullptr, 0, fsc->p, 4 * fsc->words)) : H3C_ERR_HIP;
       g_graph_stats[rc ? kDiagCaptureFail : kDiagCapture].fetch_add(1);
       if (rc) {
         gr->failed = true;
@@ -4011,6 +4196,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     const bool use_graph = gr && gr->g && !gr->failed;
     uint32_t *h_fs = &h_F[kMiscFast - kMiscOutF];  // set last by the tail (fast_outcome_to_host)
     __atomic_store_n(h_fs, 0u, __ATOMIC_RELAXED);
+    const auto t_launch = std::chrono::steady_clock::now();
     if (use_graph) {
       HIP_TRY(hipGraphLaunch(gr->g, st));
       g_graph_stats[kDiagReplay].fetch_add(1);
@@ -4026,7 +4212,13 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     }
     // the outcome word polled for up to kFastPollUs before the blocking synchronisation: a blocking wait
     // that starts while the batch runs wakes ~10-20 us after it ends
-    const bool seen = poll_host_word(h_fs, kFastPollUs);
+    const uint32_t poll_us = fast_poll_budget_us(fpred->last_us);
+    const bool seen = poll_host_word(h_fs, poll_us);
+    if (seen)
+      fpred->last_us = (uint32_t)std::max<int64_t>(
+          1, std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t_launch).count());
+    else
+      fpred->last_us = 0;  // (unknown: the next batch of the shape spins up to the default bound)
     if (seen && commit_dev && *h_fs == kFastDone && !h_F[kMiscErr - kMiscOutF]) {
       // The device-table entry, done on the fast branch: the tail has committed the states and written
       // every output before the outcome word, and no further work of this call follows, so the call
@@ -4047,7 +4239,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       drain.armed = drain_aux.armed = false;
       return H3C_OK;
     }
-    const hipError_t se = stream_wait(st, kFastPollUs);
+    const hipError_t se = stream_wait(st, seen ? std::min(poll_us, 200u) : 0u);  // (unseen: spun long enough)
     if (se != hipSuccess) {
       drain.armed = drain_aux.armed = false;
       h3c_rt::set_error("h3c_update_ios (fast branch)", se);
@@ -4110,7 +4302,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       d_hhead = carve<uint32_t>(c2, hcap);
       return (size_t)(c2 - base);
     };
-    h3c_rt::DeviceLease lease2(dev, layout2(nullptr));
+    const size_t lease2_bytes = layout2(nullptr);
+    h3c_rt::DeviceLease lease2(dev, lease2_bytes);
     if (!lease2.ok()) return H3C_ERR_HIP;
     StreamDrain drain2{st, true};
     layout2(lease2.data());
@@ -4218,7 +4411,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
         if (!r) r = phase_b(cst);
         if (!r && epi_graph) r = epilogue(cst, d_misc + kMiscOutF, cap);
         return r;
-      }, gr->g) : H3C_ERR_HIP;
+      }, gr->g, allow_of(lease2.data(), lease2_bytes, nullptr, 0)) : H3C_ERR_HIP;
       if (rc) {  // not capturable here: plain launches from now on for this shape
         gr->failed = true;
         (void)hipGetLastError();
@@ -4362,6 +4555,14 @@ extern "C" int h3c_diag_last_graph(uint64_t *out7) {
   const GraphShape &g = t_last_graph;
   const uint64_t v[7] = {g.nodes, g.roots, g.copies, g.kernels, g.reachable, g.edges, g.max_out};
   std::memcpy(out7, v, sizeof(v));
+  return H3C_OK;
+}
+
+extern "C" int h3c_diag_last_graph_audit(uint64_t *out4) {
+  if (!out4) return H3C_ERR_INVALID_ARG;
+  const GraphAudit &a = t_last_audit;
+  const uint64_t v[4] = {a.kernels, a.pointers, a.outside, a.unknown};
+  std::memcpy(out4, v, sizeof(v));
   return H3C_OK;
 }
 

@@ -90,6 +90,7 @@ _proto("h3c_test_hook", _int, _int, _u64)
 _proto("h3c_set_coalescing", _int, _int)
 _proto("h3c_diag_counter", _u64, _int)
 _proto("h3c_diag_last_graph", _int, _vp)
+_proto("h3c_diag_last_graph_audit", _int, _vp)
 _proto("h3c_diag_sync_bench", _int, _int, _u64, _int, _int, _vp, _vp)
 _proto("h3c_update_ios_dev", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp)
 _proto("h3c_serde_checksum_mark", _u32, _u32, _int)
@@ -355,13 +356,13 @@ def sync_bench(threads: int, nbytes: int, calls: int, api: str = "verify"):
 
 
 HOOK_SEG_BYTES, HOOK_DEBUG_FLAGS, HOOK_UPD_SCAN, HOOK_UPD_GRAPHS, HOOK_UPD_LOOKBACK, HOOK_UPD_FRONT = 1, 2, 3, 4, 5, 6
-HOOK_UPD_FAST, HOOK_UPD_GIVEUP = 7, 8
+HOOK_UPD_FAST, HOOK_UPD_GIVEUP, HOOK_FAST_POLL_US = 7, 8, 9
 UPD_SCAN_PATHS = {"default": 0, "fused": 1, "tiles": 2, "sort": 3}
 
 # h3c_diag_counter indices (include/h3c_crc.h): process-wide, monotonic
 DIAG_NAMES = ("graph_replays", "graph_captures", "graph_capture_failures", "redo_front_void", "rerun_phase_b_void",
               "redo_failed_a6", "redo_short_fragment_guess", "fast_batches", "fast_abandoned", "fast_recovered",
-              "graph_topology_refused")
+              "graph_topology_refused", "graph_pointer_refused")
 
 
 def diag_counter(which: int) -> int:
@@ -374,6 +375,13 @@ def diag_last_graph() -> dict:
     out = (ctypes.c_uint64 * 7)()
     _check(lib.h3c_diag_last_graph(ctypes.cast(out, ctypes.c_void_p)))
     return dict(zip(("nodes", "roots", "copies", "kernels", "reachable", "edges", "max_out"), map(int, out)))
+
+
+def diag_last_graph_audit() -> dict:
+    """h3c_diag_last_graph_audit: the pointer audit of the last UpdateIO graph this thread captured."""
+    out = (ctypes.c_uint64 * 4)()
+    _check(lib.h3c_diag_last_graph_audit(ctypes.cast(out, ctypes.c_void_p)))
+    return dict(zip(("kernels", "pointers", "outside", "unknown"), map(int, out)))
 
 
 def diag_counters() -> dict:

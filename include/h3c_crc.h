@@ -439,7 +439,9 @@ enum h3c_hook {
   H3C_HOOK_DEBUG_FLAGS = 2, /* bit0: no pipelined row loop; bit1: no small-chunk kernel; bit2: no uniform kernel */
   H3C_HOOK_UPD_SCAN = 3,    /* h3c_update_blocks: 1 fused, 2 dense tiles, 3 sort + scan_by_key */
   H3C_HOOK_UPD_GRAPHS = 4,  /* h3c_update_ios: 1 never replays its pipeline as HIP graphs, even with
-                               H3C_UPD_GRAPHS; 2 captures them without the flag */
+                               H3C_UPD_GRAPHS; 2 captures them without the flag; 3 as 2, with the first
+                               device lease left out of the pointer audit's buffers (every capture is refused:
+                               the audit's refusal path, for tests) */
   H3C_HOOK_UPD_LOOKBACK = 5, /* h3c_update_blocks fused path: 1 makes the workgroup with ticket 1 give up
                                its look-back at once, as a starved wait would (the void-batch report:
                                *n_invalid = UINT32_MAX, counters.invalid = UINT64_MAX) */
@@ -450,10 +452,13 @@ enum h3c_hook {
                                pipeline); 2 tries it first on every batch, whatever the last outcome of the
                                batch shape was (default 0: tried first unless this thread's last batch of the
                                same shape and tables did not qualify) */
-  H3C_HOOK_UPD_GIVEUP = 8    /* h3c_update_ios, bit mask: a starved wait forced (spin limit 0) in the tile or
+  H3C_HOOK_UPD_GIVEUP = 8,   /* h3c_update_ios, bit mask: a starved wait forced (spin limit 0) in the tile or
                                workgroup with ticket 1 of -- 1: uio_front_kernel (the pass is void and redone on
                                the scan-based stage), 2: uio_phaseb_kernel (phase B rerun the scan-based way),
                                4: uio_fast_kernel's look-back (results recomputed by the recovery kernel) */
+  H3C_HOOK_FAST_POLL_US = 9  /* h3c_update_ios fast branch: the most microseconds the calling thread spins on the
+                               batch's outcome word before a blocking wait (0: adaptive, twice the last batch of
+                               the same shape + 50 us, within [100, 2000]) */
 };
 int h3c_test_hook(int key, uint64_t value);
 /* Engine-internal counters (process-wide, monotonic) for tests and benches:
@@ -466,13 +471,20 @@ int h3c_test_hook(int key, uint64_t value);
  *   8 fast-branch attempts abandoned because an op did not qualify (the general pipeline ran),
  *   9 fast-branch batches whose results were recomputed after a workgroup gave up waiting,
  *   10 captured graphs refused by the topology check (a memset / memcpy node, or a kernel node not
- *      ordered after the graph's root) and run as plain launches instead. */
+ *      ordered after the graph's root) and run as plain launches instead,
+ *   11 captured graphs refused by the pointer audit (a kernel argument pointing outside every buffer
+ *      the graph cache's key names, or a kernel with no registered argument layout) and run as plain
+ *      launches instead. */
 uint64_t h3c_diag_counter(int which);
 /* The shape of the last graph this thread captured for h3c_update_ios (tests): out7 = {nodes, root
  * nodes, memset + memcpy nodes, kernel nodes, nodes reachable from the first root, edges, the largest
  * out-degree}.  A graph is instantiated only when it is one chain of kernel nodes (one root, every
  * node reachable, no memset / memcpy node); else the shape runs as plain launches (counter 10). */
 int h3c_diag_last_graph(uint64_t *out7);
+/* The pointer audit of the last graph this thread captured for h3c_update_ios (tests): out4 = {kernel
+ * nodes audited, pointer arguments checked, pointers outside the key's buffers, kernel nodes whose
+ * arguments could not be read}.  A graph is instantiated only when the last two are 0. */
+int h3c_diag_last_graph_audit(uint64_t *out4);
 
 #ifdef __cplusplus
 }

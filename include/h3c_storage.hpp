@@ -163,20 +163,26 @@ enum class ChunkState : uint8_t { COMMIT = 0, DIRTY = 1, CLEAN = 2 };
 struct ChunkVersion {
   uint32_t updateVer = 0, commitVer = 0, chainVer = 0;
   ChunkState chunkState = ChunkState::CLEAN;
+  uint64_t chunkSize = 0;  // meta.innerFileId.chunkSize (0: not known to the gate, not checked)
 };
 // One update or commit of a chunk as the gate sees it.
 struct VersionedOp {
   uint32_t chunk = 0;           // index into the batch's chunk table
   bool isCommit = false;        // ChunkReplica::commit (CommitIO) rather than ChunkReplica::update
+  bool isRemove = false;        // UpdateIO.isRemove(): no range check, the stored chunk size is its own
   uint32_t updateVer = 0;       // UpdateIO.updateVer (0: the next one) / CommitIO.commitVer
   uint32_t commitChainVer = 0;  // job.commitChainVer()
   bool isSyncing = false;       // UpdateOptions.isSyncing
   bool isForce = false;         // CommitIO.isForce
   bool checksumOk = true;       // the op's client-checksum verify passed (ChunkReplica.cc:193-207), if known
+  uint64_t chunkSize = 0;       // UpdateIO.chunkSize (0: not checked by the gate)
+  uint64_t offset = 0, length = 0;  // UpdateIO.offset / length (range-checked against chunkSize when it is set)
 };
 
 // The version / state gate that stays on the host.  ChunkReplica::update rejects an op
-// before touching its bytes when the chunk is DIRTY and the op is not syncing (4005, :181-185), when a
+// before touching its bytes, in this order: a range outside the op's own chunkSize (kInvalidArg, :141-146),
+// a chunkSize that differs from the stored chunk's (4015, :171-180; both checked only when the op and the
+// chunk carry a chunkSize), the chunk DIRTY and the op not syncing (4005, :181-185), when a
 // committed chunk's chain version is newer than the op's (4081, :186-191), and -- after the checksum
 // verify at :193-207 -- when updateVer is committed (4008), stale (4006), missing one (4007) or, for
 // updateVer 0, too far ahead (4012) (:211-239); a successful op sets updateVer and, at its end, a CLEAN
@@ -186,7 +192,10 @@ struct VersionedOp {
 // (0: admitted); `versions` end as the reference's metadata would.  The checksum verify sits between the
 // two groups of checks: an op with checksumOk == false fails with 4080 after the first group, as the
 // reference's does, and changes no version.  Ops admitted here go to h3c_update_ios; the others are
-// answered with their status and not submitted.
+// answered with their status and not submitted.  Every code the reference returns before a version change
+// is decided here (range, 4015, 4005, 4081, 4080 from the verdicts given, 4006-4012); an op admitted here is
+// one the engine applies, so the versions the gate leaves are the reference's -- provided `checksumOk` carries
+// the verify verdicts (h3c_batch_verify first) whenever a payload may fail it.
 struct VersionGate {
   static void run(std::vector<ChunkVersion> &versions, const std::vector<VersionedOp> &ops,
                   std::vector<uint32_t> &status) {
@@ -217,6 +226,15 @@ struct VersionGate {
           m.chunkState = ChunkState::COMMIT;
           m.chainVer = op.commitChainVer;
         }
+        continue;
+      }
+      if (!op.isRemove && op.chunkSize &&
+          (op.offset >= op.chunkSize || op.offset + op.length > op.chunkSize)) {  // :141-146
+        status[i] = kInvalidArg;
+        continue;
+      }
+      if (!op.isRemove && op.chunkSize && m.chunkSize && m.chunkSize != op.chunkSize) {  // :171-180
+        status[i] = kChunkSizeMismatch;
         continue;
       }
       if (m.chunkState == ChunkState::DIRTY && !op.isSyncing) {  // :181-185

@@ -413,8 +413,11 @@ static void data_iterator(bool gpu) {
 // replayed on the host in sequence order, each case of the reference once, including
 // the cascade of a failed checksum verify (the chunk's updateVer stays, so the next op misses one).
 static void version_gate() {
-  std::vector<ChunkVersion> v(4);
+  std::vector<ChunkVersion> v(5);
   v[1].chunkState = ChunkState::DIRTY;
+  v[4].chunkState = ChunkState::DIRTY;  // (a 64 KiB chunk: the chunkSize / range cases)
+  v[4].chunkSize = 64 << 10;
+  v[4].updateVer = v[4].commitVer = 2;
   v[2].chunkState = ChunkState::COMMIT;
   v[2].chainVer = 7;
   v[2].updateVer = v[2].commitVer = 5;
@@ -436,6 +439,19 @@ static void version_gate() {
     o.isForce = force;
     return o;
   };
+  auto sized = [](uint32_t c, uint32_t ver, uint64_t cs, uint64_t off, uint64_t len, bool sync = false,
+                  bool remove = false) {
+    VersionedOp o;
+    o.chunk = c;
+    o.updateVer = ver;
+    o.commitChainVer = 1;
+    o.isSyncing = sync;
+    o.isRemove = remove;
+    o.chunkSize = cs;
+    o.offset = off;
+    o.length = len;
+    return o;
+  };
   const std::vector<VersionedOp> ops = {
       up(0, 1), up(0, 2), up(0, 2),              // admitted, admitted, stale (4006)
       up(0, 4),                                  // missing one (4007)
@@ -452,9 +468,14 @@ static void version_gate() {
       commit(2, 6, 8),                           // commit 6 == updateVer: COMMIT, chainVer 8
       up(9, 1),                                  // no such chunk (kInvalidArg)
       up(3, 0), up(3, 0),                        // updateVer 0: 1 admitted, then 2 > 0 + 1 (4012)
+      sized(4, 3, 1 << 20, 0, 4096),             // DIRTY chunk 4 (64 KiB) with the wrong chunkSize: 4015 first
+      sized(4, 3, 64 << 10, 64 << 10, 1),        // range outside the op's chunkSize: kInvalidArg before 4005
+      sized(4, 3, 64 << 10, 0, 4096),            // right size, DIRTY, not syncing: 4005
+      sized(4, 10, 1 << 20, 0, 4096, true),      // syncing, wrong size: 4015 (no version change)
+      sized(4, 0, 1 << 20, 0, 0, false, true),   // REMOVE: no size or range check; DIRTY -> 4005
   };
   const std::vector<uint32_t> want = {0, 0, 4006, 4007, 4012, 0, 4008, 4080, 4007, 0, 4005, 0, 4081, 0, 4082, 4023,
-                                      0, 3, 0, 4012};
+                                      0, 3, 0, 4012, 4015, 3, 4005, 4015, 4005};
   std::vector<uint32_t> st;
   VersionGate::run(v, ops, st);
   CHECK(st == want);
@@ -462,6 +483,7 @@ static void version_gate() {
     if (st[i] != want[i]) std::fprintf(stderr, "  op %zu: %u, want %u\n", i, st[i], want[i]);
   CHECK(v[0].updateVer == 3 && v[0].commitVer == 2 && v[0].chunkState == ChunkState::CLEAN);
   CHECK(v[1].updateVer == 9 && v[1].commitVer == 8 && v[1].chunkState == ChunkState::CLEAN);
+  CHECK(v[4].updateVer == 2 && v[4].commitVer == 2 && v[4].chunkState == ChunkState::DIRTY);
   CHECK(v[2].updateVer == 6 && v[2].commitVer == 6 && v[2].chunkState == ChunkState::COMMIT && v[2].chainVer == 8);
   CHECK(v[3].updateVer == 1 && v[3].commitVer == 0);
 }

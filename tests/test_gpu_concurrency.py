@@ -363,3 +363,91 @@ def test_fast_branch_threads_beside_legacy_stream_calls(h3c, torch_dev, graphs):
     assert d["fast_batches"] == nupd * reps and d["fast_abandoned"] == 0, d
     if graphs:
         assert d["graph_capture_failures"] == 0, d
+
+
+def test_fast_branch_wide_tables_concurrent_against_oracle(h3c, torch_dev):
+    """VERDICT r04 #1 (the fast branch's early return): 4 threads, each with its own 100-127-chunk device
+    tables, stream and payloads, run fast-branch batches at once, so the leases one thread's batch returns
+    on its outcome word are taken by another's next batch at once.  Chunks 64-127 are committed by
+    uio_fast_res_kernel's wave 1; the outcome word now follows every wave's reads of misc / chunks_out and
+    its commit stores.  Each repetition restores the thread's bytes and table on its own stream and must
+    give every op's result, every final chunk state and every byte the oracle's ChunkReplica::update
+    replay gives (ChunkReplica.cc:131-394), 2 % of the ops failing A6."""
+    torch, dev = torch_dev
+    G, CL, NW, REPS = 4096, 64 << 10, 1500, 8
+    rng = np.random.default_rng(2026)
+    tabs = []
+    for k in range(4):
+        nch = 100 + 9 * k  # 100, 109, 118, 127 chunks: wave 1 commits chunks 64 and up
+        raw = torch.empty(nch * CL + G, dtype=torch.uint8, device=dev)
+        off = (-raw.data_ptr()) % G
+        slab = raw[off:off + nch * CL]
+        h3c.fill_splitmix(slab, CL, nch, CL, 900 + k)
+        host0 = slab.cpu().numpy().reshape(nch, CL).copy()
+        st = np.zeros(nch, dtype=h3c.CHUNK_STATE_DTYPE)
+        for c in range(nch):
+            st[c] = (slab.data_ptr() + c * CL, CL, CL, orc.crc32c(host0[c]), 1, 0)
+        pay = rng.integers(0, 256, (NW, G), dtype=np.uint8)
+        dpay = torch.from_numpy(pay.reshape(-1)).to(dev)
+        io = np.zeros(NW, dtype=h3c.UPDATE_IO_DTYPE)
+        wc = rng.integers(0, nch, NW)
+        wc[:nch] = np.arange(nch)  # every chunk written, the high ones included
+        wb = rng.integers(0, CL // G, NW)
+        good = rng.random(NW) >= 0.02
+        # the oracle: every op replayed in sequence order on host copies
+        host = host0.copy()
+        meta = [{"size": CL, "type": orc.CRC32C, "value": int(st["value"][c])} for c in range(nch)]
+        want = np.zeros(NW, dtype=h3c.UPDATE_RESULT_DTYPE)
+        for i in range(NW):
+            c, b = int(wc[i]), int(wb[i])
+            ck = orc.crc32c(pay[i]) ^ (0 if good[i] else 0x5A5A)
+            io[i] = (dpay.data_ptr() + i * G, c, b * G, G, ck, 1, h3c.UPD_WRITE, 0, 0, 0)
+            r, meta[c] = orc.replica_update(meta[c], host[c], CL,
+                                            {"kind": orc.UPD_WRITE, "offset": b * G, "length": G,
+                                             "type": orc.CRC32C, "value": ck}, pay[i])
+            want[i] = (r["status"], r["size"], r["value"], r["type"], 0)
+        d_init = torch.from_numpy(st.view(np.uint8).copy()).to(dev)
+        tabs.append(dict(nch=nch, slab=slab, raw=raw, dpay=dpay, bytes0=slab.clone(), d_init=d_init,
+                         d_state=d_init.clone(), d_ios=torch.from_numpy(io.view(np.uint8).copy()).to(dev),
+                         d_res=torch.zeros(NW * h3c.UPDATE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev),
+                         want=want, host=host, final=meta))
+    torch.cuda.synchronize()
+    errors = []
+    start = threading.Barrier(len(tabs))
+
+    def upd(k):
+        tb = tabs[k]
+        try:
+            s = torch.cuda.Stream(device=dev)
+            bound = h3c.UpdateIosDev(tb["d_state"], tb["d_ios"], tb["d_res"], stream=s)
+            start.wait()
+            for r in range(REPS):
+                with torch.cuda.stream(s):
+                    tb["slab"].copy_(tb["bytes0"])
+                    tb["d_state"].copy_(tb["d_init"])
+                bound.run()
+                s.synchronize()
+                res = tb["d_res"].cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)
+                for f in ("status", "size", "value", "type"):
+                    if not np.array_equal(res[f], tb["want"][f]):
+                        bad = np.nonzero(res[f] != tb["want"][f])[0]
+                        errors.append((k, r, "result " + f, int(bad[0]), len(bad)))
+                fin = tb["d_state"].cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)
+                got = [(int(fin["size"][c]), int(fin["type"][c]), int(fin["value"][c])) for c in range(tb["nch"])]
+                exp = [(m["size"], m["type"], m["value"]) for m in tb["final"]]
+                if got != exp:
+                    errors.append((k, r, "state", [c for c in range(tb["nch"]) if got[c] != exp[c]][:8]))
+            if not np.array_equal(tb["slab"].cpu().numpy().reshape(tb["nch"], CL), tb["host"]):
+                errors.append((k, "bytes"))
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    b = h3c.diag_counters()
+    threads = [threading.Thread(target=upd, args=(k,)) for k in range(len(tabs))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=100)
+    assert not errors, errors[:8]
+    d = {k: v - b[k] for k, v in h3c.diag_counters().items()}
+    assert d["fast_batches"] == len(tabs) * REPS and d["fast_abandoned"] == 0, d

@@ -1,9 +1,13 @@
-"""BASELINE config 3 at its real shape through the general UpdateIO path, pinned to the oracle.
+"""BASELINE config 3 at its real shape through both UpdateIO branches, pinned to the oracle.
 
 100k random 4 KiB WRITE UpdateIOs into 64 x 64 MiB chunks (h3c_update_ios_dev, tables in HBM),
-trusted and exact.  The reference semantics replaced are ChunkReplica::update + updateChecksum
+trusted and exact, each run once through the general pipeline (h3c_test_hook(H3C_HOOK_UPD_FAST, 1):
+prep, sort, piece pass, front, block and phase-B kernels) and once through the fast branch (hook 2:
+prep, link, uio_fast_kernel and its tail); the engine's diag counters must say which one ran.  The
+reference semantics replaced are ChunkReplica::update + updateChecksum
 (src/storage/store/ChunkReplica.cc:131-394).  What is checked against the CPU oracle
-(oracle/crc_oracle.c), not against another GPU pass:
+(oracle/crc_oracle.c), not against another GPU pass (the oracle side is computed once per mode and
+shared by both branches):
 
 * every op of 2 chunks (~3,100 ops) replayed one by one through the ChunkReplica::update
   restatement (case iv re-reads the 64 MiB chunk per op): status, size and stored checksum;
@@ -39,77 +43,99 @@ def _host_crcs(host):
     return out
 
 
-@pytest.mark.parametrize("exact", [False, True])
-def test_updio_config3_full_shape_against_oracle(h3c, torch_dev, exact):
-    torch, dev = torch_dev
+_ORACLE = {}
+
+
+def _inputs(exact):
+    """The batch (seeded) and, once per mode, what the oracle says about it."""
     rng = np.random.default_rng(SEED + exact)
     wc = rng.integers(0, NCH, NW).astype(np.uint32)
     wb = rng.integers(0, CL // G, NW).astype(np.uint32)
-    # chunks: the same splitmix generator on both sides (checked on one chunk below)
-    host = np.empty((NCH, CL), dtype=np.uint8)
-    for c in range(NCH):
-        orc.lib().orc_fill_splitmix(host[c].ctypes.data, CL, SEED, c)
-    dchunks = torch.empty(NCH * CL, dtype=torch.uint8, device=dev)
-    h3c.fill_splitmix(dchunks, CL, NCH, CL, SEED)
     pay = rng.integers(0, 256, (NW, G), dtype=np.uint8)
-    dpay = torch.from_numpy(pay).to(dev)
-    assert np.array_equal(dchunks[CL: 2 * CL].cpu().numpy(), host[1])
-    stored = _host_crcs(host)
     stale = {}
     if exact:
         stale = {c: int(rng.integers(1, 1 << 32)) for c in (int(wc[0]), int(wc[1]), 17, 40)}
-    # client checksums from the oracle
-    cks = np.array([orc.crc32c(pay[k]) for k in range(NW)], dtype=np.uint32)
+    if exact not in _ORACLE:
+        # chunks: the same splitmix generator on both sides (checked on one chunk in the test)
+        host = np.empty((NCH, CL), dtype=np.uint8)
+        for c in range(NCH):
+            orc.lib().orc_fill_splitmix(host[c].ctypes.data, CL, SEED, c)
+        chunk1 = host[1].copy()
+        stored = _host_crcs(host)
+        cks = np.array([orc.crc32c(pay[k]) for k in range(NW)], dtype=np.uint32)
+        values = stored ^ np.array([stale.get(c, 0) for c in range(NCH)], dtype=np.uint32)
+        # 2 chunks replayed op by op through ChunkReplica::update (before `host` takes every op's bytes)
+        replay = sorted({int(wc[0]), int(wc[1])} | ({(int(wc[0]) + 1) % NCH} if wc[0] == wc[1] else set()))
+        per_op, finals = {}, {}
+        for c in replay:
+            chunk = host[c].copy()
+            meta = {"size": CL, "type": orc.CRC32C, "value": int(values[c])}
+            ks = np.nonzero(wc == c)[0]
+            assert len(ks) > 1400
+            for k in ks:
+                io = {"kind": orc.UPD_WRITE, "offset": int(wb[k]) * G, "length": G, "type": orc.CRC32C,
+                      "value": int(cks[k])}
+                want, meta = orc.replica_update(meta, chunk, CL, io, pay[k])
+                per_op[int(k)] = (want["status"], want["size"], want["type"], want["value"])
+            finals[c] = (meta["size"], meta["type"], meta["value"])
+        # every op's bytes on the host: the final bytes and checksums of all 64 chunks
+        rows = host.reshape(NCH, CL // G, G)
+        slot = wc.astype(np.int64) * (CL // G) + wb
+        _, last_rev = np.unique(slot[::-1], return_index=True)
+        last = NW - 1 - last_rev  # each slot's last writer in sequence order
+        rows[wc[last], wb[last]] = pay[last]
+        _ORACLE[exact] = dict(chunk1=chunk1, cks=cks, values=values, per_op=per_op, finals=finals,
+                              final_bytes=host, want_final=_host_crcs(host))
+    return wc, wb, pay, stale, _ORACLE[exact]
+
+
+@pytest.mark.parametrize("branch", ["general", "fast"])
+@pytest.mark.parametrize("exact", [False, True])
+def test_updio_config3_full_shape_against_oracle(h3c, torch_dev, hooks, exact, branch):
+    torch, dev = torch_dev
+    wc, wb, pay, stale, o = _inputs(exact)
+    hooks(h3c.HOOK_UPD_FAST, 2 if branch == "fast" else 1)
+    dchunks = torch.empty(NCH * CL, dtype=torch.uint8, device=dev)
+    h3c.fill_splitmix(dchunks, CL, NCH, CL, SEED)
+    dpay = torch.from_numpy(pay).to(dev)
+    assert np.array_equal(dchunks[CL: 2 * CL].cpu().numpy(), o["chunk1"])
     state = np.zeros(NCH, dtype=h3c.CHUNK_STATE_DTYPE)
     state["base"] = dchunks.data_ptr() + np.arange(NCH, dtype=np.uint64) * np.uint64(CL)
     state["chunk_size"] = CL
     state["size"] = CL
-    state["value"] = stored ^ np.array([stale.get(c, 0) for c in range(NCH)], dtype=np.uint32)
+    state["value"] = o["values"]
     state["type"] = orc.CRC32C
     ios = np.zeros(NW, dtype=h3c.UPDATE_IO_DTYPE)
     ios["payload"] = dpay.data_ptr() + np.arange(NW, dtype=np.uint64) * np.uint64(G)
     ios["chunk"] = wc
     ios["offset"] = wb * G
     ios["length"] = G
-    ios["checksum_value"] = cks
+    ios["checksum_value"] = o["cks"]
     ios["checksum_type"] = orc.CRC32C
     ios["kind"] = h3c.UPD_WRITE
-    init_state = state.copy()
     d_state = torch.from_numpy(state.view(np.uint8).copy()).to(dev)
     d_ios = torch.from_numpy(ios.view(np.uint8).copy()).to(dev)
     d_res = torch.zeros(NW * h3c.UPDATE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
     d_ctr = torch.zeros(8, dtype=torch.int64, device=dev)
+    before = h3c.diag_counters()
     h3c.update_ios_dev(d_state, d_ios, d_res, exact=exact, counters=d_ctr)
     torch.cuda.synchronize()
+    diag = {k: v - before[k] for k, v in h3c.diag_counters().items()}
+    # the branch that ran is the branch named, with no redo of any kind
+    assert diag["fast_batches"] == (1 if branch == "fast" else 0), diag
+    assert diag["fast_abandoned"] == 0 and diag["fast_recovered"] == 0, diag
+    assert all(diag[k] == 0 for k in ("redo_front_void", "rerun_phase_b_void", "redo_failed_a6",
+                                      "redo_short_fragment_guess")), diag
     fin = d_state.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)
     res = d_res.cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)
     ctr = d_ctr.cpu().tolist()
-    got_bytes = dchunks.cpu().numpy().reshape(NCH, CL)
-
-    # 2 chunks replayed op by op through ChunkReplica::update (before `host` takes every op's bytes)
-    replay = sorted({int(wc[0]), int(wc[1])} | ({(int(wc[0]) + 1) % NCH} if wc[0] == wc[1] else set()))
-    for c in replay:
-        chunk = host[c].copy()
-        meta = {"size": CL, "type": orc.CRC32C, "value": int(init_state["value"][c])}
-        ks = np.nonzero(wc == c)[0]
-        for k in ks:
-            io = {"kind": orc.UPD_WRITE, "offset": int(wb[k]) * G, "length": G, "type": orc.CRC32C,
-                  "value": int(cks[k])}
-            want, meta = orc.replica_update(meta, chunk, CL, io, pay[k])
-            got = (int(res["status"][k]), int(res["size"][k]), int(res["type"][k]), int(res["value"][k]))
-            assert got == (want["status"], want["size"], want["type"], want["value"]), (c, k)
-        assert (int(fin["size"][c]), int(fin["type"][c]), int(fin["value"][c])) == \
-            (meta["size"], meta["type"], meta["value"]), c
-        assert len(ks) > 1400
-
-    # every op's bytes on the host; all 64 chunks' bytes and final stored checksums
-    rows = host.reshape(NCH, CL // G, G)
-    slot = wc.astype(np.int64) * (CL // G) + wb
-    _, last_rev = np.unique(slot[::-1], return_index=True)
-    last = NW - 1 - last_rev  # each slot's last writer in sequence order
-    rows[wc[last], wb[last]] = pay[last]
-    assert np.array_equal(got_bytes, host)
-    want_final = _host_crcs(host)
+    for k, want in o["per_op"].items():
+        got = (int(res["status"][k]), int(res["size"][k]), int(res["type"][k]), int(res["value"][k]))
+        assert got == want, (branch, k)
+    for c, want in o["finals"].items():
+        assert (int(fin["size"][c]), int(fin["type"][c]), int(fin["value"][c])) == want, c
+    assert np.array_equal(dchunks.cpu().numpy().reshape(NCH, CL), o["final_bytes"])
+    want_final = o["want_final"]
     touched = np.zeros(NCH, dtype=bool)
     touched[wc] = True
     assert touched.all()

@@ -414,3 +414,44 @@ def test_captured_pipeline_is_one_chain(h3c, torch_dev, hooks, fast):
     assert g["copies"] == 0 and g["roots"] == 1 and g["reachable"] == g["nodes"] == g["kernels"], g
     assert g["edges"] == g["nodes"] - 1 and g["max_out"] == 1, g
     assert g["nodes"] >= (5 if fast else 8), g
+    # every pointer argument of every node lies inside a buffer the graph key names
+    assert d["graph_pointer_refused"] == 0, d
+    a = h3c.diag_last_graph_audit()
+    assert a["kernels"] == g["kernels"] and a["outside"] == 0 and a["unknown"] == 0, a
+    assert a["pointers"] >= 4 * a["kernels"], a
+
+
+@pytest.mark.parametrize("fast", [False, True])
+def test_pointer_audit_refuses_a_pointer_outside_the_key(h3c, torch_dev, hooks, fast):
+    """The audit's refusal path: with H3C_HOOK_UPD_GRAPHS = 3 the first device lease (which every
+    pipeline kernel points into) is left out of the audited buffers, so every capture is refused
+    (h3c_diag_counter 11), nothing is replayed, and the batches run as plain launches with the results
+    of the plain first run (the state restored before each run)."""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_GRAPHS, 3)
+    hooks(h3c.HOOK_UPD_FAST, 2 if fast else 1)
+    rng = np.random.default_rng(41 + fast)
+    sc = fast_scenario(h3c, torch, dev, rng, nchunks=8, chunk_size=64 << 10, nops=2000, bad=0.0) if fast else \
+        random_scenario(h3c, torch, dev, rng, nchunks=8, chunk_size=64 << 10, nops=2000)
+    chunks, ios = sc.device_ios()
+    d_chunks0 = torch.from_numpy(chunks.view(np.uint8).copy()).to(dev)
+    d_chunks = d_chunks0.clone()
+    d_ios = torch.from_numpy(ios.view(np.uint8).copy()).to(dev)
+    d_res = torch.zeros(len(ios) * 16, dtype=torch.uint8, device=dev)
+    slab0 = sc.slab.clone()
+    b = h3c.diag_counters()
+    outs = []
+    for _ in range(5):
+        sc.slab.copy_(slab0)
+        d_chunks.copy_(d_chunks0)
+        torch.cuda.synchronize()
+        h3c.update_ios_dev(d_chunks, d_ios, d_res)
+        torch.cuda.synchronize()
+        outs.append((d_res.cpu().numpy().copy(), d_chunks.cpu().numpy().copy(), sc.slab.cpu().numpy().copy()))
+    d = {k: v - b[k] for k, v in h3c.diag_counters().items()}
+    assert d["graph_pointer_refused"] >= 1 and d["graph_replays"] == 0, d
+    a = h3c.diag_last_graph_audit()
+    assert a["outside"] >= 1 and a["unknown"] == 0, a
+    for o in outs[1:]:
+        for x, y in zip(o, outs[0]):
+            assert np.array_equal(x, y)
