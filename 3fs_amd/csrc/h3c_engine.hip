@@ -1028,12 +1028,12 @@ int current_device(int *dev) {
 }
 
 // h3c_test_hook state: read from the environment once, settable by tests.
-constexpr int kHooks = 10;
+constexpr int kHooks = 11;
 std::atomic<uint64_t> g_hooks[kHooks];
 const bool g_hooks_init = [] {
   const char *names[kHooks] = {nullptr, "H3C_SEG_BYTES", "H3C_DEBUG_FLAGS", "H3C_UPD_SCAN", "H3C_UPD_GRAPHS",
                                 "H3C_UPD_LOOKBACK", "H3C_UPD_FRONT", "H3C_UPD_FAST", "H3C_UPD_GIVEUP",
-                                "H3C_FAST_POLL_US"};
+                                "H3C_FAST_POLL_US", "H3C_UPD_ALIGNED"};
   for (int k = 1; k < kHooks; ++k) {
     uint64_t v = 0;
     if (const char *e = std::getenv(names[k])) {

@@ -298,6 +298,43 @@ struct FastArgs {
 };
 __device__ void fast_prep_tile(const FastArgs &fa, uint32_t i, uint32_t n, const h3c_update_io &io,
                                const h3c_chunk_state &cs, uint32_t st, uint8_t poly_type, uint32_t std_domain);
+// An op's validation status before any case analysis (ChunkReplica::update's argument checks, :141-180,
+// and the documented limits of this engine); cs is the op's chunk state (ignored for a COMMIT or a chunk
+// index out of range).
+__device__ __forceinline__ uint32_t op_status(const h3c_update_io &io, const h3c_chunk_state &cs, uint32_t nchunks,
+                                              uint8_t poly_type, uint32_t std_domain) {
+  uint32_t st = H3C_OK;
+  const uint32_t c = io.chunk;
+  const bool kind_ok = io.kind == H3C_UPD_WRITE || io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND ||
+                       io.kind == H3C_UPD_REMOVE || io.kind == H3C_UPD_COMMIT;
+  if (c >= nchunks || !kind_ok) return H3C_ERR_INVALID_ARG;
+  if (io.kind == H3C_UPD_COMMIT) return H3C_OK;
+  const bool syncing = (io.flags & H3C_IO_SYNCING) != 0;
+  if (!cs.base || (io.checksum_type != H3C_TYPE_NONE && io.checksum_type != poly_type)) st = H3C_ERR_INVALID_ARG;
+  if (cs.size > cs.chunk_size) st = H3C_ERR_INVALID_ARG;  // a corrupt chunk state
+  // documented limit: a TRUNCATE / EXTEND of a chunk stored (at the start of the batch) under the
+  // other polynomial -- its stored type would be kept (:328-332), and this batch CRCs in its own
+  if (!std_domain && (io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND) && cs.type != H3C_TYPE_NONE &&
+      cs.type != poly_type)
+    st = H3C_ERR_INVALID_ARG;
+  if (io.kind == H3C_UPD_REMOVE) {  // doRemove's form (StorageOperator.cc:808-815); no range check (:141)
+    if (io.offset || io.length || io.checksum_type != H3C_TYPE_NONE || syncing) st = H3C_ERR_INVALID_ARG;
+  } else {
+    // :141-145 against writeIO.chunkSize (H3C_IO_CHUNK_SIZE; else the chunk's own), then :171-180
+    const bool own = !std_domain && (io.flags & H3C_IO_CHUNK_SIZE);
+    const uint32_t wcs = own ? io.chunk_size : cs.chunk_size;
+    if (io.offset >= wcs || (uint64_t)io.offset + io.length > wcs) st = H3C_ERR_INVALID_ARG;
+    if (io.kind == H3C_UPD_WRITE && io.length && !io.payload) st = H3C_ERR_INVALID_ARG;
+    if (syncing && (io.kind != H3C_UPD_WRITE || io.offset)) st = H3C_ERR_INVALID_ARG;
+    if (st == H3C_OK && wcs != cs.chunk_size) st = H3C_ERR_CHUNK_SIZE_MISMATCH;
+    // A6 on a TRUNCATE / EXTEND: create(type, <no data>, length) is {NONE, 0} (:193-207);
+    // the Rust engine verifies only data (engine.rs:297)
+    if (st == H3C_OK && !std_domain && io.kind != H3C_UPD_WRITE && io.checksum_type != H3C_TYPE_NONE && io.length)
+      st = H3C_ERR_CHECKSUM_MISMATCH;
+  }
+  return st;
+}
+
 #ifndef H3C_PREP_TILE
 #define H3C_PREP_TILE 1024  // items per prep-kernel tile (a power of two, 64..1024)
 #endif
@@ -364,38 +401,10 @@ __global__ __launch_bounds__(kPrepTile) void uio_prep_kernel(
       a6[i] = 0;       // A6 verdicts (the early pass, the front / late checks, the block kernel)
     }
     const h3c_update_io io = io_pre;
-    uint32_t st = H3C_OK;
     const uint32_t c = io.chunk;
-    const bool kind_ok = io.kind == H3C_UPD_WRITE || io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND ||
-                         io.kind == H3C_UPD_REMOVE || io.kind == H3C_UPD_COMMIT;
-    if (c >= nchunks || !kind_ok) {
-      st = H3C_ERR_INVALID_ARG;
-    } else if (io.kind != H3C_UPD_COMMIT) {
-      const h3c_chunk_state cs = lean ? s_cs[c] : chunks[c];
-      const bool syncing = (io.flags & H3C_IO_SYNCING) != 0;
-      if (!cs.base || (io.checksum_type != H3C_TYPE_NONE && io.checksum_type != poly_type)) st = H3C_ERR_INVALID_ARG;
-      if (cs.size > cs.chunk_size) st = H3C_ERR_INVALID_ARG;  // a corrupt chunk state
-      // documented limit: a TRUNCATE / EXTEND of a chunk stored (at the start of the batch) under the
-      // other polynomial -- its stored type would be kept (:328-332), and this batch CRCs in its own
-      if (!std_domain && (io.kind == H3C_UPD_TRUNCATE || io.kind == H3C_UPD_EXTEND) && cs.type != H3C_TYPE_NONE &&
-          cs.type != poly_type)
-        st = H3C_ERR_INVALID_ARG;
-      if (io.kind == H3C_UPD_REMOVE) {  // doRemove's form (StorageOperator.cc:808-815); no range check (:141)
-        if (io.offset || io.length || io.checksum_type != H3C_TYPE_NONE || syncing) st = H3C_ERR_INVALID_ARG;
-      } else {
-        // :141-145 against writeIO.chunkSize (H3C_IO_CHUNK_SIZE; else the chunk's own), then :171-180
-        const bool own = !std_domain && (io.flags & H3C_IO_CHUNK_SIZE);
-        const uint32_t wcs = own ? io.chunk_size : cs.chunk_size;
-        if (io.offset >= wcs || (uint64_t)io.offset + io.length > wcs) st = H3C_ERR_INVALID_ARG;
-        if (io.kind == H3C_UPD_WRITE && io.length && !io.payload) st = H3C_ERR_INVALID_ARG;
-        if (syncing && (io.kind != H3C_UPD_WRITE || io.offset)) st = H3C_ERR_INVALID_ARG;
-        if (st == H3C_OK && wcs != cs.chunk_size) st = H3C_ERR_CHUNK_SIZE_MISMATCH;
-        // A6 on a TRUNCATE / EXTEND: create(type, <no data>, length) is {NONE, 0} (:193-207);
-        // the Rust engine verifies only data (engine.rs:297)
-        if (st == H3C_OK && !std_domain && io.kind != H3C_UPD_WRITE && io.checksum_type != H3C_TYPE_NONE && io.length)
-          st = H3C_ERR_CHECKSUM_MISMATCH;
-      }
-    }
+    h3c_chunk_state cs_v{};
+    if (c < nchunks && io.kind != H3C_UPD_COMMIT) cs_v = lean ? s_cs[c] : chunks[c];
+    const uint32_t st = op_status(io, cs_v, nchunks, poly_type, std_domain);
     if (!lean) {
       status[i] = st;
       key[i] = c < nchunks ? c : nchunks;
@@ -2461,8 +2470,14 @@ __device__ uint32_t g_fast_rot;  // workgroup b takes range (b + g_fast_rot) % g
 #define FAST_MARK(i) ((void)0)
 #endif
 constexpr uint32_t kFastCols = 128;  // chunks a fast-branch batch may name (lane c: chunks c, c + 64)
-// FastScratch words: [0] the slow word, [1, ...) the bucket heads
-constexpr uint32_t kScratchHeads = 1;
+// FastScratch words: [0] the chain-based fast branch's slow word; [64, 128) the aligned sub-branch's control
+// words (kACtlWords); [128, ...) its look-back granules (kAGranRows rows of kFastCols u64); then the fast
+// branch's bucket heads (hcap words, zero between batches) and the aligned sub-branch's (hcap words,
+// epoch-tagged).  A layout for another hcap starts from a zeroed scratch.
+constexpr uint32_t kAGranRows = 1024;  // aligned workgroups at most
+constexpr uint32_t kScratchACtl = 64, kScratchAGran = 128;
+constexpr uint32_t kScratchHeads = kScratchAGran + 2 * kAGranRows * kFastCols;
+constexpr uint32_t kAEpochBatches = 240;  // aligned batches between zeroings (epochs are 8 bits)
 #ifndef H3C_FAST_GRAB
 #define H3C_FAST_GRAB 1  // 1: a workgroup's waves take their chain starts from an LDS counter (0: static ranges)
 #endif
@@ -3100,6 +3115,612 @@ __global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uin
   ctr_add_block(sh, ctr, v);
 }
 
+// ---- the aligned sub-branch: BASELINE config 3's block-aligned 4 KiB WRITEs in two launches ----
+// A fast-branch batch whose every op is a full, block-aligned 4 KiB typed WRITE (aligned_op: config 3
+// exactly) runs as uio_aprep_kernel + uio_afused_kernel instead of the chain-based fast branch's five
+// launches.  It is the block-update scheme of h3c_update.hip (upd_tlink_kernel + upd_fused_kernel) with
+// UpdateIO's A6 check and results added:
+//   uio_aprep_kernel, per tile of 256 ops: validation (op_status) and aligned_op, each op's key (chunk,
+//     block), its previous op of the block in the tile (LDS hash), and the tile's last op of each block
+//     pushed on its bucket's list.  An op that does not qualify marks the batch (kASlow); the host then
+//     runs the chain-based fast branch (or the general pipeline) from the original tables.
+//   uio_afused_kernel, persistent: each wave takes a contiguous range of ops in sequence order (workgroups
+//     in ticket order); per op: the old bytes are the previous op's payload, or the block for the block's
+//     first op (speculated "no earlier op", the bucket walk overlapped with the first rows); crc0(new) is
+//     the A6 check (ChunkReplica.cc:193-207), crc0(new ^ old) the delta of updateChecksum case (iv)
+//     (:356-390, the checksum moved by linearity); the block's first op writes the block's final bytes
+//     (the last op's payload, itself checked first).  Per group of 64 ops the deltas shifted to the
+//     chunk's end are folded into per-chunk XORs held in the lanes; workgroups chain their per-chunk
+//     aggregates by decoupled look-back; every op's result is written directly; the last workgroup to
+//     finish writes the final states, the counters, the commit and the outcome word.
+// Nothing is zeroed per batch: the bucket heads and granules carry the batch's epoch (kAEpoch, advanced by
+// the last workgroup), the ticket and done words are reset by the last workgroup.  An A6 failure (a
+// corrupted transfer), a block whose last op fails its check, or a look-back that gave up makes the pass
+// void: the bytes are right or deferred (kADefer list), and uio_afix_kernel recomputes every result from
+// the per-op records (dv, pv) and writes the deferred blocks.
+constexpr uint32_t kATile = 256;             // uio_aprep_kernel ops per workgroup
+constexpr uint32_t kAMaxOps = (1u << 24) - 2;  // bucket entries: epoch << 24 | (op index + 1)
+enum { kAEpoch = 0, kATicket = 1, kADone = 2, kASlow = 3, kADefer = 4, kACtlWords = 64 };
+constexpr uint32_t kADoneVoid = 1u << 12;    // kADone: finished workgroups (low 12 bits) + void reports << 12
+constexpr uint32_t kASpin = 1u << 22;        // bounded look-back spins (about a quarter second)
+
+struct AlignedArgs {
+  uint32_t *ctl;                  // kACtlWords control words (the thread's FastScratch)
+  uint32_t *head;                 // bucket heads, hmask + 1 of them (FastScratch; epoch-tagged, never cleared)
+  uint32_t hmask;
+  unsigned long long *gran;       // look-back granules, kFastCols per workgroup (FastScratch; epoch-tagged)
+  unsigned long long *key;        // per op: (chunk << 36) | block address >> 12
+  uint4 *link;                    // per op: {previous op of the block in the op's tile (kNil: none), the bucket
+                                  //  list's next entry (the tile's last op of a block), 0, 0}
+  unsigned long long *dv;         // per op: {state << 32 | crc0(new ^ old)}; state 1 applied, 2 failed A6
+  uint2 *pv;                      // per op: {crc0(new), the resolved previous op of the block (kNil: none)}
+  uint32_t *inp;                  // per op: its chunk's XOR of shifted deltas in the wave's range up to it
+  uint2 *defer;                   // blocks whose first op deferred the write-back: {first op, last op}
+};
+
+// An op the aligned sub-branch takes: a fast-branch op (fast_op) that writes one whole 4 KiB block at a
+// block-aligned address from a 16-byte-aligned payload.
+__device__ __forceinline__ bool aligned_op(const h3c_update_io &io, const h3c_chunk_state &cs, uint32_t st,
+                                           uint8_t poly_type) {
+  return io.length == kBlk && ((cs.base + io.offset) & (kBlk - 1)) == 0 && (io.payload & 15) == 0 &&
+         fast_op(io, cs, st, poly_type);
+}
+__device__ __forceinline__ bool aentry_valid(uint32_t e, uint32_t E) { return (e >> 24) == E && (e & 0xFFFFFFu) != 0; }
+// crc0 of an op's 4 KiB payload as its client checksum says it is (raw register, init ~0:
+// raw = crc0(data) ^ ~0 * x^(8 * 4096); the std domain's value is ~raw)
+__device__ __forceinline__ uint32_t aexpect(uint32_t value, uint32_t std_domain, uint32_t k4096) {
+  return (std_domain ? ~value : value) ^ k4096;
+}
+
+__global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *__restrict__ ios, uint32_t n,
+                                                           const h3c_chunk_state *__restrict__ chunks,
+                                                           uint32_t nchunks, uint8_t poly_type, uint32_t std_domain,
+                                                           uint32_t *__restrict__ misc, unsigned long long *__restrict__ ctr,
+                                                           AlignedArgs aa) {
+  __shared__ h3c_chunk_state s_cs[kFastChunksLds];
+  __shared__ unsigned long long g_key[2 * kATile];
+  __shared__ uint32_t g_head[2 * kATile], g_nx[kATile];
+  const uint32_t t = threadIdx.x, base = blockIdx.x * kATile, i = base + t;
+  h3c_update_io io{};
+  if (i < n) io = ios[i];
+  if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
+  const uint32_t E = aa.ctl[kAEpoch] & 0xFFu;  // (written by the previous batch's last workgroup)
+  if (blockIdx.x == 0 && t < kMiscWords) misc[t] = t == kMiscT0 || t == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;
+  if (blockIdx.x == 0 && t < kCtrN) ctr[t] = 0;
+  for (uint32_t e = t; e < 2 * kATile; e += kATile) {
+    g_key[e] = kNoKey;
+    g_head[e] = kNil;
+  }
+  __syncthreads();
+  unsigned long long key = kNoKey;
+  bool q = false;
+  if (i < n) {
+    const uint32_t c = io.chunk;
+    h3c_chunk_state cs{};
+    if (c < nchunks && c < kFastChunksLds) cs = s_cs[c];
+    const uint32_t st = op_status(io, cs, nchunks, poly_type, std_domain);
+    q = c < kFastChunksLds && aligned_op(io, cs, st, poly_type);
+    if (q) key = ((unsigned long long)c << 36) | ((cs.base + io.offset) >> 12);
+    aa.key[i] = key;
+  }
+  if (__syncthreads_or(i < n && !q) && t == 0) st_agent(&aa.ctl[kASlow], 0x100u | E);
+  uint32_t h = kNil;
+  if (key != kNoKey) {
+    h = key_hash(key) & (2 * kATile - 1);
+    for (;;) {
+      const unsigned long long old = atomicCAS(&g_key[h], kNoKey, key);
+      if (old == kNoKey || old == key) break;
+      h = (h + 1) & (2 * kATile - 1);
+    }
+    g_nx[t] = atomicExch(&g_head[h], t);
+  }
+  __syncthreads();
+  if (i >= n) return;
+  uint32_t pin = kNil;
+  bool last = true;
+  if (h != kNil)
+    for (uint32_t u = g_head[h]; u != kNil; u = g_nx[u]) {
+      if (u < t && (pin == kNil || u > pin)) pin = u;
+      if (u > t) last = false;
+    }
+  uint4 lk = make_uint4(pin == kNil ? kNil : base + pin, 0u, 0u, 0u);
+  if (h != kNil && last) lk.y = atomicExch(&aa.head[fast_bucket(key, aa.hmask)], (E << 24) | (i + 1));
+  aa.link[i] = lk;
+}
+
+__device__ __forceinline__ unsigned long long agran(uint32_t E, uint32_t state, uint32_t v) {
+  return ((unsigned long long)((E << 8) | state) << 32) | v;
+}
+// a granule's state in batch E (0: not published in this batch)
+__device__ __forceinline__ uint32_t agran_state(unsigned long long g, uint32_t E) {
+  const uint32_t hi = (uint32_t)(g >> 32);
+  return (hi >> 8) == E ? (hi & 3u) : 0u;
+}
+
+__global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
+    const h3c_update_io *__restrict__ ios, uint32_t n, const h3c_chunk_state *__restrict__ chunks,
+    h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks, uint8_t poly_type, uint32_t std_domain,
+    const PolyConsts *__restrict__ pc, AlignedArgs aa, uint32_t *misc, h3c_update_result *__restrict__ res,
+    unsigned long long *__restrict__ ctr, uint32_t *hout, h3c_chunk_state *commit, uint32_t force_void) {
+  __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
+  __shared__ h3c_chunk_state s_cs[kFastChunksLds];
+  __shared__ uint32_t s_ticket, s_E, s_slow, s_last, s_void, s_prev;
+  const uint32_t t = threadIdx.x, lane = t & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (t == 0) {
+    s_E = ld_agent(&aa.ctl[kAEpoch]) & 0xFFu;
+    s_slow = ld_agent(&aa.ctl[kASlow]);
+    s_ticket = atomicAdd(&aa.ctl[kATicket], 1u);
+    s_void = 0;
+    atomicMin(reinterpret_cast<unsigned long long *>(misc + kMiscT0), (unsigned long long)wall_clock64());
+  }
+  if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
+  __syncthreads();
+  const uint32_t E = s_E, L = s_ticket, nwg = gridDim.x;
+  const uint32_t poly = pc->poly;
+  // the end of the batch, by the last workgroup to finish (every other one has counted itself done):
+  // the control words reset for the next batch, the epoch advanced, the outcome words to the host
+  auto finish = [&](uint32_t outcome) {
+    if (t == 0) {
+      st_agent(&aa.ctl[kATicket], 0u);
+      st_agent(&aa.ctl[kADone], 0u);
+      st_agent(&aa.ctl[kAEpoch], (E + 1) & 0xFFu);
+      misc[kMiscFast] = outcome;
+      stores_done();
+      if (hout) fast_outcome_to_host(misc, hout, outcome);
+    }
+  };
+  if (s_slow == (0x100u | E)) {  // not an aligned batch: nothing was done
+    if (t == 0) s_last = (atomicAdd(&aa.ctl[kADone], 1u) & 0xFFFu) + 1 == nwg;
+    __syncthreads();
+    if (s_last) finish(kFastAbort);
+    return;
+  }
+  const uint32_t k4096 = dgf_mul(0xFFFFFFFFu, pc->pow8[12], poly);  // ~0 * x^(8 * 4096)
+  const uint64_t gw = (uint64_t)L * kBlkWaves + wave, nw = (uint64_t)nwg * kBlkWaves;
+  const uint32_t lo = (uint32_t)(gw * n / nw), hi = (uint32_t)((gw + 1) * n / nw);
+  const uint32_t lo16 = 16u * lane;  // (32 bits: a wave-uniform base plus this offset is one saddr load)
+  auto rl64 = [](uint64_t v, uint32_t u) -> uint64_t {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, u) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), u) << 32);
+  };
+  // per group of 64 ops, lane k's op: chunk, shift x^(8(size - offset - 4096)), new / old / destination /
+  // final bytes, the A6 expectations of the op and of the block's last op, the resolved previous op
+  // (m_first: the block's first op, whose old bytes are the block itself and which writes the block back)
+  uint32_t m_c = kNil, m_exp = 0, m_fexp = 0, m_first = 0;
+  uint64_t m_new = 0, m_old = 0, m_fin = 0;
+  uint4 vn[4], vo[4];
+  bool valid = false;
+  uint64_t pnew = 0, pold = 0;
+  auto start_group = [&](uint32_t g0) {
+    const uint32_t cnt = min(64u, hi - g0);
+    const uint32_t k = g0 + lane;
+    m_c = kNil;
+    m_exp = m_fexp = m_first = 0;
+    m_new = m_old = m_fin = 0;
+    uint32_t prev = kNil;
+    unsigned long long key = kNoKey;
+    if (lane < cnt) {
+      const h3c_update_io io = ios[k];
+      const uint4 lk = aa.link[k];
+      const h3c_chunk_state cs = s_cs[io.chunk];  // (aprep: every op's chunk is < nchunks <= 128)
+      const uint64_t slot = cs.base + io.offset;
+      m_c = io.chunk;
+      m_new = io.payload;
+      m_exp = aexpect(io.checksum_value, std_domain, k4096);
+      if (lk.x != kNil) {  // an earlier op of the block in this tile: its payload is the old bytes
+        prev = lk.x;
+        m_old = ios[lk.x].payload;
+      } else {  // speculation: no earlier op of the block (the walk below checks the earlier tiles)
+        m_old = slot;
+        m_first = 1;
+        m_fin = m_new;
+        m_fexp = m_exp;
+        key = aa.key[k];
+      }
+    }
+    valid = __builtin_amdgcn_readlane(m_c, 0) != kNil;
+    pnew = rl64(m_new, 0);
+    pold = rl64(m_old, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      vn[u] = valid ? load_row(pnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+      vo[u] = valid ? load_row(pold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+    }
+    // the walk over the block's listed tile-last ops (this batch's entries), while those rows load
+    if (key != kNoKey) {
+      uint32_t p = kNil, fmax = k;
+      for (uint32_t e = aa.head[fast_bucket(key, aa.hmask)]; aentry_valid(e, E); e = aa.link[(e & 0xFFFFFFu) - 1].y) {
+        const uint32_t j = (e & 0xFFFFFFu) - 1;
+        if (j >= n) break;  // (cannot happen: this batch's entries name its ops)
+        if (aa.key[j] != key) continue;
+        if (j < k && (p == kNil || j > p)) p = j;
+        fmax = max(fmax, j);
+      }
+      if (p != kNil) {  // an earlier tile wrote the block: its payload is the old bytes; it writes back
+        prev = p;
+        m_old = ios[p].payload;
+        m_first = 0;
+        m_fin = 0;
+      } else if (fmax != k) {  // the block's first op leaves the block's last op's bytes, checked first
+        const h3c_update_io fio = ios[fmax];
+        m_fin = fio.payload;
+        m_fexp = aexpect(fio.checksum_value, std_domain, k4096);
+      }
+    }
+    if (lane < cnt) aa.pv[k].y = prev;  // (uio_afix_kernel's input; crc0(new) follows in .x)
+    const uint64_t pold2 = rl64(m_old, 0);
+    if (valid && pold2 != pold) {  // op 0 was mis-speculated: its old rows again
+      pold = pold2;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) vo[u] = load_row(pold + (uint32_t)(u * kRowBytes + lo16));
+    }
+  };
+  if (lo < hi) start_group(lo);  // the first group's links and rows load while the tables fill
+  fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
+  __syncthreads();
+  const uint32_t *red = lds + kLdsWords;
+  const char *lb = reinterpret_cast<const char *>(lds);
+  const LaneLut Lt = make_lut(lane);
+  uint32_t acc0 = 0, acc1 = 0;  // running XOR of chunks lane, lane + 64 over the wave's range
+  uint32_t my_ip = 0, my_pass = 0;
+  uint32_t wave_void = 0;
+  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
+    const uint32_t cnt = min(64u, hi - g0);
+    const uint32_t k = g0 + lane;
+    uint32_t my_d = 0;
+    my_pass = 0;
+    for (uint32_t u0 = 0; u0 < cnt; ++u0) {
+      const bool nvalid = u0 + 1 < cnt && __builtin_amdgcn_readlane(m_c, u0 + 1) != kNil;
+      uint4 wn[4], wo[4];
+      uint64_t npnew = 0, npold = 0;
+      if (nvalid) {
+        npnew = rl64(m_new, u0 + 1);
+        npold = rl64(m_old, u0 + 1);
+      }
+      // the next op's new rows now, its old rows once this op's old rows are consumed (their registers
+      // free): a load round trip is a fraction of an op's time, and both pairs in flight at once spill
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wn[u] = nvalid ? load_row(npnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+      if (valid) {
+        Streams s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          consume(s2[0], vn[u], lb, Lt);
+          consume(s2[1], xor4(vn[u], vo[u]), lb, Lt);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) wo[u] = nvalid ? load_row(npold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+        uint32_t fv[2];
+        wave_fold_tab_n<2>(s2, lane, red, fv);
+        const uint32_t P = (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[0]);
+        const uint32_t D = (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[1]);
+        const bool pass = P == (uint32_t)__builtin_amdgcn_readlane((int)m_exp, u0);
+        if (lane == 0) aa.pv[g0 + u0].x = P;
+        if (__builtin_amdgcn_readlane((int)m_first, u0)) {  // the block's first op: the block's final bytes
+          const uint64_t dst = pold;                         // (the last op's, if its check passes)
+          const uint64_t fin = rl64(m_fin, u0);
+          if (fin == pnew) {
+            if (pass) {
+#pragma unroll
+              for (int u = 0; u < 4; ++u) store_masked(dst, u * kRowBytes + lo16, vn[u], 0u, kBlk);
+            }
+          } else {
+            // (into the old rows' registers: this op's delta is folded, and the next op's rows are in wn / wo)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) vo[u] = load_row(fin + (uint32_t)(u * kRowBytes + lo16));
+            Streams sf{0, 0, 0, 0};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) consume(sf, vo[u], lb, Lt);
+            const uint32_t Pf = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_fold_tab(sf, lane, red));
+            if (Pf == (uint32_t)__builtin_amdgcn_readlane((int)m_fexp, u0)) {
+#pragma unroll
+              for (int u = 0; u < 4; ++u) store_masked(dst, u * kRowBytes + lo16, vo[u], 0u, kBlk);
+            } else {  // the last op fails A6: uio_afix_kernel writes the last passing op's bytes (if any)
+              if (lane == 0) {
+                const uint32_t d = atomicAdd(&aa.ctl[kADefer], 1u);
+                aa.defer[d] = make_uint2(g0 + u0, 0u);
+              }
+              wave_void = 1;
+            }
+          }
+        }
+        if (lane == u0) {
+          my_d = D;
+          my_pass = pass;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) wo[u] = nvalid ? load_row(npold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+      }
+      valid = nvalid;
+      pnew = npnew;
+      pold = npold;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        vn[u] = wn[u];
+        vo[u] = wo[u];
+      }
+    }
+    // the group's per-op records (uio_afix_kernel's input), each op's shifted delta, every op's chunk XOR
+    // right after it (inclusive, with the earlier groups' running value), the running values moved on
+    const bool op = lane < cnt && m_c != kNil;
+    if (op) aa.dv[k] = ((unsigned long long)(my_pass ? 1u : 2u) << 32) | my_d;
+    if (__builtin_amdgcn_ballot_w64(op && !my_pass)) wave_void = 1;
+    uint32_t v = 0;
+    if (op && my_pass) {  // the delta moved to the chunk's end: x^(8(size - offset - 4096)), offset from the key
+      const h3c_chunk_state &cs = s_cs[m_c];
+      const int64_t off = (int64_t)((aa.key[k] & ((1ull << 36) - 1)) << 12) - (int64_t)cs.base;
+      v = dgf_mul(my_d, dxpow8_fast((int64_t)cs.size - off - (int64_t)kBlk, pc, poly), poly);
+    }
+    const uint32_t src = m_c & 63;
+    const uint32_t r0 = __shfl(acc0, src, 64), r1 = __shfl(acc1, src, 64);
+    my_ip = m_c < 64 ? r0 : r1;
+    for (uint32_t u0 = 0; u0 < cnt; ++u0) {
+      const uint32_t ct = __builtin_amdgcn_readlane(m_c, u0), vt = __builtin_amdgcn_readlane(v, u0);
+      if (lane >= u0 && m_c == ct) my_ip ^= vt;
+      if (ct == lane) acc0 ^= vt;
+      if (ct == lane + 64) acc1 ^= vt;
+    }
+    if (hi - lo > 64 && lane < cnt) aa.inp[k] = my_ip;
+    if (g0 + 64 < hi) start_group(g0 + 64);
+  }
+  // the chunks' base checksums (trusted stored values), one per lane (chunks lane, lane + 64)
+  auto t0_of = [&](uint32_t c) -> uint32_t {
+    return c < nchunks ? (std_domain ? ~s_cs[c].value : s_cs[c].value) : 0u;
+  };
+  const uint32_t rb0 = t0_of(lane), rb1 = t0_of(64 + lane);
+  if (wave_void && lane == 0) atomicOr(&s_void, 1u);
+  // ---- chunk aggregates: waves of the workgroup (LDS), then workgroups (look-back in ticket order) ----
+  __syncthreads();  // the CRC tables are done with: their LDS holds the aggregates now
+  uint32_t *wagg = lds;                                 // [16][128]
+  uint32_t *wexcl = lds + kBlkWaves * kFastCols;        // [128]: the workgroup's exclusive prefix
+  wagg[wave * kFastCols + lane] = acc0;
+  wagg[wave * kFastCols + 64 + lane] = acc1;
+  __syncthreads();
+  if (wave == 0) {
+    uint32_t a0 = 0, a1 = 0;
+    for (uint32_t w = 0; w < kBlkWaves; ++w) {
+      a0 ^= wagg[w * kFastCols + lane];
+      a1 ^= wagg[w * kFastCols + 64 + lane];
+    }
+    const bool two = nchunks > 64;
+    unsigned long long *row = aa.gran + (uint64_t)L * kFastCols;
+    uint32_t x0 = 0, x1 = 0;
+    if (L > 0) {
+      if (lane < nchunks) st_agent(&row[lane], agran(E, 1u, a0));
+      if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], agran(E, 1u, a1));
+      int j0 = lane < nchunks ? (int)L - 1 : -1, j1 = two && lane + 64 < nchunks ? (int)L - 1 : -1;
+      const uint32_t limit = force_void && L == 1 ? 0u : kASpin;  // (test hook: ticket 1 gives up at once)
+      for (uint32_t spins = 0; __builtin_amdgcn_ballot_w64(j0 >= 0 || j1 >= 0) != 0;) {
+        bool moved = false;
+        auto look = [&](int &j, uint32_t &x, uint32_t col) {
+          if (j < 0) return;
+          const int top = j;
+          unsigned long long g[4];
+#pragma unroll
+          for (int w = 0; w < 4; ++w) g[w] = top - w >= 0 ? ld_agent(&aa.gran[(uint64_t)(top - w) * kFastCols + col]) : 0ull;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t state = agran_state(g[w], E);
+            if (top - w >= 0 && j == top - w && state) {
+              x ^= (uint32_t)g[w];
+              j = state == 2u ? -1 : j - 1;
+              moved = true;
+            }
+          }
+        };
+        look(j0, x0, lane);
+        look(j1, x1, 64 + lane);
+        if (__builtin_amdgcn_ballot_w64(moved) == 0 || limit == 0) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > limit) {  // a predecessor never published: the pass is void (uio_afix_kernel)
+            if (lane == 0) s_void = 1;
+            break;
+          }
+        }
+      }
+    }
+    if (lane < nchunks) st_agent(&row[lane], agran(E, 2u, x0 ^ a0));
+    if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], agran(E, 2u, x1 ^ a1));
+    wexcl[lane] = x0;
+    wexcl[64 + lane] = x1;
+  }
+  __syncthreads();
+  // every op's result: its chunk's checksum right after it (ChunkReplica.cc:174, :311; a failed op reports
+  // the stored checksum unchanged, engine.rs:303 in the std domain)
+  uint32_t e0 = wexcl[lane], e1 = wexcl[64 + lane];
+  for (uint32_t w = 0; w < wave; ++w) {
+    e0 ^= wagg[w * kFastCols + lane];
+    e1 ^= wagg[w * kFastCols + 64 + lane];
+  }
+  const uint32_t be0 = rb0 ^ e0, be1 = rb1 ^ e1;
+  uint32_t n_ok = 0, n_bad = 0;
+  auto result = [&](uint32_t j, uint32_t c, uint32_t ip, bool pass) {
+    const uint32_t x0 = __shfl(be0, c & 63, 64), x1 = __shfl(be1, c & 63, 64);
+    if (j >= hi) return;
+    const uint32_t sv = (c < 64 ? x0 : x1) ^ ip;
+    h3c_update_result o{};
+    o.status = pass ? H3C_OK : H3C_ERR_CHECKSUM_MISMATCH;
+    o.size = s_cs[c].size;
+    o.type = poly_type;
+    o.value = pass ? (std_domain ? ~sv : sv) : (std_domain ? 0u : sv);
+    res[j] = o;
+    n_ok += pass;
+    n_bad += !pass;
+  };
+  if (hi - lo <= 64) {  // one group (the common case): its chunks and XORs are still in registers
+    result(lo + lane, m_c, my_ip, my_pass != 0);
+  } else {
+    for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
+      const uint32_t j = i0 + lane;
+      uint32_t c = 0, ip = 0;
+      bool pass = false;
+      if (j < hi) {
+        c = ios[j].chunk;
+        ip = aa.inp[j];
+        pass = (uint32_t)(aa.dv[j] >> 32) == 1u;
+      }
+      result(j, c, ip, pass);
+    }
+  }
+  // the counters: updateChecksum case (iv) (:389) / copy_on_write (chunk.rs:153) per applied op, the A6
+  // failures (uio_afix_kernel rewrites them on a void pass)
+  {
+    uint32_t v8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    v8[std_domain ? kCtrRecalc : kCtrRead] = n_ok;
+    v8[kCtrMismatch] = n_bad;
+    __shared__ unsigned int sh[8];
+    if (t < 8) sh[t] = 0;
+    __syncthreads();
+    for (int q = 0; q < 8; ++q)
+      if (v8[q]) atomicAdd(&sh[q], v8[q]);
+    __syncthreads();
+    if (t < 8 && sh[t]) atomicAdd(&ctr[t], (unsigned long long)sh[t]);
+  }
+  stores_done();
+  __syncthreads();
+  if (t == 0) {
+    atomicMax(reinterpret_cast<unsigned long long *>(misc + kMiscT1), (unsigned long long)wall_clock64());
+    const uint32_t w = atomicAdd(&aa.ctl[kADone], 1u + (s_void ? kADoneVoid : 0u));
+    s_last = (w & 0xFFFu) + 1 == nwg;
+    s_prev = (w >> 12) + (s_void ? 1u : 0u);  // void reports, this one included
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the last workgroup to finish: the totals are the last ticket's inclusive granules
+  const bool vd = s_prev != 0 || force_void;
+  if (t < nchunks && !vd) {
+    const unsigned long long g = ld_agent(&aa.gran[(uint64_t)(nwg - 1) * kFastCols + t]);
+    const uint32_t a = (uint32_t)g;
+    h3c_chunk_state f = s_cs[t];
+    const uint32_t t0 = std_domain ? ~f.value : f.value;
+    f.value = std_domain ? ~(t0 ^ a) : (t0 ^ a);
+    chunks_out[t] = f;
+    if (commit) commit[t] = f;
+  }
+  stores_done();
+  __syncthreads();
+  finish(vd ? kFastVoid : kFastDone);
+}
+
+// After a void aligned pass: the deferred blocks' bytes (the last op of the block that passes A6, if any),
+// then every op's result from the per-op records -- its delta against the last passing op before it on
+// its block, or the block's original bytes (crc0 = the first op's crc0(new ^ old) ^ crc0(new)) -- the final
+// states, the counters and the commit, by one workgroup walking the ops in tiles of 1,024.
+__global__ __launch_bounds__(1024) void uio_afix_kernel(const h3c_update_io *__restrict__ ios, uint32_t n,
+                                                        const h3c_chunk_state *__restrict__ chunks,
+                                                        h3c_chunk_state *__restrict__ chunks_out, uint32_t nchunks,
+                                                        uint8_t poly_type, uint32_t std_domain,
+                                                        const PolyConsts *__restrict__ pc, AlignedArgs aa,
+                                                        uint32_t *misc, h3c_update_result *__restrict__ res,
+                                                        unsigned long long *__restrict__ ctr,
+                                                        h3c_chunk_state *commit) {
+  __shared__ uint32_t wagg[16][kFastCols], run[kFastCols], t0s[kFastCols], szs[kFastCols];
+  __shared__ unsigned int cnt_ok, cnt_bad;
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, poly = pc->poly;
+  // 1. deferred blocks, one wave each: walk back from the block's last op to the last one that passed
+  const uint32_t nd = aa.ctl[kADefer];
+  const uint32_t E = (aa.ctl[kAEpoch] + 0xFFu) & 0xFFu;  // the pass's epoch (its last workgroup advanced it)
+  for (uint32_t d = wave; d < nd; d += 16) {
+    const uint2 e = aa.defer[d];
+    // the block's last op: the largest listed op of its key (every tile's last op of the block is listed)
+    const unsigned long long key = aa.key[e.x];
+    uint32_t j = e.x;
+    for (uint32_t x = aa.head[fast_bucket(key, aa.hmask)]; aentry_valid(x, E); x = aa.link[(x & 0xFFFFFFu) - 1].y) {
+      const uint32_t i = (x & 0xFFFFFFu) - 1;
+      if (i >= n) break;
+      if (aa.key[i] == key) j = max(j, i);
+    }
+    while (j != kNil && (uint32_t)(aa.dv[j] >> 32) != 1u) j = aa.pv[j].y;
+    if (j == kNil) continue;  // every op of the block failed: it keeps its bytes
+    const h3c_update_io f = ios[e.x];
+    const uint64_t dst = chunks[f.chunk].base + f.offset, src = ios[j].payload;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      *reinterpret_cast<uint4 *>(dst + u * kRowBytes + 16u * lane) =
+          *reinterpret_cast<const uint4 *>(src + u * kRowBytes + 16u * lane);
+  }
+  if (t < kFastCols) {
+    run[t] = 0;
+    t0s[t] = t < nchunks ? (std_domain ? ~chunks[t].value : chunks[t].value) : 0u;
+    szs[t] = t < nchunks ? chunks[t].size : 0u;
+  }
+  if (t == 0) cnt_ok = cnt_bad = 0;
+  __syncthreads();
+  // 2. every op's shifted delta, the per-chunk XORs in sequence order, the results
+  for (uint32_t b = 0; b < n; b += 1024) {
+    const uint32_t j = b + t;
+    uint32_t c = kNil, v = 0;
+    bool pass = false;
+    if (j < n) {
+      const h3c_update_io io = ios[j];
+      c = io.chunk;
+      pass = (uint32_t)(aa.dv[j] >> 32) == 1u;
+      if (pass) {
+        uint32_t p = aa.pv[j].y, f = j, lastpass = kNil;
+        while (p != kNil) {  // the last passing op before j on the block, else the block's first op
+          f = p;
+          if ((uint32_t)(aa.dv[p] >> 32) == 1u) {
+            lastpass = p;
+            break;
+          }
+          p = aa.pv[p].y;
+        }
+        const uint32_t old = lastpass != kNil ? aa.pv[lastpass].x : ((uint32_t)aa.dv[f] ^ aa.pv[f].x);
+        const uint32_t sh = dxpow8_fast((int64_t)szs[c] - (int64_t)io.offset - (int64_t)kBlk, pc, poly);
+        v = dgf_mul(aa.pv[j].x ^ old, sh, poly);
+        atomicAdd(&cnt_ok, 1u);
+      } else {
+        atomicAdd(&cnt_bad, 1u);
+      }
+    }
+    uint32_t acc0 = 0, acc1 = 0, ip = 0;
+    for (uint32_t u = 0; u < 64; ++u) {
+      const uint32_t cu = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)u);
+      const uint32_t vu = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)u);
+      if (lane >= u && c == cu) ip ^= vu;
+      if (cu == lane) acc0 ^= vu;
+      if (cu == lane + 64) acc1 ^= vu;
+    }
+    wagg[wave][lane] = acc0;
+    wagg[wave][64 + lane] = acc1;
+    __syncthreads();
+    if (j < n && c < kFastCols) {
+      uint32_t e = run[c];
+      for (uint32_t w = 0; w < wave; ++w) e ^= wagg[w][c];
+      const uint32_t sv = t0s[c] ^ e ^ ip;
+      h3c_update_result o{};
+      o.status = pass ? H3C_OK : H3C_ERR_CHECKSUM_MISMATCH;
+      o.size = szs[c];
+      o.type = poly_type;
+      o.value = pass ? (std_domain ? ~sv : sv) : (std_domain ? 0u : sv);
+      res[j] = o;
+    }
+    __syncthreads();
+    if (t < kFastCols) {
+      uint32_t x = 0;
+      for (uint32_t w = 0; w < 16; ++w) x ^= wagg[w][t];
+      run[t] ^= x;
+    }
+    __syncthreads();
+  }
+  if (t < nchunks) {
+    h3c_chunk_state f = chunks[t];
+    f.value = std_domain ? ~(t0s[t] ^ run[t]) : (t0s[t] ^ run[t]);
+    chunks_out[t] = f;
+    if (commit) commit[t] = f;
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int k = 0; k < kCtrN; ++k) ctr[k] = 0;
+    ctr[std_domain ? kCtrRecalc : kCtrRead] = cnt_ok;
+    ctr[kCtrMismatch] = cnt_bad;
+    aa.ctl[kADefer] = 0;
+    misc[kMiscFast] = kFastDone;
+  }
+}
+
 // A second stream per calling thread and device: the payload CRCs run on it while the main
 // stream sorts the ops (the sort does not depend on the A6 verdicts).
 struct AuxStream {
@@ -3271,9 +3892,12 @@ hipError_t sort_pairs(void *tmp, size_t &tmp_bytes, const uint32_t *k, uint32_t 
 // h3c_diag_counter: 0 graph replays, 1 captures, 2 capture failures, 3 front-void redos, 4 phase-B
 // reruns, 5 failed-A6 redos, 6 short fragment guesses, 7 fast-branch batches, 8 fast-branch attempts
 // abandoned (an op did not qualify), 9 fast-branch recoveries, 10 graphs refused by the topology check,
-// 11 graphs refused by the pointer audit (graph_pointers_in_key)
+// 11 graphs refused by the pointer audit (graph_pointers_in_key), 12 aligned sub-branch batches (counted in 7
+// too), 13 aligned attempts abandoned (an op not a full aligned block write), 14 aligned passes recomputed by
+// uio_afix_kernel (an A6 failure, a deferred block, a look-back that gave up)
 enum { kDiagReplay, kDiagCapture, kDiagCaptureFail, kDiagFrontVoid, kDiagPBVoid, kDiagA6Redo, kDiagShortF,
-       kDiagFast, kDiagFastAbort, kDiagFastVoid, kDiagTopology, kDiagPtrAudit, kDiagN };
+       kDiagFast, kDiagFastAbort, kDiagFastVoid, kDiagTopology, kDiagPtrAudit, kDiagAligned, kDiagAlignedAbort,
+       kDiagAlignedFix, kDiagN };
 std::atomic<uint64_t> g_graph_stats[kDiagN];
 struct UpdGraphKey {
   int dev;
@@ -3307,6 +3931,8 @@ struct FastScratch {
   uint32_t *p = nullptr;
   size_t words = 0;
   bool dirty = true;
+  uint32_t hcap = 0;      // the bucket count the heads were laid out for (another one: zeroed first)
+  uint32_t abatches = 0;  // aligned batches since the last zeroing (the 8-bit epoch must not wrap onto live entries)
 };
 struct ResPool {
   std::mutex mu;
@@ -3332,6 +3958,8 @@ struct ThreadRes {
     int dev = -1;
     uint32_t flags = 0, n = 0, nchunks = 0, general_runs = 0;
     uint32_t last_us = 0;  // the last fast batch's time from its first launch to the outcome word (host clock)
+    uint8_t aslow = 0;     // the aligned sub-branch: the shape's last attempt found an op it does not take
+    uint32_t a_runs = 0;   // ... and the batches of the shape run without trying it since
     const void *chunks = nullptr, *ios = nullptr;
     uint8_t poly = 0, slow = 0;
     uint64_t used = 0;
@@ -3629,6 +4257,14 @@ struct ArgLayout<FastArgs, void> {
   }
 };
 template <>
+struct ArgLayout<AlignedArgs, void> {
+  static void fill(ArgSpec &a) {
+    struct_arg<AlignedArgs>(a, {offsetof(AlignedArgs, ctl), offsetof(AlignedArgs, head), offsetof(AlignedArgs, gran),
+                                offsetof(AlignedArgs, key), offsetof(AlignedArgs, link), offsetof(AlignedArgs, dv),
+                                offsetof(AlignedArgs, pv), offsetof(AlignedArgs, inp), offsetof(AlignedArgs, defer)});
+  }
+};
+template <>
 struct ArgLayout<TMapFn, void> {
   static void fill(ArgSpec &a) {
     struct_arg<TMapFn>(a, {offsetof(TMapFn, pos), offsetof(TMapFn, eacc), offsetof(TMapFn, payraw),
@@ -3659,7 +4295,8 @@ const std::vector<h3c_rt::KernelSig> &capturable_kernels() {
       H3C_SIG(uio_block_kernel), H3C_SIG(uio_phaseb_kernel), H3C_SIG(uio_elem_kernel<TMapFn>),
       H3C_SIG(uio_elem_kernel<SMapFn>), H3C_SIG(uio_result_kernel), H3C_SIG(uio_stale_kernel),
       H3C_SIG(uio_commit_kernel), H3C_SIG(uio_fast_link_kernel), H3C_SIG(uio_fast_kernel),
-      H3C_SIG(uio_fast_sum_kernel), H3C_SIG(uio_fast_res_kernel), h3c_rt::uio_piece_kernel_sig(),
+      H3C_SIG(uio_fast_sum_kernel), H3C_SIG(uio_fast_res_kernel), H3C_SIG(uio_aprep_kernel),
+      H3C_SIG(uio_afused_kernel), h3c_rt::uio_piece_kernel_sig(),
 #undef H3C_SIG
   };
   return sigs;
@@ -3924,6 +4561,13 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   ThreadRes::FastPred *fpred = fast_able ? &fast_pred(dev, poly_type, flags & ~H3C_UPD_GRAPHS, n, nchunks, d_chunks, d_ios)
                                          : nullptr;
   const bool try_fast = fast_able && (fast_hook == 2 || !fpred->slow || fpred->general_runs >= kFastRetry);
+  // the aligned sub-branch (uio_aprep_kernel + uio_afused_kernel): tried before the chain-based branch when
+  // every op may be a full aligned 4 KiB WRITE (trusted stored checksums), unless this thread's last batch of
+  // the shape had an op it does not take (test hook H3C_HOOK_UPD_ALIGNED: 1 never, 2 always tried)
+  const uint64_t aligned_hook = h3c_rt::hook(H3C_HOOK_UPD_ALIGNED);
+  const bool try_aligned = fast_able && !exact && n <= kAMaxOps && aligned_hook != 1 &&
+                           (aligned_hook == 2 || !fpred->aslow || fpred->a_runs >= kFastRetry);
+  AlignedArgs aa{};
   const uint32_t nwg_fast = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev)) * H3C_FAST_WG_MULT;
   const uint32_t ntiles_tail = (uint32_t)std::max<size_t>(1, ((size_t)n + 1023) / 1024);  // the tail kernels
   uint32_t hcap_fast = 256;
@@ -3973,6 +4617,9 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       d_gran = carve<unsigned long long>(cur, (size_t)ntiles_tail * kFastCols);
       d_part = carve<uint2>(cur, n);
       d_heavy = carve<uint32_t>(cur, 64 * (((size_t)n + 63) / 64) + ((size_t)n + 63) / 64);
+      aa.pv = carve<uint2>(cur, n);
+      aa.inp = carve<uint32_t>(cur, n);
+      aa.defer = carve<uint2>(cur, n);
     }
     return (size_t)(cur - base);
   };
@@ -4124,20 +4771,162 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   // ---- the fast branch: zero, prep (with the fast tables), [piece pass: exact mode's chunk CRCs],
   // uio_fast_kernel -- four launches at most, one graph on request.  An op that does not qualify makes
   // uio_fast_kernel return at once (nothing written); the general pipeline below then runs the batch.
-  if (try_fast) {
-    const uint32_t ptiles_f = (uint32_t)(((size_t)n + C + 1 + kPrepTile - 1) / kPrepTile);
-    // the slow word and the bucket heads: this thread's scratch, zero between batches (the tail clears
-    // what the batch set); a new or suspect scratch is zeroed here, before the batch and outside any capture
-    FastScratch *fsc = fast_scratch(dev, kScratchHeads + (size_t)hcap_fast);
+  // the thread's fast scratch (the slow word, the control words, granules and bucket heads): zero between
+  // batches where the branches need it so; a new, suspect or re-laid-out scratch, or one whose aligned epochs
+  // are about to wrap, is zeroed here, before the batch and outside any capture
+  FastScratch *fsc = nullptr;
+  if (try_aligned || try_fast) {
+    fsc = fast_scratch(dev, kScratchHeads + 2 * (size_t)hcap_fast);
     if (!fsc) return H3C_ERR_HIP;
+    if (fsc->hcap != hcap_fast || fsc->abatches >= kAEpochBatches) fsc->dirty = true;
     fa.slow = fsc->p;
     fa.head = fsc->p + kScratchHeads;
+    aa.ctl = fsc->p + kScratchACtl;
+    aa.gran = reinterpret_cast<unsigned long long *>(fsc->p + kScratchAGran);
+    aa.head = fsc->p + kScratchHeads + hcap_fast;
+    aa.hmask = hcap_fast - 1;
+    aa.key = fa.key;
+    aa.link = fa.link;
+    aa.dv = fa.dv;
     if (fsc->dirty) {
-      const uint32_t zw = kScratchHeads + hcap_fast, zg = std::min(1024u, (zw + 1023) / 1024);
+      const uint32_t zw = kScratchHeads + 2 * hcap_fast, zg = std::min(1024u, (zw + 1023) / 1024);
       hipLaunchKernelGGL(uio_zero_kernel, dim3(zg), dim3(256), 0, st, fsc->p, zw, nullptr, 0u, nullptr, 0u, nullptr, 0u);
       HIP_TRY(hipGetLastError());
       fsc->dirty = false;
+      fsc->hcap = hcap_fast;
+      fsc->abatches = 0;
     }
+  }
+  uint32_t *h_fs = &h_F[kMiscFast - kMiscOutF];  // the outcome word, set last by the branches' last kernel
+
+  // ---- the aligned sub-branch: uio_aprep_kernel + uio_afused_kernel, one graph on request ----
+  if (try_aligned) {
+    ScratchGuard sguard{fsc};  // (any return before the batch's outcome is read marks it suspect)
+    const uint32_t num_cu = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev));
+    // the fewest workgroups that keep the most ops per wave (as upd_fused_kernel's grid)
+    uint32_t nwg_a = std::min<uint32_t>(std::min(num_cu, kAGranRows), std::max<uint32_t>(1, (n + kBlkWaves - 1) / kBlkWaves));
+    {
+      const uint64_t per = ((uint64_t)n + (uint64_t)nwg_a * kBlkWaves - 1) / ((uint64_t)nwg_a * kBlkWaves);
+      nwg_a = (uint32_t)std::max<uint64_t>(1, ((uint64_t)n + per * kBlkWaves - 1) / (per * kBlkWaves));
+    }
+    const uint32_t force_void = (giveup & 8) ? 1u : 0u;  // (test hook H3C_HOOK_UPD_GIVEUP bit 3)
+    auto a_launch = [&](hipStream_t q) -> int {
+      hipLaunchKernelGGL(uio_aprep_kernel, dim3((n + kATile - 1) / kATile), dim3(kATile), 0, q, d_ios, n, d_chunks,
+                         nchunks, poly_type, stdf, d_misc, d_ctr, aa);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(uio_afused_kernel, dim3(nwg_a), dim3(kBlkThreads), 0, q, d_ios, n, d_chunks, d_chunks_out,
+                         nchunks, poly_type, stdf, pc, aa, d_misc, d_res, d_ctr, d_hF, commit_dev, force_void);
+      HIP_TRY(hipGetLastError());
+      return H3C_OK;
+    };
+    const UpdGraphKey akey{dev, poly_type, flags | 0x40000000u, n, nchunks, 0u, hcap_fast, d_chunks, d_chunks_out,
+                           d_ios, d_res, d_ctr, lease1.data(), fsc->p, d_hF, nullptr};
+    UpdGraphs *gr = upd_graphs(akey, st, (flags & H3C_UPD_GRAPHS) != 0);
+    if (gr && !gr->g && !gr->failed) {
+      hipStream_t cst = capture_stream(dev);
+      rc = cst ? capture_graph(cst, [&] {
+        int r = a_launch(cst);
+        if (!r && epi_graph && !commit_dev) r = epilogue(cst, d_misc + kMiscOutF, cap);
+        return r;
+      }, gr->g, allow_of(nullptr, 0, fsc->p, 4 * fsc->words)) : H3C_ERR_HIP;
+      g_graph_stats[rc ? kDiagCaptureFail : kDiagCapture].fetch_add(1);
+      if (rc) {
+        gr->failed = true;
+        (void)hipGetLastError();
+      }
+      rc = H3C_OK;
+    }
+    const bool use_graph = gr && gr->g && !gr->failed;
+    __atomic_store_n(h_fs, 0u, __ATOMIC_RELAXED);
+    const auto t_launch = std::chrono::steady_clock::now();
+    if (use_graph) {
+      HIP_TRY(hipGraphLaunch(gr->g, st));
+      g_graph_stats[kDiagReplay].fetch_add(1);
+    } else {
+      rc = a_launch(st);
+      if (rc) return rc;
+    }
+    if (!(use_graph && epi_graph) && !commit_dev) {
+      rc = epilogue(st, d_misc + kMiscOutF, cap);
+      if (rc) return rc;
+    }
+    const uint32_t poll_us = fast_poll_budget_us(fpred->last_us);
+    const bool seen = poll_host_word(h_fs, poll_us);
+    if (seen)
+      fpred->last_us = (uint32_t)std::max<int64_t>(
+          1, std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t_launch).count());
+    else
+      fpred->last_us = 0;
+    auto prof_aligned = [&]() {  // the fused kernel's own wall-clock span (first workgroup start, last end)
+      if (!h3c_rt::prof_enabled()) return;
+      uint64_t t0, t1;
+      std::memcpy(&t0, h_F + (kMiscT0 - kMiscOutF), 8);
+      std::memcpy(&t1, h_F + (kMiscT1 - kMiscOutF), 8);
+      const int khz = h3c_rt::device_wall_clock_khz(dev);
+      if (t1 > t0 && khz > 0) h3c_rt::prof_add(H3C_PROF_UPDIO, (float)((double)(t1 - t0) / khz), 3ull * kBlk * n);
+    };
+    if (seen && commit_dev && *h_fs == kFastDone && !h_F[kMiscErr - kMiscOutF]) {
+      // done on the device-table entry: the last workgroup committed the states and wrote every output before
+      // the outcome word (see the fast branch below for why the call need not wait for the stream)
+      prof_aligned();
+      g_graph_stats[kDiagFast].fetch_add(1);
+      g_graph_stats[kDiagAligned].fetch_add(1);
+      fpred->aslow = 0;
+      ++fsc->abatches;
+      sguard.f = nullptr;
+      drain.armed = drain_aux.armed = false;
+      return H3C_OK;
+    }
+    const hipError_t se = stream_wait(st, seen ? std::min(poll_us, 200u) : 0u);
+    if (se != hipSuccess) {
+      drain.armed = drain_aux.armed = false;
+      h3c_rt::set_error("h3c_update_ios (aligned branch)", se);
+      return H3C_ERR_HIP;
+    }
+    const uint32_t fs = h_F[kMiscFast - kMiscOutF];
+    if (fs != kFastDone && fs != kFastVoid && fs != kFastAbort) {
+      drain.armed = drain_aux.armed = false;
+      h3c_rt::set_error_text("h3c_update_ios: the aligned branch ended without an outcome");
+      return H3C_ERR_HIP;
+    }
+    sguard.f = nullptr;  // (the last workgroup reset the control words and advanced the epoch)
+    ++fsc->abatches;
+    if (fs == kFastDone || fs == kFastVoid) {
+      prof_aligned();
+      g_graph_stats[kDiagFast].fetch_add(1);
+      g_graph_stats[kDiagAligned].fetch_add(1);
+      fpred->aslow = 0;
+      if (fs == kFastVoid) {  // an A6 failure, a deferred block or a look-back that gave up: results from the records
+        g_graph_stats[kDiagAlignedFix].fetch_add(1);
+        hipLaunchKernelGGL(uio_afix_kernel, dim3(1), dim3(1024), 0, st, d_ios, n, d_chunks, d_chunks_out, nchunks,
+                           poly_type, stdf, pc, aa, d_misc, d_res, d_ctr, commit_dev);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(h_F, d_misc + kMiscOutF, 4 * (kMiscN - kMiscOutF), hipMemcpyDeviceToHost, st));
+        if (!commit_dev) {
+          rc = epilogue(st, d_misc + kMiscOutF, cap);
+          if (rc) return rc;
+        }
+        const hipError_t se2 = hipStreamSynchronize(st);
+        if (se2 != hipSuccess) {
+          drain.armed = drain_aux.armed = false;
+          h3c_rt::set_error("h3c_update_ios (aligned-branch recovery)", se2);
+          return H3C_ERR_HIP;
+        }
+      }
+      drain.armed = drain_aux.armed = false;
+      return H3C_OK;
+    }
+    // kFastAbort: some op is not a full aligned block write -- the chain-based fast branch (or the general
+    // pipeline) runs the batch from the original tables
+    g_graph_stats[kDiagAlignedAbort].fetch_add(1);
+    fpred->aslow = 1;
+    fpred->a_runs = 0;
+  } else if (fpred) {
+    ++fpred->a_runs;
+  }
+
+  if (try_fast) {
+    const uint32_t ptiles_f = (uint32_t)(((size_t)n + C + 1 + kPrepTile - 1) / kPrepTile);
     ScratchGuard sguard{fsc};  // (any return before the batch's outcome is read marks it suspect)
     unsigned long long *d_ts = reinterpret_cast<unsigned long long *>(d_misc + kMiscT0);
     auto fast_kernel = [&](hipStream_t q, bool timed) -> int {
@@ -4194,7 +4983,6 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       rc = H3C_OK;
     }
     const bool use_graph = gr && gr->g && !gr->failed;
-    uint32_t *h_fs = &h_F[kMiscFast - kMiscOutF];  // set last by the tail (fast_outcome_to_host)
     __atomic_store_n(h_fs, 0u, __ATOMIC_RELAXED);
     const auto t_launch = std::chrono::steady_clock::now();
     if (use_graph) {

@@ -356,13 +356,14 @@ def sync_bench(threads: int, nbytes: int, calls: int, api: str = "verify"):
 
 
 HOOK_SEG_BYTES, HOOK_DEBUG_FLAGS, HOOK_UPD_SCAN, HOOK_UPD_GRAPHS, HOOK_UPD_LOOKBACK, HOOK_UPD_FRONT = 1, 2, 3, 4, 5, 6
-HOOK_UPD_FAST, HOOK_UPD_GIVEUP, HOOK_FAST_POLL_US = 7, 8, 9
+HOOK_UPD_FAST, HOOK_UPD_GIVEUP, HOOK_FAST_POLL_US, HOOK_UPD_ALIGNED = 7, 8, 9, 10
 UPD_SCAN_PATHS = {"default": 0, "fused": 1, "tiles": 2, "sort": 3}
 
 # h3c_diag_counter indices (include/h3c_crc.h): process-wide, monotonic
 DIAG_NAMES = ("graph_replays", "graph_captures", "graph_capture_failures", "redo_front_void", "rerun_phase_b_void",
               "redo_failed_a6", "redo_short_fragment_guess", "fast_batches", "fast_abandoned", "fast_recovered",
-              "graph_topology_refused", "graph_pointer_refused")
+              "graph_topology_refused", "graph_pointer_refused", "aligned_batches", "aligned_abandoned",
+              "aligned_recovered")
 
 
 def diag_counter(which: int) -> int:

@@ -455,10 +455,16 @@ enum h3c_hook {
   H3C_HOOK_UPD_GIVEUP = 8,   /* h3c_update_ios, bit mask: a starved wait forced (spin limit 0) in the tile or
                                workgroup with ticket 1 of -- 1: uio_front_kernel (the pass is void and redone on
                                the scan-based stage), 2: uio_phaseb_kernel (phase B rerun the scan-based way),
-                               4: uio_fast_kernel's look-back (results recomputed by the recovery kernel) */
-  H3C_HOOK_FAST_POLL_US = 9  /* h3c_update_ios fast branch: the most microseconds the calling thread spins on the
+                               4: uio_fast_kernel's look-back (results recomputed by the recovery kernel),
+                               8: the aligned sub-branch's look-back in its workgroup with ticket 1 (the pass is void:
+                               uio_afix_kernel recomputes the results) */
+  H3C_HOOK_FAST_POLL_US = 9, /* h3c_update_ios fast branch: the most microseconds the calling thread spins on the
                                batch's outcome word before a blocking wait (0: adaptive, twice the last batch of
                                the same shape + 50 us, within [100, 2000]) */
+  H3C_HOOK_UPD_ALIGNED = 10  /* h3c_update_ios: 1 never tries the aligned sub-branch of the fast branch (full
+                               block-aligned 4 KiB WRITEs in two launches); 2 tries it first on every batch that
+                               may take the fast branch (default 0: unless this thread's last batch of the same
+                               shape and tables had an op it does not take) */
 };
 int h3c_test_hook(int key, uint64_t value);
 /* Engine-internal counters (process-wide, monotonic) for tests and benches:
@@ -474,7 +480,12 @@ int h3c_test_hook(int key, uint64_t value);
  *      ordered after the graph's root) and run as plain launches instead,
  *   11 captured graphs refused by the pointer audit (a kernel argument pointing outside every buffer
  *      the graph cache's key names, or a kernel with no registered argument layout) and run as plain
- *      launches instead. */
+ *      launches instead,
+ *   12 batches run by the fast branch's aligned sub-branch (uio_afused_kernel; also counted in 7),
+ *   13 aligned attempts abandoned because an op was not a full block-aligned 4 KiB typed WRITE (the
+ *      chain-based fast branch or the general pipeline ran),
+ *   14 aligned passes whose results were recomputed by uio_afix_kernel (an A6 failure, a block whose last
+ *      write failed its check, or a look-back that gave up). */
 uint64_t h3c_diag_counter(int which);
 /* The shape of the last graph this thread captured for h3c_update_ios (tests): out7 = {nodes, root
  * nodes, memset + memcpy nodes, kernel nodes, nodes reachable from the first root, edges, the largest

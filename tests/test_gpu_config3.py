@@ -2,8 +2,10 @@
 
 100k random 4 KiB WRITE UpdateIOs into 64 x 64 MiB chunks (h3c_update_ios_dev, tables in HBM),
 trusted and exact, each run once through the general pipeline (h3c_test_hook(H3C_HOOK_UPD_FAST, 1):
-prep, sort, piece pass, front, block and phase-B kernels) and once through the fast branch (hook 2:
-prep, link, uio_fast_kernel and its tail); the engine's diag counters must say which one ran.  The
+prep, sort, piece pass, front, block and phase-B kernels), once through the chain-based fast branch
+(FAST 2, H3C_HOOK_UPD_ALIGNED 1: prep, link, uio_fast_kernel and its tail) and, trusted, once through
+the aligned sub-branch (ALIGNED 2: uio_aprep_kernel + uio_afused_kernel); the engine's diag counters
+must say which one ran.  The
 reference semantics replaced are ChunkReplica::update + updateChecksum
 (src/storage/store/ChunkReplica.cc:131-394).  What is checked against the CPU oracle
 (oracle/crc_oracle.c), not against another GPU pass (the oracle side is computed once per mode and
@@ -89,12 +91,15 @@ def _inputs(exact):
     return wc, wb, pay, stale, _ORACLE[exact]
 
 
-@pytest.mark.parametrize("branch", ["general", "fast"])
+@pytest.mark.parametrize("branch", ["general", "fast", "aligned"])
 @pytest.mark.parametrize("exact", [False, True])
 def test_updio_config3_full_shape_against_oracle(h3c, torch_dev, hooks, exact, branch):
+    if exact and branch == "aligned":
+        pytest.skip("the aligned sub-branch trusts stored checksums (exact mode takes the chain-based branch)")
     torch, dev = torch_dev
     wc, wb, pay, stale, o = _inputs(exact)
-    hooks(h3c.HOOK_UPD_FAST, 2 if branch == "fast" else 1)
+    hooks(h3c.HOOK_UPD_FAST, 1 if branch == "general" else 2)
+    hooks(h3c.HOOK_UPD_ALIGNED, 2 if branch == "aligned" else 1)
     dchunks = torch.empty(NCH * CL, dtype=torch.uint8, device=dev)
     h3c.fill_splitmix(dchunks, CL, NCH, CL, SEED)
     dpay = torch.from_numpy(pay).to(dev)
@@ -122,8 +127,10 @@ def test_updio_config3_full_shape_against_oracle(h3c, torch_dev, hooks, exact, b
     torch.cuda.synchronize()
     diag = {k: v - before[k] for k, v in h3c.diag_counters().items()}
     # the branch that ran is the branch named, with no redo of any kind
-    assert diag["fast_batches"] == (1 if branch == "fast" else 0), diag
+    assert diag["fast_batches"] == (0 if branch == "general" else 1), diag
+    assert diag["aligned_batches"] == (1 if branch == "aligned" else 0), diag
     assert diag["fast_abandoned"] == 0 and diag["fast_recovered"] == 0, diag
+    assert diag["aligned_abandoned"] == 0 and diag["aligned_recovered"] == 0, diag
     assert all(diag[k] == 0 for k in ("redo_front_void", "rerun_phase_b_void", "redo_failed_a6",
                                       "redo_short_fragment_guess")), diag
     fin = d_state.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)

@@ -101,8 +101,11 @@ class Scenario:
         chunk alignments differ."""
         h3c = self.h3c
         offs, total = [], 0
+        align = getattr(self, "pay_align", 0)  # (a scenario may ask for aligned payloads: the aligned sub-branch)
         for p in self.payloads:
             total += int(self.rng.integers(0, 17))
+            if align:
+                total = -(-total // align) * align
             offs.append(total)
             total += 0 if p is None else len(p)
         pay = np.zeros(max(total, 1), dtype=np.uint8)
