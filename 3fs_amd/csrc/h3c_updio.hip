@@ -3138,6 +3138,25 @@ __global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uin
 // corrupted transfer), a block whose last op fails its check, or a look-back that gave up makes the pass
 // void: the bytes are right or deferred (kADefer list), and uio_afix_kernel recomputes every result from
 // the per-op records (dv, pv) and writes the deferred blocks.
+#ifndef H3C_AF_STORE_EARLY
+#define H3C_AF_STORE_EARLY 1  // 1: a block's only write is stored before its A6 fold (put back from the old rows
+#endif                        //    if the check fails), so the stores overlap the fold
+#ifndef H3C_AF_EXPERIMENT
+#define H3C_AF_EXPERIMENT 0  // timing-only builds: bit0 skips the A6 CRC (every check passes)
+#endif
+#ifndef H3C_AF_TRACE
+#define H3C_AF_TRACE 0  // 1: per-workgroup wall-clock stamps of the last launch (h3c_diag_af_trace, diagnostics)
+#endif
+#if H3C_AF_TRACE
+// per ticket: start, tables filled, last wave's ops done, look-back done, end; each wave's ops done;
+// the workgroup's blockIdx and hardware XCC id
+__device__ unsigned long long g_af_wg[1024 * 5];
+__device__ unsigned long long g_af_wave[1024 * 16];
+__device__ uint32_t g_af_blk[1024 * 2];
+#endif
+#ifndef H3C_AF_EARLY_OLD
+#define H3C_AF_EARLY_OLD 0  // 1: the next op's old rows load with its new rows, before this op's CRCs (A/B)
+#endif
 constexpr uint32_t kATile = 256;             // uio_aprep_kernel ops per workgroup
 constexpr uint32_t kAMaxOps = (1u << 24) - 2;  // bucket entries: epoch << 24 | (op index + 1)
 enum { kAEpoch = 0, kATicket = 1, kADone = 2, kASlow = 3, kADefer = 4, kACtlWords = 64 };
@@ -3252,11 +3271,22 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     s_slow = ld_agent(&aa.ctl[kASlow]);
     s_ticket = atomicAdd(&aa.ctl[kATicket], 1u);
     s_void = 0;
-    atomicMin(reinterpret_cast<unsigned long long *>(misc + kMiscT0), (unsigned long long)wall_clock64());
   }
   if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
   __syncthreads();
   const uint32_t E = s_E, L = s_ticket, nwg = gridDim.x;
+  // the kernel's own span (bench / profiling): the first ticket's start (one store, not one atomic per
+  // workgroup on one address) and the last workgroup's end
+  if (t == 0 && L == 0) *reinterpret_cast<unsigned long long *>(misc + kMiscT0) = wall_clock64();
+#if H3C_AF_TRACE
+  if (t == 0 && L < 1024) {
+    g_af_wg[5 * L] = wall_clock64();
+    g_af_blk[2 * L] = blockIdx.x;
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_af_blk[2 * L + 1] = xcc;
+  }
+#endif
   const uint32_t poly = pc->poly;
   // the end of the batch, by the last workgroup to finish (every other one has counted itself done):
   // the control words reset for the next batch, the epoch advanced, the outcome words to the host
@@ -3359,6 +3389,9 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   if (lo < hi) start_group(lo);  // the first group's links and rows load while the tables fill
   fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
   __syncthreads();
+#if H3C_AF_TRACE
+  if (t == 0 && L < 1024) g_af_wg[5 * L + 1] = wall_clock64();
+#endif
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
   const LaneLut Lt = make_lut(lane);
@@ -3382,28 +3415,41 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
       // free): a load round trip is a fraction of an op's time, and both pairs in flight at once spill
 #pragma unroll
       for (int u = 0; u < 4; ++u) wn[u] = nvalid ? load_row(npnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+#if H3C_AF_EARLY_OLD
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wo[u] = nvalid ? load_row(npold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+#endif
       if (valid) {
+        const bool first = __builtin_amdgcn_readlane((int)m_first, u0) != 0;
+        const bool solo = first && rl64(m_fin, u0) == pnew;  // the block's only write
+        if (H3C_AF_STORE_EARLY && solo) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) store_masked(pold, u * kRowBytes + lo16, vn[u], 0u, kBlk);
+        }
         Streams s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          consume(s2[0], vn[u], lb, Lt);
+          if (!(H3C_AF_EXPERIMENT & 1)) consume(s2[0], vn[u], lb, Lt);
           consume(s2[1], xor4(vn[u], vo[u]), lb, Lt);
         }
+#if !H3C_AF_EARLY_OLD
 #pragma unroll
         for (int u = 0; u < 4; ++u) wo[u] = nvalid ? load_row(npold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+#endif
         uint32_t fv[2];
         wave_fold_tab_n<2>(s2, lane, red, fv);
-        const uint32_t P = (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[0]);
+        const uint32_t P = (H3C_AF_EXPERIMENT & 1) ? (uint32_t)__builtin_amdgcn_readlane((int)m_exp, u0)
+                                                   : (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[0]);
         const uint32_t D = (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[1]);
         const bool pass = P == (uint32_t)__builtin_amdgcn_readlane((int)m_exp, u0);
         if (lane == 0) aa.pv[g0 + u0].x = P;
-        if (__builtin_amdgcn_readlane((int)m_first, u0)) {  // the block's first op: the block's final bytes
-          const uint64_t dst = pold;                         // (the last op's, if its check passes)
+        if (first) {  // the block's first op: the block's final bytes (the last op's, if its check passes)
+          const uint64_t dst = pold;
           const uint64_t fin = rl64(m_fin, u0);
-          if (fin == pnew) {
-            if (pass) {
+          if (solo) {
+            if (H3C_AF_STORE_EARLY ? !pass : pass) {  // (early store: a failed check puts the old rows back)
 #pragma unroll
-              for (int u = 0; u < 4; ++u) store_masked(dst, u * kRowBytes + lo16, vn[u], 0u, kBlk);
+              for (int u = 0; u < 4; ++u) store_masked(dst, u * kRowBytes + lo16, H3C_AF_STORE_EARLY ? vo[u] : vn[u], 0u, kBlk);
             }
           } else {
             // (into the old rows' registers: this op's delta is folded, and the next op's rows are in wn / wo)
@@ -3429,7 +3475,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
           my_d = D;
           my_pass = pass;
         }
-      } else {
+      } else if (!H3C_AF_EARLY_OLD) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) wo[u] = nvalid ? load_row(npold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
       }
@@ -3465,6 +3511,9 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     if (hi - lo > 64 && lane < cnt) aa.inp[k] = my_ip;
     if (g0 + 64 < hi) start_group(g0 + 64);
   }
+#if H3C_AF_TRACE
+  if (lane == 0 && L < 1024) g_af_wave[16 * L + wave] = wall_clock64();
+#endif
   // the chunks' base checksums (trusted stored values), one per lane (chunks lane, lane + 64)
   auto t0_of = [&](uint32_t c) -> uint32_t {
     return c < nchunks ? (std_domain ? ~s_cs[c].value : s_cs[c].value) : 0u;
@@ -3473,6 +3522,9 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   if (wave_void && lane == 0) atomicOr(&s_void, 1u);
   // ---- chunk aggregates: waves of the workgroup (LDS), then workgroups (look-back in ticket order) ----
   __syncthreads();  // the CRC tables are done with: their LDS holds the aggregates now
+#if H3C_AF_TRACE
+  if (t == 0 && L < 1024) g_af_wg[5 * L + 2] = wall_clock64();
+#endif
   uint32_t *wagg = lds;                                 // [16][128]
   uint32_t *wexcl = lds + kBlkWaves * kFastCols;        // [128]: the workgroup's exclusive prefix
   wagg[wave * kFastCols + lane] = acc0;
@@ -3525,6 +3577,9 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], agran(E, 2u, x1 ^ a1));
     wexcl[lane] = x0;
     wexcl[64 + lane] = x1;
+#if H3C_AF_TRACE
+    if (lane == 0 && L < 1024) g_af_wg[5 * L + 3] = wall_clock64();
+#endif
   }
   __syncthreads();
   // every op's result: its chunk's checksum right after it (ChunkReplica.cc:174, :311; a failed op reports
@@ -3535,7 +3590,6 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     e1 ^= wagg[w * kFastCols + 64 + lane];
   }
   const uint32_t be0 = rb0 ^ e0, be1 = rb1 ^ e1;
-  uint32_t n_ok = 0, n_bad = 0;
   auto result = [&](uint32_t j, uint32_t c, uint32_t ip, bool pass) {
     const uint32_t x0 = __shfl(be0, c & 63, 64), x1 = __shfl(be1, c & 63, 64);
     if (j >= hi) return;
@@ -3546,8 +3600,6 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     o.type = poly_type;
     o.value = pass ? (std_domain ? ~sv : sv) : (std_domain ? 0u : sv);
     res[j] = o;
-    n_ok += pass;
-    n_bad += !pass;
   };
   if (hi - lo <= 64) {  // one group (the common case): its chunks and XORs are still in registers
     result(lo + lane, m_c, my_ip, my_pass != 0);
@@ -3564,24 +3616,12 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
       result(j, c, ip, pass);
     }
   }
-  // the counters: updateChecksum case (iv) (:389) / copy_on_write (chunk.rs:153) per applied op, the A6
-  // failures (uio_afix_kernel rewrites them on a void pass)
-  {
-    uint32_t v8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    v8[std_domain ? kCtrRecalc : kCtrRead] = n_ok;
-    v8[kCtrMismatch] = n_bad;
-    __shared__ unsigned int sh[8];
-    if (t < 8) sh[t] = 0;
-    __syncthreads();
-    for (int q = 0; q < 8; ++q)
-      if (v8[q]) atomicAdd(&sh[q], v8[q]);
-    __syncthreads();
-    if (t < 8 && sh[t]) atomicAdd(&ctr[t], (unsigned long long)sh[t]);
-  }
   stores_done();
   __syncthreads();
+#if H3C_AF_TRACE
+  if (t == 0 && L < 1024) g_af_wg[5 * L + 4] = wall_clock64();
+#endif
   if (t == 0) {
-    atomicMax(reinterpret_cast<unsigned long long *>(misc + kMiscT1), (unsigned long long)wall_clock64());
     const uint32_t w = atomicAdd(&aa.ctl[kADone], 1u + (s_void ? kADoneVoid : 0u));
     s_last = (w & 0xFFFu) + 1 == nwg;
     s_prev = (w >> 12) + (s_void ? 1u : 0u);  // void reports, this one included
@@ -3590,6 +3630,10 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   if (!s_last) return;
   // the last workgroup to finish: the totals are the last ticket's inclusive granules
   const bool vd = s_prev != 0 || force_void;
+  // the counters (a pass that is not void has no failed check: every op is updateChecksum case (iv),
+  // :389, or copy_on_write, chunk.rs:153; uio_afix_kernel writes them for a void pass)
+  if (t < kCtrN) ctr[t] = !vd && t == (std_domain ? kCtrRecalc : kCtrRead) ? n : 0u;
+  if (t == 0) *reinterpret_cast<unsigned long long *>(misc + kMiscT1) = wall_clock64();
   if (t < nchunks && !vd) {
     const unsigned long long g = ld_agent(&aa.gran[(uint64_t)(nwg - 1) * kFastCols + t]);
     const uint32_t a = (uint32_t)g;
@@ -4432,6 +4476,20 @@ int capture_graph(hipStream_t st, Body body, hipGraphExec_t &out, const std::vec
   return H3C_OK;
 }
 
+// Host-time trace of this thread's h3c_update_ios_dev calls on the fast branches (h3c_diag_host_trace):
+// summed nanoseconds of [0] the previous call's return to this call's entry (the caller's own time),
+// [1] entry to the first launch, [2] the launches, [3] the last launch to the outcome word seen, [4] the
+// outcome to the return; [5] the number of calls.
+struct HostTrace {
+  std::chrono::steady_clock::time_point entry, last_return, launch0, launched, seen;
+  bool have_return = false;
+  uint64_t sum[6] = {0, 0, 0, 0, 0, 0};
+};
+thread_local HostTrace t_host;
+inline uint64_t ns_between(std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+  return (uint64_t)std::max<int64_t>(0, std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count());
+}
+
 // Spin (bounded) until the device sets a pinned host word; a blocking stream wait follows either way.
 // The bound: h3c_test_hook(H3C_HOOK_FAST_POLL_US) / H3C_FAST_POLL_US when set, else twice the time this
 // thread's last fast batch of the same shape took to reach its outcome (+ 50 us), within
@@ -4839,6 +4897,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     const bool use_graph = gr && gr->g && !gr->failed;
     __atomic_store_n(h_fs, 0u, __ATOMIC_RELAXED);
     const auto t_launch = std::chrono::steady_clock::now();
+    t_host.launch0 = t_launch;
     if (use_graph) {
       HIP_TRY(hipGraphLaunch(gr->g, st));
       g_graph_stats[kDiagReplay].fetch_add(1);
@@ -4846,15 +4905,17 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       rc = a_launch(st);
       if (rc) return rc;
     }
+    t_host.launched = std::chrono::steady_clock::now();
     if (!(use_graph && epi_graph) && !commit_dev) {
       rc = epilogue(st, d_misc + kMiscOutF, cap);
       if (rc) return rc;
     }
     const uint32_t poll_us = fast_poll_budget_us(fpred->last_us);
     const bool seen = poll_host_word(h_fs, poll_us);
+    t_host.seen = std::chrono::steady_clock::now();
     if (seen)
       fpred->last_us = (uint32_t)std::max<int64_t>(
-          1, std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t_launch).count());
+          1, std::chrono::duration_cast<std::chrono::microseconds>(t_host.seen - t_launch).count());
     else
       fpred->last_us = 0;
     auto prof_aligned = [&]() {  // the fused kernel's own wall-clock span (first workgroup start, last end)
@@ -5354,6 +5415,16 @@ extern "C" int h3c_diag_last_graph_audit(uint64_t *out4) {
   return H3C_OK;
 }
 
+extern "C" int h3c_diag_host_trace(uint64_t *out6, int reset) {
+  if (!out6) return H3C_ERR_INVALID_ARG;
+  std::memcpy(out6, t_host.sum, sizeof(t_host.sum));
+  if (reset) {
+    std::memset(t_host.sum, 0, sizeof(t_host.sum));
+    t_host.have_return = false;
+  }
+  return H3C_OK;
+}
+
 extern "C" uint64_t h3c_diag_counter(int which) {
   return which >= 0 && which < kDiagN ? g_graph_stats[which].load() : 0;
 }
@@ -5410,6 +5481,22 @@ extern "C" int h3c_update_ios_ex(uint8_t poly_type, h3c_chunk_state *chunks, uin
 extern "C" int h3c_update_ios_dev(uint8_t poly_type, h3c_chunk_state *chunks_dev, uint32_t nchunks,
                                   const h3c_update_io *ios_dev, uint32_t n, h3c_update_result *results_dev,
                                   uint32_t flags, h3c_update_counters *counters_dev, void *stream) {
+  t_host.entry = std::chrono::steady_clock::now();
+  t_host.launch0 = t_host.launched = t_host.seen = t_host.entry;
+  struct TraceOut {
+    ~TraceOut() {
+      HostTrace &h = t_host;
+      const auto now = std::chrono::steady_clock::now();
+      if (h.have_return) h.sum[0] += ns_between(h.last_return, h.entry);
+      h.sum[1] += ns_between(h.entry, h.launch0);
+      h.sum[2] += ns_between(h.launch0, h.launched);
+      h.sum[3] += ns_between(h.launched, h.seen);
+      h.sum[4] += ns_between(h.seen, now);
+      h.sum[5] += 1;
+      h.last_return = now;
+      h.have_return = true;
+    }
+  } trace_out;
   if (!valid_update_args(poly_type, chunks_dev, nchunks, ios_dev, n, results_dev)) return H3C_ERR_INVALID_ARG;
   int dev = 0;
   int rc = h3c_rt::current_device(&dev);
@@ -5448,6 +5535,17 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
   return h3c_update_ios_ex(poly_type, chunks, nchunks, ios, n, results, flags, nullptr, stream);
 }
 
+#if H3C_AF_TRACE
+extern "C" int h3c_diag_af_trace(unsigned long long *out, int n) {  // (trace builds only)
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_af_wg), 40ull * (unsigned)n) == hipSuccess ? 0 : -1;
+}
+extern "C" int h3c_diag_af_waves(unsigned long long *out, uint32_t *blk, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_af_wave), 128ull * (unsigned)n) == hipSuccess &&
+                 hipMemcpyFromSymbol(blk, HIP_SYMBOL(g_af_blk), 8ull * (unsigned)n) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
 #if H3C_FAST_TRACE == 3
 extern "C" int h3c_diag_fast_wg(unsigned long long *out, int n) {  // (trace builds only)
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_wg), 16ull * (unsigned)n) == hipSuccess ? 0 : -1;

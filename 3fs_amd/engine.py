@@ -91,6 +91,7 @@ _proto("h3c_set_coalescing", _int, _int)
 _proto("h3c_diag_counter", _u64, _int)
 _proto("h3c_diag_last_graph", _int, _vp)
 _proto("h3c_diag_last_graph_audit", _int, _vp)
+_proto("h3c_diag_host_trace", _int, _vp, _int)
 _proto("h3c_diag_sync_bench", _int, _int, _u64, _int, _int, _vp, _vp)
 _proto("h3c_update_ios_dev", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp)
 _proto("h3c_serde_checksum_mark", _u32, _u32, _int)
@@ -383,6 +384,15 @@ def diag_last_graph_audit() -> dict:
     out = (ctypes.c_uint64 * 4)()
     _check(lib.h3c_diag_last_graph_audit(ctypes.cast(out, ctypes.c_void_p)))
     return dict(zip(("kernels", "pointers", "outside", "unknown"), map(int, out)))
+
+
+def diag_host_trace(reset: bool = False) -> dict:
+    """h3c_diag_host_trace: this thread's mean host microseconds per h3c_update_ios_dev call, by phase."""
+    out = (ctypes.c_uint64 * 6)()
+    _check(lib.h3c_diag_host_trace(ctypes.cast(out, ctypes.c_void_p), int(reset)))
+    n = max(int(out[5]), 1)
+    names = ("caller", "to_launch", "launches", "to_outcome", "to_return")
+    return {**{k: round(int(v) / n / 1e3, 2) for k, v in zip(names, out)}, "calls": int(out[5])}
 
 
 def diag_counters() -> dict:

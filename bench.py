@@ -198,11 +198,13 @@ class Ctx:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
         return bool(t.item())
 
-    def timed(self, step, steps: int, warmup: int, kind: int):
+    def timed(self, step, steps: int, warmup: int, kind: int, after_warmup=None):
         """warmup, barrier, time `steps` calls (max over ranks); returns (elapsed_s, prof)."""
         for _ in range(warmup):
             step()
         self.barrier()
+        if after_warmup:
+            after_warmup()
         self.h3c.profile_read(reset=True, kind=kind)
         self.h3c.profile_enable(True)
         t0 = time.perf_counter()
@@ -226,6 +228,7 @@ PATTERN_CEILING = {
     "upd_fused_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
     "uio_block_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
     "uio_fast_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
+    "uio_afused_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
 }
 
 
@@ -464,15 +467,18 @@ def run_updio(args, cx: Ctx) -> dict:
                             graphs=hg).run
 
     g0 = h3c.diag_counters()
-    elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDIO)
+    elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDIO,
+                             after_warmup=lambda: h3c.diag_host_trace(reset=True))
+    host_us = h3c.diag_host_trace(reset=True)  # (the timed steps only)
     diag = {k: v - g0[k] for k, v in h3c.diag_counters().items()}
     graphs = {"replays": diag["graph_replays"], "captures": diag["graph_captures"],
               "capture_failures": diag["graph_capture_failures"]}
     # every redo / recovery / abandoned attempt the engine counts (h3c_diag_counter 3-9), over warmup +
     # timed steps: all 0 on config 3, which must run every step on the fast branch
     redo = {k: diag[k] for k in ("redo_front_void", "rerun_phase_b_void", "redo_failed_a6", "redo_short_fragment_guess",
-                                 "fast_abandoned", "fast_recovered")}
+                                 "fast_abandoned", "fast_recovered", "aligned_abandoned", "aligned_recovered")}
     fast_steps = diag["fast_batches"]
+    aligned_steps = diag["aligned_batches"]
     torch.cuda.synchronize()
     fin = d_state.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)
     res = d_res.cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)
@@ -525,7 +531,9 @@ def run_updio(args, cx: Ctx) -> dict:
     pplan.close()
     writes = nw * args.steps * cx.world
     fast = fast_steps == args.steps + args.warmup
-    rl = roofline(prof, HBM_PEAK_GBPS, kernel="uio_fast_kernel" if fast else "uio_block_kernel")
+    aligned = aligned_steps == args.steps + args.warmup
+    rl = roofline(prof, HBM_PEAK_GBPS, kernel="uio_afused_kernel" if aligned else "uio_fast_kernel" if fast
+                  else "uio_block_kernel")
     out = {
         "metric": "partial-update writes/s through the general UpdateIO path (4 KiB writes into 64 MiB chunks)",
         "value": round(writes / elapsed, 1),
@@ -544,8 +552,10 @@ def run_updio(args, cx: Ctx) -> dict:
         "algorithmic_gbps": round(writes * 3 * G / elapsed / 1e9, 1),
         "counters": counters,
         "graphs": graphs,  # the headline leg's graph use over warmup + timed steps (--updio-graphs)
-        "branch": "fast (uio_fast_kernel)" if fast else f"general ({fast_steps} of {args.steps + args.warmup} fast)",
+        "branch": "fast, aligned sub-branch (uio_aprep_kernel + uio_afused_kernel)" if aligned else
+                  "fast (uio_fast_kernel)" if fast else f"general ({fast_steps} of {args.steps + args.warmup} fast)",
         "redo": redo,
+        "host_us_per_call": host_us,  # the device-table leg's host time per call, by phase (h3c_diag_host_trace)
         "oracle_sample": {"chunks": sample, "ok": bool(oracle_ok),
                           "check": "final stored checksum == CPU oracle CRC32C of the chunk's bytes after the run"},
         "pcie_inclusive": {"entry": "h3c_update_ios_ex (host tables in pinned memory)",

@@ -496,6 +496,10 @@ int h3c_diag_last_graph(uint64_t *out7);
  * nodes audited, pointer arguments checked, pointers outside the key's buffers, kernel nodes whose
  * arguments could not be read}.  A graph is instantiated only when the last two are 0. */
 int h3c_diag_last_graph_audit(uint64_t *out4);
+/* Host-time trace of this thread's h3c_update_ios_dev calls (bench diagnostics): out6 = summed nanoseconds of
+ * {the previous call's return to this call's entry, entry to the first kernel launch, the launches, the last
+ * launch to the outcome word seen, the outcome to the return} and the number of calls; reset != 0 clears. */
+int h3c_diag_host_trace(uint64_t *out6, int reset);
 
 #ifdef __cplusplus
 }

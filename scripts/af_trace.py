@@ -1,0 +1,55 @@
+"""Per-workgroup phases of uio_afused_kernel (an H3C_AF_TRACE=1 build: scripts/build_variant.sh aftrace
+-DH3C_AF_TRACE=1): runs config-3 UpdateIO batches and prints, per ticket-ordered workgroup, its start, table
+fill, main loop, look-back and tail in microseconds from the first start (quantiles over workgroups).
+usage: H3C_LIB_PATH=.../diag/aftrace/libh3c_crc.so python scripts/af_trace.py"""
+import ctypes
+import importlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.argv = [sys.argv[0], "--workload", "updio", "--no-cpu-baseline", "--steps", "5", "--warmup", "5",
+            "--updio-graphs", "0"]
+bench = importlib.import_module("bench")
+h3c = importlib.import_module("3fs_amd")
+rc = bench.main()
+lib = h3c.engine.lib
+lib.h3c_diag_af_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
+nwg = 250
+buf = (ctypes.c_ulonglong * (5 * 1024))()
+assert lib.h3c_diag_af_trace(buf, 1024) == 0
+a = np.array(buf[:5 * nwg], dtype=np.float64).reshape(nwg, 5)
+khz = 100000.0  # the wall clock's 100 MHz
+t0 = a[:, 0].min()
+us = (a - t0) / (khz / 1000.0)
+names = ["start", "filled", "loop_end", "lookback_end", "end"]
+for q in (0, 50, 90, 99, 100):
+    print(f"q{q:3d} " + " ".join(f"{n}={np.percentile(us[:, i], q):7.1f}" for i, n in enumerate(names)))
+print("per-wg loop time (loop_end - filled): median %.1f max %.1f" % (np.median(us[:, 2] - us[:, 1]), (us[:, 2] - us[:, 1]).max()))
+print("look-back wait (lookback_end - loop_end): median %.1f max %.1f" % (np.median(us[:, 3] - us[:, 2]), (us[:, 3] - us[:, 2]).max()))
+print("tail (end - lookback_end): median %.1f max %.1f" % (np.median(us[:, 4] - us[:, 3]), (us[:, 4] - us[:, 3]).max()))
+order = np.argsort(us[:, 2])[-5:]
+print("latest loop ends (ticket, us):", [(int(i), round(float(us[i, 2]), 1)) for i in order])
+corr = np.corrcoef(np.arange(nwg), us[:, 2] - us[:, 1])[0, 1]
+print("corr(ticket, loop time) = %.2f" % corr)
+lib.h3c_diag_af_waves.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+wv = (ctypes.c_ulonglong * (16 * 1024))()
+bk = (ctypes.c_uint32 * (2 * 1024))()
+assert lib.h3c_diag_af_waves(wv, bk, 1024) == 0
+w = (np.array(wv[:16 * nwg], dtype=np.float64).reshape(nwg, 16) - t0) / (khz / 1000.0)
+blk = np.array(bk[:2 * nwg]).reshape(nwg, 2)
+spread = w.max(1) - w.min(1)
+print("per-wg wave spread (max - min wave end): median %.1f max %.1f" % (np.median(spread), spread.max()))
+print("wave ends: q0 %.1f q50 %.1f q90 %.1f q100 %.1f" % tuple(np.percentile(w, [0, 50, 90, 100])))
+for x in range(8):
+    m = blk[:, 1] == x
+    if m.any():
+        print("xcc %d: %3d wgs, loop_end median %.1f max %.1f, mean wave end %.1f" % (
+            x, m.sum(), np.median(us[m, 2]), us[m, 2].max(), w[m].mean()))
+# which waves are late: their op ranges (ticket * 16 + wave) -> position in the batch
+late = np.argsort(w.ravel())[-20:]
+print("latest waves (ticket, wave, end):", [(int(i // 16), int(i % 16), round(float(w.ravel()[i]), 1)) for i in late[-8:]])
+sys.exit(rc)
