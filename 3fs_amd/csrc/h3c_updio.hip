@@ -3153,6 +3153,7 @@ __global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uin
 __device__ unsigned long long g_af_wg[1024 * 5];
 __device__ unsigned long long g_af_wave[1024 * 16];
 __device__ uint32_t g_af_blk[1024 * 2];
+__device__ uint32_t g_af_fin[1024 * 16];  // per wave: its ops whose block has later writes (the fin path)
 #endif
 #ifndef H3C_AF_EARLY_OLD
 #define H3C_AF_EARLY_OLD 0  // 1: the next op's old rows load with its new rows, before this op's CRCs (A/B)
@@ -3175,6 +3176,8 @@ struct AlignedArgs {
   uint2 *pv;                      // per op: {crc0(new), the resolved previous op of the block (kNil: none)}
   uint32_t *inp;                  // per op: its chunk's XOR of shifted deltas in the wave's range up to it
   uint2 *defer;                   // blocks whose first op deferred the write-back: {first op, last op}
+  uint4 *rec;                     // per op, 2 x 16 bytes (uio_afused_kernel's phase 0 -> 1): new bytes, old bytes
+                                  //  (| 1: the block's first op), the block's final bytes, the A6 expectations
 };
 
 // An op the aligned sub-branch takes: a fast-branch op (fast_op) that writes one whole 4 KiB block at a
@@ -3263,7 +3266,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     unsigned long long *__restrict__ ctr, uint32_t *hout, h3c_chunk_state *commit, uint32_t force_void) {
   __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
   __shared__ h3c_chunk_state s_cs[kFastChunksLds];
-  __shared__ uint32_t s_ticket, s_E, s_slow, s_last, s_void, s_prev;
+  __shared__ uint32_t s_ticket, s_E, s_slow, s_last, s_void, s_prev, s_grab;
   const uint32_t t = threadIdx.x, lane = t & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
   if (t == 0) {
@@ -3279,6 +3282,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   // workgroup on one address) and the last workgroup's end
   if (t == 0 && L == 0) *reinterpret_cast<unsigned long long *>(misc + kMiscT0) = wall_clock64();
 #if H3C_AF_TRACE
+  if (t < 16 && L < 1024) g_af_fin[16 * L + t] = 0;
   if (t == 0 && L < 1024) {
     g_af_wg[5 * L] = wall_clock64();
     g_af_blk[2 * L] = blockIdx.x;
@@ -3307,87 +3311,66 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     return;
   }
   const uint32_t k4096 = dgf_mul(0xFFFFFFFFu, pc->pow8[12], poly);  // ~0 * x^(8 * 4096)
-  const uint64_t gw = (uint64_t)L * kBlkWaves + wave, nw = (uint64_t)nwg * kBlkWaves;
-  const uint32_t lo = (uint32_t)(gw * n / nw), hi = (uint32_t)((gw + 1) * n / nw);
+  // the workgroup's ops [wlo, whi) (ticket order) and, for the prefix, each wave's contiguous share
+  const uint32_t wlo = (uint32_t)((uint64_t)L * n / nwg), whi = (uint32_t)((uint64_t)(L + 1) * n / nwg);
+  const uint32_t wn_ops = whi - wlo;
+  const uint32_t lo = wlo + (uint32_t)((uint64_t)wave * wn_ops / kBlkWaves);
+  const uint32_t hi = wlo + (uint32_t)((uint64_t)(wave + 1) * wn_ops / kBlkWaves);
   const uint32_t lo16 = 16u * lane;  // (32 bits: a wave-uniform base plus this offset is one saddr load)
-  auto rl64 = [](uint64_t v, uint32_t u) -> uint64_t {
-    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, u) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), u) << 32);
-  };
-  // per group of 64 ops, lane k's op: chunk, shift x^(8(size - offset - 4096)), new / old / destination /
-  // final bytes, the A6 expectations of the op and of the block's last op, the resolved previous op
-  // (m_first: the block's first op, whose old bytes are the block itself and which writes the block back)
-  uint32_t m_c = kNil, m_exp = 0, m_fexp = 0, m_first = 0;
-  uint64_t m_new = 0, m_old = 0, m_fin = 0;
+  // ---- phase 0, one thread per op of the workgroup, beside the table fill: each op's old bytes (the
+  // previous op of its block: in its tile, else the last listed one of an earlier tile; none: the block
+  // itself, and the op writes the block back -- with the block's last op's bytes), its A6 expectations;
+  // one 32-byte record per op for phase 1's scalar loads ----
+  // (each wave's first op is wlo + wave: its new rows and (speculated) block rows load before the fill)
   uint4 vn[4], vo[4];
-  bool valid = false;
-  uint64_t pnew = 0, pold = 0;
-  auto start_group = [&](uint32_t g0) {
-    const uint32_t cnt = min(64u, hi - g0);
-    const uint32_t k = g0 + lane;
-    m_c = kNil;
-    m_exp = m_fexp = m_first = 0;
-    m_new = m_old = m_fin = 0;
-    uint32_t prev = kNil;
-    unsigned long long key = kNoKey;
-    if (lane < cnt) {
-      const h3c_update_io io = ios[k];
-      const uint4 lk = aa.link[k];
-      const h3c_chunk_state cs = s_cs[io.chunk];  // (aprep: every op's chunk is < nchunks <= 128)
-      const uint64_t slot = cs.base + io.offset;
-      m_c = io.chunk;
-      m_new = io.payload;
-      m_exp = aexpect(io.checksum_value, std_domain, k4096);
-      if (lk.x != kNil) {  // an earlier op of the block in this tile: its payload is the old bytes
-        prev = lk.x;
-        m_old = ios[lk.x].payload;
-      } else {  // speculation: no earlier op of the block (the walk below checks the earlier tiles)
-        m_old = slot;
-        m_first = 1;
-        m_fin = m_new;
-        m_fexp = m_exp;
-        key = aa.key[k];
-      }
-    }
-    valid = __builtin_amdgcn_readlane(m_c, 0) != kNil;
-    pnew = rl64(m_new, 0);
-    pold = rl64(m_old, 0);
+  const uint32_t j0 = wlo + wave;
+  uint64_t spec_old = 0;
+  if (j0 < whi) {
+    const h3c_update_io io = ios[j0];  // (scalar: wave-uniform)
+    spec_old = s_cs[io.chunk].base + io.offset;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      vn[u] = valid ? load_row(pnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
-      vo[u] = valid ? load_row(pold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+      vn[u] = load_row(io.payload + (uint32_t)(u * kRowBytes + lo16));
+      vo[u] = load_row(spec_old + (uint32_t)(u * kRowBytes + lo16));
     }
-    // the walk over the block's listed tile-last ops (this batch's entries), while those rows load
-    if (key != kNoKey) {
-      uint32_t p = kNil, fmax = k;
+  }
+  for (uint32_t j = wlo + t; j < whi; j += kBlkThreads) {
+    const h3c_update_io io = ios[j];
+    const uint4 lk = aa.link[j];
+    const h3c_chunk_state &cs = s_cs[io.chunk];  // (aprep: every op's chunk is < nchunks <= 128)
+    const uint32_t exp = aexpect(io.checksum_value, std_domain, k4096);
+    uint32_t prev = lk.x, fexp = 0;
+    uint64_t old = 0, fin = 0;
+    if (prev == kNil) {  // no earlier op of the block in this tile: the earlier tiles' listed last ops
+      const unsigned long long key = aa.key[j];
+      uint32_t fmax = j;
       for (uint32_t e = aa.head[fast_bucket(key, aa.hmask)]; aentry_valid(e, E); e = aa.link[(e & 0xFFFFFFu) - 1].y) {
-        const uint32_t j = (e & 0xFFFFFFu) - 1;
-        if (j >= n) break;  // (cannot happen: this batch's entries name its ops)
-        if (aa.key[j] != key) continue;
-        if (j < k && (p == kNil || j > p)) p = j;
-        fmax = max(fmax, j);
+        const uint32_t i = (e & 0xFFFFFFu) - 1;
+        if (i >= n) break;  // (cannot happen: this batch's entries name its ops)
+        if (aa.key[i] != key) continue;
+        if (i < j && (prev == kNil || i > prev)) prev = i;
+        fmax = max(fmax, i);
       }
-      if (p != kNil) {  // an earlier tile wrote the block: its payload is the old bytes; it writes back
-        prev = p;
-        m_old = ios[p].payload;
-        m_first = 0;
-        m_fin = 0;
-      } else if (fmax != k) {  // the block's first op leaves the block's last op's bytes, checked first
-        const h3c_update_io fio = ios[fmax];
-        m_fin = fio.payload;
-        m_fexp = aexpect(fio.checksum_value, std_domain, k4096);
+      if (prev == kNil) {  // the block's first op
+        old = (cs.base + io.offset) | 1u;
+        fin = io.payload;
+        fexp = exp;
+        if (fmax != j) {
+          const h3c_update_io fio = ios[fmax];
+          fin = fio.payload;
+          fexp = aexpect(fio.checksum_value, std_domain, k4096);
+        }
       }
     }
-    if (lane < cnt) aa.pv[k].y = prev;  // (uio_afix_kernel's input; crc0(new) follows in .x)
-    const uint64_t pold2 = rl64(m_old, 0);
-    if (valid && pold2 != pold) {  // op 0 was mis-speculated: its old rows again
-      pold = pold2;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) vo[u] = load_row(pold + (uint32_t)(u * kRowBytes + lo16));
-    }
-  };
-  if (lo < hi) start_group(lo);  // the first group's links and rows load while the tables fill
+    if (prev != kNil) old = ios[prev].payload;
+    aa.rec[2 * (size_t)j] = make_uint4((uint32_t)io.payload, (uint32_t)(io.payload >> 32), (uint32_t)old,
+                                       (uint32_t)(old >> 32));
+    aa.rec[2 * (size_t)j + 1] = make_uint4((uint32_t)fin, (uint32_t)(fin >> 32), exp, fexp);
+    aa.pv[j].y = prev;  // (uio_afix_kernel's input; crc0(new) follows in .x)
+  }
   fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
+  if (t == 0) s_grab = wlo + kBlkWaves;  // (each wave's first op is wlo + wave)
+  stores_done();
   __syncthreads();
 #if H3C_AF_TRACE
   if (t == 0 && L < 1024) g_af_wg[5 * L + 1] = wall_clock64();
@@ -3395,136 +3378,162 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
   const LaneLut Lt = make_lut(lane);
-  uint32_t acc0 = 0, acc1 = 0;  // running XOR of chunks lane, lane + 64 over the wave's range
-  uint32_t my_ip = 0, my_pass = 0;
+  // ---- phase 1: the workgroup's ops, taken one at a time from an LDS counter by whichever wave is free
+  // (static shares left waves up to ~30 us apart): per op the A6 CRC of the new bytes and the delta CRC of
+  // new ^ old, the block write-back by the block's first op, {state, delta} and crc0(new) published ----
+  struct Rec {
+    uint64_t pnew, pold, fin;
+    uint32_t exp, fexp;
+    bool first;
+  };
+  auto rec_of = [&](uint32_t j, Rec &r) {  // (scalar loads: j is wave-uniform)
+    const uint4 a = aa.rec[2 * (size_t)j], b = aa.rec[2 * (size_t)j + 1];
+    r.pnew = (uint64_t)a.x | ((uint64_t)a.y << 32);
+    const uint64_t o = (uint64_t)a.z | ((uint64_t)a.w << 32);
+    r.pold = o & ~uint64_t(1);
+    r.first = (o & 1u) != 0;
+    r.fin = (uint64_t)b.x | ((uint64_t)b.y << 32);
+    r.exp = b.z;
+    r.fexp = b.w;
+  };
+  auto grab = [&]() -> uint32_t {
+    uint32_t j = 0;
+    if (lane == 0) j = atomicAdd(&s_grab, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
+  };
   uint32_t wave_void = 0;
-  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
-    const uint32_t cnt = min(64u, hi - g0);
-    const uint32_t k = g0 + lane;
-    uint32_t my_d = 0;
-    my_pass = 0;
-    for (uint32_t u0 = 0; u0 < cnt; ++u0) {
-      const bool nvalid = u0 + 1 < cnt && __builtin_amdgcn_readlane(m_c, u0 + 1) != kNil;
-      uint4 wn[4], wo[4];
-      uint64_t npnew = 0, npold = 0;
-      if (nvalid) {
-        npnew = rl64(m_new, u0 + 1);
-        npold = rl64(m_old, u0 + 1);
-      }
-      // the next op's new rows now, its old rows once this op's old rows are consumed (their registers
-      // free): a load round trip is a fraction of an op's time, and both pairs in flight at once spill
+  uint32_t jc = j0 < whi ? j0 : kNil;
+  Rec rc{}, rn{};
+  if (jc != kNil) {
+    rec_of(jc, rc);
+    if (rc.pold != spec_old) {  // the first op was not its block's first: its old rows are a payload
 #pragma unroll
-      for (int u = 0; u < 4; ++u) wn[u] = nvalid ? load_row(npnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
-#if H3C_AF_EARLY_OLD
+      for (int u = 0; u < 4; ++u) vo[u] = load_row(rc.pold + (uint32_t)(u * kRowBytes + lo16));
+    }
+  }
+  uint32_t jn = jc != kNil ? grab() : kNil;
+  if (jn >= whi) jn = kNil;
+  if (jn != kNil) rec_of(jn, rn);
+  while (jc != kNil) {
+    uint4 wn[4], wo[4];
+    const bool nvalid = jn != kNil;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) wo[u] = nvalid ? load_row(npold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
-#endif
-      if (valid) {
-        const bool first = __builtin_amdgcn_readlane((int)m_first, u0) != 0;
-        const bool solo = first && rl64(m_fin, u0) == pnew;  // the block's only write
-        if (H3C_AF_STORE_EARLY && solo) {
+    for (int u = 0; u < 4; ++u) {
+      wn[u] = nvalid ? load_row(rn.pnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+      wo[u] = nvalid ? load_row(rn.pold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+    }
+    uint32_t jnn = nvalid ? grab() : kNil;  // (the op after next: its record loads meanwhile)
+    if (jnn >= whi) jnn = kNil;
+    Rec rnn{};
+    if (jnn != kNil) rec_of(jnn, rnn);
+    const bool solo = rc.first && rc.fin == rc.pnew;  // the block's only write
+    if (H3C_AF_STORE_EARLY && solo) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) store_masked(pold, u * kRowBytes + lo16, vn[u], 0u, kBlk);
+      for (int u = 0; u < 4; ++u) store_masked(rc.pold, u * kRowBytes + lo16, vn[u], 0u, kBlk);
+    }
+    Streams s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!(H3C_AF_EXPERIMENT & 1)) consume(s2[0], vn[u], lb, Lt);
+      consume(s2[1], xor4(vn[u], vo[u]), lb, Lt);
+    }
+    uint32_t fv[2];
+    wave_fold_tab_n<2>(s2, lane, red, fv);
+    const uint32_t P = (H3C_AF_EXPERIMENT & 1) ? rc.exp : (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[0]);
+    const uint32_t D = (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[1]);
+    const bool pass = P == rc.exp;
+    if (rc.first) {  // the block's first op: the block's final bytes (the last op's, if its check passes)
+      if (solo) {
+        if (H3C_AF_STORE_EARLY ? !pass : pass) {  // (early store: a failed check puts the old rows back)
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            store_masked(rc.pold, u * kRowBytes + lo16, H3C_AF_STORE_EARLY ? vo[u] : vn[u], 0u, kBlk);
         }
-        Streams s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (!(H3C_AF_EXPERIMENT & 1)) consume(s2[0], vn[u], lb, Lt);
-          consume(s2[1], xor4(vn[u], vo[u]), lb, Lt);
-        }
-#if !H3C_AF_EARLY_OLD
-#pragma unroll
-        for (int u = 0; u < 4; ++u) wo[u] = nvalid ? load_row(npold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+      } else {
+#if H3C_AF_TRACE
+        if (lane == 0 && L < 1024) atomicAdd(&g_af_fin[16 * L + wave], 1u);
 #endif
-        uint32_t fv[2];
-        wave_fold_tab_n<2>(s2, lane, red, fv);
-        const uint32_t P = (H3C_AF_EXPERIMENT & 1) ? (uint32_t)__builtin_amdgcn_readlane((int)m_exp, u0)
-                                                   : (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[0]);
-        const uint32_t D = (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[1]);
-        const bool pass = P == (uint32_t)__builtin_amdgcn_readlane((int)m_exp, u0);
-        if (lane == 0) aa.pv[g0 + u0].x = P;
-        if (first) {  // the block's first op: the block's final bytes (the last op's, if its check passes)
-          const uint64_t dst = pold;
-          const uint64_t fin = rl64(m_fin, u0);
-          if (solo) {
-            if (H3C_AF_STORE_EARLY ? !pass : pass) {  // (early store: a failed check puts the old rows back)
+        // (into the old rows' registers: this op's delta is folded, and the next op's rows are in wn / wo)
 #pragma unroll
-              for (int u = 0; u < 4; ++u) store_masked(dst, u * kRowBytes + lo16, H3C_AF_STORE_EARLY ? vo[u] : vn[u], 0u, kBlk);
-            }
-          } else {
-            // (into the old rows' registers: this op's delta is folded, and the next op's rows are in wn / wo)
+        for (int u = 0; u < 4; ++u) vo[u] = load_row(rc.fin + (uint32_t)(u * kRowBytes + lo16));
+        Streams sf{0, 0, 0, 0};
 #pragma unroll
-            for (int u = 0; u < 4; ++u) vo[u] = load_row(fin + (uint32_t)(u * kRowBytes + lo16));
-            Streams sf{0, 0, 0, 0};
+        for (int u = 0; u < 4; ++u) consume(sf, vo[u], lb, Lt);
+        const uint32_t Pf = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_fold_tab(sf, lane, red));
+        if (Pf == rc.fexp) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) consume(sf, vo[u], lb, Lt);
-            const uint32_t Pf = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_fold_tab(sf, lane, red));
-            if (Pf == (uint32_t)__builtin_amdgcn_readlane((int)m_fexp, u0)) {
-#pragma unroll
-              for (int u = 0; u < 4; ++u) store_masked(dst, u * kRowBytes + lo16, vo[u], 0u, kBlk);
-            } else {  // the last op fails A6: uio_afix_kernel writes the last passing op's bytes (if any)
-              if (lane == 0) {
-                const uint32_t d = atomicAdd(&aa.ctl[kADefer], 1u);
-                aa.defer[d] = make_uint2(g0 + u0, 0u);
-              }
-              wave_void = 1;
-            }
+          for (int u = 0; u < 4; ++u) store_masked(rc.pold, u * kRowBytes + lo16, vo[u], 0u, kBlk);
+        } else {  // the last op fails A6: uio_afix_kernel writes the last passing op's bytes (if any)
+          if (lane == 0) {
+            const uint32_t d = atomicAdd(&aa.ctl[kADefer], 1u);
+            aa.defer[d] = make_uint2(jc, 0u);
           }
+          wave_void = 1;
         }
-        if (lane == u0) {
-          my_d = D;
-          my_pass = pass;
-        }
-      } else if (!H3C_AF_EARLY_OLD) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) wo[u] = nvalid ? load_row(npold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
-      }
-      valid = nvalid;
-      pnew = npnew;
-      pold = npold;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        vn[u] = wn[u];
-        vo[u] = wo[u];
       }
     }
-    // the group's per-op records (uio_afix_kernel's input), each op's shifted delta, every op's chunk XOR
-    // right after it (inclusive, with the earlier groups' running value), the running values moved on
-    const bool op = lane < cnt && m_c != kNil;
-    if (op) aa.dv[k] = ((unsigned long long)(my_pass ? 1u : 2u) << 32) | my_d;
-    if (__builtin_amdgcn_ballot_w64(op && !my_pass)) wave_void = 1;
-    uint32_t v = 0;
-    if (op && my_pass) {  // the delta moved to the chunk's end: x^(8(size - offset - 4096)), offset from the key
-      const h3c_chunk_state &cs = s_cs[m_c];
-      const int64_t off = (int64_t)((aa.key[k] & ((1ull << 36) - 1)) << 12) - (int64_t)cs.base;
-      v = dgf_mul(my_d, dxpow8_fast((int64_t)cs.size - off - (int64_t)kBlk, pc, poly), poly);
+    if (lane == 0) {
+      aa.dv[jc] = ((unsigned long long)(pass ? 1u : 2u) << 32) | D;
+      aa.pv[jc].x = P;
     }
-    const uint32_t src = m_c & 63;
-    const uint32_t r0 = __shfl(acc0, src, 64), r1 = __shfl(acc1, src, 64);
-    my_ip = m_c < 64 ? r0 : r1;
-    for (uint32_t u0 = 0; u0 < cnt; ++u0) {
-      const uint32_t ct = __builtin_amdgcn_readlane(m_c, u0), vt = __builtin_amdgcn_readlane(v, u0);
-      if (lane >= u0 && m_c == ct) my_ip ^= vt;
-      if (ct == lane) acc0 ^= vt;
-      if (ct == lane + 64) acc1 ^= vt;
+    if (!pass) wave_void = 1;
+    jc = jn;
+    rc = rn;
+    jn = jnn;
+    rn = rnn;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      vn[u] = wn[u];
+      vo[u] = wo[u];
     }
-    if (hi - lo > 64 && lane < cnt) aa.inp[k] = my_ip;
-    if (g0 + 64 < hi) start_group(g0 + 64);
   }
 #if H3C_AF_TRACE
   if (lane == 0 && L < 1024) g_af_wave[16 * L + wave] = wall_clock64();
 #endif
+  if (wave_void && lane == 0) atomicOr(&s_void, 1u);
+  stores_done();
+  __syncthreads();  // every op of the workgroup published (the CRC tables are done with: their LDS is free)
+#if H3C_AF_TRACE
+  if (t == 0 && L < 1024) g_af_wg[5 * L + 2] = wall_clock64();
+#endif
+  // ---- phase 2: per wave, its contiguous share of the workgroup's ops in sequence order: each op's delta
+  // moved to its chunk's end, the chunk XOR right after it (lanes: one op each, in groups of 64), the
+  // running per-chunk XORs (lane c: chunks c and c + 64) ----
+  uint32_t acc0 = 0, acc1 = 0;
+  uint32_t my_ip = 0, my_pass = 0, my_c = kNil;
+  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
+    const uint32_t cnt = min(64u, hi - g0), k = g0 + lane;
+    uint32_t v = 0;
+    my_c = kNil;
+    my_pass = 0;
+    if (lane < cnt) {
+      const unsigned long long key = aa.key[k];
+      const unsigned long long g = ld_agent(&aa.dv[k]);  // (another wave's store, before the barrier)
+      my_c = (uint32_t)(key >> 36);
+      my_pass = (uint32_t)(g >> 32) == 1u;
+      if (my_pass) {  // x^(8(size - offset - 4096)), the offset from the key's block address
+        const h3c_chunk_state &cs = s_cs[my_c];
+        const int64_t off = (int64_t)((key & ((1ull << 36) - 1)) << 12) - (int64_t)cs.base;
+        v = dgf_mul((uint32_t)g, dxpow8_fast((int64_t)cs.size - off - (int64_t)kBlk, pc, poly), poly);
+      }
+    }
+    const uint32_t src = my_c & 63;
+    const uint32_t r0 = __shfl(acc0, src, 64), r1 = __shfl(acc1, src, 64);
+    my_ip = my_c < 64 ? r0 : r1;
+    for (uint32_t u0 = 0; u0 < cnt; ++u0) {
+      const uint32_t ct = __builtin_amdgcn_readlane(my_c, u0), vt = __builtin_amdgcn_readlane(v, u0);
+      if (lane >= u0 && my_c == ct) my_ip ^= vt;
+      if (ct == lane) acc0 ^= vt;
+      if (ct == lane + 64) acc1 ^= vt;
+    }
+    if (hi - lo > 64 && lane < cnt) aa.inp[k] = my_ip;
+  }
   // the chunks' base checksums (trusted stored values), one per lane (chunks lane, lane + 64)
   auto t0_of = [&](uint32_t c) -> uint32_t {
     return c < nchunks ? (std_domain ? ~s_cs[c].value : s_cs[c].value) : 0u;
   };
   const uint32_t rb0 = t0_of(lane), rb1 = t0_of(64 + lane);
-  if (wave_void && lane == 0) atomicOr(&s_void, 1u);
   // ---- chunk aggregates: waves of the workgroup (LDS), then workgroups (look-back in ticket order) ----
-  __syncthreads();  // the CRC tables are done with: their LDS holds the aggregates now
-#if H3C_AF_TRACE
-  if (t == 0 && L < 1024) g_af_wg[5 * L + 2] = wall_clock64();
-#endif
   uint32_t *wagg = lds;                                 // [16][128]
   uint32_t *wexcl = lds + kBlkWaves * kFastCols;        // [128]: the workgroup's exclusive prefix
   wagg[wave * kFastCols + lane] = acc0;
@@ -3602,7 +3611,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     res[j] = o;
   };
   if (hi - lo <= 64) {  // one group (the common case): its chunks and XORs are still in registers
-    result(lo + lane, m_c, my_ip, my_pass != 0);
+    result(lo + lane, my_c, my_ip, my_pass != 0);
   } else {
     for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
       const uint32_t j = i0 + lane;
@@ -4305,7 +4314,8 @@ struct ArgLayout<AlignedArgs, void> {
   static void fill(ArgSpec &a) {
     struct_arg<AlignedArgs>(a, {offsetof(AlignedArgs, ctl), offsetof(AlignedArgs, head), offsetof(AlignedArgs, gran),
                                 offsetof(AlignedArgs, key), offsetof(AlignedArgs, link), offsetof(AlignedArgs, dv),
-                                offsetof(AlignedArgs, pv), offsetof(AlignedArgs, inp), offsetof(AlignedArgs, defer)});
+                                offsetof(AlignedArgs, pv), offsetof(AlignedArgs, inp), offsetof(AlignedArgs, defer),
+                                offsetof(AlignedArgs, rec)});
   }
 };
 template <>
@@ -4678,6 +4688,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       aa.pv = carve<uint2>(cur, n);
       aa.inp = carve<uint32_t>(cur, n);
       aa.defer = carve<uint2>(cur, n);
+      aa.rec = carve<uint4>(cur, 2 * (size_t)n);
     }
     return (size_t)(cur - base);
   };
@@ -5539,9 +5550,10 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
 extern "C" int h3c_diag_af_trace(unsigned long long *out, int n) {  // (trace builds only)
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_af_wg), 40ull * (unsigned)n) == hipSuccess ? 0 : -1;
 }
-extern "C" int h3c_diag_af_waves(unsigned long long *out, uint32_t *blk, int n) {
+extern "C" int h3c_diag_af_waves(unsigned long long *out, uint32_t *blk, uint32_t *fin, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_af_wave), 128ull * (unsigned)n) == hipSuccess &&
-                 hipMemcpyFromSymbol(blk, HIP_SYMBOL(g_af_blk), 8ull * (unsigned)n) == hipSuccess
+                 hipMemcpyFromSymbol(blk, HIP_SYMBOL(g_af_blk), 8ull * (unsigned)n) == hipSuccess &&
+                 hipMemcpyFromSymbol(fin, HIP_SYMBOL(g_af_fin), 64ull * (unsigned)n) == hipSuccess
              ? 0
              : -1;
 }

@@ -35,10 +35,12 @@ order = np.argsort(us[:, 2])[-5:]
 print("latest loop ends (ticket, us):", [(int(i), round(float(us[i, 2]), 1)) for i in order])
 corr = np.corrcoef(np.arange(nwg), us[:, 2] - us[:, 1])[0, 1]
 print("corr(ticket, loop time) = %.2f" % corr)
-lib.h3c_diag_af_waves.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+lib.h3c_diag_af_waves.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 wv = (ctypes.c_ulonglong * (16 * 1024))()
 bk = (ctypes.c_uint32 * (2 * 1024))()
-assert lib.h3c_diag_af_waves(wv, bk, 1024) == 0
+fn = (ctypes.c_uint32 * (16 * 1024))()
+assert lib.h3c_diag_af_waves(wv, bk, fn, 1024) == 0
+fin = np.array(fn[:16 * nwg]).reshape(nwg, 16)
 w = (np.array(wv[:16 * nwg], dtype=np.float64).reshape(nwg, 16) - t0) / (khz / 1000.0)
 blk = np.array(bk[:2 * nwg]).reshape(nwg, 2)
 spread = w.max(1) - w.min(1)
@@ -47,8 +49,12 @@ print("wave ends: q0 %.1f q50 %.1f q90 %.1f q100 %.1f" % tuple(np.percentile(w, 
 for x in range(8):
     m = blk[:, 1] == x
     if m.any():
-        print("xcc %d: %3d wgs, loop_end median %.1f max %.1f, mean wave end %.1f" % (
-            x, m.sum(), np.median(us[m, 2]), us[m, 2].max(), w[m].mean()))
+        print("xcc %d: %3d wgs, loop_end median %.1f max %.1f, mean wave end %.1f, mean ticket %.0f, fin ops/wave %.2f" % (
+            x, m.sum(), np.median(us[m, 2]), us[m, 2].max(), w[m].mean(), np.arange(nwg)[m].mean(), fin[m].mean()))
+wl = (w - us[:, 1:2]).ravel()
+print("corr(wave time, fin ops) = %.2f; fin ops/wave by ticket quartile:" % np.corrcoef(wl, fin.ravel())[0, 1],
+      [round(float(fin[q * nwg // 4:(q + 1) * nwg // 4].mean()), 2) for q in range(4)])
+print("blockIdx -> xcc:", [(int(blk[i, 0]), int(blk[i, 1])) for i in range(12)])
 # which waves are late: their op ranges (ticket * 16 + wave) -> position in the batch
 late = np.argsort(w.ravel())[-20:]
 print("latest waves (ticket, wave, end):", [(int(i // 16), int(i % 16), round(float(w.ravel()[i]), 1)) for i in late[-8:]])
