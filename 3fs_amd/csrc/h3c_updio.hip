@@ -2471,12 +2471,14 @@ __device__ uint32_t g_fast_rot;  // workgroup b takes range (b + g_fast_rot) % g
 #endif
 constexpr uint32_t kFastCols = 128;  // chunks a fast-branch batch may name (lane c: chunks c, c + 64)
 // FastScratch words: [0] the chain-based fast branch's slow word; [64, 128) the aligned sub-branch's control
-// words (kACtlWords); [128, ...) its look-back granules (kAGranRows rows of kFastCols u64); then the fast
+// words (kACtlWords); [128, ...) its look-back granules (kAGranRows rows of kFastCols u64) and per-ticket
+// throughput records (kAGranRows x 3 words); then the fast
 // branch's bucket heads (hcap words, zero between batches) and the aligned sub-branch's (hcap words,
 // epoch-tagged).  A layout for another hcap starts from a zeroed scratch.
 constexpr uint32_t kAGranRows = 1024;  // aligned workgroups at most
 constexpr uint32_t kScratchACtl = 64, kScratchAGran = 128;
-constexpr uint32_t kScratchHeads = kScratchAGran + 2 * kAGranRows * kFastCols;
+constexpr uint32_t kScratchAStat = kScratchAGran + 2 * kAGranRows * kFastCols;
+constexpr uint32_t kScratchHeads = kScratchAStat + 3 * kAGranRows;
 constexpr uint32_t kAEpochBatches = 240;  // aligned batches between zeroings (epochs are 8 bits)
 #ifndef H3C_FAST_GRAB
 #define H3C_FAST_GRAB 1  // 1: a workgroup's waves take their chain starts from an LDS counter (0: static ranges)
@@ -3160,7 +3162,13 @@ __device__ uint32_t g_af_fin[1024 * 16];  // per wave: its ops whose block has l
 #endif
 constexpr uint32_t kATile = 256;             // uio_aprep_kernel ops per workgroup
 constexpr uint32_t kAMaxOps = (1u << 24) - 2;  // bucket entries: epoch << 24 | (op index + 1)
-enum { kAEpoch = 0, kATicket = 1, kADone = 2, kASlow = 3, kADefer = 4, kACtlWords = 64 };
+// control words: [kAAcc, +1] one u64: tickets taken << 40 | the workgroups' range weights summed (ranges are
+// cut in ticket order, each sized by its class's weight); [kAW, +8) the range weight of each workgroup class
+// (blockIdx % 8, one XCD each: 16.16 fixed point, 0 = 1.0), learnt from the previous batch's per-class
+// throughput (the stat records) by uio_aprep_kernel's first workgroup
+enum { kAEpoch = 0, kADone = 2, kASlow = 3, kADefer = 4, kAAcc = 8, kAW = 16, kACtlWords = 64 };
+constexpr uint32_t kAClasses = 8;
+constexpr uint32_t kAOne = 1u << 16;  // weight 1.0
 constexpr uint32_t kADoneVoid = 1u << 12;    // kADone: finished workgroups (low 12 bits) + void reports << 12
 constexpr uint32_t kASpin = 1u << 22;        // bounded look-back spins (about a quarter second)
 
@@ -3178,6 +3186,7 @@ struct AlignedArgs {
   uint2 *defer;                   // blocks whose first op deferred the write-back: {first op, last op}
   uint4 *rec;                     // per op, 2 x 16 bytes (uio_afused_kernel's phase 0 -> 1): new bytes, old bytes
                                   //  (| 1: the block's first op), the block's final bytes, the A6 expectations
+  uint32_t *stat;                 // per ticket (FastScratch): {epoch << 8 | class, ops, wall-clock ticks of its ops}
 };
 
 // An op the aligned sub-branch takes: a fast-branch op (fast_op) that writes one whole 4 KiB block at a
@@ -3209,6 +3218,39 @@ __global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *
   const uint32_t E = aa.ctl[kAEpoch] & 0xFFu;  // (written by the previous batch's last workgroup)
   if (blockIdx.x == 0 && t < kMiscWords) misc[t] = t == kMiscT0 || t == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;
   if (blockIdx.x == 0 && t < kCtrN) ctr[t] = 0;
+  if (blockIdx.x == 0) {  // the workgroup classes' range weights from the previous batch's throughput
+    __shared__ unsigned long long w_ops[kAClasses], w_ticks[kAClasses];
+    if (t < kAClasses) w_ops[t] = w_ticks[t] = 0;
+    __syncthreads();
+    const uint32_t Ep = (E + 0xFFu) & 0xFFu;  // (the previous batch's epoch)
+    for (uint32_t i = t; i < kAGranRows; i += kATile) {
+      const uint32_t a = aa.stat[3 * i];
+      if ((a >> 8) != Ep || (a & 0xFFu) >= kAClasses) continue;
+      atomicAdd(&w_ops[a & 0xFFu], (unsigned long long)aa.stat[3 * i + 1]);
+      atomicAdd(&w_ticks[a & 0xFFu], (unsigned long long)aa.stat[3 * i + 2]);
+    }
+    __syncthreads();
+    if (t == 0) {
+      double rate[kAClasses], mean = 0;
+      uint32_t have = 0;
+      for (uint32_t r = 0; r < kAClasses; ++r) {
+        rate[r] = w_ticks[r] ? (double)w_ops[r] / (double)w_ticks[r] : 0.0;
+        if (rate[r] > 0) {
+          mean += rate[r];
+          ++have;
+        }
+      }
+      if (have == kAClasses) {  // every class measured: w <- (w + rate / mean rate) / 2, within [0.5, 2]
+        mean /= kAClasses;
+        for (uint32_t r = 0; r < kAClasses; ++r) {
+          const uint32_t w0 = aa.ctl[kAW + r] ? aa.ctl[kAW + r] : kAOne;
+          double w = 0.5 * ((double)w0 / kAOne + rate[r] / mean);
+          w = w < 0.5 ? 0.5 : w > 2.0 ? 2.0 : w;
+          aa.ctl[kAW + r] = (uint32_t)(w * kAOne);
+        }
+      }
+    }
+  }
   for (uint32_t e = t; e < 2 * kATile; e += kATile) {
     g_key[e] = kNoKey;
     g_head[e] = kNil;
@@ -3266,14 +3308,30 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     unsigned long long *__restrict__ ctr, uint32_t *hout, h3c_chunk_state *commit, uint32_t force_void) {
   __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
   __shared__ h3c_chunk_state s_cs[kFastChunksLds];
-  __shared__ uint32_t s_ticket, s_E, s_slow, s_last, s_void, s_prev, s_grab;
+  __shared__ uint32_t s_ticket, s_E, s_slow, s_last, s_void, s_prev, s_grab, s_wlo, s_whi;
+  __shared__ uint64_t s_t_start;
   const uint32_t t = threadIdx.x, lane = t & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const uint32_t cls = blockIdx.x % kAClasses;  // (one XCD per class: workgroups are dealt round-robin)
   if (t == 0) {
     s_E = ld_agent(&aa.ctl[kAEpoch]) & 0xFFu;
     s_slow = ld_agent(&aa.ctl[kASlow]);
-    s_ticket = atomicAdd(&aa.ctl[kATicket], 1u);
     s_void = 0;
+    // the ticket and the range: workgroups take tickets in order, and ticket L's range is the next slice
+    // of the batch, sized by its class's weight (a slower XCD gets fewer ops)
+    uint64_t wt = 0, wmine = 0;
+    for (uint32_t r = 0; r < kAClasses; ++r) {
+      const uint32_t w = aa.ctl[kAW + r] ? aa.ctl[kAW + r] : kAOne;
+      const uint32_t cnt = gridDim.x > r ? (gridDim.x - 1 - r) / kAClasses + 1 : 0u;
+      wt += (uint64_t)cnt * w;
+      if (r == cls) wmine = w;
+    }
+    const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long *>(aa.ctl + kAAcc),
+                                             (1ull << 40) | wmine);
+    const uint64_t cum = old & ((1ull << 40) - 1);
+    s_ticket = (uint32_t)(old >> 40);
+    s_wlo = (uint32_t)(cum * n / wt);
+    s_whi = s_ticket + 1 == gridDim.x ? n : (uint32_t)((cum + wmine) * n / wt);
   }
   if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
   __syncthreads();
@@ -3296,7 +3354,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   // the control words reset for the next batch, the epoch advanced, the outcome words to the host
   auto finish = [&](uint32_t outcome) {
     if (t == 0) {
-      st_agent(&aa.ctl[kATicket], 0u);
+      st_agent(reinterpret_cast<unsigned long long *>(aa.ctl + kAAcc), 0ull);
       st_agent(&aa.ctl[kADone], 0u);
       st_agent(&aa.ctl[kAEpoch], (E + 1) & 0xFFu);
       misc[kMiscFast] = outcome;
@@ -3312,7 +3370,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   }
   const uint32_t k4096 = dgf_mul(0xFFFFFFFFu, pc->pow8[12], poly);  // ~0 * x^(8 * 4096)
   // the workgroup's ops [wlo, whi) (ticket order) and, for the prefix, each wave's contiguous share
-  const uint32_t wlo = (uint32_t)((uint64_t)L * n / nwg), whi = (uint32_t)((uint64_t)(L + 1) * n / nwg);
+  const uint32_t wlo = s_wlo, whi = s_whi;
   const uint32_t wn_ops = whi - wlo;
   const uint32_t lo = wlo + (uint32_t)((uint64_t)wave * wn_ops / kBlkWaves);
   const uint32_t hi = wlo + (uint32_t)((uint64_t)(wave + 1) * wn_ops / kBlkWaves);
@@ -3372,6 +3430,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   if (t == 0) s_grab = wlo + kBlkWaves;  // (each wave's first op is wlo + wave)
   stores_done();
   __syncthreads();
+  if (t == 0) s_t_start = wall_clock64();
 #if H3C_AF_TRACE
   if (t == 0 && L < 1024) g_af_wg[5 * L + 1] = wall_clock64();
 #endif
@@ -3493,6 +3552,12 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   if (wave_void && lane == 0) atomicOr(&s_void, 1u);
   stores_done();
   __syncthreads();  // every op of the workgroup published (the CRC tables are done with: their LDS is free)
+  if (t == 0 && L < kAGranRows) {  // this workgroup's throughput, for the next batch's range weights
+    const uint64_t t1 = wall_clock64();
+    aa.stat[3 * L] = (E << 8) | cls;
+    aa.stat[3 * L + 1] = whi - wlo;
+    aa.stat[3 * L + 2] = (uint32_t)(t1 - s_t_start);
+  }
 #if H3C_AF_TRACE
   if (t == 0 && L < 1024) g_af_wg[5 * L + 2] = wall_clock64();
 #endif
@@ -3552,7 +3617,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
       if (lane < nchunks) st_agent(&row[lane], agran(E, 1u, a0));
       if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], agran(E, 1u, a1));
       int j0 = lane < nchunks ? (int)L - 1 : -1, j1 = two && lane + 64 < nchunks ? (int)L - 1 : -1;
-      const uint32_t limit = force_void && L == 1 ? 0u : kASpin;  // (test hook: ticket 1 gives up at once)
+      const uint32_t limit = (force_void & 1) && L == 1 ? 0u : kASpin;  // (test hook: ticket 1 gives up at once)
       for (uint32_t spins = 0; __builtin_amdgcn_ballot_w64(j0 >= 0 || j1 >= 0) != 0;) {
         bool moved = false;
         auto look = [&](int &j, uint32_t &x, uint32_t col) {
@@ -4315,7 +4380,7 @@ struct ArgLayout<AlignedArgs, void> {
     struct_arg<AlignedArgs>(a, {offsetof(AlignedArgs, ctl), offsetof(AlignedArgs, head), offsetof(AlignedArgs, gran),
                                 offsetof(AlignedArgs, key), offsetof(AlignedArgs, link), offsetof(AlignedArgs, dv),
                                 offsetof(AlignedArgs, pv), offsetof(AlignedArgs, inp), offsetof(AlignedArgs, defer),
-                                offsetof(AlignedArgs, rec)});
+                                offsetof(AlignedArgs, rec), offsetof(AlignedArgs, stat)});
   }
 };
 template <>
@@ -4852,6 +4917,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     fa.head = fsc->p + kScratchHeads;
     aa.ctl = fsc->p + kScratchACtl;
     aa.gran = reinterpret_cast<unsigned long long *>(fsc->p + kScratchAGran);
+    aa.stat = fsc->p + kScratchAStat;
     aa.head = fsc->p + kScratchHeads + hcap_fast;
     aa.hmask = hcap_fast - 1;
     aa.key = fa.key;
@@ -4878,7 +4944,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       const uint64_t per = ((uint64_t)n + (uint64_t)nwg_a * kBlkWaves - 1) / ((uint64_t)nwg_a * kBlkWaves);
       nwg_a = (uint32_t)std::max<uint64_t>(1, ((uint64_t)n + per * kBlkWaves - 1) / (per * kBlkWaves));
     }
-    const uint32_t force_void = (giveup & 8) ? 1u : 0u;  // (test hook H3C_HOOK_UPD_GIVEUP bit 3)
+    // (test hook H3C_HOOK_UPD_GIVEUP bit 3: ticket 1 gives up its look-back; bit 4: the pass reports itself void)
+    const uint32_t force_void = ((giveup & 8) ? 1u : 0u) | ((giveup & 16) ? 2u : 0u);
     auto a_launch = [&](hipStream_t q) -> int {
       hipLaunchKernelGGL(uio_aprep_kernel, dim3((n + kATile - 1) / kATile), dim3(kATile), 0, q, d_ios, n, d_chunks,
                          nchunks, poly_type, stdf, d_misc, d_ctr, aa);

@@ -57,6 +57,12 @@ def check_modes(h3c, hooks, sc, expect_aligned=True, recovered=None, **kw):
     else:
         assert ad["aligned_batches"] == 0 and ad["aligned_abandoned"] == 1, ad
     assert out["fast"][4]["aligned_batches"] == 0 and out["general"][4]["fast_batches"] == 0
+    # each mode against the oracle's results first (names the mode that is wrong)
+    for m in ("aligned", "fast", "general"):
+        mr = out[m][1]
+        bad = [i for i, e in enumerate(sc.expect) if (int(mr["status"][i]), int(mr["value"][i])) !=
+               (e["status"], e["value"] & 0xFFFFFFFF)]
+        assert not bad, (m, len(bad), bad[:5])
     ac, ar, ak, ab, _ = out["aligned"]
     for other in ("fast", "general"):
         oc, orr, ok, ob, _ = out[other]
