@@ -47,7 +47,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -121,6 +123,21 @@ __global__ void upd_keys_kernel(const uint32_t *__restrict__ blk_chunk, const ui
 // stays short even when every write hammers one slot.  (A returning atomicCAS costs about
 // twice an atomicExch here: scripts/atomic_probe.hip.)
 constexpr uint32_t kLinkTile = 256;
+// control words (the workspace's, zeroed per call; or the stream's UpdScratch, left reset by each batch's last
+// workgroup): [kCtlEpoch] the scratch's batch epoch (8 bits; 0 in a zeroed workspace)
+enum { kCtlTicket = 0, kCtlErr = 1, kCtlTimeout = 2, kCtlDone = 3, kCtlEpoch = 4, kCtlWords = 64 };
+// Hash list entries: op index + 1 (0 ends a list) in a zeroed workspace; in an UpdScratch (`tagged`: never
+// cleared between batches) epoch << 24 | (op index + 1), so an entry of an earlier batch ends the list.
+constexpr uint32_t kTaggedMaxOps = (1u << 24) - 2;
+__device__ __forceinline__ uint32_t hentry(uint32_t i, uint32_t E, uint32_t tagged) {
+  return tagged ? (E << 24) | (i + 1) : i + 1;
+}
+__device__ __forceinline__ bool hvalid(uint32_t e, uint32_t E, uint32_t tagged) {
+  return tagged ? (e >> 24) == E && (e & 0xFFFFFFu) != 0 : e != 0;
+}
+__device__ __forceinline__ uint32_t hindex(uint32_t e, uint32_t tagged) { return (tagged ? e & 0xFFFFFFu : e) - 1; }
+// a chunk some write of batch E reaches (a zeroed word never matches)
+__device__ __forceinline__ uint32_t touch_mark(uint32_t E) { return 0x100u | E; }
 
 __device__ __forceinline__ uint32_t slot_hash(uint32_t key, uint32_t mask) { return (key * 0x9E3779B1u >> 7) & mask; }
 
@@ -159,19 +176,21 @@ __global__ __launch_bounds__(kLinkTile) void upd_tlink_kernel(const uint32_t *__
                                                               uint32_t nchunks, uint32_t bpc, uint32_t *hhead,
                                                               uint32_t hmask, uint32_t *__restrict__ nkey,
                                                               uint32_t *__restrict__ next, uint32_t *__restrict__ prev,
-                                                              uint32_t *__restrict__ err, uint32_t *__restrict__ touched) {
+                                                              uint32_t *ctl, uint32_t *__restrict__ touched,
+                                                              uint32_t tagged) {
   __shared__ TileGroups<kLinkTile> g;
   const uint32_t t = threadIdx.x, i0 = blockIdx.x * kLinkTile, i = i0 + t;
+  const uint32_t E = ctl[kCtlEpoch] & 0xFFu;  // (0 in a zeroed workspace)
   uint32_t key = kNone;
   if (i < n) {
     const uint32_t c = blk_chunk[i], b = blk_index[i];
     if (c < nchunks && b < bpc) {
       key = c * bpc + b;
-      touched[c] = 1u;  // chunks no write reaches keep their stored checksum
+      touched[c] = touch_mark(E);  // chunks no write reaches keep their stored checksum
     }
   }
   const int ninv = __syncthreads_count(i < n && key == kNone);  // out-of-range entries
-  if (t == 0 && ninv) atomicAdd(err, (uint32_t)ninv);
+  if (t == 0 && ninv) atomicAdd(&ctl[kCtlErr], (uint32_t)ninv);
   const uint32_t head = tile_group(g, t, key);
   uint32_t pin = kNone;
   bool last = true;
@@ -182,7 +201,7 @@ __global__ __launch_bounds__(kLinkTile) void upd_tlink_kernel(const uint32_t *__
   if (i < n) prev[i] = pin == kNone ? kNone : i0 + pin;
   if (key != kNone && last) {  // push i on its bucket's list (entries are index + 1; 0 ends a list)
     nkey[i] = key;
-    next[i] = atomicExch(&hhead[slot_hash(key, hmask)], i + 1);
+    next[i] = atomicExch(&hhead[slot_hash(key, hmask)], hentry(i, E, tagged));
   }
 }
 
@@ -401,12 +420,16 @@ constexpr uint32_t kGranAgg = 1, kGranIncl = 2;
 #endif
 constexpr uint32_t kLookWin = H3C_UPD_LOOK_WIN;  // look-back rows read per column per round trip
 constexpr uint32_t kSpinLimit = 1u << 22;  // bounded look-back spins (about a quarter second)
-enum { kCtlTicket = 0, kCtlErr = 1, kCtlTimeout = 2, kCtlDone = 3, kCtlWords = 64 };
 typedef unsigned long long __attribute__((address_space(1))) gu64;
 
-__device__ __forceinline__ void gran_store(uint64_t *p, uint32_t state, uint32_t v) {
-  __hip_atomic_store((gu64 *)p, ((unsigned long long)state << 32) | v, __ATOMIC_RELAXED,
+// granules: {epoch << 8 | state, value} (state 0: not published in batch E; a zeroed row never matches)
+__device__ __forceinline__ void gran_store(uint64_t *p, uint32_t E, uint32_t state, uint32_t v) {
+  __hip_atomic_store((gu64 *)p, ((unsigned long long)((E << 8) | state) << 32) | v, __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t gran_state(uint64_t g, uint32_t E) {
+  const uint32_t hi = (uint32_t)(g >> 32);
+  return (hi >> 8) == E ? (hi & 3u) : 0u;
 }
 __device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
   return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -431,13 +454,16 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     const uint32_t *__restrict__ raw_base, const uint32_t *__restrict__ raw_in, uint32_t exact, uint32_t reuse_case,
     const uint32_t *__restrict__ touched, uint32_t *ctl, uint64_t *gran, uint32_t *__restrict__ inpre,
     uint32_t *__restrict__ out_raw, uint32_t *__restrict__ raw_out, uint32_t *__restrict__ n_invalid,
-    unsigned long long *__restrict__ counters, uint32_t force_timeout) {
+    unsigned long long *__restrict__ counters, uint32_t force_timeout, uint32_t tagged) {
   constexpr uint32_t G4 = 4096;
   __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
-  __shared__ uint32_t s_ticket;
-  if (threadIdx.x == 0) s_ticket = (H3C_UPD_EXPERIMENT & 128) ? blockIdx.x : atomicAdd(&ctl[kCtlTicket], 1u);
+  __shared__ uint32_t s_ticket, s_E;
+  if (threadIdx.x == 0) {
+    s_ticket = (H3C_UPD_EXPERIMENT & 128) ? blockIdx.x : atomicAdd(&ctl[kCtlTicket], 1u);
+    s_E = __hip_atomic_load(&ctl[kCtlEpoch], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFFu;
+  }
   __syncthreads();
-  const uint32_t L = s_ticket, nwg = gridDim.x;
+  const uint32_t L = s_ticket, nwg = gridDim.x, E = s_E;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)L * kWavesPerBlock + wave;
@@ -488,8 +514,8 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     // the walk over the slot's listed tile-last writers, while those rows load
     if (key != kNone) {
       uint32_t p = kNone, fmax = k;
-      for (uint32_t e = hhead[slot_hash(key, hmask)]; e != 0; e = next[e - 1]) {
-        const uint32_t j = e - 1;
+      for (uint32_t e = hhead[slot_hash(key, hmask)]; hvalid(e, E, tagged); e = next[hindex(e, tagged)]) {
+        const uint32_t j = hindex(e, tagged);
         if (nkey[j] != key) continue;
         if (j < k && (p == kNone || j > p)) p = j;
         fmax = max(fmax, j);
@@ -602,8 +628,8 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     uint64_t *row = gran + (uint64_t)L * kFusedCols;
     uint32_t x0 = 0, x1 = 0;
     if (L > 0 && !(H3C_UPD_EXPERIMENT & 32)) {  // (experiment bit5: no look-back)
-      if (lane < nchunks) gran_store(row + lane, kGranAgg, a0);
-      if (two && lane + 64 < nchunks) gran_store(row + 64 + lane, kGranAgg, a1);
+      if (lane < nchunks) gran_store(row + lane, E, kGranAgg, a0);
+      if (two && lane + 64 < nchunks) gran_store(row + 64 + lane, E, kGranAgg, a1);
       int j0 = lane < nchunks ? (int)L - 1 : -1, j1 = two && lane + 64 < nchunks ? (int)L - 1 : -1;
       // test hook (H3C_HOOK_UPD_LOOKBACK): ticket 1 gives up at once, as a starved wait would
       const uint32_t limit = force_timeout && L == 1 ? 0u : kSpinLimit;
@@ -620,7 +646,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
             g[w] = top - w >= 0 ? gran_load(gran + (uint64_t)(top - w) * kFusedCols + col) : 0ull;
 #pragma unroll
           for (int w = 0; w < (int)kLookWin; ++w) {
-            const uint32_t state = (uint32_t)(g[w] >> 32);
+            const uint32_t state = gran_state(g[w], E);
             if (top - w >= 0 && j == top - w && state) {
               x ^= (uint32_t)g[w];
               j = state == kGranIncl ? -1 : j - 1;
@@ -640,8 +666,8 @@ __device__ __forceinline__ void upd_fused_kernel_body(
         }
       }
     }
-    if (lane < nchunks) gran_store(row + lane, kGranIncl, x0 ^ a0);
-    if (two && lane + 64 < nchunks) gran_store(row + 64 + lane, kGranIncl, x1 ^ a1);
+    if (lane < nchunks) gran_store(row + lane, E, kGranIncl, x0 ^ a0);
+    if (two && lane + 64 < nchunks) gran_store(row + 64 + lane, E, kGranIncl, x1 ^ a1);
     wexcl[lane] = x0;
     wexcl[64 + lane] = x1;
     // every workgroup but the last counts itself done once its flag (if it gave up) is out: the last
@@ -654,11 +680,11 @@ __device__ __forceinline__ void upd_fused_kernel_body(
       const uint32_t t0 = x0 ^ a0, t1 = x1 ^ a1;
       uint32_t stale = 0;
       if (lane < nchunks) {
-        raw_out[lane] = touched[lane] ? raw_base[lane] ^ t0 : raw_in[lane];
+        raw_out[lane] = touched[lane] == touch_mark(E) ? raw_base[lane] ^ t0 : raw_in[lane];
         stale += exact && raw_base[lane] != raw_in[lane];
       }
       if (lane + 64 < nchunks) {
-        raw_out[64 + lane] = touched[64 + lane] ? raw_base[64 + lane] ^ t1 : raw_in[64 + lane];
+        raw_out[64 + lane] = touched[64 + lane] == touch_mark(E) ? raw_base[64 + lane] ^ t1 : raw_in[64 + lane];
         stale += exact && raw_base[64 + lane] != raw_in[64 + lane];
       }
       for (int o = 32; o >= 1; o >>= 1) stale += __shfl_xor(stale, o, 64);
@@ -692,6 +718,13 @@ __device__ __forceinline__ void upd_fused_kernel_body(
           counters[6] = void_batch ? ~0ull : inv;
           counters[7] = stale;
         }
+        // the control words back to their batch-start values for the next batch on this scratch (the
+        // subtractions are exact even when a late workgroup counts itself done after this), the epoch on
+        if (!(H3C_UPD_EXPERIMENT & 128)) atomicSub(&ctl[kCtlTicket], nwg);
+        atomicSub(&ctl[kCtlDone], nwg - 1);
+        atomicSub(&ctl[kCtlErr], inv);
+        atomicExch(&ctl[kCtlTimeout], 0u);
+        __hip_atomic_store(&ctl[kCtlEpoch], (E + 1) & 0xFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -727,10 +760,10 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
     const uint32_t *__restrict__ raw_base, const uint32_t *__restrict__ raw_in, uint32_t exact, uint32_t reuse_case,
     const uint32_t *__restrict__ touched, uint32_t *ctl, uint64_t *gran, uint32_t *__restrict__ inpre,
     uint32_t *__restrict__ out_raw, uint32_t *__restrict__ raw_out, uint32_t *__restrict__ n_invalid,
-    unsigned long long *__restrict__ counters, uint32_t force_timeout,
+    unsigned long long *__restrict__ counters, uint32_t force_timeout, uint32_t tagged,
                                                              unsigned long long *ts) {  // ts: h3c_rt::prof_stamp's slot, or nullptr
   stamp_begin(ts);
-  upd_fused_kernel_body(chunk_base, nchunks, bpc, blk_chunk, blk_index, payload, n, prev, hhead, hmask, nkey, next, sh, pc, raw_base, raw_in, exact, reuse_case, touched, ctl, gran, inpre, out_raw, raw_out, n_invalid, counters, force_timeout);
+  upd_fused_kernel_body(chunk_base, nchunks, bpc, blk_chunk, blk_index, payload, n, prev, hhead, hmask, nkey, next, sh, pc, raw_base, raw_in, exact, reuse_case, touched, ctl, gran, inpre, out_raw, raw_out, n_invalid, counters, force_timeout, tagged);
   stamp_end(ts);
 }
 
@@ -1036,6 +1069,88 @@ int shift_table(int dev, uint8_t type, uint64_t chunk_len, uint32_t block_bytes,
   return H3C_OK;
 }
 
+// ---- the fused path's per-stream scratch (no per-call memset) ----
+// The control words, touched marks, look-back granules and hash heads of the fused path, owned by the
+// library per (device, stream) instead of zeroed in the caller's workspace by a memset per call: hash
+// entries, touched marks and granules carry the batch's 8-bit epoch (an entry of an earlier batch reads
+// as absent), and the batch's last workgroup puts the control words back and advances the epoch.  The
+// scratch is zeroed when it is new, re-laid out (another hash size), suspect (a call failed between its
+// launches) or 240 batches on (before the epoch wraps onto live rows).  One call at a time enqueues on a
+// scratch (its mutex), so calls from several threads on one stream stay whole; calls on different
+// streams use different scratches.  A call being captured into a graph, or one with more than
+// kTaggedMaxOps writes, uses its workspace and the memset as before.
+#ifndef H3C_UPD_SCRATCH
+#define H3C_UPD_SCRATCH 1
+#endif
+constexpr uint32_t kUsCtl = 0, kUsTouched = kCtlWords, kUsGran = kUsTouched + kFusedCols;
+constexpr uint32_t kUsHeads = kUsGran + 2 * kFusedCols * kFusedMaxWG;
+constexpr uint32_t kUsBatches = 240;
+constexpr size_t kUsMaxScratches = 64;
+struct UpdScratch {
+  int dev = -1;
+  hipStream_t st = nullptr;
+  std::thread::id tid{};  // (hipStreamPerThread: one stream per thread behind one handle)
+  uint32_t *p = nullptr;
+  size_t words = 0;
+  uint32_t hcap = 0, batches = 0;
+  bool dirty = true;
+  std::mutex mu;
+};
+std::mutex g_us_mu;
+std::vector<std::unique_ptr<UpdScratch>> g_us;
+
+// The scratch for (dev, st), locked by `lk`, laid out for `hcap` hash heads and zeroed on `st` if it must
+// be; nullptr: none (too many streams, or the allocation failed): the caller uses its workspace.
+UpdScratch *upd_scratch(int dev, hipStream_t st, uint32_t hcap, std::unique_lock<std::mutex> &lk) {
+  const std::thread::id tid = st == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id{};
+  UpdScratch *s = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_us_mu);
+    for (auto &x : g_us)
+      if (x->dev == dev && x->st == st && x->tid == tid) s = x.get();
+    if (!s) {
+      if (g_us.size() >= kUsMaxScratches) return nullptr;
+      g_us.emplace_back(new UpdScratch);
+      s = g_us.back().get();
+      s->dev = dev;
+      s->st = st;
+      s->tid = tid;
+    }
+  }
+  lk = std::unique_lock<std::mutex>(s->mu);
+  const size_t words = kUsHeads + (size_t)hcap;
+  if (s->words < words) {
+    if (s->p) {  // (this stream's earlier batches may still use it)
+      if (hipStreamSynchronize(st) != hipSuccess || hipFree(s->p) != hipSuccess) {
+        (void)hipGetLastError();
+        s->p = nullptr;
+        s->words = 0;
+        return nullptr;
+      }
+    }
+    s->p = nullptr;
+    s->words = 0;
+    if (hipMalloc(reinterpret_cast<void **>(&s->p), 4 * words) != hipSuccess) {
+      (void)hipGetLastError();
+      s->p = nullptr;
+      return nullptr;
+    }
+    s->words = words;
+    s->dirty = true;
+  }
+  if (s->dirty || s->hcap != hcap || s->batches >= kUsBatches) {
+    if (hipMemsetAsync(s->p, 0, 4 * (kUsHeads + (size_t)hcap), st) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    s->dirty = false;
+    s->hcap = hcap;
+    s->batches = 0;
+  }
+  ++s->batches;
+  return s;
+}
+
 // H3C_UPD_EXACT: raw_exact[c] = the raw CRC of chunk c's bytes (one create launch).
 int exact_checksums(hipStream_t st, int dev, uint8_t type, const uint64_t *chunk_base, uint32_t nchunks,
                     uint64_t chunk_len, const Workspace &w) {
@@ -1094,10 +1209,36 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
     fused_wg = (uint32_t)std::max<uint64_t>(1, ((uint64_t)n_blocks + per * kWavesPerBlock - 1) / (per * kWavesPerBlock));
   }
 #endif
-  // one memset: hash heads, control words, touched flags and the granule rows in use
-  const size_t zero = path == kPathFused ? (size_t)((char *)(w.gran + (size_t)fused_wg * kFusedCols) - (char *)w.hhead)
-                                         : (size_t)((char *)w.gran - (char *)w.hhead);
-  HIP_TRY(hipMemsetAsync(w.hhead, 0, zero, st));
+  // the fused path's hash heads, control words, touched marks and granules: the stream's UpdScratch, or
+  // one memset of the workspace's (and the granule rows in use)
+  std::unique_lock<std::mutex> us_lock;
+  UpdScratch *us = nullptr;
+  if (H3C_UPD_SCRATCH && path == kPathFused && n_blocks > 0 && n_blocks <= kTaggedMaxOps) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) != hipSuccess) {
+      (void)hipGetLastError();
+      cap = hipStreamCaptureStatusActive;
+    }
+    if (cap == hipStreamCaptureStatusNone) us = upd_scratch(dev, st, w.hcap, us_lock);
+  }
+  const uint32_t tagged = us ? 1u : 0u;
+  if (us) {
+    w.ctl = us->p + kUsCtl;
+    w.touched = us->p + kUsTouched;
+    w.gran = reinterpret_cast<uint64_t *>(us->p + kUsGran);
+    w.hhead = us->p + kUsHeads;
+  } else {
+    const size_t zero = path == kPathFused ? (size_t)((char *)(w.gran + (size_t)fused_wg * kFusedCols) - (char *)w.hhead)
+                                           : (size_t)((char *)w.gran - (char *)w.hhead);
+    HIP_TRY(hipMemsetAsync(w.hhead, 0, zero, st));
+  }
+  // (a failure after the first launch on the scratch leaves it suspect: the next call zeroes it)
+  struct Suspect {
+    UpdScratch *s;
+    ~Suspect() {
+      if (s) s->dirty = true;
+    }
+  } suspect{us};
   const uint32_t *raw_base = chunk_raw_in_dev;
   if (exact) {
     rc = exact_checksums(st, dev, type, chunk_base_dev, nchunks, chunk_len, w);
@@ -1114,7 +1255,7 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
   // previous-writer links: tile match + hash of per-tile last writers (no sort)
   const uint32_t nlt = (n_blocks + kLinkTile - 1) / kLinkTile;
   hipLaunchKernelGGL(upd_tlink_kernel, dim3(nlt), dim3(kLinkTile), 0, st, blk_chunk_dev, blk_index_dev, n_blocks,
-                     nchunks, bpc, w.hhead, w.hcap - 1, w.nkey, w.next, w.prev, w.ctl + kCtlErr, w.touched);
+                     nchunks, bpc, w.hhead, w.hcap - 1, w.nkey, w.next, w.prev, w.ctl, w.touched, tagged);
   HIP_TRY(hipGetLastError());
   const uint32_t *sh = nullptr;
   rc = shift_table(dev, type, chunk_len, block_bytes, pc, w.sh, st, &sh);
@@ -1126,8 +1267,9 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
                        blk_chunk_dev, blk_index_dev, static_cast<const uint8_t *>(payload_dev), n_blocks, w.prev,
                        w.hhead, w.hcap - 1, w.nkey, w.next, sh, pc, raw_base, chunk_raw_in_dev, exact ? 1u : 0u,
                        reuse_case, w.touched, w.ctl, w.gran, w.scan, out_raw_dev, chunk_raw_out_dev, n_invalid_dev,
-                       counters_dev, (uint32_t)(h3c_rt::hook(H3C_HOOK_UPD_LOOKBACK) == 1), tok.ts);
+                       counters_dev, (uint32_t)(h3c_rt::hook(H3C_HOOK_UPD_LOOKBACK) == 1), tagged, tok.ts);
     HIP_TRY(hipGetLastError());
+    suspect.s = nullptr;  // (the batch is enqueued whole: its last workgroup leaves the scratch reset)
     // algorithmic bytes: read new + read old + write back, per block write
     HIP_TRY(h3c_rt::prof_end(st, tok, H3C_PROF_UPDATE, 3ull * block_bytes * n_blocks));
     return H3C_OK;

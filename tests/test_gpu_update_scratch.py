@@ -1,0 +1,146 @@
+"""The block-update fused path's per-stream scratch (h3c_update.hip UpdScratch): no per-call memset.
+
+Hash heads, touched marks and look-back granules carry the batch's 8-bit epoch and are never cleared
+between batches; the last workgroup resets the control words.  These tests run many batches back to
+back on one stream -- sizes that change the hash layout, more batches than the re-zero period (240),
+invalid entries (the error count must not leak into the next batch), a void batch followed by good
+ones, two streams interleaved, and several threads on one stream -- and check every batch against the
+oracle: each chunk's final checksum is the CRC32C of its bytes (oracle C), the last write of each chunk
+reports it, the bytes match a host replay, and the invalid count is exact.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+
+pytestmark = pytest.mark.gpu
+G = 4096
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available()
+    return torch, torch.device("cuda:0")
+
+
+def i32(arr, torch, dev):
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(arr, dtype=np.uint32)).view(np.int32)).to(dev)
+
+
+class Store:
+    """nchunks chunks on the GPU with their host mirror and stored checksums."""
+
+    def __init__(self, torch, dev, rng, nchunks, chunk_len):
+        self.torch, self.dev, self.nchunks, self.chunk_len = torch, dev, nchunks, chunk_len
+        self.host = rng.integers(0, 256, (nchunks, chunk_len), dtype=np.uint8)
+        self.d = torch.from_numpy(self.host.copy()).to(dev)
+        self.bases = torch.tensor([self.d[c].data_ptr() for c in range(nchunks)], dtype=torch.int64, device=dev)
+        self.raw = np.array([orc.crc32c(self.host[c]) for c in range(nchunks)], dtype=np.uint32)
+
+    def batch(self, h3c, rng, n, n_invalid=0, stream=None, check=True):
+        torch, dev = self.torch, self.dev
+        bpc = self.chunk_len // G
+        wc = rng.integers(0, self.nchunks, n).astype(np.uint32)
+        wb = rng.integers(0, bpc, n).astype(np.uint32)
+        bad = rng.choice(n, size=min(n_invalid, n), replace=False) if n_invalid else []
+        for k in bad:
+            wb[k] = bpc + int(rng.integers(0, 5))  # out of range: no effect, counted
+        pay = rng.integers(0, 256, (n, G), dtype=np.uint8)
+        out = torch.zeros(n, dtype=torch.int32, device=dev)
+        raw_out = torch.zeros(self.nchunks, dtype=torch.int32, device=dev)
+        ninv = torch.full((1,), -7, dtype=torch.int32, device=dev)
+        args = (i32(self.raw, torch, dev), i32(wc, torch, dev), i32(wb, torch, dev), torch.from_numpy(pay).to(dev))
+        h3c.update_blocks(self.bases, self.chunk_len, args[0], args[1], args[2], args[3], out, raw_out,
+                          n_invalid=ninv, stream=stream)
+        if stream is not None:
+            stream.synchronize()
+        torch.cuda.synchronize()
+        for k in range(n):
+            if wb[k] < bpc:
+                self.host[wc[k], wb[k] * G:(wb[k] + 1) * G] = pay[k]
+        fin = raw_out.cpu().numpy().view(np.uint32).copy()
+        got = out.cpu().numpy().view(np.uint32)
+        if check:
+            assert int(ninv.item()) == len(bad)
+            want = np.zeros(self.nchunks, dtype=np.uint32)
+            orc.lib().orc_batch_crc32c(self.host.ctypes.data, self.chunk_len, self.nchunks, 0xFFFFFFFF, 8, 0,
+                                       want.ctypes.data)
+            assert np.array_equal(fin, want), np.nonzero(fin != want)[0][:8]
+            for c in range(self.nchunks):
+                ks = np.nonzero((wc == c) & (wb < bpc))[0]
+                if len(ks):
+                    assert int(got[ks[-1]]) == int(want[c]), c
+            assert np.array_equal(self.d.cpu().numpy(), self.host)
+        self.raw = fin
+        return int(ninv.item())
+
+
+def test_scratch_many_batches_sizes_and_invalid(h3c, torch_dev, hooks):
+    """260 batches on one stream (past the 240-batch re-zero), sizes crossing hash-size powers of two
+    (a new layout each time), every fifth batch with invalid entries."""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_SCAN, h3c.UPD_SCAN_PATHS["fused"])
+    rng = np.random.default_rng(501)
+    st = Store(torch, dev, rng, 8, 256 << 10)
+    sizes = [1, 5, 64, 300, 255, 257, 1000, 3000, 511, 513, 2048, 4100]
+    for b in range(260):
+        n = sizes[b % len(sizes)] if b < 36 else int(rng.integers(200, 700))
+        st.batch(h3c, rng, n, n_invalid=(3 if b % 5 == 0 else 0))
+
+
+def test_scratch_void_batch_then_good_batches(h3c, torch_dev, hooks):
+    """A batch whose look-back gives up (H3C_HOOK_UPD_LOOKBACK) reports void; the next batches on the
+    same scratch are exact (the timeout flag and the counts were put back)."""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_SCAN, h3c.UPD_SCAN_PATHS["fused"])
+    rng = np.random.default_rng(502)
+    st = Store(torch, dev, rng, 8, 256 << 10)
+    st.batch(h3c, rng, 3000)
+    hooks(h3c.HOOK_UPD_LOOKBACK, 1)
+    assert st.batch(h3c, rng, 20000, check=False) == -1
+    hooks(h3c.HOOK_UPD_LOOKBACK, 0)
+    st.raw = np.array([orc.crc32c(st.host[c]) for c in range(st.nchunks)], dtype=np.uint32)  # recomputed
+    for n in (20000, 3000, 20000):
+        st.batch(h3c, rng, n, n_invalid=2)
+
+
+def test_scratch_two_streams_interleaved(h3c, torch_dev, hooks):
+    """Two streams (two scratches), batches alternating between them on disjoint chunk sets."""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_SCAN, h3c.UPD_SCAN_PATHS["fused"])
+    rng = np.random.default_rng(503)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    stores = [Store(torch, dev, rng, 4, 128 << 10), Store(torch, dev, rng, 6, 128 << 10)]
+    for b in range(40):
+        k = b % 2
+        stores[k].batch(h3c, rng, int(rng.integers(1, 2500)), n_invalid=b % 3, stream=streams[k])
+
+
+def test_scratch_threads_on_one_stream(h3c, torch_dev, hooks):
+    """Four threads issue batches on the same (default) stream without waiting on each other: each
+    call's launches are enqueued whole, so each thread's chunks end exact."""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_SCAN, h3c.UPD_SCAN_PATHS["fused"])
+    seeds = np.random.SeedSequence(504).spawn(4)
+    stores = [Store(torch, dev, np.random.default_rng(s), 4, 128 << 10) for s in seeds]
+    errors = []
+
+    def work(i):
+        try:
+            torch.cuda.set_device(dev)
+            rng = np.random.default_rng(seeds[i])
+            for _ in range(12):
+                stores[i].batch(h3c, rng, int(rng.integers(100, 3000)), n_invalid=1)
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append((i, repr(e)))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
