@@ -125,7 +125,12 @@ __global__ void upd_keys_kernel(const uint32_t *__restrict__ blk_chunk, const ui
 constexpr uint32_t kLinkTile = 256;
 // control words (the workspace's, zeroed per call; or the stream's UpdScratch, left reset by each batch's last
 // workgroup): [kCtlEpoch] the scratch's batch epoch (8 bits; 0 in a zeroed workspace)
-enum { kCtlTicket = 0, kCtlErr = 1, kCtlTimeout = 2, kCtlDone = 3, kCtlEpoch = 4, kCtlWords = 64 };
+// [kCtlAcc, +1] one u64: the fused kernel's tickets taken << 40 | the range weights summed; [kCtlW, +8) each
+// workgroup class's range weight (blockIdx % 8, one XCD each; 16.16 fixed point, 0 = 1.0), learnt by
+// upd_tlink_kernel from the previous batch's per-ticket throughput records (UpdScratch only)
+enum { kCtlErr = 1, kCtlTimeout = 2, kCtlDone = 3, kCtlEpoch = 4, kCtlAcc = 8, kCtlW = 16, kCtlWords = 64 };
+constexpr uint32_t kClasses = 8;
+constexpr uint32_t kWOne = 1u << 16;  // weight 1.0
 // Hash list entries: op index + 1 (0 ends a list) in a zeroed workspace; in an UpdScratch (`tagged`: never
 // cleared between batches) epoch << 24 | (op index + 1), so an entry of an earlier batch ends the list.
 constexpr uint32_t kTaggedMaxOps = (1u << 24) - 2;
@@ -177,10 +182,44 @@ __global__ __launch_bounds__(kLinkTile) void upd_tlink_kernel(const uint32_t *__
                                                               uint32_t hmask, uint32_t *__restrict__ nkey,
                                                               uint32_t *__restrict__ next, uint32_t *__restrict__ prev,
                                                               uint32_t *ctl, uint32_t *__restrict__ touched,
-                                                              uint32_t tagged) {
+                                                              uint32_t tagged, const uint32_t *__restrict__ stat,
+                                                              uint32_t nstat) {
   __shared__ TileGroups<kLinkTile> g;
   const uint32_t t = threadIdx.x, i0 = blockIdx.x * kLinkTile, i = i0 + t;
   const uint32_t E = ctl[kCtlEpoch] & 0xFFu;  // (0 in a zeroed workspace)
+  if (stat && blockIdx.x == 0) {  // the fused kernel's range weights from the previous batch's throughput
+    __shared__ unsigned long long w_ops[kClasses], w_ticks[kClasses];
+    if (t < kClasses) w_ops[t] = w_ticks[t] = 0;
+    __syncthreads();
+    const uint32_t Ep = (E + 0xFFu) & 0xFFu;  // (the previous batch's epoch)
+    for (uint32_t r = t; r < nstat; r += kLinkTile) {
+      const uint32_t a = stat[3 * r];
+      if ((a >> 8) != Ep || (a & 0xFFu) >= kClasses) continue;
+      atomicAdd(&w_ops[a & 0xFFu], (unsigned long long)stat[3 * r + 1]);
+      atomicAdd(&w_ticks[a & 0xFFu], (unsigned long long)stat[3 * r + 2]);
+    }
+    __syncthreads();
+    if (t == 0) {
+      double rate[kClasses], mean = 0;
+      uint32_t have = 0;
+      for (uint32_t c = 0; c < kClasses; ++c) {
+        rate[c] = w_ticks[c] ? (double)w_ops[c] / (double)w_ticks[c] : 0.0;
+        if (rate[c] > 0) {
+          mean += rate[c];
+          ++have;
+        }
+      }
+      if (have == kClasses) {  // every class measured: w <- (w + rate / mean rate) / 2, within [0.5, 2]
+        mean /= kClasses;
+        for (uint32_t c = 0; c < kClasses; ++c) {
+          const uint32_t w0 = ctl[kCtlW + c] ? ctl[kCtlW + c] : kWOne;
+          double w = 0.5 * ((double)w0 / kWOne + rate[c] / mean);
+          w = w < 0.5 ? 0.5 : w > 2.0 ? 2.0 : w;
+          ctl[kCtlW + c] = (uint32_t)(w * kWOne);
+        }
+      }
+    }
+  }
   uint32_t key = kNone;
   if (i < n) {
     const uint32_t c = blk_chunk[i], b = blk_index[i];
@@ -454,21 +493,39 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     const uint32_t *__restrict__ raw_base, const uint32_t *__restrict__ raw_in, uint32_t exact, uint32_t reuse_case,
     const uint32_t *__restrict__ touched, uint32_t *ctl, uint64_t *gran, uint32_t *__restrict__ inpre,
     uint32_t *__restrict__ out_raw, uint32_t *__restrict__ raw_out, uint32_t *__restrict__ n_invalid,
-    unsigned long long *__restrict__ counters, uint32_t force_timeout, uint32_t tagged) {
+    unsigned long long *__restrict__ counters, uint32_t force_timeout, uint32_t tagged, uint32_t *stat) {
   constexpr uint32_t G4 = 4096;
   __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
-  __shared__ uint32_t s_ticket, s_E;
+  __shared__ uint32_t s_ticket, s_E, s_wlo, s_whi;
+  __shared__ uint64_t s_wt, s_t0;
+  const uint32_t cls = blockIdx.x % kClasses;  // (workgroups are dealt round-robin over the 8 XCDs)
   if (threadIdx.x == 0) {
-    s_ticket = (H3C_UPD_EXPERIMENT & 128) ? blockIdx.x : atomicAdd(&ctl[kCtlTicket], 1u);
+    // the ticket and the range: workgroups take tickets in order, and ticket L's range is the next slice
+    // of the batch, sized by its class's weight (a slower XCD gets fewer writes)
+    uint64_t wt = 0, wmine = 0;
+    for (uint32_t c = 0; c < kClasses; ++c) {
+      const uint32_t w = ctl[kCtlW + c] ? ctl[kCtlW + c] : kWOne;
+      const uint32_t cnt = gridDim.x > c ? (gridDim.x - 1 - c) / kClasses + 1 : 0u;
+      wt += (uint64_t)cnt * w;
+      if (c == cls) wmine = w;
+    }
+    const unsigned long long old =
+        (H3C_UPD_EXPERIMENT & 128) ? ((unsigned long long)blockIdx.x << 40) | (blockIdx.x * wmine)
+                                   : atomicAdd(reinterpret_cast<unsigned long long *>(ctl + kCtlAcc), (1ull << 40) | wmine);
+    const uint64_t cum = old & ((1ull << 40) - 1);
+    s_ticket = (uint32_t)(old >> 40);
+    s_wt = wt;
+    s_wlo = (uint32_t)(cum * n / wt);
+    s_whi = s_ticket + 1 == gridDim.x ? n : (uint32_t)((cum + wmine) * n / wt);
     s_E = __hip_atomic_load(&ctl[kCtlEpoch], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFFu;
   }
   __syncthreads();
   const uint32_t L = s_ticket, nwg = gridDim.x, E = s_E;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t gw = (uint64_t)L * kWavesPerBlock + wave;
-  const uint64_t nw = (uint64_t)nwg * kWavesPerBlock;
-  const uint32_t lo = (uint32_t)(gw * n / nw), hi = (uint32_t)((gw + 1) * n / nw);
+  const uint32_t wlo = s_wlo, wn = s_whi - s_wlo;  // the workgroup's writes; each wave a contiguous share
+  const uint32_t lo = wlo + (uint32_t)((uint64_t)wave * wn / kWavesPerBlock);
+  const uint32_t hi = wlo + (uint32_t)((uint64_t)(wave + 1) * wn / kWavesPerBlock);
   const uint64_t lo16 = 16u * lane;
   const uint64_t pay = (uint64_t)(uintptr_t)payload;
   auto rl64 = [](uint64_t v, uint32_t t) -> uint64_t {
@@ -538,6 +595,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
   if (lo < hi) start_group(lo);  // the first group's links and rows load while the tables fill
   fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kThreads);
   __syncthreads();
+  if (threadIdx.x == 0) s_t0 = wall_clock64();
   const uint32_t *red = lds + kLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
   const LaneLut Lt = make_lut(lane);
@@ -613,6 +671,11 @@ __device__ __forceinline__ void upd_fused_kernel_body(
   if (H3C_UPD_EXPERIMENT & 8) return;  // timing experiment: no aggregation / look-back / out_raw
   // ---- chunk aggregates: waves of the workgroup (LDS), then workgroups (look-back) ----
   __syncthreads();  // the CRC tables are done with: their LDS holds the aggregates now
+  if (stat && threadIdx.x == 0 && L < kFusedMaxWG) {  // this workgroup's throughput, for the next batch's weights
+    stat[3 * L] = (E << 8) | cls;
+    stat[3 * L + 1] = wn;
+    stat[3 * L + 2] = (uint32_t)(wall_clock64() - s_t0);
+  }
   uint32_t *wagg = lds;                               // [16][128]
   uint32_t *wexcl = lds + kWavesPerBlock * kFusedCols;  // [128]: the workgroup's exclusive prefix
   wagg[wave * kFusedCols + lane] = acc0;
@@ -720,7 +783,8 @@ __device__ __forceinline__ void upd_fused_kernel_body(
         }
         // the control words back to their batch-start values for the next batch on this scratch (the
         // subtractions are exact even when a late workgroup counts itself done after this), the epoch on
-        if (!(H3C_UPD_EXPERIMENT & 128)) atomicSub(&ctl[kCtlTicket], nwg);
+        if (!(H3C_UPD_EXPERIMENT & 128))
+          atomicAdd(reinterpret_cast<unsigned long long *>(ctl + kCtlAcc), 0ull - (((unsigned long long)nwg << 40) + s_wt));
         atomicSub(&ctl[kCtlDone], nwg - 1);
         atomicSub(&ctl[kCtlErr], inv);
         atomicExch(&ctl[kCtlTimeout], 0u);
@@ -760,10 +824,10 @@ __global__ __launch_bounds__(kThreads) void upd_fused_kernel(
     const uint32_t *__restrict__ raw_base, const uint32_t *__restrict__ raw_in, uint32_t exact, uint32_t reuse_case,
     const uint32_t *__restrict__ touched, uint32_t *ctl, uint64_t *gran, uint32_t *__restrict__ inpre,
     uint32_t *__restrict__ out_raw, uint32_t *__restrict__ raw_out, uint32_t *__restrict__ n_invalid,
-    unsigned long long *__restrict__ counters, uint32_t force_timeout, uint32_t tagged,
+    unsigned long long *__restrict__ counters, uint32_t force_timeout, uint32_t tagged, uint32_t *stat,
                                                              unsigned long long *ts) {  // ts: h3c_rt::prof_stamp's slot, or nullptr
   stamp_begin(ts);
-  upd_fused_kernel_body(chunk_base, nchunks, bpc, blk_chunk, blk_index, payload, n, prev, hhead, hmask, nkey, next, sh, pc, raw_base, raw_in, exact, reuse_case, touched, ctl, gran, inpre, out_raw, raw_out, n_invalid, counters, force_timeout, tagged);
+  upd_fused_kernel_body(chunk_base, nchunks, bpc, blk_chunk, blk_index, payload, n, prev, hhead, hmask, nkey, next, sh, pc, raw_base, raw_in, exact, reuse_case, touched, ctl, gran, inpre, out_raw, raw_out, n_invalid, counters, force_timeout, tagged, stat);
   stamp_end(ts);
 }
 
@@ -1083,7 +1147,8 @@ int shift_table(int dev, uint8_t type, uint64_t chunk_len, uint32_t block_bytes,
 #define H3C_UPD_SCRATCH 1
 #endif
 constexpr uint32_t kUsCtl = 0, kUsTouched = kCtlWords, kUsGran = kUsTouched + kFusedCols;
-constexpr uint32_t kUsHeads = kUsGran + 2 * kFusedCols * kFusedMaxWG;
+constexpr uint32_t kUsStat = kUsGran + 2 * kFusedCols * kFusedMaxWG;  // per ticket: {epoch << 8 | class, writes, ticks}
+constexpr uint32_t kUsHeads = kUsStat + 3 * kFusedMaxWG;
 constexpr uint32_t kUsBatches = 240;
 constexpr size_t kUsMaxScratches = 64;
 struct UpdScratch {
@@ -1255,7 +1320,8 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
   // previous-writer links: tile match + hash of per-tile last writers (no sort)
   const uint32_t nlt = (n_blocks + kLinkTile - 1) / kLinkTile;
   hipLaunchKernelGGL(upd_tlink_kernel, dim3(nlt), dim3(kLinkTile), 0, st, blk_chunk_dev, blk_index_dev, n_blocks,
-                     nchunks, bpc, w.hhead, w.hcap - 1, w.nkey, w.next, w.prev, w.ctl, w.touched, tagged);
+                     nchunks, bpc, w.hhead, w.hcap - 1, w.nkey, w.next, w.prev, w.ctl, w.touched, tagged,
+                     us ? us->p + kUsStat : nullptr, kFusedMaxWG);
   HIP_TRY(hipGetLastError());
   const uint32_t *sh = nullptr;
   rc = shift_table(dev, type, chunk_len, block_bytes, pc, w.sh, st, &sh);
@@ -1267,7 +1333,8 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
                        blk_chunk_dev, blk_index_dev, static_cast<const uint8_t *>(payload_dev), n_blocks, w.prev,
                        w.hhead, w.hcap - 1, w.nkey, w.next, sh, pc, raw_base, chunk_raw_in_dev, exact ? 1u : 0u,
                        reuse_case, w.touched, w.ctl, w.gran, w.scan, out_raw_dev, chunk_raw_out_dev, n_invalid_dev,
-                       counters_dev, (uint32_t)(h3c_rt::hook(H3C_HOOK_UPD_LOOKBACK) == 1), tagged, tok.ts);
+                       counters_dev, (uint32_t)(h3c_rt::hook(H3C_HOOK_UPD_LOOKBACK) == 1), tagged,
+                       us ? us->p + kUsStat : nullptr, tok.ts);
     HIP_TRY(hipGetLastError());
     suspect.s = nullptr;  // (the batch is enqueued whole: its last workgroup leaves the scratch reset)
     // algorithmic bytes: read new + read old + write back, per block write
