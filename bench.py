@@ -1009,9 +1009,10 @@ def main() -> int:
         }
     if args.workload == "verify" and args.update_extra and (args.chunks, args.chunk_kib) == (8192, 1024):
         # BASELINE config 3 in front of the driver too: 100k random 4 KiB UpdateIOs into
-        # 64 x 64 MiB chunks through h3c_update_ios_dev, 10 warm + 20 timed batches (never the `value`)
+        # 64 x 64 MiB chunks through h3c_update_ios_dev, 30 warm + 50 timed batches (never the `value`; the
+        # aligned sub-branch's range weights settle over the first ~10 batches)
         sub = argparse.Namespace(**vars(args))
-        sub.steps, sub.warmup, sub.writes, sub.exact = 20, 10, 100_000, False
+        sub.steps, sub.warmup, sub.writes, sub.exact = 50, 30, 100_000, False
         up = run_updio(sub, cx)
         res["update"] = {
             "metric": up["metric"], "config": up["config"]["workload"], "n_gpus": up["n_gpus"],
