@@ -166,7 +166,12 @@ int h3c_batch_combine(uint8_t type, const uint32_t *c1_dev, const uint32_t *c2_d
  * *n_invalid_dev == UINT32_MAX (counters.invalid == UINT64_MAX) reports a void batch: the
  * one-launch path chains its workgroups' per-chunk sums, and a workgroup that waited past its
  * bound (> 0.25 s, i.e. starved of its CU by other work) gave up.  The chunk bytes are right;
- * out_raw / chunk_raw_out of that call are not -- recompute them (h3c_plan_run over the chunks). */
+ * out_raw / chunk_raw_out of that call are not -- recompute them (h3c_plan_run over the chunks).
+ * The one-launch path (4 KiB blocks, <= 128 chunks) keeps its hash heads, control words and
+ * look-back state in a library-owned scratch per (device, stream) -- about 1 MiB plus 4 bytes
+ * per write rounded up to a power of two, never cleared between batches (epoch-tagged) -- rather
+ * than in the workspace; calls on one stream from several threads enqueue one at a time.  A call
+ * made while the stream is being captured into a graph uses the workspace instead. */
 size_t h3c_update_workspace_bytes(uint32_t n_blocks, uint32_t nchunks, uint64_t chunk_len, uint32_t block_bytes);
 int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nchunks, uint64_t chunk_len,
                       uint32_t block_bytes, const uint32_t *chunk_raw_in_dev, const uint32_t *blk_chunk_dev,
