@@ -2,7 +2,9 @@
 // r1 #8): the device / pinned lease pools, the coalescing queue, the per-thread UpdateIO aux
 // streams, the block-update shift-table cache, plan create / destroy, the profiling records and
 // (round 4) the UpdateIO fast branch's per-thread scratch, graph capture gate and outcome polling,
-// from 16 threads at once (half on their own streams, half on the default stream).
+// (round 5) the UpdateIO aligned sub-branch and the block path's per-stream scratch (the default
+// stream's one shared by eight threads), from 16 threads at once (half on their own streams, half on
+// the default stream).
 // Every result is checked against a bitwise CRC32C in this file.  Built by
 // scripts/tsan_host.sh with the host code instrumented (-Xarch_host -fsanitize=thread); GPU
 // code is built normally.
@@ -151,6 +153,45 @@ void worker(int t, int iters) {
       (void)hipFree(d_res);
     }
     (void)hipFree(d_pay);
+    // block-aligned updates (h3c_update_blocks_ex): 4 chunks of 64 KiB, random 4 KiB writes; the fused path's
+    // per-stream scratch, shared on the default stream by the even threads
+    {
+      const uint32_t bc = 4, blen = 64 << 10, bpc = blen / 4096, nw = 1 + (uint32_t)(rnd() % 200);
+      std::vector<uint8_t> bh(bc * blen), bp((size_t)nw * 4096);
+      for (auto &b : bh) b = (uint8_t)rnd();
+      for (auto &b : bp) b = (uint8_t)rnd();
+      std::vector<uint32_t> wc(nw), wb(nw), raw0(bc), fin(bc);
+      std::vector<uint64_t> bases(bc);
+      for (uint32_t i = 0; i < nw; ++i) wc[i] = (uint32_t)(rnd() % bc), wb[i] = (uint32_t)(rnd() % bpc);
+      for (uint32_t c = 0; c < bc; ++c) raw0[c] = crc_bitwise(bh.data() + (size_t)c * blen, blen, 0xFFFFFFFFu);
+      const size_t wsb = h3c_update_workspace_bytes(nw, bc, blen, 4096);
+      uint8_t *d_ch = nullptr, *d_bp = nullptr, *d_ws = nullptr;
+      uint32_t *d_u = nullptr;  // raw_in, raw_out, chunk idx, block idx, out_raw
+      uint64_t *d_bases = nullptr;
+      if (hipMalloc(&d_ch, bh.size()) != hipSuccess || hipMalloc(&d_bp, bp.size()) != hipSuccess ||
+          hipMalloc(&d_ws, wsb) != hipSuccess || hipMalloc(&d_u, 4 * (2 * bc + 3 * nw)) != hipSuccess ||
+          hipMalloc(&d_bases, 8 * bc) != hipSuccess)
+        return fail(t, "block tables", -1);
+      for (uint32_t c = 0; c < bc; ++c) bases[c] = (uint64_t)(uintptr_t)(d_ch + (size_t)c * blen);
+      uint32_t *d_rin = d_u, *d_rout = d_u + bc, *d_wc = d_u + 2 * bc, *d_wb = d_wc + nw, *d_out = d_wb + nw;
+      if (hipMemcpy(d_ch, bh.data(), bh.size(), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(d_bp, bp.data(), bp.size(), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(d_rin, raw0.data(), 4 * bc, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(d_wc, wc.data(), 4 * nw, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(d_wb, wb.data(), 4 * nw, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(d_bases, bases.data(), 8 * bc, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(t, "block upload", -1);
+      rc = h3c_update_blocks_ex(H3C_TYPE_CRC32C, d_bases, bc, blen, 4096, d_rin, d_wc, d_wb, d_bp, nw, d_out, d_rout,
+                                d_ws, wsb, nullptr, 0u, nullptr, sp);
+      if (rc) fail(t, "update_blocks", rc);
+      for (uint32_t i = 0; i < nw; ++i)
+        std::memcpy(bh.data() + (size_t)wc[i] * blen + (size_t)wb[i] * 4096, bp.data() + (size_t)i * 4096, 4096);
+      if (hipStreamSynchronize(st) != hipSuccess || hipMemcpy(fin.data(), d_rout, 4 * bc, hipMemcpyDeviceToHost) != hipSuccess)
+        fail(t, "block read back", -1);
+      for (uint32_t c = 0; c < bc && !rc; ++c)
+        if (fin[c] != crc_bitwise(bh.data() + (size_t)c * blen, blen, 0xFFFFFFFFu)) fail(t, "block update value", 0);
+      (void)hipFree(d_ch), (void)hipFree(d_bp), (void)hipFree(d_ws), (void)hipFree(d_u), (void)hipFree(d_bases);
+    }
     if (t == 0 && it % 4 == 1) h3c_set_coalescing(it % 8 == 1);  // flip the queue under load
     if (t == 1) {  // profiling records: enable, read, disable while others launch
       h3c_profile_enable(1);
