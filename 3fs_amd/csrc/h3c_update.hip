@@ -122,7 +122,10 @@ __global__ void upd_keys_kernel(const uint32_t *__restrict__ blk_chunk, const ui
 // of its slot below its own: a list holds at most one entry per tile and slot, so the walk
 // stays short even when every write hammers one slot.  (A returning atomicCAS costs about
 // twice an atomicExch here: scripts/atomic_probe.hip.)
-constexpr uint32_t kLinkTile = 256;
+#ifndef H3C_LINK_TILE
+#define H3C_LINK_TILE 256
+#endif
+constexpr uint32_t kLinkTile = H3C_LINK_TILE;
 // control words (the workspace's, zeroed per call; or the stream's UpdScratch, left reset by each batch's last
 // workgroup): [kCtlEpoch] the scratch's batch epoch (8 bits; 0 in a zeroed workspace)
 // [kCtlAcc, +1] one u64: the fused kernel's tickets taken << 40 | the range weights summed; [kCtlW, +8) each

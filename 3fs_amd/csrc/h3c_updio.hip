@@ -3160,7 +3160,10 @@ __device__ uint32_t g_af_fin[1024 * 16];  // per wave: its ops whose block has l
 #ifndef H3C_AF_EARLY_OLD
 #define H3C_AF_EARLY_OLD 0  // 1: the next op's old rows load with its new rows, before this op's CRCs (A/B)
 #endif
-constexpr uint32_t kATile = 256;             // uio_aprep_kernel ops per workgroup
+#ifndef H3C_ATILE
+#define H3C_ATILE 256
+#endif
+constexpr uint32_t kATile = H3C_ATILE;       // uio_aprep_kernel ops per workgroup
 constexpr uint32_t kAMaxOps = (1u << 24) - 2;  // bucket entries: epoch << 24 | (op index + 1)
 // control words: [kAAcc, +1] one u64: tickets taken << 40 | the workgroups' range weights summed (ranges are
 // cut in ticket order, each sized by its class's weight); [kAW, +8) the range weight of each workgroup class
