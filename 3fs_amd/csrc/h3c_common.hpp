@@ -641,6 +641,25 @@ __device__ __forceinline__ uint4 load_row(uint64_t a) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// A row load of the partial-update kernels (random 4 KiB read-modify-write: the old block, the payload).
+// Nontemporal by default, as for streamed reads; H3C_RMW_NT_LOADS=0 makes them plain (A/B).  Round 5 measured
+// the policies per kernel on config 3 (profiles/r05s_rmw_policy_ab.txt): plain *stores* for the write-back
+// take the aligned UpdateIO kernel from 265 to 244 us and the block path's from 265 to 234 us, while plain
+// loads help alone but lose beside plain stores (258 / 251 us).  Nothing in a partial-update kernel reads a
+// line another workgroup wrote in the same launch (a block is read by its first writer only, payloads are
+// never written), so write-back lines held in one XCD's L2 need no coherence inside a launch.
+#ifndef H3C_RMW_NT_LOADS
+#define H3C_RMW_NT_LOADS 1
+#endif
+__device__ __forceinline__ uint4 load_row_rmw(uint64_t a) {
+#if H3C_RMW_NT_LOADS
+  return load_row(a);
+#else
+  const v4u v = *(gv4p)a;
+  return make_uint4(v.x, v.y, v.z, v.w);
+#endif
+}
+
 // A row load of a kernel whose rows per chunk are narrower than a 128-byte line (fewer than 8 lanes x
 // 16 B: the small-chunk kernels' 4-lane groups, 64-byte rows).  Nontemporal loads skip the CU's L1, so
 // the two 64-byte halves of a line reach L2 as separate requests, and 7-8 % of the lines were fetched

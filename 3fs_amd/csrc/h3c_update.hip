@@ -62,7 +62,7 @@ namespace {
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 #ifndef H3C_NT_STORES
-#define H3C_NT_STORES 1  // write-back bytes are not re-read by this kernel: nontemporal (+2% measured)
+#define H3C_NT_STORES 0  // 1: nontemporal write-back stores (r02: +2 %; round 5: plain stores 265 -> 234 us, load_row_rmw)
 #endif
 __device__ __forceinline__ void store_row(uint64_t a, uint4 v) {
 #if H3C_NT_STORES
@@ -291,8 +291,8 @@ __device__ uint32_t delta_crc0(uint64_t pnew, uint64_t pold, uint64_t dst, uint6
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (u < (int)nb) {
-        vn[u] = load_row(pnew + (uint64_t)(r0 + u) * kRowBytes + lo);
-        vo[u] = load_row(pold + (uint64_t)(r0 + u) * kRowBytes + lo);
+        vn[u] = load_row_rmw(pnew + (uint64_t)(r0 + u) * kRowBytes + lo);
+        vo[u] = load_row_rmw(pold + (uint64_t)(r0 + u) * kRowBytes + lo);
       }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -304,7 +304,7 @@ __device__ uint32_t delta_crc0(uint64_t pnew, uint64_t pold, uint64_t dst, uint6
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (u < (int)nb) {
-          const uint4 v = fin == pnew ? vn[u] : load_row(fin + (uint64_t)(r0 + u) * kRowBytes + lo);
+          const uint4 v = fin == pnew ? vn[u] : load_row_rmw(fin + (uint64_t)(r0 + u) * kRowBytes + lo);
           *reinterpret_cast<uint4 *>(dst + (uint64_t)(r0 + u) * kRowBytes + lo) = v;
         }
     }
@@ -392,8 +392,8 @@ __device__ __forceinline__ void upd_delta_kernel_body(
     uint64_t pnew = rl64(m_new, 0), pold = rl64(m_old, 0);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      vn[u] = valid ? load_row(pnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
-      vo[u] = valid ? load_row(pold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+      vn[u] = valid ? load_row_rmw(pnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+      vo[u] = valid ? load_row_rmw(pold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
     }
     for (uint32_t t = 0; t < cnt; ++t) {
       const bool nvalid = t + 1 < cnt && __builtin_amdgcn_readlane(m_ok, t + 1) != 0;
@@ -405,8 +405,8 @@ __device__ __forceinline__ void upd_delta_kernel_body(
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        wn[u] = nvalid ? load_row(npnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
-        wo[u] = nvalid ? load_row(npold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+        wn[u] = nvalid ? load_row_rmw(npnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+        wo[u] = nvalid ? load_row_rmw(npold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
       }
       uint32_t d = 0;
       if (valid) {
@@ -424,7 +424,7 @@ __device__ __forceinline__ void upd_delta_kernel_body(
           const uint64_t fin = rl64(m_fin, t);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const uint4 v = fin == pnew ? vn[u] : load_row(fin + u * kRowBytes + lo16);
+            const uint4 v = fin == pnew ? vn[u] : load_row_rmw(fin + u * kRowBytes + lo16);
             store_row(dst + u * kRowBytes + lo16, v);
           }
         }
@@ -568,8 +568,8 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     pold = rl64(m_old, 0);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      vn[u] = valid ? load_row(pnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
-      vo[u] = valid ? load_row(pold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+      vn[u] = valid ? load_row_rmw(pnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+      vo[u] = valid ? load_row_rmw(pold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
     }
     // the walk over the slot's listed tile-last writers, while those rows load
     if (key != kNone) {
@@ -592,7 +592,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     if (valid && pold2 != pold) {  // write 0 was mis-speculated: reload its old rows
       pold = pold2;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) vo[u] = load_row(pold + u * kRowBytes + lo16);
+      for (int u = 0; u < 4; ++u) vo[u] = load_row_rmw(pold + u * kRowBytes + lo16);
     }
   };
   if (lo < hi) start_group(lo);  // the first group's links and rows load while the tables fill
@@ -619,8 +619,8 @@ __device__ __forceinline__ void upd_fused_kernel_body(
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        wn[u] = nvalid ? load_row(npnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
-        wo[u] = nvalid ? load_row(npold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+        wn[u] = nvalid ? load_row_rmw(npnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+        wo[u] = nvalid ? load_row_rmw(npold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
       }
       if (valid) {
         Streams st{0, 0, 0, 0};
@@ -637,7 +637,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
           const uint64_t fin = rl64(m_fin, t);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const uint4 v = fin == pnew ? vn[u] : load_row(fin + u * kRowBytes + lo16);
+            const uint4 v = fin == pnew ? vn[u] : load_row_rmw(fin + u * kRowBytes + lo16);
             store_row(dst + u * kRowBytes + lo16, v);
           }
         }

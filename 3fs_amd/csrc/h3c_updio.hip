@@ -1506,16 +1506,16 @@ __device__ __forceinline__ uint4 load_new(uint64_t src, uint32_t row, uint32_t r
   if (row_none(row, w0, w1)) return make_uint4(0, 0, 0, 0);
   const uint32_t s = (uint32_t)(src & 15u);
   const uint64_t a = src + rel;
-  if (row_full(row, w0, w1) && s == 0) return load_row(a);
+  if (row_full(row, w0, w1) && s == 0) return load_row_rmw(a);
   if (rel + 16 <= w0 || rel >= w1) return make_uint4(0, 0, 0, 0);
   uint4 v;
   if (s == 0) {
-    v = load_row(a);
+    v = load_row_rmw(a);
   } else {
     const uint64_t a0 = a & ~uint64_t(15);
     const uint64_t wb = src + (rel > w0 ? rel : w0), we = src + (rel + 16 < w1 ? rel + 16 : w1);
-    const uint4 lo = a0 + 16 > wb ? load_row(a0) : make_uint4(0, 0, 0, 0);
-    const uint4 hi = a0 + 16 < we ? load_row(a0 + 16) : make_uint4(0, 0, 0, 0);
+    const uint4 lo = a0 + 16 > wb ? load_row_rmw(a0) : make_uint4(0, 0, 0, 0);
+    const uint4 hi = a0 + 16 < we ? load_row_rmw(a0 + 16) : make_uint4(0, 0, 0, 0);
     v = funnel16(lo, hi, s);
   }
   return row_full(row, w0, w1) ? v : and4(v, mask16(rel, w0, w1));
@@ -1551,17 +1551,24 @@ constexpr uint32_t kBlkWaves = H3C_UIO_BLOCK_WAVES, kBlkThreads = 64 * kBlkWaves
 #ifndef H3C_UIO_FOLD_ILP
 #define H3C_UIO_FOLD_ILP 0  // 1: the fold check's CRC and the delta's interleaved (spills: 362 vs 288 us, r03c_updio_ab)
 #endif
+// Write-back store policy per kernel (1: nontemporal, 0: plain; profiles/r05s_rmw_policy_ab.txt):
 #ifndef H3C_UIO_NT_STORES
-#define H3C_UIO_NT_STORES 1
+#define H3C_UIO_NT_STORES 1  // uio_block_kernel (the general pipeline)
 #endif
+#ifndef H3C_FAST_NT_STORES
+#define H3C_FAST_NT_STORES 1  // uio_fast_kernel (the chain-based fast branch)
+#endif
+#ifndef H3C_AF_NT_STORES
+#define H3C_AF_NT_STORES 0  // uio_afused_kernel (the aligned sub-branch): plain, 265 -> 244 us
+#endif
+template <bool kNt = H3C_UIO_NT_STORES>
 __device__ __forceinline__ void store_masked(uint64_t blk, uint32_t rel, uint4 v, uint32_t k0, uint32_t k1) {
   if (rel >= k0 && rel + 16 <= k1) {
     v4u w = {v.x, v.y, v.z, v.w};
-#if H3C_UIO_NT_STORES
-    __builtin_nontemporal_store(w, (v4u __attribute__((address_space(1))) *)(blk + rel));
-#else
-    *(v4u __attribute__((address_space(1))) *)(blk + rel) = w;
-#endif
+    if (kNt)
+      __builtin_nontemporal_store(w, (v4u __attribute__((address_space(1))) *)(blk + rel));
+    else
+      *(v4u __attribute__((address_space(1))) *)(blk + rel) = w;
   } else if (rel + 16 > k0 && rel < k1) {  // a word shared with a neighbouring chunk: its own bytes only
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint8_t *p = reinterpret_cast<uint8_t *>(blk + rel);
@@ -1582,7 +1589,7 @@ __device__ __forceinline__ void load_task_rows(uint64_t blk, uint32_t k0, uint32
   for (int r = 0; r < 4; ++r) {
     const uint32_t rel = 1024u * r + 16u * lane;
 #if H3C_UIO_IMG_NT
-    b.img[r] = (rel + 16 > k0 && rel < k1) ? load_row(blk + rel) : make_uint4(0, 0, 0, 0);
+    b.img[r] = (rel + 16 > k0 && rel < k1) ? load_row_rmw(blk + rel) : make_uint4(0, 0, 0, 0);
 #else
     b.img[r] = (rel + 16 > k0 && rel < k1) ? load_plain(blk + rel) : make_uint4(0, 0, 0, 0);
 #endif
@@ -2728,7 +2735,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
       const uint64_t blk = (uint64_t)a.x | ((uint64_t)a.y << 32);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (dirty & (1u << r)) store_masked(blk, 1024u * r + 16u * lane, cur.img[r], c2.y & 0xFFFFu, c2.y >> 16);
+        if (dirty & (1u << r)) store_masked<H3C_FAST_NT_STORES>(blk, 1024u * r + 16u * lane, cur.img[r], c2.y & 0xFFFFu, c2.y >> 16);
     }
     dirty = 0;
     if (nh == kNil) break;
@@ -3391,8 +3398,8 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     spec_old = s_cs[io.chunk].base + io.offset;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      vn[u] = load_row(io.payload + (uint32_t)(u * kRowBytes + lo16));
-      vo[u] = load_row(spec_old + (uint32_t)(u * kRowBytes + lo16));
+      vn[u] = load_row_rmw(io.payload + (uint32_t)(u * kRowBytes + lo16));
+      vo[u] = load_row_rmw(spec_old + (uint32_t)(u * kRowBytes + lo16));
     }
   }
   for (uint32_t j = wlo + t; j < whi; j += kBlkThreads) {
@@ -3470,7 +3477,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     rec_of(jc, rc);
     if (rc.pold != spec_old) {  // the first op was not its block's first: its old rows are a payload
 #pragma unroll
-      for (int u = 0; u < 4; ++u) vo[u] = load_row(rc.pold + (uint32_t)(u * kRowBytes + lo16));
+      for (int u = 0; u < 4; ++u) vo[u] = load_row_rmw(rc.pold + (uint32_t)(u * kRowBytes + lo16));
     }
   }
   uint32_t jn = jc != kNil ? grab() : kNil;
@@ -3481,8 +3488,8 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     const bool nvalid = jn != kNil;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      wn[u] = nvalid ? load_row(rn.pnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
-      wo[u] = nvalid ? load_row(rn.pold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+      wn[u] = nvalid ? load_row_rmw(rn.pnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+      wo[u] = nvalid ? load_row_rmw(rn.pold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
     }
     uint32_t jnn = nvalid ? grab() : kNil;  // (the op after next: its record loads meanwhile)
     if (jnn >= whi) jnn = kNil;
@@ -3491,7 +3498,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     const bool solo = rc.first && rc.fin == rc.pnew;  // the block's only write
     if (H3C_AF_STORE_EARLY && solo) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) store_masked(rc.pold, u * kRowBytes + lo16, vn[u], 0u, kBlk);
+      for (int u = 0; u < 4; ++u) store_masked<H3C_AF_NT_STORES>(rc.pold, u * kRowBytes + lo16, vn[u], 0u, kBlk);
     }
     Streams s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
@@ -3509,7 +3516,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
         if (H3C_AF_STORE_EARLY ? !pass : pass) {  // (early store: a failed check puts the old rows back)
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            store_masked(rc.pold, u * kRowBytes + lo16, H3C_AF_STORE_EARLY ? vo[u] : vn[u], 0u, kBlk);
+            store_masked<H3C_AF_NT_STORES>(rc.pold, u * kRowBytes + lo16, H3C_AF_STORE_EARLY ? vo[u] : vn[u], 0u, kBlk);
         }
       } else {
 #if H3C_AF_TRACE
@@ -3517,14 +3524,14 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
 #endif
         // (into the old rows' registers: this op's delta is folded, and the next op's rows are in wn / wo)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) vo[u] = load_row(rc.fin + (uint32_t)(u * kRowBytes + lo16));
+        for (int u = 0; u < 4; ++u) vo[u] = load_row_rmw(rc.fin + (uint32_t)(u * kRowBytes + lo16));
         Streams sf{0, 0, 0, 0};
 #pragma unroll
         for (int u = 0; u < 4; ++u) consume(sf, vo[u], lb, Lt);
         const uint32_t Pf = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_fold_tab(sf, lane, red));
         if (Pf == rc.fexp) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) store_masked(rc.pold, u * kRowBytes + lo16, vo[u], 0u, kBlk);
+          for (int u = 0; u < 4; ++u) store_masked<H3C_AF_NT_STORES>(rc.pold, u * kRowBytes + lo16, vo[u], 0u, kBlk);
         } else {  // the last op fails A6: uio_afix_kernel writes the last passing op's bytes (if any)
           if (lane == 0) {
             const uint32_t d = atomicAdd(&aa.ctl[kADefer], 1u);

@@ -224,11 +224,14 @@ PATTERN_CEILING = {
     "seg_crc_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
     "seg_quad_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
     "seg_uni_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
-    "upd_delta_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
-    "upd_fused_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
-    "uio_block_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
-    "uio_fast_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
-    "uio_afused_kernel": (5109.0, "profiles/r01_update_pattern_ceiling.txt"),
+    # config 3's pattern: the best payload+old read alone plus the best plain write alone, back to back
+    # (198.8 us per 100k writes = 6,181 GB/s of the 12 KiB per write; the round-5 kernels beat the probe's
+    # own mixed rmw loop, so that is no ceiling: profiles/r05_rmw_ceiling.txt)
+    "upd_delta_kernel": (6181.0, "profiles/r05_rmw_ceiling.txt"),
+    "upd_fused_kernel": (6181.0, "profiles/r05_rmw_ceiling.txt"),
+    "uio_block_kernel": (6181.0, "profiles/r05_rmw_ceiling.txt"),
+    "uio_fast_kernel": (6181.0, "profiles/r05_rmw_ceiling.txt"),
+    "uio_afused_kernel": (6181.0, "profiles/r05_rmw_ceiling.txt"),
 }
 
 

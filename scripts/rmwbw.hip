@@ -14,7 +14,8 @@
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef v4u __attribute__((address_space(1))) *gv4p;
 
-// MODE bit0: read payload, bit1: read slot, bit2: write slot.  INF blocks in flight per wave.
+// MODE bit0: read payload, bit1: read slot, bit2: write slot, bit3: plain (not nontemporal) stores.
+// INF blocks in flight per wave.
 template <int MODE, int INF>
 __global__ __launch_bounds__(1024) void rmw(const char *pay, char *region, const uint32_t *slot, uint32_t n,
                                             uint32_t *out, const uint32_t *ord) {
@@ -45,7 +46,10 @@ __global__ __launch_bounds__(1024) void rmw(const char *pay, char *region, const
         if (MODE & 2) acc ^= b[f][u];
         if (MODE & 4) {
           v4u w = (MODE & 1) ? a[f][u] : v4u{lane, i, 0, 0};
-          __builtin_nontemporal_store(w, (gv4p)(s + 1024 * u));
+          if (MODE & 8)
+            *(gv4p)(s + 1024 * u) = w;
+          else
+            __builtin_nontemporal_store(w, (gv4p)(s + 1024 * u));
         } else if (MODE & 1) {
           acc ^= a[f][u];
         }
@@ -107,6 +111,9 @@ int main() {
 #define R(MODE, INF, BYTES, LABEL) RO(MODE, INF, BYTES, LABEL, slot, nullptr)
     R(7, 1, 12288, "rmw (pay+old+write)")
     R(7, 2, 12288, "rmw (pay+old+write)")
+    R(15, 1, 12288, "rmw plain stores")
+    R(15, 2, 12288, "rmw plain stores")
+    R(12, 1, 4096, "write only, plain")
     R(3, 1, 8192, "read pay+old")
     R(3, 2, 8192, "read pay+old")
     R(6, 1, 8192, "read old+write")
