@@ -660,6 +660,22 @@ __device__ __forceinline__ uint4 load_row_rmw(uint64_t a) {
 #endif
 }
 
+// The old rows of a partial update: `blk` when they are the chunk's own block (the block's first writer, which
+// writes the block back), else a previous writer's payload.  The block's rows load plainly (the same wave
+// writes the block back: the lines are then in L2 for the plain stores), the payloads nontemporally:
+// upd_fused_kernel 234.3 -> 222.8 us, uio_afused_kernel ~-2 us (profiles/r05s_rmw_policy_ab.txt, part 4);
+// H3C_RMW_BLOCK_PLAIN=0 loads both nontemporally.
+#ifndef H3C_RMW_BLOCK_PLAIN
+#define H3C_RMW_BLOCK_PLAIN 1
+#endif
+__device__ __forceinline__ uint4 load_row_old(uint64_t a, bool blk) {
+  if (H3C_RMW_BLOCK_PLAIN && blk) {
+    const v4u v = *(gv4p)a;
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return load_row_rmw(a);
+}
+
 // A row load of a kernel whose rows per chunk are narrower than a 128-byte line (fewer than 8 lanes x
 // 16 B: the small-chunk kernels' 4-lane groups, 64-byte rows).  Nontemporal loads skip the CU's L1, so
 // the two 64-byte halves of a line reach L2 as separate requests, and 7-8 % of the lines were fetched

@@ -566,10 +566,11 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     valid = __builtin_amdgcn_readlane(m_c, 0) != kNone;
     pnew = rl64(m_new, 0);
     pold = rl64(m_old, 0);
+    const bool oblk = rl64(m_dst, 0) != 0;  // (the speculated old rows are the slot's own)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       vn[u] = valid ? load_row_rmw(pnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
-      vo[u] = valid ? load_row_rmw(pold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+      vo[u] = valid ? load_row_old(pold + u * kRowBytes + lo16, oblk) : make_uint4(0, 0, 0, 0);
     }
     // the walk over the slot's listed tile-last writers, while those rows load
     if (key != kNone) {
@@ -613,14 +614,16 @@ __device__ __forceinline__ void upd_fused_kernel_body(
       const bool nvalid = t + 1 < cnt && __builtin_amdgcn_readlane(m_c, t + 1) != kNone;
       uint4 wn[4], wo[4];
       uint64_t npnew = 0, npold = 0;
+      bool nblk = false;
       if (nvalid) {
         npnew = rl64(m_new, t + 1);
         npold = rl64(m_old, t + 1);
+        nblk = rl64(m_dst, t + 1) != 0;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         wn[u] = nvalid ? load_row_rmw(npnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
-        wo[u] = nvalid ? load_row_rmw(npold + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+        wo[u] = nvalid ? load_row_old(npold + u * kRowBytes + lo16, nblk) : make_uint4(0, 0, 0, 0);
       }
       if (valid) {
         Streams st{0, 0, 0, 0};

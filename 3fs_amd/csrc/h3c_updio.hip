@@ -3399,7 +3399,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       vn[u] = load_row_rmw(io.payload + (uint32_t)(u * kRowBytes + lo16));
-      vo[u] = load_row_rmw(spec_old + (uint32_t)(u * kRowBytes + lo16));
+      vo[u] = load_row_old(spec_old + (uint32_t)(u * kRowBytes + lo16), true);
     }
   }
   for (uint32_t j = wlo + t; j < whi; j += kBlkThreads) {
@@ -3489,7 +3489,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       wn[u] = nvalid ? load_row_rmw(rn.pnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
-      wo[u] = nvalid ? load_row_rmw(rn.pold + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+      wo[u] = nvalid ? load_row_old(rn.pold + (uint32_t)(u * kRowBytes + lo16), rn.first) : make_uint4(0, 0, 0, 0);
     }
     uint32_t jnn = nvalid ? grab() : kNil;  // (the op after next: its record loads meanwhile)
     if (jnn >= whi) jnn = kNil;
