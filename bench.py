@@ -150,7 +150,8 @@ def pmc_traffic(bytes_per_launch: int, kernel: str = "seg_crc_kernel"):
             continue
         t = d.get("pmc", {}).get("traffic_bytes_per_launch")
         if t and abs(d.get("algorithmic_bytes_per_launch", 0) - bytes_per_launch) < 1:
-            best = (t, os.path.basename(f))
+            k = d.get(kernel, {})
+            best = (t, os.path.basename(f), k.get("avg_us_last_half") or k.get("avg_us"))
     return best
 
 
@@ -220,6 +221,7 @@ class Ctx:
 # Measured ceilings of the access patterns themselves (no CRC work), for context beside the
 # 8 TB/s spec peak: streaming reads of per-wave contiguous segments (scripts/readbw.hip) and
 # the update kernel's random 4 KiB read-modify-write (scripts/rmwbw.hip).
+PLAIN_STORE_KERNELS = ("upd_fused_kernel", "uio_afused_kernel")  # write-back by plain stores (round 5)
 PATTERN_CEILING = {
     "seg_crc_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
     "seg_quad_kernel": (6905.0, "profiles/r01_readbw_ceiling.txt"),
@@ -247,6 +249,13 @@ def roofline(prof, peak: float, unit: str = "GB/s", bound: str = "hbm", kernel: 
     if tr:
         r["traffic"] = int(tr[0])
         r["traffic_source"] = f"profiles/{tr[1]}"
+        if tr[2]:  # the same kernel's rocprof duration in that profile (its settled second half, where recorded)
+            r["rocprof_avg_us"] = round(tr[2], 2)
+            r["frac_rocprof"] = round(per / (tr[2] * 1e-6) / 1e9 / peak, 4)
+            if kernel in PLAIN_STORE_KERNELS:
+                r["timing_note"] = ("kernel_avg_us: the kernel's own stamps, first workgroup start to last workgroup "
+                                    "end; rocprof's duration also covers the end-of-launch L2 write-back of its plain "
+                                    "stores")
     if kernel in PATTERN_CEILING:
         ceil, src = PATTERN_CEILING[kernel]
         r["pattern_ceiling"] = {"achieved": ceil, "frac": round(achieved / ceil, 4), "source": src}

@@ -66,10 +66,21 @@ if len(sys.argv) > 2 and sys.argv[2] == "--json":
     fr, wr = fetch.get(kern, []), write.get(kern, [])
     rb = 2 * 1024 * sum(fr) / len(fr)
     wb = 1024 * sum(wr) / len(wr)
+    # the last half of the kernel's dispatches (kernels whose per-XCD range weights settle over the first
+    # batches of a stream: the steady state the bench's timed steps see)
+    durs = []
+    trace = one("kt/**/kt_kernel_trace.csv")
+    if trace:
+        for r in csv.DictReader(open(trace)):
+            if short(r["Kernel_Name"]) == kern:
+                durs.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    durs = [x for _, x in sorted(durs)]
+    tail = durs[len(durs) // 2:]
     json.dump({
         "kernel": kern,
         kern: {"calls": int(row["Calls"]), "avg_us": float(row["AverageNs"]) / 1e3,
-               "min_us": float(row["MinNs"]) / 1e3, "pct_gpu_time": float(row["Percentage"])},
+               "min_us": float(row["MinNs"]) / 1e3, "pct_gpu_time": float(row["Percentage"]),
+               "avg_us_last_half": (sum(tail) / len(tail) / 1e3) if tail else None},
         "pmc": {"FETCH_SIZE_kib_raw": sum(fr) / len(fr), "WRITE_SIZE_kib": sum(wr) / len(wr),
                 "hbm_read_bytes_per_launch": rb, "hbm_write_bytes_per_launch": wb,
                 "correction": "FETCH_SIZE x1024 x2 (gfx950 reports half of a wide streaming read); WRITE_SIZE x1024",
