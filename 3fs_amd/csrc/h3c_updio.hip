@@ -3181,6 +3181,10 @@ constexpr uint32_t kAClasses = 8;
 constexpr uint32_t kAOne = 1u << 16;  // weight 1.0
 constexpr uint32_t kADoneVoid = 1u << 12;    // kADone: finished workgroups (low 12 bits) + void reports << 12
 constexpr uint32_t kASpin = 1u << 22;        // bounded look-back spins (about a quarter second)
+#ifndef H3C_AF_LOOK_WIN
+#define H3C_AF_LOOK_WIN 4
+#endif
+constexpr uint32_t kALookWin = H3C_AF_LOOK_WIN;  // look-back rows read per column per round trip
 
 struct AlignedArgs {
   uint32_t *ctl;                  // kACtlWords control words (the thread's FastScratch)
@@ -3633,11 +3637,12 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
         auto look = [&](int &j, uint32_t &x, uint32_t col) {
           if (j < 0) return;
           const int top = j;
-          unsigned long long g[4];
+          unsigned long long g[kALookWin];
 #pragma unroll
-          for (int w = 0; w < 4; ++w) g[w] = top - w >= 0 ? ld_agent(&aa.gran[(uint64_t)(top - w) * kFastCols + col]) : 0ull;
+          for (int w = 0; w < (int)kALookWin; ++w)
+            g[w] = top - w >= 0 ? ld_agent(&aa.gran[(uint64_t)(top - w) * kFastCols + col]) : 0ull;
 #pragma unroll
-          for (int w = 0; w < 4; ++w) {
+          for (int w = 0; w < (int)kALookWin; ++w) {
             const uint32_t state = agran_state(g[w], E);
             if (top - w >= 0 && j == top - w && state) {
               x ^= (uint32_t)g[w];
