@@ -3181,6 +3181,12 @@ constexpr uint32_t kAClasses = 8;
 constexpr uint32_t kAOne = 1u << 16;  // weight 1.0
 constexpr uint32_t kADoneVoid = 1u << 12;    // kADone: finished workgroups (low 12 bits) + void reports << 12
 constexpr uint32_t kASpin = 1u << 22;        // bounded look-back spins (about a quarter second)
+#ifndef H3C_AF_LAZY
+#define H3C_AF_LAZY 0  // 1: each op's record made by the wave that takes it (no phase-0 pass)
+#endif
+#ifndef H3C_AF_STATIC
+#define H3C_AF_STATIC 0
+#endif
 #ifndef H3C_AF_LOOK_WIN
 #define H3C_AF_LOOK_WIN 4
 #endif
@@ -3395,7 +3401,11 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   // one 32-byte record per op for phase 1's scalar loads ----
   // (each wave's first op is wlo + wave: its new rows and (speculated) block rows load before the fill)
   uint4 vn[4], vo[4];
+#if H3C_AF_STATIC  // (A/B: each wave runs its contiguous share in order, no LDS counter)
+  const uint32_t j0 = lo < hi ? lo : whi;
+#else
   const uint32_t j0 = wlo + wave;
+#endif
   uint64_t spec_old = 0;
   if (j0 < whi) {
     const h3c_update_io io = ios[j0];  // (scalar: wave-uniform)
@@ -3406,7 +3416,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
       vo[u] = load_row_old(spec_old + (uint32_t)(u * kRowBytes + lo16), true);
     }
   }
-  for (uint32_t j = wlo + t; j < whi; j += kBlkThreads) {
+  for (uint32_t j = wlo + t; j < (H3C_AF_LAZY ? wlo : whi); j += kBlkThreads) {
     const h3c_update_io io = ios[j];
     const uint4 lk = aa.link[j];
     const h3c_chunk_state &cs = s_cs[io.chunk];  // (aprep: every op's chunk is < nchunks <= 128)
@@ -3459,6 +3469,46 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     uint32_t exp, fexp;
     bool first;
   };
+#if H3C_AF_LAZY
+  // the op's record made by the wave when it takes the op (scalar loads: j is wave-uniform), instead of a
+  // phase-0 pass over the workgroup's ops before the loop
+  auto rec_of = [&](uint32_t j, Rec &r) {
+    const h3c_update_io io = ios[j];
+    const uint4 lk = aa.link[j];
+    const uint32_t exp = aexpect(io.checksum_value, std_domain, k4096);
+    uint32_t prev = lk.x, fexp = 0;
+    uint64_t fin = 0;
+    bool first = false;
+    if (prev == kNil) {
+      const unsigned long long key = aa.key[j];
+      uint32_t fmax = j;
+      for (uint32_t e = aa.head[fast_bucket(key, aa.hmask)]; aentry_valid(e, E); e = aa.link[(e & 0xFFFFFFu) - 1].y) {
+        const uint32_t i = (e & 0xFFFFFFu) - 1;
+        if (i >= n) break;
+        if (aa.key[i] != key) continue;
+        if (i < j && (prev == kNil || i > prev)) prev = i;
+        fmax = max(fmax, i);
+      }
+      if (prev == kNil) {
+        first = true;
+        fin = io.payload;
+        fexp = exp;
+        if (fmax != j) {
+          const h3c_update_io fio = ios[fmax];
+          fin = fio.payload;
+          fexp = aexpect(fio.checksum_value, std_domain, k4096);
+        }
+      }
+    }
+    r.pnew = io.payload;
+    r.pold = first ? s_cs[io.chunk].base + io.offset : ios[prev].payload;
+    r.first = first;
+    r.fin = fin;
+    r.exp = exp;
+    r.fexp = fexp;
+    if (lane == 0) aa.pv[j].y = prev;  // (uio_afix_kernel's input)
+  };
+#else
   auto rec_of = [&](uint32_t j, Rec &r) {  // (scalar loads: j is wave-uniform)
     const uint4 a = aa.rec[2 * (size_t)j], b = aa.rec[2 * (size_t)j + 1];
     r.pnew = (uint64_t)a.x | ((uint64_t)a.y << 32);
@@ -3469,11 +3519,20 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     r.exp = b.z;
     r.fexp = b.w;
   };
+#endif
+#if H3C_AF_STATIC
+  uint32_t next_static = j0 + 1;
+  auto grab = [&]() -> uint32_t {
+    const uint32_t j = next_static++;
+    return j < hi ? j : whi;
+  };
+#else
   auto grab = [&]() -> uint32_t {
     uint32_t j = 0;
     if (lane == 0) j = atomicAdd(&s_grab, 1u);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
   };
+#endif
   uint32_t wave_void = 0;
   uint32_t jc = j0 < whi ? j0 : kNil;
   Rec rc{}, rn{};
