@@ -3181,6 +3181,9 @@ constexpr uint32_t kAClasses = 8;
 constexpr uint32_t kAOne = 1u << 16;  // weight 1.0
 constexpr uint32_t kADoneVoid = 1u << 12;    // kADone: finished workgroups (low 12 bits) + void reports << 12
 constexpr uint32_t kASpin = 1u << 22;        // bounded look-back spins (about a quarter second)
+#ifndef H3C_AF_PRE2
+#define H3C_AF_PRE2 0  // 1: each wave's first two ops load their rows before phase 0
+#endif
 #ifndef H3C_AF_LAZY
 #define H3C_AF_LAZY 0  // 1: each op's record made by the wave that takes it (no phase-0 pass)
 #endif
@@ -3416,6 +3419,20 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
       vo[u] = load_row_old(spec_old + (uint32_t)(u * kRowBytes + lo16), true);
     }
   }
+  uint4 wn[4], wo[4];  // (the next op's rows)
+#if H3C_AF_PRE2  // each wave's second op is wlo + 16 + wave: its rows load before phase 0 too
+  const uint32_t j1 = wlo + kBlkWaves + wave;
+  uint64_t spec_old1 = 0;
+  if (j0 < whi && j1 < whi) {
+    const h3c_update_io io1 = ios[j1];
+    spec_old1 = s_cs[io1.chunk].base + io1.offset;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      wn[u] = load_row_rmw(io1.payload + (uint32_t)(u * kRowBytes + lo16));
+      wo[u] = load_row_old(spec_old1 + (uint32_t)(u * kRowBytes + lo16), true);
+    }
+  }
+#endif
   for (uint32_t j = wlo + t; j < (H3C_AF_LAZY ? wlo : whi); j += kBlkThreads) {
     const h3c_update_io io = ios[j];
     const uint4 lk = aa.link[j];
@@ -3451,7 +3468,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     aa.pv[j].y = prev;  // (uio_afix_kernel's input; crc0(new) follows in .x)
   }
   fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
-  if (t == 0) s_grab = wlo + kBlkWaves;  // (each wave's first op is wlo + wave)
+  if (t == 0) s_grab = wlo + (H3C_AF_PRE2 ? 2 : 1) * kBlkWaves;  // (each wave's first op is wlo + wave)
   stores_done();
   __syncthreads();
   if (t == 0) s_t_start = wall_clock64();
@@ -3543,17 +3560,34 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
       for (int u = 0; u < 4; ++u) vo[u] = load_row_rmw(rc.pold + (uint32_t)(u * kRowBytes + lo16));
     }
   }
+#if H3C_AF_PRE2
+  uint32_t jn = jc != kNil ? j1 : kNil;
+#else
   uint32_t jn = jc != kNil ? grab() : kNil;
+#endif
   if (jn >= whi) jn = kNil;
   if (jn != kNil) rec_of(jn, rn);
-  while (jc != kNil) {
-    uint4 wn[4], wo[4];
-    const bool nvalid = jn != kNil;
+#if H3C_AF_PRE2
+  if (jn != kNil && rn.pold != spec_old1) {  // (not its block's first op: its old rows are a payload)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      wn[u] = nvalid ? load_row_rmw(rn.pnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
-      wo[u] = nvalid ? load_row_old(rn.pold + (uint32_t)(u * kRowBytes + lo16), rn.first) : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < 4; ++u) wo[u] = load_row_rmw(rn.pold + (uint32_t)(u * kRowBytes + lo16));
+  }
+  bool preloaded = true;
+#else
+  const bool preloaded = false;
+#endif
+  while (jc != kNil) {
+    const bool nvalid = jn != kNil;
+    if (!preloaded) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        wn[u] = nvalid ? load_row_rmw(rn.pnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+        wo[u] = nvalid ? load_row_old(rn.pold + (uint32_t)(u * kRowBytes + lo16), rn.first) : make_uint4(0, 0, 0, 0);
+      }
     }
+#if H3C_AF_PRE2
+    preloaded = false;
+#endif
     uint32_t jnn = nvalid ? grab() : kNil;  // (the op after next: its record loads meanwhile)
     if (jnn >= whi) jnn = kNil;
     Rec rnn{};
