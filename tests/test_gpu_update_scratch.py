@@ -144,3 +144,49 @@ def test_scratch_threads_on_one_stream(h3c, torch_dev, hooks):
     for t in th:
         t.join()
     assert not errors, errors
+
+
+def test_fused_path_chunk_boundaries_inside_cache_lines(h3c, torch_dev, hooks):
+    """Chunks laid out 64 bytes past a 128-byte line boundary, so every chunk boundary falls inside a cache
+    line: writes to the last block of chunk c and the first block of chunk c+1 touch the same lines from
+    different workgroups (the fused path's write-back is by plain stores since round 5, held in each XCD's
+    L2 until the launch ends).  Bytes and checksums against the oracle."""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_SCAN, h3c.UPD_SCAN_PATHS["fused"])
+    rng = np.random.default_rng(505)
+    nchunks, clen = 16, 64 << 10
+    bpc = clen // G
+    host = rng.integers(0, 256, (nchunks, clen), dtype=np.uint8)
+    buf = torch.zeros(nchunks * clen + 256, dtype=torch.uint8, device=dev)
+    off = 64 + (-buf.data_ptr()) % 128  # every chunk starts 64 bytes into a 128-byte line
+    assert (buf.data_ptr() + off) % 128 == 64 and off + nchunks * clen <= buf.numel()
+    view = buf[off: off + nchunks * clen].view(nchunks, clen)
+    view.copy_(torch.from_numpy(host))
+    bases = torch.tensor([view[c].data_ptr() for c in range(nchunks)], dtype=torch.int64, device=dev)
+    raw = np.array([orc.crc32c(host[c]) for c in range(nchunks)], dtype=np.uint32)
+    for it in range(3):
+        wc, wb = [], []
+        for c in range(nchunks):  # each chunk's first and last block, in an order that spreads them apart
+            wc += [c, c]
+            wb += [0, bpc - 1]
+        extra = 3000
+        wc += list(rng.integers(0, nchunks, extra))
+        wb += list(rng.integers(0, bpc, extra))
+        order = rng.permutation(len(wc))
+        wc = np.array(wc, dtype=np.uint32)[order]
+        wb = np.array(wb, dtype=np.uint32)[order]
+        n = len(wc)
+        pay = rng.integers(0, 256, (n, G), dtype=np.uint8)
+        out = torch.zeros(n, dtype=torch.int32, device=dev)
+        raw_out = torch.zeros(nchunks, dtype=torch.int32, device=dev)
+        h3c.update_blocks(bases, clen, i32(raw, torch, dev), i32(wc, torch, dev), i32(wb, torch, dev),
+                          torch.from_numpy(pay).to(dev), out, raw_out)
+        torch.cuda.synchronize()
+        for k in range(n):
+            host[wc[k], wb[k] * G:(wb[k] + 1) * G] = pay[k]
+        want = np.array([orc.crc32c(host[c]) for c in range(nchunks)], dtype=np.uint32)
+        got = raw_out.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, want), (it, np.nonzero(got != want)[0][:8])
+        assert np.array_equal(view.cpu().numpy(), host), it
+        assert int(buf[:off].sum().item()) == 0 and int(buf[off + nchunks * clen:].sum().item()) == 0  # no stray bytes
+        raw = want
