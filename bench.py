@@ -1044,6 +1044,10 @@ def main() -> int:
         res["rehearsal"] = True
         res["n_gpus"] = devices_used(cx.world, cx.ndev)
         res["config"]["ranks"] = cx.world
+        for sub in ("hostfed", "update"):  # (the sub-passes' n_gpus by the same rule)
+            if sub in res:
+                res[sub]["n_gpus"] = res["n_gpus"]
+                res[sub]["ranks"] = cx.world
     res["config"]["launcher"] = "bench.py --gpus (spawned ranks)" if os.environ.get("H3C_BENCH_LAUNCHED") \
         else ("torchrun" if cx.world > 1 else "single process")
     if cx.rank == 0:
