@@ -3161,7 +3161,7 @@ __global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uin
 // the workgroup's blockIdx and hardware XCC id
 __device__ unsigned long long g_af_wg[1024 * 5];
 __device__ unsigned long long g_af_wave[1024 * 16];
-__device__ uint32_t g_af_blk[1024 * 2];
+__device__ uint32_t g_af_blk[1024 * 4];  // per ticket: blockIdx, XCC, range start, range end
 __device__ uint32_t g_af_fin[1024 * 16];  // per wave: its ops whose block has later writes (the fin path)
 #endif
 #ifndef H3C_AF_EARLY_OLD
@@ -3366,10 +3366,12 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   if (t < 16 && L < 1024) g_af_fin[16 * L + t] = 0;
   if (t == 0 && L < 1024) {
     g_af_wg[5 * L] = wall_clock64();
-    g_af_blk[2 * L] = blockIdx.x;
+    g_af_blk[4 * L] = blockIdx.x;
+    g_af_blk[4 * L + 2] = s_wlo;
+    g_af_blk[4 * L + 3] = s_whi;
     uint32_t xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g_af_blk[2 * L + 1] = xcc;
+    g_af_blk[4 * L + 1] = xcc;
   }
 #endif
   const uint32_t poly = pc->poly;
@@ -5727,7 +5729,7 @@ extern "C" int h3c_diag_af_trace(unsigned long long *out, int n) {  // (trace bu
 }
 extern "C" int h3c_diag_af_waves(unsigned long long *out, uint32_t *blk, uint32_t *fin, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_af_wave), 128ull * (unsigned)n) == hipSuccess &&
-                 hipMemcpyFromSymbol(blk, HIP_SYMBOL(g_af_blk), 8ull * (unsigned)n) == hipSuccess &&
+                 hipMemcpyFromSymbol(blk, HIP_SYMBOL(g_af_blk), 16ull * (unsigned)n) == hipSuccess &&
                  hipMemcpyFromSymbol(fin, HIP_SYMBOL(g_af_fin), 64ull * (unsigned)n) == hipSuccess
              ? 0
              : -1;

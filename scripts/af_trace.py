@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.argv = [sys.argv[0], "--workload", "updio", "--no-cpu-baseline", "--steps", "5", "--warmup", "5",
+sys.argv = [sys.argv[0], "--workload", "updio", "--no-cpu-baseline", "--steps", "5", "--warmup", "30",
             "--updio-graphs", "0"]
 bench = importlib.import_module("bench")
 h3c = importlib.import_module("3fs_amd")
@@ -37,20 +37,24 @@ corr = np.corrcoef(np.arange(nwg), us[:, 2] - us[:, 1])[0, 1]
 print("corr(ticket, loop time) = %.2f" % corr)
 lib.h3c_diag_af_waves.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 wv = (ctypes.c_ulonglong * (16 * 1024))()
-bk = (ctypes.c_uint32 * (2 * 1024))()
+bk = (ctypes.c_uint32 * (4 * 1024))()
 fn = (ctypes.c_uint32 * (16 * 1024))()
 assert lib.h3c_diag_af_waves(wv, bk, fn, 1024) == 0
 fin = np.array(fn[:16 * nwg]).reshape(nwg, 16)
 w = (np.array(wv[:16 * nwg], dtype=np.float64).reshape(nwg, 16) - t0) / (khz / 1000.0)
-blk = np.array(bk[:2 * nwg]).reshape(nwg, 2)
+blk = np.array(bk[:4 * nwg]).reshape(nwg, 4)
+ops = (blk[:, 3] - blk[:, 2]).astype(np.float64)
+loop = us[:, 2] - us[:, 1]
 spread = w.max(1) - w.min(1)
 print("per-wg wave spread (max - min wave end): median %.1f max %.1f" % (np.median(spread), spread.max()))
 print("wave ends: q0 %.1f q50 %.1f q90 %.1f q100 %.1f" % tuple(np.percentile(w, [0, 50, 90, 100])))
 for x in range(8):
     m = blk[:, 1] == x
     if m.any():
-        print("xcc %d: %3d wgs, loop_end median %.1f max %.1f, mean wave end %.1f, mean ticket %.0f, fin ops/wave %.2f" % (
-            x, m.sum(), np.median(us[m, 2]), us[m, 2].max(), w[m].mean(), np.arange(nwg)[m].mean(), fin[m].mean()))
+        print("xcc %d: %3d wgs, loop_end median %.1f max %.1f, mean wave end %.1f, mean ticket %.0f, fin ops/wave %.2f, "
+              "ops/wg %.1f, loop %.1f us, ops/us %.3f" % (
+            x, m.sum(), np.median(us[m, 2]), us[m, 2].max(), w[m].mean(), np.arange(nwg)[m].mean(), fin[m].mean(),
+            ops[m].mean(), loop[m].mean(), (ops[m] / loop[m]).mean()))
 wl = (w - us[:, 1:2]).ravel()
 print("corr(wave time, fin ops) = %.2f; fin ops/wave by ticket quartile:" % np.corrcoef(wl, fin.ravel())[0, 1],
       [round(float(fin[q * nwg // 4:(q + 1) * nwg // 4].mean()), 2) for q in range(4)])
