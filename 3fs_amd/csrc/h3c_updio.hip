@@ -3181,6 +3181,9 @@ constexpr uint32_t kAClasses = 8;
 constexpr uint32_t kAOne = 1u << 16;  // weight 1.0
 constexpr uint32_t kADoneVoid = 1u << 12;    // kADone: finished workgroups (low 12 bits) + void reports << 12
 constexpr uint32_t kASpin = 1u << 22;        // bounded look-back spins (about a quarter second)
+#ifndef H3C_AF_EARLY_AGG
+#define H3C_AF_EARLY_AGG 0  // 1: the workgroup's per-chunk sums kept during the loop, its look-back before phase 2
+#endif
 #ifndef H3C_AF_PRE2
 #define H3C_AF_PRE2 0  // 1: each wave's first two ops load their rows before phase 0
 #endif
@@ -3333,6 +3336,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   __shared__ h3c_chunk_state s_cs[kFastChunksLds];
   __shared__ uint32_t s_ticket, s_E, s_slow, s_last, s_void, s_prev, s_grab, s_wlo, s_whi;
   __shared__ uint64_t s_t_start;
+  __shared__ uint32_t s_eagg[H3C_AF_EARLY_AGG ? kFastCols : 1];  // (the workgroup's per-chunk sums, kept in the loop)
   const uint32_t t = threadIdx.x, lane = t & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const uint32_t cls = blockIdx.x % kAClasses;  // (one XCD per class: workgroups are dealt round-robin)
@@ -3357,6 +3361,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     s_whi = s_ticket + 1 == gridDim.x ? n : (uint32_t)((cum + wmine) * n / wt);
   }
   if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
+  if (H3C_AF_EARLY_AGG && t < kFastCols) s_eagg[t] = 0;
   __syncthreads();
   const uint32_t E = s_E, L = s_ticket, nwg = gridDim.x;
   // the kernel's own span (bench / profiling): the first ticket's start (one store, not one atomic per
@@ -3487,6 +3492,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     uint64_t pnew, pold, fin;
     uint32_t exp, fexp;
     bool first;
+    uint32_t c, off;  // (H3C_AF_EARLY_AGG: the delta's shift)
   };
 #if H3C_AF_LAZY
   // the op's record made by the wave when it takes the op (scalar loads: j is wave-uniform), instead of a
@@ -3537,6 +3543,10 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     r.fin = (uint64_t)b.x | ((uint64_t)b.y << 32);
     r.exp = b.z;
     r.fexp = b.w;
+    if (H3C_AF_EARLY_AGG) {
+      r.c = ios[j].chunk;
+      r.off = ios[j].offset;
+    }
   };
 #endif
 #if H3C_AF_STATIC
@@ -3644,6 +3654,10 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
       aa.dv[jc] = ((unsigned long long)(pass ? 1u : 2u) << 32) | D;
       aa.pv[jc].x = P;
     }
+    if (H3C_AF_EARLY_AGG && pass) {  // the op's shifted delta into the wave's per-chunk sums (lane c: c, c + 64)
+      const uint32_t v = dgf_mul(D, dxpow8_fast((int64_t)s_cs[rc.c].size - (int64_t)rc.off - (int64_t)kBlk, pc, poly), poly);
+      if (lane == 0) atomicXor(&s_eagg[rc.c], v);
+    }
     if (!pass) wave_void = 1;
     jc = jn;
     rc = rn;
@@ -3670,38 +3684,40 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
 #if H3C_AF_TRACE
   if (t == 0 && L < 1024) g_af_wg[5 * L + 2] = wall_clock64();
 #endif
-  // ---- phase 2: per wave, its contiguous share of the workgroup's ops in sequence order: each op's delta
-  // moved to its chunk's end, the chunk XOR right after it (lanes: one op each, in groups of 64), the
-  // running per-chunk XORs (lane c: chunks c and c + 64) ----
   uint32_t acc0 = 0, acc1 = 0;
   uint32_t my_ip = 0, my_pass = 0, my_c = kNil;
-  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
-    const uint32_t cnt = min(64u, hi - g0), k = g0 + lane;
-    uint32_t v = 0;
-    my_c = kNil;
-    my_pass = 0;
-    if (lane < cnt) {
-      const unsigned long long key = aa.key[k];
-      const unsigned long long g = ld_agent(&aa.dv[k]);  // (another wave's store, before the barrier)
-      my_c = (uint32_t)(key >> 36);
-      my_pass = (uint32_t)(g >> 32) == 1u;
-      if (my_pass) {  // x^(8(size - offset - 4096)), the offset from the key's block address
-        const h3c_chunk_state &cs = s_cs[my_c];
-        const int64_t off = (int64_t)((key & ((1ull << 36) - 1)) << 12) - (int64_t)cs.base;
-        v = dgf_mul((uint32_t)g, dxpow8_fast((int64_t)cs.size - off - (int64_t)kBlk, pc, poly), poly);
+  auto phase2 = [&]() {
+    // ---- phase 2: per wave, its contiguous share of the workgroup's ops in sequence order: each op's delta
+    // moved to its chunk's end, the chunk XOR right after it (lanes: one op each, in groups of 64), the
+    // running per-chunk XORs (lane c: chunks c and c + 64) ----
+    for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
+      const uint32_t cnt = min(64u, hi - g0), k = g0 + lane;
+      uint32_t v = 0;
+      my_c = kNil;
+      my_pass = 0;
+      if (lane < cnt) {
+        const unsigned long long key = aa.key[k];
+        const unsigned long long g = ld_agent(&aa.dv[k]);  // (another wave's store, before the barrier)
+        my_c = (uint32_t)(key >> 36);
+        my_pass = (uint32_t)(g >> 32) == 1u;
+        if (my_pass) {  // x^(8(size - offset - 4096)), the offset from the key's block address
+          const h3c_chunk_state &cs = s_cs[my_c];
+          const int64_t off = (int64_t)((key & ((1ull << 36) - 1)) << 12) - (int64_t)cs.base;
+          v = dgf_mul((uint32_t)g, dxpow8_fast((int64_t)cs.size - off - (int64_t)kBlk, pc, poly), poly);
+        }
       }
+      const uint32_t src = my_c & 63;
+      const uint32_t r0 = __shfl(acc0, src, 64), r1 = __shfl(acc1, src, 64);
+      my_ip = my_c < 64 ? r0 : r1;
+      for (uint32_t u0 = 0; u0 < cnt; ++u0) {
+        const uint32_t ct = __builtin_amdgcn_readlane(my_c, u0), vt = __builtin_amdgcn_readlane(v, u0);
+        if (lane >= u0 && my_c == ct) my_ip ^= vt;
+        if (ct == lane) acc0 ^= vt;
+        if (ct == lane + 64) acc1 ^= vt;
+      }
+      if (hi - lo > 64 && lane < cnt) aa.inp[k] = my_ip;
     }
-    const uint32_t src = my_c & 63;
-    const uint32_t r0 = __shfl(acc0, src, 64), r1 = __shfl(acc1, src, 64);
-    my_ip = my_c < 64 ? r0 : r1;
-    for (uint32_t u0 = 0; u0 < cnt; ++u0) {
-      const uint32_t ct = __builtin_amdgcn_readlane(my_c, u0), vt = __builtin_amdgcn_readlane(v, u0);
-      if (lane >= u0 && my_c == ct) my_ip ^= vt;
-      if (ct == lane) acc0 ^= vt;
-      if (ct == lane + 64) acc1 ^= vt;
-    }
-    if (hi - lo > 64 && lane < cnt) aa.inp[k] = my_ip;
-  }
+  };
   // the chunks' base checksums (trusted stored values), one per lane (chunks lane, lane + 64)
   auto t0_of = [&](uint32_t c) -> uint32_t {
     return c < nchunks ? (std_domain ? ~s_cs[c].value : s_cs[c].value) : 0u;
@@ -3710,61 +3726,77 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   // ---- chunk aggregates: waves of the workgroup (LDS), then workgroups (look-back in ticket order) ----
   uint32_t *wagg = lds;                                 // [16][128]
   uint32_t *wexcl = lds + kBlkWaves * kFastCols;        // [128]: the workgroup's exclusive prefix
-  wagg[wave * kFastCols + lane] = acc0;
-  wagg[wave * kFastCols + 64 + lane] = acc1;
-  __syncthreads();
-  if (wave == 0) {
-    uint32_t a0 = 0, a1 = 0;
-    for (uint32_t w = 0; w < kBlkWaves; ++w) {
-      a0 ^= wagg[w * kFastCols + lane];
-      a1 ^= wagg[w * kFastCols + 64 + lane];
-    }
-    const bool two = nchunks > 64;
-    unsigned long long *row = aa.gran + (uint64_t)L * kFastCols;
-    uint32_t x0 = 0, x1 = 0;
-    if (L > 0) {
-      if (lane < nchunks) st_agent(&row[lane], agran(E, 1u, a0));
-      if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], agran(E, 1u, a1));
-      int j0 = lane < nchunks ? (int)L - 1 : -1, j1 = two && lane + 64 < nchunks ? (int)L - 1 : -1;
-      const uint32_t limit = (force_void & 1) && L == 1 ? 0u : kASpin;  // (test hook: ticket 1 gives up at once)
-      for (uint32_t spins = 0; __builtin_amdgcn_ballot_w64(j0 >= 0 || j1 >= 0) != 0;) {
-        bool moved = false;
-        auto look = [&](int &j, uint32_t &x, uint32_t col) {
-          if (j < 0) return;
-          const int top = j;
-          unsigned long long g[kALookWin];
-#pragma unroll
-          for (int w = 0; w < (int)kALookWin; ++w)
-            g[w] = top - w >= 0 ? ld_agent(&aa.gran[(uint64_t)(top - w) * kFastCols + col]) : 0ull;
-#pragma unroll
-          for (int w = 0; w < (int)kALookWin; ++w) {
-            const uint32_t state = agran_state(g[w], E);
-            if (top - w >= 0 && j == top - w && state) {
-              x ^= (uint32_t)g[w];
-              j = state == 2u ? -1 : j - 1;
-              moved = true;
+  auto lookback = [&]() {  // wave 0: the workgroup's sums (wagg) published, the look-back, the inclusive sums
+    if (wave == 0) {
+      uint32_t a0 = 0, a1 = 0;
+      for (uint32_t w = 0; w < kBlkWaves; ++w) {
+        a0 ^= wagg[w * kFastCols + lane];
+        a1 ^= wagg[w * kFastCols + 64 + lane];
+      }
+      const bool two = nchunks > 64;
+      unsigned long long *row = aa.gran + (uint64_t)L * kFastCols;
+      uint32_t x0 = 0, x1 = 0;
+      if (L > 0) {
+        if (lane < nchunks) st_agent(&row[lane], agran(E, 1u, a0));
+        if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], agran(E, 1u, a1));
+        int j0 = lane < nchunks ? (int)L - 1 : -1, j1 = two && lane + 64 < nchunks ? (int)L - 1 : -1;
+        const uint32_t limit = (force_void & 1) && L == 1 ? 0u : kASpin;  // (test hook: ticket 1 gives up at once)
+        for (uint32_t spins = 0; __builtin_amdgcn_ballot_w64(j0 >= 0 || j1 >= 0) != 0;) {
+          bool moved = false;
+          auto look = [&](int &j, uint32_t &x, uint32_t col) {
+            if (j < 0) return;
+            const int top = j;
+            unsigned long long g[kALookWin];
+  #pragma unroll
+            for (int w = 0; w < (int)kALookWin; ++w)
+              g[w] = top - w >= 0 ? ld_agent(&aa.gran[(uint64_t)(top - w) * kFastCols + col]) : 0ull;
+  #pragma unroll
+            for (int w = 0; w < (int)kALookWin; ++w) {
+              const uint32_t state = agran_state(g[w], E);
+              if (top - w >= 0 && j == top - w && state) {
+                x ^= (uint32_t)g[w];
+                j = state == 2u ? -1 : j - 1;
+                moved = true;
+              }
             }
-          }
-        };
-        look(j0, x0, lane);
-        look(j1, x1, 64 + lane);
-        if (__builtin_amdgcn_ballot_w64(moved) == 0 || limit == 0) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > limit) {  // a predecessor never published: the pass is void (uio_afix_kernel)
-            if (lane == 0) s_void = 1;
-            break;
+          };
+          look(j0, x0, lane);
+          look(j1, x1, 64 + lane);
+          if (__builtin_amdgcn_ballot_w64(moved) == 0 || limit == 0) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > limit) {  // a predecessor never published: the pass is void (uio_afix_kernel)
+              if (lane == 0) s_void = 1;
+              break;
+            }
           }
         }
       }
+      if (lane < nchunks) st_agent(&row[lane], agran(E, 2u, x0 ^ a0));
+      if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], agran(E, 2u, x1 ^ a1));
+      wexcl[lane] = x0;
+      wexcl[64 + lane] = x1;
+  #if H3C_AF_TRACE
+      if (lane == 0 && L < 1024) g_af_wg[5 * L + 3] = wall_clock64();
+  #endif
     }
-    if (lane < nchunks) st_agent(&row[lane], agran(E, 2u, x0 ^ a0));
-    if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], agran(E, 2u, x1 ^ a1));
-    wexcl[lane] = x0;
-    wexcl[64 + lane] = x1;
-#if H3C_AF_TRACE
-    if (lane == 0 && L < 1024) g_af_wg[5 * L + 3] = wall_clock64();
+  };
+#if H3C_AF_EARLY_AGG
+  // the workgroup's sums were kept during the loop: its look-back runs first (the later workgroups wait on
+  // it), the in-order per-op prefix after it
+  for (uint32_t c = t; c < kBlkWaves * kFastCols; c += kBlkThreads) wagg[c] = c < kFastCols ? s_eagg[c] : 0u;  // (row 0)
+  __syncthreads();
+  lookback();
+  __syncthreads();
+  phase2();
+  wagg[wave * kFastCols + lane] = acc0;  // (each wave share's sums, for the in-workgroup prefix)
+  wagg[wave * kFastCols + 64 + lane] = acc1;
+#else
+  phase2();
+  wagg[wave * kFastCols + lane] = acc0;
+  wagg[wave * kFastCols + 64 + lane] = acc1;
+  __syncthreads();
+  lookback();
 #endif
-  }
   __syncthreads();
   // every op's result: its chunk's checksum right after it (ChunkReplica.cc:174, :311; a failed op reports
   // the stored checksum unchanged, engine.rs:303 in the std domain)
