@@ -190,7 +190,8 @@ __global__ __launch_bounds__(kLinkTile) void upd_tlink_kernel(const uint32_t *__
   __shared__ TileGroups<kLinkTile> g;
   const uint32_t t = threadIdx.x, i0 = blockIdx.x * kLinkTile, i = i0 + t;
   const uint32_t E = ctl[kCtlEpoch] & 0xFFu;  // (0 in a zeroed workspace)
-  if (stat && blockIdx.x == 0) {  // the fused kernel's range weights from the previous batch's throughput
+  if (stat && blockIdx.x == gridDim.x - 1) {  // (a block of its own, no writes) the fused kernel's range weights
+                                              // from the previous batch's throughput
     __shared__ unsigned long long w_ops[kClasses], w_ticks[kClasses];
     if (t < kClasses) w_ops[t] = w_ticks[t] = 0;
     __syncthreads();
@@ -222,6 +223,7 @@ __global__ __launch_bounds__(kLinkTile) void upd_tlink_kernel(const uint32_t *__
         }
       }
     }
+    return;
   }
   uint32_t key = kNone;
   if (i < n) {
@@ -1325,7 +1327,7 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
   }
   // previous-writer links: tile match + hash of per-tile last writers (no sort)
   const uint32_t nlt = (n_blocks + kLinkTile - 1) / kLinkTile;
-  hipLaunchKernelGGL(upd_tlink_kernel, dim3(nlt), dim3(kLinkTile), 0, st, blk_chunk_dev, blk_index_dev, n_blocks,
+  hipLaunchKernelGGL(upd_tlink_kernel, dim3(nlt + (us ? 1 : 0)), dim3(kLinkTile), 0, st, blk_chunk_dev, blk_index_dev, n_blocks,
                      nchunks, bpc, w.hhead, w.hcap - 1, w.nkey, w.next, w.prev, w.ctl, w.touched, tagged,
                      us ? us->p + kUsStat : nullptr, kFusedMaxWG);
   HIP_TRY(hipGetLastError());

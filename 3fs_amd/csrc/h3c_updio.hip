@@ -3244,7 +3244,8 @@ __global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *
   const uint32_t E = aa.ctl[kAEpoch] & 0xFFu;  // (written by the previous batch's last workgroup)
   if (blockIdx.x == 0 && t < kMiscWords) misc[t] = t == kMiscT0 || t == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;
   if (blockIdx.x == 0 && t < kCtrN) ctr[t] = 0;
-  if (blockIdx.x == 0) {  // the workgroup classes' range weights from the previous batch's throughput
+  if (blockIdx.x == gridDim.x - 1) {  // (a block of its own, no ops) the workgroup classes' range weights from the
+                                      // previous batch's throughput
     __shared__ unsigned long long w_ops[kAClasses], w_ticks[kAClasses];
     if (t < kAClasses) w_ops[t] = w_ticks[t] = 0;
     __syncthreads();
@@ -3276,6 +3277,7 @@ __global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *
         }
       }
     }
+    return;
   }
   for (uint32_t e = t; e < 2 * kATile; e += kATile) {
     g_key[e] = kNoKey;
@@ -5089,7 +5091,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     // (test hook H3C_HOOK_UPD_GIVEUP bit 3: ticket 1 gives up its look-back; bit 4: the pass reports itself void)
     const uint32_t force_void = ((giveup & 8) ? 1u : 0u) | ((giveup & 16) ? 2u : 0u);
     auto a_launch = [&](hipStream_t q) -> int {
-      hipLaunchKernelGGL(uio_aprep_kernel, dim3((n + kATile - 1) / kATile), dim3(kATile), 0, q, d_ios, n, d_chunks,
+      hipLaunchKernelGGL(uio_aprep_kernel, dim3((n + kATile - 1) / kATile + 1), dim3(kATile), 0, q, d_ios, n, d_chunks,
                          nchunks, poly_type, stdf, d_misc, d_ctr, aa);
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(uio_afused_kernel, dim3(nwg_a), dim3(kBlkThreads), 0, q, d_ios, n, d_chunks, d_chunks_out,
