@@ -73,6 +73,9 @@ __device__ __forceinline__ void store_row(uint64_t a, uint4 v) {
 #endif
 }
 
+#ifndef H3C_UPD_EARLY_FILL
+#define H3C_UPD_EARLY_FILL 1  // the fused kernel's CRC tables fill before the range is known (0: after the first group starts)
+#endif
 #ifndef H3C_UPD_WG_BAL
 #define H3C_UPD_WG_BAL 1  // fused path: the fewest workgroups that keep the most writes per wave
 #endif
@@ -524,6 +527,9 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     s_whi = s_ticket + 1 == gridDim.x ? n : (uint32_t)((cum + wmine) * n / wt);
     s_E = __hip_atomic_load(&ctl[kCtlEpoch], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFFu;
   }
+  // the CRC tables fill while thread 0 takes the ticket (waves 1-15; they do not depend on the range)
+  if (H3C_UPD_EARLY_FILL && threadIdx.x >= 64)
+    fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x - 64, kThreads - 64);
   __syncthreads();
   const uint32_t L = s_ticket, nwg = gridDim.x, E = s_E;
   const uint32_t lane = threadIdx.x & 63;
@@ -599,7 +605,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     }
   };
   if (lo < hi) start_group(lo);  // the first group's links and rows load while the tables fill
-  fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kThreads);
+  if (!H3C_UPD_EARLY_FILL) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kThreads);
   __syncthreads();
   if (threadIdx.x == 0) s_t0 = wall_clock64();
   const uint32_t *red = lds + kLdsWords;

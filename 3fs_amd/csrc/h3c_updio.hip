@@ -3181,6 +3181,9 @@ constexpr uint32_t kAClasses = 8;
 constexpr uint32_t kAOne = 1u << 16;  // weight 1.0
 constexpr uint32_t kADoneVoid = 1u << 12;    // kADone: finished workgroups (low 12 bits) + void reports << 12
 constexpr uint32_t kASpin = 1u << 22;        // bounded look-back spins (about a quarter second)
+#ifndef H3C_AF_EARLY_FILL
+#define H3C_AF_EARLY_FILL 1  // the CRC tables fill before the range is known (beside thread 0's ticket; 0: after phase 0)
+#endif
 #ifndef H3C_AF_EARLY_AGG
 #define H3C_AF_EARLY_AGG 0  // 1: the workgroup's per-chunk sums kept during the loop, its look-back before phase 2
 #endif
@@ -3364,6 +3367,8 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   }
   if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
   if (H3C_AF_EARLY_AGG && t < kFastCols) s_eagg[t] = 0;
+  // the CRC tables fill while thread 0 takes the ticket (waves 1-15; they do not depend on the range)
+  if (H3C_AF_EARLY_FILL && t >= 64) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t - 64, kBlkThreads - 64);
   __syncthreads();
   const uint32_t E = s_E, L = s_ticket, nwg = gridDim.x;
   // the kernel's own span (bench / profiling): the first ticket's start (one store, not one atomic per
@@ -3476,7 +3481,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     aa.rec[2 * (size_t)j + 1] = make_uint4((uint32_t)fin, (uint32_t)(fin >> 32), exp, fexp);
     aa.pv[j].y = prev;  // (uio_afix_kernel's input; crc0(new) follows in .x)
   }
-  fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
+  if (!H3C_AF_EARLY_FILL) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
   if (t == 0) s_grab = wlo + (H3C_AF_PRE2 ? 2 : 1) * kBlkWaves;  // (each wave's first op is wlo + wave)
   stores_done();
   __syncthreads();
