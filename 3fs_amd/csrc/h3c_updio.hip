@@ -3184,15 +3184,6 @@ constexpr uint32_t kASpin = 1u << 22;        // bounded look-back spins (about a
 #ifndef H3C_AF_EARLY_FILL
 #define H3C_AF_EARLY_FILL 1  // the CRC tables fill before the range is known (beside thread 0's ticket; 0: after phase 0)
 #endif
-#ifndef H3C_AF_EARLY_AGG
-#define H3C_AF_EARLY_AGG 0  // 1: the workgroup's per-chunk sums kept during the loop, its look-back before phase 2
-#endif
-#ifndef H3C_AF_PRE2
-#define H3C_AF_PRE2 0  // 1: each wave's first two ops load their rows before phase 0
-#endif
-#ifndef H3C_AF_LAZY
-#define H3C_AF_LAZY 0  // 1: each op's record made by the wave that takes it (no phase-0 pass)
-#endif
 #ifndef H3C_AF_STATIC
 #define H3C_AF_STATIC 0
 #endif
@@ -3341,7 +3332,6 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   __shared__ h3c_chunk_state s_cs[kFastChunksLds];
   __shared__ uint32_t s_ticket, s_E, s_slow, s_last, s_void, s_prev, s_grab, s_wlo, s_whi;
   __shared__ uint64_t s_t_start;
-  __shared__ uint32_t s_eagg[H3C_AF_EARLY_AGG ? kFastCols : 1];  // (the workgroup's per-chunk sums, kept in the loop)
   const uint32_t t = threadIdx.x, lane = t & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const uint32_t cls = blockIdx.x % kAClasses;  // (one XCD per class: workgroups are dealt round-robin)
@@ -3366,7 +3356,6 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     s_whi = s_ticket + 1 == gridDim.x ? n : (uint32_t)((cum + wmine) * n / wt);
   }
   if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
-  if (H3C_AF_EARLY_AGG && t < kFastCols) s_eagg[t] = 0;
   // the CRC tables fill while thread 0 takes the ticket (waves 1-15; they do not depend on the range)
   if (H3C_AF_EARLY_FILL && t >= 64) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t - 64, kBlkThreads - 64);
   __syncthreads();
@@ -3434,20 +3423,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     }
   }
   uint4 wn[4], wo[4];  // (the next op's rows)
-#if H3C_AF_PRE2  // each wave's second op is wlo + 16 + wave: its rows load before phase 0 too
-  const uint32_t j1 = wlo + kBlkWaves + wave;
-  uint64_t spec_old1 = 0;
-  if (j0 < whi && j1 < whi) {
-    const h3c_update_io io1 = ios[j1];
-    spec_old1 = s_cs[io1.chunk].base + io1.offset;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      wn[u] = load_row_rmw(io1.payload + (uint32_t)(u * kRowBytes + lo16));
-      wo[u] = load_row_old(spec_old1 + (uint32_t)(u * kRowBytes + lo16), true);
-    }
-  }
-#endif
-  for (uint32_t j = wlo + t; j < (H3C_AF_LAZY ? wlo : whi); j += kBlkThreads) {
+  for (uint32_t j = wlo + t; j < whi; j += kBlkThreads) {
     const h3c_update_io io = ios[j];
     const uint4 lk = aa.link[j];
     const h3c_chunk_state &cs = s_cs[io.chunk];  // (aprep: every op's chunk is < nchunks <= 128)
@@ -3482,7 +3458,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     aa.pv[j].y = prev;  // (uio_afix_kernel's input; crc0(new) follows in .x)
   }
   if (!H3C_AF_EARLY_FILL) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
-  if (t == 0) s_grab = wlo + (H3C_AF_PRE2 ? 2 : 1) * kBlkWaves;  // (each wave's first op is wlo + wave)
+  if (t == 0) s_grab = wlo + kBlkWaves;  // (each wave's first op is wlo + wave)
   stores_done();
   __syncthreads();
   if (t == 0) s_t_start = wall_clock64();
@@ -3499,48 +3475,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     uint64_t pnew, pold, fin;
     uint32_t exp, fexp;
     bool first;
-    uint32_t c, off;  // (H3C_AF_EARLY_AGG: the delta's shift)
   };
-#if H3C_AF_LAZY
-  // the op's record made by the wave when it takes the op (scalar loads: j is wave-uniform), instead of a
-  // phase-0 pass over the workgroup's ops before the loop
-  auto rec_of = [&](uint32_t j, Rec &r) {
-    const h3c_update_io io = ios[j];
-    const uint4 lk = aa.link[j];
-    const uint32_t exp = aexpect(io.checksum_value, std_domain, k4096);
-    uint32_t prev = lk.x, fexp = 0;
-    uint64_t fin = 0;
-    bool first = false;
-    if (prev == kNil) {
-      const unsigned long long key = aa.key[j];
-      uint32_t fmax = j;
-      for (uint32_t e = aa.head[fast_bucket(key, aa.hmask)]; aentry_valid(e, E); e = aa.link[(e & 0xFFFFFFu) - 1].y) {
-        const uint32_t i = (e & 0xFFFFFFu) - 1;
-        if (i >= n) break;
-        if (aa.key[i] != key) continue;
-        if (i < j && (prev == kNil || i > prev)) prev = i;
-        fmax = max(fmax, i);
-      }
-      if (prev == kNil) {
-        first = true;
-        fin = io.payload;
-        fexp = exp;
-        if (fmax != j) {
-          const h3c_update_io fio = ios[fmax];
-          fin = fio.payload;
-          fexp = aexpect(fio.checksum_value, std_domain, k4096);
-        }
-      }
-    }
-    r.pnew = io.payload;
-    r.pold = first ? s_cs[io.chunk].base + io.offset : ios[prev].payload;
-    r.first = first;
-    r.fin = fin;
-    r.exp = exp;
-    r.fexp = fexp;
-    if (lane == 0) aa.pv[j].y = prev;  // (uio_afix_kernel's input)
-  };
-#else
   auto rec_of = [&](uint32_t j, Rec &r) {  // (scalar loads: j is wave-uniform)
     const uint4 a = aa.rec[2 * (size_t)j], b = aa.rec[2 * (size_t)j + 1];
     r.pnew = (uint64_t)a.x | ((uint64_t)a.y << 32);
@@ -3550,12 +3485,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     r.fin = (uint64_t)b.x | ((uint64_t)b.y << 32);
     r.exp = b.z;
     r.fexp = b.w;
-    if (H3C_AF_EARLY_AGG) {
-      r.c = ios[j].chunk;
-      r.off = ios[j].offset;
-    }
   };
-#endif
 #if H3C_AF_STATIC
   uint32_t next_static = j0 + 1;
   auto grab = [&]() -> uint32_t {
@@ -3579,34 +3509,16 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
       for (int u = 0; u < 4; ++u) vo[u] = load_row_rmw(rc.pold + (uint32_t)(u * kRowBytes + lo16));
     }
   }
-#if H3C_AF_PRE2
-  uint32_t jn = jc != kNil ? j1 : kNil;
-#else
   uint32_t jn = jc != kNil ? grab() : kNil;
-#endif
   if (jn >= whi) jn = kNil;
   if (jn != kNil) rec_of(jn, rn);
-#if H3C_AF_PRE2
-  if (jn != kNil && rn.pold != spec_old1) {  // (not its block's first op: its old rows are a payload)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) wo[u] = load_row_rmw(rn.pold + (uint32_t)(u * kRowBytes + lo16));
-  }
-  bool preloaded = true;
-#else
-  const bool preloaded = false;
-#endif
   while (jc != kNil) {
     const bool nvalid = jn != kNil;
-    if (!preloaded) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        wn[u] = nvalid ? load_row_rmw(rn.pnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
-        wo[u] = nvalid ? load_row_old(rn.pold + (uint32_t)(u * kRowBytes + lo16), rn.first) : make_uint4(0, 0, 0, 0);
-      }
+    for (int u = 0; u < 4; ++u) {
+      wn[u] = nvalid ? load_row_rmw(rn.pnew + (uint32_t)(u * kRowBytes + lo16)) : make_uint4(0, 0, 0, 0);
+      wo[u] = nvalid ? load_row_old(rn.pold + (uint32_t)(u * kRowBytes + lo16), rn.first) : make_uint4(0, 0, 0, 0);
     }
-#if H3C_AF_PRE2
-    preloaded = false;
-#endif
     uint32_t jnn = nvalid ? grab() : kNil;  // (the op after next: its record loads meanwhile)
     if (jnn >= whi) jnn = kNil;
     Rec rnn{};
@@ -3660,10 +3572,6 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     if (lane == 0) {
       aa.dv[jc] = ((unsigned long long)(pass ? 1u : 2u) << 32) | D;
       aa.pv[jc].x = P;
-    }
-    if (H3C_AF_EARLY_AGG && pass) {  // the op's shifted delta into the wave's per-chunk sums (lane c: c, c + 64)
-      const uint32_t v = dgf_mul(D, dxpow8_fast((int64_t)s_cs[rc.c].size - (int64_t)rc.off - (int64_t)kBlk, pc, poly), poly);
-      if (lane == 0) atomicXor(&s_eagg[rc.c], v);
     }
     if (!pass) wave_void = 1;
     jc = jn;
@@ -3787,23 +3695,11 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   #endif
     }
   };
-#if H3C_AF_EARLY_AGG
-  // the workgroup's sums were kept during the loop: its look-back runs first (the later workgroups wait on
-  // it), the in-order per-op prefix after it
-  for (uint32_t c = t; c < kBlkWaves * kFastCols; c += kBlkThreads) wagg[c] = c < kFastCols ? s_eagg[c] : 0u;  // (row 0)
-  __syncthreads();
-  lookback();
-  __syncthreads();
-  phase2();
-  wagg[wave * kFastCols + lane] = acc0;  // (each wave share's sums, for the in-workgroup prefix)
-  wagg[wave * kFastCols + 64 + lane] = acc1;
-#else
   phase2();
   wagg[wave * kFastCols + lane] = acc0;
   wagg[wave * kFastCols + 64 + lane] = acc1;
   __syncthreads();
   lookback();
-#endif
   __syncthreads();
   // every op's result: its chunk's checksum right after it (ChunkReplica.cc:174, :311; a failed op reports
   // the stored checksum unchanged, engine.rs:303 in the std domain)
