@@ -3335,6 +3335,9 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   const uint32_t t = threadIdx.x, lane = t & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const uint32_t cls = blockIdx.x % kAClasses;  // (one XCD per class: workgroups are dealt round-robin)
+  // the kernel's own span (bench / profiling): the first-dispatched workgroup's entry (one store, not one
+  // atomic per workgroup on one address) and the last workgroup's end
+  if (t == 0 && blockIdx.x == 0) *reinterpret_cast<unsigned long long *>(misc + kMiscT0) = wall_clock64();
   if (t == 0) {
     s_E = ld_agent(&aa.ctl[kAEpoch]) & 0xFFu;
     s_slow = ld_agent(&aa.ctl[kASlow]);
@@ -3360,9 +3363,6 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   if (H3C_AF_EARLY_FILL && t >= 64) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t - 64, kBlkThreads - 64);
   __syncthreads();
   const uint32_t E = s_E, L = s_ticket, nwg = gridDim.x;
-  // the kernel's own span (bench / profiling): the first ticket's start (one store, not one atomic per
-  // workgroup on one address) and the last workgroup's end
-  if (t == 0 && L == 0) *reinterpret_cast<unsigned long long *>(misc + kMiscT0) = wall_clock64();
 #if H3C_AF_TRACE
   if (t < 16 && L < 1024) g_af_fin[16 * L + t] = 0;
   if (t == 0 && L < 1024) {
