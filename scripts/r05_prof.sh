@@ -12,7 +12,7 @@ prof() {  # tag kernel alg_bytes description workload [bench args]
     > /dev/null || exit 1
   echo "$tag ok"
 }
-prof headline seg_crc_kernel 8589934592 "bench.py: 8192 x 1 MiB device-resident chunks (BASELINE config 2)" verify --hostfed-extra-gib 0
+prof headline seg_crc_kernel 8589934592 "bench.py: 8192 x 1 MiB device-resident chunks (BASELINE config 2), no sub-passes" verify --hostfed-extra-gib 0 --update-extra 0
 prof small4k seg_uni_kernel 8589934592 "bench.py --chunks 2097152 --chunk-kib 4: 8 GiB of 4 KiB chunks (uniform small-chunk kernel, plain sub-line loads)" verify --chunks 2097152 --chunk-kib 4 --hostfed-extra-gib 0
 KT_STEPS=60 KT_WARMUP=20 prof upd upd_fused_kernel 1228800000 "bench.py --workload update: 100000 x 4 KiB writes into 64 x 64 MiB chunks (fused path)" update
 KT_STEPS=60 KT_WARMUP=20 prof updio uio_afused_kernel 1228800000 "bench.py --workload updio: 100000 x 4 KiB UpdateIOs into 64 x 64 MiB chunks (h3c_update_ios_dev, aligned sub-branch)" updio
