@@ -190,3 +190,41 @@ def test_fused_path_chunk_boundaries_inside_cache_lines(h3c, torch_dev, hooks):
         assert np.array_equal(view.cpu().numpy(), host), it
         assert int(buf[:off].sum().item()) == 0 and int(buf[off + nchunks * clen:].sum().item()) == 0  # no stray bytes
         raw = want
+
+
+def test_fused_path_captured_into_a_caller_graph(h3c, torch_dev, hooks):
+    """A caller that captures h3c_update_blocks into its own graph gets the workspace form (the per-stream
+    scratch is never baked into a capture): three replays of [update; raw_in <- raw_out] against the oracle."""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_SCAN, h3c.UPD_SCAN_PATHS["fused"])
+    rng = np.random.default_rng(506)
+    st = Store(torch, dev, rng, 8, 256 << 10)
+    st.batch(h3c, rng, 500)  # (the shift table is cached before the capture)
+    n = 3000
+    bpc = st.chunk_len // G
+    wc = rng.integers(0, st.nchunks, n).astype(np.uint32)
+    wb = rng.integers(0, bpc, n).astype(np.uint32)
+    pay = rng.integers(0, 256, (n, G), dtype=np.uint8)
+    d_wc, d_wb, d_pay = i32(wc, torch, dev), i32(wb, torch, dev), torch.from_numpy(pay).to(dev)
+    raw_in = i32(st.raw, torch, dev)
+    raw_out = torch.zeros_like(raw_in)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    ws = torch.empty(h3c.update_workspace_bytes(n, st.nchunks, st.chunk_len, G), dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        h3c.update_blocks(st.bases, st.chunk_len, raw_in, d_wc, d_wb, d_pay, out, raw_out, workspace=ws)
+        raw_in.copy_(raw_out)
+    torch.cuda.synchronize()
+    for rep in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        for k in range(n):
+            st.host[wc[k], wb[k] * G:(wb[k] + 1) * G] = pay[k]
+        want = np.zeros(st.nchunks, dtype=np.uint32)
+        orc.lib().orc_batch_crc32c(st.host.ctypes.data, st.chunk_len, st.nchunks, 0xFFFFFFFF, 8, 0, want.ctypes.data)
+        got = raw_out.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, want), (rep, np.nonzero(got != want)[0][:8])
+        assert np.array_equal(st.d.cpu().numpy(), st.host), rep
