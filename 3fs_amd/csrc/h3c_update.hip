@@ -1173,6 +1173,7 @@ struct UpdScratch {
   size_t words = 0;
   uint32_t hcap = 0, batches = 0;
   bool dirty = true;
+  bool fresh = true;  // newly allocated: its range weights are not learnt yet (zeroed with the rest)
   std::mutex mu;
 };
 std::mutex g_us_mu;
@@ -1216,13 +1217,19 @@ UpdScratch *upd_scratch(int dev, hipStream_t st, uint32_t hcap, std::unique_lock
     }
     s->words = words;
     s->dirty = true;
+    s->fresh = true;
   }
   if (s->dirty || s->hcap != hcap || s->batches >= kUsBatches) {
-    if (hipMemsetAsync(s->p, 0, 4 * (kUsHeads + (size_t)hcap), st) != hipSuccess) {
+    // (the range weights are kept across a re-zeroing: they describe the device, not the batches)
+    const size_t w0 = s->fresh ? kUsHeads + (size_t)hcap : kUsCtl + kCtlW, w1 = s->fresh ? w0 : kUsCtl + kCtlW + kClasses;
+    if (hipMemsetAsync(s->p, 0, 4 * w0, st) != hipSuccess ||
+        (w1 < kUsHeads + (size_t)hcap &&
+         hipMemsetAsync(s->p + w1, 0, 4 * (kUsHeads + (size_t)hcap - w1), st) != hipSuccess)) {
       (void)hipGetLastError();
       return nullptr;
     }
     s->dirty = false;
+    s->fresh = false;
     s->hcap = hcap;
     s->batches = 0;
   }

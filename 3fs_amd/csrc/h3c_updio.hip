@@ -4096,6 +4096,7 @@ struct FastScratch {
   bool dirty = true;
   uint32_t hcap = 0;      // the bucket count the heads were laid out for (another one: zeroed first)
   uint32_t abatches = 0;  // aligned batches since the last zeroing (the 8-bit epoch must not wrap onto live entries)
+  bool fresh = true;      // newly allocated: its aligned range weights are not learnt yet (zeroed with the rest)
 };
 struct ResPool {
   std::mutex mu;
@@ -4183,6 +4184,7 @@ FastScratch *fast_scratch(int dev, size_t words) {
   }
   f->words = w;
   f->dirty = true;
+  f->fresh = true;
   return f;
 }
 struct ScratchGuard {  // marks the scratch suspect unless the batch's outcome was read (disarm)
@@ -4970,9 +4972,13 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     aa.dv = fa.dv;
     if (fsc->dirty) {
       const uint32_t zw = kScratchHeads + 2 * hcap_fast, zg = std::min(1024u, (zw + 1023) / 1024);
-      hipLaunchKernelGGL(uio_zero_kernel, dim3(zg), dim3(256), 0, st, fsc->p, zw, nullptr, 0u, nullptr, 0u, nullptr, 0u);
+      // (the aligned range weights are kept across a re-zeroing: they describe the device, not the batches)
+      const uint32_t w0 = fsc->fresh ? zw : kScratchACtl + kAW, w1 = fsc->fresh ? zw : kScratchACtl + kAW + kAClasses;
+      hipLaunchKernelGGL(uio_zero_kernel, dim3(zg), dim3(256), 0, st, fsc->p, w0, fsc->p + w1, zw - w1, nullptr, 0u,
+                         nullptr, 0u);
       HIP_TRY(hipGetLastError());
       fsc->dirty = false;
+      fsc->fresh = false;
       fsc->hcap = hcap_fast;
       fsc->abatches = 0;
     }
