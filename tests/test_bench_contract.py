@@ -39,6 +39,20 @@ def test_roofline_update_workload_and_unmatched_sizes():
     assert r["traffic"] is None
 
 
+def test_roofline_config3_fused_kernels_carry_rocprof_and_the_phases_bound():
+    """Round 5: the fused config-3 kernels (plain write-back stores) carry the committed profile's rocprof
+    duration beside their own stamps, and the pattern ceiling is the phases bound (198.8 us per 100k writes)."""
+    b = load_bench()
+    per = 3 * 4096 * 100000
+    for kern in ("upd_fused_kernel", "uio_afused_kernel"):
+        r = b.roofline((0.225, 1, per), b.HBM_PEAK_GBPS, kernel=kern)
+        assert r["traffic"] is not None and abs(r["traffic"] / per - 1) < 0.05, (kern, r)
+        assert r["rocprof_avg_us"] > 0 and abs(r["frac_rocprof"] - per / (r["rocprof_avg_us"] * 1e-6) / 1e9 / 8000.0) < 1e-3
+        assert "timing_note" in r
+        assert abs(r["pattern_ceiling"]["achieved"] - per / 198.8e-6 / 1e9) < 2.0
+        assert os.path.exists(os.path.join(ROOT, r["pattern_ceiling"]["source"]))
+
+
 def _bench(args, env_extra=None, timeout=120):
     import json
     import subprocess
