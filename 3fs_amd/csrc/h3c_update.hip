@@ -137,6 +137,7 @@ constexpr uint32_t kLinkTile = H3C_LINK_TILE;
 enum { kCtlErr = 1, kCtlTimeout = 2, kCtlDone = 3, kCtlEpoch = 4, kCtlAcc = 8, kCtlW = 16, kCtlWords = 64 };
 constexpr uint32_t kClasses = 8;
 constexpr uint32_t kWOne = 1u << 16;  // weight 1.0
+__device__ uint32_t g_uw_seed[kClasses];  // the device's last learnt weights (0: none yet), seeding new scratches
 // Hash list entries: op index + 1 (0 ends a list) in a zeroed workspace; in an UpdScratch (`tagged`: never
 // cleared between batches) epoch << 24 | (op index + 1), so an entry of an earlier batch ends the list.
 constexpr uint32_t kTaggedMaxOps = (1u << 24) - 2;
@@ -223,7 +224,14 @@ __global__ __launch_bounds__(kLinkTile) void upd_tlink_kernel(const uint32_t *__
           double w = 0.5 * ((double)w0 / kWOne + rate[c] / mean);
           w = w < 0.5 ? 0.5 : w > 2.0 ? 2.0 : w;
           ctl[kCtlW + c] = (uint32_t)(w * kWOne);
+          __hip_atomic_store(&g_uw_seed[c], (uint32_t)(w * kWOne), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+      } else {  // a new scratch (no weights yet): the device's last learnt ones, from any stream's scratch
+        bool none = true;
+        for (uint32_t c = 0; c < kClasses; ++c) none = none && ctl[kCtlW + c] == 0;
+        if (none)
+          for (uint32_t c = 0; c < kClasses; ++c)
+            ctl[kCtlW + c] = __hip_atomic_load(&g_uw_seed[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     return;

@@ -3179,6 +3179,7 @@ constexpr uint32_t kAMaxOps = (1u << 24) - 2;  // bucket entries: epoch << 24 | 
 enum { kAEpoch = 0, kADone = 2, kASlow = 3, kADefer = 4, kAAcc = 8, kAW = 16, kACtlWords = 64 };
 constexpr uint32_t kAClasses = 8;
 constexpr uint32_t kAOne = 1u << 16;  // weight 1.0
+__device__ uint32_t g_aw_seed[kAClasses];  // the device's last learnt weights (0: none yet), seeding new scratches
 constexpr uint32_t kADoneVoid = 1u << 12;    // kADone: finished workgroups (low 12 bits) + void reports << 12
 constexpr uint32_t kASpin = 1u << 22;        // bounded look-back spins (about a quarter second)
 #ifndef H3C_AF_EARLY_FILL
@@ -3268,7 +3269,14 @@ __global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *
           double w = 0.5 * ((double)w0 / kAOne + rate[r] / mean);
           w = w < 0.5 ? 0.5 : w > 2.0 ? 2.0 : w;
           aa.ctl[kAW + r] = (uint32_t)(w * kAOne);
+          __hip_atomic_store(&g_aw_seed[r], (uint32_t)(w * kAOne), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+      } else {  // a new scratch (no weights yet): the device's last learnt ones, from any thread's scratch
+        bool none = true;
+        for (uint32_t r = 0; r < kAClasses; ++r) none = none && aa.ctl[kAW + r] == 0;
+        if (none)
+          for (uint32_t r = 0; r < kAClasses; ++r)
+            aa.ctl[kAW + r] = __hip_atomic_load(&g_aw_seed[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     return;
