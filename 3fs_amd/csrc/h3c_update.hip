@@ -73,6 +73,9 @@ __device__ __forceinline__ void store_row(uint64_t a, uint4 v) {
 #endif
 }
 
+#ifndef H3C_UPD_SKEW
+#define H3C_UPD_SKEW 0
+#endif
 #ifndef H3C_UPD_EARLY_FILL
 #define H3C_UPD_EARLY_FILL 1  // the fused kernel's CRC tables fill before the range is known (0: after the first group starts)
 #endif
@@ -531,8 +534,17 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     const uint64_t cum = old & ((1ull << 40) - 1);
     s_ticket = (uint32_t)(old >> 40);
     s_wt = wt;
+#if H3C_UPD_SKEW  // (A/B) the cut points warped by p(f) = f - b f (1 - f), b = H3C_UPD_SKEW / 1000
+    auto warp = [&](uint64_t c) -> uint32_t {
+      const double f = (double)c / (double)wt, b = H3C_UPD_SKEW / 1000.0;
+      return (uint32_t)((f - b * f * (1.0 - f)) * (double)n);
+    };
+    s_wlo = warp(cum);
+    s_whi = s_ticket + 1 == gridDim.x ? n : warp(cum + wmine);
+#else
     s_wlo = (uint32_t)(cum * n / wt);
     s_whi = s_ticket + 1 == gridDim.x ? n : (uint32_t)((cum + wmine) * n / wt);
+#endif
     s_E = __hip_atomic_load(&ctl[kCtlEpoch], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFFu;
   }
   // the CRC tables fill while thread 0 takes the ticket (waves 1-15; they do not depend on the range)

@@ -3182,6 +3182,9 @@ constexpr uint32_t kAOne = 1u << 16;  // weight 1.0
 __device__ uint32_t g_aw_seed[kAClasses];  // the device's last learnt weights (0: none yet), seeding new scratches
 constexpr uint32_t kADoneVoid = 1u << 12;    // kADone: finished workgroups (low 12 bits) + void reports << 12
 constexpr uint32_t kASpin = 1u << 22;        // bounded look-back spins (about a quarter second)
+#ifndef H3C_AF_SKEW
+#define H3C_AF_SKEW 0
+#endif
 #ifndef H3C_AF_EARLY_FILL
 #define H3C_AF_EARLY_FILL 1  // the CRC tables fill before the range is known (beside thread 0's ticket; 0: after phase 0)
 #endif
@@ -3363,8 +3366,18 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
                                              (1ull << 40) | wmine);
     const uint64_t cum = old & ((1ull << 40) - 1);
     s_ticket = (uint32_t)(old >> 40);
+#if H3C_AF_SKEW  // (A/B) early positions carry more work per op (a block's first of several writes): the
+                  // cut points warped by p(f) = f - b f (1 - f), b = H3C_AF_SKEW / 1000
+    auto warp = [&](uint64_t c) -> uint32_t {
+      const double f = (double)c / (double)wt, b = H3C_AF_SKEW / 1000.0;
+      return (uint32_t)((f - b * f * (1.0 - f)) * (double)n);
+    };
+    s_wlo = warp(cum);
+    s_whi = s_ticket + 1 == gridDim.x ? n : warp(cum + wmine);
+#else
     s_wlo = (uint32_t)(cum * n / wt);
     s_whi = s_ticket + 1 == gridDim.x ? n : (uint32_t)((cum + wmine) * n / wt);
+#endif
   }
   if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
   // the CRC tables fill while thread 0 takes the ticket (waves 1-15; they do not depend on the range)
