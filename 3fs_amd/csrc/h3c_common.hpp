@@ -660,6 +660,12 @@ __device__ __forceinline__ uint4 load_row_rmw(uint64_t a) {
 #endif
 }
 
+// The fused config-3 kernels' per-XCD range weights move this fraction of the way to the last batch's measured
+// class rates each batch (w <- w + gain * (rate / mean - w)).
+#ifndef H3C_W_GAIN
+#define H3C_W_GAIN 0.5
+#endif
+
 // The old rows of a partial update: `blk` when they are the chunk's own block (the block's first writer, which
 // writes the block back), else a previous writer's payload.  The block's rows load plainly (the same wave
 // writes the block back: the lines are then in L2 for the plain stores), the payloads nontemporally:

@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kLinkTile) void upd_tlink_kernel(const uint32_t *__
         mean /= kClasses;
         for (uint32_t c = 0; c < kClasses; ++c) {
           const uint32_t w0 = ctl[kCtlW + c] ? ctl[kCtlW + c] : kWOne;
-          double w = 0.5 * ((double)w0 / kWOne + rate[c] / mean);
+          double w = (double)w0 / kWOne + H3C_W_GAIN * (-(double)w0 / kWOne + rate[c] / mean);
           w = w < 0.5 ? 0.5 : w > 2.0 ? 2.0 : w;
           ctl[kCtlW + c] = (uint32_t)(w * kWOne);
           __hip_atomic_store(&g_uw_seed[c], (uint32_t)(w * kWOne), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -3269,7 +3269,7 @@ __global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *
         mean /= kAClasses;
         for (uint32_t r = 0; r < kAClasses; ++r) {
           const uint32_t w0 = aa.ctl[kAW + r] ? aa.ctl[kAW + r] : kAOne;
-          double w = 0.5 * ((double)w0 / kAOne + rate[r] / mean);
+          double w = (double)w0 / kAOne + H3C_W_GAIN * (-(double)w0 / kAOne + rate[r] / mean);
           w = w < 0.5 ? 0.5 : w > 2.0 ? 2.0 : w;
           aa.ctl[kAW + r] = (uint32_t)(w * kAOne);
           __hip_atomic_store(&g_aw_seed[r], (uint32_t)(w * kAOne), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
