@@ -478,6 +478,15 @@ constexpr uint32_t kGranAgg = 1, kGranIncl = 2;
 #endif
 constexpr uint32_t kLookWin = H3C_UPD_LOOK_WIN;  // look-back rows read per column per round trip
 constexpr uint32_t kSpinLimit = 1u << 22;  // bounded look-back spins (about a quarter second)
+#ifndef H3C_UPD_WAVES
+#define H3C_UPD_WAVES 16  // upd_fused_kernel's waves per workgroup (one workgroup per CU)
+#endif
+#ifndef H3C_UPD_DEPTH
+#define H3C_UPD_DEPTH 1  // upd_fused_kernel: writes whose rows load while one is consumed
+#endif
+constexpr uint32_t kFW = H3C_UPD_WAVES, kFThreads = 64 * kFW;
+constexpr int kFD = H3C_UPD_DEPTH;
+static_assert(kFW >= 2 && kFW <= 16 && kFD >= 1 && kFD <= 4, "fused kernel shape");
 typedef unsigned long long __attribute__((address_space(1))) gu64;
 
 // granules: {epoch << 8 | state, value} (state 0: not published in batch E; a zeroed row never matches)
@@ -549,14 +558,14 @@ __device__ __forceinline__ void upd_fused_kernel_body(
   }
   // the CRC tables fill while thread 0 takes the ticket (waves 1-15; they do not depend on the range)
   if (H3C_UPD_EARLY_FILL && threadIdx.x >= 64)
-    fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x - 64, kThreads - 64);
+    fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x - 64, kFThreads - 64);
   __syncthreads();
   const uint32_t L = s_ticket, nwg = gridDim.x, E = s_E;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t wlo = s_wlo, wn = s_whi - s_wlo;  // the workgroup's writes; each wave a contiguous share
-  const uint32_t lo = wlo + (uint32_t)((uint64_t)wave * wn / kWavesPerBlock);
-  const uint32_t hi = wlo + (uint32_t)((uint64_t)(wave + 1) * wn / kWavesPerBlock);
+  const uint32_t lo = wlo + (uint32_t)((uint64_t)wave * wn / kFW);
+  const uint32_t hi = wlo + (uint32_t)((uint64_t)(wave + 1) * wn / kFW);
   const uint64_t lo16 = 16u * lane;
   const uint64_t pay = (uint64_t)(uintptr_t)payload;
   auto rl64 = [](uint64_t v, uint32_t t) -> uint64_t {
@@ -566,9 +575,27 @@ __device__ __forceinline__ void upd_fused_kernel_body(
   // per group of 64 writes: lane k's write (chunk, shift, new / old / destination / final bytes)
   uint32_t m_c = kNone, m_sh = 0;
   uint64_t m_new = 0, m_old = 0, m_dst = 0, m_fin = 0;
-  uint4 vn[4], vo[4];
-  bool valid = false;
-  uint64_t pnew = 0, pold = 0;
+  // the rows of the write being consumed ([0]) and of the next kFD ones, their validity and payload addresses
+  uint4 bn[kFD + 1][4], bo[kFD + 1][4];
+  bool bv[kFD + 1];
+  uint64_t bp[kFD + 1];
+  // write t of the group into a buffer slot (invalid past the group)
+  auto load_op = [&](uint4(&n4)[4], uint4(&o4)[4], bool &v, uint64_t &p, uint32_t t, uint32_t cnt) {
+    v = t < cnt && __builtin_amdgcn_readlane(m_c, t) != kNone;
+    p = 0;
+    uint64_t po = 0;
+    bool blk = false;
+    if (v) {
+      p = rl64(m_new, t);
+      po = rl64(m_old, t);
+      blk = rl64(m_dst, t) != 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      n4[u] = v ? load_row_rmw(p + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+      o4[u] = v ? load_row_old(po + u * kRowBytes + lo16, blk) : make_uint4(0, 0, 0, 0);
+    }
+  };
   auto start_group = [&](uint32_t g0) {
     const uint32_t cnt = min(64u, hi - g0);
     const uint32_t k = g0 + lane;
@@ -591,14 +618,15 @@ __device__ __forceinline__ void upd_fused_kernel_body(
         if (p == kNone && !(H3C_UPD_EXPERIMENT & 4)) key = c * bpc + bb;
       }
     }
-    valid = __builtin_amdgcn_readlane(m_c, 0) != kNone;
-    pnew = rl64(m_new, 0);
-    pold = rl64(m_old, 0);
+    const bool valid = __builtin_amdgcn_readlane(m_c, 0) != kNone;
+    bv[0] = valid;
+    bp[0] = rl64(m_new, 0);
+    uint64_t pold = rl64(m_old, 0);
     const bool oblk = rl64(m_dst, 0) != 0;  // (the speculated old rows are the slot's own)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      vn[u] = valid ? load_row_rmw(pnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
-      vo[u] = valid ? load_row_old(pold + u * kRowBytes + lo16, oblk) : make_uint4(0, 0, 0, 0);
+      bn[0][u] = valid ? load_row_rmw(bp[0] + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
+      bo[0][u] = valid ? load_row_old(pold + u * kRowBytes + lo16, oblk) : make_uint4(0, 0, 0, 0);
     }
     // the walk over the slot's listed tile-last writers, while those rows load
     if (key != kNone) {
@@ -621,11 +649,14 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     if (valid && pold2 != pold) {  // write 0 was mis-speculated: reload its old rows
       pold = pold2;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) vo[u] = load_row_rmw(pold + u * kRowBytes + lo16);
+      for (int u = 0; u < 4; ++u) bo[0][u] = load_row_rmw(pold + u * kRowBytes + lo16);
     }
+    // the next writes' rows (their links are resolved now)
+#pragma unroll
+    for (int i = 1; i < kFD; ++i) load_op(bn[i], bo[i], bv[i], bp[i], (uint32_t)i, cnt);
   };
   if (lo < hi) start_group(lo);  // the first group's links and rows load while the tables fill
-  if (!H3C_UPD_EARLY_FILL) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kThreads);
+  if (!H3C_UPD_EARLY_FILL) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kFThreads);
   __syncthreads();
   if (threadIdx.x == 0) s_t0 = wall_clock64();
   const uint32_t *red = lds + kLdsWords;
@@ -639,49 +670,42 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     const uint32_t k = g0 + lane;
     uint32_t my_d = 0;
     for (uint32_t t = 0; t < cnt; ++t) {
-      const bool nvalid = t + 1 < cnt && __builtin_amdgcn_readlane(m_c, t + 1) != kNone;
-      uint4 wn[4], wo[4];
-      uint64_t npnew = 0, npold = 0;
-      bool nblk = false;
-      if (nvalid) {
-        npnew = rl64(m_new, t + 1);
-        npold = rl64(m_old, t + 1);
-        nblk = rl64(m_dst, t + 1) != 0;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        wn[u] = nvalid ? load_row_rmw(npnew + u * kRowBytes + lo16) : make_uint4(0, 0, 0, 0);
-        wo[u] = nvalid ? load_row_old(npold + u * kRowBytes + lo16, nblk) : make_uint4(0, 0, 0, 0);
-      }
-      if (valid) {
+      load_op(bn[kFD], bo[kFD], bv[kFD], bp[kFD], t + kFD, cnt);
+      if (bv[0]) {
         Streams st{0, 0, 0, 0};
 #if H3C_UPD_EXPERIMENT & 2  // timing experiment: no CRC compute (loads kept alive)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) st.s0 ^= vn[u].x ^ vo[u].x ^ vn[u].y ^ vo[u].y ^ vn[u].z ^ vo[u].z ^ vn[u].w ^ vo[u].w;
+        for (int u = 0; u < 4; ++u)
+          st.s0 ^= bn[0][u].x ^ bo[0][u].x ^ bn[0][u].y ^ bo[0][u].y ^ bn[0][u].z ^ bo[0][u].z ^ bn[0][u].w ^ bo[0][u].w;
 #else
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          consume(st, make_uint4(vn[u].x ^ vo[u].x, vn[u].y ^ vo[u].y, vn[u].z ^ vo[u].z, vn[u].w ^ vo[u].w), lb, Lt);
+          consume(st,
+                  make_uint4(bn[0][u].x ^ bo[0][u].x, bn[0][u].y ^ bo[0][u].y, bn[0][u].z ^ bo[0][u].z,
+                             bn[0][u].w ^ bo[0][u].w),
+                  lb, Lt);
 #endif
         const uint64_t dst = rl64(m_dst, t);
         if (dst) {  // first writer of the slot: leave the slot's final bytes in the chunk
           const uint64_t fin = rl64(m_fin, t);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const uint4 v = fin == pnew ? vn[u] : load_row_rmw(fin + u * kRowBytes + lo16);
+            const uint4 v = fin == bp[0] ? bn[0][u] : load_row_rmw(fin + u * kRowBytes + lo16);
             store_row(dst + u * kRowBytes + lo16, v);
           }
         }
         const uint32_t d = __builtin_amdgcn_readlane(wave_fold_tab(st, lane, red), 0);
         if (lane == t) my_d = d;
       }
-      valid = nvalid;
-      pnew = npnew;
-      pold = npold;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        vn[u] = wn[u];
-        vo[u] = wo[u];
+      for (int i = 0; i < kFD; ++i) {
+        bv[i] = bv[i + 1];
+        bp[i] = bp[i + 1];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          bn[i][u] = bn[i + 1][u];
+          bo[i][u] = bo[i + 1][u];
+        }
       }
     }
     // the group's v, all lanes at once; each write's chunk XOR right after it (inclusive, with
@@ -711,13 +735,13 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     stat[3 * L + 2] = (uint32_t)(wall_clock64() - s_t0);
   }
   uint32_t *wagg = lds;                               // [16][128]
-  uint32_t *wexcl = lds + kWavesPerBlock * kFusedCols;  // [128]: the workgroup's exclusive prefix
+  uint32_t *wexcl = lds + kFW * kFusedCols;  // [128]: the workgroup's exclusive prefix
   wagg[wave * kFusedCols + lane] = acc0;
   wagg[wave * kFusedCols + 64 + lane] = acc1;
   __syncthreads();
   if (wave == 0) {
     uint32_t a0 = 0, a1 = 0;
-    for (uint32_t w = 0; w < kWavesPerBlock; ++w) {
+    for (uint32_t w = 0; w < kFW; ++w) {
       a0 ^= wagg[w * kFusedCols + lane];
       a1 ^= wagg[w * kFusedCols + 64 + lane];
     }
@@ -850,7 +874,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     if (i < hi) out_raw[i] = ok ? (c < 64 ? x0 : x1) ^ inpre[i] : 0u;
   }
 }
-__global__ __launch_bounds__(kThreads) void upd_fused_kernel(
+__global__ __launch_bounds__(kFThreads) void upd_fused_kernel(
     const uint64_t *__restrict__ chunk_base, uint32_t nchunks, uint32_t bpc, const uint32_t *__restrict__ blk_chunk,
     const uint32_t *__restrict__ blk_index, const uint8_t *payload, uint32_t n, const uint32_t *__restrict__ prev,
     const uint32_t *__restrict__ hhead, uint32_t hmask, const uint32_t *__restrict__ nkey,
@@ -1307,12 +1331,12 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
   const uint32_t poly = type == H3C_TYPE_CRC32 ? kPolyCrc32 : kPolyCrc32c;
   const uint32_t reuse_case = (uint64_t)block_bytes == chunk_len ? 1u : 0u;  // a block write replaces the chunk
   const int path = pick_path(n_blocks, nchunks, block_bytes);
-  uint32_t fused_wg = std::min<uint32_t>(std::min(num_cu, kFusedMaxWG), (n_blocks + kWavesPerBlock - 1) / kWavesPerBlock);
+  uint32_t fused_wg = std::min<uint32_t>(std::min(num_cu, kFusedMaxWG), (n_blocks + kFW - 1) / kFW);
 #if H3C_UPD_WG_BAL  // the fewest workgroups with the same most writes per wave (100k writes: 250, 25 per wave,
                     // instead of 256 with 24-25: -1 us, profiles/r04_update_tail_ab.txt)
   {
-    const uint64_t per = ((uint64_t)n_blocks + (uint64_t)fused_wg * kWavesPerBlock - 1) / ((uint64_t)fused_wg * kWavesPerBlock);
-    fused_wg = (uint32_t)std::max<uint64_t>(1, ((uint64_t)n_blocks + per * kWavesPerBlock - 1) / (per * kWavesPerBlock));
+    const uint64_t per = ((uint64_t)n_blocks + (uint64_t)fused_wg * kFW - 1) / ((uint64_t)fused_wg * kFW);
+    fused_wg = (uint32_t)std::max<uint64_t>(1, ((uint64_t)n_blocks + per * kFW - 1) / (per * kFW));
   }
 #endif
   // the fused path's hash heads, control words, touched marks and granules: the stream's UpdScratch, or
@@ -1370,7 +1394,7 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
   if (path == kPathFused) {
     h3c_rt::ProfToken tok;
     HIP_TRY(h3c_rt::prof_stamp(dev, tok));
-    hipLaunchKernelGGL(upd_fused_kernel, dim3(fused_wg), dim3(kThreads), 0, st, chunk_base_dev, nchunks, bpc,
+    hipLaunchKernelGGL(upd_fused_kernel, dim3(fused_wg), dim3(kFThreads), 0, st, chunk_base_dev, nchunks, bpc,
                        blk_chunk_dev, blk_index_dev, static_cast<const uint8_t *>(payload_dev), n_blocks, w.prev,
                        w.hhead, w.hcap - 1, w.nkey, w.next, sh, pc, raw_base, chunk_raw_in_dev, exact ? 1u : 0u,
                        reuse_case, w.touched, w.ctl, w.gran, w.scan, out_raw_dev, chunk_raw_out_dev, n_invalid_dev,
