@@ -113,6 +113,17 @@ _proto("h3c_hostfed_destroy", None, _vp)
 _proto("h3c_host_alloc", _int, _int, _u64, ctypes.POINTER(_vp), ctypes.POINTER(_int))
 _proto("h3c_host_free", _int, _vp)
 _proto("h3c_device_numa_node", _int, _int)
+_proto("h3c_multi_partition", _int, _vp, _sz, _int, _vp)
+_proto("h3c_multi_create", _int, _vp, _int, _u64, ctypes.POINTER(_vp))
+_proto("h3c_multi_destroy", None, _vp)
+_proto("h3c_multi_workers", _int, _vp)
+_proto("h3c_multi_batch_create", _int, _vp, _vp, _sz, _vp, _vp)
+_proto("h3c_multi_verify", _int, _vp, _vp, _sz, _vp, _vp, _vp, _vp)
+_proto("h3c_multi_update_ios", _int, _vp, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp)
+_proto("h3c_multi_plan_create", _int, _vp, _vp, _sz, ctypes.POINTER(_vp))
+_proto("h3c_multi_plan_verify", _int, _vp, _vp, _vp, _vp, _vp)
+_proto("h3c_multi_plan_destroy", None, _vp)
+_proto("h3c_multi_last_stats", _int, _vp, _vp, _vp, _vp)
 _proto("h3c_profile_enable", None, _int)
 _proto("h3c_profile_read", _int, _int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64), ctypes.POINTER(_u64),
        _int)
@@ -683,6 +694,131 @@ class HostFed:
     def close(self) -> None:
         if self._h:
             lib.h3c_hostfed_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------- several GPUs, one process (h3c_multi_*)
+
+
+def multi_partition(lengths: Sequence[int], world: int) -> List[Tuple[int, int]]:
+    """h3c_multi_partition: the C++ byte-balanced split the multi-GPU engine uses, as [lo, hi) ranges
+    (identical to 3fs_amd/shard.py::partition).  Host arithmetic only: needs no GPU."""
+    ln = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
+    cuts = np.zeros(world + 1 if world >= 1 else 1, dtype=np.uint64)
+    _check(lib.h3c_multi_partition(ln.ctypes.data if ln.size else None, ln.size, int(world), cuts.ctypes.data))
+    return [(int(cuts[k]), int(cuts[k + 1])) for k in range(world)]
+
+
+class Multi:
+    """One engine over several GPUs of this process (h3c_multi_*): a host worker thread per entry of
+    `devices` (a device may repeat), each batch split byte-balanced (updates by chunk) and run on every
+    worker at once, results in the caller's arrays.  Device payloads must live on a listed device."""
+
+    def __init__(self, devices: Sequence[int], hostfed_window: int = 0):
+        devs = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
+        self._h = _vp()
+        self.devices = [int(d) for d in devs]
+        _check(lib.h3c_multi_create(devs.ctypes.data, len(devs), int(hostfed_window), ctypes.byref(self._h)))
+
+    def _descs(self, items, type_, start):
+        if isinstance(items, np.ndarray) and items.dtype == DESC_DTYPE:
+            return np.ascontiguousarray(items), None
+        return _desc_array(items, type_, start)
+
+    def batch_create(self, items, type_: int = ChecksumType.CRC32C, start: int = 0xFFFFFFFF):
+        """ChecksumInfo::create over every item (or a DESC_DTYPE array): (types uint8[n], raw uint32[n])."""
+        descs, keep = self._descs(items, type_, start)
+        n = len(descs)
+        out_t, out_v = np.zeros(n, dtype=np.uint8), np.zeros(n, dtype=np.uint32)
+        _check(lib.h3c_multi_batch_create(self._h, descs.ctypes.data, n, out_t.ctypes.data, out_v.ctypes.data))
+        del keep
+        return out_t, out_v
+
+    def verify(self, items, expected, type_: int = ChecksumType.CRC32C, start: int = 0xFFFFFFFF):
+        """(raw uint32[n], ok bool[n], n_mismatch) as batch_verify, over every worker."""
+        descs, keep = self._descs(items, type_, start)
+        n = len(descs)
+        exp = np.ascontiguousarray(np.asarray(expected, dtype=np.uint32))
+        if exp.size != n:
+            raise ValueError("expected must have one entry per item")
+        out_v, ok, mis = np.zeros(n, dtype=np.uint32), np.zeros(n, dtype=np.uint8), _u64(0)
+        _check(lib.h3c_multi_verify(self._h, descs.ctypes.data, n, exp.ctypes.data, out_v.ctypes.data,
+                                    ok.ctypes.data, ctypes.byref(mis)))
+        del keep
+        return out_v, ok.astype(bool), int(mis.value)
+
+    def update_ios(self, chunks: np.ndarray, ios: np.ndarray, type_: int = ChecksumType.CRC32C,
+                   std_domain: bool = False, exact: bool = False, counters: Optional[UpdateCounters] = None,
+                   graphs: bool = False) -> np.ndarray:
+        """update_ios over every worker (h3c_multi_update_ios): chunks sharded by chunk, ops in sequence
+        order per chunk; `chunks` is updated in place, one UPDATE_RESULT_DTYPE record per op returned."""
+        if chunks.dtype != CHUNK_STATE_DTYPE or ios.dtype != UPDATE_IO_DTYPE:
+            raise TypeError("chunks / ios must use CHUNK_STATE_DTYPE / UPDATE_IO_DTYPE")
+        if not (chunks.flags.c_contiguous and ios.flags.c_contiguous):
+            raise ValueError("chunks / ios must be contiguous")
+        res = np.zeros(len(ios), dtype=UPDATE_RESULT_DTYPE)
+        flags = (UPD_STD_DOMAIN if std_domain else 0) | (UPD_EXACT if exact else 0) | (UPD_GRAPHS if graphs else 0)
+        _check(lib.h3c_multi_update_ios(self._h, int(type_), chunks.ctypes.data, len(chunks), ios.ctypes.data,
+                                        len(ios), res.ctypes.data, flags,
+                                        ctypes.byref(counters) if counters is not None else None))
+        return res
+
+    def plan(self, descs: np.ndarray) -> "MultiPlan":
+        return MultiPlan(self, descs)
+
+    def last_stats(self):
+        """The last call's share per worker: [(units, algorithmic bytes, wall ms)]."""
+        k = len(self.devices)
+        u, b, ms = np.zeros(k, dtype=np.uint64), np.zeros(k, dtype=np.uint64), np.zeros(k, dtype=np.float64)
+        _check(lib.h3c_multi_last_stats(self._h, u.ctypes.data, b.ctypes.data, ms.ctypes.data))
+        return [(int(u[i]), int(b[i]), float(ms[i])) for i in range(k)]
+
+    def close(self) -> None:
+        if self._h:
+            lib.h3c_multi_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MultiPlan:
+    """A resident chunk set (DESC_DTYPE, device memory on the engine's devices) verified repeatedly over
+    every worker (h3c_multi_plan_*): per run only expected values and results cross PCIe."""
+
+    def __init__(self, multi: Multi, descs: np.ndarray):
+        if descs.dtype != DESC_DTYPE:
+            raise TypeError("descs must use DESC_DTYPE")
+        self._m = multi
+        self._descs = np.ascontiguousarray(descs)
+        self.n = len(descs)
+        self._h = _vp()
+        _check(lib.h3c_multi_plan_create(multi._h, self._descs.ctypes.data, self.n, ctypes.byref(self._h)))
+        self.out = np.zeros(self.n, dtype=np.uint32)
+        self.ok = np.zeros(self.n, dtype=np.uint8)
+
+    def verify(self, expected) -> int:
+        """Runs one verify; results in self.out / self.ok; returns the mismatch count."""
+        exp = np.ascontiguousarray(np.asarray(expected, dtype=np.uint32))
+        if exp.size != self.n:
+            raise ValueError("expected must have one entry per descriptor")
+        mis = _u64(0)
+        _check(lib.h3c_multi_plan_verify(self._h, exp.ctypes.data, self.out.ctypes.data, self.ok.ctypes.data,
+                                         ctypes.byref(mis)))
+        return int(mis.value)
+
+    def close(self) -> None:
+        if self._h:
+            lib.h3c_multi_plan_destroy(self._h)
             self._h = _vp()
 
     def __del__(self):  # pragma: no cover

@@ -412,6 +412,56 @@ int h3c_hostfed_run(h3c_hostfed *h, const h3c_desc *d, size_t n, const uint32_t 
                     uint8_t *ok, uint64_t *n_mismatch, void *stream);
 void h3c_hostfed_destroy(h3c_hostfed *h);
 
+/* ---- several GPUs of one process (3fs_amd/csrc/h3c_multi.hip) ---- */
+
+/* The storage service is one process per node whose checksum callers are its AIO and update threads
+ * (src/storage/aio/AioReadWorker.h:26, src/storage/update/UpdateWorker.h:15); the resync scrub is one
+ * caller per target (src/storage/service/ReliableForwarding.cc:158-182 -> BatchReadJob.cc:43-54).  An
+ * h3c_multi drives a list of devices from that one process: one host worker thread per entry (hipSetDevice
+ * once, its own stream and host-fed pipeline with NUMA-local windows), each batch split across them and
+ * run at once, results written into disjoint slices of the caller's host arrays.  No collective.  A device
+ * may be listed twice (two workers on one GPU).  Calls on one object run one at a time; the entries are
+ * synchronous.
+ *
+ * Partition: contiguous index ranges balanced by payload bytes (NONE / null descriptors weigh 0); cut k is
+ * the first index whose byte prefix sum reaches k/world of the total (float64 arithmetic, identical to
+ * 3fs_amd/shard.py::partition).  cuts[world + 1] receives the range bounds.  A device-resident payload is
+ * read where it lives: a descriptor whose memory belongs to another listed device than its range's worker
+ * goes to the least-loaded worker on that device; memory on a device the object does not drive fails the
+ * call with H3C_ERR_INVALID_ARG before any work.  Place shard k of a resident chunk set on devices[k]
+ * (h3c_multi_partition over the chunk lengths) and every descriptor stays in its range. */
+typedef struct h3c_multi h3c_multi;
+int h3c_multi_partition(const uint64_t *lengths, size_t n, int world, uint64_t *cuts);
+/* hostfed_window: bytes per H2D staging window of each worker's pipeline (0: 64 MiB). */
+int h3c_multi_create(const int *devices, int ndev, uint64_t hostfed_window, h3c_multi **out);
+void h3c_multi_destroy(h3c_multi *m);
+int h3c_multi_workers(const h3c_multi *m);
+/* h3c_batch_create / h3c_batch_verify semantics per descriptor (ChecksumInfo::create, Common.h:146-177;
+ * ChunkReplica.cc:193-207, BatchReadJob.cc:43-54).  Pinned host payloads (8 MiB or more per worker, one
+ * polynomial) stream through the worker's double-buffered pipeline (h3c_hostfed_run); the rest through
+ * h3c_batch_* on the worker's stream. */
+int h3c_multi_batch_create(h3c_multi *m, const h3c_desc *d, size_t n, uint8_t *out_type, uint32_t *out_raw);
+int h3c_multi_verify(h3c_multi *m, const h3c_desc *d, size_t n, const uint32_t *expected_raw, uint32_t *out_raw,
+                     uint8_t *ok, uint64_t *n_mismatch);
+/* h3c_update_ios_ex over several devices: chunks split byte-balanced by chunk_size (then moved to the worker
+ * on the device holding their bytes), every op to its chunk's worker in sequence order, so each op's result
+ * and each chunk's final state equal one h3c_update_ios_ex call over the whole batch.  An op naming no chunk
+ * of the table fails with kInvalidArg as there; a WRITE whose payload lives on another device than its chunk
+ * fails the call with H3C_ERR_INVALID_ARG before any work.  counters: the sum over workers. */
+int h3c_multi_update_ios(h3c_multi *m, uint8_t poly_type, h3c_chunk_state *chunks, uint32_t nchunks,
+                         const h3c_update_io *ios, uint32_t n, h3c_update_result *results, uint32_t flags,
+                         h3c_update_counters *counters);
+/* A resident chunk set verified repeatedly (scrub / resync): each worker keeps an h3c_plan of its share and
+ * its result buffers; a run moves only the expected values and the results across PCIe. */
+typedef struct h3c_multi_plan h3c_multi_plan;
+int h3c_multi_plan_create(h3c_multi *m, const h3c_desc *d, size_t n, h3c_multi_plan **out);
+int h3c_multi_plan_verify(h3c_multi_plan *p, const uint32_t *expected_raw, uint32_t *out_raw, uint8_t *ok,
+                          uint64_t *n_mismatch);
+void h3c_multi_plan_destroy(h3c_multi_plan *p);
+/* The last call's share per worker (arrays of h3c_multi_workers entries, any may be NULL): descriptors or
+ * ops, algorithmic bytes, and the worker's wall time in ms. */
+int h3c_multi_last_stats(const h3c_multi *m, uint64_t *units, uint64_t *bytes, double *ms);
+
 /* ---- utilities for benches/tests (not on the reference path) ---- */
 
 /* chunk i at base + i*stride gets u64 words splitmix64(seed ^ ((first_chunk+i)<<40) ^ k). */

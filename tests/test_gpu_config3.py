@@ -13,12 +13,20 @@ shared by both branches):
 
 * every op of 2 chunks (~3,100 ops) replayed one by one through the ChunkReplica::update
   restatement (case iv re-reads the 64 MiB chunk per op): status, size and stored checksum;
+* every one of the 100,000 ops' stored checksums against a host delta chain built from the
+  oracle's own primitives: r_k = r_prev ^ shift(crc0(old ^ new), bytes after the write), where
+  `old` is the window's initial bytes or its previous writer's payload.  The chain is first
+  asserted equal to the ChunkReplica::update replay on the 2 replayed chunks, so the shortcut is
+  itself pinned to the case-(iv) restatement before it judges the other ~97k ops;
 * all 64 chunks' final bytes against a host replay of every op's bytes, and all 64 final stored
   checksums against the oracle's CRC of those bytes;
 * every op's status and the reference's case counters.
 
 In exact mode 4 chunks start with stale stored checksums (two of them replayed op by op): the
-reference's case (iv) re-reads the bytes, so the first op on such a chunk heals it.
+reference's case (iv) re-reads the bytes, so the first op on such a chunk heals it (the delta chain
+therefore starts from each chunk's true CRC in both modes).  Exact mode never takes the aligned
+sub-branch (it trusts stored checksums): with the aligned branch forced, an exact batch must be routed
+to the chain-based fast branch without an aligned attempt, and still match every op.
 """
 import numpy as np
 import pytest
@@ -80,22 +88,42 @@ def _inputs(exact):
                 want, meta = orc.replica_update(meta, chunk, CL, io, pay[k])
                 per_op[int(k)] = (want["status"], want["size"], want["type"], want["value"])
             finals[c] = (meta["size"], meta["type"], meta["value"])
-        # every op's bytes on the host: the final bytes and checksums of all 64 chunks
+        # every op's stored checksum by the delta chain (before `host` takes every op's bytes)
         rows = host.reshape(NCH, CL // G, G)
         slot = wc.astype(np.int64) * (CL // G) + wb
+        order = np.argsort(slot, kind="stable")  # by slot, sequence order within a slot
+        same = np.zeros(NW, dtype=bool)
+        same[1:] = slot[order[1:]] == slot[order[:-1]]
+        old = rows[wc, wb]  # each window's initial bytes (a copy)
+        prev = order[np.nonzero(same)[0] - 1]  # the previous writer of those ops' window
+        old[order[same]] = pay[prev]
+        np.bitwise_xor(old, pay, out=old)
+        dcrc = np.zeros(NW, dtype=np.uint32)
+        orc.lib().orc_batch_crc32c(old.ctypes.data, G, NW, 0, 16, 0, dcrc.ctypes.data)  # init 0: crc0
+        del old
+        shift = orc.lib().orc_shift
+        chain = stored.copy()  # the true CRCs: case (iv) re-reads, so a stale value heals at once
+        exp_all = np.zeros(NW, dtype=np.uint32)
+        for k in range(NW):
+            c = int(wc[k])
+            chain[c] ^= shift(int(dcrc[k]), CL - (int(wb[k]) + 1) * G, orc.POLY_CRC32C)
+            exp_all[k] = chain[c]
+        # the shortcut is pinned to the ChunkReplica::update replay before it judges every op
+        for k, want in per_op.items():
+            assert int(exp_all[k]) == want[3], k
+        # every op's bytes on the host: the final bytes and checksums of all 64 chunks
         _, last_rev = np.unique(slot[::-1], return_index=True)
         last = NW - 1 - last_rev  # each slot's last writer in sequence order
         rows[wc[last], wb[last]] = pay[last]
         _ORACLE[exact] = dict(chunk1=chunk1, cks=cks, values=values, per_op=per_op, finals=finals,
-                              final_bytes=host, want_final=_host_crcs(host))
+                              final_bytes=host, want_final=_host_crcs(host), exp_all=exp_all)
+        assert np.array_equal(chain, _ORACLE[exact]["want_final"])
     return wc, wb, pay, stale, _ORACLE[exact]
 
 
 @pytest.mark.parametrize("branch", ["general", "fast", "aligned"])
 @pytest.mark.parametrize("exact", [False, True])
 def test_updio_config3_full_shape_against_oracle(h3c, torch_dev, hooks, exact, branch):
-    if exact and branch == "aligned":
-        pytest.skip("the aligned sub-branch trusts stored checksums (exact mode takes the chain-based branch)")
     torch, dev = torch_dev
     wc, wb, pay, stale, o = _inputs(exact)
     hooks(h3c.HOOK_UPD_FAST, 1 if branch == "general" else 2)
@@ -126,9 +154,11 @@ def test_updio_config3_full_shape_against_oracle(h3c, torch_dev, hooks, exact, b
     h3c.update_ios_dev(d_state, d_ios, d_res, exact=exact, counters=d_ctr)
     torch.cuda.synchronize()
     diag = {k: v - before[k] for k, v in h3c.diag_counters().items()}
-    # the branch that ran is the branch named, with no redo of any kind
+    # the branch that ran is the branch named, with no redo of any kind; exact mode is never tried
+    # on the aligned sub-branch, even when it is forced, and takes the chain-based branch instead
+    took_aligned = branch == "aligned" and not exact
     assert diag["fast_batches"] == (0 if branch == "general" else 1), diag
-    assert diag["aligned_batches"] == (1 if branch == "aligned" else 0), diag
+    assert diag["aligned_batches"] == (1 if took_aligned else 0), diag
     assert diag["fast_abandoned"] == 0 and diag["fast_recovered"] == 0, diag
     assert diag["aligned_abandoned"] == 0 and diag["aligned_recovered"] == 0, diag
     assert all(diag[k] == 0 for k in ("redo_front_void", "rerun_phase_b_void", "redo_failed_a6",
@@ -139,6 +169,10 @@ def test_updio_config3_full_shape_against_oracle(h3c, torch_dev, hooks, exact, b
     for k, want in o["per_op"].items():
         got = (int(res["status"][k]), int(res["size"][k]), int(res["type"][k]), int(res["value"][k]))
         assert got == want, (branch, k)
+    # all 100,000 ops' stored checksums against the pinned delta chain
+    bad = np.nonzero(res["value"] != o["exp_all"])[0]
+    assert bad.size == 0, (branch, exact, bad.size, bad[:8].tolist())
+    assert (res["type"] == orc.CRC32C).all()
     for c, want in o["finals"].items():
         assert (int(fin["size"][c]), int(fin["type"][c]), int(fin["value"][c])) == want, c
     assert np.array_equal(dchunks.cpu().numpy().reshape(NCH, CL), o["final_bytes"])
@@ -154,3 +188,44 @@ def test_updio_config3_full_shape_against_oracle(h3c, torch_dev, hooks, exact, b
         assert int(res["value"][np.nonzero(wc == c)[0][-1]]) == int(want_final[c])
     # every op is updateChecksum case (iv) (ChunkReplica.cc:356-390)
     assert ctr == [0, 0, 0, NW, 0, 0, 0, len(stale)]
+
+
+def test_updio_config3_full_shape_multi_engine(h3c, torch_dev):
+    """The same 100k-op batch through h3c_multi_update_ios over devices {0, 0} (two worker threads on
+    the one GPU, the chunks split 32 / 32 by capacity): host tables, every op pinned to the delta chain."""
+    torch, dev = torch_dev
+    wc, wb, pay, stale, o = _inputs(False)
+    dchunks = torch.empty(NCH * CL, dtype=torch.uint8, device=dev)
+    h3c.fill_splitmix(dchunks, CL, NCH, CL, SEED)
+    dpay = torch.from_numpy(pay).to(dev)
+    torch.cuda.synchronize()
+    state = np.zeros(NCH, dtype=h3c.CHUNK_STATE_DTYPE)
+    state["base"] = dchunks.data_ptr() + np.arange(NCH, dtype=np.uint64) * np.uint64(CL)
+    state["chunk_size"] = CL
+    state["size"] = CL
+    state["value"] = o["values"]
+    state["type"] = orc.CRC32C
+    ios = np.zeros(NW, dtype=h3c.UPDATE_IO_DTYPE)
+    ios["payload"] = dpay.data_ptr() + np.arange(NW, dtype=np.uint64) * np.uint64(G)
+    ios["chunk"] = wc
+    ios["offset"] = wb * G
+    ios["length"] = G
+    ios["checksum_value"] = o["cks"]
+    ios["checksum_type"] = orc.CRC32C
+    ios["kind"] = h3c.UPD_WRITE
+    m = h3c.Multi([0, 0])
+    try:
+        ctr = h3c.UpdateCounters()
+        res = m.update_ios(state, ios, counters=ctr)
+        torch.cuda.synchronize()
+        stats = m.last_stats()
+    finally:
+        m.close()
+    units = [s[0] for s in stats]
+    assert sum(units) == NW and units == [int((wc < NCH // 2).sum()), int((wc >= NCH // 2).sum())], units
+    assert (res["status"] == 0).all() and (res["size"] == CL).all() and (res["type"] == orc.CRC32C).all()
+    bad = np.nonzero(res["value"] != o["exp_all"])[0]
+    assert bad.size == 0, (bad.size, bad[:8].tolist())
+    assert np.array_equal(state["value"], o["want_final"])
+    assert np.array_equal(dchunks.cpu().numpy().reshape(NCH, CL), o["final_bytes"])
+    assert ctr.as_dict()["read_chunk"] == NW and ctr.as_dict()["checksum_mismatch"] == 0
