@@ -36,12 +36,24 @@ void set_error_text(const char *text);
 // the kernel; stamp_begin / stamp_end) -- nothing is added to the stream.  prof_begin: an event
 // pair around the launch (for pipelines of copies and kernels; an event record costs the stream
 // ~6 us, profiles/r04_*_rocprof_kernel_stats.csv timelines).
+struct ProfToken;
+// Gives back what a token holds when no prof_end took it over (an early error return between the two):
+// the stamp slot's pending record is dropped, so h3c_profile_read neither waits on it nor counts it, and
+// the pool rewinds past it; an event pair is destroyed.
+void prof_cancel(const ProfToken &t);
 struct ProfToken {
   bool on = false;
   hipEvent_t a = nullptr, b = nullptr;
   unsigned long long *ts = nullptr;  // prof_stamp's slot (device), or nullptr
   int dev = -1;
   int slot = -1;
+  mutable bool closed = false;  // prof_end took over the slot or the events
+  ProfToken() = default;
+  ProfToken(const ProfToken &) = delete;
+  ProfToken &operator=(const ProfToken &) = delete;
+  ~ProfToken() {
+    if (!closed && (ts || a || b)) prof_cancel(*this);
+  }
 };
 hipError_t prof_begin(hipStream_t st, ProfToken &t);
 hipError_t prof_stamp(int dev, ProfToken &t);

@@ -1084,6 +1084,7 @@ struct StampPool {
   int next = 0;
 };
 constexpr int kProfKinds = 4;
+constexpr int kProfCancelled = -3;  // a stamp record whose launch never happened (ProfToken's early return)
 std::mutex g_prof_mu;
 std::vector<ProfRec> g_prof;
 StampPool g_stamps[kMaxDevices];
@@ -1213,7 +1214,21 @@ hipError_t prof_stamp(int dev, ProfToken &t) {
   g_prof.push_back(r);
   return hipSuccess;
 }
+void prof_cancel(const ProfToken &t) {
+  t.closed = true;
+  if (t.ts) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    for (size_t i = g_prof.size(); i-- > 0;)
+      if (g_prof[i].kind == -1 && g_prof[i].dev == t.dev && g_prof[i].slot == t.slot) {
+        g_prof[i].kind = kProfCancelled;
+        break;
+      }
+  }
+  if (t.a) (void)hipEventDestroy(t.a);
+  if (t.b) (void)hipEventDestroy(t.b);
+}
 hipError_t prof_end(hipStream_t st, const ProfToken &t, int kind, uint64_t bytes) {
+  t.closed = true;
   if (!t.on) return hipSuccess;
   if (t.ts) {  // stamped by the kernel itself: its pending record gets its kind and bytes
     std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -1607,10 +1622,13 @@ int h3c_profile_read(int kind, double *kernel_ms, uint64_t *launches, uint64_t *
     const int khz = h3c_rt::device_wall_clock_khz(d);
     bool pending = false;  // a slot handed out whose launch is not recorded yet (prof_stamp .. prof_end)
     for (auto &r : g_prof) pending = pending || (r.dev == d && r.slot >= 0 && r.kind == -1);
+    int top_pending = -1;  // the pool rewinds to just past the highest slot still in flight
+    for (auto &r : g_prof)
+      if (r.dev == d && r.slot >= 0 && r.kind == -1) top_pending = std::max(top_pending, r.slot);
     for (auto &r : g_prof) {
       if (r.dev != d || r.slot < 0 || r.kind == -1) continue;
       const unsigned long long t0 = v[2 * (size_t)r.slot], t1 = v[2 * (size_t)r.slot + 1];
-      if (t1 > t0 && t0 != ~0ull && khz > 0) {
+      if (r.kind >= 0 && t1 > t0 && t0 != ~0ull && khz > 0) {
         g_prof_ms_done[r.kind] += (double)(t1 - t0) / khz;
         g_prof_launch_done[r.kind] += 1;
         g_prof_bytes_done[r.kind] += r.bytes;
@@ -1623,7 +1641,7 @@ int h3c_profile_read(int kind, double *kernel_ms, uint64_t *launches, uint64_t *
       }
       r.slot = -2;  // (done)
     }
-    if (!pending) p.next = 0;
+    p.next = top_pending + 1;  // (0 when nothing is pending: the whole pool was re-initialised above)
   }
   std::vector<ProfRec> keep;  // pending stamp records stay for the next read
   for (auto &r : g_prof) {

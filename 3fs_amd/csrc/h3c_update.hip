@@ -1213,6 +1213,7 @@ struct UpdScratch {
   int dev = -1;
   hipStream_t st = nullptr;
   std::thread::id tid{};  // (hipStreamPerThread: one stream per thread behind one handle)
+  uint64_t used = 0;      // LRU tick
   uint32_t *p = nullptr;
   size_t words = 0;
   uint32_t hcap = 0, batches = 0;
@@ -1222,9 +1223,13 @@ struct UpdScratch {
 };
 std::mutex g_us_mu;
 std::vector<std::unique_ptr<UpdScratch>> g_us;
+uint64_t g_us_tick = 0;
 
-// The scratch for (dev, st), locked by `lk`, laid out for `hcap` hash heads and zeroed on `st` if it must
-// be; nullptr: none (too many streams, or the allocation failed): the caller uses its workspace.
+// The scratch for (dev, st), locked by `lk`, laid out for `hcap` hash heads and zeroed on `st` if it must be;
+// nullptr: none (every scratch busy, or the allocation failed): the caller uses its workspace.  At
+// kUsMaxScratches the least recently used idle scratch is freed (after a device synchronisation, so no batch of
+// its -- possibly destroyed -- stream is still in flight) and reused.  A stream that ran batches releases its
+// scratch with h3c_stream_release before it is destroyed (a new stream may get the same handle value).
 UpdScratch *upd_scratch(int dev, hipStream_t st, uint32_t hcap, std::unique_lock<std::mutex> &lk) {
   const std::thread::id tid = st == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id{};
   UpdScratch *s = nullptr;
@@ -1233,15 +1238,56 @@ UpdScratch *upd_scratch(int dev, hipStream_t st, uint32_t hcap, std::unique_lock
     for (auto &x : g_us)
       if (x->dev == dev && x->st == st && x->tid == tid) s = x.get();
     if (!s) {
-      if (g_us.size() >= kUsMaxScratches) return nullptr;
-      g_us.emplace_back(new UpdScratch);
-      s = g_us.back().get();
+      if (g_us.size() < kUsMaxScratches) {
+        g_us.emplace_back(new UpdScratch);
+        s = g_us.back().get();
+      } else {  // evict the least recently used scratch no call holds
+        for (auto &x : g_us) {
+          if (!x->mu.try_lock()) continue;
+          if (s == nullptr || x->used < s->used) {
+            if (s) s->mu.unlock();
+            s = x.get();
+          } else {
+            x->mu.unlock();
+          }
+        }
+        if (!s) return nullptr;
+        if (s->p) {
+          int prev = -1;
+          (void)hipGetDevice(&prev);
+          (void)hipSetDevice(s->dev);
+          const bool freed = hipDeviceSynchronize() == hipSuccess && hipFree(s->p) == hipSuccess;
+          (void)hipSetDevice(prev);
+          if (!freed) {
+            (void)hipGetLastError();
+            s->mu.unlock();
+            return nullptr;
+          }
+        }
+        s->p = nullptr;
+        s->words = 0;
+        s->mu.unlock();
+      }
       s->dev = dev;
       s->st = st;
       s->tid = tid;
+      s->dirty = true;
+      s->fresh = true;
+      s->hcap = 0;
+      s->batches = 0;
     }
+    s->used = ++g_us_tick;
   }
   lk = std::unique_lock<std::mutex>(s->mu);
+  bool same;
+  {
+    std::lock_guard<std::mutex> g(g_us_mu);  // (the key fields change only under g_us_mu)
+    same = s->st == st && s->dev == dev && s->tid == tid;
+  }
+  if (!same) {  // evicted for another stream between the two locks
+    lk.unlock();
+    return nullptr;
+  }
   const size_t words = kUsHeads + (size_t)hcap;
   if (s->words < words) {
     if (s->p) {  // (this stream's earlier batches may still use it)
@@ -1458,6 +1504,36 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
 }  // namespace
 
 extern "C" {
+
+int h3c_stream_release(void *stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const std::thread::id tid = st == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id{};
+  std::vector<std::unique_ptr<UpdScratch>> gone;
+  {
+    std::lock_guard<std::mutex> g(g_us_mu);
+    for (size_t i = 0; i < g_us.size();) {
+      if (g_us[i]->st == st && g_us[i]->tid == tid) {
+        std::lock_guard<std::mutex> one(g_us[i]->mu);  // (waits out a call enqueueing on it)
+        gone.push_back(std::move(g_us[i]));
+        g_us.erase(g_us.begin() + (ptrdiff_t)i);
+      } else {
+        ++i;
+      }
+    }
+  }
+  if (gone.empty()) return H3C_OK;
+  HIP_TRY(hipStreamSynchronize(st));  // its batches end before their scratch goes
+  for (auto &x : gone)
+    if (x->p) {
+      int prev = -1;
+      (void)hipGetDevice(&prev);
+      (void)hipSetDevice(x->dev);
+      const hipError_t e = hipFree(x->p);
+      (void)hipSetDevice(prev);
+      HIP_TRY(e);
+    }
+  return H3C_OK;
+}
 
 size_t h3c_update_workspace_bytes(uint32_t n_blocks, uint32_t nchunks, uint64_t chunk_len, uint32_t block_bytes) {
   if (!block_bytes) return 0;

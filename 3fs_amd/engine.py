@@ -81,6 +81,7 @@ _proto("h3c_plan_destroy", None, _vp)
 _proto("h3c_batch_combine", _int, _u8, _vp, _vp, _vp, _sz, _vp, _vp)
 _proto("h3c_fill_splitmix", _int, _vp, _u64, _u64, _u64, _u64, _u64, _vp)
 _proto("h3c_update_workspace_bytes", _sz, _u32, _u32, _u64, _u32)
+_proto("h3c_stream_release", _int, _vp)
 _proto("h3c_update_blocks", _int, _u8, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp)
 _proto("h3c_update_ios", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp)
 _proto("h3c_update_ios_ex", _int, _u8, _vp, _u32, _vp, _u32, _vp, _u32, _vp, _vp)
@@ -350,6 +351,12 @@ def update_blocks(chunk_bases, chunk_len: int, raw_in, blk_chunk, blk_index, pay
                                     n_invalid.data_ptr() if n_invalid is not None else None,
                                     UPD_EXACT if exact else 0,
                                     counters.data_ptr() if counters is not None else None, _stream_handle(stream)))
+
+
+def stream_release(stream) -> None:
+    """h3c_stream_release: free the update scratch the library keeps for `stream` (call before the stream
+    is destroyed; its handle value may be reused by a new stream)."""
+    _check(lib.h3c_stream_release(_stream_handle(stream)))
 
 
 def set_coalescing(on: bool) -> None:

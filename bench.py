@@ -86,14 +86,22 @@ def cpu_baseline(gpu_raw_first: np.ndarray, chunk_len: int, seconds: float = 8.0
     for c in range(n):
         L.orc_fill_splitmix(host[c * chunk_len:].ctypes.data, chunk_len, SEED, c)
     out = np.zeros(n, dtype=np.uint32)
-    L.orc_batch_crc32c(host.ctypes.data, chunk_len, n, 0xFFFFFFFF, 1, 0, out.ctypes.data)  # warm
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        L.orc_batch_crc32c(host.ctypes.data, chunk_len, n, 0xFFFFFFFF, 1, 0, out.ctypes.data)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
+    # one thread pinned to one core ("one thread pinned with taskset"): the calling
+    # thread's affinity, which the oracle's worker pthread inherits; restored afterwards
+    allowed = sorted(os.sched_getaffinity(0))
+    core = allowed[0]
+    os.sched_setaffinity(0, {core})
+    try:
+        L.orc_batch_crc32c(host.ctypes.data, chunk_len, n, 0xFFFFFFFF, 1, 0, out.ctypes.data)  # warm
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            L.orc_batch_crc32c(host.ctypes.data, chunk_len, n, 0xFFFFFFFF, 1, 0, out.ctypes.data)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        os.sched_setaffinity(0, set(allowed))
     gibps = reps * n * chunk_len / el / 2**30
     # context only (BASELINE.md "all-cores run"): the same restatement on every core this
     # process may use (the GPU box grants a share of the host, not all of nproc)
@@ -121,7 +129,8 @@ def cpu_baseline(gpu_raw_first: np.ndarray, chunk_len: int, seconds: float = 8.0
         "cores": 1,
         "kind": "port",
         "sample": f"{reps} x (1024 x {chunk_len >> 20} MiB splitmix chunks), folly-faithful 3-way SSE4.2 crc32q, "
-                  f"1 thread, {el:.1f} s",
+                  f"1 thread pinned to core {core}, {el:.1f} s",
+        "pinned_core": core,
         "gpu_values_match": bool(np.array_equal(out, gpu_raw_first[:n])),
         "cpu_model": _cpu_model(),
         "nproc": os.cpu_count(),
@@ -253,12 +262,24 @@ def roofline(prof, peak: float, unit: str = "GB/s", bound: str = "hbm", kernel: 
             r["rocprof_avg_us"] = round(tr[2], 2)
             r["frac_rocprof"] = round(per / (tr[2] * 1e-6) / 1e9 / peak, 4)
             if kernel in PLAIN_STORE_KERNELS:
+                # the kernel's own stamps end before the end-of-launch L2 write-back of its plain stores,
+                # which rocprof's duration covers: lead with the slower of the two
+                r["frac_stamps"] = r["frac"]
+                r["achieved_stamps"] = r["achieved"]
+                if tr[2] > r["kernel_avg_us"]:
+                    achieved = per / (tr[2] * 1e-6) / 1e9
+                    r["achieved"] = round(achieved, 1)
+                    r["frac"] = r["frac_rocprof"]
+                    r["frac_source"] = "rocprof (committed profile of this launch shape): slower than the stamps"
                 r["timing_note"] = ("kernel_avg_us: the kernel's own stamps, first workgroup start to last workgroup "
                                     "end; rocprof's duration also covers the end-of-launch L2 write-back of its plain "
-                                    "stores")
+                                    "stores, so `frac` is the slower of the two")
     if kernel in PATTERN_CEILING:
         ceil, src = PATTERN_CEILING[kernel]
         r["pattern_ceiling"] = {"achieved": ceil, "frac": round(achieved / ceil, 4), "source": src}
+        if src.endswith("r05_rmw_ceiling.txt"):
+            r["pattern_ceiling"]["kind"] = ("synthetic: the best read-only probe and the best write-only probe timed "
+                                            "separately and summed (not a measured read-modify-write loop)")
     return r
 
 
@@ -328,6 +349,80 @@ def run_verify(args, cx: Ctx) -> dict:
     if cx.world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(stored_host, clen, args.cpu_seconds)
     return res
+
+
+def run_inproc(args, cx: Ctx, devices) -> dict:
+    """The product path over several GPUs of ONE process (h3c_multi_*): one worker thread
+    per entry of `devices`, each holding `chunks` x `chunk_kib` resident on its device (chunk indices
+    [k*n, (k+1)*n) on device k, 5% flipped), verified as one batch per step through
+    h3c_multi_plan_verify -- host arrays in and out, as a C++ storage service calls it.  The byte-balanced
+    partition puts device k's share on worker k."""
+    torch, h3c = cx.torch, cx.h3c
+    n, clen = args.chunks, args.chunk_kib << 10
+    W = len(devices)
+    bufs, descs, flips_all, stored = [], [], [], []
+    m = h3c.Multi(devices)
+    try:
+        for k, dv in enumerate(devices):
+            dev = torch.device(f"cuda:{dv}")
+            buf = torch.empty(n * clen, dtype=torch.uint8, device=dev)
+            with torch.cuda.device(dev):
+                h3c.fill_splitmix(buf, clen, n, clen, SEED, first_chunk=k * n)
+            d = np.zeros(n, dtype=h3c.engine.DESC_DTYPE)
+            d["ptr"] = buf.data_ptr() + np.arange(n, dtype=np.uint64) * np.uint64(clen)
+            d["len"] = clen
+            d["start_raw"] = 0xFFFFFFFF
+            d["type"] = 1
+            d["mem"] = 0
+            bufs.append(buf)
+            descs.append(d)
+        for dv in set(devices):
+            torch.cuda.synchronize(dv)
+        d = np.concatenate(descs)
+        _, want = m.batch_create(d)  # the stored checksums (h3c_multi_batch_create)
+        g = torch.Generator().manual_seed(SEED + 17)
+        for k, buf in enumerate(bufs):
+            nflip = int(n * args.flip_frac)
+            fl = torch.randperm(n, generator=g)[:nflip].sort().values
+            pos = fl * clen + torch.randint(0, clen, (nflip,), generator=g)
+            bits = (1 << torch.randint(0, 8, (nflip,), generator=g)).to(torch.uint8)
+            pos_d = pos.to(buf.device)
+            buf[pos_d] ^= bits.to(buf.device)
+            flips_all.append(fl.numpy() + k * n)
+        for dv in set(devices):
+            torch.cuda.synchronize(dv)
+        plan = m.plan(d)
+        try:
+            for _ in range(args.warmup):
+                plan.verify(want)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                nbad = plan.verify(want)
+            el = time.perf_counter() - t0
+            stats = m.last_stats()
+            flips = np.concatenate(flips_all)
+            bad = np.nonzero(plan.ok == 0)[0]
+            ok = nbad == flips.size and np.array_equal(bad, flips)
+            ok = ok and np.array_equal(np.delete(plan.out, flips), np.delete(want, flips))
+        finally:
+            plan.close()
+    finally:
+        m.close()
+    total = W * n * clen
+    return {
+        "metric": METRIC, "value": round(total * args.steps / el / 2**30, 2), "unit": "GiB/s",
+        "n_gpus": len(set(devices)), "workers": W, "devices": list(devices), "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64 chunks generated in HBM; 5% of chunks carry one flipped bit)",
+        "config": {"workload": f"{n} x {clen >> 10} KiB device-resident chunks per worker, verified as one batch "
+                               f"through h3c_multi_plan_verify (host expected / results arrays, one process)",
+                   "parallelism": f"inproc{W}", "launcher": "in-process (h3c_multi)"},
+        "verified": bool(ok),
+        "per_worker": [{"device": dv, "chunks": u, "bytes": b, "last_ms": round(ms, 3)}
+                       for dv, (u, b, ms) in zip(devices, stats)],
+        "note": "wall time of whole synchronous calls: expected values in, results and flags out over PCIe",
+    }
 
 
 def cpu_baseline_update(samples: int = 40) -> dict:
@@ -439,12 +534,21 @@ def run_updio(args, cx: Ctx) -> dict:
     h3c.fill_splitmix(chunks, clen, nchunks, clen, SEED, first_chunk=cx.rank * nchunks)
     payload = torch.empty(nw * G, dtype=torch.uint8, device=cx.dev)
     h3c.fill_splitmix(payload, G, nw, G, SEED + 1, first_chunk=cx.rank * nw)
+    # `tables` seeded op tables (different chunk / offset draws over the same payloads), run in rotation:
+    # every timed batch differs from the one before it, as on a real update stream, so nothing the
+    # kernels learn from the previous batch (the aligned branch's per-XCD range weights) flatters them
+    ntab = max(1, int(getattr(args, "updio_tables", 4)))
+    draws = []
+    for t in range(ntab):
+        g = np.random.default_rng(SEED + cx.rank + 7919 * t)
+        wc = g.integers(0, nchunks, nw).astype(np.uint32)
+        wb = g.integers(0, bpc, nw).astype(np.uint32)
+        if getattr(args, "updio_order", "random") == "chunk":  # diagnostics: the ops grouped by chunk
+            o = np.argsort(wc, kind="stable")
+            wc, wb = wc[o], wb[o]
+        draws.append((wc, wb))
+    wc, wb = draws[0]
     g = np.random.default_rng(SEED + cx.rank)
-    wc = g.integers(0, nchunks, nw).astype(np.uint32)
-    wb = g.integers(0, bpc, nw).astype(np.uint32)
-    if getattr(args, "updio_order", "random") == "chunk":  # diagnostics: the ops grouped by chunk
-        o = np.argsort(wc, kind="stable")
-        wc, wb = wc[o], wb[o]
     plan = h3c.Plan.uniform(chunks.data_ptr(), clen, nchunks, device=cx.local)
     raw0 = torch.zeros(nchunks, dtype=torch.int32, device=cx.dev)
     plan.run(raw0, stream=cx.stream)
@@ -458,25 +562,36 @@ def run_updio(args, cx: Ctx) -> dict:
     state["size"] = clen
     state["value"] = raw0.cpu().numpy().view(np.uint32)
     state["type"] = 1
-    ios, _it = _pinned_records(torch, nw, h3c.UPDATE_IO_DTYPE)
-    ios["payload"] = payload.data_ptr() + np.arange(nw, dtype=np.uint64) * np.uint64(G)
-    ios["chunk"] = wc
-    ios["offset"] = wb * G
-    ios["length"] = G
-    ios["checksum_value"] = praw.cpu().numpy().view(np.uint32)
-    ios["checksum_type"] = 1
-    ios["kind"] = h3c.UPD_WRITE
+    praw_np = praw.cpu().numpy().view(np.uint32)
+    tabs = []
+    for twc, twb in draws:
+        t_ios, t_keep = _pinned_records(torch, nw, h3c.UPDATE_IO_DTYPE)
+        t_ios["payload"] = payload.data_ptr() + np.arange(nw, dtype=np.uint64) * np.uint64(G)
+        t_ios["chunk"] = twc
+        t_ios["offset"] = twb * G
+        t_ios["length"] = G
+        t_ios["checksum_value"] = praw_np
+        t_ios["checksum_type"] = 1
+        t_ios["kind"] = h3c.UPD_WRITE
+        tabs.append({"ios": t_ios, "keep": t_keep, "wc": twc,
+                     "d_ios": torch.from_numpy(t_ios.view(np.uint8).copy()).to(cx.dev),
+                     "d_res": torch.zeros(nw * h3c.UPDATE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=cx.dev)})
+    ios = tabs[0]["ios"]
     exact = bool(getattr(args, "exact", False))
     d_state = torch.from_numpy(state.view(np.uint8).copy()).to(cx.dev)
-    d_ios = torch.from_numpy(ios.view(np.uint8).copy()).to(cx.dev)
-    d_res = torch.zeros(nw * h3c.UPDATE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=cx.dev)
+    d_ios, d_res = tabs[0]["d_ios"], tabs[0]["d_res"]
     d_ctr = torch.zeros(8, dtype=torch.int64, device=cx.dev)
 
-    # (bound once: the step is the C call, as for a C++ caller; update_ios_dev re-checks the tensors).
-    # --updio-graphs picks the headline form; the other is timed beside it (`other_form`)
+    # (bound once per table: the step is the C call, as for a C++ caller; update_ios_dev re-checks the
+    # tensors).  --updio-graphs picks the headline form; the other is timed beside it (`other_form`)
     hg = bool(getattr(args, "updio_graphs", 1))
-    step = h3c.UpdateIosDev(d_state, d_ios, d_res, stream=cx.stream, exact=exact, counters=d_ctr,
-                            graphs=hg).run
+    tsteps = [h3c.UpdateIosDev(d_state, t["d_ios"], t["d_res"], stream=cx.stream, exact=exact, counters=d_ctr,
+                               graphs=hg).run for t in tabs]
+    nxt = [0]
+
+    def step():
+        tsteps[nxt[0] % ntab]()
+        nxt[0] += 1
 
     g0 = h3c.diag_counters()
     elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDIO,
@@ -492,8 +607,9 @@ def run_updio(args, cx: Ctx) -> dict:
     fast_steps = diag["fast_batches"]
     aligned_steps = diag["aligned_batches"]
     torch.cuda.synchronize()
+    last_tab = tabs[(nxt[0] - 1) % ntab]
     fin = d_state.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)
-    res = d_res.cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)
+    res = last_tab["d_res"].cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)
     counters = dict(zip((f for f, _ in h3c.UpdateCounters._fields_), d_ctr.cpu().tolist()))
     fresh = torch.zeros(nchunks, dtype=torch.int32, device=cx.dev)
     plan.run(fresh, stream=cx.stream)
@@ -501,6 +617,24 @@ def run_updio(args, cx: Ctx) -> dict:
     fresh_np = fresh.cpu().numpy().view(np.uint32)
     ok = bool((res["status"] == 0).all()) and np.array_equal(fresh_np, fin["value"])
     ok = ok and counters["read_chunk"] == nw and not any(redo.values())
+    # every table once more, each checked right after its run: all ops OK, each chunk's last op reports the
+    # chunk's stored checksum, and that equals a fresh GPU CRC of the chunk's bytes
+    tables_ok = []
+    for ti, t in enumerate(tabs):
+        tsteps[ti]()
+        torch.cuda.synchronize()
+        tfin = d_state.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)
+        tres = t["d_res"].cpu().numpy().view(h3c.UPDATE_RESULT_DTYPE)
+        plan.run(fresh, stream=cx.stream)
+        torch.cuda.synchronize()
+        last = np.full(nchunks, -1, dtype=np.int64)
+        np.maximum.at(last, t["wc"].astype(np.int64), np.arange(nw))  # each chunk's last op
+        hit = last >= 0
+        tok = bool((tres["status"] == 0).all()) and np.array_equal(fresh.cpu().numpy().view(np.uint32), tfin["value"])
+        tok = tok and np.array_equal(tres["value"][last[hit]], tfin["value"][hit])
+        tables_ok.append(tok)
+    ok = ok and all(tables_ok)
+    fin = d_state.cpu().numpy().view(h3c.CHUNK_STATE_DTYPE)
     # independent of the GPU: a sample of chunks copied back and CRC'd by the CPU oracle (the chunks'
     # stored checksums after every batch must be the CRC32C of their bytes, ChunkReplica.cc:356-390)
     L = _oracle()
@@ -557,8 +691,11 @@ def run_updio(args, cx: Ctx) -> dict:
         "config": {"workload": f"BASELINE config 3 via h3c_update_ios_dev{' (H3C_UPD_EXACT)' if exact else ''}: "
                                f"{nw} random 4 KiB UpdateIOs into {nchunks} x 64 MiB chunks per GPU, op / chunk / "
                                f"result tables in HBM",
-                   "parallelism": f"shard{cx.world}", "exact": exact},
+                   "parallelism": f"shard{cx.world}", "exact": exact, "tables": ntab,
+                   "table_rotation": f"{ntab} seeded op tables run in turn (batch k uses table k mod {ntab}); "
+                                     "host-array and other-form legs use table 0"},
         "verified": verified,
+        "tables_verified": tables_ok,
         # the minimum traffic per write: its payload read, its block read and written (3 x 4 KiB);
         # the A6 check of a one-block write runs inside the block kernel on the payload it reads
         "algorithmic_gbps": round(writes * 3 * G / elapsed / 1e9, 1),
@@ -948,6 +1085,28 @@ def dry_run_launch(args) -> int:
     return 0
 
 
+def main_inproc(args) -> int:
+    """bench.py --gpus N --inproc [--devices LIST]: the headline verify over N GPUs from this one process
+    through the C-ABI multi engine (h3c_multi_*), the way a C++ storage service drives them."""
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
+        print("bench.py: --inproc runs in one process; do not launch it with torchrun", file=sys.stderr, flush=True)
+        return 2
+    import torch
+
+    devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    ndev = torch.cuda.device_count()
+    if any(d >= ndev for d in devices) or len(devices) != args.gpus:
+        print(f"bench.py: --inproc wants {args.gpus} device(s) {devices}, {ndev} visible", file=sys.stderr, flush=True)
+        return 2
+    cx = Ctx()
+    res = run_inproc(args, cx, devices)
+    res["config"]["devices_visible"] = ndev
+    if len(set(devices)) < len(devices):
+        res["rehearsal"] = True  # workers share devices: n_gpus counts distinct GPUs
+    print(json.dumps(res), flush=True)
+    return 0 if res["verified"] else 1
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--dry-run-launch", type=int, default=None, help=argparse.SUPPRESS)
@@ -964,6 +1123,14 @@ def main() -> int:
                     help="default verify run: also a short host-fed pass of this many GiB per GPU (0: off)")
     ap.add_argument("--update-extra", type=int, choices=[0, 1], default=1,
                     help="default verify run: also a short BASELINE config-3 UpdateIO pass (the `update` object)")
+    ap.add_argument("--shard4m-extra", type=int, choices=[0, 1], default=1,
+                    help="default verify run: also config 4's per-GPU share, 8192 x 4 MiB (the `shard4m` object)")
+    ap.add_argument("--inproc-extra", type=int, choices=[0, 1], default=1,
+                    help="default verify run: also the in-process multi-GPU product path (the `inproc` object)")
+    ap.add_argument("--inproc", action="store_true",
+                    help="one process drives --gpus devices through h3c_multi_* (no launcher, no torch.distributed)")
+    ap.add_argument("--devices", default=None,
+                    help="--inproc: comma-separated device list (a device may repeat: workers sharing one GPU)")
     ap.add_argument("--mixed-gib", type=int, default=8)
     ap.add_argument("--mixed-aligned", action="store_true", help="no ragged lengths (every chunk 64 KiB-aligned)")
     ap.add_argument("--window-mib", type=int, default=64)
@@ -980,6 +1147,8 @@ def main() -> int:
     ap.add_argument("--updio-graphs", type=int, choices=[0, 1], default=1,
                     help="updio: the headline leg as one replayed graph per batch (1) or plain launches (0); "
                          "the other form is timed beside it")
+    ap.add_argument("--updio-tables", type=int, default=4,
+                    help="updio: seeded op tables run in rotation (every batch differs from the last)")
     ap.add_argument("--sync-threads", type=int, default=32)
     ap.add_argument("--sync-kib", default="4,128,1024", help="sync: buffer sizes (KiB), comma-separated")
     args = ap.parse_args()
@@ -987,6 +1156,8 @@ def main() -> int:
     if err:
         print(f"bench.py: {err}", file=sys.stderr, flush=True)
         return 2
+    if args.inproc:
+        return main_inproc(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus, sys.argv[1:], float(os.environ.get("H3C_BENCH_GRACE_S", "60")))
     if args.dry_run_launch is not None:
@@ -1029,6 +1200,7 @@ def main() -> int:
         res["update"] = {
             "metric": up["metric"], "config": up["config"]["workload"], "n_gpus": up["n_gpus"],
             "steps": up["steps"], "warmup": up["warmup"], "ms_per_step": up["ms_per_step"],
+            "tables": up["config"]["tables"], "tables_verified": up["tables_verified"],
             "writes_per_s": up["value"], "unit": "writes/s", "scaling": "weak", "verified": up["verified"],
             "branch": up["branch"], "redo": up["redo"], "counters": up["counters"],
             "oracle_sample": up["oracle_sample"], "algorithmic_gbps": up["algorithmic_gbps"],
@@ -1038,6 +1210,35 @@ def main() -> int:
         if "cpu_baseline" in up:
             res["update"]["cpu_baseline"] = up["cpu_baseline"]
         res["verified"] = res["verified"] and up["verified"]
+    if args.workload == "verify" and args.shard4m_extra and (args.chunks, args.chunk_kib) == (8192, 1024):
+        # BASELINE config 4's per-GPU share in front of the driver: 8192 x 4 MiB = 32 GiB, the
+        # N=8 share of 256 GiB, verified against 5% flipped chunks (never the `value`)
+        sub = argparse.Namespace(**vars(args))
+        sub.chunks, sub.chunk_kib, sub.steps, sub.warmup, sub.no_cpu_baseline = 8192, 4096, 20, 5, True
+        r4 = run_verify(sub, cx)
+        res["shard4m"] = {
+            "metric": "GiB/s CRC32C verified (4 MiB chunks, the per-GPU share of 256 GiB at 8 GPUs)",
+            "value": r4["value"], "unit": "GiB/s", "n_gpus": r4["n_gpus"], "steps": r4["steps"],
+            "warmup": r4["warmup"], "ms_per_step": r4["ms_per_step"], "scaling": "weak",
+            "config": f"BASELINE config 4 share: 8192 x 4 MiB = 32 GiB device-resident per GPU "
+                      f"({cx.world} x 32 GiB in this job), 5% of chunks with one flipped bit",
+            "verified": r4["verified"], "roofline": r4["roofline"],
+            "note": "at N=8 the job verifies the whole 256 GiB of config 4; not the headline value",
+        }
+        res["verified"] = res["verified"] and r4["verified"]
+    if args.workload == "verify" and args.inproc_extra and (args.chunks, args.chunk_kib) == (8192, 1024):
+        # the product path over all of this job's GPUs from ONE process (h3c_multi_*): rank 0 drives every
+        # device of the job while the other ranks wait at a barrier (never the `value`)
+        cx.barrier()
+        if cx.rank == 0:
+            sub = argparse.Namespace(**vars(args))
+            sub.steps, sub.warmup = 20, 3
+            ip = run_inproc(sub, cx, [r % max(cx.ndev, 1) for r in range(cx.world)])
+            res["inproc"] = {k: ip[k] for k in ("value", "unit", "n_gpus", "workers", "devices", "steps", "warmup",
+                                                 "ms_per_step", "verified", "per_worker", "note")}
+            res["inproc"]["config"] = ip["config"]["workload"]
+        ok_ip = cx.all_true(res.get("inproc", {}).get("verified", True))
+        res["verified"] = res["verified"] and ok_ip
     # N ranks on fewer devices (--allow-shared-devices) is a rehearsal: n_gpus is the devices used
     res.setdefault("config", {})["devices_visible"] = cx.ndev
     if cx.world > cx.ndev:

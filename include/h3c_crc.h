@@ -171,7 +171,11 @@ int h3c_batch_combine(uint8_t type, const uint32_t *c1_dev, const uint32_t *c2_d
  * look-back state in a library-owned scratch per (device, stream) -- about 1 MiB plus 4 bytes
  * per write rounded up to a power of two, never cleared between batches (epoch-tagged) -- rather
  * than in the workspace; calls on one stream from several threads enqueue one at a time.  A call
- * made while the stream is being captured into a graph uses the workspace instead. */
+ * made while the stream is being captured into a graph uses the workspace instead.  Up to 64 such scratches
+ * live at once; past that the least recently used idle one is freed (after a device synchronisation) and
+ * reused.  A stream that ran h3c_update_blocks batches is released with h3c_stream_release before it is
+ * destroyed: a new stream may come back with the same handle value and must not inherit the scratch. */
+int h3c_stream_release(void *stream);
 size_t h3c_update_workspace_bytes(uint32_t n_blocks, uint32_t nchunks, uint64_t chunk_len, uint32_t block_bytes);
 int h3c_update_blocks(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nchunks, uint64_t chunk_len,
                       uint32_t block_bytes, const uint32_t *chunk_raw_in_dev, const uint32_t *blk_chunk_dev,

@@ -120,6 +120,25 @@ def test_scratch_two_streams_interleaved(h3c, torch_dev, hooks):
         stores[k].batch(h3c, rng, int(rng.integers(1, 2500)), n_invalid=b % 3, stream=streams[k])
 
 
+def test_scratch_more_streams_than_the_table_and_release(h3c, torch_dev, hooks):
+    """72 streams, each one batch then another round (more than the 64 scratches the library keeps: the
+    least recently used idle one is evicted and reused), then every stream released before it goes
+    (h3c_stream_release); all batches exact.  (scratches were never freed, a 65th stream fell
+    back to the workspace for good, and a recycled stream handle inherited a live scratch.)"""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_SCAN, h3c.UPD_SCAN_PATHS["fused"])
+    rng = np.random.default_rng(505)
+    streams = [torch.cuda.Stream() for _ in range(72)]
+    store = Store(torch, dev, rng, 4, 128 << 10)
+    for rnd in range(2):
+        for k, s in enumerate(streams):
+            store.batch(h3c, rng, int(rng.integers(100, 1200)), n_invalid=k % 2, stream=s)
+    for s in streams:
+        h3c.stream_release(s)
+    h3c.stream_release(streams[0])  # (again: nothing left to release)
+    store.batch(h3c, rng, 2000, stream=streams[3])  # a released stream gets a fresh scratch
+
+
 def test_scratch_threads_on_one_stream(h3c, torch_dev, hooks):
     """Four threads issue batches on the same (default) stream without waiting on each other: each
     call's launches are enqueued whole, so each thread's chunks end exact."""
