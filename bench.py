@@ -540,7 +540,7 @@ def run_updio(args, cx: Ctx) -> dict:
     ntab = max(1, int(getattr(args, "updio_tables", 4)))
     draws = []
     for t in range(ntab):
-        g = np.random.default_rng(SEED + cx.rank + 7919 * t)
+        g = np.random.default_rng(SEED + cx.rank + (0 if getattr(args, "updio_same_tables", False) else 7919 * t))
         wc = g.integers(0, nchunks, nw).astype(np.uint32)
         wb = g.integers(0, bpc, nw).astype(np.uint32)
         if getattr(args, "updio_order", "random") == "chunk":  # diagnostics: the ops grouped by chunk
@@ -1149,6 +1149,7 @@ def main() -> int:
                          "the other form is timed beside it")
     ap.add_argument("--updio-tables", type=int, default=4,
                     help="updio: seeded op tables run in rotation (every batch differs from the last)")
+    ap.add_argument("--updio-same-tables", action="store_true", help=argparse.SUPPRESS)  # (diagnostics: one draw)
     ap.add_argument("--sync-threads", type=int, default=32)
     ap.add_argument("--sync-kib", default="4,128,1024", help="sync: buffer sizes (KiB), comma-separated")
     args = ap.parse_args()

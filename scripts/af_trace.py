@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.argv = [sys.argv[0], "--workload", "updio", "--no-cpu-baseline", "--steps", "5", "--warmup", "30",
+sys.argv = [sys.argv[0], "--workload", "updio", "--no-cpu-baseline", "--steps", "5", "--warmup", "30", "--updio-tables", os.environ.get("AF_TABLES", "4"),
             "--updio-graphs", "0"]
 bench = importlib.import_module("bench")
 h3c = importlib.import_module("3fs_amd")

@@ -6,7 +6,7 @@ name=$1; shift
 R=$(cd $(dirname $0)/.. && pwd)
 O=$R/3fs_amd/_lib/diag/$name
 mkdir -p $O/obj
-for f in h3c_engine h3c_update h3c_hostfed h3c_updio h3c_formats; do
+for f in h3c_engine h3c_update h3c_hostfed h3c_updio h3c_formats h3c_multi; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I $R/include "$@" -c $R/3fs_amd/csrc/$f.hip -o $O/obj/$f.o &
 done
 wait

@@ -247,3 +247,19 @@ def test_aligned_std_domain_matches_other_branches(h3c, torch_dev, hooks):
     assert ak["recalculate"] == int((ar["status"] == 0).sum()) and ak["read_chunk"] == 0
     for c in range(n):
         assert int(ac[c]["value"]) == (~orc.crc32c(ab[c])) & MASK
+
+
+@pytest.mark.parametrize("giveup", [8, 16])
+def test_aligned_void_pass_multi_write_blocks_first_writer_failed(h3c, torch_dev, hooks, giveup):
+    """A void aligned pass (GIVEUP bit 3: ticket 1 gives up its look-back; bit 4: the pass reports itself void)
+    over hot multi-write blocks where 30 % of the checks fail, first writers included: uio_afix_kernel must
+    rebuild each op's delta against the last passing op before it on its block, or -- when every earlier op of
+    the block failed -- against the block's original bytes through the FIRST op's records (crc0(old) =
+    D_first ^ crc0(new_first)).  r05l (work-in-progress code, never committed) returned wrong results from
+    the first block-first-writer op of a forced void pass onward; check_modes' per-mode oracle comparison
+    names the mode and the ops."""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_UPD_GIVEUP, giveup)
+    rng = np.random.default_rng(61 + giveup)
+    sc = aligned_scenario(h3c, torch, dev, rng, nchunks=8, chunk_size=64 << 10, nops=6000, bad=0.3, hot_blocks=5)
+    check_modes(h3c, hooks, sc, recovered=1, dev_api=True)
