@@ -3163,6 +3163,7 @@ __device__ unsigned long long g_af_wg[1024 * 5];
 __device__ unsigned long long g_af_wave[1024 * 16];
 __device__ uint32_t g_af_blk[1024 * 4];  // per ticket: blockIdx, XCC, range start, range end
 __device__ uint32_t g_af_fin[1024 * 16];  // per wave: its ops whose block has later writes (the fin path)
+__device__ unsigned long long g_af_entry[1024 * 2];  // per blockIdx: kernel entry, ticket taken
 #endif
 #ifndef H3C_AF_EARLY_OLD
 #define H3C_AF_EARLY_OLD 0  // 1: the next op's old rows load with its new rows, before this op's CRCs (A/B)
@@ -3349,6 +3350,9 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   // the kernel's own span (bench / profiling): the first-dispatched workgroup's entry (one store, not one
   // atomic per workgroup on one address) and the last workgroup's end
   if (t == 0 && blockIdx.x == 0) *reinterpret_cast<unsigned long long *>(misc + kMiscT0) = wall_clock64();
+#if H3C_AF_TRACE
+  if (t == 0 && blockIdx.x < 1024) g_af_entry[2 * blockIdx.x] = wall_clock64();
+#endif
   if (t == 0) {
     s_E = ld_agent(&aa.ctl[kAEpoch]) & 0xFFu;
     s_slow = ld_agent(&aa.ctl[kASlow]);
@@ -3366,6 +3370,9 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
                                              (1ull << 40) | wmine);
     const uint64_t cum = old & ((1ull << 40) - 1);
     s_ticket = (uint32_t)(old >> 40);
+#if H3C_AF_TRACE
+    if (blockIdx.x < 1024) g_af_entry[2 * blockIdx.x + 1] = wall_clock64();
+#endif
 #if H3C_AF_SKEW  // (A/B) early positions carry more work per op (a block's first of several writes): the
                   // cut points warped by p(f) = f - b f (1 - f), b = H3C_AF_SKEW / 1000
     auto warp = [&](uint64_t c) -> uint32_t {
@@ -5688,6 +5695,9 @@ extern "C" int h3c_update_ios(uint8_t poly_type, h3c_chunk_state *chunks, uint32
 #if H3C_AF_TRACE
 extern "C" int h3c_diag_af_trace(unsigned long long *out, int n) {  // (trace builds only)
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_af_wg), 40ull * (unsigned)n) == hipSuccess ? 0 : -1;
+}
+extern "C" int h3c_diag_af_entry(unsigned long long *out, int n) {  // (trace builds only)
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_af_entry), 16ull * (unsigned)n) == hipSuccess ? 0 : -1;
 }
 extern "C" int h3c_diag_af_waves(unsigned long long *out, uint32_t *blk, uint32_t *fin, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_af_wave), 128ull * (unsigned)n) == hipSuccess &&

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.argv = [sys.argv[0], "--workload", "updio", "--no-cpu-baseline", "--steps", "5", "--warmup", "30", "--updio-tables", os.environ.get("AF_TABLES", "4"),
+sys.argv = [sys.argv[0], "--workload", "updio", "--no-cpu-baseline", "--steps", "5", "--warmup", "30", "--updio-tables", os.environ.get("AF_TABLES", "4"), "--updio-headline-only",
             "--updio-graphs", "0"]
 bench = importlib.import_module("bench")
 h3c = importlib.import_module("3fs_amd")
@@ -26,6 +26,18 @@ khz = 100000.0  # the wall clock's 100 MHz
 t0 = a[:, 0].min()
 us = (a - t0) / (khz / 1000.0)
 names = ["start", "filled", "loop_end", "lookback_end", "end"]
+lib.h3c_diag_af_entry.argtypes = [ctypes.c_void_p, ctypes.c_int]
+ent = (ctypes.c_ulonglong * (2 * 1024))()
+assert lib.h3c_diag_af_entry(ent, 1024) == 0
+e = np.array(ent[:2 * nwg], dtype=np.float64).reshape(nwg, 2)
+e0 = e[:, 0].min()
+eu = (e - e0) / (khz / 1000.0)
+print("kernel entry -> post-fill sync (us): first entry 0; entry q0/q50/q100 = %.1f/%.1f/%.1f; ticket taken "
+      "q0/q50/q100 = %.1f/%.1f/%.1f; sync passed q0/q100 = %.1f/%.1f" % (
+          *np.percentile(eu[:, 0], [0, 50, 100]), *np.percentile(eu[:, 1], [0, 50, 100]),
+          (a[:, 0].min() - e0) / (khz / 1000.0), (a[:, 0].max() - e0) / (khz / 1000.0)))
+print("entry order vs ticket wait (us), first 8 by entry:", [(round(float(x), 1), round(float(y - x), 1))
+                                                          for x, y in sorted(eu.tolist())[:8]])
 for q in (0, 50, 90, 99, 100):
     print(f"q{q:3d} " + " ".join(f"{n}={np.percentile(us[:, i], q):7.1f}" for i, n in enumerate(names)))
 print("per-wg loop time (loop_end - filled): median %.1f max %.1f" % (np.median(us[:, 2] - us[:, 1]), (us[:, 2] - us[:, 1]).max()))
