@@ -149,7 +149,6 @@ constexpr uint32_t kFlagNone = 1u;
 // base + i * stride with result i, no descriptor reads.
 struct UniformBatch {
   uint32_t lanes = 0;  // 4, 8 or 16 lanes per chunk; 0: not uniform
-  bool pair = false;   // 8 lanes walk two chunks each (seg_uni_kernel<8, 2>)
   uint32_t rows = 0;   // rows of 16 * lanes bytes per chunk
   uint32_t xs = 0;     // the shared start's share of the raw CRC
   bool contiguous = false;
@@ -467,36 +466,19 @@ __device__ __forceinline__ uint32_t dxpow8_fast(int64_t e, const PolyConsts *__r
   return dxpow8s(e, pc, poly);
 }
 
-#ifndef H3C_PERM_LAYOUT
-#define H3C_PERM_LAYOUT 1
-#endif
-#ifndef H3C_FAST_FILL
-#define H3C_FAST_FILL 1  // fill_tables: one load per table entry (0: one per LDS dword, for A/B)
-#endif
-#ifndef H3C_XOR3_ASM
-#define H3C_XOR3_ASM 1
-#endif
 
 // Per-lane LDS addressing of the replicated tables (see kernel header comment): two registers;
 // the tables' remaining offsets ride in the ds_read immediate.
-#ifndef H3C_LUT2
-#define H3C_LUT2 1  // 0: four offset registers (round 2's form, for A/B)
-#endif
 struct LaneLut {
-  uint32_t off[H3C_LUT2 ? 2 : 4];
+  uint32_t off[2];
 };
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-#if H3C_XOR3_ASM
   uint32_t d;  // gfx950 has no v_xor3_b32; v_bitop3_b32 with truth table 0x96 is a^b^c
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
   return d;
-#else
-  return a ^ b ^ c;
-#endif
 }
 
-#if H3C_PERM_LAYOUT
 // Layout: table t (0..3), entry b, copy c at byte address
 //   (t>>1)*64 KiB + b*256 + (t&1)*128 + c*4,
 // i.e. each 256-byte LDS row holds entry b of two tables x 32 copies.  ds_read_b32
@@ -504,7 +486,6 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // address is one v_perm_b32: byte1 <- byte k of r, bytes 0 and 2 <- the lane's
 // lane offset (byte0 = c<<2, byte2 = t>>1: off[t>>1]), byte3 <- 0; the (t&1)<<7 of tables 1 and 3
 // is the ds_read's immediate offset (two offset registers a lane instead of four).
-#if H3C_LUT2
 __device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
   LaneLut L;
   const uint32_t c4 = (lane & 31u) * 4u;
@@ -523,26 +504,6 @@ __device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const L
   const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3 + 128);
   return xor3(t0, t1, t2) ^ t3;
 }
-#else
-__device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
-  LaneLut L;
-  const uint32_t c4 = (lane & 31u) * 4u;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) L.off[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) << 7) | c4;
-  return L;
-}
-__device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const LaneLut &L) {
-  const uint32_t a0 = __builtin_amdgcn_perm(r, L.off[0], 0x0C020400u);
-  const uint32_t a1 = __builtin_amdgcn_perm(r, L.off[1], 0x0C020500u);
-  const uint32_t a2 = __builtin_amdgcn_perm(r, L.off[2], 0x0C020600u);
-  const uint32_t a3 = __builtin_amdgcn_perm(r, L.off[3], 0x0C020700u);
-  const uint32_t t0 = *reinterpret_cast<const uint32_t *>(lb + a0);
-  const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1);
-  const uint32_t t2 = *reinterpret_cast<const uint32_t *>(lb + a2);
-  const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3);
-  return xor3(t0, t1, t2) ^ t3;
-}
-#endif
 // LDS dword i holds table ((i>>14)<<1 | (i>>5)&1), entry (i>>6)&255.
 __device__ __forceinline__ uint32_t fill_value_of(const uint32_t (*tab)[256], int i) {
   return tab[((i >> 14) << 1) | ((i >> 5) & 1)][(i >> 6) & 255];
@@ -573,29 +534,6 @@ __device__ __forceinline__ uint32_t row_step16(uint32_t r, const char *lb, const
 __device__ __forceinline__ uint32_t fill_value16_of(const uint32_t (*tab)[256], int i) {
   return tab[(i >> 4) & 3][(i >> 6) & 255];
 }
-#else
-// Layout: table k, entry b, copy c at byte address k*32 KiB + b*128 + c*4.
-__device__ __forceinline__ LaneLut make_lut(uint32_t lane) {
-  LaneLut L;
-  L.off[0] = (lane & 31u) * 4u;
-  L.off[1] = L.off[0] + 65536u;
-  return L;
-}
-__device__ __forceinline__ uint32_t row_step(uint32_t r, const char *lb, const LaneLut &L) {
-  const uint32_t a0 = ((r << 7) & 0x7F80u) | L.off[0];
-  const uint32_t a1 = ((r >> 1) & 0x7F80u) | L.off[0];
-  const uint32_t a2 = ((r >> 9) & 0x7F80u) | L.off[1];
-  const uint32_t a3 = ((r >> 17) & 0x7F80u) | L.off[1];
-  const uint32_t t0 = *reinterpret_cast<const uint32_t *>(lb + a0);
-  const uint32_t t1 = *reinterpret_cast<const uint32_t *>(lb + a1 + 32768);
-  const uint32_t t2 = *reinterpret_cast<const uint32_t *>(lb + a2);
-  const uint32_t t3 = *reinterpret_cast<const uint32_t *>(lb + a3 + 32768);
-  return xor3(t0, t1, t2) ^ t3;
-}
-__device__ __forceinline__ uint32_t fill_value_of(const uint32_t (*tab)[256], int i) {
-  return tab[i >> 13][(i >> 5) & 255];
-}
-#endif
 // The replicated stride tables and the fold tables into LDS (no barrier: the caller's).  With
 // the 32-copy layout each table entry is loaded from HBM / L2 once and its 32 copies -- 128
 // contiguous bytes -- written with 8 ds_write_b128 (the dword-per-copy loop loaded every entry 32
@@ -603,7 +541,6 @@ __device__ __forceinline__ uint32_t fill_value_of(const uint32_t (*tab)[256], in
 // `lds` must be 16-byte aligned; `red_words` a multiple of 4.
 __device__ __forceinline__ void fill_tables(uint32_t *lds, const uint32_t (*tab)[256], const uint32_t *red_g,
                                             uint32_t red_words, uint32_t tid, uint32_t nthreads) {
-#if H3C_PERM_LAYOUT && H3C_FAST_FILL
   for (uint32_t e = tid; e < 1024u; e += nthreads) {
     const uint32_t t = e >> 8, b = e & 255u;
     const uint32_t v = tab[t][b];
@@ -615,10 +552,6 @@ __device__ __forceinline__ void fill_tables(uint32_t *lds, const uint32_t (*tab)
   const uint4 *rs = reinterpret_cast<const uint4 *>(red_g);
   uint4 *rd = reinterpret_cast<uint4 *>(lds + kLdsWords);
   for (uint32_t i = tid; i < red_words / 4u; i += nthreads) rd[i] = rs[i];
-#else
-  for (uint32_t i = tid; i < (uint32_t)kLdsWords; i += nthreads) lds[i] = fill_value_of(tab, i);
-  for (uint32_t i = tid; i < red_words; i += nthreads) lds[kLdsWords + i] = red_g[i];
-#endif
 }
 // The LDS image of the 1 KiB-stride tables (rows of 64 lanes x 16 B).
 __device__ __forceinline__ uint32_t fill_value(const PolyConsts *__restrict__ pc, int i) {
@@ -734,14 +667,12 @@ __device__ __forceinline__ void consume(Streams &st, uint4 v, const char *lb, co
   st.s2 = row_step(st.s2 ^ v.z, lb, L);
   st.s3 = row_step(st.s3 ^ v.w, lb, L);
 }
-#if H3C_PERM_LAYOUT
 __device__ __forceinline__ void consume16(Streams &st, uint4 v, const char *lb, const LaneLut &L) {
   st.s0 = row_step16(st.s0 ^ v.x, lb, L);
   st.s1 = row_step16(st.s1 ^ v.y, lb, L);
   st.s2 = row_step16(st.s2 ^ v.z, lb, L);
   st.s3 = row_step16(st.s3 ^ v.w, lb, L);
 }
-#endif
 
 // a * C for the constant whose byte tables start at `t` (4 x 256 dwords in LDS).
 __device__ __forceinline__ uint32_t tab_mul(uint32_t a, const uint32_t *t) {
@@ -802,12 +733,6 @@ __device__ __forceinline__ void wave_fold_tab_n(const Streams (&st)[N], uint32_t
 constexpr uint32_t kSmallRows = 8;  // segments of at most this many rows load all rows at once
 constexpr int kUnroll = H3C_UNROLL;  // rows in flight per batch (x2 with the prefetch)
 
-#ifndef H3C_SEG_ABS_ROWS
-#define H3C_SEG_ABS_ROWS 1  // rows on absolute 1 KiB boundaries (else: ending at the segment end)
-#endif
-#ifndef H3C_SEG_FOLD_TAB
-#define H3C_SEG_FOLD_TAB 1  // table-driven wave fold (else: 4 bit-serial GF(2) multiplies per lane)
-#endif
 
 // init-0 CRC of bytes [S, E) (E > S), computed by one wavefront; valid in lane 0.
 // The rows are the 1 KiB blocks [A, B) of absolute addresses covering [S, E), so every
@@ -818,13 +743,8 @@ constexpr int kUnroll = H3C_UNROLL;  // rows in flight per batch (x2 with the pr
 __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, const char *lb, const LaneLut &L,
                                         const uint32_t fix[4], const uint32_t *red,
                                         const PolyConsts *__restrict__ pc, uint32_t poly, uint32_t dbg) {
-#if H3C_SEG_ABS_ROWS
   const uint64_t A = S & ~uint64_t(kRowBytes - 1);
   const uint64_t B = (E + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
-#else
-  const uint64_t B = (E + 15) & ~uint64_t(15);
-  const uint64_t A = B - ((B - (S & ~uint64_t(15)) + kRowBytes - 1) / kRowBytes) * kRowBytes;
-#endif
   const uint32_t K = (uint32_t)((B - A) / kRowBytes);
   const uint64_t base = A + 16u * lane;
 
@@ -885,29 +805,6 @@ __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, c
     uint4 a[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) a[u] = ld(r + u);
-#if H3C_PINGPONG
-    // The two-buffer ping-pong form of the note above, kept as the miscompile reproducer
-    // (scripts/pingpong_repro.sh builds it at -O3 and -O1; profiles/r02_pingpong_repro.txt).
-    for (;;) {
-      uint4 b[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) b[u] = ld(r + kUnroll + u);
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) consume(st, a[u], lb, L);
-      r += kUnroll;
-      if (r + kUnroll > plain_end) {
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) a[u] = b[u];
-        break;
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) a[u] = ld(r + kUnroll + u);
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) consume(st, b[u], lb, L);
-      r += kUnroll;
-      if (r + kUnroll > plain_end) break;
-    }
-#else
     for (;;) {
       uint4 b[kUnroll];
 #pragma unroll
@@ -919,7 +816,6 @@ __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, c
       for (int u = 0; u < kUnroll; ++u) a[u] = b[u];
       if (r + kUnroll > plain_end) break;
     }
-#endif
     // a[] holds rows r .. r+kUnroll-1; fewer than kUnroll plain rows remain.
 #pragma unroll
     for (int u = 0; u < kUnroll - 1; ++u)
@@ -931,20 +827,8 @@ __device__ inline uint32_t segment_crc0(uint64_t S, uint64_t E, uint32_t lane, c
   if (K >= 2 && !tail_done) consume(st, load_masked(base + (uint64_t)(K - 1) * kRowBytes, S, E), lb, L);
 
   // Move every stream back to B (stream (l, j) ends 16l + 4j bytes past it).
-#if H3C_SEG_FOLD_TAB
   (void)fix;
   uint32_t acc = wave_fold_tab(st, lane, red);
-#else
-  (void)red;
-  // The per-lane constants are made opaque so the compiler does not hoist 4 x 32
-  // shifted copies of them out of the segment loop (that spills).
-  uint32_t f0 = fix[0], f1 = fix[1], f2 = fix[2], f3 = fix[3];
-  asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
-  uint32_t acc = dgf_mul(f0, st.s0, poly) ^ dgf_mul(f1, st.s1, poly) ^ dgf_mul(f2, st.s2, poly) ^
-                 dgf_mul(f3, st.s3, poly);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
-#endif
   // ... then drop the B - E trailing zeros: x^-(8*pad) = x^-(8*16*(pad>>4)) * x^-(8*(pad&15))
   const uint32_t pad = (uint32_t)(B - E);
   if (pad >> 4) acc = dgf_mul(acc, pc->fix[4 * (pad >> 4)], poly);

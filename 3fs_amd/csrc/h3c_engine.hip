@@ -45,15 +45,9 @@
 
 #include "h3c_common.hpp"
 
-#ifndef H3C_SMALL_EXP
-#define H3C_SMALL_EXP 0  // timing-only builds of seg_small_kernel: bit0 no lookups, bit1 no fold
-#endif
 
 namespace {
 
-#ifndef H3C_SEG_FUSE_FIN
-#define H3C_SEG_FUSE_FIN 1  // batches of one segment per chunk finish in seg_crc_kernel (0: finalize_kernel, A/B)
-#endif
 // Kernel A: one wave per segment; waves take contiguous segment ranges.  With `fin` (every chunk
 // exactly one segment: config 2's 1 MiB chunks) the wave finishes its chunk itself -- the init's
 // share, the result, the verify flag and count -- and no finalize launch follows.
@@ -64,8 +58,8 @@ __device__ __forceinline__ void seg_crc_kernel_body(const DevChunk *__restrict__
                                                            const uint32_t *__restrict__ expected,
                                                            uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
                                                            uint32_t *__restrict__ mismatch) {
-  __shared__ alignas(16) uint32_t lds[kLdsWords + (H3C_SEG_FOLD_TAB ? kRedWords : 0)];
-  fill_tables(lds, pc->tab, &pc->red[0][0][0], H3C_SEG_FOLD_TAB ? kRedWords : 0, threadIdx.x, kThreads);
+  __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
+  fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kThreads);
   __syncthreads();
   const uint32_t *red = lds + kLdsWords;
 
@@ -133,26 +127,7 @@ __global__ __launch_bounds__(kThreads) void seg_crc_kernel(const DevChunk *__res
   stamp_end(ts);
 }
 
-// Kernel A': batches whose every chunk is one short segment (<= kSmallRows rows, e.g. 4 KiB
-// read / write buffers).  Per segment the big kernel pays dependent metadata loads and a
-// drained pipeline; here a wave loads the descriptors of 64 chunks at once (lane k holds
-// chunk k's), issues the next chunk's rows before folding the current one, and writes the
-// final raw value (and verify flag) itself -- no finalize launch.
-__device__ __forceinline__ uint32_t small_rows(uint64_t S, uint64_t E) {
-  return (uint32_t)((((E + kRowBytes - 1) & ~uint64_t(kRowBytes - 1)) - (S & ~uint64_t(kRowBytes - 1))) / kRowBytes);
-}
-// All R row loads of a chunk, unconditionally (a fixed count keeps the compiler's vmcnt
-// bookkeeping exact, so the next chunk's loads stay in flight while this one is folded):
-// rows past the chunk's last re-read it (cache hits).  Whole 1 KiB rows are read; they
-// never leave the 4 KiB pages that hold payload bytes, and bytes outside [S, E) are
-// masked off when the row is consumed.
-template <int R>
-__device__ __forceinline__ void small_load(uint64_t S, uint64_t E, uint32_t lane, uint4 (&v)[R]) {
-  const uint64_t base = (S & ~uint64_t(kRowBytes - 1)) + 16u * lane;
-  const uint32_t K = small_rows(S, E);
-#pragma unroll
-  for (int u = 0; u < R; ++u) v[u] = load_row(base + (uint64_t)min((uint32_t)u, K - 1) * kRowBytes);
-}
+// Bytes of a row outside a chunk's [S, E) masked off (the small-chunk kernels' edge rows).
 __device__ __forceinline__ uint4 mask_row(uint4 v, uint64_t a, uint64_t S, uint64_t E) {
   v.x &= byte_mask(a, S, E);
   v.y &= byte_mask(a + 4, S, E);
@@ -161,137 +136,14 @@ __device__ __forceinline__ uint4 mask_row(uint4 v, uint64_t a, uint64_t S, uint6
   return v;
 }
 
-template <int R>
-__device__ __forceinline__ void seg_small_kernel_body(const DevChunk *__restrict__ chunks, uint32_t nchunks,
-                                                             const PolyConsts *__restrict__ pc,
-                                                             const uint32_t *__restrict__ expected,
-                                                             uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
-                                                             uint32_t *__restrict__ mismatch) {
-  __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
-  fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kThreads);
-  __syncthreads();
-  const uint32_t *red = lds + kLdsWords;
-  const char *lb = reinterpret_cast<const char *>(lds);
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint32_t lo = (uint32_t)(gw * nchunks / nw), hi = (uint32_t)((gw + 1) * nchunks / nw);
-  if (lo >= hi) return;
-  const uint32_t poly = pc->poly;
-  const LaneLut L = make_lut(lane);
-  auto rl64 = [](uint64_t v, uint32_t t) -> uint64_t {
-    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32);
-  };
-  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
-    const uint32_t cnt = min(64u, hi - g0);
-    uint64_t m_ptr = 0, m_len = 0;
-    uint32_t m_xs = 0, m_out = 0, m_exp = 0;
-    if (lane < cnt) {
-      const DevChunk &ch = chunks[g0 + lane];
-      m_ptr = ch.ptr;
-      m_len = ch.len;
-      m_xs = ch.xstart;
-      m_out = ch.out_idx;
-      if (expected) m_exp = expected[m_out];  // with the descriptors: no load on the per-chunk path
-    }
-    uint64_t S = rl64(m_ptr, 0), E = S + rl64(m_len, 0);
-    uint4 cur[R];
-    small_load<R>(S, E, lane, cur);
-    // Chunks in groups of kFoldGroup: each chunk's rows are folded into its stream set as
-    // they arrive (the next chunk's loads in flight), then the group's wave folds run
-    // interleaved.
-    constexpr int kFoldGroup = R <= 4 ? 4 : 2;  // R = 8 with 4 groups spills
-    for (uint32_t t0 = 0; t0 < cnt; t0 += kFoldGroup) {
-      Streams st[kFoldGroup];
-      uint64_t gS[kFoldGroup], gE[kFoldGroup];
-#pragma unroll
-      for (int j = 0; j < kFoldGroup; ++j) {
-        st[j] = Streams{0, 0, 0, 0};
-        gS[j] = S;
-        gE[j] = E;
-        const uint32_t t = t0 + j;
-        if (t < cnt) {
-          uint4 nxt[R];
-          uint64_t nS = S, nE = E;
-          if (t + 1 < cnt) {
-            nS = rl64(m_ptr, t + 1);
-            nE = nS + rl64(m_len, t + 1);
-          }
-          small_load<R>(nS, nE, lane, nxt);  // unconditional (the last one re-reads the current chunk)
-          const uint32_t K = small_rows(S, E);
-          const uint64_t base = (S & ~uint64_t(kRowBytes - 1)) + 16u * lane;
-#if H3C_SMALL_EXP & 1  // timing experiment: no table lookups
-#pragma unroll
-          for (int u = 0; u < R; ++u) st[j].s0 ^= cur[u].x ^ cur[u].y ^ cur[u].z ^ cur[u].w;
-#else
-#pragma unroll
-          for (int u = 0; u < R; ++u)
-            if ((uint32_t)u < K) {
-              uint4 x = cur[u];
-              // masks only where the chunk starts or ends inside a row (uniform branches)
-              if ((u == 0 && (S & (kRowBytes - 1))) || ((uint32_t)u + 1 == K && (E & (kRowBytes - 1))))
-                x = mask_row(x, base + (uint64_t)u * kRowBytes, S, E);
-              consume(st[j], x, lb, L);
-            }
-#endif
-          S = nS;
-          E = nE;
-#pragma unroll
-          for (int u = 0; u < R; ++u) cur[u] = nxt[u];
-        }
-      }
-      uint32_t acc[kFoldGroup];
-#if H3C_SMALL_EXP & 2  // timing experiment: no wave fold
-#pragma unroll
-      for (int j = 0; j < kFoldGroup; ++j) acc[j] = st[j].s0 ^ st[j].s1 ^ st[j].s2 ^ st[j].s3;
-#else
-      wave_fold_tab_n<kFoldGroup>(st, lane, red, acc);
-#endif
-#pragma unroll
-      for (int j = 0; j < kFoldGroup; ++j) {
-        const uint32_t t = t0 + j;
-        if (t >= cnt) break;
-        uint32_t a = acc[j];
-        const uint32_t pad = (uint32_t)(((gE[j] + kRowBytes - 1) & ~uint64_t(kRowBytes - 1)) - gE[j]);
-        if (pad >> 4) a = dgf_mul(a, pc->fix[4 * (pad >> 4)], poly);
-        if (pad & 15) a = dgf_mul(a, pc->fixz[pad & 15], poly);
-        if (lane == 0) {
-          const uint32_t raw = a ^ (uint32_t)__builtin_amdgcn_readlane(m_xs, t);
-          const uint32_t o = (uint32_t)__builtin_amdgcn_readlane(m_out, t);
-          out_raw[o] = raw;
-          if (expected) {
-            const bool good = raw == (uint32_t)__builtin_amdgcn_readlane(m_exp, t);
-            ok[o] = good ? 1 : 0;
-            if (!good && mismatch) atomicAdd(mismatch, 1u);
-          }
-        }
-      }
-    }
-  }
-}
-template <int R>
-__global__ __launch_bounds__(kThreads) void seg_small_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
-                                                             const PolyConsts *__restrict__ pc,
-                                                             const uint32_t *__restrict__ expected,
-                                                             uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
-                                                             uint32_t *__restrict__ mismatch,
-                                                             unsigned long long *ts) {  // ts: h3c_rt::prof_stamp's slot, or nullptr
-  stamp_begin(ts);
-  seg_small_kernel_body<R>(chunks, nchunks, pc, expected, out_raw, ok, mismatch);
-  stamp_end(ts);
-}
 
 // Kernel A'': the same batches with several chunks per wave.  A group of G lanes owns one
 // chunk and walks it in rows of 16*G bytes (tables with stride x^(8*16*G)); the 64/G
 // groups' Horner passes and their log2(G)-level shuffle trees run in the same
 // instructions, so a chunk pays G/64 of a wave fold instead of a whole one (the fold was
-// about a third of seg_small_kernel's instructions per chunk).  G = 4 for chunks up to
+// about a third of a one-chunk-per-wave kernel's instructions per chunk; that form,
+// seg_small_kernel, is gone).  G = 4 for chunks up to
 // ~5 KiB, 16 above.
-#ifndef H3C_SMALL_QUAD
-#define H3C_SMALL_QUAD 1
-#endif
 #ifndef H3C_SMALL_LANES_LO
 #define H3C_SMALL_LANES_LO 4  // lanes per chunk for chunks of at most 6 rows of 1 KiB (4 or 8)
 #endif
@@ -322,15 +174,8 @@ constexpr int kUniCopies = H3C_UNI_COPIES;
 constexpr int kUniThreads = kUniCopies == 16 ? 768 : kThreads;
 constexpr int kUniWaves = kUniThreads / 64;
 constexpr int kUniLdsWords = kUniCopies == 16 ? kLdsWords16 : kLdsWords;
-#ifndef H3C_UNI_DYNAMIC
-#define H3C_UNI_DYNAMIC 1  // seg_uni_kernel: waves take steps from a per-workgroup counter (0: static split)
-#endif
 #ifndef H3C_UNI_LANES_HI
 #define H3C_UNI_LANES_HI 16
-#endif
-#ifndef H3C_UNI_PAIR
-#define H3C_UNI_PAIR 0  // 1: uniform chunks of <= 6 rows, 128-byte multiples take 8 lanes x 2 chunks instead of
-                        // 4 lanes x 1 -- measured 10 % slower at 4 KiB (profiles/r03_small_pair_ab.txt)
 #endif
 
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
@@ -547,7 +392,6 @@ __device__ __forceinline__ void seg_uni_kernel_body(const DevChunk *__restrict__
     }
   }
   const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
-#if H3C_UNI_DYNAMIC
   // The workgroup owns a contiguous range; its waves take steps of kStep chunks from an LDS
   // counter, so a wave slowed by its neighbours does not leave the others idle at the end
   // (a static split per wave kept waves alive 81 % of the kernel at 8 lanes per chunk).
@@ -561,13 +405,6 @@ __device__ __forceinline__ void seg_uni_kernel_body(const DevChunk *__restrict__
     return (uint32_t)__builtin_amdgcn_readfirstlane(q);
   };
   const uint32_t lo = grab();
-#else
-  __syncthreads();
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t gw = (uint64_t)blockIdx.x * kUniWaves + wave;
-  const uint64_t nw = (uint64_t)gridDim.x * kUniWaves;
-  const uint32_t lo = (uint32_t)(gw * nchunks / nw), hi = (uint32_t)((gw + 1) * nchunks / nw);
-#endif
   if (lo >= hi) return;
   const uint32_t *red = lds + kUniLdsWords;
   const char *lb = reinterpret_cast<const char *>(lds);
@@ -601,13 +438,8 @@ __device__ __forceinline__ void seg_uni_kernel_body(const DevChunk *__restrict__
 #pragma unroll
     for (int b = 0; b < kUniBatch; ++b)
       cur[j][b] = valid[j] && (uint32_t)b < K ? load_row_w<kQ * C>(la[j] + (uint64_t)b * kQ) : make_uint4(0, 0, 0, 0);
-#if H3C_UNI_DYNAMIC
   for (uint32_t q0 = lo; q0 < hi;) {
     const uint32_t qn = grab();  // the next step, taken now so its rows load during this one's last batch
-#else
-  for (uint32_t q0 = lo; q0 < hi; q0 += kStep) {
-    const uint32_t qn = q0 + kStep;
-#endif
     uint64_t la1[C];
     uint32_t o1[C], want1[C];
     bool valid1[C];
@@ -686,9 +518,7 @@ __device__ __forceinline__ void seg_uni_kernel_body(const DevChunk *__restrict__
       want[j] = want1[j];
       valid[j] = valid1[j];
     }
-#if H3C_UNI_DYNAMIC
     q0 = qn;
-#endif
   }
 }
 template <int G, int C = 1>
@@ -1267,7 +1097,7 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
     const uint32_t blocks = std::min<uint32_t>(ctx.num_cu, (nchunks + kWavesPerBlock - 1) / kWavesPerBlock);
     ProfToken tok;
     if (prof_kind >= 0) HIP_TRY(prof_stamp(dev, tok));
-    if (H3C_SMALL_QUAD && uni && uni->lanes && !(dbg & 4u)) {  // test hook: H3C_DEBUG_FLAGS bit2 disables it
+    if (uni && uni->lanes && !(dbg & 4u)) {  // test hook: H3C_DEBUG_FLAGS bit2 disables it
       const DevChunk *dc = uni->contiguous ? nullptr : d_chunks;
       const uint32_t ublocks = std::min<uint32_t>(ctx.num_cu * (kUniCopies == 16 ? 2 : 1),
                                                   (nchunks + kUniWaves - 1) / kUniWaves);
@@ -1280,36 +1110,27 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
       else if (uni->lanes == 4)
         hipLaunchKernelGGL(seg_uni_kernel<4>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
                            nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch, tok.ts);
-      else if (uni->lanes == 8 && uni->pair)
-        hipLaunchKernelGGL((seg_uni_kernel<8, 2>), dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
-                           nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch, tok.ts);
       else if (uni->lanes == 8)
         hipLaunchKernelGGL(seg_uni_kernel<8>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
                            nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch, tok.ts);
       else
         hipLaunchKernelGGL(seg_uni_kernel<16>, dim3(ublocks), dim3(kUniThreads), 0, st, dc, uni->base, uni->stride,
                            nchunks, uni->rows, uni->xs, pc, expected, out_raw, ok, mismatch, tok.ts);
-    } else if (H3C_SMALL_QUAD)
+    } else if (small_rows <= 6) {
       // up to ~5 KiB chunks 4 lanes per chunk (4 KiB: +8 % over 8 lanes, +13 % over 16);
       // 16 lanes above (4 lanes lose 10 % at 8 and 16 KiB): profiles/r01d_small_lanes_ab.txt
-      if (small_rows <= 6)
-        hipLaunchKernelGGL((seg_quad_kernel<H3C_SMALL_LANES_LO, H3C_SMALL_PIECES_LO>), dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks,
-                           pc, expected, out_raw, ok, mismatch, tok.ts);
-      else
-        hipLaunchKernelGGL((seg_quad_kernel<H3C_SMALL_LANES_HI, H3C_SMALL_PIECES_HI>), dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
-                           out_raw, ok, mismatch, tok.ts);
-    else if (small_rows <= 4)
-      hipLaunchKernelGGL(seg_small_kernel<4>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
+      hipLaunchKernelGGL((seg_quad_kernel<H3C_SMALL_LANES_LO, H3C_SMALL_PIECES_LO>), dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks,
+                         pc, expected, out_raw, ok, mismatch, tok.ts);
+    } else {
+      hipLaunchKernelGGL((seg_quad_kernel<H3C_SMALL_LANES_HI, H3C_SMALL_PIECES_HI>), dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
                          out_raw, ok, mismatch, tok.ts);
-    else
-      hipLaunchKernelGGL(seg_small_kernel<8>, dim3(blocks), dim3(kThreads), 0, st, d_chunks, nchunks, pc, expected,
-                         out_raw, ok, mismatch, tok.ts);
+    }
     HIP_TRY(hipGetLastError());
     if (prof_kind >= 0) HIP_TRY(prof_end(st, tok, prof_kind, payload_bytes));
     return H3C_OK;
   }
   // every chunk exactly one segment: the segment kernel finishes the chunks (no finalize launch)
-  const bool fin = H3C_SEG_FUSE_FIN && total_segs && total_segs == nchunks && max_chunk_segs == 1;
+  const bool fin = total_segs && total_segs == nchunks && max_chunk_segs == 1;
   if (total_segs) {
     const uint32_t blocks = std::min<uint32_t>(ctx.num_cu, (total_segs + kWavesPerBlock - 1) / kWavesPerBlock);
     ProfToken tok;
@@ -1361,7 +1182,7 @@ KernelSig uio_piece_kernel_sig() { return kernel_sig(op_piece_crc_kernel<UioPiec
 // the batch is one segment: seg_quad_kernel beats the segment kernel + finalize up to
 // 16 KiB chunks and loses from 32 KiB (profiles/r01d_small_path_threshold.txt).
 #ifndef H3C_SMALL_PATH_ROWS
-#define H3C_SMALL_PATH_ROWS (H3C_SMALL_QUAD ? 16 : 8)
+#define H3C_SMALL_PATH_ROWS 16
 #endif
 constexpr uint32_t kSmallPathRows = H3C_SMALL_PATH_ROWS;
 
@@ -1389,13 +1210,6 @@ void uniform_for(const DevChunk *c, size_t n, uint32_t small_rows, UniformBatch 
   if (!n || !small_rows) return;
   uint32_t lanes = small_rows <= 6 ? H3C_UNI_LANES_LO : H3C_UNI_LANES_HI;
   if (lanes != 1 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16) return;
-  // short chunks whose rows are whole 128-byte lines: 8 lanes, two chunks per group
-  bool pair = false;
-  if (H3C_UNI_PAIR && lanes == 4 && c[0].len && c[0].len % 128 == 0) {
-    pair = true;
-    for (size_t i = 0; i < n && pair; ++i) pair = c[i].ptr % 128 == 0;
-    if (pair) lanes = 8;
-  }
   const uint64_t row = 16u * lanes, len = c[0].len;
   if (!len || len % row) return;
   const uint64_t stride = n > 1 ? c[1].ptr - c[0].ptr : len;
@@ -1405,7 +1219,6 @@ void uniform_for(const DevChunk *c, size_t n, uint32_t small_rows, UniformBatch 
     contiguous = contiguous && c[i].out_idx == i && c[i].ptr == c[0].ptr + i * stride;
   }
   u.lanes = lanes;
-  u.pair = pair;
   u.rows = (uint32_t)(len / row);
   u.xs = c[0].xstart;
   u.contiguous = contiguous;

@@ -61,32 +61,26 @@ namespace {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
-#ifndef H3C_NT_STORES
-#define H3C_NT_STORES 0  // 1: nontemporal write-back stores (r02: +2 %; round 5: plain stores 265 -> 234 us, load_row_rmw)
+// Write-back store policy per kernel.  upd_fused_kernel: plain stores (round 5: 265 -> 234 us with
+// load_row_rmw, profiles/r05s_rmw_policy_ab).  The separate-kernel delta path (upd_delta_kernel, the tiles and
+// sort paths) keeps nontemporal stores, the policy it was measured and tested with (r02: +2 %); the round-5
+// A/B covered the fused kernels only.
+#ifndef H3C_FUSED_NT_STORES
+#define H3C_FUSED_NT_STORES 0
 #endif
+#ifndef H3C_DELTA_NT_STORES
+#define H3C_DELTA_NT_STORES 1
+#endif
+template <bool NT>
 __device__ __forceinline__ void store_row(uint64_t a, uint4 v) {
-#if H3C_NT_STORES
-  v4u w = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(w, (v4u __attribute__((address_space(1))) *)a);
-#else
-  *reinterpret_cast<uint4 *>(a) = v;
-#endif
+  if (NT) {
+    v4u w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (v4u __attribute__((address_space(1))) *)a);
+  } else {
+    *reinterpret_cast<uint4 *>(a) = v;
+  }
 }
 
-#ifndef H3C_UPD_SKEW
-#define H3C_UPD_SKEW 0
-#endif
-#ifndef H3C_UPD_EARLY_FILL
-#define H3C_UPD_EARLY_FILL 1  // the fused kernel's CRC tables fill before the range is known (0: after the first group starts)
-#endif
-#ifndef H3C_UPD_WG_BAL
-#define H3C_UPD_WG_BAL 1  // fused path: the fewest workgroups that keep the most writes per wave
-#endif
-#ifndef H3C_UPD_EXPERIMENT
-#define H3C_UPD_EXPERIMENT 0  // timing-only builds: bit0 skips write-back, bit1 skips the CRC math,
-                              // fused kernel: bit2 skips the hash walk, bit3 stops after the writes,
-                              // bit5 skips the look-back, bit6 the last workgroup's wait, bit7 the ticket
-#endif
 
 // rocPRIM picks merge sort below this many items.  Forcing its onesweep radix passes
 // (limit 0) measured slower at 100k items: 4 x 23 us lookback-bound iterations.
@@ -427,21 +421,16 @@ __device__ __forceinline__ void upd_delta_kernel_body(
       uint32_t d = 0;
       if (valid) {
         Streams st{0, 0, 0, 0};
-#if H3C_UPD_EXPERIMENT & 2  // timing experiment: no CRC compute (loads kept alive)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) st.s0 ^= vn[u].x ^ vo[u].x ^ vn[u].y ^ vo[u].y ^ vn[u].z ^ vo[u].z ^ vn[u].w ^ vo[u].w;
-#else
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           consume(st, make_uint4(vn[u].x ^ vo[u].x, vn[u].y ^ vo[u].y, vn[u].z ^ vo[u].z, vn[u].w ^ vo[u].w), lb, L);
-#endif
-        const uint64_t dst = (H3C_UPD_EXPERIMENT & 1) ? 0 : rl64(m_dst, t);  // experiment bit0: no write-back
+        const uint64_t dst = rl64(m_dst, t);
         if (dst) {  // first writer of the slot: leave the slot's final bytes in the chunk
           const uint64_t fin = rl64(m_fin, t);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const uint4 v = fin == pnew ? vn[u] : load_row_rmw(fin + u * kRowBytes + lo16);
-            store_row(dst + u * kRowBytes + lo16, v);
+            store_row<H3C_DELTA_NT_STORES>(dst + u * kRowBytes + lo16, v);
           }
         }
         d = wave_fold_tab(st, lane, red);  // lane 0; the block's x^(8*bytes after it) is applied in gather
@@ -538,26 +527,16 @@ __device__ __forceinline__ void upd_fused_kernel_body(
       if (c == cls) wmine = w;
     }
     const unsigned long long old =
-        (H3C_UPD_EXPERIMENT & 128) ? ((unsigned long long)blockIdx.x << 40) | (blockIdx.x * wmine)
-                                   : atomicAdd(reinterpret_cast<unsigned long long *>(ctl + kCtlAcc), (1ull << 40) | wmine);
+        atomicAdd(reinterpret_cast<unsigned long long *>(ctl + kCtlAcc), (1ull << 40) | wmine);
     const uint64_t cum = old & ((1ull << 40) - 1);
     s_ticket = (uint32_t)(old >> 40);
     s_wt = wt;
-#if H3C_UPD_SKEW  // (A/B) the cut points warped by p(f) = f - b f (1 - f), b = H3C_UPD_SKEW / 1000
-    auto warp = [&](uint64_t c) -> uint32_t {
-      const double f = (double)c / (double)wt, b = H3C_UPD_SKEW / 1000.0;
-      return (uint32_t)((f - b * f * (1.0 - f)) * (double)n);
-    };
-    s_wlo = warp(cum);
-    s_whi = s_ticket + 1 == gridDim.x ? n : warp(cum + wmine);
-#else
     s_wlo = (uint32_t)(cum * n / wt);
     s_whi = s_ticket + 1 == gridDim.x ? n : (uint32_t)((cum + wmine) * n / wt);
-#endif
     s_E = __hip_atomic_load(&ctl[kCtlEpoch], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFFu;
   }
   // the CRC tables fill while thread 0 takes the ticket (waves 1-15; they do not depend on the range)
-  if (H3C_UPD_EARLY_FILL && threadIdx.x >= 64)
+  if (threadIdx.x >= 64)
     fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x - 64, kFThreads - 64);
   __syncthreads();
   const uint32_t L = s_ticket, nwg = gridDim.x, E = s_E;
@@ -615,7 +594,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
         m_old = p == kNone ? slot : pay + (uint64_t)p * G4;
         m_dst = p == kNone ? slot : 0;
         m_fin = p == kNone ? m_new : 0;
-        if (p == kNone && !(H3C_UPD_EXPERIMENT & 4)) key = c * bpc + bb;
+        if (p == kNone) key = c * bpc + bb;
       }
     }
     const bool valid = __builtin_amdgcn_readlane(m_c, 0) != kNone;
@@ -656,7 +635,6 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     for (int i = 1; i < kFD; ++i) load_op(bn[i], bo[i], bv[i], bp[i], (uint32_t)i, cnt);
   };
   if (lo < hi) start_group(lo);  // the first group's links and rows load while the tables fill
-  if (!H3C_UPD_EARLY_FILL) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, threadIdx.x, kFThreads);
   __syncthreads();
   if (threadIdx.x == 0) s_t0 = wall_clock64();
   const uint32_t *red = lds + kLdsWords;
@@ -673,25 +651,19 @@ __device__ __forceinline__ void upd_fused_kernel_body(
       load_op(bn[kFD], bo[kFD], bv[kFD], bp[kFD], t + kFD, cnt);
       if (bv[0]) {
         Streams st{0, 0, 0, 0};
-#if H3C_UPD_EXPERIMENT & 2  // timing experiment: no CRC compute (loads kept alive)
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          st.s0 ^= bn[0][u].x ^ bo[0][u].x ^ bn[0][u].y ^ bo[0][u].y ^ bn[0][u].z ^ bo[0][u].z ^ bn[0][u].w ^ bo[0][u].w;
-#else
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           consume(st,
                   make_uint4(bn[0][u].x ^ bo[0][u].x, bn[0][u].y ^ bo[0][u].y, bn[0][u].z ^ bo[0][u].z,
                              bn[0][u].w ^ bo[0][u].w),
                   lb, Lt);
-#endif
         const uint64_t dst = rl64(m_dst, t);
         if (dst) {  // first writer of the slot: leave the slot's final bytes in the chunk
           const uint64_t fin = rl64(m_fin, t);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const uint4 v = fin == bp[0] ? bn[0][u] : load_row_rmw(fin + u * kRowBytes + lo16);
-            store_row(dst + u * kRowBytes + lo16, v);
+            store_row<H3C_FUSED_NT_STORES>(dst + u * kRowBytes + lo16, v);
           }
         }
         const uint32_t d = __builtin_amdgcn_readlane(wave_fold_tab(st, lane, red), 0);
@@ -714,7 +686,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     const uint32_t src = m_c & 63;
     const uint32_t r0 = __shfl(acc0, src, 64), r1 = __shfl(acc1, src, 64);
     my_ip = m_c < 64 ? r0 : r1;
-    for (uint32_t t = 0; t < ((H3C_UPD_EXPERIMENT & 16) ? 0u : cnt); ++t) {
+    for (uint32_t t = 0; t < cnt; ++t) {
       const uint32_t ct = __builtin_amdgcn_readlane(m_c, t), vt = __builtin_amdgcn_readlane(v, t);
       if (lane >= t && m_c == ct) my_ip ^= vt;
       if (ct == lane) acc0 ^= vt;
@@ -726,7 +698,6 @@ __device__ __forceinline__ void upd_fused_kernel_body(
   // the chunks' base checksums, one per lane (chunks lane, lane + 64)
   const uint32_t rb0 = lane < nchunks ? raw_base[lane] : 0u, rb1 = lane + 64 < nchunks ? raw_base[64 + lane] : 0u;
 
-  if (H3C_UPD_EXPERIMENT & 8) return;  // timing experiment: no aggregation / look-back / out_raw
   // ---- chunk aggregates: waves of the workgroup (LDS), then workgroups (look-back) ----
   __syncthreads();  // the CRC tables are done with: their LDS holds the aggregates now
   if (stat && threadIdx.x == 0 && L < kFusedMaxWG) {  // this workgroup's throughput, for the next batch's weights
@@ -748,7 +719,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
     const bool two = nchunks > 64;
     uint64_t *row = gran + (uint64_t)L * kFusedCols;
     uint32_t x0 = 0, x1 = 0;
-    if (L > 0 && !(H3C_UPD_EXPERIMENT & 32)) {  // (experiment bit5: no look-back)
+    if (L > 0) {
       if (lane < nchunks) gran_store(row + lane, E, kGranAgg, a0);
       if (two && lane + 64 < nchunks) gran_store(row + 64 + lane, E, kGranAgg, a1);
       int j0 = lane < nchunks ? (int)L - 1 : -1, j1 = two && lane + 64 < nchunks ? (int)L - 1 : -1;
@@ -813,7 +784,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
         // wait (bounded) for every other workgroup's done count; a count that never comes voids the batch
         // (the counts and flags are agent-scope atomics at the coherence point: no L2 write-back needed)
         bool late = false;
-        for (uint32_t spins = 0; !(H3C_UPD_EXPERIMENT & 64) &&  // (experiment bit6: no wait for the counts)
+        for (uint32_t spins = 0;
              __hip_atomic_load(&ctl[kCtlDone], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nwg - 1;) {
           __builtin_amdgcn_s_sleep(2);
           if (++spins > kSpinLimit) {
@@ -841,8 +812,7 @@ __device__ __forceinline__ void upd_fused_kernel_body(
         }
         // the control words back to their batch-start values for the next batch on this scratch (the
         // subtractions are exact even when a late workgroup counts itself done after this), the epoch on
-        if (!(H3C_UPD_EXPERIMENT & 128))
-          atomicAdd(reinterpret_cast<unsigned long long *>(ctl + kCtlAcc), 0ull - (((unsigned long long)nwg << 40) + s_wt));
+        atomicAdd(reinterpret_cast<unsigned long long *>(ctl + kCtlAcc), 0ull - (((unsigned long long)nwg << 40) + s_wt));
         atomicSub(&ctl[kCtlDone], nwg - 1);
         atomicSub(&ctl[kCtlErr], inv);
         atomicExch(&ctl[kCtlTimeout], 0u);
@@ -1378,13 +1348,11 @@ int update_blocks_impl(uint8_t type, const uint64_t *chunk_base_dev, uint32_t nc
   const uint32_t reuse_case = (uint64_t)block_bytes == chunk_len ? 1u : 0u;  // a block write replaces the chunk
   const int path = pick_path(n_blocks, nchunks, block_bytes);
   uint32_t fused_wg = std::min<uint32_t>(std::min(num_cu, kFusedMaxWG), (n_blocks + kFW - 1) / kFW);
-#if H3C_UPD_WG_BAL  // the fewest workgroups with the same most writes per wave (100k writes: 250, 25 per wave,
                     // instead of 256 with 24-25: -1 us, profiles/r04_update_tail_ab.txt)
   {
     const uint64_t per = ((uint64_t)n_blocks + (uint64_t)fused_wg * kFW - 1) / ((uint64_t)fused_wg * kFW);
     fused_wg = (uint32_t)std::max<uint64_t>(1, ((uint64_t)n_blocks + per * kFW - 1) / (per * kFW));
   }
-#endif
   // the fused path's hash heads, control words, touched marks and granules: the stream's UpdScratch, or
   // one memset of the workspace's (and the granule rows in use)
   std::unique_lock<std::mutex> us_lock;

@@ -192,9 +192,6 @@ constexpr uint32_t kFragCrc = 1u, kFragWrite = 2u, kFragHead = 4u, kFragA6 = 8u;
 // bit-serial GF(2) multiply issued by the whole wave for lane 0.  Other fragments XOR their
 // shifted contributions into eacc[2p] (eacc[2p+1] stays 0: nothing left to multiply).
 constexpr uint32_t kFragSolo = 16u;
-#ifndef H3C_UIO_SOLO
-#define H3C_UIO_SOLO 1  // 0: every fragment's contribution shifted in the block kernel (A/B)
-#endif
 
 // counters: a workgroup-aggregated add -- wave sums into LDS, one global atomic per counter
 // and workgroup (call from workgroup-uniform control flow; `sh` holds kCtrN slots)
@@ -823,7 +820,7 @@ __global__ void uio_frag_kernel(const OpPos *__restrict__ pos, const uint32_t *_
   uint64_t key;
   uint32_t praw = 0;
   const FragDesc d = make_frag(r, p, k - fbase[p], c, chunks[c], ios[r.op], pc, std_domain,
-                               H3C_UIO_SOLO && fbase[p + 1] - fbase[p] == 1,
+                               fbase[p + 1] - fbase[p] == 1,
                                key, praw);
   frags[k] = d;
   fkey[k] = key;
@@ -994,12 +991,6 @@ __device__ void fast_prep_tile(const FastArgs &fa, uint32_t i, uint32_t n, const
 //      walk their bucket's list for the largest earlier fragment of their key.
 // Waits are bounded: a tile that gives up sets bit 1 of misc[kMiscA6] -- the pass is void, the
 // block kernel writes nothing and the host redoes the batch on the scan-based stage.
-#ifndef H3C_PB_TRACE
-#define H3C_PB_TRACE 0  // 1: phase B tiles 0, 1, the middle one and the last print their step times
-#endif
-#ifndef H3C_FRONT_TRACE
-#define H3C_FRONT_TRACE 0  // 1: tiles 0, 1, the middle one and the last print their step times (diagnostics)
-#endif
 constexpr uint32_t kFrontTile = 1024;
 constexpr uint32_t kFrontSpin = 1u << 21;
 constexpr uint32_t kPending = 0xFFFFFFFEu;  // gnext[] entry pushed, its next pointer not yet stored
@@ -1126,13 +1117,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
   if (p0 >= n) return;  // (whole workgroup)
   const uint32_t cnt = min(T, n - p0), tlast = cnt - 1;
   const uint32_t poly = pc->poly;
-#if H3C_FRONT_TRACE
-  uint64_t tr[8];
-  tr[0] = wall_clock64();
-#define FRONT_MARK(i) (tr[i] = wall_clock64())
-#else
 #define FRONT_MARK(i) ((void)0)
-#endif
   const bool valid = t < cnt;
   const uint32_t p = p0 + t;
   const uint32_t c = valid ? skey[p] : 0xFFFFFFFFu;
@@ -1358,7 +1343,7 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
       uint64_t k64;
       uint32_t praw = 0;
       const FragDesc d = make_frag(rq, p0 + a, kk - s_fex[a], cq, chunks[cq], ios[rq.op], pc, std_domain,
-                                   H3C_UIO_SOLO && s_fex[a + 1] - s_fex[a] == 1, k64, praw);
+                                   s_fex[a + 1] - s_fex[a] == 1, k64, praw);
       frags[g] = d;  // plain stores: only this thread writes the record (its head flag below)
       st_agent(reinterpret_cast<unsigned long long *>(&fkey[g]), (unsigned long long)k64);  // read by later tiles
       if (d.flags & kFragA6) payraw[rq.op] = praw;
@@ -1443,15 +1428,6 @@ __global__ __launch_bounds__(kFrontTile) void uio_front_kernel(
       frags[g].flags |= kFragHead;  // this thread wrote the record (step 4)
     }
   }
-#if H3C_FRONT_TRACE
-  __syncthreads();
-  FRONT_MARK(5);
-  const uint32_t ntl = (n + T - 1) / T;
-  if (t == 0 && (k < 2 || k == ntl / 2 || k + 1 == ntl))
-    printf("front tile %u start %llu sz %llu nf %llu links %llu wait %llu end %llu (ticks)\n", k,
-           (unsigned long long)tr[0], (unsigned long long)(tr[1] - tr[0]), (unsigned long long)(tr[2] - tr[0]),
-           (unsigned long long)(tr[3] - tr[0]), (unsigned long long)(tr[4] - tr[0]), (unsigned long long)(tr[5] - tr[0]));
-#endif
 }
 
 // ---- the block kernel ----
@@ -1527,30 +1503,6 @@ __device__ __forceinline__ uint4 load_new(uint64_t src, uint32_t row, uint32_t r
 #define H3C_UIO_BLOCK_WAVES 16
 #endif
 constexpr uint32_t kBlkWaves = H3C_UIO_BLOCK_WAVES, kBlkThreads = 64 * kBlkWaves;
-#ifndef H3C_UIO_SERIAL
-#define H3C_UIO_SERIAL 1  // the front path on one stream (0: the piece pass, A6 and t0 on a second stream)
-#endif
-#ifndef H3C_UIO_LATE_JOIN
-#define H3C_UIO_LATE_JOIN 0  // timing experiment only: the block kernel does not wait for the second stream
-#endif                       // (unsafe: a failed non-fold A6 check would not stop its writes)
-#ifndef H3C_UIO_EARLY
-#define H3C_UIO_EARLY 1  // block kernel: the first fragment's rows load before the LDS table fill
-#endif
-#ifndef H3C_UIO_GRAB
-#define H3C_UIO_GRAB 0  // block kernel: fragments a wave takes per grab from an LDS counter (0: one fixed range per wave; 2 spills, 353 vs 282 us: r03i)
-#endif
-#ifndef H3C_UIO_IMG_NT
-#define H3C_UIO_IMG_NT 0  // 1: the old block rows by nontemporal loads (A/B)
-#endif
-#ifndef H3C_BLOCK_TRACE
-#define H3C_BLOCK_TRACE 0  // 1: every block-kernel wave prints its start / end (diagnostics)
-#endif
-#ifndef H3C_UIO_SFIELDS
-#define H3C_UIO_SFIELDS 1  // block kernel: per-fragment fields by scalar loads (0: all in the lanes)
-#endif
-#ifndef H3C_UIO_FOLD_ILP
-#define H3C_UIO_FOLD_ILP 0  // 1: the fold check's CRC and the delta's interleaved (spills: 362 vs 288 us, r03c_updio_ab)
-#endif
 // Write-back store policy per kernel (1: nontemporal, 0: plain; profiles/r05s_rmw_policy_ab.txt):
 #ifndef H3C_UIO_NT_STORES
 #define H3C_UIO_NT_STORES 1  // uio_block_kernel (the general pipeline)
@@ -1588,11 +1540,7 @@ __device__ __forceinline__ void load_task_rows(uint64_t blk, uint32_t k0, uint32
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const uint32_t rel = 1024u * r + 16u * lane;
-#if H3C_UIO_IMG_NT
-    b.img[r] = (rel + 16 > k0 && rel < k1) ? load_row_rmw(blk + rel) : make_uint4(0, 0, 0, 0);
-#else
     b.img[r] = (rel + 16 > k0 && rel < k1) ? load_plain(blk + rel) : make_uint4(0, 0, 0, 0);
-#endif
     b.nw[r] = load_new(src, r, rel, w0, w1);
   }
 }
@@ -1612,7 +1560,7 @@ struct GenSink {
   uint32_t poly;
   __device__ void fail(uint32_t op) const { a6[op] = 1u; }
   __device__ void crc(uint32_t p, uint32_t v, uint32_t mult, uint32_t flags) const {
-    if (H3C_UIO_SOLO && (flags & kFragSolo)) {
+    if (flags & kFragSolo) {
       *reinterpret_cast<uint2 *>(eacc + 2 * p) = make_uint2(v, mult);
     } else {
       const uint32_t cv = dgf_mul_fast(v, mult, poly);
@@ -1632,28 +1580,6 @@ __device__ __forceinline__ uint32_t apply_fragment(uint4 (&img)[4], const uint4 
                                                    const char *lb, const LaneLut &L, const uint32_t *red,
                                                    const FoldIo &fx, const Sink &sink) {
   const uint32_t w0 = w & 0xFFFFu, w1 = w >> 16, q0 = q & 0xFFFFu, q1 = q >> 16, z0 = z & 0xFFFFu, z1 = z >> 16;
-#if H3C_UIO_FOLD_ILP
-  if ((flags & (kFragA6 | kFragCrc)) == (kFragA6 | kFragCrc)) {
-    // the check and the delta side by side: two independent stream sets per row and one
-    // two-way fold, so the LDS round trips of the two folds' Horner / tree chains overlap
-    Streams s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t rel = 1024u * r + 16u * lane;
-      const uint4 old = row_full(r, q0, q1) ? img[r] : and4(img[r], row_mask(r, rel, q0, q1));
-      consume(s2[0], nw[r], lb, L);
-      consume(s2[1], xor4(nw[r], old), lb, L);
-    }
-    uint32_t fv[2];
-    wave_fold_tab_n<2>(s2, lane, red, fv);
-    if (__builtin_amdgcn_readfirstlane(fv[0]) != fx.expect) {
-      if (lane == 0) sink.fail(fx.op);
-      return 0u;
-    }
-    if (lane == 0) sink.crc(p, fv[1], mult, flags);
-    flags &= ~(kFragA6 | kFragCrc);
-  }
-#endif
   if (flags & kFragA6) {
     Streams sn{0, 0, 0, 0};  // the new bytes alone (one stream set at a time: the registers are full)
 #pragma unroll
@@ -1712,7 +1638,7 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
     if (threadIdx.x == 0) lds[kLdsWords + kRedWords] = 0;  // the waves' range counter (H3C_UIO_GRAB)
     __syncthreads();
   };
-  constexpr bool kEarlyRows = H3C_UIO_EARLY && H3C_UIO_SFIELDS && !H3C_UIO_GRAB;  // first rows before the fill
+  constexpr bool kEarlyRows = true;  // first rows before the fill
   if (!kEarlyRows) fill_lds();
   const uint32_t F = misc[kMiscA6] ? 0u : frag_count(d_F, cap);  // a failed A6: this pass writes nothing
   const uint32_t *red = lds + kLdsWords;
@@ -1721,21 +1647,11 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kBlkWaves + wave;
   const uint64_t nw = (uint64_t)gridDim.x * kBlkWaves;
-#if H3C_UIO_SFIELDS && H3C_UIO_GRAB
-  (void)gw;
-  (void)nw;
-  // this workgroup's share; its waves take it in ranges from the LDS counter (lds[kLdsWords + kRedWords])
-  uint32_t *grab = lds + kLdsWords + kRedWords;
-  const uint32_t wg_lo = (uint32_t)((uint64_t)blockIdx.x * F / gridDim.x);
-  const uint32_t wg_hi = (uint32_t)((uint64_t)(blockIdx.x + 1) * F / gridDim.x);
-#else
   const uint32_t lo = (uint32_t)(gw * F / nw), hi = (uint32_t)((gw + 1) * F / nw);
   if (!kEarlyRows && lo >= hi) return;
-#endif
   const uint32_t poly = pc->poly;
   const GenSink sink{eacc, a6, poly};
   const LaneLut L = make_lut(lane);
-#if H3C_UIO_SFIELDS
   // Every field comes from uniform (scalar) loads: the wave walks its fragments in order, the
   // rows of fragment g + 1 in flight while g is processed and the addresses of g + 2 loaded
   // meanwhile.  No per-lane copies of the records: 128 VGPRs hold the rows with no spill (a
@@ -1781,56 +1697,6 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
   uint64_t c_blk, c_src, n_blk = 0, n_src = 0;
   uint32_t c_w, c_k, n_w = 0, n_k = 0;
   BlockRows cur, nxt;
-#if H3C_UIO_GRAB
-  // Dynamic ranges: the workgroup's share of the fragments is handed to its waves
-  // H3C_UIO_GRAB at a time from an LDS counter (an LDS atomic: ~100 cycles, counted in lgkmcnt,
-  // so it never waits behind the wave's row loads) instead of a fixed share per wave, so a wave
-  // that meets slow blocks does not set the kernel's end.  A range is asked for two fragments
-  // before it is needed.
-  constexpr uint32_t G = H3C_UIO_GRAB;
-  static_assert(G >= 2, "a range holds at least two fragments (the addresses run two ahead)");
-  const uint32_t whi = wg_hi;
-  auto ask = [&]() -> uint32_t {
-    uint32_t v = 0;
-    if (lane == 0) v = atomicAdd(grab, G);
-    return wg_lo + (uint32_t)__builtin_amdgcn_readfirstlane(v);
-  };
-  uint32_t xb = ask();  // this range: [xb, xb + G)
-  if (xb >= whi) return;
-  uint32_t nb = 0, j = 0;  // the next range's base (asked for when first needed); x = xb + j
-  bool nb_read = false;
-  auto at = [&](uint32_t k) -> uint32_t {  // the k-th fragment from xb in this wave's order (k < 2G)
-    if (k < G) return xb + k;
-    if (!nb_read) {
-      nb = ask();
-      nb_read = true;
-    }
-    return nb + (k - G);
-  };
-  addr_of(xb, c_blk, c_src, c_w, c_k);
-  load_task_rows(c_blk, c_k & 0xFFFFu, c_k >> 16, c_src, c_w & 0xFFFFu, c_w >> 16, lane, cur);
-  if (at(1) < whi) addr_of(at(1), n_blk, n_src, n_w, n_k);
-  for (;;) {
-    const uint32_t x = xb + j, s1 = at(j + 1);  // (indices past whi: none, the ranges come in order)
-    const uint64_t blk = c_blk;
-    const uint32_t kk = c_k;
-    if (s1 < whi) {
-      load_task_rows(n_blk, n_k & 0xFFFFu, n_k >> 16, n_src, n_w & 0xFFFFu, n_w >> 16, lane, nxt);
-      c_blk = n_blk;
-      c_k = n_k;
-      const uint32_t s2 = at(j + 2);
-      if (s2 < whi) addr_of(s2, n_blk, n_src, n_w, n_k);
-    }
-    process(x, blk, kk, cur);
-    if (s1 >= whi) break;
-    if (++j == G) {  // into the next range
-      xb = nb;
-      j = 0;
-      nb_read = false;
-    }
-    cur = nxt;
-  }
-#else
   // the first fragment's rows are in flight while the workgroup fills its LDS tables (a wave with
   // no fragment still takes part in the fill's barrier)
   if (lo < hi) {
@@ -1854,83 +1720,8 @@ __device__ __forceinline__ void uio_block_body(const FragDesc *__restrict__ frag
     process(g, blk, kk, cur);
     cur = nxt;
   }
-#endif
-#else
-  auto rl = [](uint32_t v, uint32_t t) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane(v, t); };
-  auto rl64 = [](uint64_t v, uint32_t t) -> uint64_t {
-    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, t) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), t) << 32);
-  };
-  for (uint32_t g0 = lo; g0 < hi; g0 += 64) {
-    const uint32_t cnt = min(64u, hi - g0);
-    // lane k: fragment g0 + k
-    uint64_t m_blk = 0, m_src = 0;
-    uint32_t m_p = 0, m_next = kNil, m_w = 0, m_q = 0, m_z = 0, m_k = 0, m_mult = 0, m_flags = 0;
-    if (lane < cnt) {
-      const FragDesc &d = frags[g0 + lane];
-      m_blk = d.blk;
-      m_src = d.src;
-      m_p = d.p;
-      m_next = fnext[g0 + lane];
-      m_w = (uint32_t)d.w0 | ((uint32_t)d.w1 << 16);
-      m_q = (uint32_t)d.q0 | ((uint32_t)d.q1 << 16);
-      m_z = (uint32_t)d.z0 | ((uint32_t)d.z1 << 16);
-      m_k = (uint32_t)d.k0 | ((uint32_t)d.k1 << 16);
-      m_mult = d.mult;
-      m_flags = d.flags;
-    }
-    BlockRows cur, nxt;
-    {
-      const uint32_t k = rl(m_k, 0), w = rl(m_w, 0);
-      load_task_rows(rl64(m_blk, 0), k & 0xFFFFu, k >> 16, rl64(m_src, 0), w & 0xFFFFu, w >> 16, lane, cur);
-    }
-    for (uint32_t t = 0; t < cnt; ++t) {
-      // the next fragment's rows in flight while this one is processed (a fragment that is
-      // not a chain head -- a later write to an already written block -- loads them in vain)
-      if (t + 1 < cnt) {
-        const uint32_t k = rl(m_k, t + 1), w = rl(m_w, t + 1);
-        load_task_rows(rl64(m_blk, t + 1), k & 0xFFFFu, k >> 16, rl64(m_src, t + 1), w & 0xFFFFu, w >> 16, lane, nxt);
-      }
-      const uint32_t flags = rl(m_flags, t);
-      if (flags & kFragHead) {
-        const uint64_t blk = rl64(m_blk, t);
-        const uint32_t kk = rl(m_k, t), k0 = kk & 0xFFFFu, k1 = kk >> 16;
-        // a fold fragment's op / checksum / length: scalar loads of the record the lanes just read
-        FoldIo fx{0, 0, 0, std_domain, pc, payraw, a6};
-        if (flags & kFragA6) {
-          const FragDesc *dh = frags + (g0 + t);
-          fx.op = dh->op;
-          fx.expect = dh->expect;
-          fx.len = dh->len;
-        }
-        uint32_t dirty = apply_fragment(cur.img, cur.nw, flags, rl(m_w, t), rl(m_q, t), rl(m_z, t), rl(m_mult, t),
-                                        rl(m_p, t), lane, lb, L, red, fx, sink);
-        for (uint32_t f = rl(m_next, t); f != kNil;) {  // later fragments of the same block
-          const FragDesc d = frags[f];
-          uint4 nw4[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) nw4[r] = load_new(d.src, r, 1024u * r + 16u * lane, d.w0, d.w1);
-          const FoldIo fd{d.op, d.expect, d.len, std_domain, pc, payraw, a6};
-          dirty |= apply_fragment(cur.img, nw4, d.flags, (uint32_t)d.w0 | ((uint32_t)d.w1 << 16),
-                                  (uint32_t)d.q0 | ((uint32_t)d.q1 << 16), (uint32_t)d.z0 | ((uint32_t)d.z1 << 16),
-                                  d.mult, d.p, lane, lb, L, red, fd, sink);
-          f = fnext[f];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (dirty & (1u << r)) store_masked(blk, 1024u * r + 16u * lane, cur.img[r], k0, k1);
-      }
-      cur = nxt;
-    }
-  }
-#endif
 }
 
-#if H3C_BLOCK_TRACE
-__device__ unsigned int g_btr[67] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                                     0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                                     0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x7FFFFFFFu};
-#endif
 // ts (nullable): [0] the earliest workgroup start, [1] the latest workgroup end (wall clock).
 __global__ __launch_bounds__(kBlkThreads) void uio_block_kernel(const FragDesc *__restrict__ frags, const uint32_t *__restrict__ fnext,
                                                              const uint32_t *__restrict__ d_F, uint32_t cap,
@@ -1947,29 +1738,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_block_kernel(const FragDesc *
     for (uint32_t i = threadIdx.x; i < pbz_words; i += blockDim.x) pbz[i] = 0;
     if (threadIdx.x == 0) misc_w[kMiscPBVoid] = misc_w[kMiscPBDone] = 0;
   }
-#if H3C_BLOCK_TRACE
-  const uint64_t tb0 = wall_clock64();
-  if ((threadIdx.x & 63) == 0) atomicMin(&g_btr[66], (unsigned int)(tb0 & 0x7FFFFFFFu));
-#endif
   uio_block_body(frags, fnext, d_F, cap, pc, eacc, misc, lds, std_domain, payraw, a6, misc_w);
-#if H3C_BLOCK_TRACE  // diagnostics: a histogram of the waves' end times (5 us bins from the earliest start)
-  if ((threadIdx.x & 63) == 0) {
-    const uint64_t te = wall_clock64();
-    __builtin_amdgcn_s_sleep(100);  // every workgroup has stamped its start by now (one per CU)
-    const uint32_t rel = (uint32_t)((te & 0x7FFFFFFFu) - __hip_atomic_load(&g_btr[66], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    atomicAdd(&g_btr[min(rel / 500u, 63u)], 1u);
-    if (atomicAdd(&g_btr[64], 1u) + 1 == gridDim.x * (blockDim.x / 64)) {
-      printf("btrace waves by end time (5 us bins):");
-      for (int b = 0; b < 64; ++b) {
-        const unsigned int v = atomicExch(&g_btr[b], 0u);
-        if (v) printf(" %d:%u", b * 5, v);
-      }
-      printf("\n");
-      g_btr[64] = 0;
-      g_btr[66] = 0x7FFFFFFFu;
-    }
-  }
-#endif
   if (ts) {  // one stamp per workgroup, once all its waves are done
     __syncthreads();
     if (threadIdx.x == 0) atomicMax(&ts[1], (unsigned long long)wall_clock64());
@@ -2247,13 +2016,7 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
   if (p0 >= n) return;  // (whole workgroup)
   const uint32_t cnt = min(T, n - p0), tlast = cnt - 1;
   const bool valid = t < cnt;
-#if H3C_PB_TRACE
-  uint64_t tr[6];
-  tr[0] = wall_clock64();
-#define PB_MARK(j) (tr[j] = wall_clock64())
-#else
 #define PB_MARK(j) ((void)0)
-#endif
   const uint32_t p = p0 + t;
   const uint32_t c = valid ? skey[p] : 0xFFFFFFFFu;
   OpPos r{};
@@ -2320,17 +2083,6 @@ __global__ __launch_bounds__(kPhaseBTile) void uio_phaseb_kernel(
   __shared__ unsigned int sh[8];
   ctr_add_block(sh, ctr, v);
   if (s_void && t == 0) atomicOr(&misc[kMiscPBVoid], 1u);  // the host reruns phase B the scan-based way
-#if H3C_PB_TRACE
-  __syncthreads();
-  PB_MARK(4);
-  {
-    const uint32_t ntl = (n + T - 1) / T;
-    if (t == 0 && (k < 2 || k == ntl / 2 || k + 1 == ntl))
-      printf("phaseb tile %u start %llu loads %llu tscan %llu sscan %llu results %llu (ticks)\n", k,
-             (unsigned long long)tr[0], (unsigned long long)(tr[1] - tr[0]), (unsigned long long)(tr[2] - tr[0]),
-             (unsigned long long)(tr[3] - tr[0]), (unsigned long long)(tr[4] - tr[0]));
-  }
-#endif
   if (hout && t == 0) {
     // the last tile to finish hands the outcome words straight to the caller's pinned host buffer
     // (no device-to-host copy after the kernel); every tile's misc traffic is at the coherence
@@ -2459,9 +2211,6 @@ struct FastSink {  // apply_fragment's results on the fast branch: dv[op] = {1, 
   __device__ void fail(uint32_t op) const { st_agent(&dv[op], 2ull << 32); }
   __device__ void crc(uint32_t p, uint32_t v, uint32_t, uint32_t) const { st_agent(&dv[p], (1ull << 32) | v); }
 };
-#ifndef H3C_FX
-#define H3C_FX 0
-#endif
 #ifndef H3C_FAST_TRACE
 #define H3C_FAST_TRACE 0  // 1: workgroups 0, 1, the middle one and the last print their step times (diagnostics)
 #endif
@@ -2487,14 +2236,8 @@ constexpr uint32_t kScratchACtl = 64, kScratchAGran = 128;
 constexpr uint32_t kScratchAStat = kScratchAGran + 2 * kAGranRows * kFastCols;
 constexpr uint32_t kScratchHeads = kScratchAStat + 3 * kAGranRows;
 constexpr uint32_t kAEpochBatches = 240;  // aligned batches between zeroings (epochs are 8 bits)
-#ifndef H3C_FAST_GRAB
-#define H3C_FAST_GRAB 1  // 1: a workgroup's waves take their chain starts from an LDS counter (0: static ranges)
-#endif
 #ifndef H3C_FAST_WG_MULT
 #define H3C_FAST_WG_MULT 1  // uio_fast_kernel workgroups per CU over the launch (one resident at a time)
-#endif
-#ifndef H3C_FAST_LPT
-#define H3C_FAST_LPT 1  // the counter hands out the chains with later ops first, then the one-op chains
 #endif
 constexpr unsigned long long kGranApplied = 4ull << 32;  // look-back granule bit: some op of the chunk applied
 
@@ -2540,8 +2283,8 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
     bool hd = false, cn = false;
     if (j < hi) {
       const uint4 ch = chain[j];
-      hd = (H3C_FX & 64) ? true : (ch.x >> 31) != 0;  // (FX 64: timing experiment, every op its own chain: wrong results)
-      cn = hd && ch.y != kNil && !(H3C_FX & 64);
+      hd = (ch.x >> 31) != 0;
+      cn = hd && ch.y != kNil;
     }
     cm = __builtin_amdgcn_ballot_w64(cn);
     return __builtin_amdgcn_ballot_w64(hd);
@@ -2581,7 +2324,6 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
   uint64_t hm = 0, cm = 0;
   bool cont = false, ncont = false, ncont2 = false;
   Addr an{}, an2{};
-#if H3C_FAST_GRAB
   // Dynamic: a chain's later ops run on the wave of its start, so static ranges leave waves with a few
   // chains more than others finishing last.  The workgroup's ops [wlo, whi) are handed out one at a
   // time by an LDS counter (a wave skips the ops that do not start a chain); each wave's first op is
@@ -2607,7 +2349,6 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
     rows_at(a0, cur);
   }
   if (t == 0) s_grab = wlo + kBlkWaves;  // (the LPT form resets it below)
-#if H3C_FAST_LPT
   // Longest first: after the static first ops, the counter hands out the starts of chains with later ops
   // (their continuations' exposed round trips), a second counter then the one-op chains, so the
   // workgroup's last waves end on short work.  The chains with later ops come from the link kernel's list,
@@ -2646,22 +2387,11 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
       }
     }
   };
-#else
-  auto grab = [&](bool &cn) -> uint32_t {
-    for (;;) {
-      uint32_t j = 0;
-      if (lane == 0) j = atomicAdd(&s_grab, 1u);
-      j = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
-      if (j >= whi) return kNil;
-      if (is_start(j, cn)) return j;
-    }
-  };
-#endif
   FAST_MARK(1);
   fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
   __syncthreads();
   FAST_MARK(2);
-  if (first < whi && is_start(first, cont) && (!H3C_FAST_LPT || !cont)) {  // (LPT: those are on the list)
+  if (first < whi && is_start(first, cont) && !cont) {  // (LPT: those are on the list)
     op = first;
   } else {
     op = grab(cont);
@@ -2679,33 +2409,6 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
       if (nh2 != kNil) addr_of(nh2, an2);
     }
   }
-#else
-  if (lo < hi) {
-    // speculation: the range's first op starts its chain (~95 % on random writes), so its rows load
-    // before the chain starts are known; if it does not, the first start's rows load afterwards
-    Addr a0;
-    addr_of(lo, a0);
-    rows_at(a0, cur);
-    hm = starts(lo, cm);
-    op = next_start(g0, hm, cm, cont);
-    if (op != kNil) {
-      if (op != lo) {
-        addr_of(op, a0);
-        rows_at(a0, cur);
-      }
-      nh = next_start(g0, hm, cm, ncont);
-      if (nh != kNil) {
-        addr_of(nh, an);
-        nh2 = next_start(g0, hm, cm, ncont2);
-        if (nh2 != kNil) addr_of(nh2, an2);
-      }
-    }
-  }
-  FAST_MARK(1);
-  fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
-  __syncthreads();
-  FAST_MARK(2);
-#endif
   uint32_t head_op = op, dirty = 0;
   while (op != kNil) {
     if (op == head_op && nh != kNil) rows_at(an, nxt);  // the next chain's rows, in flight meanwhile
@@ -2747,11 +2450,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_fast_kernel(uint32_t n, uint3
     ncont = ncont2;
     nh2 = kNil;
     if (nh != kNil) {  // the addresses two chains ahead
-#if H3C_FAST_GRAB
       nh2 = grab(ncont2);
-#else
-      nh2 = next_start(g0, hm, cm, ncont2);
-#endif
       if (nh2 != kNil) addr_of(nh2, an2);
     }
   }
@@ -3147,12 +2846,6 @@ __global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uin
 // corrupted transfer), a block whose last op fails its check, or a look-back that gave up makes the pass
 // void: the bytes are right or deferred (kADefer list), and uio_afix_kernel recomputes every result from
 // the per-op records (dv, pv) and writes the deferred blocks.
-#ifndef H3C_AF_STORE_EARLY
-#define H3C_AF_STORE_EARLY 1  // 1: a block's only write is stored before its A6 fold (put back from the old rows
-#endif                        //    if the check fails), so the stores overlap the fold
-#ifndef H3C_AF_EXPERIMENT
-#define H3C_AF_EXPERIMENT 0  // timing-only builds: bit0 skips the A6 CRC (every check passes)
-#endif
 #ifndef H3C_AF_TRACE
 #define H3C_AF_TRACE 0  // 1: per-workgroup wall-clock stamps of the last launch (h3c_diag_af_trace, diagnostics)
 #endif
@@ -3164,9 +2857,6 @@ __device__ unsigned long long g_af_wave[1024 * 16];
 __device__ uint32_t g_af_blk[1024 * 4];  // per ticket: blockIdx, XCC, range start, range end
 __device__ uint32_t g_af_fin[1024 * 16];  // per wave: its ops whose block has later writes (the fin path)
 __device__ unsigned long long g_af_entry[1024 * 2];  // per blockIdx: kernel entry, ticket taken
-#endif
-#ifndef H3C_AF_EARLY_OLD
-#define H3C_AF_EARLY_OLD 0  // 1: the next op's old rows load with its new rows, before this op's CRCs (A/B)
 #endif
 #ifndef H3C_ATILE
 #define H3C_ATILE 256
@@ -3183,15 +2873,6 @@ constexpr uint32_t kAOne = 1u << 16;  // weight 1.0
 __device__ uint32_t g_aw_seed[kAClasses];  // the device's last learnt weights (0: none yet), seeding new scratches
 constexpr uint32_t kADoneVoid = 1u << 12;    // kADone: finished workgroups (low 12 bits) + void reports << 12
 constexpr uint32_t kASpin = 1u << 22;        // bounded look-back spins (about a quarter second)
-#ifndef H3C_AF_SKEW
-#define H3C_AF_SKEW 0
-#endif
-#ifndef H3C_AF_EARLY_FILL
-#define H3C_AF_EARLY_FILL 1  // the CRC tables fill before the range is known (beside thread 0's ticket; 0: after phase 0)
-#endif
-#ifndef H3C_AF_STATIC
-#define H3C_AF_STATIC 0
-#endif
 #ifndef H3C_AF_LOOK_WIN
 #define H3C_AF_LOOK_WIN 4
 #endif
@@ -3373,22 +3054,12 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
 #if H3C_AF_TRACE
     if (blockIdx.x < 1024) g_af_entry[2 * blockIdx.x + 1] = wall_clock64();
 #endif
-#if H3C_AF_SKEW  // (A/B) early positions carry more work per op (a block's first of several writes): the
-                  // cut points warped by p(f) = f - b f (1 - f), b = H3C_AF_SKEW / 1000
-    auto warp = [&](uint64_t c) -> uint32_t {
-      const double f = (double)c / (double)wt, b = H3C_AF_SKEW / 1000.0;
-      return (uint32_t)((f - b * f * (1.0 - f)) * (double)n);
-    };
-    s_wlo = warp(cum);
-    s_whi = s_ticket + 1 == gridDim.x ? n : warp(cum + wmine);
-#else
     s_wlo = (uint32_t)(cum * n / wt);
     s_whi = s_ticket + 1 == gridDim.x ? n : (uint32_t)((cum + wmine) * n / wt);
-#endif
   }
   if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
   // the CRC tables fill while thread 0 takes the ticket (waves 1-15; they do not depend on the range)
-  if (H3C_AF_EARLY_FILL && t >= 64) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t - 64, kBlkThreads - 64);
+  if (t >= 64) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t - 64, kBlkThreads - 64);
   __syncthreads();
   const uint32_t E = s_E, L = s_ticket, nwg = gridDim.x;
 #if H3C_AF_TRACE
@@ -3435,11 +3106,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   // one 32-byte record per op for phase 1's scalar loads ----
   // (each wave's first op is wlo + wave: its new rows and (speculated) block rows load before the fill)
   uint4 vn[4], vo[4];
-#if H3C_AF_STATIC  // (A/B: each wave runs its contiguous share in order, no LDS counter)
-  const uint32_t j0 = lo < hi ? lo : whi;
-#else
   const uint32_t j0 = wlo + wave;
-#endif
   uint64_t spec_old = 0;
   if (j0 < whi) {
     const h3c_update_io io = ios[j0];  // (scalar: wave-uniform)
@@ -3485,7 +3152,6 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     aa.rec[2 * (size_t)j + 1] = make_uint4((uint32_t)fin, (uint32_t)(fin >> 32), exp, fexp);
     aa.pv[j].y = prev;  // (uio_afix_kernel's input; crc0(new) follows in .x)
   }
-  if (!H3C_AF_EARLY_FILL) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
   if (t == 0) s_grab = wlo + kBlkWaves;  // (each wave's first op is wlo + wave)
   stores_done();
   __syncthreads();
@@ -3514,19 +3180,11 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     r.exp = b.z;
     r.fexp = b.w;
   };
-#if H3C_AF_STATIC
-  uint32_t next_static = j0 + 1;
-  auto grab = [&]() -> uint32_t {
-    const uint32_t j = next_static++;
-    return j < hi ? j : whi;
-  };
-#else
   auto grab = [&]() -> uint32_t {
     uint32_t j = 0;
     if (lane == 0) j = atomicAdd(&s_grab, 1u);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
   };
-#endif
   uint32_t wave_void = 0;
   uint32_t jc = j0 < whi ? j0 : kNil;
   Rec rc{}, rn{};
@@ -3552,27 +3210,27 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     Rec rnn{};
     if (jnn != kNil) rec_of(jnn, rnn);
     const bool solo = rc.first && rc.fin == rc.pnew;  // the block's only write
-    if (H3C_AF_STORE_EARLY && solo) {
+    if (solo) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) store_masked<H3C_AF_NT_STORES>(rc.pold, u * kRowBytes + lo16, vn[u], 0u, kBlk);
     }
     Streams s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (!(H3C_AF_EXPERIMENT & 1)) consume(s2[0], vn[u], lb, Lt);
+      consume(s2[0], vn[u], lb, Lt);
       consume(s2[1], xor4(vn[u], vo[u]), lb, Lt);
     }
     uint32_t fv[2];
     wave_fold_tab_n<2>(s2, lane, red, fv);
-    const uint32_t P = (H3C_AF_EXPERIMENT & 1) ? rc.exp : (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[0]);
+    const uint32_t P = (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[0]);
     const uint32_t D = (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[1]);
     const bool pass = P == rc.exp;
     if (rc.first) {  // the block's first op: the block's final bytes (the last op's, if its check passes)
       if (solo) {
-        if (H3C_AF_STORE_EARLY ? !pass : pass) {  // (early store: a failed check puts the old rows back)
+        if (!pass) {  // (the early store: a failed check puts the old rows back)
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            store_masked<H3C_AF_NT_STORES>(rc.pold, u * kRowBytes + lo16, H3C_AF_STORE_EARLY ? vo[u] : vn[u], 0u, kBlk);
+            store_masked<H3C_AF_NT_STORES>(rc.pold, u * kRowBytes + lo16, vo[u], 0u, kBlk);
         }
       } else {
 #if H3C_AF_TRACE
@@ -4907,7 +4565,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     // one stream on the front path: the prep kernel scans the piece counts itself, the piece pass
     // follows the sort, and the A6 verdicts and t0 come with the front kernel -- no fork and join
     // between streams (each cost ~7-10 us in graph replay: profiles/r03l_*)
-    const bool serial = front && H3C_UIO_SERIAL;
+    const bool serial = front;
     // (a kernel, not hipMemsetAsync: a memset node at the head of the captured graph was not
     // ordered before the prep kernel in replays -- stale tickets, r03m-r03p)
     if (serial) {
@@ -5150,7 +4808,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     auto fast_kernel = [&](hipStream_t q, bool timed) -> int {
       hipLaunchKernelGGL(uio_fast_kernel, dim3(nwg_fast), dim3(kBlkThreads), 0, q, n, stdf, pc, fa.frag, fa.chain,
                          fa.dv, fa.slow, timed ? d_ts : nullptr, fa.key, fa.head, fa.hmask,
-                         H3C_FAST_LPT ? d_heavy : nullptr, d_heavy + 64 * (((size_t)n + 63) / 64));
+                         d_heavy, d_heavy + 64 * (((size_t)n + 63) / 64));
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(uio_fast_sum_kernel, dim3(ntiles_tail), dim3(kTailTile), 0, q, n, pc, fa.frag, fa.key, fa.dv,
                          fa.slow, fa.head, fa.hmask, d_gran, d_part, d_misc + kMiscErr);
@@ -5178,7 +4836,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       }
       hipLaunchKernelGGL(uio_fast_link_kernel, dim3((n + 255) / 256), dim3(256), 0, q, fa.link, fa.key, fa.head,
                          fa.hmask, n, fa.slow, fa.chain, d_ios, d_chunks, nchunks, poly_type, stdf, pc, fa.frag,
-                         H3C_FAST_LPT ? d_heavy : nullptr, d_heavy + 64 * (((size_t)n + 63) / 64));
+                         d_heavy, d_heavy + 64 * (((size_t)n + 63) / 64));
       HIP_TRY(hipGetLastError());
       return H3C_OK;
     };
@@ -5321,9 +4979,8 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
                            d_skey, n, d_chunks, nchunks, d_status, poly_type, stdf, pc, d_pos, d_nfrag, d_fbase,
                            d_late, d_payraw, d_a6, d_misc, d_frag, d_fkey, cap, d_hhead, hcap - 1, d_gnext, d_prev,
                            d_fnext, d_fslot, d_paycrc0, exactf, d_t0, d_chunks_out,
-                           H3C_UIO_SERIAL ? d_sstate : nullptr, giveup & 1u);
+                           d_sstate, giveup & 1u);
         HIP_TRY(hipGetLastError());
-        if (!H3C_UIO_LATE_JOIN && !H3C_UIO_SERIAL) HIP_TRY(hipStreamWaitEvent(q, aux->done, 0));  // the A6 verdicts, t0
         return H3C_OK;
       }
       if (attempt) HIP_TRY(hipMemsetAsync(d_ctr, 0, 8 * kCtrN, q));  // the first attempt's counters
@@ -5366,7 +5023,6 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       return H3C_OK;
     };
     auto phase_b = [&](hipStream_t q) -> int {
-      if (H3C_UIO_LATE_JOIN && !H3C_UIO_SERIAL && front && attempt == 0) HIP_TRY(hipStreamWaitEvent(q, aux->done, 0));
       if (pb1) {
         hipLaunchKernelGGL(uio_phaseb_kernel, dim3(std::max(ntiles_pb, 1u)), dim3(kPhaseBTile), 0, q, d_pos, d_skey, n,
                            d_eacc, d_payraw, pc, d_a6, d_t0, d_chunks, d_chunks_out, nchunks, poly_type, stdf, d_res,

@@ -267,6 +267,10 @@ struct VersionGate {
       m.commitVer = cv;
       m.chainVer = op.commitChainVer;  // :241
       m.chunkState = ChunkState::CLEAN;  // DIRTY during the write, CLEAN at :298
+      // a chunk the gate knew no size for takes the admitted op's: the reference's createChunk path stores
+      // meta.innerFileId.chunkSize = writeIO.chunkSize (:163), and an existing chunk of another size would have
+      // failed this op with 4015, so later ops of the batch are checked against it
+      if (!op.isRemove && op.chunkSize && !m.chunkSize) m.chunkSize = op.chunkSize;
     }
   }
 };

@@ -413,7 +413,7 @@ static void data_iterator(bool gpu) {
 // replayed on the host in sequence order, each case of the reference once, including
 // the cascade of a failed checksum verify (the chunk's updateVer stays, so the next op misses one).
 static void version_gate() {
-  std::vector<ChunkVersion> v(5);
+  std::vector<ChunkVersion> v(6);
   v[1].chunkState = ChunkState::DIRTY;
   v[4].chunkState = ChunkState::DIRTY;  // (a 64 KiB chunk: the chunkSize / range cases)
   v[4].chunkSize = 64 << 10;
@@ -473,9 +473,12 @@ static void version_gate() {
       sized(4, 3, 64 << 10, 0, 4096),            // right size, DIRTY, not syncing: 4005
       sized(4, 10, 1 << 20, 0, 4096, true),      // syncing, wrong size: 4015 (no version change)
       sized(4, 0, 1 << 20, 0, 0, false, true),   // REMOVE: no size or range check; DIRTY -> 4005
+      sized(5, 1, 64 << 10, 0, 4096),            // a new chunk (size unknown): admitted, and it takes 64 KiB
+      sized(5, 2, 1 << 20, 0, 4096),             // the next op of it with another chunkSize: 4015 (ChunkReplica.cc:163)
+      sized(5, 2, 64 << 10, 4096, 4096),         // the same size: admitted
   };
   const std::vector<uint32_t> want = {0, 0, 4006, 4007, 4012, 0, 4008, 4080, 4007, 0, 4005, 0, 4081, 0, 4082, 4023,
-                                      0, 3, 0, 4012, 4015, 3, 4005, 4015, 4005};
+                                      0, 3, 0, 4012, 4015, 3, 4005, 4015, 4005, 0, 4015, 0};
   std::vector<uint32_t> st;
   VersionGate::run(v, ops, st);
   CHECK(st == want);
@@ -486,6 +489,7 @@ static void version_gate() {
   CHECK(v[4].updateVer == 2 && v[4].commitVer == 2 && v[4].chunkState == ChunkState::DIRTY);
   CHECK(v[2].updateVer == 6 && v[2].commitVer == 6 && v[2].chunkState == ChunkState::COMMIT && v[2].chainVer == 8);
   CHECK(v[3].updateVer == 1 && v[3].commitVer == 0);
+  CHECK(v[5].chunkSize == (64 << 10) && v[5].updateVer == 2);
 }
 
 int main(int argc, char **argv) {
