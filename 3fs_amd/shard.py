@@ -35,30 +35,47 @@ def partition(lengths: Sequence[int], world: int) -> List[Tuple[int, int]]:
     return [(cuts[k], cuts[k + 1]) for k in range(world)]
 
 
+def _gather_bytes(mine: np.ndarray, sizes: Sequence[int], group=None) -> List[np.ndarray]:
+    """Every rank's byte array (rank k's has sizes[k] bytes, known to all ranks from the partition): one
+    all_gather of equal-length uint8 tensors (padded to the largest), no pickling."""
+    import torch
+    import torch.distributed as dist
+
+    width = max(max(sizes), 1)
+    buf = torch.zeros(width, dtype=torch.uint8)
+    if mine.size:
+        buf[: mine.size] = torch.from_numpy(np.ascontiguousarray(mine).view(np.uint8).reshape(-1))
+    outs = [torch.empty(width, dtype=torch.uint8) for _ in sizes]
+    dist.all_gather(outs, buf, group=group)
+    return [o.numpy()[:k] for o, k in zip(outs, sizes)]
+
+
 def run_sharded(items: Sequence, expected: Sequence[int], verify_fn: Callable, rank: int, world: int,
                 lengths: Sequence[int] = None, group=None):
     """Verify this rank's slice with ``verify_fn(items, expected) -> (raw, ok)`` and
-    gather every rank's results (control-plane gather of 5 B per chunk).
+    gather every rank's results (control-plane gather of 5 B per chunk: one all_gather of
+    fixed-size byte tensors, each rank's slice length known to all from the partition).
 
     Returns (raw uint32[n], ok bool[n]) for the whole batch on every rank."""
-    import torch.distributed as dist
-
     if lengths is None:
         lengths = [getattr(it, "nbytes", None) or len(it) for it in items]
-    lo, hi = partition(lengths, world)[rank]
+    parts = partition(lengths, world)
+    lo, hi = parts[rank]
     raw, ok = verify_fn(items[lo:hi], list(expected[lo:hi]))
-    mine = (lo, np.asarray(raw, dtype=np.uint32), np.asarray(ok, dtype=bool))
-    if world == 1:
-        parts = [mine]
-    else:
-        parts = [None] * world
-        dist.all_gather_object(parts, mine, group=group)
     n = len(items)
     out_raw = np.zeros(n, dtype=np.uint32)
     out_ok = np.zeros(n, dtype=bool)
-    for lo_k, raw_k, ok_k in parts:
-        out_raw[lo_k: lo_k + raw_k.size] = raw_k
-        out_ok[lo_k: lo_k + ok_k.size] = ok_k
+    rec = np.zeros(hi - lo, dtype=[("raw", "<u4"), ("ok", "u1")])
+    rec["raw"] = np.asarray(raw, dtype=np.uint32)
+    rec["ok"] = np.asarray(ok, dtype=bool)
+    if world == 1:
+        got = [rec.view(np.uint8)]
+    else:
+        got = _gather_bytes(rec.view(np.uint8), [(b - a) * rec.dtype.itemsize for a, b in parts], group)
+    for (a, b), g in zip(parts, got):
+        r = g.view(rec.dtype)
+        out_raw[a:b] = r["raw"]
+        out_ok[a:b] = r["ok"].astype(bool)
     return out_raw, out_ok
 
 
@@ -82,19 +99,17 @@ def run_sharded_updates(op_chunk: Sequence[int], chunk_bytes: Sequence[int], app
                         world: int, group=None):
     """Apply this rank's ops with ``apply_fn(op_indices) -> per-op result records`` (numpy
     structured or 1-D array, one entry per index) and gather every rank's results in the
-    original op order (control-plane gather of the small per-op records)."""
-    import torch.distributed as dist
-
-    mine_idx = partition_updates(op_chunk, chunk_bytes, world)[rank]
-    mine = (mine_idx, np.asarray(apply_fn(mine_idx)))
-    if world == 1:
-        parts = [mine]
-    else:
-        parts = [None] * world
-        dist.all_gather_object(parts, mine, group=group)
+    original op order (control-plane gather of the small per-op records: one all_gather of fixed-size
+    byte tensors, no pickling; every rank's records share one dtype)."""
+    owners = partition_updates(op_chunk, chunk_bytes, world)
+    mine = np.ascontiguousarray(np.asarray(apply_fn(owners[rank])))
     n = len(op_chunk)
-    proto = next(p[1] for p in parts if p[1].size) if any(p[1].size for p in parts) else np.zeros(0)
-    out = np.zeros(n, dtype=proto.dtype)
-    for idx, res in parts:
-        out[idx] = res
+    out = np.zeros(n, dtype=mine.dtype)
+    if world == 1:
+        out[owners[0]] = mine
+        return out
+    # every rank knows every rank's op indices (the partition) and the record type (its own results')
+    got = _gather_bytes(mine.view(np.uint8), [len(ix) * mine.dtype.itemsize for ix in owners], group)
+    for ix, g in zip(owners, got):
+        out[ix] = g.view(mine.dtype)
     return out

@@ -1,4 +1,4 @@
-"""Multi-rank sharding (CPU, gloo, world_size 2): partition + gather of per-chunk results.
+"""Multi-rank sharding (CPU, gloo, world_size 2 and 4): partition + gather of per-chunk results.
 
 The per-rank compute function here is the oracle (this runs without a GPU); on
 the GPU box the same run_sharded() drives the HIP engine, one rank per GPU.
@@ -67,11 +67,12 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world2_sharded_verify():
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_sharded_verify(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
@@ -136,11 +137,12 @@ def _upd_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world2_sharded_updates():
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_sharded_updates(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_upd_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_upd_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
