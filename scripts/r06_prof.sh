@@ -16,5 +16,5 @@ NOX="--hostfed-extra-gib 0 --update-extra 0 --shard4m-extra 0 --inproc-extra 0"
 prof headline seg_crc_kernel 8589934592 "bench.py: 8192 x 1 MiB device-resident chunks (BASELINE config 2), no sub-passes" verify $NOX
 prof shard4m seg_crc_kernel 34359738368 "bench.py --chunks 8192 --chunk-kib 4096: 8192 x 4 MiB = 32 GiB (BASELINE config 4's per-GPU share at 8 GPUs; the default line's shard4m object)" verify --chunks 8192 --chunk-kib 4096 $NOX
 prof mixed seg_crc_kernel 8620183509 "bench.py --workload mixed: 8 GiB of 64 KiB-64 MiB chunks, 10% ragged, packed unaligned" mixed
-KT_STEPS=60 KT_WARMUP=20 prof updio uio_afused_kernel 1228800000 "bench.py --workload updio: 100000 x 4 KiB UpdateIOs into 64 x 64 MiB chunks, 4 rotating op tables (aligned sub-branch)" updio
+KT_STEPS=60 KT_WARMUP=20 prof updio uio_afused_kernel 1228800000 "bench.py --workload updio --updio-headline-only: 100000 x 4 KiB UpdateIOs into 64 x 64 MiB chunks, 4 rotating op tables (aligned sub-branch), the timed leg only" updio --updio-headline-only
 echo R06PROF_OK
