@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -117,11 +118,35 @@ struct h3c_multi {
   uint64_t gen = 0;
   int pending = 0;
   bool stop = false;
+  // Mirrors of gen / pending / stop (written under mu): a worker between jobs and a caller waiting for its
+  // workers spin on them for a while before blocking on the condition variables, so that back-to-back
+  // batches do not pay a futex wake each way (~30 us of a 1.3 ms config-2 call, profiles/r06_bench_default.json)
+  std::atomic<uint64_t> agen{0};
+  std::atomic<int> apending{0};
+  std::atomic<bool> astop{false};
+#ifndef H3C_MULTI_SPIN
+#define H3C_MULTI_SPIN 1  // 0: block at once (the same-box A/B, scripts/r06_multi_spin_ab.sh)
+#endif
+  static constexpr double kWorkerSpinUs = H3C_MULTI_SPIN ? 300 : 0, kCallerSpinUs = H3C_MULTI_SPIN ? 20000 : 0;
+
+  template <class F>
+  static bool spin_until(F done, double us) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 0;; ++k) {
+      if (done()) return true;
+      __builtin_ia32_pause();
+      if ((k & 255) == 255 &&
+          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > us)
+        return false;
+    }
+  }
 
   void loop(Worker *me) {
     uint64_t seen = 0;
     for (;;) {
       std::function<int(Worker &)> job;
+      spin_until([&] { return astop.load(std::memory_order_acquire) || agen.load(std::memory_order_acquire) != seen; },
+                 kWorkerSpinUs);
       {
         std::unique_lock<std::mutex> lk(mu);
         cv_work.wait(lk, [&] { return stop || gen != seen; });
@@ -138,7 +163,8 @@ struct h3c_multi {
         me->rc = rc;
         me->err.swap(err);
         me->ms = ms;
-        if (--pending == 0) cv_done.notify_all();
+        apending.store(--pending, std::memory_order_release);
+        if (pending == 0) cv_done.notify_all();
       }
     }
   }
@@ -153,10 +179,13 @@ struct h3c_multi {
         w[k]->rc = H3C_OK;
       }
       pending = (int)w.size();
+      apending.store(pending, std::memory_order_release);
       ++gen;
+      agen.store(gen, std::memory_order_release);
     }
     cv_work.notify_all();
-    std::unique_lock<std::mutex> lk(mu);
+    spin_until([&] { return apending.load(std::memory_order_acquire) == 0; }, kCallerSpinUs);
+    std::unique_lock<std::mutex> lk(mu);  // (the workers' results were written under mu)
     cv_done.wait(lk, [&] { return pending == 0; });
     for (size_t k = 0; k < w.size(); ++k) w[k]->job = nullptr;
     for (size_t k = 0; k < w.size(); ++k)
@@ -365,6 +394,7 @@ void h3c_multi_destroy(h3c_multi *m) {
   {
     std::lock_guard<std::mutex> lk(m->mu);
     m->stop = true;
+    m->astop.store(true, std::memory_order_release);
   }
   m->cv_work.notify_all();
   for (auto &w : m->w)
