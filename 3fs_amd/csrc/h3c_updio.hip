@@ -2891,16 +2891,20 @@ struct AlignedArgs {
   uint32_t *inp;                  // per op: its chunk's XOR of shifted deltas in the wave's range up to it
   uint2 *defer;                   // blocks whose first op deferred the write-back: {first op, last op}
   uint4 *rec;                     // per op, 2 x 16 bytes (uio_afused_kernel's phase 0 -> 1): new bytes, old bytes
-                                  //  (| 1: the block's first op), the block's final bytes, the A6 expectations
+                                  //  (| 1: the block's first op), the block's final bytes, the A6 expectations; in
+                                  //  the addresses' top 16 bits the op's shift to its chunk's end and its chunk
+  uint2 *pr;                      // per op (phase 1 -> 2): {its delta moved to its chunk's end (0: a failed
+                                  //  check), chunk | passed << 31}
   uint32_t *stat;                 // per ticket (FastScratch): {epoch << 8 | class, ops, wall-clock ticks of its ops}
 };
 
 // An op the aligned sub-branch takes: a fast-branch op (fast_op) that writes one whole 4 KiB block at a
-// block-aligned address from a 16-byte-aligned payload.
+// block-aligned address from a 16-byte-aligned payload, both below 2^48 (the records carry 16 bits in the
+// addresses' top bits; device addresses are 48-bit).
 __device__ __forceinline__ bool aligned_op(const h3c_update_io &io, const h3c_chunk_state &cs, uint32_t st,
                                            uint8_t poly_type) {
   return io.length == kBlk && ((cs.base + io.offset) & (kBlk - 1)) == 0 && (io.payload & 15) == 0 &&
-         fast_op(io, cs, st, poly_type);
+         (io.payload >> 48) == 0 && ((cs.base + io.offset) >> 48) == 0 && fast_op(io, cs, st, poly_type);
 }
 __device__ __forceinline__ bool aentry_valid(uint32_t e, uint32_t E) { return (e >> 24) == E && (e & 0xFFFFFFu) != 0; }
 // crc0 of an op's 4 KiB payload as its client checksum says it is (raw register, init ~0:
@@ -3024,6 +3028,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   __shared__ alignas(16) uint32_t lds[kLdsWords + kRedWords];
   __shared__ h3c_chunk_state s_cs[kFastChunksLds];
   __shared__ uint32_t s_ticket, s_E, s_slow, s_last, s_void, s_prev, s_grab, s_wlo, s_whi;
+  __shared__ uint32_t s_agg[kFastCols];  // the workgroup's per-chunk XOR of its ops' deltas at their chunks' ends
   __shared__ uint64_t s_t_start;
   const uint32_t t = threadIdx.x, lane = t & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -3058,6 +3063,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     s_whi = s_ticket + 1 == gridDim.x ? n : (uint32_t)((cum + wmine) * n / wt);
   }
   if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
+  if (t < kFastCols) s_agg[t] = 0;
   // the CRC tables fill while thread 0 takes the ticket (waves 1-15; they do not depend on the range)
   if (t >= 64) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t - 64, kBlkThreads - 64);
   __syncthreads();
@@ -3147,9 +3153,11 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
       }
     }
     if (prev != kNil) old = ios[prev].payload;
-    aa.rec[2 * (size_t)j] = make_uint4((uint32_t)io.payload, (uint32_t)(io.payload >> 32), (uint32_t)old,
-                                       (uint32_t)(old >> 32));
-    aa.rec[2 * (size_t)j + 1] = make_uint4((uint32_t)fin, (uint32_t)(fin >> 32), exp, fexp);
+    // x^(8(size - offset - 4096)): the op's delta moved to its chunk's end (phase 1 applies it)
+    const uint32_t xs = dxpow8_fast((int64_t)cs.size - (int64_t)io.offset - (int64_t)kBlk, pc, poly);
+    aa.rec[2 * (size_t)j] = make_uint4((uint32_t)io.payload, (uint32_t)(io.payload >> 32) | (xs & 0xFFFF0000u),
+                                       (uint32_t)old, (uint32_t)(old >> 32) | (xs << 16));
+    aa.rec[2 * (size_t)j + 1] = make_uint4((uint32_t)fin, (uint32_t)(fin >> 32) | (io.chunk << 16), exp, fexp);
     aa.pv[j].y = prev;  // (uio_afix_kernel's input; crc0(new) follows in .x)
   }
   if (t == 0) s_grab = wlo + kBlkWaves;  // (each wave's first op is wlo + wave)
@@ -3167,18 +3175,20 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   // new ^ old, the block write-back by the block's first op, {state, delta} and crc0(new) published ----
   struct Rec {
     uint64_t pnew, pold, fin;
-    uint32_t exp, fexp;
+    uint32_t exp, fexp, xs, c;
     bool first;
   };
   auto rec_of = [&](uint32_t j, Rec &r) {  // (scalar loads: j is wave-uniform)
     const uint4 a = aa.rec[2 * (size_t)j], b = aa.rec[2 * (size_t)j + 1];
-    r.pnew = (uint64_t)a.x | ((uint64_t)a.y << 32);
-    const uint64_t o = (uint64_t)a.z | ((uint64_t)a.w << 32);
+    r.pnew = (uint64_t)a.x | ((uint64_t)(a.y & 0xFFFFu) << 32);
+    const uint64_t o = (uint64_t)a.z | ((uint64_t)(a.w & 0xFFFFu) << 32);
     r.pold = o & ~uint64_t(1);
     r.first = (o & 1u) != 0;
-    r.fin = (uint64_t)b.x | ((uint64_t)b.y << 32);
+    r.fin = (uint64_t)b.x | ((uint64_t)(b.y & 0xFFFFu) << 32);
     r.exp = b.z;
     r.fexp = b.w;
+    r.xs = (a.y & 0xFFFF0000u) | (a.w >> 16);
+    r.c = b.y >> 16;
   };
   auto grab = [&]() -> uint32_t {
     uint32_t j = 0;
@@ -3255,9 +3265,14 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
         }
       }
     }
+    // the delta moved to the chunk's end: phase 2's input, and the workgroup's per-chunk XOR (published as
+    // its aggregate as soon as the loop ends)
+    const uint32_t v = pass ? dgf_mul(D, rc.xs, poly) : 0u;
     if (lane == 0) {
       aa.dv[jc] = ((unsigned long long)(pass ? 1u : 2u) << 32) | D;
       aa.pv[jc].x = P;
+      aa.pr[jc] = make_uint2(v, rc.c | (pass ? 0x80000000u : 0u));
+      atomicXor(&s_agg[rc.c], v);
     }
     if (!pass) wave_void = 1;
     jc = jn;
@@ -3276,6 +3291,13 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   if (wave_void && lane == 0) atomicOr(&s_void, 1u);
   stores_done();
   __syncthreads();  // every op of the workgroup published (the CRC tables are done with: their LDS is free)
+  // the workgroup's aggregate, at once: a successor's look-back waits for nothing after this loop
+  unsigned long long *row = aa.gran + (uint64_t)L * kFastCols;
+  const bool two = nchunks > 64;
+  if (wave == 0 && L > 0) {
+    if (lane < nchunks) st_agent(&row[lane], agran(E, 1u, s_agg[lane]));
+    if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], agran(E, 1u, s_agg[64 + lane]));
+  }
   if (t == 0 && L < kAGranRows) {  // this workgroup's throughput, for the next batch's range weights
     const uint64_t t1 = wall_clock64();
     aa.stat[3 * L] = (E << 8) | cls;
@@ -3296,16 +3318,11 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
       uint32_t v = 0;
       my_c = kNil;
       my_pass = 0;
-      if (lane < cnt) {
-        const unsigned long long key = aa.key[k];
-        const unsigned long long g = ld_agent(&aa.dv[k]);  // (another wave's store, before the barrier)
-        my_c = (uint32_t)(key >> 36);
-        my_pass = (uint32_t)(g >> 32) == 1u;
-        if (my_pass) {  // x^(8(size - offset - 4096)), the offset from the key's block address
-          const h3c_chunk_state &cs = s_cs[my_c];
-          const int64_t off = (int64_t)((key & ((1ull << 36) - 1)) << 12) - (int64_t)cs.base;
-          v = dgf_mul((uint32_t)g, dxpow8_fast((int64_t)cs.size - off - (int64_t)kBlk, pc, poly), poly);
-        }
+      if (lane < cnt) {  // (the workgroup's own stores, before the barrier)
+        const uint2 q = aa.pr[k];
+        v = q.x;
+        my_c = q.y & 0x7FFFFFFFu;
+        my_pass = q.y >> 31;
       }
       const uint32_t src = my_c & 63;
       const uint32_t r0 = __shfl(acc0, src, 64), r1 = __shfl(acc1, src, 64);
@@ -3327,19 +3344,11 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   // ---- chunk aggregates: waves of the workgroup (LDS), then workgroups (look-back in ticket order) ----
   uint32_t *wagg = lds;                                 // [16][128]
   uint32_t *wexcl = lds + kBlkWaves * kFastCols;        // [128]: the workgroup's exclusive prefix
-  auto lookback = [&]() {  // wave 0: the workgroup's sums (wagg) published, the look-back, the inclusive sums
+  auto lookback = [&]() {  // wave 0: the look-back (the aggregate is out), the inclusive sums
     if (wave == 0) {
-      uint32_t a0 = 0, a1 = 0;
-      for (uint32_t w = 0; w < kBlkWaves; ++w) {
-        a0 ^= wagg[w * kFastCols + lane];
-        a1 ^= wagg[w * kFastCols + 64 + lane];
-      }
-      const bool two = nchunks > 64;
-      unsigned long long *row = aa.gran + (uint64_t)L * kFastCols;
+      const uint32_t a0 = s_agg[lane], a1 = s_agg[64 + lane];
       uint32_t x0 = 0, x1 = 0;
       if (L > 0) {
-        if (lane < nchunks) st_agent(&row[lane], agran(E, 1u, a0));
-        if (two && lane + 64 < nchunks) st_agent(&row[64 + lane], agran(E, 1u, a1));
         int j0 = lane < nchunks ? (int)L - 1 : -1, j1 = two && lane + 64 < nchunks ? (int)L - 1 : -1;
         const uint32_t limit = (force_void & 1) && L == 1 ? 0u : kASpin;  // (test hook: ticket 1 gives up at once)
         for (uint32_t spins = 0; __builtin_amdgcn_ballot_w64(j0 >= 0 || j1 >= 0) != 0;) {
@@ -4113,7 +4122,8 @@ struct ArgLayout<AlignedArgs, void> {
     struct_arg<AlignedArgs>(a, {offsetof(AlignedArgs, ctl), offsetof(AlignedArgs, head), offsetof(AlignedArgs, gran),
                                 offsetof(AlignedArgs, key), offsetof(AlignedArgs, link), offsetof(AlignedArgs, dv),
                                 offsetof(AlignedArgs, pv), offsetof(AlignedArgs, inp), offsetof(AlignedArgs, defer),
-                                offsetof(AlignedArgs, rec), offsetof(AlignedArgs, stat)});
+                                offsetof(AlignedArgs, rec), offsetof(AlignedArgs, pr),
+                                offsetof(AlignedArgs, stat)});
   }
 };
 template <>
@@ -4487,6 +4497,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
       aa.inp = carve<uint32_t>(cur, n);
       aa.defer = carve<uint2>(cur, n);
       aa.rec = carve<uint4>(cur, 2 * (size_t)n);
+      aa.pr = carve<uint2>(cur, n);
     }
     return (size_t)(cur - base);
   };

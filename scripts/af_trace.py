@@ -70,6 +70,14 @@ for x in range(8):
 wl = (w - us[:, 1:2]).ravel()
 print("corr(wave time, fin ops) = %.2f; fin ops/wave by ticket quartile:" % np.corrcoef(wl, fin.ravel())[0, 1],
       [round(float(fin[q * nwg // 4:(q + 1) * nwg // 4].mean()), 2) for q in range(4)])
+# the look-back's own latency: from the moment every ticket up to L (itself included) has ended its loop
+pre = np.maximum.accumulate(us[:, 2])
+exc = us[:, 3] - pre
+print("look-back latency after the last predecessor's loop end: q50 %.1f q90 %.1f max %.1f (ticket %d)" % (
+    np.median(exc), np.percentile(exc, 90), exc.max(), int(exc.argmax())))
+lo = np.argsort(us[:, 3])[-8:]
+print("latest look-back ends (ticket, loop_end, predecessors' last loop end, lookback_end):",
+      [(int(i), round(float(us[i, 2]), 1), round(float(pre[i]), 1), round(float(us[i, 3]), 1)) for i in lo])
 print("blockIdx -> xcc:", [(int(blk[i, 0]), int(blk[i, 1])) for i in range(12)])
 # which waves are late: their op ranges (ticket * 16 + wave) -> position in the batch
 late = np.argsort(w.ravel())[-20:]
