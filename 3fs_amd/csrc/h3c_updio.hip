@@ -2896,6 +2896,8 @@ struct AlignedArgs {
   uint2 *pr;                      // per op (phase 1 -> 2): {its delta moved to its chunk's end (0: a failed
                                   //  check), chunk | passed << 31}
   uint32_t *stat;                 // per ticket (FastScratch): {epoch << 8 | class, ops, wall-clock ticks of its ops}
+  uint32_t *hand;                 // per op (FastScratch; epoch-tagged): the hand-over word of a block's last op
+                                  //  between it and the block's first op (kHandRead / kHandPending)
 };
 
 // An op the aligned sub-branch takes: a fast-branch op (fast_op) that writes one whole 4 KiB block at a
@@ -3007,10 +3009,19 @@ __global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *
       if (u > t) last = false;
     }
   uint4 lk = make_uint4(pin == kNil ? kNil : base + pin, 0u, 0u, 0u);
-  if (h != kNil && last) lk.y = atomicExch(&aa.head[fast_bucket(key, aa.hmask)], (E << 24) | (i + 1));
+  if (h != kNil && last) {  // (listed: .z marks it)
+    lk.y = atomicExch(&aa.head[fast_bucket(key, aa.hmask)], (E << 24) | (i + 1));
+    lk.z = 1;
+  }
   aa.link[i] = lk;
 }
 
+// The hand-over of a block's final bytes between its first op (which reads the block) and its last op (whose
+// bytes are final): each exchanges its mark into the last op's word; whichever comes second writes the block
+// -- the last op from its own rows if the first op has read the block, else the first op from the last op's
+// payload.  The words carry the batch's epoch (trusted in the zeroed FastScratch only).
+__device__ __forceinline__ uint32_t ahand(uint32_t E, uint32_t state) { return 0x01000000u | (E << 8) | state; }
+constexpr uint32_t kHandRead = 1, kHandPending = 2;
 __device__ __forceinline__ unsigned long long agran(uint32_t E, uint32_t state, uint32_t v) {
   return ((unsigned long long)((E << 8) | state) << 32) | v;
 }
@@ -3129,35 +3140,33 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     const uint4 lk = aa.link[j];
     const h3c_chunk_state &cs = s_cs[io.chunk];  // (aprep: every op's chunk is < nchunks <= 128)
     const uint32_t exp = aexpect(io.checksum_value, std_domain, k4096);
-    uint32_t prev = lk.x, fexp = 0;
-    uint64_t old = 0, fin = 0;
-    if (prev == kNil) {  // no earlier op of the block in this tile: the earlier tiles' listed last ops
+    // the block's previous op (in this tile, else the last listed one of an earlier tile) and, for an op listed
+    // as its tile's last of the block, whether a later tile lists the block too (fmax: the largest listed op)
+    uint32_t prev = lk.x, fmax = j;
+    const bool tile_first = prev == kNil, listed = lk.z != 0;
+    uint64_t old = 0, f = 0;
+    if (tile_first || listed) {
       const unsigned long long key = aa.key[j];
-      uint32_t fmax = j;
       for (uint32_t e = aa.head[fast_bucket(key, aa.hmask)]; aentry_valid(e, E); e = aa.link[(e & 0xFFFFFFu) - 1].y) {
         const uint32_t i = (e & 0xFFFFFFu) - 1;
         if (i >= n) break;  // (cannot happen: this batch's entries name its ops)
         if (aa.key[i] != key) continue;
-        if (i < j && (prev == kNil || i > prev)) prev = i;
+        if (tile_first && i < j && (prev == kNil || i > prev)) prev = i;
         fmax = max(fmax, i);
       }
-      if (prev == kNil) {  // the block's first op
-        old = (cs.base + io.offset) | 1u;
-        fin = io.payload;
-        fexp = exp;
-        if (fmax != j) {
-          const h3c_update_io fio = ios[fmax];
-          fin = fio.payload;
-          fexp = aexpect(fio.checksum_value, std_domain, k4096);
-        }
-      }
     }
-    if (prev != kNil) old = ios[prev].payload;
+    if (prev == kNil) {  // the block's first op; of several: its last op's index (the hand-over word)
+      old = (cs.base + io.offset) | 1u;
+      if (fmax != j) f = ((uint64_t)fmax << 2) | 1u;
+    } else {
+      old = ios[prev].payload;
+      if (listed && fmax == j) f = (cs.base + io.offset) | 2u;  // the block's last op of several: the block
+    }
     // x^(8(size - offset - 4096)): the op's delta moved to its chunk's end (phase 1 applies it)
     const uint32_t xs = dxpow8_fast((int64_t)cs.size - (int64_t)io.offset - (int64_t)kBlk, pc, poly);
     aa.rec[2 * (size_t)j] = make_uint4((uint32_t)io.payload, (uint32_t)(io.payload >> 32) | (xs & 0xFFFF0000u),
                                        (uint32_t)old, (uint32_t)(old >> 32) | (xs << 16));
-    aa.rec[2 * (size_t)j + 1] = make_uint4((uint32_t)fin, (uint32_t)(fin >> 32) | (io.chunk << 16), exp, fexp);
+    aa.rec[2 * (size_t)j + 1] = make_uint4((uint32_t)f, (uint32_t)(f >> 32) | (io.chunk << 16), exp, 0u);
     aa.pv[j].y = prev;  // (uio_afix_kernel's input; crc0(new) follows in .x)
   }
   if (t == 0) s_grab = wlo + kBlkWaves;  // (each wave's first op is wlo + wave)
@@ -3174,8 +3183,8 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   // (static shares left waves up to ~30 us apart): per op the A6 CRC of the new bytes and the delta CRC of
   // new ^ old, the block write-back by the block's first op, {state, delta} and crc0(new) published ----
   struct Rec {
-    uint64_t pnew, pold, fin;
-    uint32_t exp, fexp, xs, c;
+    uint64_t pnew, pold, f;  // f: 0; (the block's last op << 2) | 1 (a first op of several); the block | 2 (a last op)
+    uint32_t exp, xs, c;
     bool first;
   };
   auto rec_of = [&](uint32_t j, Rec &r) {  // (scalar loads: j is wave-uniform)
@@ -3184,9 +3193,8 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     const uint64_t o = (uint64_t)a.z | ((uint64_t)(a.w & 0xFFFFu) << 32);
     r.pold = o & ~uint64_t(1);
     r.first = (o & 1u) != 0;
-    r.fin = (uint64_t)b.x | ((uint64_t)(b.y & 0xFFFFu) << 32);
+    r.f = (uint64_t)b.x | ((uint64_t)(b.y & 0xFFFFu) << 32);
     r.exp = b.z;
-    r.fexp = b.w;
     r.xs = (a.y & 0xFFFF0000u) | (a.w >> 16);
     r.c = b.y >> 16;
   };
@@ -3219,7 +3227,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     if (jnn >= whi) jnn = kNil;
     Rec rnn{};
     if (jnn != kNil) rec_of(jnn, rnn);
-    const bool solo = rc.first && rc.fin == rc.pnew;  // the block's only write
+    const bool solo = rc.first && rc.f == 0;  // the block's only write
     if (solo) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) store_masked<H3C_AF_NT_STORES>(rc.pold, u * kRowBytes + lo16, vn[u], 0u, kBlk);
@@ -3235,34 +3243,42 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     const uint32_t P = (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[0]);
     const uint32_t D = (uint32_t)__builtin_amdgcn_readfirstlane((int)fv[1]);
     const bool pass = P == rc.exp;
-    if (rc.first) {  // the block's first op: the block's final bytes (the last op's, if its check passes)
-      if (solo) {
-        if (!pass) {  // (the early store: a failed check puts the old rows back)
+    if (solo && !pass) {  // the block's only write fails its check: the early store undone (old rows back)
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
-            store_masked<H3C_AF_NT_STORES>(rc.pold, u * kRowBytes + lo16, vo[u], 0u, kBlk);
-        }
-      } else {
+      for (int u = 0; u < 4; ++u) store_masked<H3C_AF_NT_STORES>(rc.pold, u * kRowBytes + lo16, vo[u], 0u, kBlk);
+    }
+    if (rc.f & 1u) {  // the first op of several: the block is read (its rows are folded into D: the asm
+                      // keeps the exchange after that), hand over to the block's last op
+      asm volatile("" ::"s"(D) : "memory");
+      const uint32_t fm = (uint32_t)(rc.f >> 2);
+      uint32_t o = 0;
+      if (lane == 0) o = atomicExch(&aa.hand[fm], ahand(E, kHandRead));
+      if ((uint32_t)__builtin_amdgcn_readfirstlane((int)o) == ahand(E, kHandPending)) {
+        // the last op came first (and passed its check): its bytes to the block, from its payload
 #if H3C_AF_TRACE
         if (lane == 0 && L < 1024) atomicAdd(&g_af_fin[16 * L + wave], 1u);
 #endif
-        // (into the old rows' registers: this op's delta is folded, and the next op's rows are in wn / wo)
+        const uint64_t lp = ios[fm].payload;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) vo[u] = load_row_rmw(rc.fin + (uint32_t)(u * kRowBytes + lo16));
-        Streams sf{0, 0, 0, 0};
+        for (int u = 0; u < 4; ++u) vo[u] = load_row_rmw(lp + (uint32_t)(u * kRowBytes + lo16));
 #pragma unroll
-        for (int u = 0; u < 4; ++u) consume(sf, vo[u], lb, Lt);
-        const uint32_t Pf = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_fold_tab(sf, lane, red));
-        if (Pf == rc.fexp) {
+        for (int u = 0; u < 4; ++u) store_masked<H3C_AF_NT_STORES>(rc.pold, u * kRowBytes + lo16, vo[u], 0u, kBlk);
+      }
+    } else if (rc.f & 2u) {  // the last op of several: its bytes are the block's final bytes
+      if (pass) {
+        uint32_t o = 0;
+        if (lane == 0) o = atomicExch(&aa.hand[jc], ahand(E, kHandPending));
+        if ((uint32_t)__builtin_amdgcn_readfirstlane((int)o) == ahand(E, kHandRead)) {  // the block is read
+          const uint64_t blk = rc.f & ~uint64_t(3);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) store_masked<H3C_AF_NT_STORES>(rc.pold, u * kRowBytes + lo16, vo[u], 0u, kBlk);
-        } else {  // the last op fails A6: uio_afix_kernel writes the last passing op's bytes (if any)
-          if (lane == 0) {
-            const uint32_t d = atomicAdd(&aa.ctl[kADefer], 1u);
-            aa.defer[d] = make_uint2(jc, 0u);
-          }
-          wave_void = 1;
+          for (int u = 0; u < 4; ++u) store_masked<H3C_AF_NT_STORES>(blk, u * kRowBytes + lo16, vn[u], 0u, kBlk);
         }
+      } else {  // it fails A6: uio_afix_kernel writes the last passing op's bytes (if any)
+        if (lane == 0) {
+          const uint32_t d = atomicAdd(&aa.ctl[kADefer], 1u);
+          aa.defer[d] = make_uint2(jc, 0u);
+        }
+        wave_void = 1;
       }
     }
     // the delta moved to the chunk's end: phase 2's input, and the workgroup's per-chunk XOR (published as
@@ -4123,7 +4139,7 @@ struct ArgLayout<AlignedArgs, void> {
                                 offsetof(AlignedArgs, key), offsetof(AlignedArgs, link), offsetof(AlignedArgs, dv),
                                 offsetof(AlignedArgs, pv), offsetof(AlignedArgs, inp), offsetof(AlignedArgs, defer),
                                 offsetof(AlignedArgs, rec), offsetof(AlignedArgs, pr),
-                                offsetof(AlignedArgs, stat)});
+                                offsetof(AlignedArgs, stat), offsetof(AlignedArgs, hand)});
   }
 };
 template <>
@@ -4654,7 +4670,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   // are about to wrap, is zeroed here, before the batch and outside any capture
   FastScratch *fsc = nullptr;
   if (try_aligned || try_fast) {
-    fsc = fast_scratch(dev, kScratchHeads + 2 * (size_t)hcap_fast);
+    fsc = fast_scratch(dev, kScratchHeads + 3 * (size_t)hcap_fast);
     if (!fsc) return H3C_ERR_HIP;
     if (fsc->hcap != hcap_fast || fsc->abatches >= kAEpochBatches) fsc->dirty = true;
     fa.slow = fsc->p;
@@ -4663,12 +4679,13 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     aa.gran = reinterpret_cast<unsigned long long *>(fsc->p + kScratchAGran);
     aa.stat = fsc->p + kScratchAStat;
     aa.head = fsc->p + kScratchHeads + hcap_fast;
+    aa.hand = fsc->p + kScratchHeads + 2 * (size_t)hcap_fast;  // (hcap_fast >= 2n)
     aa.hmask = hcap_fast - 1;
     aa.key = fa.key;
     aa.link = fa.link;
     aa.dv = fa.dv;
     if (fsc->dirty) {
-      const uint32_t zw = kScratchHeads + 2 * hcap_fast, zg = std::min(1024u, (zw + 1023) / 1024);
+      const uint32_t zw = kScratchHeads + 3 * hcap_fast, zg = std::min(1024u, (zw + 1023) / 1024);
       // (the aligned range weights are kept across a re-zeroing: they describe the device, not the batches)
       const uint32_t w0 = fsc->fresh ? zw : kScratchACtl + kAW, w1 = fsc->fresh ? zw : kScratchACtl + kAW + kAClasses;
       hipLaunchKernelGGL(uio_zero_kernel, dim3(zg), dim3(256), 0, st, fsc->p, w0, fsc->p + w1, zw - w1, nullptr, 0u,

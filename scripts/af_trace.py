@@ -78,6 +78,15 @@ print("look-back latency after the last predecessor's loop end: q50 %.1f q90 %.1
 lo = np.argsort(us[:, 3])[-8:]
 print("latest look-back ends (ticket, loop_end, predecessors' last loop end, lookback_end):",
       [(int(i), round(float(us[i, 2]), 1), round(float(pre[i]), 1), round(float(us[i, 3]), 1)) for i in lo])
+# per-workgroup loop time against its ops and its fin-path ops (a block's first of several writes)
+finw = fin.sum(1).astype(np.float64)
+A = np.stack([ops, finw], 1)
+coef, *_ = np.linalg.lstsq(A, loop, rcond=None)
+print("loop time ~ %.4f us/op + %.4f us/fin-op (fin-op extra cost = %.2f ops); residual std %.1f us" % (
+    coef[0], coef[1], coef[1] / coef[0], np.std(loop - A @ coef)))
+q4 = [slice(q * nwg // 4, (q + 1) * nwg // 4) for q in range(4)]
+print("by ticket quartile: ops", [round(float(ops[s_].mean()), 1) for s_ in q4], "fin ops", [round(float(finw[s_].mean()), 1) for s_ in q4],
+      "loop us", [round(float(loop[s_].mean()), 1) for s_ in q4], "loop_end", [round(float(us[s_, 2].mean()), 1) for s_ in q4])
 print("blockIdx -> xcc:", [(int(blk[i, 0]), int(blk[i, 1])) for i in range(12)])
 # which waves are late: their op ranges (ticket * 16 + wave) -> position in the batch
 late = np.argsort(w.ravel())[-20:]

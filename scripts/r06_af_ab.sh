@@ -5,7 +5,7 @@ set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 out=gpurun_out/r06_af_ab.txt
 : > $out
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_updio_aligned.py tests/test_gpu_config3.py > gpurun_out/r06_af_tests.log 2>&1 || { echo TESTS_FAIL; tail -30 gpurun_out/r06_af_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_updio_aligned.py tests/test_gpu_config3.py tests/test_gpu_updio_fast.py tests/test_gpu_concurrency.py > gpurun_out/r06_af_tests.log 2>&1 || { echo TESTS_FAIL; tail -30 gpurun_out/r06_af_tests.log; exit 1; }
 tail -2 gpurun_out/r06_af_tests.log
 run() {  # label, lib, extra args
   H3C_LIB_PATH=$2 timeout -k 10 120 python -u bench.py --workload updio --no-cpu-baseline $3 > gpurun_out/r06_tab.json || exit 1
