@@ -2836,10 +2836,13 @@ __global__ void uio_stale_kernel(const h3c_chunk_state *__restrict__ chunks, uin
 //     in ticket order); per op: the old bytes are the previous op's payload, or the block for the block's
 //     first op (speculated "no earlier op", the bucket walk overlapped with the first rows); crc0(new) is
 //     the A6 check (ChunkReplica.cc:193-207), crc0(new ^ old) the delta of updateChecksum case (iv)
-//     (:356-390, the checksum moved by linearity); the block's first op writes the block's final bytes
-//     (the last op's payload, itself checked first).  Per group of 64 ops the deltas shifted to the
-//     chunk's end are folded into per-chunk XORs held in the lanes; workgroups chain their per-chunk
-//     aggregates by decoupled look-back; every op's result is written directly; the last workgroup to
+//     (:356-390, the checksum moved by linearity); a block's only op writes its bytes; of several, the
+//     first op (which reads the block) and the last op (whose bytes are final) meet in an exchange word,
+//     and the second to arrive writes the block (the last op from its rows, or the first op from the last
+//     op's payload).  Each op's delta shifted to its chunk's end is XORed into the workgroup's per-chunk
+//     aggregate (LDS), published as soon as the loop ends; then per group of 64 ops the shifted deltas
+//     are folded into per-chunk XORs held in the lanes; workgroups chain their per-chunk aggregates by
+//     decoupled look-back; every op's result is written directly; the last workgroup to
 //     finish writes the final states, the counters, the commit and the outcome word.
 // Nothing is zeroed per batch: the bucket heads and granules carry the batch's epoch (kAEpoch, advanced by
 // the last workgroup), the ticket and done words are reset by the last workgroup.  An A6 failure (a
