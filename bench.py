@@ -464,9 +464,14 @@ def run_update(args, cx: Ctx) -> dict:
     h3c.fill_splitmix(chunks, clen, nchunks, clen, SEED, first_chunk=cx.rank * nchunks)
     payload = torch.empty(nw * G, dtype=torch.uint8, device=cx.dev)
     h3c.fill_splitmix(payload, G, nw, G, SEED + 1, first_chunk=cx.rank * nw)
-    g = torch.Generator().manual_seed(SEED + cx.rank)
-    wc = torch.randint(0, nchunks, (nw,), generator=g, dtype=torch.int32).to(cx.dev)
-    wb = torch.randint(0, bpc, (nw,), generator=g, dtype=torch.int32).to(cx.dev)
+    # `tables` seeded write tables in rotation (as run_updio): each step applies the next table on top of the
+    # previous state, so the kernel's per-XCD range weights never see the same batch twice in a row
+    ntab = max(1, int(getattr(args, "update_tables", 4)))
+    tabs = []
+    for t in range(ntab):
+        g = torch.Generator().manual_seed(SEED + cx.rank + 7919 * t)
+        tabs.append((torch.randint(0, nchunks, (nw,), generator=g, dtype=torch.int32).to(cx.dev),
+                     torch.randint(0, bpc, (nw,), generator=g, dtype=torch.int32).to(cx.dev)))
     plan = h3c.Plan.uniform(chunks.data_ptr(), clen, nchunks, device=cx.local)
     raw = [torch.zeros(nchunks, dtype=torch.int32, device=cx.dev) for _ in range(2)]
     plan.run(raw[0], stream=cx.stream)
@@ -475,13 +480,15 @@ def run_update(args, cx: Ctx) -> dict:
     ws = torch.empty(h3c.update_workspace_bytes(nw, nchunks, clen, G), dtype=torch.uint8, device=cx.dev)
     ctr = torch.zeros(8, dtype=torch.int64, device=cx.dev)
     exact = bool(getattr(args, "exact", False))
-    cur = [0]
+    cur = [0, 0]
 
-    def step():  # apply the batch again on top of the previous state: same traffic, new checksums
+    def step():  # the next table on top of the previous state: same traffic, new checksums
         i = cur[0]
+        wc, wb = tabs[cur[1] % ntab]
         h3c.update_blocks(bases, clen, raw[i], wc, wb, payload, out, raw[1 - i], block_bytes=G, workspace=ws,
                           stream=cx.stream, exact=exact, counters=ctr)
         cur[0] = 1 - i
+        cur[1] += 1
 
     elapsed, prof = cx.timed(step, args.steps, args.warmup, h3c.engine.PROF_UPDATE)
     fresh = torch.zeros(nchunks, dtype=torch.int32, device=cx.dev)
@@ -501,7 +508,8 @@ def run_update(args, cx: Ctx) -> dict:
         "data": "synthetic (splitmix64 chunks and payloads in HBM, seeded uniform chunk/offset)",
         "config": {"workload": f"BASELINE config 3: {nw} random 4 KiB writes into {nchunks} x 64 MiB chunks per GPU"
                                + (" (H3C_UPD_EXACT: the chunks re-CRC'd from their bytes every step)" if exact else ""),
-                   "parallelism": f"shard{cx.world}", "exact": exact},
+                   "parallelism": f"shard{cx.world}", "exact": exact, "tables": ntab,
+                   "table_rotation": "each step applies the next of `tables` seeded write tables"},
         "verified": verified,
         "counters": counters,
         "algorithmic_gbps": round(writes * 3 * G / elapsed / 1e9, 1),
@@ -1157,6 +1165,8 @@ def main() -> int:
                          "the other form is timed beside it")
     ap.add_argument("--updio-tables", type=int, default=4,
                     help="updio: seeded op tables run in rotation (every batch differs from the last)")
+    ap.add_argument("--update-tables", type=int, default=4,
+                    help="update (block path): seeded write tables run in rotation")
     ap.add_argument("--updio-same-tables", action="store_true", help=argparse.SUPPRESS)  # (diagnostics: one draw)
     ap.add_argument("--updio-headline-only", action="store_true", help=argparse.SUPPRESS)  # (diagnostics: timed leg only)
     ap.add_argument("--sync-threads", type=int, default=32)
