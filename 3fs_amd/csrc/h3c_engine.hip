@@ -663,8 +663,20 @@ __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(Src src, const u
       if (pad >> 4) v = dgf_mul(v, pc->fix[4 * (pad >> 4)], poly);
       if (pad & 15) v = dgf_mul(v, pc->fixz[pad & 15], poly);
       if (shift) v = dgf_mul_fast(v, dxpow8_fast(shift, pc, poly), poly);
-      atomicXor(&crc0_out[op], v);
     }
+    // The step's NG pieces are consecutive, so their items never decrease: the pieces of one item form a run of
+    // groups, XORed together (a suffix scan over the groups) and sent by the run's first group as one atomic.
+    // (A 64 MiB chunk is 16,384 pieces: one atomic each on one address serialised the pass, ~3.4 ms for 4 GiB.)
+    uint32_t x = gl == 0 && valid ? v : 0u;
+    const uint32_t myop = valid ? op : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t d = 1; d < (uint32_t)NG; d <<= 1) {
+      const uint32_t xo = (uint32_t)__shfl_down((int)x, G * d, 64);
+      const uint32_t oo = (uint32_t)__shfl_down((int)myop, G * d, 64);
+      if (grp + d < (uint32_t)NG && oo == myop) x ^= xo;
+    }
+    const uint32_t prev_op = (uint32_t)__shfl_up((int)myop, G, 64);
+    if (gl == 0 && valid && (grp == 0 || prev_op != myop)) atomicXor(&crc0_out[op], x);
   }
 }
 

@@ -2870,7 +2870,9 @@ constexpr uint32_t kAMaxOps = (1u << 24) - 2;  // bucket entries: epoch << 24 | 
 // cut in ticket order, each sized by its class's weight); [kAW, +8) the range weight of each workgroup class
 // (blockIdx % 8, one XCD each: 16.16 fixed point, 0 = 1.0), learnt from the previous batch's per-class
 // throughput (the stat records) by uio_aprep_kernel's first workgroup
-enum { kAEpoch = 0, kADone = 2, kASlow = 3, kADefer = 4, kAAcc = 8, kAW = 16, kACtlWords = 64 };
+// [kAHas, +8): exact mode's chunks that some op of the batch writes, one 128-bit set per epoch parity (set by
+// uio_aprep_kernel; the batch's last workgroup clears the other parity's set for the next batch)
+enum { kAEpoch = 0, kADone = 2, kASlow = 3, kADefer = 4, kAAcc = 8, kAW = 16, kAHas = 32, kACtlWords = 64 };
 constexpr uint32_t kAClasses = 8;
 constexpr uint32_t kAOne = 1u << 16;  // weight 1.0
 __device__ uint32_t g_aw_seed[kAClasses];  // the device's last learnt weights (0: none yet), seeding new scratches
@@ -2901,6 +2903,8 @@ struct AlignedArgs {
   uint32_t *stat;                 // per ticket (FastScratch): {epoch << 8 | class, ops, wall-clock ticks of its ops}
   uint32_t *hand;                 // per op (FastScratch; epoch-tagged): the hand-over word of a block's last op
                                   //  between it and the block's first op (kHandRead / kHandPending)
+  const uint32_t *crc0;           // H3C_UPD_EXACT: each chunk's crc0 of its bytes before the batch (the piece
+                                  //  pass), t0 from the bytes; null: the stored checksums are trusted
 };
 
 // An op the aligned sub-branch takes: a fast-branch op (fast_op) that writes one whole 4 KiB block at a
@@ -2916,6 +2920,32 @@ __device__ __forceinline__ bool aentry_valid(uint32_t e, uint32_t E) { return (e
 // raw = crc0(data) ^ ~0 * x^(8 * 4096); the std domain's value is ~raw)
 __device__ __forceinline__ uint32_t aexpect(uint32_t value, uint32_t std_domain, uint32_t k4096) {
   return (std_domain ? ~value : value) ^ k4096;
+}
+// A chunk's base checksum t0 (raw domain): its stored value, or in exact mode the CRC of its bytes (fast_t0)
+__device__ __forceinline__ uint32_t at0(const h3c_chunk_state &cs, uint32_t c, const AlignedArgs &aa,
+                                        uint32_t std_domain, const PolyConsts *__restrict__ pc) {
+  return fast_t0(cs, c, aa.crc0 ? 1u : 0u, std_domain, aa.crc0, pc);
+}
+// exact mode: whether some op of the batch (epoch E) writes chunk c
+__device__ __forceinline__ bool ahas(const AlignedArgs &aa, uint32_t E, uint32_t c) {
+  return (aa.ctl[kAHas + 4 * (E & 1u) + (c >> 5)] >> (c & 31u)) & 1u;
+}
+
+// Exact mode's piece table for the aligned sub-branch: the chunks' bytes only, as items 0..C-1 of a piece pass
+// with no payload items (the ops' payloads are CRC'd by uio_afused_kernel itself; a piece then finds its item
+// in a table of C + 1 entries), its total, and the chunks' crc0 accumulators zeroed.  One thread.
+__global__ void uio_apiece_kernel(const h3c_chunk_state *__restrict__ chunks, uint32_t nchunks, uint8_t poly_type,
+                                  uint32_t *__restrict__ pbase, uint32_t *__restrict__ total, uint32_t *__restrict__ crc0) {
+  if (threadIdx.x != 0) return;
+  const uint32_t C = nchunks ? nchunks : 1u;
+  uint32_t acc = 0;
+  for (uint32_t c = 0; c < C; ++c) {
+    pbase[c] = acc;
+    crc0[c] = 0;
+    if (c < nchunks && needs_init(chunks[c], poly_type, 1u)) acc += (chunks[c].size + kPieceBytes - 1) / kPieceBytes;
+  }
+  pbase[C] = acc;
+  *total = acc;
 }
 
 __global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *__restrict__ ios, uint32_t n,
@@ -2975,10 +3005,12 @@ __global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *
     }
     return;
   }
+  __shared__ uint32_t s_has[4];
   for (uint32_t e = t; e < 2 * kATile; e += kATile) {
     g_key[e] = kNoKey;
     g_head[e] = kNil;
   }
+  if (t < 4) s_has[t] = 0;
   __syncthreads();
   unsigned long long key = kNoKey;
   bool q = false;
@@ -2989,6 +3021,7 @@ __global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *
     const uint32_t st = op_status(io, cs, nchunks, poly_type, std_domain);
     q = c < kFastChunksLds && aligned_op(io, cs, st, poly_type);
     if (q) key = ((unsigned long long)c << 36) | ((cs.base + io.offset) >> 12);
+    if (q && aa.crc0) atomicOr(&s_has[c >> 5], 1u << (c & 31u));
     aa.key[i] = key;
   }
   if (__syncthreads_or(i < n && !q) && t == 0) st_agent(&aa.ctl[kASlow], 0x100u | E);
@@ -3003,6 +3036,7 @@ __global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *
     g_nx[t] = atomicExch(&g_head[h], t);
   }
   __syncthreads();
+  if (aa.crc0 && t < 4 && s_has[t]) atomicOr(&aa.ctl[kAHas + 4 * (E & 1u) + t], s_has[t]);
   if (i >= n) return;
   uint32_t pin = kNil;
   bool last = true;
@@ -3043,6 +3077,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   __shared__ h3c_chunk_state s_cs[kFastChunksLds];
   __shared__ uint32_t s_ticket, s_E, s_slow, s_last, s_void, s_prev, s_grab, s_wlo, s_whi;
   __shared__ uint32_t s_agg[kFastCols];  // the workgroup's per-chunk XOR of its ops' deltas at their chunks' ends
+  __shared__ uint32_t s_stale;           // (the last workgroup, exact mode: chunks whose stored value is stale)
   __shared__ uint64_t s_t_start;
   const uint32_t t = threadIdx.x, lane = t & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -3078,6 +3113,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   }
   if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
   if (t < kFastCols) s_agg[t] = 0;
+  if (t == 0) s_stale = 0;
   // the CRC tables fill while thread 0 takes the ticket (waves 1-15; they do not depend on the range)
   if (t >= 64) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t - 64, kBlkThreads - 64);
   __syncthreads();
@@ -3102,6 +3138,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
       st_agent(reinterpret_cast<unsigned long long *>(aa.ctl + kAAcc), 0ull);
       st_agent(&aa.ctl[kADone], 0u);
       st_agent(&aa.ctl[kAEpoch], (E + 1) & 0xFFu);
+      for (uint32_t k = 0; k < 4; ++k) st_agent(&aa.ctl[kAHas + 4 * ((E + 1) & 1u) + k], 0u);
       misc[kMiscFast] = outcome;
       stores_done();
       if (hout) fast_outcome_to_host(misc, hout, outcome);
@@ -3356,9 +3393,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     }
   };
   // the chunks' base checksums (trusted stored values), one per lane (chunks lane, lane + 64)
-  auto t0_of = [&](uint32_t c) -> uint32_t {
-    return c < nchunks ? (std_domain ? ~s_cs[c].value : s_cs[c].value) : 0u;
-  };
+  auto t0_of = [&](uint32_t c) -> uint32_t { return c < nchunks ? at0(s_cs[c], c, aa, std_domain, pc) : 0u; };
   const uint32_t rb0 = t0_of(lane), rb1 = t0_of(64 + lane);
   // ---- chunk aggregates: waves of the workgroup (LDS), then workgroups (look-back in ticket order) ----
   uint32_t *wagg = lds;                                 // [16][128]
@@ -3467,17 +3502,22 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   // :389, or copy_on_write, chunk.rs:153; uio_afix_kernel writes them for a void pass)
   if (t < kCtrN) ctr[t] = !vd && t == (std_domain ? kCtrRecalc : kCtrRead) ? n : 0u;
   if (t == 0) *reinterpret_cast<unsigned long long *>(misc + kMiscT1) = wall_clock64();
-  if (t < nchunks && !vd) {
+  if (t < nchunks && !vd) {  // (exact mode: a chunk no op writes keeps its stored value, stale or not)
     const unsigned long long g = ld_agent(&aa.gran[(uint64_t)(nwg - 1) * kFastCols + t]);
     const uint32_t a = (uint32_t)g;
     h3c_chunk_state f = s_cs[t];
-    const uint32_t t0 = std_domain ? ~f.value : f.value;
-    f.value = std_domain ? ~(t0 ^ a) : (t0 ^ a);
+    const uint32_t t0 = at0(f, t, aa, std_domain, pc);
+    if (aa.crc0 && f.size && f.type == poly_type && t0 != (std_domain ? ~f.value : f.value)) atomicAdd(&s_stale, 1u);
+    if (!aa.crc0 || ahas(aa, E, t)) {
+      f.value = std_domain ? ~(t0 ^ a) : (t0 ^ a);
+      f.type = poly_type;
+    }
     chunks_out[t] = f;
     if (commit) commit[t] = f;
   }
   stores_done();
   __syncthreads();
+  if (t == 0 && !vd && aa.crc0) ctr[kCtrStale] = s_stale;
   finish(vd ? kFastVoid : kFastDone);
 }
 
@@ -3494,7 +3534,7 @@ __global__ __launch_bounds__(1024) void uio_afix_kernel(const h3c_update_io *__r
                                                         unsigned long long *__restrict__ ctr,
                                                         h3c_chunk_state *commit) {
   __shared__ uint32_t wagg[16][kFastCols], run[kFastCols], t0s[kFastCols], szs[kFastCols];
-  __shared__ unsigned int cnt_ok, cnt_bad;
+  __shared__ unsigned int cnt_ok, cnt_bad, app[kFastCols], stale;
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, poly = pc->poly;
   // 1. deferred blocks, one wave each: walk back from the block's last op to the last one that passed
   const uint32_t nd = aa.ctl[kADefer];
@@ -3520,10 +3560,11 @@ __global__ __launch_bounds__(1024) void uio_afix_kernel(const h3c_update_io *__r
   }
   if (t < kFastCols) {
     run[t] = 0;
-    t0s[t] = t < nchunks ? (std_domain ? ~chunks[t].value : chunks[t].value) : 0u;
+    app[t] = 0;
+    t0s[t] = t < nchunks ? at0(chunks[t], t, aa, std_domain, pc) : 0u;
     szs[t] = t < nchunks ? chunks[t].size : 0u;
   }
-  if (t == 0) cnt_ok = cnt_bad = 0;
+  if (t == 0) cnt_ok = cnt_bad = stale = 0;
   __syncthreads();
   // 2. every op's shifted delta, the per-chunk XORs in sequence order, the results
   for (uint32_t b = 0; b < n; b += 1024) {
@@ -3548,6 +3589,7 @@ __global__ __launch_bounds__(1024) void uio_afix_kernel(const h3c_update_io *__r
         const uint32_t sh = dxpow8_fast((int64_t)szs[c] - (int64_t)io.offset - (int64_t)kBlk, pc, poly);
         v = dgf_mul(aa.pv[j].x ^ old, sh, poly);
         atomicAdd(&cnt_ok, 1u);
+        if (c < kFastCols) atomicOr(&app[c], 1u);
       } else {
         atomicAdd(&cnt_bad, 1u);
       }
@@ -3582,9 +3624,13 @@ __global__ __launch_bounds__(1024) void uio_afix_kernel(const h3c_update_io *__r
     }
     __syncthreads();
   }
-  if (t < nchunks) {
+  if (t < nchunks) {  // (exact mode: a chunk with no applied op keeps its stored value)
     h3c_chunk_state f = chunks[t];
-    f.value = std_domain ? ~(t0s[t] ^ run[t]) : (t0s[t] ^ run[t]);
+    if (aa.crc0 && f.size && f.type == poly_type && t0s[t] != (std_domain ? ~f.value : f.value)) atomicAdd(&stale, 1u);
+    if (!aa.crc0 || app[t]) {
+      f.value = std_domain ? ~(t0s[t] ^ run[t]) : (t0s[t] ^ run[t]);
+      f.type = poly_type;
+    }
     chunks_out[t] = f;
     if (commit) commit[t] = f;
   }
@@ -3593,6 +3639,7 @@ __global__ __launch_bounds__(1024) void uio_afix_kernel(const h3c_update_io *__r
     for (int k = 0; k < kCtrN; ++k) ctr[k] = 0;
     ctr[std_domain ? kCtrRecalc : kCtrRead] = cnt_ok;
     ctr[kCtrMismatch] = cnt_bad;
+    if (aa.crc0) ctr[kCtrStale] = stale;
     aa.ctl[kADefer] = 0;
     misc[kMiscFast] = kFastDone;
   }
@@ -4142,7 +4189,8 @@ struct ArgLayout<AlignedArgs, void> {
                                 offsetof(AlignedArgs, key), offsetof(AlignedArgs, link), offsetof(AlignedArgs, dv),
                                 offsetof(AlignedArgs, pv), offsetof(AlignedArgs, inp), offsetof(AlignedArgs, defer),
                                 offsetof(AlignedArgs, rec), offsetof(AlignedArgs, pr),
-                                offsetof(AlignedArgs, stat), offsetof(AlignedArgs, hand)});
+                                offsetof(AlignedArgs, stat), offsetof(AlignedArgs, hand),
+                                offsetof(AlignedArgs, crc0)});
   }
 };
 template <>
@@ -4177,7 +4225,7 @@ const std::vector<h3c_rt::KernelSig> &capturable_kernels() {
       H3C_SIG(uio_elem_kernel<SMapFn>), H3C_SIG(uio_result_kernel), H3C_SIG(uio_stale_kernel),
       H3C_SIG(uio_commit_kernel), H3C_SIG(uio_fast_link_kernel), H3C_SIG(uio_fast_kernel),
       H3C_SIG(uio_fast_sum_kernel), H3C_SIG(uio_fast_res_kernel), H3C_SIG(uio_aprep_kernel),
-      H3C_SIG(uio_afused_kernel), h3c_rt::uio_piece_kernel_sig(),
+      H3C_SIG(uio_afused_kernel), H3C_SIG(uio_apiece_kernel), h3c_rt::uio_piece_kernel_sig(),
 #undef H3C_SIG
   };
   return sigs;
@@ -4460,7 +4508,7 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
   // every op may be a full aligned 4 KiB WRITE (trusted stored checksums), unless this thread's last batch of
   // the shape had an op it does not take (test hook H3C_HOOK_UPD_ALIGNED: 1 never, 2 always tried)
   const uint64_t aligned_hook = h3c_rt::hook(H3C_HOOK_UPD_ALIGNED);
-  const bool try_aligned = fast_able && !exact && n <= kAMaxOps && aligned_hook != 1 &&
+  const bool try_aligned = fast_able && n <= kAMaxOps && aligned_hook != 1 &&
                            (aligned_hook == 2 || !fpred->aslow || fpred->a_runs >= kFastRetry);
   AlignedArgs aa{};
   const uint32_t nwg_fast = (uint32_t)std::max(1, h3c_rt::device_num_cu(dev)) * H3C_FAST_WG_MULT;
@@ -4714,7 +4762,16 @@ int update_core(uint8_t poly_type, const h3c_chunk_state *d_chunks, h3c_chunk_st
     }
     // (test hook H3C_HOOK_UPD_GIVEUP bit 3: ticket 1 gives up its look-back; bit 4: the pass reports itself void)
     const uint32_t force_void = ((giveup & 8) ? 1u : 0u) | ((giveup & 16) ? 2u : 0u);
+    aa.crc0 = exact ? d_paycrc0 + n : nullptr;
     auto a_launch = [&](hipStream_t q) -> int {
+      if (exact) {  // t0 from the bytes: the chunks' CRCs before uio_afused_kernel writes them
+        hipLaunchKernelGGL(uio_apiece_kernel, dim3(1), dim3(64), 0, q, d_chunks, nchunks, poly_type, d_pbase,
+                           d_sstate + 2, d_paycrc0 + n);
+        HIP_TRY(hipGetLastError());
+        const int r = h3c_rt::launch_uio_piece_crc(q, dev, poly_type, d_ios, 0u, d_chunks, nchunks, d_pbase, d_sstate + 2,
+                                                   d_paycrc0 + n, nullptr, kPrepTile, d_misc + kMiscErr);
+        if (r) return r;
+      }
       hipLaunchKernelGGL(uio_aprep_kernel, dim3((n + kATile - 1) / kATile + 1), dim3(kATile), 0, q, d_ios, n, d_chunks,
                          nchunks, poly_type, stdf, d_misc, d_ctr, aa);
       HIP_TRY(hipGetLastError());

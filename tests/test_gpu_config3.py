@@ -3,9 +3,9 @@
 100k random 4 KiB WRITE UpdateIOs into 64 x 64 MiB chunks (h3c_update_ios_dev, tables in HBM),
 trusted and exact, each run once through the general pipeline (h3c_test_hook(H3C_HOOK_UPD_FAST, 1):
 prep, sort, piece pass, front, block and phase-B kernels), once through the chain-based fast branch
-(FAST 2, H3C_HOOK_UPD_ALIGNED 1: prep, link, uio_fast_kernel and its tail) and, trusted, once through
-the aligned sub-branch (ALIGNED 2: uio_aprep_kernel + uio_afused_kernel); the engine's diag counters
-must say which one ran.  The
+(FAST 2, H3C_HOOK_UPD_ALIGNED 1: prep, link, uio_fast_kernel and its tail) and once through the
+aligned sub-branch (ALIGNED 2: uio_aprep_kernel + uio_afused_kernel; exact mode adds the chunks' piece
+pass first); the engine's diag counters must say which one ran.  The
 reference semantics replaced are ChunkReplica::update + updateChecksum
 (src/storage/store/ChunkReplica.cc:131-394).  What is checked against the CPU oracle
 (oracle/crc_oracle.c), not against another GPU pass (the oracle side is computed once per mode and
@@ -24,9 +24,8 @@ shared by both branches):
 
 In exact mode 4 chunks start with stale stored checksums (two of them replayed op by op): the
 reference's case (iv) re-reads the bytes, so the first op on such a chunk heals it (the delta chain
-therefore starts from each chunk's true CRC in both modes).  Exact mode never takes the aligned
-sub-branch (it trusts stored checksums): with the aligned branch forced, an exact batch must be routed
-to the chain-based fast branch without an aligned attempt, and still match every op.
+therefore starts from each chunk's true CRC in both modes).  Since round 6 the aligned sub-branch takes
+exact batches too: t0 from the chunks' bytes, every op and the stale count as the other branches.
 """
 import numpy as np
 import pytest
@@ -154,9 +153,8 @@ def test_updio_config3_full_shape_against_oracle(h3c, torch_dev, hooks, exact, b
     h3c.update_ios_dev(d_state, d_ios, d_res, exact=exact, counters=d_ctr)
     torch.cuda.synchronize()
     diag = {k: v - before[k] for k, v in h3c.diag_counters().items()}
-    # the branch that ran is the branch named, with no redo of any kind; exact mode is never tried
-    # on the aligned sub-branch, even when it is forced, and takes the chain-based branch instead
-    took_aligned = branch == "aligned" and not exact
+    # the branch that ran is the branch named, with no redo of any kind
+    took_aligned = branch == "aligned"
     assert diag["fast_batches"] == (0 if branch == "general" else 1), diag
     assert diag["aligned_batches"] == (1 if took_aligned else 0), diag
     assert diag["fast_abandoned"] == 0 and diag["fast_recovered"] == 0, diag

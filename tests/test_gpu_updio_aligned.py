@@ -82,9 +82,9 @@ def check_modes(h3c, hooks, sc, expect_aligned=True, recovered=None, **kw):
 
 
 def aligned_scenario(h3c, torch, dev, rng, nchunks, chunk_size, nops, bad=0.0, hot_blocks=None, type_=orc.CRC32C,
-                     full_size=True):
+                     full_size=True, stale=0.0):
     sc = fast_scenario(h3c, torch, dev, rng, nchunks=nchunks, chunk_size=chunk_size, nops=nops, aligned=1.0, bad=bad,
-                       hot_blocks=hot_blocks, type_=type_, full_size=full_size)
+                       hot_blocks=hot_blocks, type_=type_, full_size=full_size, stale=stale)
     sc.pay_align = 16
     return sc
 
@@ -107,6 +107,35 @@ def test_aligned_failed_checks_recovered(h3c, torch_dev, hooks, bad, dev_api):
     rng = np.random.default_rng(int(bad * 100) + 7 * dev_api)
     sc = aligned_scenario(h3c, torch, dev, rng, nchunks=8, chunk_size=64 << 10, nops=2500, bad=bad, hot_blocks=6)
     check_modes(h3c, hooks, sc, recovered=1, dev_api=dev_api)
+
+
+@pytest.mark.parametrize("stale", [0.0, 0.6])
+@pytest.mark.parametrize("dev_api", [False, True])
+def test_aligned_exact_mode(h3c, torch_dev, hooks, stale, dev_api):
+    """H3C_UPD_EXACT on the aligned sub-branch: t0 from the chunks' bytes (uio_apiece_kernel + the piece
+    pass), so a stale stored value is healed by the chunk's first write (case iv re-reads,
+    ChunkReplica.cc:356-390) and counted; against the oracle and both other branches, all exact."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(41 + int(stale * 10) + 3 * dev_api)
+    sc = aligned_scenario(h3c, torch, dev, rng, nchunks=12, chunk_size=128 << 10, nops=2000, stale=stale,
+                          full_size=False)
+    check_modes(h3c, hooks, sc, recovered=0, exact=True, dev_api=dev_api)
+    assert int(sc.counters.stale_chunks) == sc.stale_chunks
+
+
+def test_aligned_exact_mode_untouched_chunks_and_failed_checks(h3c, torch_dev, hooks):
+    """Exact mode with chunks no op writes (they keep their stored values, stale ones included) and, in a
+    second batch, failed A6 checks over hot blocks (a void pass: uio_afix_kernel recomputes in exact mode)."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(47)
+    sc = aligned_scenario(h3c, torch, dev, rng, nchunks=16, chunk_size=64 << 10, nops=24, stale=0.7)
+    check_modes(h3c, hooks, sc, recovered=0, exact=True)
+    assert int(sc.counters.stale_chunks) == sc.stale_chunks
+    rng = np.random.default_rng(48)
+    sc = aligned_scenario(h3c, torch, dev, rng, nchunks=8, chunk_size=64 << 10, nops=2500, bad=0.2, hot_blocks=6,
+                          stale=0.5)
+    check_modes(h3c, hooks, sc, recovered=1, exact=True)
+    assert int(sc.counters.stale_chunks) == sc.stale_chunks
 
 
 def test_aligned_hot_blocks_chains_across_tiles(h3c, torch_dev, hooks):
