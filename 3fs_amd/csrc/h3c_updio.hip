@@ -3114,9 +3114,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
   if (t < kFastCols) s_agg[t] = 0;
   if (t == 0) s_stale = 0;
-  // the CRC tables fill while thread 0 takes the ticket (waves 1-15; they do not depend on the range)
-  if (t >= 64) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t - 64, kBlkThreads - 64);
-  __syncthreads();
+  __syncthreads();  // (the ticket; the CRC tables fill beside phase 0, below)
   const uint32_t E = s_E, L = s_ticket, nwg = gridDim.x;
 #if H3C_AF_TRACE
   if (t < 16 && L < 1024) g_af_fin[16 * L + t] = 0;
@@ -3161,7 +3159,12 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
   // previous op of its block: in its tile, else the last listed one of an earlier tile; none: the block
   // itself, and the op writes the block back -- with the block's last op's bytes), its A6 expectations;
   // one 32-byte record per op for phase 1's scalar loads ----
-  // (each wave's first op is wlo + wave: its new rows and (speculated) block rows load before the fill)
+  // the CRC tables fill beside phase 0, by the waves its first pass leaves idle (they fill before loading their
+  // first op's rows: vmcnt is counted in order); by every thread after phase 0 when no wave is idle
+  const uint32_t p0w = (wn_ops + 63) / 64;  // waves with ops in phase 0's first pass
+  if (p0w < kBlkWaves && wave >= p0w)
+    fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t - 64 * p0w, kBlkThreads - 64 * p0w);
+  // (each wave's first op is wlo + wave: its new rows and (speculated) block rows load before phase 0)
   uint4 vn[4], vo[4];
   const uint32_t j0 = wlo + wave;
   uint64_t spec_old = 0;
@@ -3209,6 +3212,7 @@ __global__ __launch_bounds__(kBlkThreads) void uio_afused_kernel(
     aa.rec[2 * (size_t)j + 1] = make_uint4((uint32_t)f, (uint32_t)(f >> 32) | (io.chunk << 16), exp, 0u);
     aa.pv[j].y = prev;  // (uio_afix_kernel's input; crc0(new) follows in .x)
   }
+  if (p0w >= kBlkWaves) fill_tables(lds, pc->tab, &pc->red[0][0][0], kRedWords, t, kBlkThreads);
   if (t == 0) s_grab = wlo + kBlkWaves;  // (each wave's first op is wlo + wave)
   stores_done();
   __syncthreads();
