@@ -135,6 +135,27 @@ def test_multi_update_ios_matches_replica_replay(h3c, torch_dev, multi, seed):
     assert sum(units) == len(ios) and min(units) > 0
 
 
+def test_multi_update_ios_exact_aligned_with_stale_chunks(h3c, torch_dev, multi):
+    """H3C_UPD_EXACT through h3c_multi_update_ios: an aligned batch (each worker's share runs the aligned
+    sub-branch after its chunks' piece pass) on chunks whose stored checksums are partly stale; results,
+    states and the summed stale count against the ChunkReplica::update replay."""
+    from test_gpu_updio_aligned import aligned_scenario
+
+    torch, dev = torch_dev
+    rng = np.random.default_rng(61)
+    sc = aligned_scenario(h3c, torch, dev, rng, nchunks=10, chunk_size=128 << 10, nops=1500, stale=0.6,
+                          full_size=False)
+    chunks, ios = sc.device_ios()
+    sc.counters = h3c.UpdateCounters()
+    before = h3c.diag_counters()
+    res = multi.update_ios(chunks, ios, exact=True, counters=sc.counters)
+    torch.cuda.synchronize()
+    diag = {k: v - before[k] for k, v in h3c.diag_counters().items()}
+    sc.check(chunks, res)
+    assert sc.stale_chunks > 0 and int(sc.counters.stale_chunks) == sc.stale_chunks
+    assert diag["aligned_batches"] == 2 and diag["aligned_abandoned"] == 0, diag
+
+
 def test_multi_rejects_payload_on_a_device_it_does_not_drive(h3c, torch_dev):
     """Descriptors on device 0 given to an engine that does not list device 0 cannot be routed: only
     checkable with 2+ GPUs, so here the engine over {0} must accept what {0, 0} accepts."""
