@@ -1282,16 +1282,19 @@ uint64_t pick_seg_for(const h3c_desc *d, size_t n, int num_cu) {
   for (size_t i = 0; i < n; ++i)
     if ((d[i].type == H3C_TYPE_CRC32C || d[i].type == H3C_TYPE_CRC32) && d[i].ptr) total += d[i].len;
   if (total == 0) return kMinSegBytes;
-  uint64_t best = kMinSegBytes;
-  double best_eff = -1;
+  // the segment size whose busiest wave finishes first: ceil(segs / waves) segments of `seg` bytes each,
+  // plus a fixed cost per segment worth ~8 KiB of streaming (its fold and result).  Mixed 64 KiB-64 MiB
+  // batches: 128 KiB (1.326 ms) against the balance-only rule's 64 KiB (1.341 ms), profiles/r06_mixed_seg.txt;
+  // 1 MiB and 4 MiB chunks keep 1 MiB segments
+  constexpr uint64_t kSegCost = 8u << 10;
+  uint64_t best = kMinSegBytes, best_t = ~0ull;
   for (uint64_t seg = kMaxSegBytes; seg >= kMinSegBytes; seg >>= 1) {
     uint64_t segs = 0;
     for (size_t i = 0; i < n; ++i)
       if ((d[i].type == H3C_TYPE_CRC32C || d[i].type == H3C_TYPE_CRC32) && d[i].ptr) segs += (d[i].len + seg - 1) / seg;
-    const double eff = (double)total / ((double)waves * (double)((segs + waves - 1) / waves) * (double)seg);
-    if (eff >= 0.97) return seg;
-    if (eff > best_eff) {
-      best_eff = eff;
+    const uint64_t t = (segs + waves - 1) / waves * (seg + kSegCost);
+    if (t < best_t) {
+      best_t = t;
       best = seg;
     }
   }
