@@ -681,8 +681,7 @@ __global__ __launch_bounds__(kThreads) void op_piece_crc_kernel(Src src, const u
 }
 
 // Kernel B: per chunk, fold segment CRCs, apply start, optionally compare.
-// Chunks with more segments than this are folded by a whole wave (finalize_big_kernel);
-// one thread folding thousands of segments serially took ~1 ms for a 64 MiB chunk.
+// Chunks with more segments than this are folded by a whole wave (finalize_kernel's second mapping).
 constexpr uint32_t kSmallFold = 16;
 
 __device__ __forceinline__ void finalize_store(const DevChunk &ch, uint32_t raw, const uint32_t *__restrict__ expected,
@@ -704,9 +703,20 @@ __device__ __forceinline__ void build_seg_table(uint32_t *T, uint32_t seg_mul, u
   __syncthreads();
 }
 
-// Kernel B: per chunk (one thread), fold segment CRCs, apply start, optionally compare.
+// Kernel B: per chunk, fold segment CRCs, apply start, optionally compare; one launch, two
+// mappings.  Blocks [0, small_blocks): one thread per chunk of <= kSmallFold segments.  The rest:
+// one wave per chunk of more (a thread folding thousands of segments serially took ~1 ms for a
+// 64 MiB chunk): the full segments' CRCs are the coefficients of a polynomial in X =
+// x^(8*seg_bytes); lane j Horner-evaluates q consecutive coefficients (virtual zeros in front are
+// harmless), then six butterfly levels combine lane results with X^(q*2^t); the last segment joins
+// with x^(8r).  Every load a chunk's fold needs (its segment CRCs, the expected value, the X^q
+// factors) is issued before the table build, so the fold's latency is one round trip, not a
+// chain of them.
+constexpr uint32_t kBigBatch = 8;  // segment CRCs a lane loads per round trip
+
 __global__ __launch_bounds__(256) void finalize_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
-                                                       uint32_t total_segs, uint32_t seg_mul, uint32_t need_table,
+                                                       uint32_t total_segs, uint64_t seg_bytes, uint32_t seg_mul,
+                                                       uint32_t need_table, uint32_t small_blocks,
                                                        const PolyConsts *__restrict__ pc,
                                                        const uint32_t *__restrict__ seg_crc,
                                                        const uint32_t *__restrict__ expected,
@@ -714,57 +724,90 @@ __global__ __launch_bounds__(256) void finalize_kernel(const DevChunk *__restric
                                                        uint32_t *__restrict__ mismatch) {
   __shared__ uint32_t T[1024];
   const uint32_t poly = pc->poly;
-  if (need_table) build_seg_table(T, seg_mul, poly);  // only chunks of >= 3 segments use it
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nchunks) return;
-  const DevChunk ch = chunks[i];
-  uint32_t raw = 0;
-  if (!(ch.flags & kFlagNone)) {
-    const uint32_t b = ch.seg_begin;
-    const uint32_t e = (i + 1 < nchunks) ? chunks[i + 1].seg_begin : total_segs;
-    if (e - b > kSmallFold) return;  // finalize_big_kernel's
-    uint32_t crc0 = 0;
-    if (e > b) {
-      crc0 = seg_crc[b];
-      for (uint32_t s = b + 1; s + 1 < e; ++s) crc0 = tab_mul(crc0, T) ^ seg_crc[s];  // full segments
-      if (e - b >= 2) crc0 = dgf_mul(crc0, ch.xlast, poly) ^ seg_crc[e - 1];          // the last one
+  if (blockIdx.x < small_blocks) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    DevChunk ch{};
+    uint32_t m = 0, sc[kSmallFold], last = 0, ex = 0;
+    bool mine = false;
+    if (i < nchunks) {
+      ch = chunks[i];
+      const uint32_t e = (i + 1 < nchunks) ? chunks[i + 1].seg_begin : total_segs;
+      m = e - ch.seg_begin;
+      mine = m <= kSmallFold || (ch.flags & kFlagNone);  // (else the wave mapping's)
+      if (mine && !(ch.flags & kFlagNone)) {
+#pragma unroll
+        for (uint32_t t = 0; t < kSmallFold; ++t) sc[t] = t + 1 < m ? seg_crc[ch.seg_begin + t] : 0u;
+        if (m) last = seg_crc[e - 1];
+      }
+      if (mine && expected) ex = expected[ch.out_idx];
     }
-    raw = crc0 ^ ch.xstart;
+    if (need_table) build_seg_table(T, seg_mul, poly);  // only chunks of >= 3 segments use it
+    if (!mine) return;
+    uint32_t raw = 0;
+    if (!(ch.flags & kFlagNone)) {
+      uint32_t crc0 = 0;
+      if (m == 1) crc0 = last;
+      if (m >= 2) {
+        crc0 = sc[0];
+#pragma unroll
+        for (uint32_t t = 1; t + 1 < kSmallFold; ++t)
+          if (t + 1 < m) crc0 = tab_mul(crc0, T) ^ sc[t];  // full segments
+        crc0 = dgf_mul(crc0, ch.xlast, poly) ^ last;       // the last one
+      }
+      raw = crc0 ^ ch.xstart;
+    }
+    out_raw[ch.out_idx] = raw;
+    if (expected) {
+      const bool good = raw == ex;
+      ok[ch.out_idx] = good ? 1 : 0;
+      if (!good && mismatch) atomicAdd(mismatch, 1u);
+    }
+    return;
   }
-  finalize_store(ch, raw, expected, out_raw, ok, mismatch);
-}
-
-// Kernel B': one wave per chunk with > kSmallFold segments.  The full segments' CRCs are
-// the coefficients of a polynomial in X = x^(8*seg_bytes): lane j Horner-evaluates q
-// consecutive coefficients (virtual zeros in front are harmless), then six butterfly
-// levels combine lane results with X^(q*2^t); the last segment joins with x^(8r).
-__global__ __launch_bounds__(256) void finalize_big_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
-                                                           uint32_t total_segs, uint64_t seg_bytes, uint32_t seg_mul,
-                                                           const PolyConsts *__restrict__ pc,
-                                                           const uint32_t *__restrict__ seg_crc,
-                                                           const uint32_t *__restrict__ expected,
-                                                           uint32_t *__restrict__ out_raw, uint8_t *__restrict__ ok,
-                                                           uint32_t *__restrict__ mismatch) {
-  __shared__ uint32_t T[1024];
-  const uint32_t poly = pc->poly;
-  build_seg_table(T, seg_mul, poly);
-  const uint32_t i = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint32_t i = __builtin_amdgcn_readfirstlane((blockIdx.x - small_blocks) * (blockDim.x / 64) + (threadIdx.x >> 6));
   const uint32_t j = threadIdx.x & 63;
-  if (i >= nchunks) return;
-  const DevChunk ch = chunks[i];
-  if (ch.flags & kFlagNone) return;
-  const uint32_t b = ch.seg_begin;
-  const uint32_t e = (i + 1 < nchunks) ? chunks[i + 1].seg_begin : total_segs;
-  const uint32_t m = e - b;
-  if (m <= kSmallFold) return;
-  const uint32_t q = (m - 1 + 63) / 64;
-  const int64_t k0 = (int64_t)(m - 1) - (int64_t)(64 - j) * q;
-  uint32_t h = 0;
-  for (uint32_t t = 0; t < q; ++t) {
-    const int64_t k = k0 + t;
-    h = tab_mul(h, T) ^ (k >= 0 ? seg_crc[b + (uint32_t)k] : 0u);
+  DevChunk ch{};
+  uint32_t b = 0, m = 0, q = 0, last = 0, ex = 0, ya = kOne, yb = kOne;
+  uint32_t sc[kBigBatch];
+  int64_t k0 = 0;
+  bool mine = false;
+  if (i < nchunks) {
+    ch = chunks[i];
+    b = ch.seg_begin;
+    const uint32_t e = (i + 1 < nchunks) ? chunks[i + 1].seg_begin : total_segs;
+    m = e - b;
+    mine = m > kSmallFold && !(ch.flags & kFlagNone);
   }
-  uint32_t Y = dxpow8n((uint64_t)q * seg_bytes, pc, poly);
+  if (mine) {
+    q = (m - 1 + 63) / 64;
+    k0 = (int64_t)(m - 1) - (int64_t)(64 - j) * q;
+#pragma unroll
+    for (uint32_t t = 0; t < kBigBatch; ++t) sc[t] = t < q && k0 + t >= 0 ? seg_crc[b + (uint32_t)(k0 + t)] : 0u;
+    last = seg_crc[b + m - 1];
+    if (expected) ex = expected[ch.out_idx];
+    const uint64_t e8 = (uint64_t)q * seg_bytes;  // X^q = x^(8 e8): two table words, one multiply
+    if (e8 < (1ull << 26)) {
+      ya = pc->x4k[e8 >> 12];
+      yb = pc->xb[e8 & 4095];
+    }
+  }
+  build_seg_table(T, seg_mul, poly);
+  if (!mine) return;
+  uint32_t h = 0;
+  for (uint32_t t0 = 0; t0 < q; t0 += kBigBatch) {
+    if (t0) {
+#pragma unroll
+      for (uint32_t t = 0; t < kBigBatch; ++t) {
+        const int64_t k = k0 + t0 + t;
+        sc[t] = t0 + t < q && k >= 0 ? seg_crc[b + (uint32_t)k] : 0u;
+      }
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < kBigBatch; ++t)
+      if (t0 + t < q) h = tab_mul(h, T) ^ sc[t];
+  }
+  const uint64_t e8 = (uint64_t)q * seg_bytes;
+  uint32_t Y = e8 < (1ull << 26) ? dgf_mul_fast(ya, yb, poly) : dxpow8n(e8, pc, poly);
 #pragma unroll
   for (int t = 0; t < 6; ++t) {
     const uint32_t other = __shfl_down(h, 1u << t, 64);
@@ -772,9 +815,13 @@ __global__ __launch_bounds__(256) void finalize_big_kernel(const DevChunk *__res
     Y = dgf_mul(Y, Y, poly);
   }
   if (j == 0) {
-    const uint32_t crc0 = dgf_mul(h, ch.xlast, poly) ^ seg_crc[b + m - 1];
-    const uint32_t raw = crc0 ^ ch.xstart;
-    finalize_store(ch, raw, expected, out_raw, ok, mismatch);
+    const uint32_t raw = (dgf_mul(h, ch.xlast, poly) ^ last) ^ ch.xstart;
+    out_raw[ch.out_idx] = raw;
+    if (expected) {
+      const bool good = raw == ex;
+      ok[ch.out_idx] = good ? 1 : 0;
+      if (!good && mismatch) atomicAdd(mismatch, 1u);
+    }
   }
 }
 
@@ -1155,15 +1202,10 @@ int launch_crc(hipStream_t st, int dev, int type, const DevChunk *d_chunks, uint
   if (fin) return H3C_OK;
   const uint32_t seg_mul = hxpow8n(seg_bytes, poly);
   const uint32_t fb = (nchunks + 255) / 256;
-  hipLaunchKernelGGL(finalize_kernel, dim3(fb), dim3(256), 0, st, d_chunks, nchunks, total_segs, seg_mul,
-                     max_chunk_segs >= 3 ? 1u : 0u, pc, d_segcrc, expected, out_raw, ok, mismatch);
+  const uint32_t bb = max_chunk_segs > kSmallFold ? (nchunks + 3) / 4 : 0;  // 4 waves (chunks) per block
+  hipLaunchKernelGGL(finalize_kernel, dim3(fb + bb), dim3(256), 0, st, d_chunks, nchunks, total_segs, seg_bytes,
+                     seg_mul, max_chunk_segs >= 3 ? 1u : 0u, fb, pc, d_segcrc, expected, out_raw, ok, mismatch);
   HIP_TRY(hipGetLastError());
-  if (max_chunk_segs > kSmallFold) {
-    const uint32_t bb = (nchunks + 3) / 4;  // 4 waves (chunks) per 256-thread block
-    hipLaunchKernelGGL(finalize_big_kernel, dim3(bb), dim3(256), 0, st, d_chunks, nchunks, total_segs, seg_bytes,
-                       seg_mul, pc, d_segcrc, expected, out_raw, ok, mismatch);
-    HIP_TRY(hipGetLastError());
-  }
   return H3C_OK;
 }
 
