@@ -708,10 +708,11 @@ __device__ __forceinline__ void build_seg_table(uint32_t *T, uint32_t seg_mul, u
 // one wave per chunk of more (a thread folding thousands of segments serially took ~1 ms for a
 // 64 MiB chunk): the full segments' CRCs are the coefficients of a polynomial in X =
 // x^(8*seg_bytes); lane j Horner-evaluates q consecutive coefficients (virtual zeros in front are
-// harmless), then six butterfly levels combine lane results with X^(q*2^t); the last segment joins
-// with x^(8r).  Every load a chunk's fold needs (its segment CRCs, the expected value, the X^q
-// factors) is issued before the table build, so the fold's latency is one round trip, not a
-// chain of them.
+// harmless), multiplies its sum by its own shift X^(q*(63-j)) * x^(8r) (r the last segment's
+// length; two table words and one multiply), and the lanes XOR-reduce: two multiplies on the
+// critical path where a butterfly over the lanes takes twelve.  Every load a chunk's fold needs
+// (its segment CRCs, the expected value, the lane's shift words) is issued before the table
+// build, so the fold's latency is one round trip, not a chain of them.
 constexpr uint32_t kBigBatch = 8;  // segment CRCs a lane loads per round trip
 
 __global__ __launch_bounds__(256) void finalize_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
@@ -785,8 +786,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(const DevChunk *__restric
     for (uint32_t t = 0; t < kBigBatch; ++t) sc[t] = t < q && k0 + t >= 0 ? seg_crc[b + (uint32_t)(k0 + t)] : 0u;
     last = seg_crc[b + m - 1];
     if (expected) ex = expected[ch.out_idx];
-    const uint64_t e8 = (uint64_t)q * seg_bytes;  // X^q = x^(8 e8): two table words, one multiply
-    if (e8 < (1ull << 26)) {
+    const uint64_t e8 = (uint64_t)(63 - j) * q * seg_bytes + (ch.len - (uint64_t)(m - 1) * seg_bytes);
+    if (e8 < (1ull << 26)) {  // the lane's shift x^(8 e8): two table words, one multiply
       ya = pc->x4k[e8 >> 12];
       yb = pc->xb[e8 & 4095];
     }
@@ -806,16 +807,12 @@ __global__ __launch_bounds__(256) void finalize_kernel(const DevChunk *__restric
     for (uint32_t t = 0; t < kBigBatch; ++t)
       if (t0 + t < q) h = tab_mul(h, T) ^ sc[t];
   }
-  const uint64_t e8 = (uint64_t)q * seg_bytes;
-  uint32_t Y = e8 < (1ull << 26) ? dgf_mul_fast(ya, yb, poly) : dxpow8n(e8, pc, poly);
+  const uint64_t e8 = (uint64_t)(63 - j) * q * seg_bytes + (ch.len - (uint64_t)(m - 1) * seg_bytes);
+  h = dgf_mul_fast(h, e8 < (1ull << 26) ? dgf_mul_fast(ya, yb, poly) : dxpow8n(e8, pc, poly), poly);
 #pragma unroll
-  for (int t = 0; t < 6; ++t) {
-    const uint32_t other = __shfl_down(h, 1u << t, 64);
-    if ((j & ((2u << t) - 1)) == 0) h = dgf_mul(h, Y, poly) ^ other;
-    Y = dgf_mul(Y, Y, poly);
-  }
+  for (int t = 0; t < 6; ++t) h ^= (uint32_t)__shfl_xor((int)h, 1 << t, 64);
   if (j == 0) {
-    const uint32_t raw = (dgf_mul(h, ch.xlast, poly) ^ last) ^ ch.xstart;
+    const uint32_t raw = (h ^ last) ^ ch.xstart;
     out_raw[ch.out_idx] = raw;
     if (expected) {
       const bool good = raw == ex;

@@ -268,6 +268,28 @@ def test_forced_segment_sizes_and_paths(h3c, torch_dev, seg, dbg, hooks):
     assert [int(x) for x in got] == want
 
 
+@pytest.mark.parametrize("seg", [0, 65536])
+def test_wave_fold_beyond_the_shift_tables(h3c, torch_dev, seg, hooks):
+    """Chunks of > 16 segments are folded by a wave whose lanes shift their Horner sums by x^(8e)
+    from the x4k / xb tables when e < 2^26 and by the square-and-multiply chain beyond: a 72 MiB
+    chunk (1,152 segments of 64 KiB forced; lanes on both sides of 2^26) and ragged neighbours,
+    against the oracle (seg 0: the plan's own segment pick)."""
+    torch, dev = torch_dev
+    if seg:
+        hooks(h3c.HOOK_SEG_BYTES, seg)
+    rng = np.random.default_rng(72 + seg)
+    sizes = [(72 << 20) + 4093, (17 << 20) + 1, (1 << 20) * 3 + 11, 4096, 77]
+    host = rng.integers(0, 256, sum(sizes) + 64, dtype=np.uint8)
+    buf = to_dev(torch, dev, host)
+    items, want, off = [], [], 3
+    for n in sizes:
+        items.append((buf[off: off + n], n))
+        want.append(orc.crc32c(host[off: off + n]))
+        off += n
+    _, got = h3c.batch_create(items)
+    assert [int(x) for x in got] == want
+
+
 @pytest.mark.parametrize("flags", ["0", "2"])
 def test_small_chunk_batches(h3c, torch_dev, hooks, flags):
     """Batches whose every chunk is one short segment run seg_small_kernel (flags 0); flags 2
