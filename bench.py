@@ -669,8 +669,11 @@ def run_updio(args, cx: Ctx) -> dict:
     hctr = h3c.UpdateCounters()
     hsteps = max(1, min(args.steps, 20))
 
+    hn = [0]
+
     def hstep():
-        h3c.update_ios(state, ios, stream=cx.stream, out=hres, exact=exact, counters=hctr)
+        h3c.update_ios(state, tabs[hn[0] % ntab]["ios"], stream=cx.stream, out=hres, exact=exact, counters=hctr)
+        hn[0] += 1
 
     helapsed, _ = cx.timed(hstep, hsteps, min(args.warmup, 2), h3c.engine.PROF_UPDIO)
 
@@ -731,7 +734,7 @@ def run_updio(args, cx: Ctx) -> dict:
                           "check": "final stored checksum == CPU oracle CRC32C of the chunk's bytes after the run"},
         "pcie_inclusive": {"entry": "h3c_update_ios_ex (host tables in pinned memory)",
                            "value": round(nw * hsteps * cx.world / helapsed, 1), "unit": "writes/s",
-                           "ms_per_step": round(helapsed / hsteps * 1e3, 4), "steps": hsteps, "tables": 1},
+                           "ms_per_step": round(helapsed / hsteps * 1e3, 4), "steps": hsteps, "tables": ntab},
         "other_form": {"entry": "h3c_update_ios_dev, " + ("plain launches" if hg else
                                                            "H3C_UPD_GRAPHS: one graph replay per batch"),
                        "value": round(nw * hsteps * cx.world / pelapsed, 1), "unit": "writes/s",
