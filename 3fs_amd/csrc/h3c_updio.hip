@@ -2956,24 +2956,36 @@ __global__ __launch_bounds__(kATile) void uio_aprep_kernel(const h3c_update_io *
   __shared__ h3c_chunk_state s_cs[kFastChunksLds];
   __shared__ unsigned long long g_key[2 * kATile];
   __shared__ uint32_t g_head[2 * kATile], g_nx[kATile];
-  const uint32_t t = threadIdx.x, base = blockIdx.x * kATile, i = base + t;
+  // block 0: the range weights (first dispatched, so its chain of loads does not end the launch); the
+  // ops' tiles are blocks 1..
+  const uint32_t t = threadIdx.x, base = (blockIdx.x - 1u) * kATile, i = blockIdx.x ? base + t : n;
   h3c_update_io io{};
   if (i < n) io = ios[i];
   if (t < nchunks && t < kFastChunksLds) s_cs[t] = chunks[t];
   const uint32_t E = aa.ctl[kAEpoch] & 0xFFu;  // (written by the previous batch's last workgroup)
   if (blockIdx.x == 0 && t < kMiscWords) misc[t] = t == kMiscT0 || t == kMiscT0 + 1 ? 0xFFFFFFFFu : 0u;
   if (blockIdx.x == 0 && t < kCtrN) ctr[t] = 0;
-  if (blockIdx.x == gridDim.x - 1) {  // (a block of its own, no ops) the workgroup classes' range weights from the
-                                      // previous batch's throughput
+  if (blockIdx.x == 0) {  // (a block of its own, no ops) the workgroup classes' range weights from the
+                         // previous batch's throughput
     __shared__ unsigned long long w_ops[kAClasses], w_ticks[kAClasses];
+    static_assert(kAGranRows % kATile == 0, "whole rows per thread");
+    constexpr uint32_t kR = kAGranRows / kATile;
+    uint32_t ra[kR], ro[kR], rt[kR];  // (every row's words loaded before any is used: one round trip)
+#pragma unroll
+    for (uint32_t u = 0; u < kR; ++u) {
+      const uint32_t r = t + u * kATile;
+      ra[u] = aa.stat[3 * r];
+      ro[u] = aa.stat[3 * r + 1];
+      rt[u] = aa.stat[3 * r + 2];
+    }
     if (t < kAClasses) w_ops[t] = w_ticks[t] = 0;
     __syncthreads();
     const uint32_t Ep = (E + 0xFFu) & 0xFFu;  // (the previous batch's epoch)
-    for (uint32_t i = t; i < kAGranRows; i += kATile) {
-      const uint32_t a = aa.stat[3 * i];
-      if ((a >> 8) != Ep || (a & 0xFFu) >= kAClasses) continue;
-      atomicAdd(&w_ops[a & 0xFFu], (unsigned long long)aa.stat[3 * i + 1]);
-      atomicAdd(&w_ticks[a & 0xFFu], (unsigned long long)aa.stat[3 * i + 2]);
+#pragma unroll
+    for (uint32_t u = 0; u < kR; ++u) {
+      if ((ra[u] >> 8) != Ep || (ra[u] & 0xFFu) >= kAClasses) continue;
+      atomicAdd(&w_ops[ra[u] & 0xFFu], (unsigned long long)ro[u]);
+      atomicAdd(&w_ticks[ra[u] & 0xFFu], (unsigned long long)rt[u]);
     }
     __syncthreads();
     if (t == 0) {
