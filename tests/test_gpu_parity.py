@@ -290,6 +290,26 @@ def test_wave_fold_beyond_the_shift_tables(h3c, torch_dev, seg, hooks):
     assert [int(x) for x in got] == want
 
 
+def test_none_type_chunks_among_multi_segment_folds(h3c, torch_dev, hooks):
+    """NONE-type chunks long enough for many segments, beside chunks folded by both finalize mappings
+    (thread per <= 16 segments, wave per more): {NONE, 0} for them, the oracle's value for the rest."""
+    torch, dev = torch_dev
+    hooks(h3c.HOOK_SEG_BYTES, 65536)
+    T = h3c.ChecksumType
+    rng = np.random.default_rng(4242)
+    sizes = [(3 << 20) + 5, (3 << 20) + 5, 700000, 700000, 65536 * 17 + 1, 65536 * 17 + 1, 333]
+    kinds = [T.NONE, T.CRC32C, T.NONE, T.CRC32C, T.NONE, T.CRC32C, T.CRC32C]
+    host = rng.integers(0, 256, sum(sizes) + 64, dtype=np.uint8)
+    buf = to_dev(torch, dev, host)
+    items, want, off = [], [], 1
+    for n, k in zip(sizes, kinds):
+        items.append((buf[off: off + n], n, 0xFFFFFFFF, k))
+        want.append(orc.create(orc.NONE, host[off: off + n].tobytes()) if k == T.NONE else (1, orc.crc32c(host[off: off + n])))
+        off += n
+    t, v = h3c.batch_create(items)
+    assert [(int(a), int(b)) for a, b in zip(t, v)] == want
+
+
 @pytest.mark.parametrize("flags", ["0", "2"])
 def test_small_chunk_batches(h3c, torch_dev, hooks, flags):
     """Batches whose every chunk is one short segment run seg_small_kernel (flags 0); flags 2
