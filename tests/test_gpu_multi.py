@@ -116,6 +116,11 @@ def test_multi_plan_resident_set_with_flips(h3c, torch_dev, multi):
         assert plan.verify(exp) == len(flips)
         assert sorted(np.nonzero(plan.ok == 0)[0].tolist()) == flips
         assert np.array_equal(plan.out, want)
+        # expected values change from call to call: nothing of the previous call's may be seen
+        assert plan.verify(want) == 0 and plan.ok.all()
+        exp = want.copy()
+        exp[[3, 300]] ^= 1
+        assert plan.verify(exp) == 2 and sorted(np.nonzero(plan.ok == 0)[0].tolist()) == [3, 300]
     finally:
         plan.close()
 
