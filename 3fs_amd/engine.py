@@ -800,7 +800,8 @@ class Multi:
 
 class MultiPlan:
     """A resident chunk set (DESC_DTYPE, device memory on the engine's devices) verified repeatedly over
-    every worker (h3c_multi_plan_*): per run only expected values and results cross PCIe."""
+    every worker (h3c_multi_plan_*): per run only expected values and results cross PCIe, read and
+    written in place by the kernels through each worker's pinned mirror."""
 
     def __init__(self, multi: Multi, descs: np.ndarray):
         if descs.dtype != DESC_DTYPE:

@@ -8,7 +8,8 @@ device both workers share).  What each test pins:
 * a mixed batch (device, pinned host through the workers' H2D pipelines, pageable host, NONE,
   null, empty, CRC32) through h3c_multi_batch_create / h3c_multi_verify equals the oracle's
   ChecksumInfo::create (Common.h:146-177) and flags exactly the corrupted expectations;
-* h3c_multi_plan_* (the resync scrub shape, BatchReadJob.cc:43-54) over a resident 1 MiB set;
+* h3c_multi_plan_* (the resync scrub shape, BatchReadJob.cc:43-54) over a resident 1 MiB set and a
+  mixed-size one, results written in place through the workers' pinned mirrors;
 * h3c_multi_update_ios over a random mix of WRITE / TRUNCATE / EXTEND / invalid ops equals the
   ChunkReplica::update replay (ChunkReplica.cc:131-394) op by op, chunk bytes and counters included.
 
@@ -121,6 +122,40 @@ def test_multi_plan_resident_set_with_flips(h3c, torch_dev, multi):
         exp = want.copy()
         exp[[3, 300]] ^= 1
         assert plan.verify(exp) == 2 and sorted(np.nonzero(plan.ok == 0)[0].tolist()) == [3, 300]
+    finally:
+        plan.close()
+
+
+def test_multi_plan_mixed_sizes_in_place(h3c, torch_dev, multi):
+    """A resident set of mixed, ragged, unaligned chunks (one segment each up to many: the segment
+    kernel, both finalize mappings and the small-chunk kernels write their results straight into the
+    workers' pinned mirrors), NONE-type chunks among them, verified three times with changing
+    expectations against the oracle."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(919)
+    sizes = [int(x) for x in rng.choice([777, 4096, 65536 + 3, 300000, (1 << 20) + 11, (3 << 20) - 5, 9 << 20], 160)]
+    kinds = [orc.NONE if i % 13 == 5 else orc.CRC32C for i in range(len(sizes))]
+    host = rng.integers(0, 256, sum(sizes) + 64, dtype=np.uint8)
+    buf = torch.from_numpy(host).to(dev)
+    eng = importlib.import_module("3fs_amd.engine")
+    d = np.zeros(len(sizes), dtype=eng.DESC_DTYPE)
+    offs = 7 + np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    d["ptr"] = np.uint64(buf.data_ptr()) + offs
+    d["len"] = sizes
+    d["start_raw"] = 0xFFFFFFFF
+    d["type"] = kinds
+    d["mem"] = 0
+    want = np.array([orc.create(k, host[o: o + n].tobytes())[1] for k, o, n in zip(kinds, offs.tolist(), sizes)],
+                    dtype=np.uint32)
+    plan = multi.plan(d)
+    try:
+        assert plan.verify(want) == 0 and plan.ok.all() and np.array_equal(plan.out, want)
+        for flips in ([0, 17, 159], [5, 18, 40, 41]):
+            exp = want.copy()
+            exp[flips] ^= 0x10000
+            assert plan.verify(exp) == len(flips)
+            assert sorted(np.nonzero(plan.ok == 0)[0].tolist()) == flips
+            assert np.array_equal(plan.out, want)
     finally:
         plan.close()
 
