@@ -1643,6 +1643,9 @@ int h3c_plan_run(h3c_plan *p, const uint32_t *expected_raw_dev, uint32_t *out_ra
 // so concurrent callers on their own streams never force a device-wide synchronisation
 // (hipMalloc / hipFree would; hipMallocAsync pools are not used, see DeviceLease).
 constexpr uint64_t kZeroCopyMin = 64u << 10;  // pinned payloads above this are read in place
+#ifndef H3C_SYNC_IN_PLACE
+#define H3C_SYNC_IN_PLACE 1  // 0: results copied back from the device arena (the same-box A/B)
+#endif
 
 static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uint8_t *out_type, uint32_t *out_raw,
                       uint8_t *ok, uint64_t *n_mismatch, void *stream) {
@@ -1745,10 +1748,18 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
     DevChunk *d_chunks[2] = {reinterpret_cast<DevChunk *>(arena + off_chunks0),
                              reinterpret_cast<DevChunk *>(arena + off_chunks1)};
     uint32_t *d_seg = reinterpret_cast<uint32_t *>(arena + off_seg);
-    uint32_t *d_out = reinterpret_cast<uint32_t *>(arena + off_out);
     uint32_t *d_exp = expected ? reinterpret_cast<uint32_t *>(arena + off_exp) : nullptr;
+#if H3C_SYNC_IN_PLACE
+    // the results and flags go straight into the pinned lease (no copy back on the call's path); the
+    // mismatch count is taken from the flags below
+    uint32_t *d_out = reinterpret_cast<uint32_t *>(pb + off_out);
+    uint8_t *d_ok = expected ? reinterpret_cast<uint8_t *>(pb + off_ok) : nullptr;
+    uint32_t *d_mis = nullptr;
+#else
+    uint32_t *d_out = reinterpret_cast<uint32_t *>(arena + off_out);
     uint8_t *d_ok = expected ? reinterpret_cast<uint8_t *>(arena + off_ok) : nullptr;
     uint32_t *d_mis = expected ? reinterpret_cast<uint32_t *>(arena + off_mis) : nullptr;
+#endif
     for (int k = 0; k < 2; ++k) {
       if (gl.hc[k].empty()) continue;
       const int r = h3c_rt::launch_crc(st, dev, k == 0 ? H3C_TYPE_CRC32C : H3C_TYPE_CRC32, d_chunks[k],
@@ -1757,7 +1768,9 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
                                        gl.small[k], &gl.uni[k]);
       if (r) return r;
     }
+#if !H3C_SYNC_IN_PLACE
     HIP_TRY(hipMemcpyAsync(pb + off_mis, arena + off_mis, off_seg - off_mis, hipMemcpyDeviceToHost, st));
+#endif
     return H3C_OK;
   };
   rc = body();
@@ -1770,7 +1783,10 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
   std::memcpy(out_raw, pb + off_out, 4ull * n);
   if (expected) {
     std::memcpy(ok, pb + off_ok, n);
-    std::memcpy(&mis, pb + off_mis, 4);
+    if (H3C_SYNC_IN_PLACE)
+      for (size_t i = 0; i < n; ++i) mis += ok[i] == 0;
+    else
+      std::memcpy(&mis, pb + off_mis, 4);
   }
   if (out_type)
     for (size_t i = 0; i < n; ++i) {
