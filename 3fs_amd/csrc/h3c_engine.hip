@@ -1701,9 +1701,10 @@ static int batch_sync(const h3c_desc *d, size_t n, const uint32_t *expected, uin
     if (rc) return rc;
   }
   // one layout for the device arena and the pinned staging buffer, so that everything going
-  // up is one copy and everything coming back is one copy:
+  // up is one copy; the results come back by the kernels' own stores into the pinned buffer
+  // (H3C_SYNC_IN_PLACE 0: one D2H copy):
   //   [staged payloads | DevChunk lists | expected | mismatch | results out | ok] [segment partials]
-  //   |<--------------------- H2D ----------------------------->|<------- D2H ------->|
+  //   |<--------------------- H2D ----------------------------->|<- in place -->|
   const uint64_t off_chunks0 = align(off_stage + host_bytes);
   const uint64_t off_chunks1 = align(off_chunks0 + gl.hc[0].size() * sizeof(DevChunk));
   const uint64_t off_exp = align(off_chunks1 + gl.hc[1].size() * sizeof(DevChunk));
